@@ -1,0 +1,173 @@
+/*
+ * kcc.h — C-ABI of the MI355X capacity engine (libkcc.so).
+ *
+ * This is the drop-in boundary for the hot path of
+ * AshutoshNirkhe/KubernetesClusterCapacity, src/KubeAPI/ClusterCapacity.go (CC):
+ *
+ *   (a) the per-container request summation inside getPodCPUMemoryRequestsLimits
+ *       (CC:255-299, the adds at CC:290-293)           -> kcc_reduce_requests*
+ *   (b) the per-node fit + pod-slot clamp + total in main's node loop
+ *       (CC:101-140, findMin CC:159-164)               -> kcc_fit*
+ *
+ * generalised from the reference's single pod spec to a batch of S what-if specs.
+ * The Go host keeps flags, client-go listing and printing; a cgo package binds
+ * these symbols.  Every result is bit-exact to the Go integer
+ * arithmetic (uint64/int64 wrap, Go `int` = int64 on amd64, signed min, clamp quirk).
+ *
+ * Conventions
+ *   - Return 0 (KCC_OK) on success, a negative KCC_E* code otherwise; the message
+ *     is available from kcc_last_error(ctx) until the next call on ctx.
+ *   - Host-array entry points (no suffix) are synchronous: they copy inputs to the
+ *     device, run, copy results back and never retain a caller pointer.
+ *   - *_async entry points take DEVICE pointers and a hipStream_t (as void*, NULL =
+ *     the null stream) and only enqueue work: they never synchronise, and allocate
+ *     only when the context workspace must grow — call kcc_reserve first and they
+ *     can be captured into a hipGraph.  Container arrays must be 16-byte aligned.
+ *   - A context is not thread-safe; every entry calls hipSetDevice(ctx device), so
+ *     Go OS-thread migration between cgo calls is harmless.
+ *   - There is no CPU backend: without a usable gfx950 device kcc_create fails.
+ */
+#ifndef KCC_H
+#define KCC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KCC_ABI_VERSION 1
+
+enum {
+  KCC_OK = 0,
+  KCC_EINVAL = -1,   /* bad argument (null pointer, negative size, malformed CSR) */
+  KCC_ENOMEM = -2,   /* device allocation failed                                  */
+  KCC_EHIP = -3,     /* HIP runtime error                                         */
+  KCC_ENODEV = -4,   /* no usable device                                          */
+  KCC_ERCCL = -5     /* RCCL error (multi-GPU contexts)                           */
+};
+
+typedef struct kcc_ctx kcc_ctx;
+
+/* Library / ABI version (KCC_ABI_VERSION). */
+int kcc_abi_version(void);
+
+/* Create a context on `n_gpus` devices starting at `first_device`.
+ * n_gpus == 1: one device.  n_gpus > 1: nodes are sharded in contiguous ranges
+ * over devices first_device .. first_device+n_gpus-1 and the per-spec totals are
+ * combined with an RCCL int64 all-reduce (replaces nothing in the reference: the
+ * reference is single-threaded, CC:105).  n_gpus <= 0 is KCC_EINVAL. */
+int kcc_create(kcc_ctx** out, int first_device, int n_gpus);
+void kcc_destroy(kcc_ctx* ctx);
+const char* kcc_last_error(const kcc_ctx* ctx);
+/* Thread-local message of the last failed kcc_create (ctx did not exist yet). */
+const char* kcc_create_error(void);
+
+/* Pre-size the device workspace used by the *_async entry points (device 0 of ctx). */
+int kcc_reserve(kcc_ctx* ctx, int64_t max_nodes, int64_t max_containers, int64_t max_specs);
+
+/* ---------------------------------------------------------------------------
+ * (a) Segmented request reduction.  Replaces the accumulation at CC:290-293:
+ *       cpuRequestsMiliTotal     += cpuRequestsMili     (uint64, wraps)
+ *       cpuLimitsMiliTotal       += cpuLimitsMili       (uint64, wraps)
+ *       memoryRequestsBytesTotal += memoryRequestsBytes (int64,  wraps)
+ *       memoryLimitsBytesTotal   += memoryLimitsBytes   (int64,  wraps)
+ *     over every container of every non-terminated pod of a node.
+ *   Containers are grouped by node in CSR form: node i owns containers
+ *   [node_ptr[i], node_ptr[i+1]); node_ptr[0] == 0, non-decreasing,
+ *   node_ptr[n_nodes] == n_containers.  Empty nodes get 0 sums.
+ *   cpu_lim/mem_lim may both be NULL (then lim_cpu/lim_mem are ignored): the limit
+ *   sums are only printed by the reference (CC:110, CC:115-117).
+ * ------------------------------------------------------------------------- */
+int kcc_reduce_requests(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containers,
+                        const int64_t* node_ptr, const uint64_t* cpu_req,
+                        const int64_t* mem_req, const uint64_t* cpu_lim,
+                        const int64_t* mem_lim, uint64_t* used_cpu, int64_t* used_mem,
+                        uint64_t* lim_cpu, int64_t* lim_mem);
+
+int kcc_reduce_requests_async(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containers,
+                              const int64_t* d_node_ptr, const uint64_t* d_cpu_req,
+                              const int64_t* d_mem_req, const uint64_t* d_cpu_lim,
+                              const int64_t* d_mem_lim, uint64_t* d_used_cpu,
+                              int64_t* d_used_mem, uint64_t* d_lim_cpu,
+                              int64_t* d_lim_mem, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * (b) Fit.  Replaces main's node loop CC:105-140 for S specs at once:
+ *   for every node row i (zero rows for unhealthy nodes included, CC:221-226):
+ *     qc = alloc_cpu[i] <= used_cpu[i] ? 0 : int((alloc_cpu[i]-used_cpu[i]) / spec_cpu[s])   CC:119-124
+ *     qm = alloc_mem[i] <= used_mem[i] ? 0 :     (alloc_mem[i]-used_mem[i]) / spec_mem[s]    CC:125-130
+ *     q  = findMin(qc, qm)                                                                   CC:133
+ *     if q >= alloc_pods[i] { q = alloc_pods[i] - pod_count[i] }                             CC:134-136
+ *     totals[s] += q                                                                         CC:138
+ *   spec_err[s] = 1 iff the Go code would panic with an integer divide by zero
+ *   (spec_cpu[s] == 0 reached on a row with free CPU, or spec_mem[s] == 0 on a row
+ *   with free memory); totals[s] is then 0.  pod_count = len(pods) (CC:106, CC:135).
+ *   The verdict (CC:144) is totals[s] >= replicas[s], left to the caller.
+ * ------------------------------------------------------------------------- */
+int kcc_fit(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* alloc_cpu,
+            const int64_t* alloc_mem, const int64_t* alloc_pods,
+            const int64_t* pod_count, const uint64_t* used_cpu, const int64_t* used_mem,
+            int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
+            int64_t* totals, int32_t* spec_err);
+
+/* Fused (a)+(b): containers -> used sums -> fit, one device round trip. */
+int kcc_capacity(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containers,
+                 const int64_t* node_ptr, const uint64_t* cpu_req, const int64_t* mem_req,
+                 const uint64_t* alloc_cpu, const int64_t* alloc_mem,
+                 const int64_t* alloc_pods, const int64_t* pod_count, int64_t n_specs,
+                 const uint64_t* spec_cpu, const int64_t* spec_mem, int64_t* totals,
+                 int32_t* spec_err);
+
+/* Device-level fit, split so that a node-sharded caller can all-reduce in between:
+ *   kcc_fit_partial_async: partial[0..S)  = wrapping Σ over this call's nodes of q(i,s)
+ *                          partial[S..2S) = number of divide-by-zero rows
+ *                          (both in an internal spec order; zeroed by this call)
+ *   <optional all-reduce(sum, int64) of partial[0..2S) over node shards>
+ *   kcc_fit_finalize_async: totals[s], spec_err[s] in caller order.
+ * All ranks of a sharded run must pass the same specs.  `d_partial` holds 2*S int64. */
+int kcc_fit_partial_async(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* d_alloc_cpu,
+                          const int64_t* d_alloc_mem, const int64_t* d_alloc_pods,
+                          const int64_t* d_pod_count, const uint64_t* d_used_cpu,
+                          const int64_t* d_used_mem, int64_t n_specs,
+                          const uint64_t* d_spec_cpu, const int64_t* d_spec_mem,
+                          int64_t* d_partial, void* stream);
+int kcc_fit_finalize_async(kcc_ctx* ctx, int64_t n_specs, const int64_t* d_partial,
+                           int64_t* d_totals, int32_t* d_spec_err, void* stream);
+/* kcc_fit_partial_async == kcc_fit_prepare_async + kcc_fit_run_async:
+ *   prepare: zero d_partial, partition the specs (fast-path specs first) and build
+ *            the per-node free-capacity records in the context workspace;
+ *   run:     the nodes x specs fit kernel alone (what a profiler should attribute
+ *            to the fit), accumulating into d_partial.
+ * run must follow prepare on the same stream with the same sizes. */
+int kcc_fit_prepare_async(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* d_alloc_cpu,
+                          const int64_t* d_alloc_mem, const int64_t* d_alloc_pods,
+                          const int64_t* d_pod_count, const uint64_t* d_used_cpu,
+                          const int64_t* d_used_mem, int64_t n_specs,
+                          const uint64_t* d_spec_cpu, const int64_t* d_spec_mem,
+                          int64_t* d_partial, void* stream);
+int kcc_fit_run_async(kcc_ctx* ctx, int64_t n_nodes, int64_t n_specs, int64_t* d_partial,
+                      void* stream);
+
+/* Convenience: partial + finalize on one device. */
+int kcc_fit_async(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* d_alloc_cpu,
+                  const int64_t* d_alloc_mem, const int64_t* d_alloc_pods,
+                  const int64_t* d_pod_count, const uint64_t* d_used_cpu,
+                  const int64_t* d_used_mem, int64_t n_specs, const uint64_t* d_spec_cpu,
+                  const int64_t* d_spec_mem, int64_t* d_totals, int32_t* d_spec_err,
+                  void* stream);
+
+/* Fraction of (node, spec) pairs of the last kcc_fit* call that took the exact
+ * 64-bit path instead of the saturating fast path (diagnostic; host-computed from
+ * the class counters the fit kernel keeps).  -1 if unknown. */
+double kcc_last_slow_fraction(const kcc_ctx* ctx);
+
+/* Same counter for the last kcc_fit_partial_async / kcc_fit_async on device 0 of
+ * ctx: (node, spec) pairs that took the exact path, and all pairs.  Synchronises
+ * the device. */
+int kcc_fit_slow_pairs(kcc_ctx* ctx, int64_t* slow_pairs, int64_t* pairs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KCC_H */

@@ -1,0 +1,79 @@
+"""ctypes binding of libkcc.so (include/kcc.h).
+
+The product path is the HIP library: if libkcc.so is missing or cannot be loaded
+this module raises immediately — there is no Python or CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkcc.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "kcc.h")
+
+KCC_OK = 0
+KCC_EINVAL = -1
+KCC_ENOMEM = -2
+KCC_EHIP = -3
+KCC_ENODEV = -4
+KCC_ERCCL = -5
+ERROR_NAMES = {
+    KCC_EINVAL: "KCC_EINVAL", KCC_ENOMEM: "KCC_ENOMEM", KCC_EHIP: "KCC_EHIP",
+    KCC_ENODEV: "KCC_ENODEV", KCC_ERCCL: "KCC_ERCCL",
+}
+
+_i64, _i32, _int, _vp, _dbl = C.c_int64, C.c_int32, C.c_int, C.c_void_p, C.c_double
+
+# symbol -> (restype, argtypes); pointers are passed as c_void_p
+SIGNATURES = {
+    "kcc_abi_version": (_int, []),
+    "kcc_create": (_int, [C.POINTER(_vp), _int, _int]),
+    "kcc_destroy": (None, [_vp]),
+    "kcc_last_error": (C.c_char_p, [_vp]),
+    "kcc_create_error": (C.c_char_p, []),
+    "kcc_reserve": (_int, [_vp, _i64, _i64, _i64]),
+    "kcc_reduce_requests": (_int, [_vp, _i64, _i64] + [_vp] * 9),
+    "kcc_reduce_requests_async": (_int, [_vp, _i64, _i64] + [_vp] * 10),
+    "kcc_fit": (_int, [_vp, _i64] + [_vp] * 6 + [_i64] + [_vp] * 4),
+    "kcc_capacity": (_int, [_vp, _i64, _i64] + [_vp] * 7 + [_i64] + [_vp] * 4),
+    "kcc_fit_partial_async": (_int, [_vp, _i64] + [_vp] * 6 + [_i64] + [_vp] * 4),
+    "kcc_fit_prepare_async": (_int, [_vp, _i64] + [_vp] * 6 + [_i64] + [_vp] * 4),
+    "kcc_fit_run_async": (_int, [_vp, _i64, _i64, _vp, _vp]),
+    "kcc_fit_finalize_async": (_int, [_vp, _i64, _vp, _vp, _vp, _vp]),
+    "kcc_fit_async": (_int, [_vp, _i64] + [_vp] * 6 + [_i64] + [_vp] * 5),
+    "kcc_last_slow_fraction": (_dbl, [_vp]),
+    "kcc_fit_slow_pairs": (_int, [_vp, C.POINTER(_i64), C.POINTER(_i64)]),
+}
+
+
+def header_symbols(path: str = HEADER_PATH) -> list[str]:
+    """Every function the C-ABI header declares."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(kcc_[a-z0-9_]+)\s*\(", text)))
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(
+            f"libkcc.so not found at {path}: build it with "
+            "`make -C kubernetesclustercapacity_amd/csrc` (or __graft_entry__.build()). "
+            "There is no CPU fallback.")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_LIB = None
+
+
+def lib() -> C.CDLL:
+    global _LIB
+    if _LIB is None:
+        _LIB = load()
+    return _LIB

@@ -1,0 +1,591 @@
+// kcc_abi.cpp — the C-ABI of libkcc.so (include/kcc.h): contexts, device
+// workspaces, host<->device staging, node sharding over devices and the RCCL
+// all-reduce of per-spec totals.  No CPU compute path: every result comes from
+// the gfx950 kernels in kcc_kernels.hip.
+#include "kcc.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kcc_internal.h"
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+hipError_t ensure(DevBuf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.bytes >= bytes) return hipSuccess;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if (e == hipSuccess) b.bytes = bytes;
+  return e;
+}
+
+template <class T>
+T* as(DevBuf& b) {
+  return static_cast<T*>(b.p);
+}
+
+struct Dev {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // workspace of the *_async entry points
+  DevBuf wave_node, fast, slow, sc, sm, smd, src, srm, sperm, snormal, counters;
+  int64_t last_pairs = 0;  // node x spec pairs of the last fit_prepare on this device
+  int64_t prep_nodes = -1, prep_specs = -1;  // sizes the workspace was last prepared for
+  // staging of the host-array entry points
+  DevBuf ptr, cpu, mem, cpul, meml, used_cpu, used_mem, lim_cpu, lim_mem;
+  DevBuf alloc_cpu, alloc_mem, alloc_pods, pod_count, spec_cpu, spec_mem, partial, totals, err;
+};
+
+}  // namespace
+
+struct kcc_ctx {
+  std::vector<Dev> devs;
+  std::vector<ncclComm_t> comms;
+  std::string err;
+  double slow_frac = -1.0;
+};
+
+namespace {
+
+thread_local std::string g_create_error;
+
+int fail(kcc_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+#define KCC_HIP(ctx, expr)                                                              \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail((ctx), e_ == hipErrorOutOfMemory ? KCC_ENOMEM : KCC_EHIP,             \
+                  std::string(#expr) + ": " + hipGetErrorString(e_));                   \
+  } while (0)
+
+#define KCC_NCCL(ctx, expr)                                                             \
+  do {                                                                                  \
+    ncclResult_t r_ = (expr);                                                           \
+    if (r_ != ncclSuccess)                                                              \
+      return fail((ctx), KCC_ERCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// CSR sanity on the host (the host-array entry points): a malformed offset array is
+// rejected here instead of reaching the device.
+int check_csr(kcc_ctx* ctx, int64_t n_nodes, int64_t n_cont, const int64_t* ptr) {
+  if (n_nodes < 0 || n_cont < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (n_nodes == 0) {
+    if (n_cont != 0) return fail(ctx, KCC_EINVAL, "containers without nodes");
+    return KCC_OK;
+  }
+  if (!ptr) return fail(ctx, KCC_EINVAL, "node_ptr is NULL");
+  if (ptr[0] != 0) return fail(ctx, KCC_EINVAL, "node_ptr[0] != 0");
+  for (int64_t i = 0; i < n_nodes; ++i)
+    if (ptr[i + 1] < ptr[i]) return fail(ctx, KCC_EINVAL, "node_ptr is not non-decreasing");
+  if (ptr[n_nodes] != n_cont) return fail(ctx, KCC_EINVAL, "node_ptr[n_nodes] != n_containers");
+  return KCC_OK;
+}
+
+// Contiguous node ranges, balanced by node count (the fit dominates).
+void shard_nodes(int64_t n_nodes, int n, std::vector<int64_t>& lo, std::vector<int64_t>& hi) {
+  lo.resize(n);
+  hi.resize(n);
+  for (int d = 0; d < n; ++d) {
+    lo[d] = n_nodes * d / n;
+    hi[d] = n_nodes * (d + 1) / n;
+  }
+}
+
+template <class T>
+int h2d(kcc_ctx* ctx, Dev& dv, DevBuf& buf, const T* src, int64_t count) {
+  KCC_HIP(ctx, ensure(buf, sizeof(T) * (size_t)(count > 0 ? count : 1)));
+  if (count > 0)
+    KCC_HIP(ctx, hipMemcpyAsync(buf.p, src, sizeof(T) * (size_t)count, hipMemcpyHostToDevice,
+                                dv.stream));
+  return KCC_OK;
+}
+
+// ---- device-level pipeline pieces (no host sync, no allocation beyond growth) ----
+
+int reduce_async_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, const int64_t* ptr,
+                     const uint64_t* cpu, const int64_t* mem, const uint64_t* cpul,
+                     const int64_t* meml, uint64_t* used_cpu, int64_t* used_mem,
+                     uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s) {
+  if (n_nodes < 0 || n_cont < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (n_nodes == 0) return n_cont == 0 ? KCC_OK : fail(ctx, KCC_EINVAL, "containers without nodes");
+  if (!ptr || !used_cpu || !used_mem) return fail(ctx, KCC_EINVAL, "NULL node_ptr/output");
+  if (n_cont > 0 && (!cpu || !mem)) return fail(ctx, KCC_EINVAL, "NULL cpu_req/mem_req");
+  const bool lim = cpul != nullptr || meml != nullptr;
+  if (lim && (!cpul || !meml || !lim_cpu || !lim_mem))
+    return fail(ctx, KCC_EINVAL, "limits need cpu_lim, mem_lim, lim_cpu and lim_mem");
+  if (!aligned16(cpu) || !aligned16(mem) || (lim && (!aligned16(cpul) || !aligned16(meml))))
+    return fail(ctx, KCC_EINVAL, "container arrays must be 16-byte aligned");
+  const int64_t waves = kcc::reduce_n_waves(n_cont);
+  KCC_HIP(ctx, ensure(dv.wave_node, sizeof(int64_t) * (size_t)(waves > 0 ? waves : 1)));
+  KCC_HIP(ctx, kcc::launch_reduce_mark(n_nodes, n_cont, ptr, as<int64_t>(dv.wave_node), used_cpu,
+                                       used_mem, lim ? lim_cpu : nullptr,
+                                       lim ? lim_mem : nullptr, s));
+  KCC_HIP(ctx, kcc::launch_reduce(n_nodes, n_cont, ptr, cpu, mem, lim ? cpul : nullptr,
+                                  lim ? meml : nullptr, as<int64_t>(dv.wave_node), used_cpu,
+                                  used_mem, lim ? lim_cpu : nullptr, lim ? lim_mem : nullptr, s));
+  return KCC_OK;
+}
+
+kcc::SpecPrep spec_prep_of(Dev& dv) {
+  kcc::SpecPrep sp;
+  sp.c = as<uint64_t>(dv.sc);
+  sp.m = as<int64_t>(dv.sm);
+  sp.md = as<double>(dv.smd);
+  sp.rc = as<float>(dv.src);
+  sp.rm = as<float>(dv.srm);
+  sp.perm = as<int32_t>(dv.sperm);
+  sp.normal = as<int32_t>(dv.snormal);
+  return sp;
+}
+
+int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t n_specs) {
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  const size_t N = (size_t)(n_nodes > 0 ? n_nodes : 1);
+  const size_t S = (size_t)(n_specs > 0 ? n_specs : 1);
+  const int64_t waves = kcc::reduce_n_waves(n_cont > 0 ? n_cont : 1);
+  KCC_HIP(ctx, ensure(dv.wave_node, sizeof(int64_t) * (size_t)waves));
+  KCC_HIP(ctx, ensure(dv.fast, sizeof(kcc::FitNode) * N));
+  KCC_HIP(ctx, ensure(dv.slow, sizeof(kcc::SlowNode) * N));
+  KCC_HIP(ctx, ensure(dv.sc, 8 * S));
+  KCC_HIP(ctx, ensure(dv.sm, 8 * S));
+  KCC_HIP(ctx, ensure(dv.smd, 8 * S));
+  KCC_HIP(ctx, ensure(dv.src, 4 * S));
+  KCC_HIP(ctx, ensure(dv.srm, 4 * S));
+  KCC_HIP(ctx, ensure(dv.sperm, 4 * S));
+  KCC_HIP(ctx, ensure(dv.snormal, 4 * S));
+  KCC_HIP(ctx, ensure(dv.counters, 64));
+  return KCC_OK;
+}
+
+int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* alloc_cpu,
+                    const int64_t* alloc_mem, const int64_t* alloc_pods,
+                    const int64_t* pod_count, const uint64_t* used_cpu,
+                    const int64_t* used_mem, int64_t n_specs, const uint64_t* spec_cpu,
+                    const int64_t* spec_mem, int64_t* partial, hipStream_t s) {
+  if (n_nodes < 0 || n_specs < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (n_specs > 0x7fffffffLL) return fail(ctx, KCC_EINVAL, "too many specs (max 2^31-1)");
+  if (n_specs > 0 && (!spec_cpu || !spec_mem || !partial))
+    return fail(ctx, KCC_EINVAL, "NULL spec array / partial");
+  if (n_nodes > 0 && (!alloc_cpu || !alloc_mem || !alloc_pods || !pod_count || !used_cpu || !used_mem))
+    return fail(ctx, KCC_EINVAL, "NULL node array");
+  int rc = reserve_dev(ctx, dv, n_nodes, 0, n_specs);
+  if (rc) return rc;
+  dv.last_pairs = n_nodes * n_specs;
+  dv.prep_nodes = n_nodes;
+  dv.prep_specs = n_specs;
+  if (n_specs == 0) return KCC_OK;
+  KCC_HIP(ctx, hipMemsetAsync(partial, 0, sizeof(int64_t) * 2 * (size_t)n_specs, s));
+  KCC_HIP(ctx, hipMemsetAsync(dv.counters.p, 0, 64, s));
+  KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv), s));
+  if (n_nodes == 0) return KCC_OK;
+  KCC_HIP(ctx, kcc::launch_node_prep(n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count,
+                                     used_cpu, used_mem, as<kcc::FitNode>(dv.fast),
+                                     as<kcc::SlowNode>(dv.slow), s));
+  return KCC_OK;
+}
+
+int fit_run_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_specs, int64_t* partial,
+                hipStream_t s) {
+  if (n_nodes != dv.prep_nodes || n_specs != dv.prep_specs)
+    return fail(ctx, KCC_EINVAL, "fit_run sizes differ from the preceding fit_prepare");
+  if (n_nodes == 0 || n_specs == 0) return KCC_OK;
+  if (!partial) return fail(ctx, KCC_EINVAL, "NULL partial");
+  KCC_HIP(ctx, kcc::launch_fit(n_nodes, as<kcc::FitNode>(dv.fast), as<kcc::SlowNode>(dv.slow),
+                               n_specs, spec_prep_of(dv), partial,
+                               as<unsigned long long>(dv.counters), s));
+  return KCC_OK;
+}
+
+int fit_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* alloc_cpu,
+                    const int64_t* alloc_mem, const int64_t* alloc_pods,
+                    const int64_t* pod_count, const uint64_t* used_cpu,
+                    const int64_t* used_mem, int64_t n_specs, const uint64_t* spec_cpu,
+                    const int64_t* spec_mem, int64_t* partial, hipStream_t s) {
+  int rc = fit_prepare_dev(ctx, dv, n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count,
+                           used_cpu, used_mem, n_specs, spec_cpu, spec_mem, partial, s);
+  if (rc) return rc;
+  return fit_run_dev(ctx, dv, n_nodes, n_specs, partial, s);
+}
+
+int fit_finalize_dev(kcc_ctx* ctx, Dev& dv, int64_t n_specs, const int64_t* partial,
+                     int64_t* totals, int32_t* spec_err, hipStream_t s) {
+  if (n_specs < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (n_specs == 0) return KCC_OK;
+  if (!partial || !totals || !spec_err) return fail(ctx, KCC_EINVAL, "NULL partial/totals/err");
+  if (dv.sperm.bytes < sizeof(int32_t) * (size_t)n_specs)
+    return fail(ctx, KCC_EINVAL, "finalize without a matching fit_partial");
+  KCC_HIP(ctx, kcc::launch_fit_finalize(n_specs, partial, as<int32_t>(dv.sperm), totals,
+                                        spec_err, s));
+  return KCC_OK;
+}
+
+// Host-array pipeline shared by kcc_fit / kcc_capacity: per device upload its node
+// shard (and container shard), reduce (optional), fit_partial; all-reduce partials
+// over RCCL when sharded; finalize on device 0; copy back.
+int run_host(kcc_ctx* ctx, bool with_reduce, int64_t n_nodes, int64_t n_cont,
+             const int64_t* node_ptr, const uint64_t* cpu_req, const int64_t* mem_req,
+             const uint64_t* alloc_cpu, const int64_t* alloc_mem, const int64_t* alloc_pods,
+             const int64_t* pod_count, const uint64_t* used_cpu_in, const int64_t* used_mem_in,
+             int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
+             int64_t* totals, int32_t* spec_err) {
+  if (n_nodes < 0 || n_specs < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (n_specs > 0 && (!spec_cpu || !spec_mem || !totals || !spec_err))
+    return fail(ctx, KCC_EINVAL, "NULL spec array / output");
+  if (n_nodes > 0 && (!alloc_cpu || !alloc_mem || !alloc_pods || !pod_count))
+    return fail(ctx, KCC_EINVAL, "NULL node array");
+  if (with_reduce) {
+    int rc = check_csr(ctx, n_nodes, n_cont, node_ptr);
+    if (rc) return rc;
+    if (n_cont > 0 && (!cpu_req || !mem_req)) return fail(ctx, KCC_EINVAL, "NULL container array");
+  } else if (n_nodes > 0 && (!used_cpu_in || !used_mem_in)) {
+    return fail(ctx, KCC_EINVAL, "NULL used array");
+  }
+  if (n_specs == 0) return KCC_OK;
+  const int nd = (int)ctx->devs.size();
+  std::vector<int64_t> lo, hi;
+  shard_nodes(n_nodes, nd, lo, hi);
+  std::vector<std::vector<int64_t>> rebased(nd);  // per device: copies may still be in flight
+  for (int d = 0; d < nd; ++d) {
+    Dev& dv = ctx->devs[d];
+    KCC_HIP(ctx, hipSetDevice(dv.device));
+    const int64_t n = hi[d] - lo[d];
+    int rc;
+    if ((rc = h2d(ctx, dv, dv.alloc_cpu, alloc_cpu + lo[d], n))) return rc;
+    if ((rc = h2d(ctx, dv, dv.alloc_mem, alloc_mem + lo[d], n))) return rc;
+    if ((rc = h2d(ctx, dv, dv.alloc_pods, alloc_pods + lo[d], n))) return rc;
+    if ((rc = h2d(ctx, dv, dv.pod_count, pod_count + lo[d], n))) return rc;
+    if ((rc = h2d(ctx, dv, dv.spec_cpu, spec_cpu, n_specs))) return rc;
+    if ((rc = h2d(ctx, dv, dv.spec_mem, spec_mem, n_specs))) return rc;
+    KCC_HIP(ctx, ensure(dv.partial, sizeof(int64_t) * 2 * (size_t)n_specs));
+    if (with_reduce) {
+      const int64_t c0 = n > 0 ? node_ptr[lo[d]] : 0, c1 = n > 0 ? node_ptr[hi[d]] : 0;
+      std::vector<int64_t>& rb = rebased[d];
+      rb.resize((size_t)n + 1);
+      for (int64_t k = 0; k <= n; ++k) rb[k] = n > 0 ? node_ptr[lo[d] + k] - c0 : 0;
+      if ((rc = h2d(ctx, dv, dv.ptr, rb.data(), n + 1))) return rc;
+      if ((rc = h2d(ctx, dv, dv.cpu, cpu_req + c0, c1 - c0))) return rc;
+      if ((rc = h2d(ctx, dv, dv.mem, mem_req + c0, c1 - c0))) return rc;
+      KCC_HIP(ctx, ensure(dv.used_cpu, 8 * (size_t)(n > 0 ? n : 1)));
+      KCC_HIP(ctx, ensure(dv.used_mem, 8 * (size_t)(n > 0 ? n : 1)));
+      if (n > 0) {
+        rc = reduce_async_dev(ctx, dv, n, c1 - c0, as<int64_t>(dv.ptr), as<uint64_t>(dv.cpu),
+                              as<int64_t>(dv.mem), nullptr, nullptr, as<uint64_t>(dv.used_cpu),
+                              as<int64_t>(dv.used_mem), nullptr, nullptr, dv.stream);
+        if (rc) return rc;
+      }
+    } else {
+      if ((rc = h2d(ctx, dv, dv.used_cpu, used_cpu_in + lo[d], n))) return rc;
+      if ((rc = h2d(ctx, dv, dv.used_mem, used_mem_in + lo[d], n))) return rc;
+    }
+    rc = fit_partial_dev(ctx, dv, n, as<uint64_t>(dv.alloc_cpu), as<int64_t>(dv.alloc_mem),
+                         as<int64_t>(dv.alloc_pods), as<int64_t>(dv.pod_count),
+                         as<uint64_t>(dv.used_cpu), as<int64_t>(dv.used_mem), n_specs,
+                         as<uint64_t>(dv.spec_cpu), as<int64_t>(dv.spec_mem),
+                         as<int64_t>(dv.partial), dv.stream);
+    if (rc) return rc;
+  }
+  if (nd > 1) {
+    KCC_NCCL(ctx, ncclGroupStart());
+    for (int d = 0; d < nd; ++d) {
+      Dev& dv = ctx->devs[d];
+      KCC_NCCL(ctx, ncclAllReduce(dv.partial.p, dv.partial.p, 2 * (size_t)n_specs, ncclInt64,
+                                  ncclSum, ctx->comms[d], dv.stream));
+    }
+    KCC_NCCL(ctx, ncclGroupEnd());
+  }
+  Dev& d0 = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(d0.device));
+  KCC_HIP(ctx, ensure(d0.totals, 8 * (size_t)n_specs));
+  KCC_HIP(ctx, ensure(d0.err, 4 * (size_t)n_specs));
+  int rc = fit_finalize_dev(ctx, d0, n_specs, as<int64_t>(d0.partial), as<int64_t>(d0.totals),
+                            as<int32_t>(d0.err), d0.stream);
+  if (rc) return rc;
+  KCC_HIP(ctx, hipMemcpyAsync(totals, d0.totals.p, 8 * (size_t)n_specs, hipMemcpyDeviceToHost,
+                              d0.stream));
+  KCC_HIP(ctx, hipMemcpyAsync(spec_err, d0.err.p, 4 * (size_t)n_specs, hipMemcpyDeviceToHost,
+                              d0.stream));
+  unsigned long long slow_pairs = 0;
+  for (int d = 0; d < nd; ++d) {
+    Dev& dv = ctx->devs[d];
+    KCC_HIP(ctx, hipSetDevice(dv.device));
+    unsigned long long c = 0;
+    KCC_HIP(ctx, hipMemcpyAsync(&c, dv.counters.p, sizeof(c), hipMemcpyDeviceToHost, dv.stream));
+    KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
+    slow_pairs += c;
+  }
+  const double pairs = (double)n_nodes * (double)n_specs;
+  ctx->slow_frac = pairs > 0 ? (double)slow_pairs / pairs : 0.0;
+  return KCC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kcc_abi_version(void) { return KCC_ABI_VERSION; }
+
+const char* kcc_create_error(void) { return g_create_error.c_str(); }
+
+int kcc_create(kcc_ctx** out, int first_device, int n_gpus) {
+  g_create_error.clear();
+  if (!out) { g_create_error = "out is NULL"; return KCC_EINVAL; }
+  *out = nullptr;
+  if (n_gpus <= 0 || first_device < 0) {
+    g_create_error = "n_gpus must be >= 1 and first_device >= 0 (there is no CPU backend)";
+    return KCC_EINVAL;
+  }
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count <= 0) {
+    g_create_error = std::string("no HIP device: ") + hipGetErrorString(e);
+    return KCC_ENODEV;
+  }
+  if (first_device + n_gpus > count) {
+    g_create_error = "requested devices [" + std::to_string(first_device) + ", " +
+                     std::to_string(first_device + n_gpus) + ") but only " +
+                     std::to_string(count) + " visible";
+    return KCC_ENODEV;
+  }
+  kcc_ctx* ctx = new kcc_ctx();
+  ctx->devs.resize(n_gpus);
+  std::vector<int> ids(n_gpus);
+  for (int d = 0; d < n_gpus; ++d) {
+    Dev& dv = ctx->devs[d];
+    dv.device = first_device + d;
+    ids[d] = dv.device;
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, dv.device)) != hipSuccess ||
+        std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+      g_create_error = "device " + std::to_string(dv.device) + " is not gfx950 (" +
+                       (e == hipSuccess ? std::string(prop.gcnArchName)
+                                        : std::string(hipGetErrorString(e))) +
+                       "): libkcc is built for MI355X only";
+      kcc_destroy(ctx);
+      return KCC_ENODEV;
+    }
+    if ((e = hipSetDevice(dv.device)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&dv.stream, hipStreamNonBlocking)) != hipSuccess) {
+      g_create_error = std::string("stream creation failed: ") + hipGetErrorString(e);
+      kcc_destroy(ctx);
+      return KCC_EHIP;
+    }
+  }
+  if (n_gpus > 1) {
+    ctx->comms.resize(n_gpus);
+    ncclResult_t r = ncclCommInitAll(ctx->comms.data(), n_gpus, ids.data());
+    if (r != ncclSuccess) {
+      ctx->comms.clear();
+      g_create_error = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+      kcc_destroy(ctx);
+      return KCC_ERCCL;
+    }
+  }
+  *out = ctx;
+  return KCC_OK;
+}
+
+void kcc_destroy(kcc_ctx* ctx) {
+  if (!ctx) return;
+  for (auto& c : ctx->comms) ncclCommDestroy(c);
+  for (Dev& dv : ctx->devs) {
+    (void)hipSetDevice(dv.device);
+    if (dv.stream) (void)hipStreamSynchronize(dv.stream);
+    DevBuf* bufs[] = {&dv.wave_node, &dv.fast,      &dv.slow,      &dv.sc,        &dv.sm,
+                      &dv.smd,       &dv.src,       &dv.srm,       &dv.sperm,     &dv.snormal,
+                      &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
+                      &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,
+                      &dv.alloc_cpu, &dv.alloc_mem, &dv.alloc_pods, &dv.pod_count, &dv.spec_cpu,
+                      &dv.spec_mem,  &dv.partial,   &dv.totals,    &dv.err};
+    for (DevBuf* b : bufs)
+      if (b->p) (void)hipFree(b->p);
+    if (dv.stream) (void)hipStreamDestroy(dv.stream);
+  }
+  delete ctx;
+}
+
+const char* kcc_last_error(const kcc_ctx* ctx) { return ctx ? ctx->err.c_str() : "NULL context"; }
+
+int kcc_reserve(kcc_ctx* ctx, int64_t max_nodes, int64_t max_containers, int64_t max_specs) {
+  if (!ctx) return KCC_EINVAL;
+  if (max_nodes < 0 || max_containers < 0 || max_specs < 0)
+    return fail(ctx, KCC_EINVAL, "negative size");
+  return reserve_dev(ctx, ctx->devs[0], max_nodes, max_containers, max_specs);
+}
+
+int kcc_reduce_requests_async(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containers,
+                              const int64_t* d_node_ptr, const uint64_t* d_cpu_req,
+                              const int64_t* d_mem_req, const uint64_t* d_cpu_lim,
+                              const int64_t* d_mem_lim, uint64_t* d_used_cpu,
+                              int64_t* d_used_mem, uint64_t* d_lim_cpu, int64_t* d_lim_mem,
+                              void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  return reduce_async_dev(ctx, dv, n_nodes, n_containers, d_node_ptr, d_cpu_req, d_mem_req,
+                          d_cpu_lim, d_mem_lim, d_used_cpu, d_used_mem, d_lim_cpu, d_lim_mem,
+                          static_cast<hipStream_t>(stream));
+}
+
+int kcc_reduce_requests(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containers,
+                        const int64_t* node_ptr, const uint64_t* cpu_req, const int64_t* mem_req,
+                        const uint64_t* cpu_lim, const int64_t* mem_lim, uint64_t* used_cpu,
+                        int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem) {
+  if (!ctx) return KCC_EINVAL;
+  int rc = check_csr(ctx, n_nodes, n_containers, node_ptr);
+  if (rc) return rc;
+  if (n_nodes == 0) return KCC_OK;
+  if (!used_cpu || !used_mem) return fail(ctx, KCC_EINVAL, "NULL output");
+  if (n_containers > 0 && (!cpu_req || !mem_req)) return fail(ctx, KCC_EINVAL, "NULL container array");
+  const bool lim = cpu_lim != nullptr || mem_lim != nullptr;
+  if (lim && (!cpu_lim || !mem_lim || !lim_cpu || !lim_mem))
+    return fail(ctx, KCC_EINVAL, "limits need cpu_lim, mem_lim, lim_cpu and lim_mem");
+  // the reduce is cheap next to the fit: run it on the first device
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  if ((rc = h2d(ctx, dv, dv.ptr, node_ptr, n_nodes + 1))) return rc;
+  if ((rc = h2d(ctx, dv, dv.cpu, cpu_req, n_containers))) return rc;
+  if ((rc = h2d(ctx, dv, dv.mem, mem_req, n_containers))) return rc;
+  if (lim) {
+    if ((rc = h2d(ctx, dv, dv.cpul, cpu_lim, n_containers))) return rc;
+    if ((rc = h2d(ctx, dv, dv.meml, mem_lim, n_containers))) return rc;
+    KCC_HIP(ctx, ensure(dv.lim_cpu, 8 * (size_t)n_nodes));
+    KCC_HIP(ctx, ensure(dv.lim_mem, 8 * (size_t)n_nodes));
+  }
+  KCC_HIP(ctx, ensure(dv.used_cpu, 8 * (size_t)n_nodes));
+  KCC_HIP(ctx, ensure(dv.used_mem, 8 * (size_t)n_nodes));
+  rc = reduce_async_dev(ctx, dv, n_nodes, n_containers, as<int64_t>(dv.ptr), as<uint64_t>(dv.cpu),
+                        as<int64_t>(dv.mem), lim ? as<uint64_t>(dv.cpul) : nullptr,
+                        lim ? as<int64_t>(dv.meml) : nullptr, as<uint64_t>(dv.used_cpu),
+                        as<int64_t>(dv.used_mem), lim ? as<uint64_t>(dv.lim_cpu) : nullptr,
+                        lim ? as<int64_t>(dv.lim_mem) : nullptr, dv.stream);
+  if (rc) return rc;
+  KCC_HIP(ctx, hipMemcpyAsync(used_cpu, dv.used_cpu.p, 8 * (size_t)n_nodes,
+                              hipMemcpyDeviceToHost, dv.stream));
+  KCC_HIP(ctx, hipMemcpyAsync(used_mem, dv.used_mem.p, 8 * (size_t)n_nodes,
+                              hipMemcpyDeviceToHost, dv.stream));
+  if (lim) {
+    KCC_HIP(ctx, hipMemcpyAsync(lim_cpu, dv.lim_cpu.p, 8 * (size_t)n_nodes,
+                                hipMemcpyDeviceToHost, dv.stream));
+    KCC_HIP(ctx, hipMemcpyAsync(lim_mem, dv.lim_mem.p, 8 * (size_t)n_nodes,
+                                hipMemcpyDeviceToHost, dv.stream));
+  }
+  KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
+  return KCC_OK;
+}
+
+int kcc_fit(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* alloc_cpu, const int64_t* alloc_mem,
+            const int64_t* alloc_pods, const int64_t* pod_count, const uint64_t* used_cpu,
+            const int64_t* used_mem, int64_t n_specs, const uint64_t* spec_cpu,
+            const int64_t* spec_mem, int64_t* totals, int32_t* spec_err) {
+  if (!ctx) return KCC_EINVAL;
+  return run_host(ctx, false, n_nodes, 0, nullptr, nullptr, nullptr, alloc_cpu, alloc_mem,
+                  alloc_pods, pod_count, used_cpu, used_mem, n_specs, spec_cpu, spec_mem, totals,
+                  spec_err);
+}
+
+int kcc_capacity(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containers, const int64_t* node_ptr,
+                 const uint64_t* cpu_req, const int64_t* mem_req, const uint64_t* alloc_cpu,
+                 const int64_t* alloc_mem, const int64_t* alloc_pods, const int64_t* pod_count,
+                 int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
+                 int64_t* totals, int32_t* spec_err) {
+  if (!ctx) return KCC_EINVAL;
+  return run_host(ctx, true, n_nodes, n_containers, node_ptr, cpu_req, mem_req, alloc_cpu,
+                  alloc_mem, alloc_pods, pod_count, nullptr, nullptr, n_specs, spec_cpu, spec_mem,
+                  totals, spec_err);
+}
+
+int kcc_fit_partial_async(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* d_alloc_cpu,
+                          const int64_t* d_alloc_mem, const int64_t* d_alloc_pods,
+                          const int64_t* d_pod_count, const uint64_t* d_used_cpu,
+                          const int64_t* d_used_mem, int64_t n_specs, const uint64_t* d_spec_cpu,
+                          const int64_t* d_spec_mem, int64_t* d_partial, void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  return fit_partial_dev(ctx, dv, n_nodes, d_alloc_cpu, d_alloc_mem, d_alloc_pods, d_pod_count,
+                         d_used_cpu, d_used_mem, n_specs, d_spec_cpu, d_spec_mem, d_partial,
+                         static_cast<hipStream_t>(stream));
+}
+
+int kcc_fit_prepare_async(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* d_alloc_cpu,
+                          const int64_t* d_alloc_mem, const int64_t* d_alloc_pods,
+                          const int64_t* d_pod_count, const uint64_t* d_used_cpu,
+                          const int64_t* d_used_mem, int64_t n_specs, const uint64_t* d_spec_cpu,
+                          const int64_t* d_spec_mem, int64_t* d_partial, void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  return fit_prepare_dev(ctx, dv, n_nodes, d_alloc_cpu, d_alloc_mem, d_alloc_pods, d_pod_count,
+                         d_used_cpu, d_used_mem, n_specs, d_spec_cpu, d_spec_mem, d_partial,
+                         static_cast<hipStream_t>(stream));
+}
+
+int kcc_fit_run_async(kcc_ctx* ctx, int64_t n_nodes, int64_t n_specs, int64_t* d_partial,
+                      void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  return fit_run_dev(ctx, dv, n_nodes, n_specs, d_partial, static_cast<hipStream_t>(stream));
+}
+
+int kcc_fit_finalize_async(kcc_ctx* ctx, int64_t n_specs, const int64_t* d_partial,
+                           int64_t* d_totals, int32_t* d_spec_err, void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  return fit_finalize_dev(ctx, dv, n_specs, d_partial, d_totals, d_spec_err,
+                          static_cast<hipStream_t>(stream));
+}
+
+int kcc_fit_async(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* d_alloc_cpu,
+                  const int64_t* d_alloc_mem, const int64_t* d_alloc_pods,
+                  const int64_t* d_pod_count, const uint64_t* d_used_cpu,
+                  const int64_t* d_used_mem, int64_t n_specs, const uint64_t* d_spec_cpu,
+                  const int64_t* d_spec_mem, int64_t* d_totals, int32_t* d_spec_err,
+                  void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  KCC_HIP(ctx, ensure(dv.partial, sizeof(int64_t) * 2 * (size_t)(n_specs > 0 ? n_specs : 1)));
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  int rc = fit_partial_dev(ctx, dv, n_nodes, d_alloc_cpu, d_alloc_mem, d_alloc_pods, d_pod_count,
+                           d_used_cpu, d_used_mem, n_specs, d_spec_cpu, d_spec_mem,
+                           as<int64_t>(dv.partial), s);
+  if (rc) return rc;
+  return fit_finalize_dev(ctx, dv, n_specs, as<int64_t>(dv.partial), d_totals, d_spec_err, s);
+}
+
+double kcc_last_slow_fraction(const kcc_ctx* ctx) { return ctx ? ctx->slow_frac : -1.0; }
+
+int kcc_fit_slow_pairs(kcc_ctx* ctx, int64_t* slow_pairs, int64_t* pairs) {
+  if (!ctx || !slow_pairs || !pairs) return ctx ? fail(ctx, KCC_EINVAL, "NULL output") : KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  KCC_HIP(ctx, hipDeviceSynchronize());
+  unsigned long long c = 0;
+  if (dv.counters.p) KCC_HIP(ctx, hipMemcpy(&c, dv.counters.p, sizeof(c), hipMemcpyDeviceToHost));
+  *slow_pairs = (int64_t)c;
+  *pairs = dv.last_pairs;
+  return KCC_OK;
+}
+
+}  // extern "C"

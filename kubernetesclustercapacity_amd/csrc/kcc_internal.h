@@ -1,0 +1,88 @@
+// kcc_internal.h — launch interface between the C-ABI layer (kcc_abi.cpp) and the
+// gfx950 kernels (kcc_kernels.hip).  Internal: not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kcc {
+
+// ---- (a) segmented request reduce -------------------------------------------
+// One wavefront owns a contiguous range of RED_RANGE containers and walks it in
+// tiles of RED_TILE (2 containers per lane, one 16-B load per lane per array).
+constexpr int RED_TILE = 128;
+constexpr int RED_TILES_PER_WAVE = 32;
+constexpr int64_t RED_RANGE = (int64_t)RED_TILE * RED_TILES_PER_WAVE;  // 4096
+constexpr int RED_WAVES_PER_BLOCK = 4;
+
+inline int64_t reduce_n_waves(int64_t n_containers) {
+  return (n_containers + RED_RANGE - 1) / RED_RANGE;
+}
+
+// Zeroes the per-node outputs and records, for every wave range, the node that owns
+// the range's first container (wave_node[n_waves]).
+hipError_t launch_reduce_mark(int64_t n_nodes, int64_t n_containers, const int64_t* node_ptr,
+                              int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem,
+                              uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s);
+
+hipError_t launch_reduce(int64_t n_nodes, int64_t n_containers, const int64_t* node_ptr,
+                         const uint64_t* cpu_req, const int64_t* mem_req,
+                         const uint64_t* cpu_lim, const int64_t* mem_lim,
+                         const int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem,
+                         uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s);
+
+// ---- (b) fit -----------------------------------------------------------------
+// Per-node record streamed by the fit kernel through the scalar cache (32 B, one
+// s_load_dwordx8).  fc_i < 0 marks a node that needs the exact 64-bit path.
+struct __attribute__((aligned(32))) FitNode {
+  double fm_d;   // free memory (bytes), exact in f64 on the fast path
+  float fc_f;    // free CPU (millicores), rounded to f32 — quotient estimate only
+  float fm_f;    // free memory, rounded to f32 — quotient estimate only
+  int32_t fc_i;  // free CPU, exact (fast path: 0 <= fc < 2^31), or -1
+  float P_f;     // allocatable pods as f32 (exact on the fast path)
+  int32_t P_i;   // allocatable pods
+  int32_t cl_i;  // clamp value allocatable pods - podCount (CC:135)
+};
+static_assert(sizeof(FitNode) == 32, "FitNode must be 32 B");
+
+// Raw per-node values for the exact path (fc/fm are 0 where the reference's
+// `alloc <= used` branch yields 0, i.e. no division happens).
+struct __attribute__((aligned(32))) SlowNode {
+  uint64_t fc;
+  int64_t fm;
+  int64_t P;
+  int64_t cl;
+};
+static_assert(sizeof(SlowNode) == 32, "SlowNode must be 32 B");
+
+// Spec arrays in the kernel's internal (partitioned) order: specs that satisfy the
+// fast-path bounds first, the rest after (so at most one wavefront mixes both).
+struct SpecPrep {
+  uint64_t* c;     // cpu request (millicores)
+  int64_t* m;      // memory request (bytes)
+  double* md;      // m as f64
+  float* rc;       // 1/c (f32)
+  float* rm;       // 1/m (f32)
+  int32_t* perm;   // internal index -> caller index
+  int32_t* normal; // 1 if the spec satisfies the fast-path bounds
+};
+
+hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
+                            const int64_t* alloc_mem, const int64_t* alloc_pods,
+                            const int64_t* pod_count, const uint64_t* used_cpu,
+                            const int64_t* used_mem, FitNode* fast, SlowNode* slow,
+                            hipStream_t s);
+
+hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
+                            const int64_t* spec_mem, SpecPrep sp, hipStream_t s);
+
+// partial[0..S) += Σ_i q(i,s), partial[S..2S) += #div-by-zero rows (internal order);
+// counters[0] += (node, spec) pairs that took the exact path.
+hipError_t launch_fit(int64_t n_nodes, const FitNode* fast, const SlowNode* slow,
+                      int64_t n_specs, SpecPrep sp, int64_t* partial,
+                      unsigned long long* counters, hipStream_t s);
+
+hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial,
+                               const int32_t* perm, int64_t* totals, int32_t* spec_err,
+                               hipStream_t s);
+
+}  // namespace kcc

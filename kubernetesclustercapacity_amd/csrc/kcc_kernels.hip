@@ -1,0 +1,547 @@
+// kcc_kernels.hip — gfx950 kernels of the capacity engine.
+//
+// Hot path of AshutoshNirkhe/KubernetesClusterCapacity, src/KubeAPI/ClusterCapacity.go (CC):
+//   (a) reduce_kernel: the per-container request sums of getPodCPUMemoryRequestsLimits
+//       (CC:276-294, adds at CC:290-293), as a segmented int64 reduction over a CSR
+//       container list (one segment per node).
+//   (b) fit_kernel: main's per-node fit (CC:119-136, findMin CC:159-164) and the
+//       total (CC:138), for a batch of S specs (nodes x specs), reduced per spec.
+// Both are integer work: no MFMA (no contraction), HBM-bound (a) / VALU-bound (b).
+// Results are bit-exact to Go's uint64/int64 wrapping arithmetic.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kcc_internal.h"
+
+namespace kcc {
+
+namespace {
+
+constexpr int32_t HEAD_END = 0x7fffffff;  // "end of data" head marker
+
+__device__ __forceinline__ unsigned long long atomic_add_u64(uint64_t* p, uint64_t v) {
+  return atomicAdd(reinterpret_cast<unsigned long long*>(p),
+                   static_cast<unsigned long long>(v));
+}
+
+// ----------------------------------------------------------------------------
+// (a) segmented reduce
+// ----------------------------------------------------------------------------
+
+// Zero the outputs; for every wave range x*RED_RANGE record the node owning it.
+__global__ void reduce_mark_kernel(int64_t n_nodes, int64_t n_cont,
+                                   const int64_t* __restrict__ ptr,
+                                   int64_t* __restrict__ wave_node, uint64_t* __restrict__ o0,
+                                   uint64_t* __restrict__ o1, uint64_t* __restrict__ o2,
+                                   uint64_t* __restrict__ o3) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n_nodes; j += stride) {
+    o0[j] = 0;
+    o1[j] = 0;
+    if (o2) o2[j] = 0;
+    if (o3) o3[j] = 0;
+    int64_t b = ptr[j], e = ptr[j + 1];
+    b = b < 0 ? 0 : b;
+    e = e > n_cont ? n_cont : e;
+    if (e > b) {
+      for (int64_t x = (b + RED_RANGE - 1) / RED_RANGE * RED_RANGE; x < e; x += RED_RANGE)
+        wave_node[x / RED_RANGE] = j;
+    }
+  }
+}
+
+template <int NA>
+__device__ __forceinline__ void load_pairs(const uint64_t* const* in, int64_t p, int64_t n_cont,
+                                           uint64_t (&a)[NA], uint64_t (&b)[NA]) {
+  if (p + 1 < n_cont) {
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const ulonglong2 x = reinterpret_cast<const ulonglong2*>(in[k])[p >> 1];
+      a[k] = x.x;
+      b[k] = x.y;
+    }
+  } else if (p < n_cont) {
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      a[k] = in[k][p];
+      b[k] = 0;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      a[k] = 0;
+      b[k] = 0;
+    }
+  }
+}
+
+// One wavefront walks a contiguous range of RED_RANGE containers in 128-container
+// tiles (2 per lane, 16-B coalesced SoA loads, next tile prefetched).  Per tile:
+//   1. the nodes starting inside the tile are found from a coalesced read of the
+//      next 64 CSR offsets and written as head marks into a per-wave LDS strip;
+//   2. a wave-level segmented inclusive scan (shuffles) sums each node's run;
+//   3. the lane holding a run's last container stores the node's sum — a plain
+//      store when the run started inside this wave's range, an atomic add only
+//      for the (at most two) runs crossing the range boundaries.
+// Empty nodes are never visited (zeroed by reduce_mark_kernel).
+template <int NA>
+__global__ __launch_bounds__(256) void reduce_kernel(
+    int64_t n_nodes, int64_t n_cont, const int64_t* __restrict__ ptr,
+    const uint64_t* __restrict__ in0, const uint64_t* __restrict__ in1,
+    const uint64_t* __restrict__ in2, const uint64_t* __restrict__ in3,
+    const int64_t* __restrict__ wave_node, uint64_t* __restrict__ out0,
+    uint64_t* __restrict__ out1, uint64_t* __restrict__ out2, uint64_t* __restrict__ out3) {
+  __shared__ int32_t heads_s[RED_WAVES_PER_BLOCK][RED_TILE + 4];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t w = (int64_t)blockIdx.x * RED_WAVES_PER_BLOCK + wv;
+  const int64_t wb = w * RED_RANGE;
+  if (wb >= n_cont) return;  // wave-uniform; no block-level barrier in this kernel
+  const int64_t we = wb + RED_RANGE < n_cont ? wb + RED_RANGE : n_cont;
+  int32_t* heads = heads_s[wv];
+  const uint64_t* in[4] = {in0, in1, in2, in3};
+  uint64_t* out[4] = {out0, out1, out2, out3};
+
+  const int64_t node0 = wave_node[w];
+  const bool first_open = ptr[node0] < wb;  // node0's run began in an earlier range
+  int64_t cur = node0;                      // node owning the current tile's first item
+  uint64_t carry[NA];
+#pragma unroll
+  for (int k = 0; k < NA; ++k) carry[k] = 0;
+
+  uint64_t na[NA], nb[NA];
+  load_pairs<NA>(in, wb + 2 * lane, n_cont, na, nb);
+
+  for (int64_t base = wb; base < we; base += RED_TILE) {
+    uint64_t a[NA], b[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      a[k] = na[k];
+      b[k] = nb[k];
+    }
+    if (base + RED_TILE < we) load_pairs<NA>(in, base + RED_TILE + 2 * lane, n_cont, na, nb);
+
+    // --- 1. head marks --------------------------------------------------------
+    heads[2 * lane] = -1;
+    heads[2 * lane + 1] = -1;
+    if (lane == 0) heads[RED_TILE] = -1;
+    const int64_t X = base + RED_TILE;
+    int64_t cnt = 0;  // nodes j > cur with ptr[j] <= X  ->  next tile's cur = cur + cnt
+    for (int64_t r = 0;; r += 64) {
+      const int64_t j = cur + 1 + r + lane;
+      const int64_t sj = ptr[j < n_nodes ? j : n_nodes];
+      int64_t sj1 = __shfl_down(sj, 1);
+      if (lane == 63) sj1 = ptr[j + 1 < n_nodes ? j + 1 : n_nodes];
+      const bool in_range = (j < n_nodes) && (sj <= X);
+      if (in_range && sj1 > sj && sj > base && sj < n_cont)
+        heads[sj - base] = (int32_t)(j - cur);
+      const unsigned long long bal = __ballot(in_range);
+      cnt += __popcll(bal);
+      if (!((bal >> 63) & 1ull)) break;
+    }
+    if (lane == 0 && n_cont > base && n_cont <= X) heads[n_cont - base] = HEAD_END;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+
+    const int32_t hA = heads[2 * lane], hB = heads[2 * lane + 1], hC = heads[2 * lane + 2];
+    const bool fA = hA >= 0, fB = hB >= 0, fC = hC >= 0;
+
+    // node of each item, relative to cur: running max of head ids
+    int32_t im = hA > hB ? hA : hB;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t u = __shfl_up(im, d);
+      if (lane >= d) im = im > u ? im : u;
+    }
+    int32_t em = __shfl_up(im, 1);
+    if (lane == 0 || em < 0) em = 0;
+    const int32_t relA = em > hA ? em : hA;
+    const int32_t relB = relA > hB ? relA : hB;
+
+    // --- 2. segmented inclusive scan of the lane pair sums ---------------------
+    bool f = fA || fB;
+    uint64_t v[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) v[k] = fB ? b[k] : a[k] + b[k];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int fu = __shfl_up((int)f, d);
+#pragma unroll
+      for (int k = 0; k < NA; ++k) {
+        const uint64_t u = __shfl_up(v[k], d);
+        if (lane >= d && !f) v[k] += u;
+      }
+      if (lane >= d) f = f || (fu != 0);
+    }
+#pragma unroll
+    for (int k = 0; k < NA; ++k)
+      if (!f) v[k] += carry[k];
+
+    // --- 3. emit node sums at run ends ---------------------------------------
+    const int64_t pA = base + 2 * lane;
+    const bool endA = fB && pA < n_cont;      // run containing A ends at A
+    const bool endB = fC && pA + 1 < n_cont;  // run containing B ends at B
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      uint64_t e = __shfl_up(v[k], 1);
+      if (lane == 0) e = carry[k];
+      if (endA) {
+        const int64_t nd = cur + relA;
+        const uint64_t tot = fA ? a[k] : e + a[k];
+        if (nd < n_nodes) {
+          if (nd == node0 && first_open) atomic_add_u64(&out[k][nd], tot);
+          else out[k][nd] = tot;
+        }
+      }
+      if (endB) {
+        const int64_t nd = cur + relB;
+        if (nd < n_nodes) {
+          if (nd == node0 && first_open) atomic_add_u64(&out[k][nd], v[k]);
+          else out[k][nd] = v[k];
+        }
+      }
+    }
+    const bool last_end = (__ballot(fC) >> 63) & 1ull;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) carry[k] = last_end ? 0 : __shfl(v[k], 63);
+    cur += cnt;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  // the run open at the end of the range continues into the next wave's range
+  if (we < n_cont && lane == 0 && cur < n_nodes) {
+#pragma unroll
+    for (int k = 0; k < NA; ++k)
+      if (carry[k] != 0) atomic_add_u64(&out[k][cur], carry[k]);
+  }
+}
+
+// ----------------------------------------------------------------------------
+// (b) fit
+// ----------------------------------------------------------------------------
+
+// Fast-path bounds (see DESIGN.md "fit kernel: exactness argument").
+constexpr uint64_t FAST_FC_MAX = 1ull << 31;    // free CPU < 2^31
+constexpr int64_t FAST_FM_MAX = 1ll << 53;      // 0 <= free mem < 2^53
+constexpr int64_t FAST_P_MAX = 1ll << 16;       // allocatable pods <= 2^16
+constexpr int64_t FAST_P_MIN = -(1ll << 20);
+constexpr int64_t FAST_CL_ABS = 1ll << 20;      // |allocPods - podCount| <= 2^20
+constexpr uint64_t FAST_C_MAX = 1ull << 23;     // 1 <= spec cpu < 2^23
+constexpr int64_t FAST_M_MAX = 1ll << 37;       // 1 <= spec mem < 2^37
+
+__device__ __forceinline__ bool spec_is_normal(uint64_t c, int64_t m) {
+  return c >= 1 && c < FAST_C_MAX && m >= 1 && m < FAST_M_MAX;
+}
+
+__global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_cpu,
+                                 const int64_t* __restrict__ alloc_mem,
+                                 const int64_t* __restrict__ alloc_pods,
+                                 const int64_t* __restrict__ pod_count,
+                                 const uint64_t* __restrict__ used_cpu,
+                                 const int64_t* __restrict__ used_mem,
+                                 FitNode* __restrict__ fast, SlowNode* __restrict__ slow) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t ac = alloc_cpu[i], uc = used_cpu[i];
+    const int64_t am = alloc_mem[i], um = used_mem[i];
+    const int64_t P = alloc_pods[i], pc = pod_count[i];
+    const uint64_t fc = ac > uc ? ac - uc : 0;                                    // CC:119-123
+    const int64_t fm = am > um ? (int64_t)((uint64_t)am - (uint64_t)um) : 0;     // CC:125-129
+    const int64_t cl = (int64_t)((uint64_t)P - (uint64_t)pc);                    // CC:135
+    const bool ok = fc < FAST_FC_MAX && fm >= 0 && fm < FAST_FM_MAX && P >= FAST_P_MIN &&
+                    P <= FAST_P_MAX && cl >= -FAST_CL_ABS && cl <= FAST_CL_ABS;
+    FitNode f;
+    f.fm_d = ok ? (double)fm : 0.0;
+    f.fc_f = (float)fc;
+    f.fm_f = (float)fm;
+    f.fc_i = ok ? (int32_t)fc : -1;
+    f.P_f = ok ? (float)P : 0.f;
+    f.P_i = ok ? (int32_t)P : 0;
+    f.cl_i = ok ? (int32_t)cl : 0;
+    fast[i] = f;
+    SlowNode s;
+    s.fc = fc;
+    s.fm = fm;
+    s.P = P;
+    s.cl = cl;
+    slow[i] = s;
+  }
+}
+
+// Single-workgroup stable partition of the specs: fast-path specs first.
+__global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64_t* __restrict__ c_in,
+                                                         const int64_t* __restrict__ m_in,
+                                                         SpecPrep sp) {
+  __shared__ int wn[16], wa[16], on[16], oa[16];
+  __shared__ int64_t tot_n_s, run_n_s, run_a_s;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int64_t local = 0;
+  for (int64_t i = tid; i < S; i += 1024) local += spec_is_normal(c_in[i], m_in[i]) ? 1 : 0;
+  for (int d = 32; d >= 1; d >>= 1) local += __shfl_xor(local, d);
+  if (lane == 0) wn[wv] = (int)local;
+  if (tid == 0) { run_n_s = 0; run_a_s = 0; }
+  __syncthreads();
+  if (tid == 0) {
+    int64_t t = 0;
+    for (int k = 0; k < 16; ++k) t += wn[k];
+    tot_n_s = t;
+  }
+  __syncthreads();
+  const int64_t tot_n = tot_n_s;
+  for (int64_t base = 0; base < S; base += 1024) {
+    const int64_t i = base + tid;
+    const bool valid = i < S;
+    const uint64_t c = valid ? c_in[i] : 0;
+    const int64_t m = valid ? m_in[i] : 0;
+    const bool nm = valid && spec_is_normal(c, m);
+    const bool ab = valid && !nm;
+    const unsigned long long bn = __ballot(nm), ba = __ballot(ab);
+    if (lane == 0) { wn[wv] = __popcll(bn); wa[wv] = __popcll(ba); }
+    __syncthreads();
+    if (tid == 0) {
+      int sn = 0, sa = 0;
+      for (int k = 0; k < 16; ++k) { on[k] = sn; oa[k] = sa; sn += wn[k]; sa += wa[k]; }
+    }
+    __syncthreads();
+    if (valid) {
+      const int64_t pos = nm ? run_n_s + on[wv] + __popcll(bn & lt)
+                             : tot_n + run_a_s + oa[wv] + __popcll(ba & lt);
+      sp.c[pos] = c;
+      sp.m[pos] = m;
+      sp.md[pos] = (double)m;
+      sp.rc[pos] = nm ? 1.0f / (float)c : 0.f;
+      sp.rm[pos] = nm ? 1.0f / (float)m : 0.f;
+      sp.perm[pos] = (int32_t)i;
+      sp.normal[pos] = nm ? 1 : 0;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int sn = 0, sa = 0;
+      for (int k = 0; k < 16; ++k) { sn += wn[k]; sa += wa[k]; }
+      run_n_s += sn;
+      run_a_s += sa;
+    }
+    __syncthreads();
+  }
+}
+
+// Lane = spec (its request, reciprocals and running total live in VGPRs); the node
+// stream is wave-uniform, so each 32-B FitNode arrives by one scalar load and feeds
+// the VALU as SGPR operands.  No cross-lane reduction until the block's end (one
+// 64-bit atomic add per spec per block).
+//
+// Fast path per (node, spec), exact: t = min(qc, qm, P) from an f32
+// quotient estimate k (|k - t| <= 1), corrected by the sign of the exact remainders
+//   rcpu = fc - k*c   (i32, v_mul_i32_i24: |k*c| < 2^31 is checked per node)
+//   rmem = fm - k*m   (f64 fma: every operand and the result are integers < 2^53)
+// then contribution = t >= P ? P - podCount : t   (CC:133-136).
+__global__ __launch_bounds__(256) void fit_kernel(
+    int64_t n_nodes, int64_t nodes_per_block, const FitNode* __restrict__ fast,
+    const SlowNode* __restrict__ slow, int64_t S, const uint64_t* __restrict__ sc,
+    const int64_t* __restrict__ sm, const double* __restrict__ smd,
+    const float* __restrict__ src, const float* __restrict__ srm,
+    const int32_t* __restrict__ snormal, int64_t* __restrict__ partial,
+    unsigned long long* __restrict__ counters) {
+  const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool active = s < S;
+  const uint64_t c = active ? sc[s] : 1;
+  const int64_t m = active ? sm[s] : 1;
+  const double md = active ? smd[s] : 1.0;
+  const float rc = active ? src[s] : 1.f;
+  const float rm = active ? srm[s] : 1.f;
+  const bool normal = active ? (snormal[s] != 0) : true;
+  const bool wave_fast = __all(normal);
+  uint32_t cm = normal ? (uint32_t)c : 0u;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t o = __shfl_xor(cm, d);
+    cm = cm > o ? cm : o;
+  }
+  const uint32_t cmax = __builtin_amdgcn_readfirstlane(cm);
+  // node fast iff P * cmax < 2^31 (so k*c fits i32): P <= lim_P
+  const int32_t lim_P = wave_fast ? (int32_t)(0x7fffffffu / (cmax > 0 ? cmax : 1u)) : INT32_MIN;
+  const int32_t c32 = (int32_t)(uint32_t)c;
+  const int32_t negc = -c32;
+
+  const int64_t n0 = (int64_t)blockIdx.y * nodes_per_block;
+  const int64_t n1 = n0 + nodes_per_block < n_nodes ? n0 + nodes_per_block : n_nodes;
+  uint64_t acc = 0;
+  uint64_t errs = 0;
+  uint32_t slow_iters = 0;
+
+  auto eval_fast = [&](const FitNode& nd) -> int32_t {
+    const float e = fmaxf(fminf(fminf(nd.fc_f * rc, nd.fm_f * rm), nd.P_f), 0.f);
+    const int32_t k = (int32_t)e;
+    const int32_t rcpu = __mul24(k, negc) + nd.fc_i;
+    const double rmem = fma(-(double)k, md, nd.fm_d);
+    const int32_t down = (rcpu < 0) | (rmem < 0.0);
+    const int32_t up = (rcpu >= c32) & (rmem >= md) & (k < nd.P_i);
+    const int32_t t = k - down + up;
+    return (t >= nd.P_i) ? nd.cl_i : t;
+  };
+  // exact Go semantics, 64-bit (CC:119-136)
+  auto eval_slow = [&](int64_t i) {
+    ++slow_iters;
+    const SlowNode sn = slow[i];
+    int64_t qc = 0, qm = 0;
+    bool z = false;
+    if (sn.fc != 0) {
+      if (c == 0) z = true;
+      else qc = (int64_t)(sn.fc / c);
+    }
+    if (sn.fm != 0) {
+      if (m == 0) z = true;
+      else if (m == -1) qm = (int64_t)(0ull - (uint64_t)sn.fm);
+      else qm = sn.fm / m;
+    }
+    int64_t q = qc <= qm ? qc : qm;
+    if (q >= sn.P) q = sn.cl;
+    if (z) ++errs;
+    else acc += (uint64_t)q;
+  };
+  auto is_fast = [&](const FitNode& nd) { return nd.fc_i >= 0 && nd.P_i <= lim_P; };
+
+  for (int64_t cb = n0; cb < n1; cb += 1024) {
+    const int64_t ce = cb + 1024 < n1 ? cb + 1024 : n1;
+    int32_t acc32 = 0;  // |contribution| <= 2^20 on the fast path: 1024 of them fit
+    int64_t i = cb;
+    // 4 nodes (128 B of scalar loads) per uniform check
+    for (; i + 4 <= ce; i += 4) {
+      const FitNode a0 = fast[i], a1 = fast[i + 1], a2 = fast[i + 2], a3 = fast[i + 3];
+      if (is_fast(a0) && is_fast(a1) && is_fast(a2) && is_fast(a3)) {
+        acc32 += eval_fast(a0);
+        acc32 += eval_fast(a1);
+        acc32 += eval_fast(a2);
+        acc32 += eval_fast(a3);
+      } else {
+        if (is_fast(a0)) acc32 += eval_fast(a0); else eval_slow(i);
+        if (is_fast(a1)) acc32 += eval_fast(a1); else eval_slow(i + 1);
+        if (is_fast(a2)) acc32 += eval_fast(a2); else eval_slow(i + 2);
+        if (is_fast(a3)) acc32 += eval_fast(a3); else eval_slow(i + 3);
+      }
+    }
+    for (; i < ce; ++i) {
+      const FitNode a0 = fast[i];
+      if (is_fast(a0)) acc32 += eval_fast(a0);
+      else eval_slow(i);
+    }
+    acc += (uint64_t)(int64_t)acc32;
+  }
+  if (active) {
+    atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[s]), acc);
+    if (errs) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[S + s]), errs);
+  }
+  const unsigned long long act = __ballot(active);
+  if (slow_iters && (threadIdx.x & 63) == 0)
+    atomicAdd(counters, (unsigned long long)slow_iters * (unsigned long long)__popcll(act));
+}
+
+__global__ void fit_finalize_kernel(int64_t S, const int64_t* __restrict__ partial,
+                                    const int32_t* __restrict__ perm, int64_t* __restrict__ totals,
+                                    int32_t* __restrict__ spec_err) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S) return;
+  const int32_t dst = perm[i];
+  const bool err = partial[S + i] != 0;
+  totals[dst] = err ? 0 : partial[i];
+  spec_err[dst] = err ? 1 : 0;
+}
+
+inline unsigned grid_for(int64_t n, int block, int64_t cap) {
+  int64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+}  // namespace
+
+hipError_t launch_reduce_mark(int64_t n_nodes, int64_t n_containers, const int64_t* node_ptr,
+                              int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem,
+                              uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s) {
+  if (n_nodes <= 0) return hipSuccess;
+  hipLaunchKernelGGL(reduce_mark_kernel, dim3(grid_for(n_nodes, 256, 8192)), dim3(256), 0, s,
+                     n_nodes, n_containers, node_ptr, wave_node, used_cpu,
+                     reinterpret_cast<uint64_t*>(used_mem), lim_cpu,
+                     reinterpret_cast<uint64_t*>(lim_mem));
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce(int64_t n_nodes, int64_t n_containers, const int64_t* node_ptr,
+                         const uint64_t* cpu_req, const int64_t* mem_req,
+                         const uint64_t* cpu_lim, const int64_t* mem_lim,
+                         const int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem,
+                         uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s) {
+  if (n_nodes <= 0 || n_containers <= 0) return hipSuccess;
+  const int64_t waves = reduce_n_waves(n_containers);
+  const unsigned blocks = (unsigned)((waves + RED_WAVES_PER_BLOCK - 1) / RED_WAVES_PER_BLOCK);
+  const bool lim = cpu_lim && mem_lim && lim_cpu && lim_mem;
+  if (lim) {
+    hipLaunchKernelGGL(reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, n_nodes, n_containers,
+                       node_ptr, cpu_req, reinterpret_cast<const uint64_t*>(mem_req), cpu_lim,
+                       reinterpret_cast<const uint64_t*>(mem_lim), wave_node, used_cpu,
+                       reinterpret_cast<uint64_t*>(used_mem), lim_cpu,
+                       reinterpret_cast<uint64_t*>(lim_mem));
+  } else {
+    hipLaunchKernelGGL(reduce_kernel<2>, dim3(blocks), dim3(256), 0, s, n_nodes, n_containers,
+                       node_ptr, cpu_req, reinterpret_cast<const uint64_t*>(mem_req),
+                       (const uint64_t*)nullptr, (const uint64_t*)nullptr, wave_node, used_cpu,
+                       reinterpret_cast<uint64_t*>(used_mem), (uint64_t*)nullptr,
+                       (uint64_t*)nullptr);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
+                            const int64_t* alloc_mem, const int64_t* alloc_pods,
+                            const int64_t* pod_count, const uint64_t* used_cpu,
+                            const int64_t* used_mem, FitNode* fast, SlowNode* slow,
+                            hipStream_t s) {
+  if (n_nodes <= 0) return hipSuccess;
+  hipLaunchKernelGGL(node_prep_kernel, dim3(grid_for(n_nodes, 256, 8192)), dim3(256), 0, s,
+                     n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu, used_mem,
+                     fast, slow);
+  return hipGetLastError();
+}
+
+hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
+                            SpecPrep sp, hipStream_t s) {
+  if (n_specs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(spec_prep_kernel, dim3(1), dim3(1024), 0, s, n_specs, spec_cpu, spec_mem,
+                     sp);
+  return hipGetLastError();
+}
+
+hipError_t launch_fit(int64_t n_nodes, const FitNode* fast, const SlowNode* slow,
+                      int64_t n_specs, SpecPrep sp, int64_t* partial,
+                      unsigned long long* counters, hipStream_t s) {
+  if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
+  const int64_t gx = (n_specs + 255) / 256;
+  // aim for ~4096 workgroups (16 per CU) so the tail is short; >= 64 nodes each
+  int64_t gy_target = 4096 / gx;
+  if (gy_target < 1) gy_target = 1;
+  int64_t npb = (n_nodes + gy_target - 1) / gy_target;
+  if (npb < 64) npb = 64;
+  int64_t gy = (n_nodes + npb - 1) / npb;
+  if (gy > 65535) {
+    gy = 65535;
+    npb = (n_nodes + gy - 1) / gy;
+    gy = (n_nodes + npb - 1) / npb;
+  }
+  hipLaunchKernelGGL(fit_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, s, n_nodes, npb,
+                     fast, slow, n_specs, sp.c, sp.m, sp.md, sp.rc, sp.rm, sp.normal, partial,
+                     counters);
+  return hipGetLastError();
+}
+
+hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial, const int32_t* perm,
+                               int64_t* totals, int32_t* spec_err, hipStream_t s) {
+  if (n_specs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fit_finalize_kernel, dim3(grid_for(n_specs, 256, 1 << 30)), dim3(256), 0, s,
+                     n_specs, partial, perm, totals, spec_err);
+  return hipGetLastError();
+}
+
+}  // namespace kcc

@@ -1,0 +1,201 @@
+"""Python face of libkcc.so: the reference's hot-path operations, batched.
+
+Names follow the reference (AshutoshNirkhe/KubernetesClusterCapacity,
+src/KubeAPI/ClusterCapacity.go = CC):
+
+  get_pod_cpu_memory_requests_limits  <- getPodCPUMemoryRequestsLimits (CC:255-299)
+  total_possible_max_replicas          <- main's node loop (CC:101-140)
+
+Every call goes through the C-ABI into the gfx950 kernels; nothing is computed here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+
+
+class KccError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{_lib.ERROR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+def _arr(x, dtype) -> np.ndarray:
+    a = np.ascontiguousarray(x, dtype=dtype)
+    return a
+
+
+def _p(a) -> C.c_void_p | None:
+    if a is None:
+        return None
+    return C.c_void_p(a.ctypes.data) if a.size else C.c_void_p(a.ctypes.data or 16)
+
+
+def _dp(t) -> C.c_void_p | None:
+    """Device pointer of a torch tensor (or None)."""
+    if t is None:
+        return None
+    return C.c_void_p(t.data_ptr())
+
+
+@dataclass
+class RequestSums:
+    """Per-node sums, in the return order of getPodCPUMemoryRequestsLimits (CC:298)
+    but as arrays: (cpu limits, cpu requests, memory limits, memory requests)."""
+    cpu_limits: np.ndarray | None
+    cpu_requests: np.ndarray
+    memory_limits: np.ndarray | None
+    memory_requests: np.ndarray
+
+
+class CapacityEngine:
+    """One libkcc context (one device, or n_gpus devices with node sharding + RCCL)."""
+
+    def __init__(self, device: int = 0, n_gpus: int = 1):
+        self._lib = _lib.lib()
+        h = C.c_void_p()
+        rc = self._lib.kcc_create(C.byref(h), device, n_gpus)
+        if rc != 0:
+            raise KccError(rc, self._lib.kcc_create_error().decode())
+        self._h = h
+        self.device = device
+        self.n_gpus = n_gpus
+
+    # -- lifecycle -------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.kcc_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != 0:
+            raise KccError(rc, self._lib.kcc_last_error(self._h).decode())
+
+    def reserve(self, max_nodes: int, max_containers: int, max_specs: int):
+        self._check(self._lib.kcc_reserve(self._h, max_nodes, max_containers, max_specs))
+
+    # -- host-array API (synchronous) -----------------------------------------
+    def get_pod_cpu_memory_requests_limits(self, node_ptr, cpu_req, mem_req, cpu_lim=None,
+                                           mem_lim=None) -> RequestSums:
+        """CC:255-299 for every node at once: containers grouped per node (CSR)."""
+        node_ptr = _arr(node_ptr, np.int64)
+        n = node_ptr.size - 1
+        if n < 0:
+            raise ValueError("node_ptr must hold n_nodes + 1 offsets")
+        cpu_req = _arr(cpu_req, np.uint64)
+        mem_req = _arr(mem_req, np.int64)
+        lim = cpu_lim is not None or mem_lim is not None
+        if lim and (cpu_lim is None or mem_lim is None):
+            raise ValueError("pass both cpu_lim and mem_lim, or neither")
+        cpu_lim = _arr(cpu_lim, np.uint64) if lim else None
+        mem_lim = _arr(mem_lim, np.int64) if lim else None
+        nc = cpu_req.size
+        if mem_req.size != nc or (lim and (cpu_lim.size != nc or mem_lim.size != nc)):
+            raise ValueError("container arrays differ in length")
+        used_cpu = np.zeros(max(n, 0), np.uint64)
+        used_mem = np.zeros(max(n, 0), np.int64)
+        lim_cpu = np.zeros(max(n, 0), np.uint64) if lim else None
+        lim_mem = np.zeros(max(n, 0), np.int64) if lim else None
+        self._check(self._lib.kcc_reduce_requests(
+            self._h, n, nc, _p(node_ptr), _p(cpu_req), _p(mem_req), _p(cpu_lim), _p(mem_lim),
+            _p(used_cpu), _p(used_mem), _p(lim_cpu), _p(lim_mem)))
+        return RequestSums(lim_cpu, used_cpu, lim_mem, used_mem)
+
+    def total_possible_max_replicas(self, alloc_cpu, alloc_mem, alloc_pods, pod_count,
+                                    used_cpu, used_mem, spec_cpu, spec_mem):
+        """CC:101-140 for S specs.  Returns (totals int64[S], spec_err int32[S])."""
+        a = [_arr(alloc_cpu, np.uint64), _arr(alloc_mem, np.int64), _arr(alloc_pods, np.int64),
+             _arr(pod_count, np.int64), _arr(used_cpu, np.uint64), _arr(used_mem, np.int64)]
+        n = a[0].size
+        if any(x.size != n for x in a):
+            raise ValueError("node arrays differ in length")
+        sc, sm = _arr(spec_cpu, np.uint64), _arr(spec_mem, np.int64)
+        if sc.size != sm.size:
+            raise ValueError("spec arrays differ in length")
+        totals = np.zeros(sc.size, np.int64)
+        err = np.zeros(sc.size, np.int32)
+        self._check(self._lib.kcc_fit(self._h, n, *[_p(x) for x in a], sc.size, _p(sc), _p(sm),
+                                      _p(totals), _p(err)))
+        return totals, err
+
+    def capacity(self, node_ptr, cpu_req, mem_req, alloc_cpu, alloc_mem, alloc_pods, pod_count,
+                 spec_cpu, spec_mem):
+        """Fused (a)+(b) on host arrays.  Returns (totals, spec_err)."""
+        node_ptr = _arr(node_ptr, np.int64)
+        n = node_ptr.size - 1
+        cpu_req, mem_req = _arr(cpu_req, np.uint64), _arr(mem_req, np.int64)
+        a = [_arr(alloc_cpu, np.uint64), _arr(alloc_mem, np.int64), _arr(alloc_pods, np.int64),
+             _arr(pod_count, np.int64)]
+        if any(x.size != n for x in a):
+            raise ValueError("node arrays differ in length")
+        if cpu_req.size != mem_req.size:
+            raise ValueError("container arrays differ in length")
+        sc, sm = _arr(spec_cpu, np.uint64), _arr(spec_mem, np.int64)
+        totals = np.zeros(sc.size, np.int64)
+        err = np.zeros(sc.size, np.int32)
+        self._check(self._lib.kcc_capacity(
+            self._h, n, cpu_req.size, _p(node_ptr), _p(cpu_req), _p(mem_req),
+            *[_p(x) for x in a], sc.size, _p(sc), _p(sm), _p(totals), _p(err)))
+        return totals, err
+
+    def last_slow_fraction(self) -> float:
+        return float(self._lib.kcc_last_slow_fraction(self._h))
+
+    # -- device API (torch tensors, enqueue on `stream`) -------------------------
+    def reduce_requests_async(self, node_ptr, cpu_req, mem_req, used_cpu, used_mem,
+                              cpu_lim=None, mem_lim=None, lim_cpu=None, lim_mem=None,
+                              stream=None):
+        n = node_ptr.numel() - 1
+        self._check(self._lib.kcc_reduce_requests_async(
+            self._h, n, cpu_req.numel(), _dp(node_ptr), _dp(cpu_req), _dp(mem_req),
+            _dp(cpu_lim), _dp(mem_lim), _dp(used_cpu), _dp(used_mem), _dp(lim_cpu),
+            _dp(lim_mem), _stream(stream)))
+
+    def fit_prepare_async(self, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu, used_mem,
+                          spec_cpu, spec_mem, partial, stream=None):
+        self._check(self._lib.kcc_fit_prepare_async(
+            self._h, alloc_cpu.numel(), _dp(alloc_cpu), _dp(alloc_mem), _dp(alloc_pods),
+            _dp(pod_count), _dp(used_cpu), _dp(used_mem), spec_cpu.numel(), _dp(spec_cpu),
+            _dp(spec_mem), _dp(partial), _stream(stream)))
+
+    def fit_run_async(self, n_nodes, n_specs, partial, stream=None):
+        self._check(self._lib.kcc_fit_run_async(self._h, n_nodes, n_specs, _dp(partial),
+                                                _stream(stream)))
+
+    def fit_finalize_async(self, n_specs, partial, totals, spec_err, stream=None):
+        self._check(self._lib.kcc_fit_finalize_async(self._h, n_specs, _dp(partial),
+                                                     _dp(totals), _dp(spec_err),
+                                                     _stream(stream)))
+
+    def fit_slow_pairs(self):
+        a, b = C.c_int64(), C.c_int64()
+        self._check(self._lib.kcc_fit_slow_pairs(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+
+def _stream(stream):
+    if stream is None:
+        return None
+    h = getattr(stream, "cuda_stream", stream)
+    return C.c_void_p(int(h)) if h else None
+
+
+def verdict(totals, replicas):
+    """CC:144: `totalPossibleMaxReplicas >= replicas`, per spec."""
+    return np.asarray(totals, np.int64) >= np.asarray(replicas, np.int64)

@@ -1,0 +1,56 @@
+/*
+ * kcc_oracle.h — CPU restatement of the reference hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this.
+ * It is the checker, never the product: libkcc.so does not link or call it.
+ *
+ * Reference: AshutoshNirkhe/KubernetesClusterCapacity
+ *   CC = src/KubeAPI/ClusterCapacity.go, BF = src/bytefmt/bytes.go
+ * Parity pinning: the reference publishes no tests, fixtures or golden vectors
+ *  and Go is absent from this image, so this restatement is
+ * pinned by hand-derived known-answer tests (tests/test_oracle_kat.py, K1-K8 of
+ * SURVEY §8c) and cross-checked against an independent Python big-int
+ * restatement (oracle/pyoracle.py).
+ */
+#ifndef KCC_ORACLE_H
+#define KCC_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* CC:255-299 — per-node sums over a CSR container list (uint64/int64 wrap). */
+void kcco_reduce_requests(int64_t n_nodes, const int64_t* node_ptr,
+                          const uint64_t* cpu_req, const int64_t* mem_req,
+                          const uint64_t* cpu_lim, const int64_t* mem_lim,
+                          uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu,
+                          int64_t* lim_mem);
+
+/* CC:119-136 for one (node row, spec): the node's contribution maxReplicas.
+ * *div0 is set to 1 when Go would panic (integer divide by zero). */
+int64_t kcco_fit_one(uint64_t alloc_cpu, int64_t alloc_mem, int64_t alloc_pods,
+                     int64_t pod_count, uint64_t used_cpu, int64_t used_mem,
+                     uint64_t spec_cpu, int64_t spec_mem, int* div0);
+
+/* CC:101-140 for S specs; totals[s]=0 and spec_err[s]=1 where Go would panic.
+ * n_threads > 1 splits specs over pthreads (CPU baseline timing only). */
+void kcco_fit(int64_t n_nodes, const uint64_t* alloc_cpu, const int64_t* alloc_mem,
+              const int64_t* alloc_pods, const int64_t* pod_count,
+              const uint64_t* used_cpu, const int64_t* used_mem, int64_t n_specs,
+              const uint64_t* spec_cpu, const int64_t* spec_mem, int64_t* totals,
+              int32_t* spec_err, int n_threads);
+
+/* CC:159-164 */
+int64_t kcco_find_min(int64_t x, int64_t y);
+
+/* CC:301-319 — returns the value; *ok = 0 when Atoi failed (Go prints an error and
+ * returns 0). */
+uint64_t kcco_convert_cpu_to_milis(const char* s, int* ok);
+
+/* BF:75-105 — returns 0 on success, -1 on error (value then 0). */
+int kcco_to_bytes(const char* s, int64_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

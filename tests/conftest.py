@@ -1,0 +1,28 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and libkcc.so")
+
+
+def have_gpu() -> bool:
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def engine():
+    """One libkcc context for the whole GPU session (device 0)."""
+    from kubernetesclustercapacity_amd import CapacityEngine
+    eng = CapacityEngine(0, 1)
+    yield eng
+    eng.close()
