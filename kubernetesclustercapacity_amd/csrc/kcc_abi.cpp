@@ -41,7 +41,7 @@ struct Dev {
   int device = 0;
   hipStream_t stream = nullptr;
   // workspace of the *_async entry points
-  DevBuf wave_node, fast, slow, sc, sm, smd, src, srm, sperm, snormal, counters;
+  DevBuf wave_node, fast, slow, slow_list, sc, sm, smd, src, srm, sperm, snormal, counters;
   int64_t last_pairs = 0;  // node x spec pairs of the last fit_prepare on this device
   int64_t prep_nodes = -1, prep_specs = -1;  // sizes the workspace was last prepared for
   // staging of the host-array entry points
@@ -165,6 +165,7 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.wave_node, sizeof(int64_t) * (size_t)waves));
   KCC_HIP(ctx, ensure(dv.fast, sizeof(kcc::FitNode) * N));
   KCC_HIP(ctx, ensure(dv.slow, sizeof(kcc::SlowNode) * N));
+  KCC_HIP(ctx, ensure(dv.slow_list, sizeof(int64_t) * N));
   KCC_HIP(ctx, ensure(dv.sc, 8 * S));
   KCC_HIP(ctx, ensure(dv.sm, 8 * S));
   KCC_HIP(ctx, ensure(dv.smd, 8 * S));
@@ -195,11 +196,13 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
   if (n_specs == 0) return KCC_OK;
   KCC_HIP(ctx, hipMemsetAsync(partial, 0, sizeof(int64_t) * 2 * (size_t)n_specs, s));
   KCC_HIP(ctx, hipMemsetAsync(dv.counters.p, 0, 64, s));
-  KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv), s));
+  KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv),
+                                     as<unsigned long long>(dv.counters), s));
   if (n_nodes == 0) return KCC_OK;
   KCC_HIP(ctx, kcc::launch_node_prep(n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count,
                                      used_cpu, used_mem, as<kcc::FitNode>(dv.fast),
-                                     as<kcc::SlowNode>(dv.slow), s));
+                                     as<kcc::SlowNode>(dv.slow), as<int64_t>(dv.slow_list),
+                                     as<unsigned long long>(dv.counters), s));
   return KCC_OK;
 }
 
@@ -210,7 +213,7 @@ int fit_run_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_specs, int64_t
   if (n_nodes == 0 || n_specs == 0) return KCC_OK;
   if (!partial) return fail(ctx, KCC_EINVAL, "NULL partial");
   KCC_HIP(ctx, kcc::launch_fit(n_nodes, as<kcc::FitNode>(dv.fast), as<kcc::SlowNode>(dv.slow),
-                               n_specs, spec_prep_of(dv), partial,
+                               as<int64_t>(dv.slow_list), n_specs, spec_prep_of(dv), partial,
                                as<unsigned long long>(dv.counters), s));
   return KCC_OK;
 }
@@ -409,7 +412,7 @@ void kcc_destroy(kcc_ctx* ctx) {
   for (Dev& dv : ctx->devs) {
     (void)hipSetDevice(dv.device);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
-    DevBuf* bufs[] = {&dv.wave_node, &dv.fast,      &dv.slow,      &dv.sc,        &dv.sm,
+    DevBuf* bufs[] = {&dv.wave_node, &dv.slow_list, &dv.fast,      &dv.slow,      &dv.sc,        &dv.sm,
                       &dv.smd,       &dv.src,       &dv.srm,       &dv.sperm,     &dv.snormal,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
                       &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,

@@ -32,15 +32,17 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t n_containers, const int64_t* n
 
 // ---- (b) fit -----------------------------------------------------------------
 // Per-node record streamed by the fit kernel through the scalar cache (32 B, one
-// s_load_dwordx8).  fc_i < 0 marks a node that needs the exact 64-bit path.
+// s_load_dwordx8).
+// Rows outside the fast-path bounds hold a zero record (Pm1 = clm1 = -1, the rest 0:
+// contributes exactly 0) and are listed in slow_list for the exact path.
 struct __attribute__((aligned(32))) FitNode {
   double fm_d;   // free memory (bytes), exact in f64 on the fast path
   float fc_f;    // free CPU (millicores), rounded to f32 — quotient estimate only
   float fm_f;    // free memory, rounded to f32 — quotient estimate only
-  int32_t fc_i;  // free CPU, exact (fast path: 0 <= fc < 2^31), or -1
-  float P_f;     // allocatable pods as f32 (exact on the fast path)
-  int32_t P_i;   // allocatable pods
-  int32_t cl_i;  // clamp value allocatable pods - podCount (CC:135)
+  int32_t fc_i;  // free CPU, exact (fast path: 0 <= fc < 2^31)
+  float P_f;     // max(allocatable pods, 0) as f32 (exact on the fast path)
+  int32_t Pm1;   // allocatable pods - 1
+  int32_t clm1;  // clamp value (allocatable pods - podCount, CC:135) - 1
 };
 static_assert(sizeof(FitNode) == 32, "FitNode must be 32 B");
 
@@ -66,19 +68,22 @@ struct SpecPrep {
   int32_t* normal; // 1 if the spec satisfies the fast-path bounds
 };
 
+// counters (zeroed before spec_prep): [0] (node, spec) pairs on the exact path,
+// [1] rows in slow_list, [2] largest fast-path spec cpu request.
+// spec_prep writes counters[2]; node_prep reads it and appends to slow_list.
+hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
+                            const int64_t* spec_mem, SpecPrep sp, unsigned long long* counters,
+                            hipStream_t s);
+
 hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitNode* fast, SlowNode* slow,
-                            hipStream_t s);
+                            int64_t* slow_list, unsigned long long* counters, hipStream_t s);
 
-hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
-                            const int64_t* spec_mem, SpecPrep sp, hipStream_t s);
-
-// partial[0..S) += Σ_i q(i,s), partial[S..2S) += #div-by-zero rows (internal order);
-// counters[0] += (node, spec) pairs that took the exact path.
+// partial[0..S) += Σ_i q(i,s), partial[S..2S) += #div-by-zero rows (internal order).
 hipError_t launch_fit(int64_t n_nodes, const FitNode* fast, const SlowNode* slow,
-                      int64_t n_specs, SpecPrep sp, int64_t* partial,
+                      const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, hipStream_t s);
 
 hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial,

@@ -234,59 +234,94 @@ __device__ __forceinline__ bool spec_is_normal(uint64_t c, int64_t m) {
   return c >= 1 && c < FAST_C_MAX && m >= 1 && m < FAST_M_MAX;
 }
 
+// Per-node free capacity (CC:119-135 operands).  Rows that fit the fast-path
+// bounds get an exact FitNode; the others get a FitNode that contributes exactly 0
+// on the fast path and are appended to slow_list for the exact 64-bit path.
+// counters[2] holds the largest fast-path spec cpu request (from spec_prep), which
+// bounds P so that k*c fits in i32 for every spec.
 __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_cpu,
                                  const int64_t* __restrict__ alloc_mem,
                                  const int64_t* __restrict__ alloc_pods,
                                  const int64_t* __restrict__ pod_count,
                                  const uint64_t* __restrict__ used_cpu,
                                  const int64_t* __restrict__ used_mem,
-                                 FitNode* __restrict__ fast, SlowNode* __restrict__ slow) {
+                                 FitNode* __restrict__ fast, SlowNode* __restrict__ slow,
+                                 int64_t* __restrict__ slow_list,
+                                 unsigned long long* __restrict__ counters) {
+  const uint64_t cmax = counters[2];
+  int64_t p_cap = cmax ? (int64_t)(0x7fffffffull / cmax) : 0x7fffffffll;
+  if (p_cap > FAST_P_MAX) p_cap = FAST_P_MAX;
+  const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint64_t ac = alloc_cpu[i], uc = used_cpu[i];
-    const int64_t am = alloc_mem[i], um = used_mem[i];
-    const int64_t P = alloc_pods[i], pc = pod_count[i];
-    const uint64_t fc = ac > uc ? ac - uc : 0;                                    // CC:119-123
-    const int64_t fm = am > um ? (int64_t)((uint64_t)am - (uint64_t)um) : 0;     // CC:125-129
-    const int64_t cl = (int64_t)((uint64_t)P - (uint64_t)pc);                    // CC:135
-    const bool ok = fc < FAST_FC_MAX && fm >= 0 && fm < FAST_FM_MAX && P >= FAST_P_MIN &&
-                    P <= FAST_P_MAX && cl >= -FAST_CL_ABS && cl <= FAST_CL_ABS;
-    FitNode f;
-    f.fm_d = ok ? (double)fm : 0.0;
-    f.fc_f = (float)fc;
-    f.fm_f = (float)fm;
-    f.fc_i = ok ? (int32_t)fc : -1;
-    f.P_f = ok ? (float)P : 0.f;
-    f.P_i = ok ? (int32_t)P : 0;
-    f.cl_i = ok ? (int32_t)cl : 0;
-    fast[i] = f;
-    SlowNode s;
-    s.fc = fc;
-    s.fm = fm;
-    s.P = P;
-    s.cl = cl;
-    slow[i] = s;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i - lane < n; i += stride) {
+    const bool valid = i < n;
+    bool ok = false;
+    if (valid) {
+      const uint64_t ac = alloc_cpu[i], uc = used_cpu[i];
+      const int64_t am = alloc_mem[i], um = used_mem[i];
+      const int64_t P = alloc_pods[i], pc = pod_count[i];
+      const uint64_t fc = ac > uc ? ac - uc : 0;                                  // CC:119-123
+      const int64_t fm = am > um ? (int64_t)((uint64_t)am - (uint64_t)um) : 0;   // CC:125-129
+      const int64_t cl = (int64_t)((uint64_t)P - (uint64_t)pc);                  // CC:135
+      ok = fc < FAST_FC_MAX && fm >= 0 && fm < FAST_FM_MAX && P >= FAST_P_MIN &&
+           P <= p_cap && cl >= -FAST_CL_ABS && cl <= FAST_CL_ABS;
+      FitNode f;
+      f.fm_d = ok ? (double)fm : 0.0;
+      f.fc_f = ok ? (float)fc : 0.f;
+      f.fm_f = ok ? (float)fm : 0.f;
+      f.fc_i = ok ? (int32_t)fc : 0;
+      f.P_f = ok && P > 0 ? (float)P : 0.f;
+      f.Pm1 = ok ? (int32_t)P - 1 : -1;     // zero record: contributes exactly 0
+      f.clm1 = ok ? (int32_t)cl - 1 : -1;
+      fast[i] = f;
+      SlowNode sn;
+      sn.fc = fc;
+      sn.fm = fm;
+      sn.P = P;
+      sn.cl = cl;
+      slow[i] = sn;
+    }
+    const unsigned long long b = __ballot(valid && !ok);
+    if (b) {
+      unsigned long long base = 0;
+      if (lane == 0) base = atomicAdd(&counters[1], (unsigned long long)__popcll(b));
+      base = __shfl(base, 0);
+      if (valid && !ok) slow_list[base + __popcll(b & ((1ull << lane) - 1ull))] = i;
+    }
   }
 }
 
 // Single-workgroup stable partition of the specs: fast-path specs first.
 __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64_t* __restrict__ c_in,
                                                          const int64_t* __restrict__ m_in,
-                                                         SpecPrep sp) {
+                                                         SpecPrep sp,
+                                                         unsigned long long* __restrict__ counters) {
   __shared__ int wn[16], wa[16], on[16], oa[16];
+  __shared__ unsigned long long wmax[16];
   __shared__ int64_t tot_n_s, run_n_s, run_a_s;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const unsigned long long lt = (1ull << lane) - 1ull;
   int64_t local = 0;
-  for (int64_t i = tid; i < S; i += 1024) local += spec_is_normal(c_in[i], m_in[i]) ? 1 : 0;
-  for (int d = 32; d >= 1; d >>= 1) local += __shfl_xor(local, d);
-  if (lane == 0) wn[wv] = (int)local;
+  unsigned long long cmax = 0;  // largest fast-path cpu request (bounds P in node_prep)
+  for (int64_t i = tid; i < S; i += 1024) {
+    const bool nm = spec_is_normal(c_in[i], m_in[i]);
+    local += nm ? 1 : 0;
+    if (nm && c_in[i] > cmax) cmax = c_in[i];
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    local += __shfl_xor(local, d);
+    const unsigned long long o = __shfl_xor(cmax, d);
+    cmax = o > cmax ? o : cmax;
+  }
+  if (lane == 0) { wn[wv] = (int)local; wmax[wv] = cmax; }
   if (tid == 0) { run_n_s = 0; run_a_s = 0; }
   __syncthreads();
   if (tid == 0) {
     int64_t t = 0;
-    for (int k = 0; k < 16; ++k) t += wn[k];
+    unsigned long long mx = 0;
+    for (int k = 0; k < 16; ++k) { t += wn[k]; mx = wmax[k] > mx ? wmax[k] : mx; }
     tot_n_s = t;
+    counters[2] = mx;
   }
   __syncthreads();
   const int64_t tot_n = tot_n_s;
@@ -329,21 +364,49 @@ __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64
 
 // Lane = spec (its request, reciprocals and running total live in VGPRs); the node
 // stream is wave-uniform, so each 32-B FitNode arrives by one scalar load and feeds
-// the VALU as SGPR operands.  No cross-lane reduction until the block's end (one
-// 64-bit atomic add per spec per block).
+// the VALU as SGPR operands.  The main loop is branch-free: rows outside the fast
+// bounds carry a zero-contribution FitNode and are re-done exactly from slow_list.
+// No cross-lane reduction until the block's end (one 64-bit atomic per spec).
 //
-// Fast path per (node, spec), exact: t = min(qc, qm, P) from an f32
-// quotient estimate k (|k - t| <= 1), corrected by the sign of the exact remainders
-//   rcpu = fc - k*c   (i32, v_mul_i32_i24: |k*c| < 2^31 is checked per node)
-//   rmem = fm - k*m   (f64 fma: every operand and the result are integers < 2^53)
-// then contribution = t >= P ? P - podCount : t   (CC:133-136).
+// Fast path per (node, spec), exact (DESIGN.md "fit kernel: exactness argument"):
+//   k    = floor(min(fc*(1/c), fm*(1/m), P)) in f32, |k - t| <= 1, t = min(qc, qm, P)
+//   rcpu = fc - k*c      i32 (v_mad_i32_i24; k*c < 2^31 by node_prep's P cap)
+//   rmem = fm - k*m      f64 fma, exact (integers < 2^53); rmem2 = rmem - m
+//   t    = k - [rcpu < 0 or rmem < 0] + [rcpu >= c and rmem2 >= 0 and k < P]
+//          (sign bits of exact integers: no f64 compares)
+//   contribution = t >= P ? P - podCount : t                       (CC:133-136)
+// fit_fast returns contribution - 1 (P-1 and clamp-1 are stored per node); the
+// caller adds the count of evaluations back once per chunk.
+__device__ __forceinline__ int32_t fit_fast(const FitNode& nd, float rc, float rm, double md,
+                                            int32_t c32, int32_t negc) {
+  const float e = fminf(fminf(nd.fc_f * rc, nd.fm_f * rm), nd.P_f);  // >= 0
+  const int32_t k = (int32_t)e;
+  const int32_t rcpu = __mul24(k, negc) + nd.fc_i;
+  const double rmem = fma(-(double)k, md, nd.fm_d);
+  const double rmem2 = rmem - md;
+  const int32_t hi1 = (int32_t)(__double_as_longlong(rmem) >> 32);
+  const int32_t hi2 = (int32_t)(__double_as_longlong(rmem2) >> 32);
+  const int32_t dm = (rcpu | hi1) >> 31;                          // -1: k too large
+  const int32_t um = ((rcpu - c32) | hi2 | (nd.Pm1 - k)) >> 31;   // 0: k too small
+  const int32_t t1 = k + dm + um;                                 // t - 1
+  return (t1 >= nd.Pm1) ? nd.clm1 : t1;                           // contribution - 1
+}
+
+constexpr int FIT_UNROLL = 8;
+typedef int32_t i32x8 __attribute__((ext_vector_type(8)));
+
+// one s_load_dwordx8 per record (a vector load is never split into field loads)
+__device__ __forceinline__ FitNode load_node(const i32x8* __restrict__ q, int i) {
+  return __builtin_bit_cast(FitNode, q[i]);
+}
+
 __global__ __launch_bounds__(256) void fit_kernel(
     int64_t n_nodes, int64_t nodes_per_block, const FitNode* __restrict__ fast,
-    const SlowNode* __restrict__ slow, int64_t S, const uint64_t* __restrict__ sc,
-    const int64_t* __restrict__ sm, const double* __restrict__ smd,
-    const float* __restrict__ src, const float* __restrict__ srm,
-    const int32_t* __restrict__ snormal, int64_t* __restrict__ partial,
-    unsigned long long* __restrict__ counters) {
+    const SlowNode* __restrict__ slow, const int64_t* __restrict__ slow_list, int64_t S,
+    const uint64_t* __restrict__ sc, const int64_t* __restrict__ sm,
+    const double* __restrict__ smd, const float* __restrict__ src,
+    const float* __restrict__ srm, const int32_t* __restrict__ snormal,
+    int64_t* __restrict__ partial, unsigned long long* __restrict__ counters) {
   const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const bool active = s < S;
   const uint64_t c = active ? sc[s] : 1;
@@ -353,15 +416,6 @@ __global__ __launch_bounds__(256) void fit_kernel(
   const float rm = active ? srm[s] : 1.f;
   const bool normal = active ? (snormal[s] != 0) : true;
   const bool wave_fast = __all(normal);
-  uint32_t cm = normal ? (uint32_t)c : 0u;
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint32_t o = __shfl_xor(cm, d);
-    cm = cm > o ? cm : o;
-  }
-  const uint32_t cmax = __builtin_amdgcn_readfirstlane(cm);
-  // node fast iff P * cmax < 2^31 (so k*c fits i32): P <= lim_P
-  const int32_t lim_P = wave_fast ? (int32_t)(0x7fffffffu / (cmax > 0 ? cmax : 1u)) : INT32_MIN;
   const int32_t c32 = (int32_t)(uint32_t)c;
   const int32_t negc = -c32;
 
@@ -371,16 +425,6 @@ __global__ __launch_bounds__(256) void fit_kernel(
   uint64_t errs = 0;
   uint32_t slow_iters = 0;
 
-  auto eval_fast = [&](const FitNode& nd) -> int32_t {
-    const float e = fmaxf(fminf(fminf(nd.fc_f * rc, nd.fm_f * rm), nd.P_f), 0.f);
-    const int32_t k = (int32_t)e;
-    const int32_t rcpu = __mul24(k, negc) + nd.fc_i;
-    const double rmem = fma(-(double)k, md, nd.fm_d);
-    const int32_t down = (rcpu < 0) | (rmem < 0.0);
-    const int32_t up = (rcpu >= c32) & (rmem >= md) & (k < nd.P_i);
-    const int32_t t = k - down + up;
-    return (t >= nd.P_i) ? nd.cl_i : t;
-  };
   // exact Go semantics, 64-bit (CC:119-136)
   auto eval_slow = [&](int64_t i) {
     ++slow_iters;
@@ -401,34 +445,34 @@ __global__ __launch_bounds__(256) void fit_kernel(
     if (z) ++errs;
     else acc += (uint64_t)q;
   };
-  auto is_fast = [&](const FitNode& nd) { return nd.fc_i >= 0 && nd.P_i <= lim_P; };
 
-  for (int64_t cb = n0; cb < n1; cb += 1024) {
-    const int64_t ce = cb + 1024 < n1 ? cb + 1024 : n1;
-    int32_t acc32 = 0;  // |contribution| <= 2^20 on the fast path: 1024 of them fit
-    int64_t i = cb;
-    // 4 nodes (128 B of scalar loads) per uniform check
-    for (; i + 4 <= ce; i += 4) {
-      const FitNode a0 = fast[i], a1 = fast[i + 1], a2 = fast[i + 2], a3 = fast[i + 3];
-      if (is_fast(a0) && is_fast(a1) && is_fast(a2) && is_fast(a3)) {
-        acc32 += eval_fast(a0);
-        acc32 += eval_fast(a1);
-        acc32 += eval_fast(a2);
-        acc32 += eval_fast(a3);
-      } else {
-        if (is_fast(a0)) acc32 += eval_fast(a0); else eval_slow(i);
-        if (is_fast(a1)) acc32 += eval_fast(a1); else eval_slow(i + 1);
-        if (is_fast(a2)) acc32 += eval_fast(a2); else eval_slow(i + 2);
-        if (is_fast(a3)) acc32 += eval_fast(a3); else eval_slow(i + 3);
+  if (wave_fast) {
+    const i32x8* p = reinterpret_cast<const i32x8*>(fast + n0);
+    const int cnt = (int)(n1 - n0);
+    for (int cb = 0; cb < cnt; cb += 1024) {
+      const int ce = cb + 1024 < cnt ? cb + 1024 : cnt;
+      int32_t acc32 = 0;  // |contribution| <= 2^20: 1024 of them fit in i32
+      int i = cb;
+      for (; i + FIT_UNROLL <= ce; i += FIT_UNROLL) {
+        // index opaque to loop-strength reduction: one base per group, positive
+        // immediate offsets -> FIT_UNROLL s_load_dwordx8, no per-field address math
+        int io = i;
+        asm volatile("" : "+s"(io));
+        const i32x8* q = p + io;
+#pragma unroll
+        for (int u = 0; u < FIT_UNROLL; ++u)
+          acc32 += fit_fast(load_node(q, u), rc, rm, md, c32, negc);
       }
+      for (; i < ce; ++i) acc32 += fit_fast(load_node(p, i), rc, rm, md, c32, negc);
+      acc += (uint64_t)(int64_t)(acc32 + (ce - cb));
     }
-    for (; i < ce; ++i) {
-      const FitNode a0 = fast[i];
-      if (is_fast(a0)) acc32 += eval_fast(a0);
-      else eval_slow(i);
-    }
-    acc += (uint64_t)(int64_t)acc32;
+    // rows outside the fast bounds, shared out over the node-chunk blocks
+    const int64_t n_slow = (int64_t)counters[1];
+    for (int64_t j = blockIdx.y; j < n_slow; j += gridDim.y) eval_slow(slow_list[j]);
+  } else {
+    for (int64_t i = n0; i < n1; ++i) eval_slow(i);
   }
+
   if (active) {
     atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[s]), acc);
     if (errs) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[S + s]), errs);
@@ -498,24 +542,24 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitNode* fast, SlowNode* slow,
-                            hipStream_t s) {
+                            int64_t* slow_list, unsigned long long* counters, hipStream_t s) {
   if (n_nodes <= 0) return hipSuccess;
   hipLaunchKernelGGL(node_prep_kernel, dim3(grid_for(n_nodes, 256, 8192)), dim3(256), 0, s,
                      n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu, used_mem,
-                     fast, slow);
+                     fast, slow, slow_list, counters);
   return hipGetLastError();
 }
 
 hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
-                            SpecPrep sp, hipStream_t s) {
+                            SpecPrep sp, unsigned long long* counters, hipStream_t s) {
   if (n_specs <= 0) return hipSuccess;
   hipLaunchKernelGGL(spec_prep_kernel, dim3(1), dim3(1024), 0, s, n_specs, spec_cpu, spec_mem,
-                     sp);
+                     sp, counters);
   return hipGetLastError();
 }
 
 hipError_t launch_fit(int64_t n_nodes, const FitNode* fast, const SlowNode* slow,
-                      int64_t n_specs, SpecPrep sp, int64_t* partial,
+                      const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, hipStream_t s) {
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
   const int64_t gx = (n_specs + 255) / 256;
@@ -531,8 +575,8 @@ hipError_t launch_fit(int64_t n_nodes, const FitNode* fast, const SlowNode* slow
     gy = (n_nodes + npb - 1) / npb;
   }
   hipLaunchKernelGGL(fit_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, s, n_nodes, npb,
-                     fast, slow, n_specs, sp.c, sp.m, sp.md, sp.rc, sp.rm, sp.normal, partial,
-                     counters);
+                     fast, slow, slow_list, n_specs, sp.c, sp.m, sp.md, sp.rc, sp.rm, sp.normal,
+                     partial, counters);
   return hipGetLastError();
 }
 
