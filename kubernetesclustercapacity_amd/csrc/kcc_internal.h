@@ -8,9 +8,10 @@ namespace kcc {
 
 // ---- (a) segmented request reduce -------------------------------------------
 // One wavefront owns a contiguous range of RED_RANGE containers and walks it in
-// tiles of RED_TILE (2 containers per lane, one 16-B load per lane per array).
-constexpr int RED_TILE = 128;
-constexpr int RED_TILES_PER_WAVE = 32;
+// tiles of RED_TILE (RED_IPL containers per lane: two 16-B loads per lane per array).
+constexpr int RED_IPL = 4;
+constexpr int RED_TILE = 64 * RED_IPL;  // 256
+constexpr int RED_TILES_PER_WAVE = 16;
 constexpr int64_t RED_RANGE = (int64_t)RED_TILE * RED_TILES_PER_WAVE;  // 4096
 constexpr int RED_WAVES_PER_BLOCK = 4;
 

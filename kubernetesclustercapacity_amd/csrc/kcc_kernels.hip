@@ -51,36 +51,76 @@ __global__ void reduce_mark_kernel(int64_t n_nodes, int64_t n_cont,
   }
 }
 
-template <int NA>
-__device__ __forceinline__ void load_pairs(const uint64_t* const* in, int64_t p, int64_t n_cont,
-                                           uint64_t (&a)[NA], uint64_t (&b)[NA]) {
-  if (p + 1 < n_cont) {
-#pragma unroll
-    for (int k = 0; k < NA; ++k) {
-      const ulonglong2 x = reinterpret_cast<const ulonglong2*>(in[k])[p >> 1];
-      a[k] = x.x;
-      b[k] = x.y;
-    }
-  } else if (p < n_cont) {
-#pragma unroll
-    for (int k = 0; k < NA; ++k) {
-      a[k] = in[k][p];
-      b[k] = 0;
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < NA; ++k) {
-      a[k] = 0;
-      b[k] = 0;
-    }
-  }
+// DPP controls (gfx9 family): row_shr:n, row_bcast:15/31, wave_shl:1.
+constexpr int DPP_ROW_SHR = 0x110;
+constexpr int DPP_ROW_BCAST15 = 0x142;
+constexpr int DPP_ROW_BCAST31 = 0x143;
+constexpr int DPP_WAVE_SHL1 = 0x130;
+
+template <int CTRL, int ROW_MASK, int BANK_MASK>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)v, CTRL, ROW_MASK, BANK_MASK, false);
+  const uint32_t hi =
+      __builtin_amdgcn_update_dpp(0u, (uint32_t)(v >> 32), CTRL, ROW_MASK, BANK_MASK, false);
+  return ((uint64_t)hi << 32) | lo;
 }
 
-// One wavefront walks a contiguous range of RED_RANGE containers in 128-container
-// tiles (2 per lane, 16-B coalesced SoA loads, next tile prefetched).  Per tile:
-//   1. the nodes starting inside the tile are found from a coalesced read of the
-//      next 64 CSR offsets and written as head marks into a per-wave LDS strip;
-//   2. a wave-level segmented inclusive scan (shuffles) sums each node's run;
+// Inclusive prefix sum of a 64-bit value over the 64 lanes, wrapping mod 2^64 —
+// all VALU (DPP row shifts within 16-lane rows, then row broadcasts), no LDS.
+__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
+  v += dpp_u64<DPP_ROW_SHR + 1, 0xf, 0xf>(v);
+  v += dpp_u64<DPP_ROW_SHR + 2, 0xf, 0xf>(v);
+  v += dpp_u64<DPP_ROW_SHR + 4, 0xf, 0xf>(v);
+  v += dpp_u64<DPP_ROW_SHR + 8, 0xf, 0xf>(v);
+  v += dpp_u64<DPP_ROW_BCAST15, 0xa, 0xf>(v);
+  v += dpp_u64<DPP_ROW_BCAST31, 0xc, 0xf>(v);
+  return v;
+}
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// CSR offset of node j relative to the wave range start, clamped into int32.
+__device__ __forceinline__ int32_t rel_clamp(int64_t raw, int64_t wb) {
+  const int64_t v = raw - wb;
+  return (int32_t)(v < -1 ? -1 : (v > RED_RANGE + 2 ? RED_RANGE + 2 : v));
+}
+__device__ __forceinline__ int64_t ptr_at(const int64_t* __restrict__ ptr, int64_t j,
+                                          int64_t n_nodes) {
+  return ptr[j < n_nodes ? j : n_nodes];
+}
+__device__ __forceinline__ int32_t rel_ptr(const int64_t* __restrict__ ptr, int64_t j,
+                                           int64_t n_nodes, int64_t wb) {
+  return rel_clamp(ptr_at(ptr, j, n_nodes), wb);
+}
+
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+// RED_IPL (=4) consecutive 64-bit values of one array for this lane: two 16-B
+// range-checked buffer loads (outside the descriptor's range they read 0), so the
+// prefetch is branch-free and never waits where it is issued.
+__device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff, uint64_t (&x)[4]) {
+  const u64x2 lo = __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+  const u64x2 hi = __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16, 0, 0));
+  x[0] = lo.x;
+  x[1] = lo.y;
+  x[2] = hi.x;
+  x[3] = hi.y;
+}
+
+// One wavefront walks a contiguous range of RED_RANGE containers in tiles of
+// RED_TILE = 256 (4 per lane, coalesced SoA buffer loads, next tile prefetched).
+// Per tile:
+//   1. nodes starting inside the tile: the next 64 CSR offsets come from a sliding
+//      register window (3 x 64 offsets, the third prefetched), gathered with
+//      ds_bpermute, and are written as head marks into a per-wave LDS strip;
+//   2. per lane a 4-item running sum, then one DPP inclusive prefix sum (64-bit,
+//      all VALU) of the lane totals; a run's sum = prefix at its end - prefix
+//      before its head, the head prefix coming from the lane that holds the head
+//      (one ds_bpermute) or from the carry of the previous tile;
 //   3. the lane holding a run's last container stores the node's sum — a plain
 //      store when the run started inside this wave's range, an atomic add only
 //      for the (at most two) runs crossing the range boundaries.
@@ -92,16 +132,24 @@ __global__ __launch_bounds__(256) void reduce_kernel(
     const uint64_t* __restrict__ in2, const uint64_t* __restrict__ in3,
     const int64_t* __restrict__ wave_node, uint64_t* __restrict__ out0,
     uint64_t* __restrict__ out1, uint64_t* __restrict__ out2, uint64_t* __restrict__ out3) {
-  __shared__ int32_t heads_s[RED_WAVES_PER_BLOCK][RED_TILE + 4];
+  constexpr int HS = RED_TILE + 4;  // LDS strip per wave (positions 0..RED_TILE)
+  __shared__ __attribute__((aligned(16))) int32_t heads_s[RED_WAVES_PER_BLOCK * HS];
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const int64_t w = (int64_t)blockIdx.x * RED_WAVES_PER_BLOCK + wv;
-  const int64_t wb = w * RED_RANGE;
+  // wave index made provably uniform (T20: no waterfall loops around the buffer ops)
+  const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)(blockIdx.x * RED_WAVES_PER_BLOCK +
+                                                             (threadIdx.x >> 6)));
+  const int64_t wb = (int64_t)w * RED_RANGE;
   if (wb >= n_cont) return;  // wave-uniform; no block-level barrier in this kernel
-  const int64_t we = wb + RED_RANGE < n_cont ? wb + RED_RANGE : n_cont;
-  int32_t* heads = heads_s[wv];
+  const int32_t len = (int32_t)(n_cont - wb < RED_RANGE ? n_cont - wb : RED_RANGE);
+  int32_t* heads = heads_s + (threadIdx.x >> 6) * HS;
   const uint64_t* in[4] = {in0, in1, in2, in3};
   uint64_t* out[4] = {out0, out1, out2, out3};
+  __amdgpu_buffer_rsrc_t rs[NA];
+#pragma unroll
+  for (int k = 0; k < NA; ++k)  // whole 16-B pairs only: an odd last item is fixed up below
+    rs[k] = __builtin_amdgcn_make_buffer_rsrc((void*)(in[k] + wb), (short)0,
+                                              (int)((len & ~1) * 8), 0x00020000);
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
 
   const int64_t node0 = wave_node[w];
   const bool first_open = ptr[node0] < wb;  // node0's run began in an earlier range
@@ -110,107 +158,127 @@ __global__ __launch_bounds__(256) void reduce_kernel(
 #pragma unroll
   for (int k = 0; k < NA; ++k) carry[k] = 0;
 
-  uint64_t na[NA], nb[NA];
-  load_pairs<NA>(in, wb + 2 * lane, n_cont, na, nb);
+  // sliding window of CSR offsets: win0/win1 (relative, clamped) hold nodes
+  // [wbase, wbase+64), [wbase+64, +128); win2r (raw, still in flight) the next 64
+  int64_t wbase = cur + 1;
+  int32_t win0 = rel_ptr(ptr, wbase + lane, n_nodes, wb);
+  int32_t win1 = rel_ptr(ptr, wbase + 64 + lane, n_nodes, wb);
+  int64_t win2r = ptr_at(ptr, wbase + 128 + lane, n_nodes);
+  const int32_t end_rel = (int32_t)(n_cont - wb < RED_RANGE + 2 ? n_cont - wb : RED_RANGE + 2);
 
-  for (int64_t base = wb; base < we; base += RED_TILE) {
-    uint64_t a[NA], b[NA];
+  // Two statically named tile buffers (ping-pong): the loads for tile t+1 are
+  // issued unconditionally (range-checked) at the top of tile t, so they stay in
+  // flight across the whole tile and no register copy forces an early wait.
+  uint64_t xa[NA][4], xb[NA][4];
 #pragma unroll
-    for (int k = 0; k < NA; ++k) {
-      a[k] = na[k];
-      b[k] = nb[k];
+  for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 32, xa[k]);
+
+  auto tile = [&](uint64_t (&x)[NA][4], uint64_t (&nx)[NA][4], const int32_t tb) {
+#pragma unroll
+    for (int k = 0; k < NA; ++k) load_quad(rs[k], (tb + RED_TILE) * 8 + lane * 32, nx[k]);
+    const int32_t p0 = tb + 4 * lane;  // relative position of this lane's first item
+    if ((len & 1) && p0 <= len - 1 && len - 1 < p0 + 4) {  // odd tail: last item alone
+#pragma unroll
+      for (int k = 0; k < NA; ++k) {
+        const uint64_t v = in[k][wb + len - 1];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)  // static indices only (no scratch)
+          if (p0 + i == len - 1) x[k][i] = v;
+      }
     }
-    if (base + RED_TILE < we) load_pairs<NA>(in, base + RED_TILE + 2 * lane, n_cont, na, nb);
 
     // --- 1. head marks --------------------------------------------------------
-    heads[2 * lane] = -1;
-    heads[2 * lane + 1] = -1;
+    *reinterpret_cast<int4*>(&heads[4 * lane]) = make_int4(-1, -1, -1, -1);
     if (lane == 0) heads[RED_TILE] = -1;
-    const int64_t X = base + RED_TILE;
-    int64_t cnt = 0;  // nodes j > cur with ptr[j] <= X  ->  next tile's cur = cur + cnt
-    for (int64_t r = 0;; r += 64) {
-      const int64_t j = cur + 1 + r + lane;
-      const int64_t sj = ptr[j < n_nodes ? j : n_nodes];
-      int64_t sj1 = __shfl_down(sj, 1);
-      if (lane == 63) sj1 = ptr[j + 1 < n_nodes ? j + 1 : n_nodes];
-      const bool in_range = (j < n_nodes) && (sj <= X);
-      if (in_range && sj1 > sj && sj > base && sj < n_cont)
-        heads[sj - base] = (int32_t)(j - cur);
-      const unsigned long long bal = __ballot(in_range);
-      cnt += __popcll(bal);
-      if (!((bal >> 63) & 1ull)) break;
+    const int32_t X = tb + RED_TILE;
+    while (cur + 1 - wbase >= 64) {  // slide the window (rarely more than once)
+      win0 = win1;
+      win1 = rel_clamp(win2r, wb);
+      wbase += 64;
+      win2r = ptr_at(ptr, wbase + 128 + lane, n_nodes);
     }
-    if (lane == 0 && n_cont > base && n_cont <= X) heads[n_cont - base] = HEAD_END;
+    const int off = (int)(cur + 1 - wbase);  // 0..63
+    const int idx = off + lane;               // 0..126
+    const int32_t g0 = __shfl(win0, idx & 63), g1 = __shfl(win1, idx & 63);
+    const int32_t sj = idx < 64 ? g0 : g1;
+    int32_t sj1 = __builtin_amdgcn_update_dpp(0, sj, DPP_WAVE_SHL1, 0xf, 0xf, false);
+    const int32_t nxt = __shfl(win1, off);  // node cur+65
+    if (lane == 63) sj1 = nxt;
+    const int64_t j0 = cur + 1 + lane;
+    const bool in_range = (j0 < n_nodes) && (sj <= X);
+    if (in_range && sj1 > sj && sj > tb && sj < end_rel) heads[sj - tb] = (int32_t)(j0 - cur);
+    unsigned long long bal = __ballot(in_range);
+    int64_t cnt = __popcll(bal);
+    // more than 64 node starts in this tile (runs of tiny or empty nodes): direct loads
+    for (int64_t r = 64; (bal >> 63) & 1ull; r += 64) {
+      const int64_t j = cur + 1 + r + lane;
+      const int32_t s2 = rel_ptr(ptr, j, n_nodes, wb);
+      const int32_t s21 = rel_ptr(ptr, j + 1, n_nodes, wb);
+      const bool ir = (j < n_nodes) && (s2 <= X);
+      if (ir && s21 > s2 && s2 > tb && s2 < end_rel) heads[s2 - tb] = (int32_t)(j - cur);
+      bal = __ballot(ir);
+      cnt += __popcll(bal);
+    }
+    if (lane == 0 && end_rel > tb && end_rel <= X) heads[end_rel - tb] = HEAD_END;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 
-    const int32_t hA = heads[2 * lane], hB = heads[2 * lane + 1], hC = heads[2 * lane + 2];
-    const bool fA = hA >= 0, fB = hB >= 0, fC = hC >= 0;
+    const int4 h4 = *reinterpret_cast<const int4*>(&heads[4 * lane]);
+    const int32_t h[5] = {h4.x, h4.y, h4.z, h4.w, heads[4 * lane + 4]};
+    bool f[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) f[i] = h[i] >= 0;
+    const bool any = f[0] || f[1] || f[2] || f[3];
+    const unsigned long long hm = __ballot(any);
+    const unsigned long long before = hm & lt_mask;
+    const int L = before ? 63 - __clzll(before) : 0;  // last lane before me with a head
+    const int32_t lid = f[3] ? h[3] : f[2] ? h[2] : f[1] ? h[1] : h[0];
+    // every cross-lane read below runs on all 64 lanes, then selects
+    const int32_t got_id = __shfl(lid, L);
+    const int32_t prev_id = before ? got_id : 0;
+    const bool last_end = (__ballot(f[4]) >> 63) & 1ull;
 
-    // node of each item, relative to cur: running max of head ids
-    int32_t im = hA > hB ? hA : hB;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int32_t u = __shfl_up(im, d);
-      if (lane >= d) im = im > u ? im : u;
-    }
-    int32_t em = __shfl_up(im, 1);
-    if (lane == 0 || em < 0) em = 0;
-    const int32_t relA = em > hA ? em : hA;
-    const int32_t relB = relA > hB ? relA : hB;
-
-    // --- 2. segmented inclusive scan of the lane pair sums ---------------------
-    bool f = fA || fB;
-    uint64_t v[NA];
-#pragma unroll
-    for (int k = 0; k < NA; ++k) v[k] = fB ? b[k] : a[k] + b[k];
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int fu = __shfl_up((int)f, d);
-#pragma unroll
-      for (int k = 0; k < NA; ++k) {
-        const uint64_t u = __shfl_up(v[k], d);
-        if (lane >= d && !f) v[k] += u;
-      }
-      if (lane >= d) f = f || (fu != 0);
-    }
-#pragma unroll
-    for (int k = 0; k < NA; ++k)
-      if (!f) v[k] += carry[k];
-
-    // --- 3. emit node sums at run ends ---------------------------------------
-    const int64_t pA = base + 2 * lane;
-    const bool endA = fB && pA < n_cont;      // run containing A ends at A
-    const bool endB = fC && pA + 1 < n_cont;  // run containing B ends at B
+    // --- 2./3. prefix sums, run sums, emit ---------------------------------------
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
-      uint64_t e = __shfl_up(v[k], 1);
-      if (lane == 0) e = carry[k];
-      if (endA) {
-        const int64_t nd = cur + relA;
-        const uint64_t tot = fA ? a[k] : e + a[k];
-        if (nd < n_nodes) {
-          if (nd == node0 && first_open) atomic_add_u64(&out[k][nd], tot);
-          else out[k][nd] = tot;
-        }
-      }
-      if (endB) {
-        const int64_t nd = cur + relB;
-        if (nd < n_nodes) {
-          if (nd == node0 && first_open) atomic_add_u64(&out[k][nd], v[k]);
-          else out[k][nd] = v[k];
-        }
-      }
-    }
-    const bool last_end = (__ballot(fC) >> 63) & 1ull;
+      uint64_t q[4];  // running sums within the lane
+      q[0] = x[k][0];
 #pragma unroll
-    for (int k = 0; k < NA; ++k) carry[k] = last_end ? 0 : __shfl(v[k], 63);
+      for (int i = 1; i < 4; ++i) q[i] = q[i - 1] + x[k][i];
+      const uint64_t P = wave_incl_scan_u64(q[3]);
+      const uint64_t Pex = P - q[3];
+      const uint64_t lhp = Pex + (f[3] ? q[2] : f[2] ? q[1] : f[1] ? q[0] : 0ull);
+      const uint64_t got = shfl_u64(lhp, L);
+      uint64_t sp = before ? got : (0ull - carry[k]);  // prefix before the open run's head
+      int32_t cid = prev_id;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (f[i]) {
+          sp = Pex + (i ? q[i - 1] : 0ull);
+          cid = h[i];
+        }
+        if (f[i + 1] && p0 + i < len) {  // run ends at item i
+          const int64_t nd = cur + cid;
+          const uint64_t tot = Pex + q[i] - sp;
+          if (nd < n_nodes) {
+            if (nd == node0 && first_open) atomic_add_u64(&out[k][nd], tot);
+            else out[k][nd] = tot;
+          }
+        }
+      }
+      const uint64_t tail = shfl_u64(P - sp, 63);
+      carry[k] = last_end ? 0 : tail;
+    }
     cur += cnt;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+  };
+  for (int32_t tb = 0; tb < len; tb += 2 * RED_TILE) {
+    tile(xa, xb, tb);
+    if (tb + RED_TILE < len) tile(xb, xa, tb + RED_TILE);
   }
   // the run open at the end of the range continues into the next wave's range
-  if (we < n_cont && lane == 0 && cur < n_nodes) {
+  if (wb + len < n_cont && lane == 0 && cur < n_nodes) {
 #pragma unroll
     for (int k = 0; k < NA; ++k)
       if (carry[k] != 0) atomic_add_u64(&out[k][cur], carry[k]);
