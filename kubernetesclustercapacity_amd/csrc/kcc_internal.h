@@ -34,16 +34,16 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t n_containers, const int64_t* n
 // ---- (b) fit -----------------------------------------------------------------
 // Per-node record streamed by the fit kernel through the scalar cache (32 B, one
 // s_load_dwordx8).
-// Rows outside the fast-path bounds hold a zero record (Pm1 = clm1 = -1, the rest 0:
-// contributes exactly 0) and are listed in slow_list for the exact path.
+// Rows outside the fast-path bounds hold an all-zero record (contributes exactly 0)
+// and are listed in slow_list for the exact path.
 struct __attribute__((aligned(32))) FitNode {
   double fm_d;   // free memory (bytes), exact in f64 on the fast path
   float fc_f;    // free CPU (millicores), rounded to f32 — quotient estimate only
   float fm_f;    // free memory, rounded to f32 — quotient estimate only
   int32_t fc_i;  // free CPU, exact (fast path: 0 <= fc < 2^31)
   float P_f;     // max(allocatable pods, 0) as f32 (exact on the fast path)
-  int32_t Pm1;   // allocatable pods - 1
-  int32_t clm1;  // clamp value (allocatable pods - podCount, CC:135) - 1
+  int32_t P_i;   // allocatable pods
+  int32_t cl_i;  // clamp value allocatable pods - podCount (CC:135)
 };
 static_assert(sizeof(FitNode) == 32, "FitNode must be 32 B");
 
@@ -63,8 +63,8 @@ struct SpecPrep {
   uint64_t* c;     // cpu request (millicores)
   int64_t* m;      // memory request (bytes)
   double* md;      // m as f64
-  float* rc;       // 1/c (f32)
-  float* rm;       // 1/m (f32)
+  float* rc;       // (1 + 2^-20)/c (f32): biased up, see fit_fast
+  float* rm;       // (1 + 2^-20)/m (f32)
   int32_t* perm;   // internal index -> caller index
   int32_t* normal; // 1 if the spec satisfies the fast-path bounds
 };

@@ -297,6 +297,7 @@ constexpr int64_t FAST_P_MIN = -(1ll << 20);
 constexpr int64_t FAST_CL_ABS = 1ll << 20;      // |allocPods - podCount| <= 2^20
 constexpr uint64_t FAST_C_MAX = 1ull << 23;     // 1 <= spec cpu < 2^23
 constexpr int64_t FAST_M_MAX = 1ll << 37;       // 1 <= spec mem < 2^37
+constexpr double FIT_RECIP_BIAS = 1.0 + 0x1p-20;  // see fit_fast
 
 __device__ __forceinline__ bool spec_is_normal(uint64_t c, int64_t m) {
   return c >= 1 && c < FAST_C_MAX && m >= 1 && m < FAST_M_MAX;
@@ -333,14 +334,14 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
       const int64_t cl = (int64_t)((uint64_t)P - (uint64_t)pc);                  // CC:135
       ok = fc < FAST_FC_MAX && fm >= 0 && fm < FAST_FM_MAX && P >= FAST_P_MIN &&
            P <= p_cap && cl >= -FAST_CL_ABS && cl <= FAST_CL_ABS;
-      FitNode f;
+      FitNode f;  // rows off the fast path: all-zero record, contributes exactly 0
       f.fm_d = ok ? (double)fm : 0.0;
-      f.fc_f = ok ? (float)fc : 0.f;
-      f.fm_f = ok ? (float)fm : 0.f;
+      f.fc_f = ok ? (float)fc : 0.f;                  // one rounding (fc < 2^31)
+      f.fm_f = ok ? (float)(double)fm : 0.f;          // exact in f64, one rounding to f32
       f.fc_i = ok ? (int32_t)fc : 0;
       f.P_f = ok && P > 0 ? (float)P : 0.f;
-      f.Pm1 = ok ? (int32_t)P - 1 : -1;     // zero record: contributes exactly 0
-      f.clm1 = ok ? (int32_t)cl - 1 : -1;
+      f.P_i = ok ? (int32_t)P : 0;
+      f.cl_i = ok ? (int32_t)cl : 0;
       fast[i] = f;
       SlowNode sn;
       sn.fc = fc;
@@ -414,8 +415,10 @@ __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64
       sp.c[pos] = c;
       sp.m[pos] = m;
       sp.md[pos] = (double)m;
-      sp.rc[pos] = nm ? 1.0f / (float)c : 0.f;
-      sp.rm[pos] = nm ? 1.0f / (float)m : 0.f;
+      // reciprocals biased up by 2^-20 so the fit's quotient estimate never
+      // undershoots (f64 division, then one rounding to f32)
+      sp.rc[pos] = nm ? (float)(FIT_RECIP_BIAS / (double)c) : 0.f;
+      sp.rm[pos] = nm ? (float)(FIT_RECIP_BIAS / (double)m) : 0.f;
       sp.perm[pos] = (int32_t)i;
       sp.normal[pos] = nm ? 1 : 0;
     }
@@ -437,27 +440,26 @@ __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64
 // No cross-lane reduction until the block's end (one 64-bit atomic per spec).
 //
 // Fast path per (node, spec), exact (DESIGN.md "fit kernel: exactness argument"):
-//   k    = floor(min(fc*(1/c), fm*(1/m), P)) in f32, |k - t| <= 1, t = min(qc, qm, P)
-//   rcpu = fc - k*c      i32 (v_mad_i32_i24; k*c < 2^31 by node_prep's P cap)
-//   rmem = fm - k*m      f64 fma, exact (integers < 2^53); rmem2 = rmem - m
-//   t    = k - [rcpu < 0 or rmem < 0] + [rcpu >= c and rmem2 >= 0 and k < P]
-//          (sign bits of exact integers: no f64 compares)
+//   the spec reciprocals are biased up by 2^-20 (spec_prep), so the f32 estimate
+//   e = min(fc*rc, fm*rm, P) satisfies t <= e < t + 1 for t = min(qc, qm, P)
+//   (its relative error is below 4*2^-24, and t <= P <= 2^16): k = floor(e) is t
+//   or t + 1, never below.  One exact check fixes it:
+//     rcpu = fc - k*c      i32 (v_mad_i32_i24; k*c < 2^31 by node_prep's P cap)
+//     rmem = fm - k*m      f64 fma, exact (every value an integer < 2^53)
+//     t    = k - [rcpu < 0 or rmem < 0]          (sign bits: no compares)
 //   contribution = t >= P ? P - podCount : t                       (CC:133-136)
-// fit_fast returns contribution - 1 (P-1 and clamp-1 are stored per node); the
-// caller adds the count of evaluations back once per chunk.
-__device__ __forceinline__ int32_t fit_fast(const FitNode& nd, float rc, float rm, double md,
-                                            int32_t c32, int32_t negc) {
-  const float e = fminf(fminf(nd.fc_f * rc, nd.fm_f * rm), nd.P_f);  // >= 0
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int32_t fit_fast(const FitNode& nd, f32x2 rcm, double md,
+                                            int32_t negc) {
+  const f32x2 q = f32x2{nd.fc_f, nd.fm_f} * rcm;  // one v_pk_mul_f32
+  const float e = fminf(fminf(q.x, q.y), nd.P_f);  // t <= e < t + 1
   const int32_t k = (int32_t)e;
   const int32_t rcpu = __mul24(k, negc) + nd.fc_i;
   const double rmem = fma(-(double)k, md, nd.fm_d);
-  const double rmem2 = rmem - md;
-  const int32_t hi1 = (int32_t)(__double_as_longlong(rmem) >> 32);
-  const int32_t hi2 = (int32_t)(__double_as_longlong(rmem2) >> 32);
-  const int32_t dm = (rcpu | hi1) >> 31;                          // -1: k too large
-  const int32_t um = ((rcpu - c32) | hi2 | (nd.Pm1 - k)) >> 31;   // 0: k too small
-  const int32_t t1 = k + dm + um;                                 // t - 1
-  return (t1 >= nd.Pm1) ? nd.clm1 : t1;                           // contribution - 1
+  const int32_t hi = (int32_t)(__double_as_longlong(rmem) >> 32);
+  const int32_t t = k + ((rcpu | hi) >> 31);
+  return (t >= nd.P_i) ? nd.cl_i : t;
 }
 
 constexpr int FIT_UNROLL = 8;
@@ -484,8 +486,8 @@ __global__ __launch_bounds__(256) void fit_kernel(
   const float rm = active ? srm[s] : 1.f;
   const bool normal = active ? (snormal[s] != 0) : true;
   const bool wave_fast = __all(normal);
-  const int32_t c32 = (int32_t)(uint32_t)c;
-  const int32_t negc = -c32;
+  const int32_t negc = -(int32_t)(uint32_t)c;
+  const f32x2 rcm = {rc, rm};
 
   const int64_t n0 = (int64_t)blockIdx.y * nodes_per_block;
   const int64_t n1 = n0 + nodes_per_block < n_nodes ? n0 + nodes_per_block : n_nodes;
@@ -528,11 +530,10 @@ __global__ __launch_bounds__(256) void fit_kernel(
         asm volatile("" : "+s"(io));
         const i32x8* q = p + io;
 #pragma unroll
-        for (int u = 0; u < FIT_UNROLL; ++u)
-          acc32 += fit_fast(load_node(q, u), rc, rm, md, c32, negc);
+        for (int u = 0; u < FIT_UNROLL; ++u) acc32 += fit_fast(load_node(q, u), rcm, md, negc);
       }
-      for (; i < ce; ++i) acc32 += fit_fast(load_node(p, i), rc, rm, md, c32, negc);
-      acc += (uint64_t)(int64_t)(acc32 + (ce - cb));
+      for (; i < ce; ++i) acc32 += fit_fast(load_node(p, i), rcm, md, negc);
+      acc += (uint64_t)(int64_t)acc32;
     }
     // rows outside the fast bounds, shared out over the node-chunk blocks
     const int64_t n_slow = (int64_t)counters[1];

@@ -1,0 +1,78 @@
+"""Node sharding over ranks, world_size 2 on CPU with gloo.
+
+Each rank generates only its node range of the cluster (synth is shard-stable),
+computes its per-spec partial vector [sums | div-by-zero counts] (the oracle stands
+in for kcc_fit_partial_async here: no GPU in this suite), all-reduces it with
+shard.allreduce_partial and applies the finalize rule.  The result must equal the
+unsharded computation bit for bit — the same exchange bench.py runs over RCCL.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from kubernetesclustercapacity_amd import shard, synth
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _partial(c, sc, sm):
+    from oracle import coracle
+    uc, um, _, _ = coracle.reduce_requests(c.node_ptr, c.cpu_req, c.mem_req)
+    t, e = coracle.fit(c.alloc_cpu, c.alloc_mem, c.alloc_pods, c.pod_count, uc, um, sc, sm)
+    return np.concatenate([t, e.astype(np.int64)])
+
+
+def _finalize(partial, S):
+    err = partial[S:] != 0
+    return np.where(err, 0, partial[:S]), err.astype(np.int32)
+
+
+def _worker(rank, world, port, n, pods, S, adversarial, out):
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard.node_range(n, rank, world)
+    c = synth.make_cluster(n, pods, seed=77, node_lo=lo, node_hi=hi, adversarial=adversarial,
+                           chunk=256)
+    sc, sm = synth.make_specs(S, seed=77, adversarial=adversarial)
+    p = torch.from_numpy(_partial(c, sc, sm))
+    shard.allreduce_partial(p)
+    if rank == 0:
+        t, e = _finalize(p.numpy(), S)
+        np.save(out, np.concatenate([t, e.astype(np.int64)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("adversarial", [False, True])
+def test_two_rank_shards_equal_whole(tmp_path, adversarial):
+    n, pods, S, world = 3_001, 50_000, 40, 2
+    out = str(tmp_path / "r0.npy")
+    mp.spawn(_worker, args=(world, _free_port(), n, pods, S, adversarial, out), nprocs=world,
+             join=True)
+    got = np.load(out)
+    c = synth.make_cluster(n, pods, seed=77, adversarial=adversarial, chunk=256)
+    sc, sm = synth.make_specs(S, seed=77, adversarial=adversarial)
+    from oracle import coracle
+    uc, um, _, _ = coracle.reduce_requests(c.node_ptr, c.cpu_req, c.mem_req)
+    t, e = coracle.fit(c.alloc_cpu, c.alloc_mem, c.alloc_pods, c.pod_count, uc, um, sc, sm)
+    np.testing.assert_array_equal(got[:S], t)
+    np.testing.assert_array_equal(got[S:], e)
+
+
+def test_node_range_partitions_exactly():
+    for n in (0, 1, 7, 1_000_000, 5_000_003):
+        for world in (1, 2, 3, 4, 8):
+            b = shard.shard_bounds(n, world)
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+            sizes = [h - l for l, h in b]
+            assert max(sizes) - min(sizes) <= 1
