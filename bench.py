@@ -25,6 +25,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# VALU accounting of the fit kernel (DESIGN.md "Roofline accounting"):
+#  - VALU instructions per (node, 64-spec wavefront) on the fast path, counted in the
+#    kernel's ISA (pinned by tests/test_isa.py);
+#  - issue peak: one wave64 VALU instruction per SIMD per 4 cycles (PMC: every
+#    SQ_INSTS_VALU costs one SQ_ACTIVE_INST_VALU quad-cycle), 256 CUs x 4 SIMDs x 2.4 GHz.
+FIT_VALU_PER_NODE_WAVE = 12.625
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions / s
 METRIC = "node×spec fit evals/sec at 1M nodes × 4K specs; % of HBM roofline"
 
 
@@ -133,6 +140,7 @@ def main():
     fit_bytes = n * 32 + S * 16 + S * 8            # FitNode records + specs in, totals out
     red_bytes = C * 16 + (n + 1) * 8 + n * 16      # requests + CSR offsets in, sums out
     fit_gbs = fit_bytes / (fit_ms * 1e-3) / 1e9
+    fit_valu = n * ((S + 63) // 64) * FIT_VALU_PER_NODE_WAVE / (fit_ms * 1e-3)
     red_gbs = red_bytes / (red_ms * 1e-3) / 1e9
 
     out = {
@@ -161,6 +169,13 @@ def main():
             "bytes_per_launch": fit_bytes, "ms_per_launch": fit_ms,
             "note": "fit is VALU-bound (no contraction, 64-bit compare/divide work per eval); "
                     "HBM frac reported per the BASELINE metric; see roofline_reduce",
+        },
+        "roofline_valu": {
+            "bound": "valu", "kernel": "fit_kernel", "achieved": fit_valu / 1e9,
+            "peak": VALU_ISSUE_PEAK / 1e9, "unit": "G wave-instr/s",
+            "frac": fit_valu / VALU_ISSUE_PEAK,
+            "valu_per_node_wave": FIT_VALU_PER_NODE_WAVE,
+            "fit_evals_per_s": n * S / (fit_ms * 1e-3),
         },
         "roofline_reduce": {
             "bound": "hbm", "kernel": "reduce_mark_kernel+reduce_kernel<2>",

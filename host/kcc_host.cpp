@@ -1,0 +1,221 @@
+// kcc_host.cpp — see kcc_host.hpp.  Reference: CC = src/KubeAPI/ClusterCapacity.go,
+// BF = src/bytefmt/bytes.go of AshutoshNirkhe/KubernetesClusterCapacity.
+#include "kcc_host.hpp"
+
+#include <cctype>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <sstream>
+
+namespace kcchost {
+
+namespace {
+
+// Go strconv.Atoi (ParseInt(s, 10, 0) on 64-bit): [+-]digits, within int64.
+bool goAtoi(const std::string& s, int64_t& out) {
+  size_t i = 0;
+  bool neg = false;
+  if (s.empty()) return false;
+  if (s[0] == '+' || s[0] == '-') {
+    neg = s[0] == '-';
+    i = 1;
+  }
+  if (i == s.size()) return false;
+  uint64_t v = 0;
+  const uint64_t lim = neg ? (uint64_t)1 << 63 : ((uint64_t)1 << 63) - 1;
+  for (; i < s.size(); ++i) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    const uint64_t d = (uint64_t)(s[i] - '0');
+    if (v > (lim - d) / 10) return false;  // ErrRange
+    v = v * 10 + d;
+  }
+  out = neg ? (int64_t)(0 - v) : (int64_t)v;
+  return true;
+}
+
+}  // namespace
+
+uint64_t convertCPUToMilis(const std::string& cpu_in, bool* ok, bool print) {
+  std::string cpu = cpu_in;
+  bool flag = true;
+  if (!cpu.empty() && cpu.back() == 'm') {  // strings.HasSuffix / TrimSuffix
+    cpu.pop_back();
+    flag = false;
+  }
+  int64_t cpuMili = 0;
+  if (goAtoi(cpu, cpuMili)) {
+    if (flag) cpuMili = (int64_t)((uint64_t)cpuMili * 1000u);  // Go int multiply wraps
+    if (ok) *ok = true;
+  } else {
+    cpuMili = 0;
+    if (print) std::printf("\nError converting string to int for %s\n", cpu.c_str());
+    if (ok) *ok = false;
+  }
+  return (uint64_t)cpuMili;  // CC:318
+}
+
+std::pair<int64_t, bool> ToBytes(const std::string& in) {
+  // strings.TrimSpace + strings.ToUpper
+  size_t b = 0, e = in.size();
+  while (b < e && std::isspace((unsigned char)in[b])) ++b;
+  while (e > b && std::isspace((unsigned char)in[e - 1])) --e;
+  std::string s = in.substr(b, e - b);
+  for (char& ch : s) ch = (char)std::toupper((unsigned char)ch);
+  size_t i = 0;  // strings.IndexFunc(s, unicode.IsLetter)
+  while (i < s.size() && !(std::isalpha((unsigned char)s[i]) || (unsigned char)s[i] >= 0x80)) ++i;
+  if (i == s.size()) return {0, false};
+  const std::string num = s.substr(0, i), mult = s.substr(i);
+  // strconv.ParseFloat on a letter-free string: [sign] digits [. digits]
+  size_t k = (!num.empty() && (num[0] == '+' || num[0] == '-')) ? 1 : 0;
+  size_t digits = 0;
+  bool dot = false;
+  for (; k < num.size(); ++k) {
+    if (std::isdigit((unsigned char)num[k])) ++digits;
+    else if (num[k] == '.' && !dot) dot = true;
+    else return {0, false};
+  }
+  if (digits == 0) return {0, false};
+  const double bytes = std::strtod(num.c_str(), nullptr);  // correctly rounded, like Go
+  if (std::isinf(bytes) || !(bytes > 0)) return {0, false};
+  double unit;
+  if (mult == "T" || mult == "TB" || mult == "TIB") unit = 1099511627776.0;
+  else if (mult == "G" || mult == "GB" || mult == "GIB") unit = 1073741824.0;
+  else if (mult == "M" || mult == "MB" || mult == "MIB" || mult == "MI") unit = 1048576.0;
+  else if (mult == "K" || mult == "KB" || mult == "KIB" || mult == "KI") unit = 1024.0;
+  else if (mult == "B") unit = 1.0;
+  else return {0, false};
+  const double v = bytes * unit;
+  // Go int64(float64) on amd64 (CVTTSD2SQ): out of range -> 0x8000000000000000
+  if (std::isnan(v) || v >= 9223372036854775808.0 || v < -9223372036854775808.0)
+    return {INT64_MIN, true};
+  return {(int64_t)v, true};
+}
+
+bool loadCluster(const std::string& path, Cluster& out, std::string& err) {
+  std::ifstream f(path);
+  if (!f) {
+    err = "cannot open cluster file " + path;
+    return false;
+  }
+  std::string line;
+  int ln = 0;
+  while (std::getline(f, line)) {
+    ++ln;
+    const size_t hash = line.find('#');
+    if (hash != std::string::npos) line.resize(hash);
+    std::istringstream is(line);
+    std::string kind;
+    if (!(is >> kind)) continue;
+    auto bad = [&](const char* what) {
+      err = path + ":" + std::to_string(ln) + ": " + what;
+      return false;
+    };
+    if (kind == "node") {
+      NodeObj n;
+      if (!(is >> n.name >> n.cpu >> n.memory >> n.pods)) return bad("node <name> <cpu> <memory> <pods> <c0..c3>");
+      std::string c;
+      while (is >> c) n.conditions.push_back(c);
+      if (n.conditions.size() < 4) return bad("a node needs 4 condition statuses (CC:212-213)");
+      out.nodes.push_back(n);
+    } else if (kind == "pod") {
+      Pod p;
+      if (!(is >> p.nodeName >> p.ns >> p.name >> p.phase)) return bad("pod <node|-> <ns> <name> <phase>");
+      if (p.nodeName == "-") p.nodeName.clear();
+      std::string extra;
+      if (is >> extra) p.getFails = extra == "missing";
+      out.pods.push_back(p);
+    } else if (kind == "container") {
+      if (out.pods.empty()) return bad("container before any pod");
+      Container c;
+      if (!(is >> c.cpuRequest >> c.cpuLimit >> c.memRequest >> c.memLimit))
+        return bad("container <cpuReq> <cpuLim> <memReqBytes> <memLimBytes>");
+      out.pods.back().containers.push_back(c);
+    } else {
+      return bad("unknown record");
+    }
+  }
+  return true;
+}
+
+std::vector<node> getHealthyNodes(const Cluster& c, bool print) {
+  const size_t noOfNodes = c.nodes.size();
+  if (print) std::printf("\nThere are total %zu nodes in the cluster\n\n", noOfNodes);
+  std::vector<node> healthy(noOfNodes);  // zero rows stay for unhealthy nodes (CC:221-226)
+  for (size_t i = 0; i < noOfNodes; ++i) {
+    const NodeObj& n = c.nodes[i];
+    const uint64_t cpu = convertCPUToMilis(n.cpu, nullptr, print);  // CC:196-197
+    auto mem = ToBytes(n.memory);                                    // CC:202-206
+    const int64_t memAlloc = mem.second ? mem.first : 0;
+    bool flagHealthy = true;
+    for (int j = 0; j < 4; ++j) {  // CC:212-219
+      if (n.conditions[j] != "False") {
+        if (print) std::printf("Skipping node %s as it is not healthy\n", n.name.c_str());
+        flagHealthy = false;
+        break;
+      }
+    }
+    if (flagHealthy) {
+      healthy[i].name = n.name;
+      healthy[i].allocatableCPU = cpu;
+      healthy[i].allocatableMemory = memAlloc;
+      healthy[i].allocatablePods = n.pods;
+    }
+  }
+  return healthy;
+}
+
+std::vector<size_t> getNonTerminatedPodsForNode(const Cluster& c, const std::string& nodeName) {
+  std::vector<size_t> out;
+  for (size_t i = 0; i < c.pods.size(); ++i) {  // field selector of CC:236
+    const Pod& p = c.pods[i];
+    if (p.nodeName != nodeName) continue;
+    if (p.phase == "Pending" || p.phase == "Succeeded" || p.phase == "Failed" ||
+        p.phase == "Unknown")
+      continue;
+    out.push_back(i);
+  }
+  return out;
+}
+
+EngineInputs buildInputs(const Cluster& c, const std::vector<node>& rows) {
+  EngineInputs in;
+  for (const node& r : rows) {  // CC:105: every row, zero rows included (name "")
+    const std::vector<size_t> pods = getNonTerminatedPodsForNode(c, r.name);
+    for (size_t pi : pods) {
+      const Pod& p = c.pods[pi];
+      if (p.getFails) continue;  // NotFound: skipped by the sum (CC:267-268), still counted
+      for (const Container& ct : p.containers) {  // CC:277-293
+        in.cpu_req.push_back(convertCPUToMilis(ct.cpuRequest, nullptr, false));
+        in.cpu_lim.push_back(convertCPUToMilis(ct.cpuLimit, nullptr, false));
+        in.mem_req.push_back(ct.memRequest);
+        in.mem_lim.push_back(ct.memLimit);
+      }
+    }
+    in.node_ptr.push_back((int64_t)in.cpu_req.size());
+    in.alloc_cpu.push_back(r.allocatableCPU);
+    in.alloc_mem.push_back(r.allocatableMemory);
+    in.alloc_pods.push_back(r.allocatablePods);
+    in.pod_count.push_back((int64_t)pods.size());  // len(pods), CC:106/135
+  }
+  return in;
+}
+
+}  // namespace kcchost
+
+// C entry points for tests (ctypes) — the parsers only; no device work.
+extern "C" {
+uint64_t kcchost_convert_cpu_to_milis(const char* s, int* ok) {
+  bool b = false;
+  const uint64_t v = kcchost::convertCPUToMilis(s, &b, false);
+  if (ok) *ok = b ? 1 : 0;
+  return v;
+}
+int kcchost_to_bytes(const char* s, int64_t* out) {
+  const auto r = kcchost::ToBytes(s);
+  *out = r.first;
+  return r.second ? 0 : -1;
+}
+}

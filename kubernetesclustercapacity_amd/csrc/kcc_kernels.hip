@@ -512,8 +512,8 @@ __global__ __launch_bounds__(256) void fit_kernel(
     }
     int64_t q = qc <= qm ? qc : qm;
     if (q >= sn.P) q = sn.cl;
-    if (z) ++errs;
-    else acc += (uint64_t)q;
+    errs += z ? 1u : 0u;  // branch-free: a select between &acc and &errs spills to scratch
+    acc += z ? 0ull : (uint64_t)q;
   };
 
   if (wave_fast) {

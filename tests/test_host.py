@@ -1,0 +1,199 @@
+"""The C++ host mirror (host/): parsers, cluster selection rules and the CLI.
+
+CPU: convertCPUToMilis / bytefmt.ToBytes of the C++ host vs the KATs and both oracles
+(incl. a seeded fuzz over flag-like strings); CLI flag/error behaviour (CC:64-83).
+GPU: the CLI end to end on a cluster file with unhealthy nodes, unscheduled pods,
+excluded phases and failing pod Gets, vs the oracle.
+"""
+import ctypes as C
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import coracle, pyoracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOST = os.path.join(ROOT, "host")
+CLI = os.path.join(HOST, "cluster_capacity")
+
+
+@pytest.fixture(scope="module")
+def hostlib():
+    path = os.path.join(HOST, "libkcc_host.so")
+    if not os.path.exists(path):
+        subprocess.run(["make", "-C", HOST, "libkcc_host.so"], check=True)
+    L = C.CDLL(path)
+    L.kcchost_convert_cpu_to_milis.argtypes = [C.c_char_p, C.POINTER(C.c_int)]
+    L.kcchost_convert_cpu_to_milis.restype = C.c_uint64
+    L.kcchost_to_bytes.argtypes = [C.c_char_p, C.POINTER(C.c_int64)]
+    L.kcchost_to_bytes.restype = C.c_int
+    return L
+
+
+def host_cpu(L, s):
+    ok = C.c_int()
+    v = L.kcchost_convert_cpu_to_milis(s.encode(), C.byref(ok))
+    return v, bool(ok.value)
+
+
+def host_bytes(L, s):
+    out = C.c_int64()
+    rc = L.kcchost_to_bytes(s.encode(), C.byref(out))
+    return out.value, rc == 0
+
+
+def _strings(seed, n):
+    rng = random.Random(seed)
+    alphabet = "0123456789.+-mkKMGTBbiI e"
+    units = ["", "m", "mb", "MB", "Mi", "MI", "Gi", "G", "GiB", "KB", "Ki", "k", "T", "TB",
+             "B", "b", "TIB", "u", "x"]
+    out = []
+    for _ in range(n):
+        if rng.random() < 0.6:
+            num = str(rng.choice([0, 1, 5, 100, 250, 4000, 2**31, 2**63 - 1, 2**63, 10**25]))
+            if rng.random() < 0.3:
+                num += "." + str(rng.randint(0, 999))
+            if rng.random() < 0.2:
+                num = "-" + num
+            out.append(num + rng.choice(units))
+        else:
+            out.append("".join(rng.choice(alphabet) for _ in range(rng.randint(0, 8))))
+    return out
+
+
+def test_parsers_match_oracles(hostlib):
+    for s in _strings(1, 4000) + ["200m", "250mb", "16331524Ki", "16Gi", "0.5B", "1", "  2KB "]:
+        assert host_cpu(hostlib, s) == coracle.convert_cpu_to_milis(s) == \
+            pyoracle.convert_cpu_to_milis(s), s
+        assert host_bytes(hostlib, s) == coracle.to_bytes(s) == pyoracle.to_bytes(s), s
+
+
+def test_k1_flags(hostlib):
+    assert host_cpu(hostlib, "200m") == (200, True)
+    assert host_bytes(hostlib, "250mb") == (262_144_000, True)
+    assert host_cpu(hostlib, "100m") == (100, True)
+    assert host_bytes(hostlib, "100mb") == (104_857_600, True)
+
+
+def _run(args, **kw):
+    return subprocess.run([CLI] + args, capture_output=True, text=True, timeout=120, **kw)
+
+
+@pytest.fixture(scope="module")
+def cli():
+    if not os.path.exists(CLI):
+        subprocess.run(["make", "-C", HOST], check=True)
+    return CLI
+
+
+def test_cli_input_errors(cli):
+    r = _run(["-memRequests=16Gi"])  # GI is not a bytefmt unit (BF:94)
+    assert r.returncode == 1
+    assert r.stdout.startswith("ERROR : Invalid input memRequests = 0 byte quantity must be")
+    r = _run(["-replicas", "ten"])
+    assert r.returncode == 1 and 'parsing "ten": invalid syntax' in r.stdout
+    r = _run(["-memLimits=1"])       # a bare number is rejected (BF:81-83)
+    assert r.returncode == 1 and r.stdout.startswith("ERROR : Invalid input memLimits")
+    r = _run(["-nosuchflag=1"])
+    assert r.returncode == 2 and "flag provided but not defined" in r.stderr
+    r = _run(["-cpuRequests=0.5", "-cluster", "/nonexistent"])  # Atoi fails -> 0, printed
+    assert "Error converting string to int for 0.5" in r.stdout
+    assert "parsed from input : 200 0 209715200 104857600 1" in r.stdout
+
+
+# ---- cluster files -------------------------------------------------------------------
+def write_cluster(path, seed=5, n=60):
+    """A random cluster file + the engine-level arrays the reference would build."""
+    rng = np.random.default_rng(seed)
+    lines, phases = [], ["Running", "Running", "Running", "Pending", "Succeeded", "Failed",
+                         "Unknown"]
+    pods = []  # (nodeName, phase, missing, containers)
+    for i in range(n):
+        cpu = rng.choice(["4", "8", "3920m", "15890m", "64"])
+        mem = rng.choice(["16331524Ki", "65840760Ki", "131784048Ki", "16Gi"])  # 16Gi -> 0
+        P = int(rng.choice([110, 250, 3]))
+        healthy = rng.random() > 0.15
+        conds = ["False"] * 4 if healthy else ["False", "True", "False", "False"]
+        lines.append(f"node n{i} {cpu} {mem} {P} " + " ".join(conds))
+        for _ in range(int(rng.poisson(8))):
+            pods.append((f"n{i}", str(rng.choice(phases)), rng.random() < 0.05))
+    for _ in range(5):
+        pods.append(("-", "Running", False))  # unscheduled: listed for the "" rows
+    for node, phase, missing in pods:
+        lines.append(f"pod {node} ns p{len(lines)} {phase}" + (" missing" if missing else ""))
+        for _ in range(int(rng.integers(1, 4))):
+            creq = rng.choice(["100m", "250m", "1", "2", "0", "500m"])
+            lines.append(f"container {creq} {creq} {int(rng.integers(0, 4 << 30))} 0")
+    open(path, "w").write("\n".join(lines) + "\n")
+    return path
+
+
+def parse_expected(path):
+    """Independent Python restatement of getHealthyNodes / getNonTerminatedPodsForNode /
+    getPodCPUMemoryRequestsLimits over the file (CC:99-140), then the oracle fit."""
+    nodes, pods = [], []
+    for line in open(path):
+        f = line.split()
+        if not f:
+            continue
+        if f[0] == "node":
+            nodes.append(f[1:])
+        elif f[0] == "pod":
+            pods.append({"node": "" if f[1] == "-" else f[1], "phase": f[4],
+                         "missing": len(f) > 5 and f[5] == "missing", "c": []})
+        elif f[0] == "container":
+            pods[-1]["c"].append(f[1:])
+    rows = []
+    for name, cpu, mem, P, *conds in nodes:
+        healthy = all(c == "False" for c in conds[:4])
+        cv, _ = pyoracle.convert_cpu_to_milis(cpu)
+        mv, ok = pyoracle.to_bytes(mem)
+        rows.append((name, cv, mv if ok else 0, int(P)) if healthy else ("", 0, 0, 0))
+    ac, am, ap, pc, uc, um = [], [], [], [], [], []
+    for name, cpu, mem, P in rows:
+        sel = [p for p in pods if p["node"] == name and p["phase"] not in
+               ("Pending", "Succeeded", "Failed", "Unknown")]
+        u_c = u_m = 0
+        for p in sel:
+            if p["missing"]:
+                continue
+            for creq, _clim, mreq, _mlim in p["c"]:
+                u_c = pyoracle.u64(u_c + pyoracle.convert_cpu_to_milis(creq)[0])
+                u_m = pyoracle.i64(u_m + int(mreq))
+        ac.append(cpu); am.append(mem); ap.append(P); pc.append(len(sel))
+        uc.append(u_c); um.append(u_m)
+    return ac, am, ap, pc, uc, um
+
+
+@pytest.mark.gpu
+def test_cli_end_to_end(cli, tmp_path):
+    path = write_cluster(str(tmp_path / "cluster.txt"))
+    arrays = parse_expected(path)
+    for cpu, mem, reps in [("200m", "250mb", "10"), ("1", "1G", "100000"), ("100m", "100mb", "1")]:
+        r = _run(["-cluster", path, f"-cpuRequests={cpu}", f"-memRequests={mem}",
+                  f"-replicas={reps}"])
+        assert r.returncode == 0, r.stderr
+        sc, _ = pyoracle.convert_cpu_to_milis(cpu)
+        sm, _ = pyoracle.to_bytes(mem)
+        t, e = pyoracle.fit(*arrays, [sc], [sm])
+        assert e == [0]
+        assert f"Total possible replicas for the pod with required input specs : {t[0]}" in r.stdout
+        verdict = "So you can go ahead" if t[0] >= int(reps) else "Unfortunately"
+        assert verdict in r.stdout
+    # batch mode and the divide-by-zero panic
+    specs = tmp_path / "specs.txt"
+    specs.write_text("200m 250mb 10\n0.5 1G 3\n1 0.5B 3\n")
+    r = _run(["-cluster", path, "-specs", str(specs)])
+    assert r.returncode == 0, r.stderr
+    out = r.stdout.strip().splitlines()[-3:]
+    t, _ = pyoracle.fit(*arrays, [200], [262_144_000])
+    assert out[0] == f"200m 250mb 10 total={t[0]} {'yes' if t[0] >= 10 else 'no'}"
+    assert out[1].endswith("panic: integer divide by zero")  # cpu 0.5 -> Atoi fails -> 0
+    assert out[2].endswith("panic: integer divide by zero")  # 0.5B -> int64(0.5) == 0
+    r = _run(["-cluster", path, "-cpuRequests=0.5"])
+    assert r.returncode == 2 and "integer divide by zero" in r.stderr
+    r = _run(["-cluster", path, "-v"])
+    assert r.returncode == 0 and r.stdout.count("Max replicas :") == 60

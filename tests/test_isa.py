@@ -1,0 +1,57 @@
+"""Static ISA checks of the gfx950 kernels (CPU: hipcc cross-compiles).
+
+  - the fit kernel's fast loop: FIT_UNROLL s_load_dwordx8 node loads, no vector
+    memory, no 64-bit integer division, and exactly bench.FIT_VALU_PER_NODE_WAVE VALU
+    instructions per node (the VALU-roofline accounting of bench.py);
+  - no kernel spills to scratch.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "kubernetesclustercapacity_amd", "csrc", "kcc_kernels.hip")
+
+pytestmark = pytest.mark.skipif(shutil.which("hipcc") is None, reason="hipcc not available")
+
+
+@pytest.fixture(scope="module")
+def asm(tmp_path_factory):
+    out = tmp_path_factory.mktemp("isa") / "kcc.s"
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-S",
+                    "--cuda-device-only", SRC, "-o", str(out)], check=True,
+                   capture_output=True)
+    return out.read_text()
+
+
+def kernel_body(asm, name):
+    m = re.search(rf"^(_ZN3kcc12_GLOBAL__N_1\d+{name}\w*):\s*;", asm, re.M)
+    assert m, name
+    start = m.end()
+    return asm[start:asm.index("s_endpgm", start)]
+
+
+def test_fit_fast_loop(asm):
+    import bench
+    body = kernel_body(asm, "fit_kernel")
+    i = body.index(";;#ASMSTART")
+    loop = body[i:body.index("s_cbranch", i)]
+    lines = [ln.strip() for ln in loop.splitlines()]
+    valu = [ln for ln in lines if ln.startswith("v_")]
+    unroll = 8
+    width = {"s_load_dword": 1, "s_load_dwordx2": 2, "s_load_dwordx4": 4, "s_load_dwordx8": 8,
+             "s_load_dwordx16": 16}
+    dwords = sum(width[ln.split()[0]] for ln in lines if ln.startswith("s_load_dword"))
+    assert dwords == unroll * 8  # exactly the 32-B FitNode of each node, scalar loads
+    assert not any(ln.startswith(("global_load", "flat_load", "buffer_load")) for ln in lines)
+    assert len(valu) / unroll == pytest.approx(bench.FIT_VALU_PER_NODE_WAVE, abs=1e-9), \
+        f"{len(valu)} VALU / {unroll} nodes: update bench.FIT_VALU_PER_NODE_WAVE"
+    assert any(ln.startswith("v_pk_mul_f32") for ln in lines)
+
+
+def test_no_scratch(asm):
+    for m in re.finditer(r"\.private_segment_fixed_size:\s*(\d+)", asm):
+        assert int(m.group(1)) == 0
