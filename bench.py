@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU time of the oracle's fit sample")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="diagnostic: run only rank 0's node shard of a world of this size "
+                         "(no all-reduce) to estimate per-rank step time at N GPUs")
     return ap.parse_args()
 
 
@@ -71,6 +74,8 @@ def main():
     n_total = cfg["n_nodes"] * (world if args.scaling == "weak" else 1)
     pods_total = cfg["pods"] * (world if args.scaling == "weak" else 1)
     lo, hi = node_range(n_total, rank, world)
+    if args.emulate_world > 1:
+        lo, hi = node_range(n_total, 0, args.emulate_world)
     t0 = time.time()
     cl = synth.make_cluster(n_total, pods_total, seed=20261015 + int(args.config[1:]),
                             node_lo=lo, node_hi=hi, skew=cfg["skew"])
@@ -135,6 +140,8 @@ def main():
     fit_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
     slow_pairs, pairs = eng.fit_slow_pairs()
     value = n_total * S / (elapsed / args.steps)
+    if args.emulate_world > 1:  # per-rank rate x world (no all-reduce): an upper bound
+        value = n * S * args.emulate_world / (elapsed / args.steps)
 
     # algorithmic bytes per launch (DESIGN.md "Roofline accounting")
     fit_bytes = n * 32 + S * 16 + S * 8            # FitNode records + specs in, totals out
@@ -186,6 +193,8 @@ def main():
         "fast_path_fraction": 1.0 - (slow_pairs / pairs if pairs else 0.0),
         "gen_seconds": gen_s,
     }
+    if args.emulate_world > 1:
+        out["emulated_world"] = args.emulate_world
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cl, sc, sm, totals.cpu().numpy(), err.cpu().numpy(),

@@ -194,9 +194,8 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
   dv.prep_nodes = n_nodes;
   dv.prep_specs = n_specs;
   if (n_specs == 0) return KCC_OK;
-  KCC_HIP(ctx, hipMemsetAsync(partial, 0, sizeof(int64_t) * 2 * (size_t)n_specs, s));
-  KCC_HIP(ctx, hipMemsetAsync(dv.counters.p, 0, 64, s));
-  KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv),
+  // spec_prep also zeroes `partial` and the counters (no memset launches)
+  KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv), partial,
                                      as<unsigned long long>(dv.counters), s));
   if (n_nodes == 0) return KCC_OK;
   KCC_HIP(ctx, kcc::launch_node_prep(n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count,

@@ -69,12 +69,12 @@ struct SpecPrep {
   int32_t* normal; // 1 if the spec satisfies the fast-path bounds
 };
 
-// counters (zeroed before spec_prep): [0] (node, spec) pairs on the exact path,
-// [1] rows in slow_list, [2] largest fast-path spec cpu request.
-// spec_prep writes counters[2]; node_prep reads it and appends to slow_list.
+// counters: [0] (node, spec) pairs on the exact path, [1] rows in slow_list,
+// [2] largest fast-path spec cpu request.  spec_prep zeroes partial[0..2S) and
+// counters[0..1] and writes counters[2]; node_prep reads it and appends to slow_list.
 hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
-                            const int64_t* spec_mem, SpecPrep sp, unsigned long long* counters,
-                            hipStream_t s);
+                            const int64_t* spec_mem, SpecPrep sp, int64_t* partial,
+                            unsigned long long* counters, hipStream_t s);
 
 hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,

@@ -166,16 +166,19 @@ __global__ __launch_bounds__(256) void reduce_kernel(
   int64_t win2r = ptr_at(ptr, wbase + 128 + lane, n_nodes);
   const int32_t end_rel = (int32_t)(n_cont - wb < RED_RANGE + 2 ? n_cont - wb : RED_RANGE + 2);
 
-  // Two statically named tile buffers (ping-pong): the loads for tile t+1 are
-  // issued unconditionally (range-checked) at the top of tile t, so they stay in
-  // flight across the whole tile and no register copy forces an early wait.
-  uint64_t xa[NA][4], xb[NA][4];
+  // Three statically named tile buffers in rotation: the loads for tile t+2 are
+  // issued unconditionally (range-checked) at the top of tile t, so two tiles per
+  // wave stay in flight and no register copy forces an early wait.
+  uint64_t xa[NA][4], xb[NA][4], xc[NA][4];
 #pragma unroll
-  for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 32, xa[k]);
+  for (int k = 0; k < NA; ++k) {
+    load_quad(rs[k], lane * 32, xa[k]);
+    load_quad(rs[k], RED_TILE * 8 + lane * 32, xb[k]);
+  }
 
   auto tile = [&](uint64_t (&x)[NA][4], uint64_t (&nx)[NA][4], const int32_t tb) {
 #pragma unroll
-    for (int k = 0; k < NA; ++k) load_quad(rs[k], (tb + RED_TILE) * 8 + lane * 32, nx[k]);
+    for (int k = 0; k < NA; ++k) load_quad(rs[k], (tb + 2 * RED_TILE) * 8 + lane * 32, nx[k]);
     const int32_t p0 = tb + 4 * lane;  // relative position of this lane's first item
     if ((len & 1) && p0 <= len - 1 && len - 1 < p0 + 4) {  // odd tail: last item alone
 #pragma unroll
@@ -273,9 +276,10 @@ __global__ __launch_bounds__(256) void reduce_kernel(
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   };
-  for (int32_t tb = 0; tb < len; tb += 2 * RED_TILE) {
-    tile(xa, xb, tb);
+  for (int32_t tb = 0; tb < len; tb += 3 * RED_TILE) {
+    tile(xa, xc, tb);
     if (tb + RED_TILE < len) tile(xb, xa, tb + RED_TILE);
+    if (tb + 2 * RED_TILE < len) tile(xc, xb, tb + 2 * RED_TILE);
   }
   // the run open at the end of the range continues into the next wave's range
   if (wb + len < n_cont && lane == 0 && cur < n_nodes) {
@@ -360,76 +364,74 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
   }
 }
 
-// Single-workgroup stable partition of the specs: fast-path specs first.
+// Single-workgroup stable partition of the specs (fast-path specs first), in two
+// passes over contiguous per-thread chunks with one block-wide exclusive scan in
+// between.  Also zeroes partial[0..2S) and counters[0..1] (no memset launches) and
+// writes counters[2] = the largest fast-path cpu request.
 __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64_t* __restrict__ c_in,
                                                          const int64_t* __restrict__ m_in,
-                                                         SpecPrep sp,
+                                                         SpecPrep sp, int64_t* __restrict__ partial,
                                                          unsigned long long* __restrict__ counters) {
-  __shared__ int wn[16], wa[16], on[16], oa[16];
+  __shared__ int64_t wsum[16];
   __shared__ unsigned long long wmax[16];
-  __shared__ int64_t tot_n_s, run_n_s, run_a_s;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  int64_t local = 0;
-  unsigned long long cmax = 0;  // largest fast-path cpu request (bounds P in node_prep)
-  for (int64_t i = tid; i < S; i += 1024) {
-    const bool nm = spec_is_normal(c_in[i], m_in[i]);
-    local += nm ? 1 : 0;
-    if (nm && c_in[i] > cmax) cmax = c_in[i];
+  const int64_t per = (S + 1023) / 1024;
+  const int64_t b0 = tid * per < S ? tid * per : S;
+  const int64_t b1 = b0 + per < S ? b0 + per : S;
+  int64_t cnt = 0;
+  unsigned long long cmax = 0;
+  for (int64_t i = b0; i < b1; ++i) {
+    const uint64_t c = c_in[i];
+    if (spec_is_normal(c, m_in[i])) {
+      ++cnt;
+      cmax = c > cmax ? c : cmax;
+    }
   }
+  // block exclusive scan of cnt (wave shuffles + 16 wave totals in LDS)
+  int64_t incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t u = __shfl_up(incl, d);
+    if (lane >= d) incl += u;
+  }
+  unsigned long long mx = cmax;
+#pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
-    local += __shfl_xor(local, d);
-    const unsigned long long o = __shfl_xor(cmax, d);
-    cmax = o > cmax ? o : cmax;
+    const unsigned long long o = __shfl_xor(mx, d);
+    mx = o > mx ? o : mx;
   }
-  if (lane == 0) { wn[wv] = (int)local; wmax[wv] = cmax; }
-  if (tid == 0) { run_n_s = 0; run_a_s = 0; }
+  if (lane == 63) wsum[wv] = incl;
+  if (lane == 0) wmax[wv] = mx;
   __syncthreads();
+  int64_t wbase = 0, tot_n = 0;
+  unsigned long long gmax = 0;
+  for (int k = 0; k < 16; ++k) {
+    if (k < wv) wbase += wsum[k];
+    tot_n += wsum[k];
+    gmax = wmax[k] > gmax ? wmax[k] : gmax;
+  }
+  int64_t pn = wbase + incl - cnt;  // my first fast-path slot
+  int64_t pa = tot_n + (b0 - (wbase + incl - cnt));  // my first exact-path slot
+  for (int64_t i = b0; i < b1; ++i) {
+    const uint64_t c = c_in[i];
+    const int64_t m = m_in[i];
+    const bool nm = spec_is_normal(c, m);
+    const int64_t pos = nm ? pn++ : pa++;
+    sp.c[pos] = c;
+    sp.m[pos] = m;
+    sp.md[pos] = (double)m;
+    // reciprocals biased up by 2^-20 so the fit's quotient estimate never
+    // undershoots (f64 division, then one rounding to f32)
+    sp.rc[pos] = nm ? (float)(FIT_RECIP_BIAS / (double)c) : 0.f;
+    sp.rm[pos] = nm ? (float)(FIT_RECIP_BIAS / (double)m) : 0.f;
+    sp.perm[pos] = (int32_t)i;
+    sp.normal[pos] = nm ? 1 : 0;
+  }
+  for (int64_t i = tid; i < 2 * S; i += 1024) partial[i] = 0;
   if (tid == 0) {
-    int64_t t = 0;
-    unsigned long long mx = 0;
-    for (int k = 0; k < 16; ++k) { t += wn[k]; mx = wmax[k] > mx ? wmax[k] : mx; }
-    tot_n_s = t;
-    counters[2] = mx;
-  }
-  __syncthreads();
-  const int64_t tot_n = tot_n_s;
-  for (int64_t base = 0; base < S; base += 1024) {
-    const int64_t i = base + tid;
-    const bool valid = i < S;
-    const uint64_t c = valid ? c_in[i] : 0;
-    const int64_t m = valid ? m_in[i] : 0;
-    const bool nm = valid && spec_is_normal(c, m);
-    const bool ab = valid && !nm;
-    const unsigned long long bn = __ballot(nm), ba = __ballot(ab);
-    if (lane == 0) { wn[wv] = __popcll(bn); wa[wv] = __popcll(ba); }
-    __syncthreads();
-    if (tid == 0) {
-      int sn = 0, sa = 0;
-      for (int k = 0; k < 16; ++k) { on[k] = sn; oa[k] = sa; sn += wn[k]; sa += wa[k]; }
-    }
-    __syncthreads();
-    if (valid) {
-      const int64_t pos = nm ? run_n_s + on[wv] + __popcll(bn & lt)
-                             : tot_n + run_a_s + oa[wv] + __popcll(ba & lt);
-      sp.c[pos] = c;
-      sp.m[pos] = m;
-      sp.md[pos] = (double)m;
-      // reciprocals biased up by 2^-20 so the fit's quotient estimate never
-      // undershoots (f64 division, then one rounding to f32)
-      sp.rc[pos] = nm ? (float)(FIT_RECIP_BIAS / (double)c) : 0.f;
-      sp.rm[pos] = nm ? (float)(FIT_RECIP_BIAS / (double)m) : 0.f;
-      sp.perm[pos] = (int32_t)i;
-      sp.normal[pos] = nm ? 1 : 0;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int sn = 0, sa = 0;
-      for (int k = 0; k < 16; ++k) { sn += wn[k]; sa += wa[k]; }
-      run_n_s += sn;
-      run_a_s += sa;
-    }
-    __syncthreads();
+    counters[0] = 0;
+    counters[1] = 0;
+    counters[2] = gmax;
   }
 }
 
@@ -476,8 +478,15 @@ __global__ __launch_bounds__(256) void fit_kernel(
     const uint64_t* __restrict__ sc, const int64_t* __restrict__ sm,
     const double* __restrict__ smd, const float* __restrict__ src,
     const float* __restrict__ srm, const int32_t* __restrict__ snormal,
-    int64_t* __restrict__ partial, unsigned long long* __restrict__ counters) {
-  const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t gx,
+    int32_t gy) {
+  // XCD-aware order (speed only, never correctness): workgroups are dealt round-robin
+  // over the 8 XCDs, so give every spec group of one node chunk the same b % 8 — the
+  // chunk's FitNode records then stay in that XCD's L2 for all of them.
+  const int32_t b = blockIdx.x, xcd = b & 7, r = b >> 3;
+  const int32_t bx = r % gx, by = (r / gx) * 8 + xcd;
+  if (by >= gy) return;  // padding of gy up to a multiple of 8 (whole workgroup)
+  const int64_t s = (int64_t)bx * 256 + threadIdx.x;
   const bool active = s < S;
   const uint64_t c = active ? sc[s] : 1;
   const int64_t m = active ? sm[s] : 1;
@@ -489,7 +498,7 @@ __global__ __launch_bounds__(256) void fit_kernel(
   const int32_t negc = -(int32_t)(uint32_t)c;
   const f32x2 rcm = {rc, rm};
 
-  const int64_t n0 = (int64_t)blockIdx.y * nodes_per_block;
+  const int64_t n0 = (int64_t)by * nodes_per_block;
   const int64_t n1 = n0 + nodes_per_block < n_nodes ? n0 + nodes_per_block : n_nodes;
   uint64_t acc = 0;
   uint64_t errs = 0;
@@ -537,7 +546,7 @@ __global__ __launch_bounds__(256) void fit_kernel(
     }
     // rows outside the fast bounds, shared out over the node-chunk blocks
     const int64_t n_slow = (int64_t)counters[1];
-    for (int64_t j = blockIdx.y; j < n_slow; j += gridDim.y) eval_slow(slow_list[j]);
+    for (int64_t j = by; j < n_slow; j += gy) eval_slow(slow_list[j]);
   } else {
     for (int64_t i = n0; i < n1; ++i) eval_slow(i);
   }
@@ -620,10 +629,11 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
 }
 
 hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
-                            SpecPrep sp, unsigned long long* counters, hipStream_t s) {
+                            SpecPrep sp, int64_t* partial, unsigned long long* counters,
+                            hipStream_t s) {
   if (n_specs <= 0) return hipSuccess;
   hipLaunchKernelGGL(spec_prep_kernel, dim3(1), dim3(1024), 0, s, n_specs, spec_cpu, spec_mem,
-                     sp, counters);
+                     sp, partial, counters);
   return hipGetLastError();
 }
 
@@ -638,14 +648,15 @@ hipError_t launch_fit(int64_t n_nodes, const FitNode* fast, const SlowNode* slow
   int64_t npb = (n_nodes + gy_target - 1) / gy_target;
   if (npb < 64) npb = 64;
   int64_t gy = (n_nodes + npb - 1) / npb;
-  if (gy > 65535) {
-    gy = 65535;
-    npb = (n_nodes + gy - 1) / gy;
+  // 1-D grid of gx * roundup(gy, 8) workgroups, remapped XCD-aware in the kernel
+  while (gx * ((gy + 7) / 8 * 8) > 0x7fffffffLL) {
+    npb *= 2;
     gy = (n_nodes + npb - 1) / npb;
   }
-  hipLaunchKernelGGL(fit_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, s, n_nodes, npb,
-                     fast, slow, slow_list, n_specs, sp.c, sp.m, sp.md, sp.rc, sp.rm, sp.normal,
-                     partial, counters);
+  const int64_t blocks = gx * ((gy + 7) / 8 * 8);
+  hipLaunchKernelGGL(fit_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, npb, fast,
+                     slow, slow_list, n_specs, sp.c, sp.m, sp.md, sp.rc, sp.rm, sp.normal,
+                     partial, counters, (int32_t)gx, (int32_t)gy);
   return hipGetLastError();
 }
 
