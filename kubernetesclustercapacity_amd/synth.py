@@ -61,7 +61,11 @@ def _chunk(seed: int, ci: int, n: int, mean_pods: float, skew: bool, unhealthy: 
     alloc_mem = rng.integers(8 * GIB // KIB, 512 * GIB // KIB, n, dtype=np.int64) * KIB
     alloc_pods = rng.choice(np.array([110, 250], np.int64), n)
     if skew:
-        pods = np.minimum(rng.zipf(1.2, n) - 1 + rng.poisson(mean_pods * 0.5, n), 2 * alloc_pods)
+        # heavy-tailed pods/node (lognormal, sigma 1) with the configured mean, capped at
+        # 2x allocatable pods: ~1-2% of nodes hold more pods than allocatable (negative
+        # clamps, CC:135)
+        raw = rng.lognormal(np.log(max(mean_pods, 1e-9)) - 0.5, 1.0, n)
+        pods = np.minimum(np.floor(raw).astype(np.int64), 2 * alloc_pods)
     else:
         pods = rng.poisson(mean_pods, n)
     pods = pods.astype(np.int64)
