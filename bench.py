@@ -8,8 +8,11 @@ Inputs are resident in HBM before the timed region; value = nodes x specs of the
 whole job / step time (max over ranks).
 
 Default workload = BASELINE config C4 (1M nodes, ~20M pods / ~40M containers, 4096
-specs), which fits one MI355X; --gpus N shards the same 1M nodes over N ranks
-(strong scaling, one process per GPU, launched by torch.distributed.run).
+specs), which fits one MI355X.  --gpus N (one process per GPU, torch.distributed.run):
+the cluster is partitioned by nodes; by default each rank owns one C4-sized partition
+of an N x 1M-node cluster (weak scaling: N=1 is exactly C4) and the only exchange is
+the RCCL all-reduce of the per-spec partials.  --scaling strong shards the same 1M
+nodes over the N ranks instead.
 """
 from __future__ import annotations
 
@@ -41,10 +44,13 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C5"])
-    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    ap.add_argument("--scaling", default="weak", choices=["strong", "weak"],
+                    help="weak: a C4-sized node partition per rank; strong: C4 split over ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU time of the oracle's fit sample")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, production); gloo only to rehearse several ranks on one GPU")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="diagnostic: run only rank 0's node shard of a world of this size "
                          "(no all-reduce) to estimate per-rank step time at N GPUs")
@@ -65,10 +71,14 @@ def main():
     if args.gpus != world and rank == 0:
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: running {world} rank(s)",
               file=sys.stderr)
+    local = local % max(torch.cuda.device_count(), 1)  # rehearsal: several ranks, one GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     cfg = synth.CONFIGS[args.config]
     n_total = cfg["n_nodes"] * (world if args.scaling == "weak" else 1)
@@ -196,6 +206,11 @@ def main():
     if args.emulate_world > 1:
         out["emulated_world"] = args.emulate_world
 
+    # order-independent fingerprint of the per-spec totals: identical for every N
+    tot_np = totals.cpu().numpy().view(np.uint64)
+    out["totals_checksum"] = int(((tot_np * np.uint64(0x9E3779B97F4A7C15)) ^ (tot_np >> np.uint64(29)))
+                                 .sum(dtype=np.uint64))
+    out["spec_errors"] = int(err.cpu().numpy().sum())
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cl, sc, sm, totals.cpu().numpy(), err.cpu().numpy(),
                                            args.cpu_seconds)

@@ -41,7 +41,7 @@ struct Dev {
   int device = 0;
   hipStream_t stream = nullptr;
   // workspace of the *_async entry points
-  DevBuf wave_node, fast, slow, slow_list, sc, sm, smd, src, srm, sperm, snormal, counters;
+  DevBuf wave_node, fast, slow, slow_list, srec, sperm, counters;
   int64_t last_pairs = 0;  // node x spec pairs of the last fit_prepare on this device
   int64_t prep_nodes = -1, prep_specs = -1;  // sizes the workspace was last prepared for
   // staging of the host-array entry points
@@ -134,7 +134,7 @@ int reduce_async_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, con
     return fail(ctx, KCC_EINVAL, "limits need cpu_lim, mem_lim, lim_cpu and lim_mem");
   if (!aligned16(cpu) || !aligned16(mem) || (lim && (!aligned16(cpul) || !aligned16(meml))))
     return fail(ctx, KCC_EINVAL, "container arrays must be 16-byte aligned");
-  const int64_t waves = kcc::reduce_n_waves(n_cont);
+  const int64_t waves = kcc::reduce_max_waves(n_cont);
   KCC_HIP(ctx, ensure(dv.wave_node, sizeof(int64_t) * (size_t)(waves > 0 ? waves : 1)));
   KCC_HIP(ctx, kcc::launch_reduce_mark(n_nodes, n_cont, ptr, as<int64_t>(dv.wave_node), used_cpu,
                                        used_mem, lim ? lim_cpu : nullptr,
@@ -147,13 +147,8 @@ int reduce_async_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, con
 
 kcc::SpecPrep spec_prep_of(Dev& dv) {
   kcc::SpecPrep sp;
-  sp.c = as<uint64_t>(dv.sc);
-  sp.m = as<int64_t>(dv.sm);
-  sp.md = as<double>(dv.smd);
-  sp.rc = as<float>(dv.src);
-  sp.rm = as<float>(dv.srm);
+  sp.rec = as<kcc::SpecRec>(dv.srec);
   sp.perm = as<int32_t>(dv.sperm);
-  sp.normal = as<int32_t>(dv.snormal);
   return sp;
 }
 
@@ -161,18 +156,13 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, hipSetDevice(dv.device));
   const size_t N = (size_t)(n_nodes > 0 ? n_nodes : 1);
   const size_t S = (size_t)(n_specs > 0 ? n_specs : 1);
-  const int64_t waves = kcc::reduce_n_waves(n_cont > 0 ? n_cont : 1);
+  const int64_t waves = kcc::reduce_max_waves(n_cont > 0 ? n_cont : 1);
   KCC_HIP(ctx, ensure(dv.wave_node, sizeof(int64_t) * (size_t)waves));
   KCC_HIP(ctx, ensure(dv.fast, sizeof(kcc::FitNode) * N));
   KCC_HIP(ctx, ensure(dv.slow, sizeof(kcc::SlowNode) * N));
   KCC_HIP(ctx, ensure(dv.slow_list, sizeof(int64_t) * N));
-  KCC_HIP(ctx, ensure(dv.sc, 8 * S));
-  KCC_HIP(ctx, ensure(dv.sm, 8 * S));
-  KCC_HIP(ctx, ensure(dv.smd, 8 * S));
-  KCC_HIP(ctx, ensure(dv.src, 4 * S));
-  KCC_HIP(ctx, ensure(dv.srm, 4 * S));
+  KCC_HIP(ctx, ensure(dv.srec, sizeof(kcc::SpecRec) * S));
   KCC_HIP(ctx, ensure(dv.sperm, 4 * S));
-  KCC_HIP(ctx, ensure(dv.snormal, 4 * S));
   KCC_HIP(ctx, ensure(dv.counters, 64));
   return KCC_OK;
 }
@@ -411,8 +401,8 @@ void kcc_destroy(kcc_ctx* ctx) {
   for (Dev& dv : ctx->devs) {
     (void)hipSetDevice(dv.device);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
-    DevBuf* bufs[] = {&dv.wave_node, &dv.slow_list, &dv.fast,      &dv.slow,      &dv.sc,        &dv.sm,
-                      &dv.smd,       &dv.src,       &dv.srm,       &dv.sperm,     &dv.snormal,
+    DevBuf* bufs[] = {&dv.wave_node, &dv.slow_list, &dv.fast,      &dv.slow,      &dv.srec,
+                      &dv.sperm,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
                       &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,
                       &dv.alloc_cpu, &dv.alloc_mem, &dv.alloc_pods, &dv.pod_count, &dv.spec_cpu,

@@ -7,16 +7,39 @@
 namespace kcc {
 
 // ---- (a) segmented request reduce -------------------------------------------
-// One wavefront owns a contiguous range of RED_RANGE containers and walks it in
+// One wavefront owns a contiguous range of reduce_range() containers and walks it in
 // tiles of RED_TILE (RED_IPL containers per lane: two 16-B loads per lane per array).
+#ifndef KCC_RED_TILES_PER_WAVE
+#define KCC_RED_TILES_PER_WAVE 16  // longest wave range (tiles)
+#endif
+#ifndef KCC_RED_TARGET_WAVES
+#define KCC_RED_TARGET_WAVES 8192  // shorten ranges until this many waves exist
+#endif
+#ifndef KCC_RED_PREFETCH
+#define KCC_RED_PREFETCH 1  // tiles in flight ahead of the one being reduced (1 or 2)
+#endif
 constexpr int RED_IPL = 4;
 constexpr int RED_TILE = 64 * RED_IPL;  // 256
-constexpr int RED_TILES_PER_WAVE = 16;
-constexpr int64_t RED_RANGE = (int64_t)RED_TILE * RED_TILES_PER_WAVE;  // 4096
+constexpr int RED_TILES_PER_WAVE = KCC_RED_TILES_PER_WAVE;
 constexpr int RED_WAVES_PER_BLOCK = 4;
 
+// Containers per wave range: whole tiles, long (<= 16 tiles) for big inputs, short
+// enough for small ones (a node shard of an 8-GPU run) that ~KCC_RED_TARGET_WAVES
+// waves exist and every SIMD has several in flight.
+inline int32_t reduce_range(int64_t n_containers) {
+  int64_t t = (n_containers + (int64_t)RED_TILE * KCC_RED_TARGET_WAVES - 1) /
+              ((int64_t)RED_TILE * KCC_RED_TARGET_WAVES);
+  if (t < 1) t = 1;
+  if (t > RED_TILES_PER_WAVE) t = RED_TILES_PER_WAVE;
+  return (int32_t)(t * RED_TILE);
+}
 inline int64_t reduce_n_waves(int64_t n_containers) {
-  return (n_containers + RED_RANGE - 1) / RED_RANGE;
+  const int64_t r = reduce_range(n_containers);
+  return (n_containers + r - 1) / r;
+}
+// workspace bound for wave_node (shortest range)
+inline int64_t reduce_max_waves(int64_t n_containers) {
+  return (n_containers + RED_TILE - 1) / RED_TILE + 1;
 }
 
 // Zeroes the per-node outputs and records, for every wave range, the node that owns
@@ -57,16 +80,21 @@ struct __attribute__((aligned(32))) SlowNode {
 };
 static_assert(sizeof(SlowNode) == 32, "SlowNode must be 32 B");
 
-// Spec arrays in the kernel's internal (partitioned) order: specs that satisfy the
-// fast-path bounds first, the rest after (so at most one wavefront mixes both).
+// One 32-B record per spec, in the kernel's internal (partitioned) order: specs that
+// satisfy the fast-path bounds first, the rest after (so at most one wavefront mixes
+// both).  rc == 0 marks a spec for the exact path (a fast-path rc is > 0).
+struct __attribute__((aligned(32))) SpecRec {
+  uint64_t c;   // cpu request (millicores)
+  int64_t m;    // memory request (bytes)
+  double md;    // m as f64
+  float rc;     // (1 + 2^-20)/c (f32): biased up, see fit_fast; 0 off the fast path
+  float rm;     // (1 + 2^-20)/m (f32)
+};
+static_assert(sizeof(SpecRec) == 32, "SpecRec must be 32 B");
+
 struct SpecPrep {
-  uint64_t* c;     // cpu request (millicores)
-  int64_t* m;      // memory request (bytes)
-  double* md;      // m as f64
-  float* rc;       // (1 + 2^-20)/c (f32): biased up, see fit_fast
-  float* rm;       // (1 + 2^-20)/m (f32)
-  int32_t* perm;   // internal index -> caller index
-  int32_t* normal; // 1 if the spec satisfies the fast-path bounds
+  SpecRec* rec;
+  int32_t* perm;  // internal index -> caller index
 };
 
 // counters: [0] (node, spec) pairs on the exact path, [1] rows in slow_list,

@@ -29,8 +29,8 @@ __device__ __forceinline__ unsigned long long atomic_add_u64(uint64_t* p, uint64
 // (a) segmented reduce
 // ----------------------------------------------------------------------------
 
-// Zero the outputs; for every wave range x*RED_RANGE record the node owning it.
-__global__ void reduce_mark_kernel(int64_t n_nodes, int64_t n_cont,
+// Zero the outputs; for every wave range x*range record the node owning it.
+__global__ void reduce_mark_kernel(int64_t n_nodes, int64_t n_cont, int32_t range,
                                    const int64_t* __restrict__ ptr,
                                    int64_t* __restrict__ wave_node, uint64_t* __restrict__ o0,
                                    uint64_t* __restrict__ o1, uint64_t* __restrict__ o2,
@@ -45,8 +45,8 @@ __global__ void reduce_mark_kernel(int64_t n_nodes, int64_t n_cont,
     b = b < 0 ? 0 : b;
     e = e > n_cont ? n_cont : e;
     if (e > b) {
-      for (int64_t x = (b + RED_RANGE - 1) / RED_RANGE * RED_RANGE; x < e; x += RED_RANGE)
-        wave_node[x / RED_RANGE] = j;
+      for (int64_t x = (b + range - 1) / range * range; x < e; x += range)
+        wave_node[x / range] = j;
     }
   }
 }
@@ -85,15 +85,16 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
 
 // CSR offset of node j relative to the wave range start, clamped into int32.
 __device__ __forceinline__ int32_t rel_clamp(int64_t raw, int64_t wb) {
-  const int64_t v = raw - wb;
-  return (int32_t)(v < -1 ? -1 : (v > RED_RANGE + 2 ? RED_RANGE + 2 : v));
+  const int64_t v = raw - wb;  // any range is <= RED_TILE * RED_TILES_PER_WAVE
+  constexpr int64_t HI = (int64_t)RED_TILE * RED_TILES_PER_WAVE + 2;
+  return (int32_t)(v < -1 ? -1 : (v > HI ? HI : v));
 }
 __device__ __forceinline__ int64_t ptr_at(const int64_t* __restrict__ ptr, int64_t j,
                                           int64_t n_nodes) {
   return ptr[j < n_nodes ? j : n_nodes];
 }
 __device__ __forceinline__ int32_t rel_ptr(const int64_t* __restrict__ ptr, int64_t j,
-                                           int64_t n_nodes, int64_t wb) {
+                                           int64_t n_nodes, int64_t wb) {  // NOLINT
   return rel_clamp(ptr_at(ptr, j, n_nodes), wb);
 }
 
@@ -111,7 +112,7 @@ __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff
   x[3] = hi.y;
 }
 
-// One wavefront walks a contiguous range of RED_RANGE containers in tiles of
+// One wavefront walks a contiguous range of `range` containers in tiles of
 // RED_TILE = 256 (4 per lane, coalesced SoA buffer loads, next tile prefetched).
 // Per tile:
 //   1. nodes starting inside the tile: the next 64 CSR offsets come from a sliding
@@ -127,7 +128,7 @@ __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff
 // Empty nodes are never visited (zeroed by reduce_mark_kernel).
 template <int NA>
 __global__ __launch_bounds__(256) void reduce_kernel(
-    int64_t n_nodes, int64_t n_cont, const int64_t* __restrict__ ptr,
+    int64_t n_nodes, int64_t n_cont, int32_t range, const int64_t* __restrict__ ptr,
     const uint64_t* __restrict__ in0, const uint64_t* __restrict__ in1,
     const uint64_t* __restrict__ in2, const uint64_t* __restrict__ in3,
     const int64_t* __restrict__ wave_node, uint64_t* __restrict__ out0,
@@ -138,9 +139,9 @@ __global__ __launch_bounds__(256) void reduce_kernel(
   // wave index made provably uniform (T20: no waterfall loops around the buffer ops)
   const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)(blockIdx.x * RED_WAVES_PER_BLOCK +
                                                              (threadIdx.x >> 6)));
-  const int64_t wb = (int64_t)w * RED_RANGE;
+  const int64_t wb = (int64_t)w * range;
   if (wb >= n_cont) return;  // wave-uniform; no block-level barrier in this kernel
-  const int32_t len = (int32_t)(n_cont - wb < RED_RANGE ? n_cont - wb : RED_RANGE);
+  const int32_t len = (int32_t)(n_cont - wb < range ? n_cont - wb : range);
   int32_t* heads = heads_s + (threadIdx.x >> 6) * HS;
   const uint64_t* in[4] = {in0, in1, in2, in3};
   uint64_t* out[4] = {out0, out1, out2, out3};
@@ -164,21 +165,27 @@ __global__ __launch_bounds__(256) void reduce_kernel(
   int32_t win0 = rel_ptr(ptr, wbase + lane, n_nodes, wb);
   int32_t win1 = rel_ptr(ptr, wbase + 64 + lane, n_nodes, wb);
   int64_t win2r = ptr_at(ptr, wbase + 128 + lane, n_nodes);
-  const int32_t end_rel = (int32_t)(n_cont - wb < RED_RANGE + 2 ? n_cont - wb : RED_RANGE + 2);
+  const int32_t end_rel = (int32_t)(n_cont - wb < range + 2 ? n_cont - wb : range + 2);
 
-  // Three statically named tile buffers in rotation: the loads for tile t+2 are
-  // issued unconditionally (range-checked) at the top of tile t, so two tiles per
-  // wave stay in flight and no register copy forces an early wait.
-  uint64_t xa[NA][4], xb[NA][4], xc[NA][4];
+  // Statically named tile buffers in rotation: the loads for tile t+KCC_RED_PREFETCH
+  // are issued unconditionally (range-checked) at the top of tile t, so they stay in
+  // flight across whole tiles and no register copy forces an early wait.
+  uint64_t xa[NA][4], xb[NA][4];
+#if KCC_RED_PREFETCH == 2
+  uint64_t xc[NA][4];
+#endif
 #pragma unroll
   for (int k = 0; k < NA; ++k) {
     load_quad(rs[k], lane * 32, xa[k]);
+#if KCC_RED_PREFETCH == 2
     load_quad(rs[k], RED_TILE * 8 + lane * 32, xb[k]);
+#endif
   }
 
   auto tile = [&](uint64_t (&x)[NA][4], uint64_t (&nx)[NA][4], const int32_t tb) {
 #pragma unroll
-    for (int k = 0; k < NA; ++k) load_quad(rs[k], (tb + 2 * RED_TILE) * 8 + lane * 32, nx[k]);
+    for (int k = 0; k < NA; ++k)
+      load_quad(rs[k], (tb + KCC_RED_PREFETCH * RED_TILE) * 8 + lane * 32, nx[k]);
     const int32_t p0 = tb + 4 * lane;  // relative position of this lane's first item
     if ((len & 1) && p0 <= len - 1 && len - 1 < p0 + 4) {  // odd tail: last item alone
 #pragma unroll
@@ -276,11 +283,18 @@ __global__ __launch_bounds__(256) void reduce_kernel(
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   };
+#if KCC_RED_PREFETCH == 2
   for (int32_t tb = 0; tb < len; tb += 3 * RED_TILE) {
     tile(xa, xc, tb);
     if (tb + RED_TILE < len) tile(xb, xa, tb + RED_TILE);
     if (tb + 2 * RED_TILE < len) tile(xc, xb, tb + 2 * RED_TILE);
   }
+#else
+  for (int32_t tb = 0; tb < len; tb += 2 * RED_TILE) {
+    tile(xa, xb, tb);
+    if (tb + RED_TILE < len) tile(xb, xa, tb + RED_TILE);
+  }
+#endif
   // the run open at the end of the range continues into the next wave's range
   if (wb + len < n_cont && lane == 0 && cur < n_nodes) {
 #pragma unroll
@@ -378,11 +392,42 @@ __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64
   const int64_t per = (S + 1023) / 1024;
   const int64_t b0 = tid * per < S ? tid * per : S;
   const int64_t b1 = b0 + per < S ? b0 + per : S;
+  // up to 8 specs per thread (S <= 8192) stay in registers: all loads issue at once
+  constexpr int REG = 8;
+  const bool in_regs = per <= REG;
+  uint64_t rc_[REG];
+  int64_t rm_[REG];
+  if (in_regs) {
+#pragma unroll
+    for (int u = 0; u < REG; ++u) {
+      const bool v = b0 + u < b1;
+      rc_[u] = v ? c_in[b0 + u] : 0;
+      rm_[u] = v ? m_in[b0 + u] : 0;
+    }
+  }
+  auto spec_c = [&](int64_t i) -> uint64_t {
+    if (in_regs) {
+      uint64_t r = 0;
+#pragma unroll
+      for (int u = 0; u < REG; ++u) r = (i - b0 == u) ? rc_[u] : r;  // static indices only
+      return r;
+    }
+    return c_in[i];
+  };
+  auto spec_m = [&](int64_t i) -> int64_t {
+    if (in_regs) {
+      int64_t r = 0;
+#pragma unroll
+      for (int u = 0; u < REG; ++u) r = (i - b0 == u) ? rm_[u] : r;
+      return r;
+    }
+    return m_in[i];
+  };
   int64_t cnt = 0;
   unsigned long long cmax = 0;
   for (int64_t i = b0; i < b1; ++i) {
-    const uint64_t c = c_in[i];
-    if (spec_is_normal(c, m_in[i])) {
+    const uint64_t c = spec_c(i);
+    if (spec_is_normal(c, spec_m(i))) {
       ++cnt;
       cmax = c > cmax ? c : cmax;
     }
@@ -413,19 +458,20 @@ __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64
   int64_t pn = wbase + incl - cnt;  // my first fast-path slot
   int64_t pa = tot_n + (b0 - (wbase + incl - cnt));  // my first exact-path slot
   for (int64_t i = b0; i < b1; ++i) {
-    const uint64_t c = c_in[i];
-    const int64_t m = m_in[i];
+    const uint64_t c = spec_c(i);
+    const int64_t m = spec_m(i);
     const bool nm = spec_is_normal(c, m);
     const int64_t pos = nm ? pn++ : pa++;
-    sp.c[pos] = c;
-    sp.m[pos] = m;
-    sp.md[pos] = (double)m;
+    SpecRec r;
+    r.c = c;
+    r.m = m;
+    r.md = (double)m;
     // reciprocals biased up by 2^-20 so the fit's quotient estimate never
     // undershoots (f64 division, then one rounding to f32)
-    sp.rc[pos] = nm ? (float)(FIT_RECIP_BIAS / (double)c) : 0.f;
-    sp.rm[pos] = nm ? (float)(FIT_RECIP_BIAS / (double)m) : 0.f;
+    r.rc = nm ? (float)(FIT_RECIP_BIAS / (double)c) : 0.f;
+    r.rm = nm ? (float)(FIT_RECIP_BIAS / (double)m) : 0.f;
+    sp.rec[pos] = r;
     sp.perm[pos] = (int32_t)i;
-    sp.normal[pos] = nm ? 1 : 0;
   }
   for (int64_t i = tid; i < 2 * S; i += 1024) partial[i] = 0;
   if (tid == 0) {
@@ -465,6 +511,9 @@ __device__ __forceinline__ int32_t fit_fast(const FitNode& nd, f32x2 rcm, double
 }
 
 constexpr int FIT_UNROLL = 8;
+#ifndef KCC_FIT_TARGET_BLOCKS
+#define KCC_FIT_TARGET_BLOCKS 16384
+#endif
 typedef int32_t i32x8 __attribute__((ext_vector_type(8)));
 
 // one s_load_dwordx8 per record (a vector load is never split into field loads)
@@ -475,10 +524,8 @@ __device__ __forceinline__ FitNode load_node(const i32x8* __restrict__ q, int i)
 __global__ __launch_bounds__(256) void fit_kernel(
     int64_t n_nodes, int64_t nodes_per_block, const FitNode* __restrict__ fast,
     const SlowNode* __restrict__ slow, const int64_t* __restrict__ slow_list, int64_t S,
-    const uint64_t* __restrict__ sc, const int64_t* __restrict__ sm,
-    const double* __restrict__ smd, const float* __restrict__ src,
-    const float* __restrict__ srm, const int32_t* __restrict__ snormal,
-    int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t gx,
+    const SpecRec* __restrict__ specs, int64_t* __restrict__ partial,
+    unsigned long long* __restrict__ counters, int32_t gx,
     int32_t gy) {
   // XCD-aware order (speed only, never correctness): workgroups are dealt round-robin
   // over the 8 XCDs, so give every spec group of one node chunk the same b % 8 — the
@@ -488,12 +535,21 @@ __global__ __launch_bounds__(256) void fit_kernel(
   if (by >= gy) return;  // padding of gy up to a multiple of 8 (whole workgroup)
   const int64_t s = (int64_t)bx * 256 + threadIdx.x;
   const bool active = s < S;
-  const uint64_t c = active ? sc[s] : 1;
-  const int64_t m = active ? sm[s] : 1;
-  const double md = active ? smd[s] : 1.0;
-  const float rc = active ? src[s] : 1.f;
-  const float rm = active ? srm[s] : 1.f;
-  const bool normal = active ? (snormal[s] != 0) : true;
+  SpecRec sr;  // one 32-B record per lane (two 16-B loads)
+  if (active) {
+    sr = specs[s];
+  } else {
+    sr.c = 1;
+    sr.m = 1;
+    sr.md = 1.0;
+    sr.rc = 1.f;
+    sr.rm = 1.f;
+  }
+  const uint64_t c = sr.c;
+  const int64_t m = sr.m;
+  const double md = sr.md;
+  const float rc = sr.rc, rm = sr.rm;
+  const bool normal = rc > 0.f;
   const bool wave_fast = __all(normal);
   const int32_t negc = -(int32_t)(uint32_t)c;
   const f32x2 rcm = {rc, rm};
@@ -551,10 +607,14 @@ __global__ __launch_bounds__(256) void fit_kernel(
     for (int64_t i = n0; i < n1; ++i) eval_slow(i);
   }
 
+#ifdef KCC_FIT_DIAG_NO_ATOMICS  // diagnostic timing build only: results are wrong
+  if (active && acc == 0x5A5A5A5A5A5A5A5Aull) partial[s] = (int64_t)acc;
+#else
   if (active) {
     atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[s]), acc);
     if (errs) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[S + s]), errs);
   }
+#endif
   const unsigned long long act = __ballot(active);
   if (slow_iters && (threadIdx.x & 63) == 0)
     atomicAdd(counters, (unsigned long long)slow_iters * (unsigned long long)__popcll(act));
@@ -585,7 +645,7 @@ hipError_t launch_reduce_mark(int64_t n_nodes, int64_t n_containers, const int64
                               uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s) {
   if (n_nodes <= 0) return hipSuccess;
   hipLaunchKernelGGL(reduce_mark_kernel, dim3(grid_for(n_nodes, 256, 8192)), dim3(256), 0, s,
-                     n_nodes, n_containers, node_ptr, wave_node, used_cpu,
+                     n_nodes, n_containers, reduce_range(n_containers), node_ptr, wave_node, used_cpu,
                      reinterpret_cast<uint64_t*>(used_mem), lim_cpu,
                      reinterpret_cast<uint64_t*>(lim_mem));
   return hipGetLastError();
@@ -597,18 +657,19 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t n_containers, const int64_t* n
                          const int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem,
                          uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s) {
   if (n_nodes <= 0 || n_containers <= 0) return hipSuccess;
+  const int32_t range = reduce_range(n_containers);
   const int64_t waves = reduce_n_waves(n_containers);
   const unsigned blocks = (unsigned)((waves + RED_WAVES_PER_BLOCK - 1) / RED_WAVES_PER_BLOCK);
   const bool lim = cpu_lim && mem_lim && lim_cpu && lim_mem;
   if (lim) {
     hipLaunchKernelGGL(reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, n_nodes, n_containers,
-                       node_ptr, cpu_req, reinterpret_cast<const uint64_t*>(mem_req), cpu_lim,
+                       range, node_ptr, cpu_req, reinterpret_cast<const uint64_t*>(mem_req), cpu_lim,
                        reinterpret_cast<const uint64_t*>(mem_lim), wave_node, used_cpu,
                        reinterpret_cast<uint64_t*>(used_mem), lim_cpu,
                        reinterpret_cast<uint64_t*>(lim_mem));
   } else {
     hipLaunchKernelGGL(reduce_kernel<2>, dim3(blocks), dim3(256), 0, s, n_nodes, n_containers,
-                       node_ptr, cpu_req, reinterpret_cast<const uint64_t*>(mem_req),
+                       range, node_ptr, cpu_req, reinterpret_cast<const uint64_t*>(mem_req),
                        (const uint64_t*)nullptr, (const uint64_t*)nullptr, wave_node, used_cpu,
                        reinterpret_cast<uint64_t*>(used_mem), (uint64_t*)nullptr,
                        (uint64_t*)nullptr);
@@ -642,8 +703,9 @@ hipError_t launch_fit(int64_t n_nodes, const FitNode* fast, const SlowNode* slow
                       unsigned long long* counters, hipStream_t s) {
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
   const int64_t gx = (n_specs + 255) / 256;
-  // aim for ~4096 workgroups (16 per CU) so the tail is short; >= 64 nodes each
-  int64_t gy_target = 4096 / gx;
+  // aim for KCC_FIT_TARGET_BLOCKS workgroups (2048 = one full round at 8 per CU); >= 64
+  // nodes each
+  int64_t gy_target = KCC_FIT_TARGET_BLOCKS / gx;
   if (gy_target < 1) gy_target = 1;
   int64_t npb = (n_nodes + gy_target - 1) / gy_target;
   if (npb < 64) npb = 64;
@@ -655,8 +717,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitNode* fast, const SlowNode* slow
   }
   const int64_t blocks = gx * ((gy + 7) / 8 * 8);
   hipLaunchKernelGGL(fit_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, npb, fast,
-                     slow, slow_list, n_specs, sp.c, sp.m, sp.md, sp.rc, sp.rm, sp.normal,
-                     partial, counters, (int32_t)gx, (int32_t)gy);
+                     slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)gx, (int32_t)gy);
   return hipGetLastError();
 }
 

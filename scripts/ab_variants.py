@@ -1,0 +1,118 @@
+"""A/B timing of compile-time kernel variants in ONE process (interleaved rounds).
+
+  python scripts/ab_variants.py build  NAME="-DKNOB=.." ...   (CPU: builds variants/libkcc_NAME.so)
+  python scripts/ab_variants.py run [--config C4] [--rounds 5] [--reps 10] NAME ...   (GPU)
+
+Each variant is the same sources with -D knobs (kcc_internal.h: KCC_RED_PREFETCH,
+KCC_RED_TILES_PER_WAVE, ...), loaded side by side with ctypes.  Times the segmented
+reduce (reduce_requests_async) and the fit (prepare + run) on the same device tensors,
+checks every variant's outputs are identical, prints one JSON line per variant.
+"""
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+VDIR = os.path.join(ROOT, "variants")
+
+
+def build(specs):
+    os.makedirs(VDIR, exist_ok=True)
+    for spec in specs:
+        name, _, flags = spec.partition("=")
+        out = os.path.join(VDIR, f"libkcc_{name}.so")
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "kubernetesclustercapacity_amd", "csrc"),
+                        "variant", f"VOUT={out}", f"EXTRA={flags}"], check=True)
+        print("built", out, flags)
+
+
+def run(names, config, rounds, reps, shard=1):
+    import numpy as np
+    import torch
+
+    from kubernetesclustercapacity_amd import _lib, synth
+
+    dev = torch.device("cuda", 0)
+    n_all = synth.CONFIGS[config]["n_nodes"]
+    cl = synth.config_cluster(config, node_lo=0, node_hi=n_all // shard)  # rank 0 of `shard`
+    sc, sm = synth.config_specs(config)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+    ptr, cpu, mem = T(cl.node_ptr), T(cl.cpu_req), T(cl.mem_req)
+    ac, am, ap, pc = T(cl.alloc_cpu), T(cl.alloc_mem), T(cl.alloc_pods), T(cl.pod_count)
+    s_cpu, s_mem = T(sc), T(sm)
+    n, S, nc = cl.n_nodes, sc.size, cl.n_containers
+    libs, ctxs, outs = {}, {}, {}
+    for nm in names:
+        L = _lib.load(os.path.join(VDIR, f"libkcc_{nm}.so"))
+        h = C.c_void_p()
+        assert L.kcc_create(C.byref(h), 0, 1) == 0, L.kcc_create_error()
+        assert L.kcc_reserve(h, n, nc, S) == 0
+        libs[nm], ctxs[nm] = L, h
+        outs[nm] = dict(uc=torch.empty(n, dtype=torch.int64, device=dev),
+                        um=torch.empty(n, dtype=torch.int64, device=dev),
+                        part=torch.empty(2 * S, dtype=torch.int64, device=dev))
+    P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    stream = torch.cuda.Stream(dev)
+    sh = C.c_void_p(stream.cuda_stream)
+
+    def reduce(nm):
+        o = outs[nm]
+        rc = libs[nm].kcc_reduce_requests_async(ctxs[nm], n, nc, P(ptr), P(cpu), P(mem), None,
+                                                None, P(o["uc"]), P(o["um"]), None, None, sh)
+        assert rc == 0
+
+    def fit(nm):
+        o = outs[nm]
+        L = libs[nm]
+        assert L.kcc_fit_prepare_async(ctxs[nm], n, P(ac), P(am), P(ap), P(pc), P(o["uc"]),
+                                       P(o["um"]), S, P(s_cpu), P(s_mem), P(o["part"]), sh) == 0
+        assert L.kcc_fit_run_async(ctxs[nm], n, S, P(o["part"]), sh) == 0
+
+    times = {nm: {"reduce": [], "fit": []} for nm in names}
+    with torch.cuda.stream(stream):
+        for nm in names:  # warm up
+            reduce(nm)
+            fit(nm)
+        torch.cuda.synchronize()
+        for _ in range(rounds):
+            for nm in names:
+                for what, fn in (("reduce", reduce), ("fit", fit)):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    for _ in range(reps):
+                        fn(nm)
+                    e1.record(stream)
+                    e1.synchronize()
+                    times[nm][what].append(e0.elapsed_time(e1) / reps)
+    ref = names[0]
+    for nm in names:
+        for k in ("uc", "um", "part"):
+            if not nm.startswith("diag_"):  # diagnostic builds are timing-only
+                assert torch.equal(outs[nm][k], outs[ref][k]), f"{nm} differs from {ref} in {k}"
+        r = times[nm]
+        print(json.dumps({"variant": nm, "config": config, "shard": shard,
+                          "reduce_ms_median": float(np.median(r["reduce"])),
+                          "reduce_ms_min": float(np.min(r["reduce"])),
+                          "fit_ms_median": float(np.median(r["fit"])),
+                          "fit_ms_min": float(np.min(r["fit"])),
+                          "reduce_GBps": (nc * 16 + (n + 1) * 8 + n * 16) / (np.median(r["reduce"]) * 1e-3) / 1e9,
+                          "identical_outputs": not nm.startswith("diag_")}))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build(sys.argv[2:])
+    else:
+        import argparse
+        ap = argparse.ArgumentParser()
+        ap.add_argument("cmd")
+        ap.add_argument("names", nargs="+")
+        ap.add_argument("--config", default="C4")
+        ap.add_argument("--rounds", type=int, default=5)
+        ap.add_argument("--reps", type=int, default=10)
+        ap.add_argument("--shard", type=int, default=1, help="use rank 0's nodes of this many")
+        a = ap.parse_args()
+        run(a.names, a.config, a.rounds, a.reps, a.shard)

@@ -1,0 +1,26 @@
+#!/bin/bash
+# Rehearse the multi-rank bench path on a 1-GPU box: N=1 reference, then 2 ranks sharing
+# the GPU over gloo (RCCL refuses two ranks on one device).  The totals checksum must match.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+CFG=${1:-C3}
+timeout -k 10 300 python -u bench.py --config $CFG --no-cpu-baseline --steps 5 --scaling strong > gpurun_out/mr_n1.log 2>&1 || exit $?
+timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+  --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --config $CFG \
+  --dist-backend gloo --steps 5 --scaling strong > gpurun_out/mr_n2.log 2>&1 || exit $?
+timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+  --master-addr 127.0.0.1 --master-port 29532 bench.py --gpus 2 --config $CFG \
+  --dist-backend gloo --steps 5 > gpurun_out/mr_n2w.log 2>&1 || exit $?
+python - <<'PY'
+import json
+a = json.loads(open("gpurun_out/mr_n1.log").read().strip().splitlines()[-1])
+b = json.loads(open("gpurun_out/mr_n2.log").read().strip().splitlines()[-1])
+print("n1", a["value"], a["totals_checksum"], a["n_gpus"])
+print("n2", b["value"], b["totals_checksum"], b["n_gpus"], b["config"]["parallelism"])
+assert a["totals_checksum"] == b["totals_checksum"], "sharded totals differ"
+w = json.loads(open("gpurun_out/mr_n2w.log").read().strip().splitlines()[-1])
+print("n2 weak", w["value"], w["scaling"], w["config"]["nodes"])
+assert w["scaling"] == "weak" and w["config"]["nodes"] == 2 * a["config"]["nodes"]
+print("MULTIRANK OK")
+PY
