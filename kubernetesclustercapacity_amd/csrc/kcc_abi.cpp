@@ -158,7 +158,7 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   const size_t S = (size_t)(n_specs > 0 ? n_specs : 1);
   const int64_t waves = kcc::reduce_max_waves(n_cont > 0 ? n_cont : 1);
   KCC_HIP(ctx, ensure(dv.wave_node, sizeof(int64_t) * (size_t)waves));
-  KCC_HIP(ctx, ensure(dv.fast, sizeof(kcc::FitNode) * N));
+  KCC_HIP(ctx, ensure(dv.fast, sizeof(kcc::FitGroup) * (size_t)kcc::fit_groups((int64_t)N)));
   KCC_HIP(ctx, ensure(dv.slow, sizeof(kcc::SlowNode) * N));
   KCC_HIP(ctx, ensure(dv.slow_list, sizeof(int64_t) * N));
   KCC_HIP(ctx, ensure(dv.srec, sizeof(kcc::SpecRec) * S));
@@ -189,7 +189,7 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
                                      as<unsigned long long>(dv.counters), s));
   if (n_nodes == 0) return KCC_OK;
   KCC_HIP(ctx, kcc::launch_node_prep(n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count,
-                                     used_cpu, used_mem, as<kcc::FitNode>(dv.fast),
+                                     used_cpu, used_mem, as<kcc::FitGroup>(dv.fast),
                                      as<kcc::SlowNode>(dv.slow), as<int64_t>(dv.slow_list),
                                      as<unsigned long long>(dv.counters), s));
   return KCC_OK;
@@ -201,7 +201,7 @@ int fit_run_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_specs, int64_t
     return fail(ctx, KCC_EINVAL, "fit_run sizes differ from the preceding fit_prepare");
   if (n_nodes == 0 || n_specs == 0) return KCC_OK;
   if (!partial) return fail(ctx, KCC_EINVAL, "NULL partial");
-  KCC_HIP(ctx, kcc::launch_fit(n_nodes, as<kcc::FitNode>(dv.fast), as<kcc::SlowNode>(dv.slow),
+  KCC_HIP(ctx, kcc::launch_fit(n_nodes, as<kcc::FitGroup>(dv.fast), as<kcc::SlowNode>(dv.slow),
                                as<int64_t>(dv.slow_list), n_specs, spec_prep_of(dv), partial,
                                as<unsigned long long>(dv.counters), s));
   return KCC_OK;

@@ -55,20 +55,21 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t n_containers, const int64_t* n
                          uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s);
 
 // ---- (b) fit -----------------------------------------------------------------
-// Per-node record streamed by the fit kernel through the scalar cache (32 B, one
-// s_load_dwordx8).
-// Rows outside the fast-path bounds hold an all-zero record (contributes exactly 0)
-// and are listed in slow_list for the exact path.
-struct __attribute__((aligned(32))) FitNode {
-  double fm_d;   // free memory (bytes), exact in f64 on the fast path
-  float fc_f;    // free CPU (millicores), rounded to f32 — quotient estimate only
-  float fm_f;    // free memory, rounded to f32 — quotient estimate only
-  int32_t fc_i;  // free CPU, exact (fast path: 0 <= fc < 2^31)
-  float P_f;     // max(allocatable pods, 0) as f32 (exact on the fast path)
-  int32_t P_i;   // allocatable pods
-  int32_t cl_i;  // clamp value allocatable pods - podCount (CC:135)
+// Node stream of the fit kernel: groups of FIT_GROUP nodes, field-major inside the
+// group (160 B).  fc/P/fm arrive through the scalar cache (SGPR operands of the VALU),
+// cl by one uniform-address vector load (it is a v_cndmask operand, and gfx9 allows a
+// single SGPR/VCC read per VALU instruction).  Rows outside the fast-path bounds, and
+// the padding of the last group, hold all-zero fields (contribute exactly 0: x = 0 >=
+// P = 0 selects cl = 0) and are listed in slow_list for the exact path.
+constexpr int FIT_GROUP = 8;
+struct __attribute__((aligned(32))) FitGroup {
+  float fc[FIT_GROUP];    // free CPU (millicores), exact in f32 on the fast path (< 2^21)
+  int32_t P[FIT_GROUP];   // allocatable pods
+  double fm[FIT_GROUP];   // free memory (bytes), exact in f64 on the fast path (< 2^50)
+  int32_t cl[FIT_GROUP];  // clamp value allocatable pods - podCount (CC:135)
 };
-static_assert(sizeof(FitNode) == 32, "FitNode must be 32 B");
+static_assert(sizeof(FitGroup) == 160, "FitGroup must be 160 B");
+__host__ __device__ inline int64_t fit_groups(int64_t n_nodes) { return (n_nodes + FIT_GROUP - 1) / FIT_GROUP; }
 
 // Raw per-node values for the exact path (fc/fm are 0 where the reference's
 // `alloc <= used` branch yields 0, i.e. no division happens).
@@ -84,11 +85,11 @@ static_assert(sizeof(SlowNode) == 32, "SlowNode must be 32 B");
 // satisfy the fast-path bounds first, the rest after (so at most one wavefront mixes
 // both).  rc == 0 marks a spec for the exact path (a fast-path rc is > 0).
 struct __attribute__((aligned(32))) SpecRec {
-  uint64_t c;   // cpu request (millicores)
-  int64_t m;    // memory request (bytes)
-  double md;    // m as f64
-  float rc;     // (1 + 2^-20)/c (f32): biased up, see fit_fast; 0 off the fast path
-  float rm;     // (1 + 2^-20)/m (f32)
+  uint64_t c;    // cpu request (millicores)
+  int64_t m;     // memory request (bytes)
+  double rm;     // smallest f64 >= 1/m (see fit_fast)
+  float rc;      // smallest f32 >= 1/c; 0 marks a spec off the fast path
+  uint32_t pad;
 };
 static_assert(sizeof(SpecRec) == 32, "SpecRec must be 32 B");
 
@@ -97,9 +98,8 @@ struct SpecPrep {
   int32_t* perm;  // internal index -> caller index
 };
 
-// counters: [0] (node, spec) pairs on the exact path, [1] rows in slow_list,
-// [2] largest fast-path spec cpu request.  spec_prep zeroes partial[0..2S) and
-// counters[0..1] and writes counters[2]; node_prep reads it and appends to slow_list.
+// counters: [0] (node, spec) pairs on the exact path, [1] rows in slow_list.
+// spec_prep zeroes partial[0..2S) and counters[0..1]; node_prep appends to slow_list.
 hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
                             const int64_t* spec_mem, SpecPrep sp, int64_t* partial,
                             unsigned long long* counters, hipStream_t s);
@@ -107,11 +107,11 @@ hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
 hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
-                            const int64_t* used_mem, FitNode* fast, SlowNode* slow,
+                            const int64_t* used_mem, FitGroup* fast, SlowNode* slow,
                             int64_t* slow_list, unsigned long long* counters, hipStream_t s);
 
 // partial[0..S) += Σ_i q(i,s), partial[S..2S) += #div-by-zero rows (internal order).
-hipError_t launch_fit(int64_t n_nodes, const FitNode* fast, const SlowNode* slow,
+hipError_t launch_fit(int64_t n_nodes, const FitGroup* fast, const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, hipStream_t s);
 

@@ -307,42 +307,40 @@ __global__ __launch_bounds__(256) void reduce_kernel(
 // (b) fit
 // ----------------------------------------------------------------------------
 
-// Fast-path bounds (see DESIGN.md "fit kernel: exactness argument").
-constexpr uint64_t FAST_FC_MAX = 1ull << 31;    // free CPU < 2^31
-constexpr int64_t FAST_FM_MAX = 1ll << 53;      // 0 <= free mem < 2^53
-constexpr int64_t FAST_P_MAX = 1ll << 16;       // allocatable pods <= 2^16
-constexpr int64_t FAST_P_MIN = -(1ll << 20);
+// Fast-path bounds (see DESIGN.md "Fit fast path: exactness argument").
+constexpr uint64_t FAST_FC_MAX = 1ull << 21;    // free CPU < 2^21 (f32 quotient exact)
+constexpr int64_t FAST_FM_MAX = 1ll << 50;      // 0 <= free mem < 2^50 (f64 quotient exact)
+constexpr int64_t FAST_P_ABS = 1ll << 20;       // |allocatable pods| <= 2^20
 constexpr int64_t FAST_CL_ABS = 1ll << 20;      // |allocPods - podCount| <= 2^20
-constexpr uint64_t FAST_C_MAX = 1ull << 23;     // 1 <= spec cpu < 2^23
-constexpr int64_t FAST_M_MAX = 1ll << 37;       // 1 <= spec mem < 2^37
-constexpr double FIT_RECIP_BIAS = 1.0 + 0x1p-20;  // see fit_fast
+constexpr uint64_t FAST_C_MAX = 1ull << 22;     // 1 <= spec cpu < 2^22
+constexpr int64_t FAST_M_MAX = 1ll << 51;       // 1 <= spec mem < 2^51
 
 __device__ __forceinline__ bool spec_is_normal(uint64_t c, int64_t m) {
   return c >= 1 && c < FAST_C_MAX && m >= 1 && m < FAST_M_MAX;
 }
 
 // Per-node free capacity (CC:119-135 operands).  Rows that fit the fast-path
-// bounds get an exact FitNode; the others get a FitNode that contributes exactly 0
-// on the fast path and are appended to slow_list for the exact 64-bit path.
-// counters[2] holds the largest fast-path spec cpu request (from spec_prep), which
-// bounds P so that k*c fits in i32 for every spec.
+// bounds get exact FitGroup fields; the others get all-zero fields (contribute
+// exactly 0 on the fast path) and are appended to slow_list for the exact 64-bit
+// path.  Covers the padding of the last group too (zero fields, not listed).
 __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_cpu,
                                  const int64_t* __restrict__ alloc_mem,
                                  const int64_t* __restrict__ alloc_pods,
                                  const int64_t* __restrict__ pod_count,
                                  const uint64_t* __restrict__ used_cpu,
                                  const int64_t* __restrict__ used_mem,
-                                 FitNode* __restrict__ fast, SlowNode* __restrict__ slow,
+                                 FitGroup* __restrict__ fast, SlowNode* __restrict__ slow,
                                  int64_t* __restrict__ slow_list,
                                  unsigned long long* __restrict__ counters) {
-  const uint64_t cmax = counters[2];
-  int64_t p_cap = cmax ? (int64_t)(0x7fffffffull / cmax) : 0x7fffffffll;
-  if (p_cap > FAST_P_MAX) p_cap = FAST_P_MAX;
   const int lane = threadIdx.x & 63;
+  const int64_t n_pad = fit_groups(n) * FIT_GROUP;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i - lane < n; i += stride) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i - lane < n_pad; i += stride) {
     const bool valid = i < n;
     bool ok = false;
+    float fc_f = 0.f;
+    double fm_d = 0.0;
+    int32_t P_i = 0, cl_i = 0;
     if (valid) {
       const uint64_t ac = alloc_cpu[i], uc = used_cpu[i];
       const int64_t am = alloc_mem[i], um = used_mem[i];
@@ -350,23 +348,28 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
       const uint64_t fc = ac > uc ? ac - uc : 0;                                  // CC:119-123
       const int64_t fm = am > um ? (int64_t)((uint64_t)am - (uint64_t)um) : 0;   // CC:125-129
       const int64_t cl = (int64_t)((uint64_t)P - (uint64_t)pc);                  // CC:135
-      ok = fc < FAST_FC_MAX && fm >= 0 && fm < FAST_FM_MAX && P >= FAST_P_MIN &&
-           P <= p_cap && cl >= -FAST_CL_ABS && cl <= FAST_CL_ABS;
-      FitNode f;  // rows off the fast path: all-zero record, contributes exactly 0
-      f.fm_d = ok ? (double)fm : 0.0;
-      f.fc_f = ok ? (float)fc : 0.f;                  // one rounding (fc < 2^31)
-      f.fm_f = ok ? (float)(double)fm : 0.f;          // exact in f64, one rounding to f32
-      f.fc_i = ok ? (int32_t)fc : 0;
-      f.P_f = ok && P > 0 ? (float)P : 0.f;
-      f.P_i = ok ? (int32_t)P : 0;
-      f.cl_i = ok ? (int32_t)cl : 0;
-      fast[i] = f;
+      ok = fc < FAST_FC_MAX && fm >= 0 && fm < FAST_FM_MAX && P >= -FAST_P_ABS &&
+           P <= FAST_P_ABS && cl >= -FAST_CL_ABS && cl <= FAST_CL_ABS;
+      if (ok) {
+        fc_f = (float)fc;  // exact (< 2^21)
+        fm_d = (double)fm;  // exact (< 2^50)
+        P_i = (int32_t)P;
+        cl_i = (int32_t)cl;
+      }
       SlowNode sn;
       sn.fc = fc;
       sn.fm = fm;
       sn.P = P;
       sn.cl = cl;
       slow[i] = sn;
+    }
+    if (i < n_pad) {
+      FitGroup& g = fast[i / FIT_GROUP];
+      const int k = (int)(i % FIT_GROUP);
+      g.fc[k] = fc_f;
+      g.P[k] = P_i;
+      g.fm[k] = fm_d;
+      g.cl[k] = cl_i;
     }
     const unsigned long long b = __ballot(valid && !ok);
     if (b) {
@@ -378,16 +381,27 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
   }
 }
 
+// Smallest f32 >= 1/c and smallest f64 >= 1/m (the fit's quotients never undershoot).
+__device__ __forceinline__ float recip_up_f32(uint64_t c) {
+  float r = (float)(1.0 / (double)c);               // c < 2^22: r*c is exact in f64
+  if ((double)r * (double)c < 1.0) r = __uint_as_float(__float_as_uint(r) + 1u);  // next f32 up
+  return r;
+}
+__device__ __forceinline__ double recip_up_f64(int64_t m) {
+  const double md = (double)m;                       // exact (m < 2^51)
+  double r = 1.0 / md;
+  if (fma(r, md, -1.0) < 0.0) r = __longlong_as_double(__double_as_longlong(r) + 1);  // next up
+  return r;
+}
+
 // Single-workgroup stable partition of the specs (fast-path specs first), in two
 // passes over contiguous per-thread chunks with one block-wide exclusive scan in
-// between.  Also zeroes partial[0..2S) and counters[0..1] (no memset launches) and
-// writes counters[2] = the largest fast-path cpu request.
+// between.  Also zeroes partial[0..2S) and counters[0..1] (no memset launches).
 __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64_t* __restrict__ c_in,
                                                          const int64_t* __restrict__ m_in,
                                                          SpecPrep sp, int64_t* __restrict__ partial,
                                                          unsigned long long* __restrict__ counters) {
   __shared__ int64_t wsum[16];
-  __shared__ unsigned long long wmax[16];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t per = (S + 1023) / 1024;
   const int64_t b0 = tid * per < S ? tid * per : S;
@@ -424,14 +438,7 @@ __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64
     return m_in[i];
   };
   int64_t cnt = 0;
-  unsigned long long cmax = 0;
-  for (int64_t i = b0; i < b1; ++i) {
-    const uint64_t c = spec_c(i);
-    if (spec_is_normal(c, spec_m(i))) {
-      ++cnt;
-      cmax = c > cmax ? c : cmax;
-    }
-  }
+  for (int64_t i = b0; i < b1; ++i) cnt += spec_is_normal(spec_c(i), spec_m(i)) ? 1 : 0;
   // block exclusive scan of cnt (wave shuffles + 16 wave totals in LDS)
   int64_t incl = cnt;
 #pragma unroll
@@ -439,21 +446,12 @@ __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64
     const int64_t u = __shfl_up(incl, d);
     if (lane >= d) incl += u;
   }
-  unsigned long long mx = cmax;
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const unsigned long long o = __shfl_xor(mx, d);
-    mx = o > mx ? o : mx;
-  }
   if (lane == 63) wsum[wv] = incl;
-  if (lane == 0) wmax[wv] = mx;
   __syncthreads();
   int64_t wbase = 0, tot_n = 0;
-  unsigned long long gmax = 0;
   for (int k = 0; k < 16; ++k) {
     if (k < wv) wbase += wsum[k];
     tot_n += wsum[k];
-    gmax = wmax[k] > gmax ? wmax[k] : gmax;
   }
   int64_t pn = wbase + incl - cnt;  // my first fast-path slot
   int64_t pa = tot_n + (b0 - (wbase + incl - cnt));  // my first exact-path slot
@@ -465,11 +463,9 @@ __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64
     SpecRec r;
     r.c = c;
     r.m = m;
-    r.md = (double)m;
-    // reciprocals biased up by 2^-20 so the fit's quotient estimate never
-    // undershoots (f64 division, then one rounding to f32)
-    r.rc = nm ? (float)(FIT_RECIP_BIAS / (double)c) : 0.f;
-    r.rm = nm ? (float)(FIT_RECIP_BIAS / (double)m) : 0.f;
+    r.rm = nm ? recip_up_f64(m) : 0.0;
+    r.rc = nm ? recip_up_f32(c) : 0.f;
+    r.pad = 0;
     sp.rec[pos] = r;
     sp.perm[pos] = (int32_t)i;
   }
@@ -477,59 +473,54 @@ __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64
   if (tid == 0) {
     counters[0] = 0;
     counters[1] = 0;
-    counters[2] = gmax;
   }
 }
 
 // Lane = spec (its request, reciprocals and running total live in VGPRs); the node
-// stream is wave-uniform, so each 32-B FitNode arrives by one scalar load and feeds
-// the VALU as SGPR operands.  The main loop is branch-free: rows outside the fast
-// bounds carry a zero-contribution FitNode and are re-done exactly from slow_list.
-// No cross-lane reduction until the block's end (one 64-bit atomic per spec).
+// stream is wave-uniform: fc/P/fm of a FitGroup arrive by scalar loads and feed the
+// VALU as SGPR operands, cl by one uniform-address buffer load.  The main loop is
+// branch-free: rows outside the fast bounds carry zero fields and are re-done exactly
+// from slow_list.  No cross-lane reduction until the block's end (one 64-bit atomic
+// per spec).
 //
-// Fast path per (node, spec), exact (DESIGN.md "fit kernel: exactness argument"):
-//   the spec reciprocals are biased up by 2^-20 (spec_prep), so the f32 estimate
-//   e = min(fc*rc, fm*rm, P) satisfies t <= e < t + 1 for t = min(qc, qm, P)
-//   (its relative error is below 4*2^-24, and t <= P <= 2^16): k = floor(e) is t
-//   or t + 1, never below.  One exact check fixes it:
-//     rcpu = fc - k*c      i32 (v_mad_i32_i24; k*c < 2^31 by node_prep's P cap)
-//     rmem = fm - k*m      f64 fma, exact (every value an integer < 2^53)
-//     t    = k - [rcpu < 0 or rmem < 0]          (sign bits: no compares)
-//   contribution = t >= P ? P - podCount : t                       (CC:133-136)
+// Fast path per (node, spec), exact (DESIGN.md "Fit fast path: exactness argument"):
+//   rc = smallest f32 >= 1/c, rm = smallest f64 >= 1/m (spec_prep); fc < 2^21 and
+//   fm < 2^50 are exact in f32 / f64.  Then with round-to-nearest products
+//     qc = trunc(RN32(fc * rc)) = floor(fc / c)          (fc < 2^21, c < 2^22)
+//     qm = sat_i32(trunc(RN64(fm * rm))) = min(floor(fm / m), 2^31 - 1)
+//   with no correction step: an integer quotient is never rounded below (the
+//   reciprocal is rounded up), and a non-integer one lies >= 1/c below the next
+//   integer, more than the relative error 2^-23 (2^-52) can cover at these sizes.
+//   x = min(qc, qm)                       findMin (CC:159-164)
+//   contribution = x >= P ? P - podCount : x                       (CC:133-136)
+// (x only saturates far above P <= 2^20, where the comparison is the same.)
+// Per node and 64-spec wavefront: v_pk_mul_f32 (two nodes), 2x v_cvt, v_mul_f64,
+// v_min_i32, v_cmp, v_cndmask, v_add3_u32 (two nodes) = 7 VALU instructions.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef int32_t i32x8 __attribute__((ext_vector_type(8)));
+typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ int32_t fit_fast(const FitNode& nd, f32x2 rcm, double md,
-                                            int32_t negc) {
-  const f32x2 q = f32x2{nd.fc_f, nd.fm_f} * rcm;  // one v_pk_mul_f32
-  const float e = fminf(fminf(q.x, q.y), nd.P_f);  // t <= e < t + 1
-  const int32_t k = (int32_t)e;
-  const int32_t rcpu = __mul24(k, negc) + nd.fc_i;
-  const double rmem = fma(-(double)k, md, nd.fm_d);
-  const int32_t hi = (int32_t)(__double_as_longlong(rmem) >> 32);
-  const int32_t t = k + ((rcpu | hi) >> 31);
-  return (t >= nd.P_i) ? nd.cl_i : t;
+// v_cvt_i32_f64 saturates out-of-range values in hardware (C's conversion is UB there)
+__device__ __forceinline__ int32_t cvt_i32_sat(double x) {
+  int32_t r;
+  asm("v_cvt_i32_f64 %0, %1" : "=v"(r) : "v"(x));
+  return r;
 }
 
-constexpr int FIT_UNROLL = 8;
+constexpr int FIT_CHUNK_GROUPS = 128;  // 1024 nodes: |sum of contributions| <= 2^30 in i32
 #ifndef KCC_FIT_TARGET_BLOCKS
 #define KCC_FIT_TARGET_BLOCKS 16384
 #endif
-typedef int32_t i32x8 __attribute__((ext_vector_type(8)));
-
-// one s_load_dwordx8 per record (a vector load is never split into field loads)
-__device__ __forceinline__ FitNode load_node(const i32x8* __restrict__ q, int i) {
-  return __builtin_bit_cast(FitNode, q[i]);
-}
 
 __global__ __launch_bounds__(256) void fit_kernel(
-    int64_t n_nodes, int64_t nodes_per_block, const FitNode* __restrict__ fast,
+    int64_t n_nodes, int64_t groups_per_block, const FitGroup* __restrict__ fast,
     const SlowNode* __restrict__ slow, const int64_t* __restrict__ slow_list, int64_t S,
     const SpecRec* __restrict__ specs, int64_t* __restrict__ partial,
-    unsigned long long* __restrict__ counters, int32_t gx,
-    int32_t gy) {
+    unsigned long long* __restrict__ counters, int32_t gx, int32_t gy) {
   // XCD-aware order (speed only, never correctness): workgroups are dealt round-robin
   // over the 8 XCDs, so give every spec group of one node chunk the same b % 8 — the
-  // chunk's FitNode records then stay in that XCD's L2 for all of them.
+  // chunk's FitGroup records then stay in that XCD's L2 for all of them.
   const int32_t b = blockIdx.x, xcd = b & 7, r = b >> 3;
   const int32_t bx = r % gx, by = (r / gx) * 8 + xcd;
   if (by >= gy) return;  // padding of gy up to a multiple of 8 (whole workgroup)
@@ -541,21 +532,20 @@ __global__ __launch_bounds__(256) void fit_kernel(
   } else {
     sr.c = 1;
     sr.m = 1;
-    sr.md = 1.0;
+    sr.rm = 1.0;
     sr.rc = 1.f;
-    sr.rm = 1.f;
   }
   const uint64_t c = sr.c;
   const int64_t m = sr.m;
-  const double md = sr.md;
-  const float rc = sr.rc, rm = sr.rm;
+  const double rm = sr.rm;
+  const float rc = sr.rc;
   const bool normal = rc > 0.f;
   const bool wave_fast = __all(normal);
-  const int32_t negc = -(int32_t)(uint32_t)c;
-  const f32x2 rcm = {rc, rm};
+  const f32x2 rcc = {rc, rc};
 
-  const int64_t n0 = (int64_t)by * nodes_per_block;
-  const int64_t n1 = n0 + nodes_per_block < n_nodes ? n0 + nodes_per_block : n_nodes;
+  const int64_t n_groups = fit_groups(n_nodes);
+  const int64_t g0 = (int64_t)by * groups_per_block;
+  const int64_t g1 = g0 + groups_per_block < n_groups ? g0 + groups_per_block : n_groups;
   uint64_t acc = 0;
   uint64_t errs = 0;
   uint32_t slow_iters = 0;
@@ -582,29 +572,53 @@ __global__ __launch_bounds__(256) void fit_kernel(
   };
 
   if (wave_fast) {
-    const i32x8* p = reinterpret_cast<const i32x8*>(fast + n0);
-    const int cnt = (int)(n1 - n0);
-    for (int cb = 0; cb < cnt; cb += 1024) {
-      const int ce = cb + 1024 < cnt ? cb + 1024 : cnt;
-      int32_t acc32 = 0;  // |contribution| <= 2^20: 1024 of them fit in i32
-      int i = cb;
-      for (; i + FIT_UNROLL <= ce; i += FIT_UNROLL) {
-        // index opaque to loop-strength reduction: one base per group, positive
-        // immediate offsets -> FIT_UNROLL s_load_dwordx8, no per-field address math
-        int io = i;
+    // cl through a buffer descriptor over this block's groups: uniform offsets, no VGPR
+    // address (every lane reads the same 16 B)
+    const FitGroup* gbase = fast + g0;
+    const int cnt = (int)(g1 - g0);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)gbase, (short)0, cnt * (int)sizeof(FitGroup), 0x00020000);
+    for (int cb = 0; cb < cnt; cb += FIT_CHUNK_GROUPS) {
+      const int ce = cb + FIT_CHUNK_GROUPS < cnt ? cb + FIT_CHUNK_GROUPS : cnt;
+      int32_t acc32 = 0;
+      for (int gi = cb; gi < ce; ++gi) {
+        // index opaque to loop-strength reduction: one base per group, immediate offsets
+        int io = gi;
         asm volatile("" : "+s"(io));
-        const i32x8* q = p + io;
+        const FitGroup* g = gbase + io;
+        const int so = io * (int)sizeof(FitGroup) + (int)offsetof(FitGroup, cl);
+        const i32x4 c0 = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, so, 0));
+        const i32x4 c1 = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, so + 16, 0));
+        const i32x8 fcv = *reinterpret_cast<const i32x8*>(g->fc);
+        const i32x8 Pv = *reinterpret_cast<const i32x8*>(g->P);
+        const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
+        const int32_t cl[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
-        for (int u = 0; u < FIT_UNROLL; ++u) acc32 += fit_fast(load_node(q, u), rcm, md, negc);
+        for (int u = 0; u < FIT_GROUP / 2; ++u) {
+          const f32x2 fc2 = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
+          const f32x2 ec = fc2 * rcc;  // one v_pk_mul_f32 for two nodes
+          int32_t x[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int k = 2 * u + h;
+            const double fmk = __longlong_as_double(((int64_t)(uint32_t)fmv[2 * k + 1] << 32) |
+                                                    (uint32_t)fmv[2 * k]);
+            const int32_t qc = (int32_t)ec[h];
+            const int32_t qm = cvt_i32_sat(fmk * rm);
+            const int32_t xm = qc < qm ? qc : qm;
+            x[h] = xm >= Pv[k] ? cl[k] : xm;
+          }
+          acc32 += x[0] + x[1];
+        }
       }
-      for (; i < ce; ++i) acc32 += fit_fast(load_node(p, i), rcm, md, negc);
       acc += (uint64_t)(int64_t)acc32;
     }
     // rows outside the fast bounds, shared out over the node-chunk blocks
     const int64_t n_slow = (int64_t)counters[1];
     for (int64_t j = by; j < n_slow; j += gy) eval_slow(slow_list[j]);
   } else {
-    for (int64_t i = n0; i < n1; ++i) eval_slow(i);
+    const int64_t i1 = g1 * FIT_GROUP < n_nodes ? g1 * FIT_GROUP : n_nodes;
+    for (int64_t i = g0 * FIT_GROUP; i < i1; ++i) eval_slow(i);
   }
 
 #ifdef KCC_FIT_DIAG_NO_ATOMICS  // diagnostic timing build only: results are wrong
@@ -680,10 +694,10 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t n_containers, const int64_t* n
 hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
-                            const int64_t* used_mem, FitNode* fast, SlowNode* slow,
+                            const int64_t* used_mem, FitGroup* fast, SlowNode* slow,
                             int64_t* slow_list, unsigned long long* counters, hipStream_t s) {
   if (n_nodes <= 0) return hipSuccess;
-  hipLaunchKernelGGL(node_prep_kernel, dim3(grid_for(n_nodes, 256, 8192)), dim3(256), 0, s,
+  hipLaunchKernelGGL(node_prep_kernel, dim3(grid_for(fit_groups(n_nodes) * FIT_GROUP, 256, 8192)), dim3(256), 0, s,
                      n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu, used_mem,
                      fast, slow, slow_list, counters);
   return hipGetLastError();
@@ -698,25 +712,28 @@ hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu, const int
   return hipGetLastError();
 }
 
-hipError_t launch_fit(int64_t n_nodes, const FitNode* fast, const SlowNode* slow,
+hipError_t launch_fit(int64_t n_nodes, const FitGroup* fast, const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, hipStream_t s) {
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
   const int64_t gx = (n_specs + 255) / 256;
-  // aim for KCC_FIT_TARGET_BLOCKS workgroups (2048 = one full round at 8 per CU); >= 64
-  // nodes each
+  const int64_t n_groups = fit_groups(n_nodes);
+  // aim for KCC_FIT_TARGET_BLOCKS workgroups (2048 = one full round at 8 per CU); >= 8
+  // groups (64 nodes) each
   int64_t gy_target = KCC_FIT_TARGET_BLOCKS / gx;
   if (gy_target < 1) gy_target = 1;
-  int64_t npb = (n_nodes + gy_target - 1) / gy_target;
-  if (npb < 64) npb = 64;
-  int64_t gy = (n_nodes + npb - 1) / npb;
-  // 1-D grid of gx * roundup(gy, 8) workgroups, remapped XCD-aware in the kernel
+  int64_t gpb = (n_groups + gy_target - 1) / gy_target;
+  if (gpb < 8) gpb = 8;
+  int64_t gy = (n_groups + gpb - 1) / gpb;
+  // 1-D grid of gx * roundup(gy, 8) workgroups, remapped XCD-aware in the kernel; the
+  // buffer descriptor of a block's groups needs gpb * 160 B < 2^31
   while (gx * ((gy + 7) / 8 * 8) > 0x7fffffffLL) {
-    npb *= 2;
-    gy = (n_nodes + npb - 1) / npb;
+    gpb *= 2;
+    gy = (n_groups + gpb - 1) / gpb;
   }
+  if (gpb * (int64_t)sizeof(FitGroup) >= 0x7fffffffLL) return hipErrorInvalidValue;
   const int64_t blocks = gx * ((gy + 7) / 8 * 8);
-  hipLaunchKernelGGL(fit_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, npb, fast,
+  hipLaunchKernelGGL(fit_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, gpb, fast,
                      slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)gx, (int32_t)gy);
   return hipGetLastError();
 }

@@ -42,6 +42,11 @@ def edge_case():
         (2**31, 2**53, 110, 0, []),                                     # just past them
         (5, 5, 110, 200, [(1, 1), (1, 1), (1, 1)]),                     # tiny free
         (100, 100, 3, 1 << 30, []),                                     # |clamp| > 2^20
+        (2**21 - 1, 2**50 - 1, 110, 0, []),                             # fit fast-path edges
+        (2**21, 2**50, 110, 0, []),                                     # just past them
+        (2**21 - 1, 2**50 - 1, 1 << 20, 0, []),                         # P at its bound
+        (2**21 - 1, 2**50 - 1, (1 << 20) + 1, 0, []),                   # P past it
+        (4_194_302, 2**51 - 2, 2, 1, []),                               # 2 x (spec edge)
     ]
     alloc_cpu = np.array([r[0] for r in rows], np.uint64)
     alloc_mem = np.array([r[1] for r in rows], np.int64)
@@ -55,10 +60,12 @@ def edge_case():
         ptr.append(len(cpu))
     cpu = np.array(cpu, np.uint64)
     mem = np.array(mem, np.int64)
-    spec_cpu = np.array([200, 100, 1, 3, 7, 8000, 0, 1 << 23, 2**63, 50, 1, 2**23 - 1],
+    spec_cpu = np.array([200, 100, 1, 3, 7, 8000, 0, 1 << 23, 2**63, 50, 1, 2**23 - 1,
+                         2**22 - 1, 2**22, 2**21 - 1, 1],
                         np.uint64)
     spec_mem = np.array([262_144_000, 104_857_600, 1, 1 << 20, -1, 1 << 35, 1 << 20, 0,
-                         -(1 << 63), 2**37, 2**37 - 1, 3], np.int64)
+                         -(1 << 63), 2**37, 2**37 - 1, 3, 2**51 - 1, 7, 2**50 - 1, 2**51],
+                        np.int64)
     return dict(alloc_cpu=alloc_cpu, alloc_mem=alloc_mem, alloc_pods=alloc_pods,
                 pod_count=pod_count, node_ptr=np.array(ptr, np.int64), cpu_req=cpu,
                 mem_req=mem, cpu_lim=cpu * np.uint64(3), mem_lim=mem * 3,

@@ -134,9 +134,11 @@ def test_fast_path_boundaries(engine):
     """Quotients landing exactly on / next to integers and on the pod clamp."""
     rng = np.random.default_rng(5)
     n = 6_000
-    sc = np.array([1, 2, 3, 7, 50, 100, 200, 250, 333, 1000, 4096, 8000, 8388607], np.uint64)
+    sc = np.array([1, 2, 3, 7, 50, 100, 200, 250, 333, 1000, 4096, 8000, 8388607, 4194303,
+                   1048573, 2**21], np.uint64)
     sm = np.array([1, 3, 1 << 20, 104_857_600, 262_144_000, 1 << 30, 3 << 30, 2**37 - 1,
-                   999_999_937, 5, 64 << 20, 1_000_000, 7], np.int64)
+                   999_999_937, 5, 64 << 20, 1_000_000, 7, 2**51 - 1, 2**44 + 7, 2**47 - 5],
+                  np.int64)
     k = rng.integers(0, 300, n)
     j = rng.integers(0, len(sc), n)
     alloc_cpu = (k * sc[j].astype(np.int64) + rng.integers(-1, 2, n)).clip(0).astype(np.uint64)

@@ -1,8 +1,9 @@
 """Static ISA checks of the gfx950 kernels (CPU: hipcc cross-compiles).
 
-  - the fit kernel's fast loop: FIT_UNROLL s_load_dwordx8 node loads, no vector
-    memory, no 64-bit integer division, and exactly bench.FIT_VALU_PER_NODE_WAVE VALU
-    instructions per node (the VALU-roofline accounting of bench.py);
+  - the fit kernel's fast loop, one 8-node FitGroup per iteration: 32 dwords of scalar
+    loads (fc, P, fm), two uniform 16-B buffer loads (cl), no 64-bit integer division,
+    no correction multiply, and exactly bench.FIT_VALU_PER_NODE_WAVE VALU instructions
+    per node (the VALU-roofline accounting of bench.py);
   - no kernel spills to scratch.
 """
 import os
@@ -38,18 +39,24 @@ def test_fit_fast_loop(asm):
     import bench
     body = kernel_body(asm, "fit_kernel")
     i = body.index(";;#ASMSTART")
-    loop = body[i:body.index("s_cbranch", i)]
-    lines = [ln.strip() for ln in loop.splitlines()]
+    loop = body[body.rfind(".LBB", 0, i):body.index("s_cbranch", i)]
+    lines = [ln.strip() for ln in loop.splitlines()
+             if ln.strip() and not ln.strip().startswith(";")]
     valu = [ln for ln in lines if ln.startswith("v_")]
-    unroll = 8
+    group = 8  # nodes per FitGroup = per loop iteration
     width = {"s_load_dword": 1, "s_load_dwordx2": 2, "s_load_dwordx4": 4, "s_load_dwordx8": 8,
              "s_load_dwordx16": 16}
     dwords = sum(width[ln.split()[0]] for ln in lines if ln.startswith("s_load_dword"))
-    assert dwords == unroll * 8  # exactly the 32-B FitNode of each node, scalar loads
-    assert not any(ln.startswith(("global_load", "flat_load", "buffer_load")) for ln in lines)
-    assert len(valu) / unroll == pytest.approx(bench.FIT_VALU_PER_NODE_WAVE, abs=1e-9), \
-        f"{len(valu)} VALU / {unroll} nodes: update bench.FIT_VALU_PER_NODE_WAVE"
-    assert any(ln.startswith("v_pk_mul_f32") for ln in lines)
+    assert dwords == group * 4  # fc (f32), P (i32), fm (f64) of each node
+    vmem = [ln for ln in lines if ln.startswith(("global_load", "flat_load", "buffer_load"))]
+    assert len(vmem) == 2 and all(ln.startswith("buffer_load_dwordx4") and ", off," in ln
+                                  for ln in vmem)  # cl: uniform address, no VGPR offset
+    assert len(valu) / group == pytest.approx(bench.FIT_VALU_PER_NODE_WAVE, abs=1e-9), \
+        f"{len(valu)} VALU / {group} nodes: update bench.FIT_VALU_PER_NODE_WAVE"
+    ops = [ln.split()[0] for ln in valu]
+    assert ops.count("v_pk_mul_f32") == group // 2
+    assert ops.count("v_mul_f64") == group and ops.count("v_cvt_i32_f64") == group
+    assert not any(o.startswith(("v_mad", "v_fma", "v_mul_lo", "v_mul_hi")) for o in ops)
 
 
 def test_no_scratch(asm):
