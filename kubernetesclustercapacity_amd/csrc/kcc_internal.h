@@ -56,19 +56,19 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t n_containers, const int64_t* n
 
 // ---- (b) fit -----------------------------------------------------------------
 // Node stream of the fit kernel: groups of FIT_GROUP nodes, field-major inside the
-// group (160 B).  fc/P/fm arrive through the scalar cache (SGPR operands of the VALU),
+// group (192 B).  fc/fm/P arrive through the scalar cache (SGPR operands of the VALU),
 // cl by one uniform-address vector load (it is a v_cndmask operand, and gfx9 allows a
 // single SGPR/VCC read per VALU instruction).  Rows outside the fast-path bounds, and
 // the padding of the last group, hold all-zero fields (contribute exactly 0: x = 0 >=
 // P = 0 selects cl = 0) and are listed in slow_list for the exact path.
 constexpr int FIT_GROUP = 8;
-struct __attribute__((aligned(32))) FitGroup {
-  float fc[FIT_GROUP];    // free CPU (millicores), exact in f32 on the fast path (< 2^21)
-  int32_t P[FIT_GROUP];   // allocatable pods
+struct __attribute__((aligned(64))) FitGroup {
+  double fc[FIT_GROUP];   // free CPU (millicores), exact in f64 on the fast path (< 2^50)
   double fm[FIT_GROUP];   // free memory (bytes), exact in f64 on the fast path (< 2^50)
+  int32_t P[FIT_GROUP];   // allocatable pods
   int32_t cl[FIT_GROUP];  // clamp value allocatable pods - podCount (CC:135)
 };
-static_assert(sizeof(FitGroup) == 160, "FitGroup must be 160 B");
+static_assert(sizeof(FitGroup) == 192, "FitGroup must be 192 B");
 __host__ __device__ inline int64_t fit_groups(int64_t n_nodes) { return (n_nodes + FIT_GROUP - 1) / FIT_GROUP; }
 
 // Raw per-node values for the exact path (fc/fm are 0 where the reference's
@@ -87,9 +87,8 @@ static_assert(sizeof(SlowNode) == 32, "SlowNode must be 32 B");
 struct __attribute__((aligned(32))) SpecRec {
   uint64_t c;    // cpu request (millicores)
   int64_t m;     // memory request (bytes)
-  double rm;     // smallest f64 >= 1/m (see fit_fast)
-  float rc;      // smallest f32 >= 1/c; 0 marks a spec off the fast path
-  uint32_t pad;
+  double rc;     // smallest f64 >= 1/c (see fit_kernel); 0 marks a spec off the fast path
+  double rm;     // smallest f64 >= 1/m
 };
 static_assert(sizeof(SpecRec) == 32, "SpecRec must be 32 B");
 

@@ -308,11 +308,11 @@ __global__ __launch_bounds__(256) void reduce_kernel(
 // ----------------------------------------------------------------------------
 
 // Fast-path bounds (see DESIGN.md "Fit fast path: exactness argument").
-constexpr uint64_t FAST_FC_MAX = 1ull << 21;    // free CPU < 2^21 (f32 quotient exact)
+constexpr uint64_t FAST_FC_MAX = 1ull << 50;    // free CPU < 2^50 (f64 quotient exact)
 constexpr int64_t FAST_FM_MAX = 1ll << 50;      // 0 <= free mem < 2^50 (f64 quotient exact)
 constexpr int64_t FAST_P_ABS = 1ll << 20;       // |allocatable pods| <= 2^20
 constexpr int64_t FAST_CL_ABS = 1ll << 20;      // |allocPods - podCount| <= 2^20
-constexpr uint64_t FAST_C_MAX = 1ull << 22;     // 1 <= spec cpu < 2^22
+constexpr uint64_t FAST_C_MAX = 1ull << 51;     // 1 <= spec cpu < 2^51
 constexpr int64_t FAST_M_MAX = 1ll << 51;       // 1 <= spec mem < 2^51
 
 __device__ __forceinline__ bool spec_is_normal(uint64_t c, int64_t m) {
@@ -338,8 +338,7 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i - lane < n_pad; i += stride) {
     const bool valid = i < n;
     bool ok = false;
-    float fc_f = 0.f;
-    double fm_d = 0.0;
+    double fc_d = 0.0, fm_d = 0.0;
     int32_t P_i = 0, cl_i = 0;
     if (valid) {
       const uint64_t ac = alloc_cpu[i], uc = used_cpu[i];
@@ -351,7 +350,7 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
       ok = fc < FAST_FC_MAX && fm >= 0 && fm < FAST_FM_MAX && P >= -FAST_P_ABS &&
            P <= FAST_P_ABS && cl >= -FAST_CL_ABS && cl <= FAST_CL_ABS;
       if (ok) {
-        fc_f = (float)fc;  // exact (< 2^21)
+        fc_d = (double)fc;  // exact (< 2^50)
         fm_d = (double)fm;  // exact (< 2^50)
         P_i = (int32_t)P;
         cl_i = (int32_t)cl;
@@ -366,7 +365,7 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
     if (i < n_pad) {
       FitGroup& g = fast[i / FIT_GROUP];
       const int k = (int)(i % FIT_GROUP);
-      g.fc[k] = fc_f;
+      g.fc[k] = fc_d;
       g.P[k] = P_i;
       g.fm[k] = fm_d;
       g.cl[k] = cl_i;
@@ -381,16 +380,12 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
   }
 }
 
-// Smallest f32 >= 1/c and smallest f64 >= 1/m (the fit's quotients never undershoot).
-__device__ __forceinline__ float recip_up_f32(uint64_t c) {
-  float r = (float)(1.0 / (double)c);               // c < 2^22: r*c is exact in f64
-  if ((double)r * (double)c < 1.0) r = __uint_as_float(__float_as_uint(r) + 1u);  // next f32 up
-  return r;
-}
-__device__ __forceinline__ double recip_up_f64(int64_t m) {
-  const double md = (double)m;                       // exact (m < 2^51)
-  double r = 1.0 / md;
-  if (fma(r, md, -1.0) < 0.0) r = __longlong_as_double(__double_as_longlong(r) + 1);  // next up
+// Smallest f64 >= 1/v (1 <= v < 2^51, exact in f64): the fit's quotients never
+// undershoot.
+__device__ __forceinline__ double recip_up_f64(uint64_t v) {
+  const double vd = (double)v;
+  double r = 1.0 / vd;                                   // correctly rounded
+  if (fma(r, vd, -1.0) < 0.0) r = __longlong_as_double(__double_as_longlong(r) + 1);  // next up
   return r;
 }
 
@@ -463,9 +458,8 @@ __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64
     SpecRec r;
     r.c = c;
     r.m = m;
-    r.rm = nm ? recip_up_f64(m) : 0.0;
-    r.rc = nm ? recip_up_f32(c) : 0.f;
-    r.pad = 0;
+    r.rc = nm ? recip_up_f64(c) : 0.0;
+    r.rm = nm ? recip_up_f64((uint64_t)m) : 0.0;
     sp.rec[pos] = r;
     sp.perm[pos] = (int32_t)i;
   }
@@ -484,19 +478,18 @@ __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64
 // per spec).
 //
 // Fast path per (node, spec), exact (DESIGN.md "Fit fast path: exactness argument"):
-//   rc = smallest f32 >= 1/c, rm = smallest f64 >= 1/m (spec_prep); fc < 2^21 and
-//   fm < 2^50 are exact in f32 / f64.  Then with round-to-nearest products
-//     qc = trunc(RN32(fc * rc)) = floor(fc / c)          (fc < 2^21, c < 2^22)
-//     qm = sat_i32(trunc(RN64(fm * rm))) = min(floor(fm / m), 2^31 - 1)
-//   with no correction step: an integer quotient is never rounded below (the
+//   rc = smallest f64 >= 1/c, rm = smallest f64 >= 1/m (spec_prep); fc, fm < 2^50
+//   are exact in f64.  With round-to-nearest products
+//     floor(RN(fc * rc)) = floor(fc / c),  floor(RN(fm * rm)) = floor(fm / m)
+//   and no correction step: an integer quotient is never rounded below (the
 //   reciprocal is rounded up), and a non-integer one lies >= 1/c below the next
-//   integer, more than the relative error 2^-23 (2^-52) can cover at these sizes.
-//   x = min(qc, qm)                       findMin (CC:159-164)
+//   integer, more than the relative error (< 2^-51) can cover while 3a + b < 2^53.
+//   floor is monotone, so x = sat_i32(trunc(min(RN(fc*rc), RN(fm*rm))))
+//                          = min(floor(fc/c), floor(fm/m), 2^31 - 1)  findMin (CC:159-164)
 //   contribution = x >= P ? P - podCount : x                       (CC:133-136)
 // (x only saturates far above P <= 2^20, where the comparison is the same.)
-// Per node and 64-spec wavefront: v_pk_mul_f32 (two nodes), 2x v_cvt, v_mul_f64,
-// v_min_i32, v_cmp, v_cndmask, v_add3_u32 (two nodes) = 7 VALU instructions.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
+// Per node and 64-spec wavefront: 2x v_mul_f64, v_min_f64, v_cvt_i32_f64, v_cmp,
+// v_cndmask, v_add3_u32 (two nodes) = 6.5 VALU instructions.
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef int32_t i32x8 __attribute__((ext_vector_type(8)));
 typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
@@ -533,15 +526,13 @@ __global__ __launch_bounds__(256) void fit_kernel(
     sr.c = 1;
     sr.m = 1;
     sr.rm = 1.0;
-    sr.rc = 1.f;
+    sr.rc = 1.0;
   }
   const uint64_t c = sr.c;
   const int64_t m = sr.m;
-  const double rm = sr.rm;
-  const float rc = sr.rc;
-  const bool normal = rc > 0.f;
+  const double rm = sr.rm, rc = sr.rc;
+  const bool normal = rc > 0.0;
   const bool wave_fast = __all(normal);
-  const f32x2 rcc = {rc, rc};
 
   const int64_t n_groups = fit_groups(n_nodes);
   const int64_t g0 = (int64_t)by * groups_per_block;
@@ -589,23 +580,21 @@ __global__ __launch_bounds__(256) void fit_kernel(
         const int so = io * (int)sizeof(FitGroup) + (int)offsetof(FitGroup, cl);
         const i32x4 c0 = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, so, 0));
         const i32x4 c1 = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, so + 16, 0));
-        const i32x8 fcv = *reinterpret_cast<const i32x8*>(g->fc);
-        const i32x8 Pv = *reinterpret_cast<const i32x8*>(g->P);
+        const i32x16 fcv = *reinterpret_cast<const i32x16*>(g->fc);
         const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
+        const i32x8 Pv = *reinterpret_cast<const i32x8*>(g->P);
         const int32_t cl[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
         for (int u = 0; u < FIT_GROUP / 2; ++u) {
-          const f32x2 fc2 = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
-          const f32x2 ec = fc2 * rcc;  // one v_pk_mul_f32 for two nodes
           int32_t x[2];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int k = 2 * u + h;
+            const double fck = __longlong_as_double(((int64_t)(uint32_t)fcv[2 * k + 1] << 32) |
+                                                    (uint32_t)fcv[2 * k]);
             const double fmk = __longlong_as_double(((int64_t)(uint32_t)fmv[2 * k + 1] << 32) |
                                                     (uint32_t)fmv[2 * k]);
-            const int32_t qc = (int32_t)ec[h];
-            const int32_t qm = cvt_i32_sat(fmk * rm);
-            const int32_t xm = qc < qm ? qc : qm;
+            const int32_t xm = cvt_i32_sat(__builtin_fmin(fck * rc, fmk * rm));
             x[h] = xm >= Pv[k] ? cl[k] : xm;
           }
           acc32 += x[0] + x[1];

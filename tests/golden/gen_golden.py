@@ -47,6 +47,9 @@ def edge_case():
         (2**21 - 1, 2**50 - 1, 1 << 20, 0, []),                         # P at its bound
         (2**21 - 1, 2**50 - 1, (1 << 20) + 1, 0, []),                   # P past it
         (4_194_302, 2**51 - 2, 2, 1, []),                               # 2 x (spec edge)
+        (2**50 - 1, 2**50 - 1, 300, 0, []),                             # f64 quotient bounds
+        (2**50, 2**50 - 1, 300, 0, []),                                 # free CPU past it
+        (2**51 - 2, 2**49 + 3, 7, 2, []),
     ]
     alloc_cpu = np.array([r[0] for r in rows], np.uint64)
     alloc_mem = np.array([r[1] for r in rows], np.int64)
@@ -61,10 +64,11 @@ def edge_case():
     cpu = np.array(cpu, np.uint64)
     mem = np.array(mem, np.int64)
     spec_cpu = np.array([200, 100, 1, 3, 7, 8000, 0, 1 << 23, 2**63, 50, 1, 2**23 - 1,
-                         2**22 - 1, 2**22, 2**21 - 1, 1],
+                         2**22 - 1, 2**22, 2**21 - 1, 1, 2**51 - 1, 2**51, 2**49 + 1],
                         np.uint64)
     spec_mem = np.array([262_144_000, 104_857_600, 1, 1 << 20, -1, 1 << 35, 1 << 20, 0,
-                         -(1 << 63), 2**37, 2**37 - 1, 3, 2**51 - 1, 7, 2**50 - 1, 2**51],
+                         -(1 << 63), 2**37, 2**37 - 1, 3, 2**51 - 1, 7, 2**50 - 1, 2**51,
+                         5, 2**40 + 1, 2**49 + 1],
                         np.int64)
     return dict(alloc_cpu=alloc_cpu, alloc_mem=alloc_mem, alloc_pods=alloc_pods,
                 pod_count=pod_count, node_ptr=np.array(ptr, np.int64), cpu_req=cpu,

@@ -1,7 +1,7 @@
 """Static ISA checks of the gfx950 kernels (CPU: hipcc cross-compiles).
 
-  - the fit kernel's fast loop, one 8-node FitGroup per iteration: 32 dwords of scalar
-    loads (fc, P, fm), two uniform 16-B buffer loads (cl), no 64-bit integer division,
+  - the fit kernel's fast loop, one 8-node FitGroup per iteration: 40 dwords of scalar
+    loads (fc, fm, P), two uniform 16-B buffer loads (cl), no 64-bit integer division,
     no correction multiply, and exactly bench.FIT_VALU_PER_NODE_WAVE VALU instructions
     per node (the VALU-roofline accounting of bench.py);
   - no kernel spills to scratch.
@@ -47,15 +47,15 @@ def test_fit_fast_loop(asm):
     width = {"s_load_dword": 1, "s_load_dwordx2": 2, "s_load_dwordx4": 4, "s_load_dwordx8": 8,
              "s_load_dwordx16": 16}
     dwords = sum(width[ln.split()[0]] for ln in lines if ln.startswith("s_load_dword"))
-    assert dwords == group * 4  # fc (f32), P (i32), fm (f64) of each node
+    assert dwords == group * 5  # fc (f64), fm (f64), P (i32) of each node
     vmem = [ln for ln in lines if ln.startswith(("global_load", "flat_load", "buffer_load"))]
     assert len(vmem) == 2 and all(ln.startswith("buffer_load_dwordx4") and ", off," in ln
                                   for ln in vmem)  # cl: uniform address, no VGPR offset
     assert len(valu) / group == pytest.approx(bench.FIT_VALU_PER_NODE_WAVE, abs=1e-9), \
         f"{len(valu)} VALU / {group} nodes: update bench.FIT_VALU_PER_NODE_WAVE"
     ops = [ln.split()[0] for ln in valu]
-    assert ops.count("v_pk_mul_f32") == group // 2
-    assert ops.count("v_mul_f64") == group and ops.count("v_cvt_i32_f64") == group
+    assert ops.count("v_mul_f64") == 2 * group and ops.count("v_min_f64") == group
+    assert ops.count("v_cvt_i32_f64") == group and ops.count("v_add3_u32") == group // 2
     assert not any(o.startswith(("v_mad", "v_fma", "v_mul_lo", "v_mul_hi")) for o in ops)
 
 
