@@ -18,8 +18,6 @@ namespace kcc {
 
 namespace {
 
-constexpr int32_t HEAD_END = 0x7fffffff;  // "end of data" head marker
-
 __device__ __forceinline__ unsigned long long atomic_add_u64(uint64_t* p, uint64_t v) {
   return atomicAdd(reinterpret_cast<unsigned long long*>(p),
                    static_cast<unsigned long long>(v));
@@ -51,11 +49,11 @@ __global__ void reduce_mark_kernel(int64_t n_nodes, int64_t n_cont, int32_t rang
   }
 }
 
-// DPP controls (gfx9 family): row_shr:n, row_bcast:15/31, wave_shl:1.
+// DPP controls (gfx9 family): row_shr:n, row_bcast:15/31, wave_shr:1.
 constexpr int DPP_ROW_SHR = 0x110;
 constexpr int DPP_ROW_BCAST15 = 0x142;
 constexpr int DPP_ROW_BCAST31 = 0x143;
-constexpr int DPP_WAVE_SHL1 = 0x130;
+constexpr int DPP_WAVE_SHR1 = 0x138;
 
 template <int CTRL, int ROW_MASK, int BANK_MASK>
 __device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
@@ -75,12 +73,6 @@ __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
   v += dpp_u64<DPP_ROW_BCAST15, 0xa, 0xf>(v);
   v += dpp_u64<DPP_ROW_BCAST31, 0xc, 0xf>(v);
   return v;
-}
-
-__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src);
-  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
-  return ((uint64_t)hi << 32) | lo;
 }
 
 // CSR offset of node j relative to the wave range start, clamped into int32.
@@ -114,17 +106,19 @@ __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff
 
 // One wavefront walks a contiguous range of `range` containers in tiles of
 // RED_TILE = 256 (4 per lane, coalesced SoA buffer loads, next tile prefetched).
-// Per tile:
-//   1. nodes starting inside the tile: the next 64 CSR offsets come from a sliding
-//      register window (3 x 64 offsets, the third prefetched), gathered with
-//      ds_bpermute, and are written as head marks into a per-wave LDS strip;
-//   2. per lane a 4-item running sum, then one DPP inclusive prefix sum (64-bit,
-//      all VALU) of the lane totals; a run's sum = prefix at its end - prefix
-//      before its head, the head prefix coming from the lane that holds the head
-//      (one ds_bpermute) or from the carry of the previous tile;
-//   3. the lane holding a run's last container stores the node's sum — a plain
-//      store when the run started inside this wave's range, an atomic add only
-//      for the (at most two) runs crossing the range boundaries.
+// Per tile and array:
+//   1. the tile-local inclusive prefix sum of the 256 values: a 4-item running sum per
+//      lane, one DPP inclusive scan (64-bit, all VALU) of the lane totals, written to
+//      a per-wave LDS strip pre[0..255];
+//   2. lane k takes node cur + k (cur = the node holding the tile's first item): its
+//      end offset comes from a sliding register window of CSR offsets (3 x 64, the
+//      third prefetched), its start is lane k-1's end (DPP shift).  A node ending in
+//      this tile gets sum = pre[end-1] - pre[start-1], or pre[end-1] + carry when it
+//      began in an earlier tile (carry = its running sum so far, wave-uniform), all
+//      in wrapping uint64 arithmetic, so the differences are exact;
+//   3. the node's sum is stored by its lane — a plain store when the node lies
+//      inside this wave's range, a 64-bit atomic add only for the (at most two) nodes
+//      crossing the range boundaries.
 // Empty nodes are never visited (zeroed by reduce_mark_kernel).
 template <int NA>
 __global__ __launch_bounds__(256) void reduce_kernel(
@@ -133,8 +127,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(
     const uint64_t* __restrict__ in2, const uint64_t* __restrict__ in3,
     const int64_t* __restrict__ wave_node, uint64_t* __restrict__ out0,
     uint64_t* __restrict__ out1, uint64_t* __restrict__ out2, uint64_t* __restrict__ out3) {
-  constexpr int HS = RED_TILE + 4;  // LDS strip per wave (positions 0..RED_TILE)
-  __shared__ __attribute__((aligned(16))) int32_t heads_s[RED_WAVES_PER_BLOCK * HS];
+  __shared__ __attribute__((aligned(16))) uint64_t pre_s[RED_WAVES_PER_BLOCK][NA][RED_TILE];
   const int lane = threadIdx.x & 63;
   // wave index made provably uniform (T20: no waterfall loops around the buffer ops)
   const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)(blockIdx.x * RED_WAVES_PER_BLOCK +
@@ -142,7 +135,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(
   const int64_t wb = (int64_t)w * range;
   if (wb >= n_cont) return;  // wave-uniform; no block-level barrier in this kernel
   const int32_t len = (int32_t)(n_cont - wb < range ? n_cont - wb : range);
-  int32_t* heads = heads_s + (threadIdx.x >> 6) * HS;
+  uint64_t (*pre)[RED_TILE] = pre_s[threadIdx.x >> 6];
   const uint64_t* in[4] = {in0, in1, in2, in3};
   uint64_t* out[4] = {out0, out1, out2, out3};
   __amdgpu_buffer_rsrc_t rs[NA];
@@ -150,26 +143,23 @@ __global__ __launch_bounds__(256) void reduce_kernel(
   for (int k = 0; k < NA; ++k)  // whole 16-B pairs only: an odd last item is fixed up below
     rs[k] = __builtin_amdgcn_make_buffer_rsrc((void*)(in[k] + wb), (short)0,
                                               (int)((len & ~1) * 8), 0x00020000);
-  const unsigned long long lt_mask = (1ull << lane) - 1ull;
 
   const int64_t node0 = wave_node[w];
-  const bool first_open = ptr[node0] < wb;  // node0's run began in an earlier range
-  int64_t cur = node0;                      // node owning the current tile's first item
-  uint64_t carry[NA];
+  const int64_t start0 = ptr[node0];
+  const bool first_open = start0 < wb;  // node0 began in an earlier range
+  int64_t cur = node0;                  // node holding the current tile's first item
+  int32_t cur_start = rel_clamp(start0, wb);
+  uint64_t carry[NA];                   // node cur's running sum over [cur_start, tb)
 #pragma unroll
   for (int k = 0; k < NA; ++k) carry[k] = 0;
 
-  // sliding window of CSR offsets: win0/win1 (relative, clamped) hold nodes
-  // [wbase, wbase+64), [wbase+64, +128); win2r (raw, still in flight) the next 64
+  // sliding window of CSR end offsets: win0/win1 (relative, clamped) hold the ends
+  // of nodes [wbase-1, wbase+63), [wbase+63, +127); win2r (raw, in flight) the next 64
   int64_t wbase = cur + 1;
   int32_t win0 = rel_ptr(ptr, wbase + lane, n_nodes, wb);
   int32_t win1 = rel_ptr(ptr, wbase + 64 + lane, n_nodes, wb);
   int64_t win2r = ptr_at(ptr, wbase + 128 + lane, n_nodes);
-  const int32_t end_rel = (int32_t)(n_cont - wb < range + 2 ? n_cont - wb : range + 2);
 
-  // Statically named tile buffers in rotation: the loads for tile t+KCC_RED_PREFETCH
-  // are issued unconditionally (range-checked) at the top of tile t, so they stay in
-  // flight across whole tiles and no register copy forces an early wait.
   uint64_t xa[NA][4], xb[NA][4];
 #if KCC_RED_PREFETCH == 2
   uint64_t xc[NA][4];
@@ -197,10 +187,24 @@ __global__ __launch_bounds__(256) void reduce_kernel(
       }
     }
 
-    // --- 1. head marks --------------------------------------------------------
-    *reinterpret_cast<int4*>(&heads[4 * lane]) = make_int4(-1, -1, -1, -1);
-    if (lane == 0) heads[RED_TILE] = -1;
-    const int32_t X = tb + RED_TILE;
+    // --- 1. tile-local inclusive prefix sums -> LDS -----------------------------
+    uint64_t tot[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const uint64_t q0 = x[k][0], q1 = q0 + x[k][1], q2 = q1 + x[k][2], q3 = q2 + x[k][3];
+      const uint64_t P = wave_incl_scan_u64(q3);
+      const uint64_t ex = P - q3;
+      u64x2* dst = reinterpret_cast<u64x2*>(&pre[k][4 * lane]);
+      dst[0] = u64x2{ex + q0, ex + q1};
+      dst[1] = u64x2{ex + q2, P};
+      tot[k] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(P >> 32), 63) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((uint32_t)P, 63);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+
+    // --- 2./3. nodes ending in this tile ------------------------------------------
+    const int32_t lim = tb + RED_TILE < len ? tb + RED_TILE : len;
     while (cur + 1 - wbase >= 64) {  // slide the window (rarely more than once)
       win0 = win1;
       win1 = rel_clamp(win2r, wb);
@@ -210,76 +214,49 @@ __global__ __launch_bounds__(256) void reduce_kernel(
     const int off = (int)(cur + 1 - wbase);  // 0..63
     const int idx = off + lane;               // 0..126
     const int32_t g0 = __shfl(win0, idx & 63), g1 = __shfl(win1, idx & 63);
-    const int32_t sj = idx < 64 ? g0 : g1;
-    int32_t sj1 = __builtin_amdgcn_update_dpp(0, sj, DPP_WAVE_SHL1, 0xf, 0xf, false);
-    const int32_t nxt = __shfl(win1, off);  // node cur+65
-    if (lane == 63) sj1 = nxt;
-    const int64_t j0 = cur + 1 + lane;
-    const bool in_range = (j0 < n_nodes) && (sj <= X);
-    if (in_range && sj1 > sj && sj > tb && sj < end_rel) heads[sj - tb] = (int32_t)(j0 - cur);
-    unsigned long long bal = __ballot(in_range);
-    int64_t cnt = __popcll(bal);
-    // more than 64 node starts in this tile (runs of tiny or empty nodes): direct loads
-    for (int64_t r = 64; (bal >> 63) & 1ull; r += 64) {
-      const int64_t j = cur + 1 + r + lane;
-      const int32_t s2 = rel_ptr(ptr, j, n_nodes, wb);
-      const int32_t s21 = rel_ptr(ptr, j + 1, n_nodes, wb);
-      const bool ir = (j < n_nodes) && (s2 <= X);
-      if (ir && s21 > s2 && s2 > tb && s2 < end_rel) heads[s2 - tb] = (int32_t)(j - cur);
-      bal = __ballot(ir);
-      cnt += __popcll(bal);
-    }
-    if (lane == 0 && end_rel > tb && end_rel <= X) heads[end_rel - tb] = HEAD_END;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-
-    const int4 h4 = *reinterpret_cast<const int4*>(&heads[4 * lane]);
-    const int32_t h[5] = {h4.x, h4.y, h4.z, h4.w, heads[4 * lane + 4]};
-    bool f[5];
+    const int32_t e = idx < 64 ? g0 : g1;    // end of node cur + lane
+    int32_t s = __builtin_amdgcn_update_dpp(0, e, DPP_WAVE_SHR1, 0xf, 0xf, false);
+    if (lane == 0) s = cur_start;
+    const int64_t j = cur + lane;
+    bool ends = (j < n_nodes) && (e <= lim);
+    if (ends && e > s) {
 #pragma unroll
-    for (int i = 0; i < 5; ++i) f[i] = h[i] >= 0;
-    const bool any = f[0] || f[1] || f[2] || f[3];
-    const unsigned long long hm = __ballot(any);
-    const unsigned long long before = hm & lt_mask;
-    const int L = before ? 63 - __clzll(before) : 0;  // last lane before me with a head
-    const int32_t lid = f[3] ? h[3] : f[2] ? h[2] : f[1] ? h[1] : h[0];
-    // every cross-lane read below runs on all 64 lanes, then selects
-    const int32_t got_id = __shfl(lid, L);
-    const int32_t prev_id = before ? got_id : 0;
-    const bool last_end = (__ballot(f[4]) >> 63) & 1ull;
-
-    // --- 2./3. prefix sums, run sums, emit ---------------------------------------
-#pragma unroll
-    for (int k = 0; k < NA; ++k) {
-      uint64_t q[4];  // running sums within the lane
-      q[0] = x[k][0];
-#pragma unroll
-      for (int i = 1; i < 4; ++i) q[i] = q[i - 1] + x[k][i];
-      const uint64_t P = wave_incl_scan_u64(q[3]);
-      const uint64_t Pex = P - q[3];
-      const uint64_t lhp = Pex + (f[3] ? q[2] : f[2] ? q[1] : f[1] ? q[0] : 0ull);
-      const uint64_t got = shfl_u64(lhp, L);
-      uint64_t sp = before ? got : (0ull - carry[k]);  // prefix before the open run's head
-      int32_t cid = prev_id;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (f[i]) {
-          sp = Pex + (i ? q[i - 1] : 0ull);
-          cid = h[i];
-        }
-        if (f[i + 1] && p0 + i < len) {  // run ends at item i
-          const int64_t nd = cur + cid;
-          const uint64_t tot = Pex + q[i] - sp;
-          if (nd < n_nodes) {
-            if (nd == node0 && first_open) atomic_add_u64(&out[k][nd], tot);
-            else out[k][nd] = tot;
-          }
-        }
+      for (int k = 0; k < NA; ++k) {
+        const uint64_t endp = pre[k][e - 1 - tb];
+        const uint64_t startp = s > tb ? pre[k][s - 1 - tb] : (0ull - carry[k]);
+        const uint64_t sum = endp - startp;
+        if (j == node0 && first_open) atomic_add_u64(&out[k][j], sum);
+        else out[k][j] = sum;
       }
-      const uint64_t tail = shfl_u64(P - sp, 63);
-      carry[k] = last_end ? 0 : tail;
     }
-    cur += cnt;
+    unsigned long long bal = __ballot(ends);
+    int64_t cnt = __popcll(bal);
+    int32_t last_end = 0;  // end of the last node that ended in this tile
+    if (cnt) last_end = __builtin_amdgcn_readlane(e, (int)cnt - 1);
+    // more than 64 nodes end in this tile (runs of tiny or empty nodes): direct loads
+    for (int64_t r = 64; (bal >> 63) & 1ull; r += 64) {
+      const int64_t j2 = cur + r + lane;
+      const int32_t s2 = rel_ptr(ptr, j2, n_nodes, wb);
+      const int32_t e2 = rel_ptr(ptr, j2 + 1, n_nodes, wb);
+      const bool ends2 = (j2 < n_nodes) && (e2 <= lim);
+      if (ends2 && e2 > s2) {  // s2 > tb: these nodes start after node cur's end
+#pragma unroll
+        for (int k = 0; k < NA; ++k) out[k][j2] = pre[k][e2 - 1 - tb] - pre[k][s2 - 1 - tb];
+      }
+      bal = __ballot(ends2);
+      const int c2 = __popcll(bal);
+      if (c2) last_end = __builtin_amdgcn_readlane(e2, c2 - 1);
+      cnt += c2;
+    }
+    if (cnt) {  // a new node is open at the tile end: its sum so far
+      cur += cnt;
+      cur_start = last_end;  // > tb
+#pragma unroll
+      for (int k = 0; k < NA; ++k) carry[k] = tot[k] - pre[k][last_end - 1 - tb];
+    } else {
+#pragma unroll
+      for (int k = 0; k < NA; ++k) carry[k] += tot[k];
+    }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   };
@@ -295,7 +272,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(
     if (tb + RED_TILE < len) tile(xb, xa, tb + RED_TILE);
   }
 #endif
-  // the run open at the end of the range continues into the next wave's range
+  // the node open at the end of the range continues into the next wave's range
   if (wb + len < n_cont && lane == 0 && cur < n_nodes) {
 #pragma unroll
     for (int k = 0; k < NA; ++k)
