@@ -36,6 +36,18 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 FIT_VALU_PER_NODE_WAVE = 6.5
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions / s
 METRIC = "node×spec fit evals/sec at 1M nodes × 4K specs; % of HBM roofline"
+# per-launch HBM traffic of each kernel from rocprofv3 PMC passes of this same bench
+# command (scripts/profile.sh + scripts/summarize_prof.py); null when absent
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def pmc_traffic(kernel):
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+        return t["kernels"][kernel]["hbm_bytes_per_launch"], t["source"]
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def parse():
@@ -159,6 +171,8 @@ def main():
     fit_gbs = fit_bytes / (fit_ms * 1e-3) / 1e9
     fit_valu = n * ((S + 63) // 64) * FIT_VALU_PER_NODE_WAVE / (fit_ms * 1e-3)
     red_gbs = red_bytes / (red_ms * 1e-3) / 1e9
+    fit_traffic, tsrc = pmc_traffic("fit_kernel") if args.config == "C4" and world == 1 else (None, None)
+    red_traffic, _ = pmc_traffic("reduce_kernel<2>") if tsrc else (None, None)
 
     out = {
         "metric": METRIC,
@@ -182,7 +196,8 @@ def main():
         },
         "roofline": {
             "bound": "hbm", "kernel": "fit_kernel", "achieved": fit_gbs, "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": fit_gbs / HBM_PEAK_GBS, "traffic": None,
+            "unit": "GB/s", "frac": fit_gbs / HBM_PEAK_GBS, "traffic": fit_traffic,
+            "traffic_source": tsrc and f"profiles/pmc_traffic.json ({tsrc}); bytes per launch",
             "bytes_per_launch": fit_bytes, "ms_per_launch": fit_ms,
             "note": "fit is VALU-bound (no contraction, 64-bit compare/divide work per eval); "
                     "HBM frac reported per the BASELINE metric; see roofline_reduce",
@@ -198,6 +213,7 @@ def main():
             "bound": "hbm", "kernel": "reduce_mark_kernel+reduce_kernel<2>",
             "achieved": red_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": red_gbs / HBM_PEAK_GBS, "bytes_per_launch": red_bytes, "ms_per_launch": red_ms,
+            "traffic": red_traffic,
         },
         "fit_prepare_ms": prep_ms,
         "fast_path_fraction": 1.0 - (slow_pairs / pairs if pairs else 0.0),

@@ -95,9 +95,14 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 // RED_IPL (=4) consecutive 64-bit values of one array for this lane: two 16-B
 // range-checked buffer loads (outside the descriptor's range they read 0), so the
 // prefetch is branch-free and never waits where it is issued.
-__device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff, uint64_t (&x)[4]) {
-  const u64x2 lo = __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
-  const u64x2 hi = __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16, 0, 0));
+// The lane offset (voff) is loop-invariant and the tile offset goes in soffset, so no
+// address VGPR is recomputed per tile (a recomputed address register that the
+// allocator shares with an in-flight load's destination forces a vmcnt(0) wait).
+__device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff, int32_t soff,
+                                          uint64_t (&x)[4]) {
+  const u64x2 lo = __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+  const u64x2 hi =
+      __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16, soff, 0));
   x[0] = lo.x;
   x[1] = lo.y;
   x[2] = hi.x;
@@ -166,16 +171,16 @@ __global__ __launch_bounds__(256) void reduce_kernel(
 #endif
 #pragma unroll
   for (int k = 0; k < NA; ++k) {
-    load_quad(rs[k], lane * 32, xa[k]);
+    load_quad(rs[k], lane * 32, 0, xa[k]);
 #if KCC_RED_PREFETCH == 2
-    load_quad(rs[k], RED_TILE * 8 + lane * 32, xb[k]);
+    load_quad(rs[k], lane * 32, RED_TILE * 8, xb[k]);
 #endif
   }
 
   auto tile = [&](uint64_t (&x)[NA][4], uint64_t (&nx)[NA][4], const int32_t tb) {
 #pragma unroll
     for (int k = 0; k < NA; ++k)
-      load_quad(rs[k], (tb + KCC_RED_PREFETCH * RED_TILE) * 8 + lane * 32, nx[k]);
+      load_quad(rs[k], lane * 32, (tb + KCC_RED_PREFETCH * RED_TILE) * 8, nx[k]);
     const int32_t p0 = tb + 4 * lane;  // relative position of this lane's first item
     if ((len & 1) && p0 <= len - 1 && len - 1 < p0 + 4) {  // odd tail: last item alone
 #pragma unroll
@@ -478,9 +483,15 @@ __device__ __forceinline__ int32_t cvt_i32_sat(double x) {
   return r;
 }
 
+#ifndef KCC_FIT_SPECS_PER_WG
+#define KCC_FIT_SPECS_PER_WG 256  // 64/128 (waves split the node chunk, LDS-reduced atomics) measured slower
+#endif
+constexpr int FIT_SPW = KCC_FIT_SPECS_PER_WG;  // specs per 256-thread workgroup (64 or 256)
+constexpr int FIT_SPLIT = 256 / FIT_SPW;       // waves per spec group (node chunk split)
+static_assert(FIT_SPW == 64 || FIT_SPW == 128 || FIT_SPW == 256, "FIT_SPW");
 constexpr int FIT_CHUNK_GROUPS = 128;  // 1024 nodes: |sum of contributions| <= 2^30 in i32
 #ifndef KCC_FIT_TARGET_BLOCKS
-#define KCC_FIT_TARGET_BLOCKS 16384
+#define KCC_FIT_TARGET_BLOCKS 32768
 #endif
 
 __global__ __launch_bounds__(256) void fit_kernel(
@@ -494,7 +505,9 @@ __global__ __launch_bounds__(256) void fit_kernel(
   const int32_t b = blockIdx.x, xcd = b & 7, r = b >> 3;
   const int32_t bx = r % gx, by = (r / gx) * 8 + xcd;
   if (by >= gy) return;  // padding of gy up to a multiple of 8 (whole workgroup)
-  const int64_t s = (int64_t)bx * 256 + threadIdx.x;
+  // FIT_SPW specs per workgroup; its FIT_SPLIT waves share them and split the node chunk
+  const int32_t wv = __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6) / (FIT_SPW / 64));
+  const int64_t s = (int64_t)bx * FIT_SPW + (threadIdx.x % FIT_SPW);
   const bool active = s < S;
   SpecRec sr;  // one 32-B record per lane (two 16-B loads)
   if (active) {
@@ -512,8 +525,13 @@ __global__ __launch_bounds__(256) void fit_kernel(
   const bool wave_fast = __all(normal);
 
   const int64_t n_groups = fit_groups(n_nodes);
-  const int64_t g0 = (int64_t)by * groups_per_block;
-  const int64_t g1 = g0 + groups_per_block < n_groups ? g0 + groups_per_block : n_groups;
+  int64_t g0 = (int64_t)by * groups_per_block;
+  int64_t g1 = g0 + groups_per_block < n_groups ? g0 + groups_per_block : n_groups;
+  if (FIT_SPLIT > 1) {  // this wave's part of the workgroup's node chunk
+    const int64_t part = (g1 - g0 + FIT_SPLIT - 1) / FIT_SPLIT;
+    g0 = g0 + wv * part < g1 ? g0 + wv * part : g1;
+    g1 = g0 + part < g1 ? g0 + part : g1;
+  }
   uint64_t acc = 0;
   uint64_t errs = 0;
   uint32_t slow_iters = 0;
@@ -579,14 +597,32 @@ __global__ __launch_bounds__(256) void fit_kernel(
       }
       acc += (uint64_t)(int64_t)acc32;
     }
-    // rows outside the fast bounds, shared out over the node-chunk blocks
+    // rows outside the fast bounds, shared out over the node-chunk waves
     const int64_t n_slow = (int64_t)counters[1];
-    for (int64_t j = by; j < n_slow; j += gy) eval_slow(slow_list[j]);
+    for (int64_t j = (int64_t)by * FIT_SPLIT + wv; j < n_slow; j += (int64_t)gy * FIT_SPLIT)
+      eval_slow(slow_list[j]);
   } else {
     const int64_t i1 = g1 * FIT_GROUP < n_nodes ? g1 * FIT_GROUP : n_nodes;
     for (int64_t i = g0 * FIT_GROUP; i < i1; ++i) eval_slow(i);
   }
 
+  {  // (node, spec) pairs evaluated on the exact path (statistics)
+    const unsigned long long act = __ballot(active);
+    if (slow_iters && (threadIdx.x & 63) == 0)
+      atomicAdd(counters, (unsigned long long)slow_iters * (unsigned long long)__popcll(act));
+  }
+  if (FIT_SPLIT > 1) {  // the waves of one spec group meet in LDS: one atomic per spec
+    __shared__ uint64_t red_s[2][FIT_SPLIT][FIT_SPW];
+    red_s[0][wv][threadIdx.x % FIT_SPW] = acc;
+    red_s[1][wv][threadIdx.x % FIT_SPW] = errs;
+    __syncthreads();
+    if (wv != 0) return;
+#pragma unroll
+    for (int k = 1; k < FIT_SPLIT; ++k) {
+      acc += red_s[0][k][threadIdx.x];
+      errs += red_s[1][k][threadIdx.x];
+    }
+  }
 #ifdef KCC_FIT_DIAG_NO_ATOMICS  // diagnostic timing build only: results are wrong
   if (active && acc == 0x5A5A5A5A5A5A5A5Aull) partial[s] = (int64_t)acc;
 #else
@@ -595,9 +631,6 @@ __global__ __launch_bounds__(256) void fit_kernel(
     if (errs) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[S + s]), errs);
   }
 #endif
-  const unsigned long long act = __ballot(active);
-  if (slow_iters && (threadIdx.x & 63) == 0)
-    atomicAdd(counters, (unsigned long long)slow_iters * (unsigned long long)__popcll(act));
 }
 
 __global__ void fit_finalize_kernel(int64_t S, const int64_t* __restrict__ partial,
@@ -682,9 +715,10 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroup* fast, const SlowNode* slo
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, hipStream_t s) {
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
-  const int64_t gx = (n_specs + 255) / 256;
+  const int64_t gx = (n_specs + FIT_SPW - 1) / FIT_SPW;
   const int64_t n_groups = fit_groups(n_nodes);
-  // aim for KCC_FIT_TARGET_BLOCKS workgroups (2048 = one full round at 8 per CU); >= 8
+  // aim for KCC_FIT_TARGET_BLOCKS workgroups (2048 = one round at 8 per CU; 16 rounds keep
+  // the ragged end of the last round short; measured best of 4k..128k at C4); >= 8
   // groups (64 nodes) each
   int64_t gy_target = KCC_FIT_TARGET_BLOCKS / gx;
   if (gy_target < 1) gy_target = 1;
