@@ -56,19 +56,20 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t n_containers, const int64_t* n
 
 // ---- (b) fit -----------------------------------------------------------------
 // Node stream of the fit kernel: groups of FIT_GROUP nodes, field-major inside the
-// group (192 B).  fc/fm/P arrive through the scalar cache (SGPR operands of the VALU),
+// group (224 B).  fc/fm/Pb arrive through the scalar cache (SGPR operands of the VALU),
 // cl by one uniform-address vector load (it is a v_cndmask operand, and gfx9 allows a
 // single SGPR/VCC read per VALU instruction).  Rows outside the fast-path bounds, and
-// the padding of the last group, hold all-zero fields (contribute exactly 0: x = 0 >=
-// P = 0 selects cl = 0) and are listed in slow_list for the exact path.
+// the padding of the last group, hold all-zero fields (contribute exactly 0: x' = 2^52
+// >= Pb = 0 selects cl = 0) and are listed in slow_list for the exact path.
 constexpr int FIT_GROUP = 8;
-struct __attribute__((aligned(64))) FitGroup {
+constexpr double FIT_BIAS = 4503599627370496.0;  // 2^52: integers in [2^52, 2^53) have ulp 1
+struct __attribute__((aligned(32))) FitGroup {
   double fc[FIT_GROUP];   // free CPU (millicores), exact in f64 on the fast path (< 2^50)
   double fm[FIT_GROUP];   // free memory (bytes), exact in f64 on the fast path (< 2^50)
-  int32_t P[FIT_GROUP];   // allocatable pods
+  double Pb[FIT_GROUP];   // 2^52 + allocatable pods (|P| <= 2^20: exact), the biased compare operand
   int32_t cl[FIT_GROUP];  // clamp value allocatable pods - podCount (CC:135)
 };
-static_assert(sizeof(FitGroup) == 192, "FitGroup must be 192 B");
+static_assert(sizeof(FitGroup) == 224, "FitGroup must be 224 B");
 __host__ __device__ inline int64_t fit_groups(int64_t n_nodes) { return (n_nodes + FIT_GROUP - 1) / FIT_GROUP; }
 
 // Raw per-node values for the exact path (fc/fm are 0 where the reference's

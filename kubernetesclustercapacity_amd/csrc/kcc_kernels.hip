@@ -320,8 +320,8 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i - lane < n_pad; i += stride) {
     const bool valid = i < n;
     bool ok = false;
-    double fc_d = 0.0, fm_d = 0.0;
-    int32_t P_i = 0, cl_i = 0;
+    double fc_d = 0.0, fm_d = 0.0, Pb_d = 0.0;
+    int32_t cl_i = 0;
     if (valid) {
       const uint64_t ac = alloc_cpu[i], uc = used_cpu[i];
       const int64_t am = alloc_mem[i], um = used_mem[i];
@@ -334,7 +334,7 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
       if (ok) {
         fc_d = (double)fc;  // exact (< 2^50)
         fm_d = (double)fm;  // exact (< 2^50)
-        P_i = (int32_t)P;
+        Pb_d = FIT_BIAS + (double)P;  // exact (|P| <= 2^20)
         cl_i = (int32_t)cl;
       }
       SlowNode sn;
@@ -348,7 +348,7 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
       FitGroup& g = fast[i / FIT_GROUP];
       const int k = (int)(i % FIT_GROUP);
       g.fc[k] = fc_d;
-      g.P[k] = P_i;
+      g.Pb[k] = Pb_d;
       g.fm[k] = fm_d;
       g.cl[k] = cl_i;
     }
@@ -461,26 +461,48 @@ __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64
 //
 // Fast path per (node, spec), exact (DESIGN.md "Fit fast path: exactness argument"):
 //   rc = smallest f64 >= 1/c, rm = smallest f64 >= 1/m (spec_prep); fc, fm < 2^50
-//   are exact in f64.  With round-to-nearest products
-//     floor(RN(fc * rc)) = floor(fc / c),  floor(RN(fm * rm)) = floor(fm / m)
-//   and no correction step: an integer quotient is never rounded below (the
-//   reciprocal is rounded up), and a non-integer one lies >= 1/c below the next
-//   integer, more than the relative error (< 2^-51) can cover while 3a + b < 2^53.
-//   floor is monotone, so x = sat_i32(trunc(min(RN(fc*rc), RN(fm*rm))))
-//                          = min(floor(fc/c), floor(fm/m), 2^31 - 1)  findMin (CC:159-164)
-//   contribution = x >= P ? P - podCount : x                       (CC:133-136)
-// (x only saturates far above P <= 2^20, where the comparison is the same.)
-// Per node and 64-spec wavefront: 2x v_mul_f64, v_min_f64, v_cvt_i32_f64, v_cmp,
-// v_cndmask, v_add3_u32 (two nodes) = 6.5 VALU instructions.
+//   are exact in f64.  The loop runs with the f64 rounding mode set to round toward
+//   -inf, and one fused multiply-add per quotient does floor AND the conversion:
+//     qc' = RD(fc * rc + 2^52) = 2^52 + floor(fc / c)
+//     qm' = RD(fm * rm + 2^52) = 2^52 + floor(fm / m)
+//   (the fused product is exact; an integer quotient is never below it since the
+//   reciprocal is rounded up, a non-integer one lies >= 1/c below the next integer,
+//   more than the relative error (< 2^-52) can cover while fc < 2^52; in [2^52, 2^53)
+//   the ulp is 1, so rounding down IS floor).  Then
+//     x' = min(qc', qm') = 2^52 + findMin(qc, qm)                      (CC:159-164)
+//     contribution = x' >= 2^52 + P ? P - podCount : low32(x')          (CC:133-136)
+//   low32(x') = x exactly whenever it is used (x < P <= 2^20).
+// Per node and 64-spec wavefront: 2x v_fma_f64, v_min_f64, v_cmp_ge_f64, v_cndmask,
+// v_add3_u32 (two nodes) = 5.5 VALU instructions.
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef int32_t i32x8 __attribute__((ext_vector_type(8)));
 typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
 
-// v_cvt_i32_f64 saturates out-of-range values in hardware (C's conversion is UB there)
-__device__ __forceinline__ int32_t cvt_i32_sat(double x) {
-  int32_t r;
-  asm("v_cvt_i32_f64 %0, %1" : "=v"(r) : "v"(x));
-  return r;
+// MODE register FP_ROUND[3:2] (f64/f16 rounding): 0 nearest-even, 2 toward -inf.  The
+// fit's fast loop runs in round-toward--inf; f32 rounding (FP_ROUND[1:0], used by the
+// compiler's 64-bit integer division expansion on the exact path) stays nearest-even.
+// Both the mode switch and the rounding-sensitive FMA are inline asm: LLVM's
+// SIModeRegister pass assumes the function's default FP mode for every FP instruction
+// it emits and would re-insert a switch back to nearest-even in front of a compiler-
+// generated v_fma_f64.  (v_min_f64 and v_cmp_*_f64 do not round.)
+__device__ __forceinline__ void set_f64_round_down() {
+  asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 2\n\ts_nop 1" ::: "memory");
+}
+__device__ __forceinline__ void set_f64_round_nearest() {
+  asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 0\n\ts_nop 1" ::: "memory");
+}
+// a * r + b rounded by the current f64 mode; a is wave-uniform (SGPR operand)
+__device__ __forceinline__ double fma_f64_s(double a, double r, double b) {
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "s"(a), "v"(r), "v"(b));
+  return d;
+}
+// min of two FMA results (asm: the compiler cannot see they are canonical and would
+// quiet them with a v_max_f64 each first)
+__device__ __forceinline__ double min_f64(double a, double b) {
+  double d;
+  asm("v_min_f64 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
 }
 
 #ifndef KCC_FIT_SPECS_PER_WG
@@ -521,6 +543,7 @@ __global__ __launch_bounds__(256) void fit_kernel(
   const uint64_t c = sr.c;
   const int64_t m = sr.m;
   const double rm = sr.rm, rc = sr.rc;
+  const double bias = FIT_BIAS;
   const bool normal = rc > 0.0;
   const bool wave_fast = __all(normal);
 
@@ -564,6 +587,7 @@ __global__ __launch_bounds__(256) void fit_kernel(
     const int cnt = (int)(g1 - g0);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)gbase, (short)0, cnt * (int)sizeof(FitGroup), 0x00020000);
+    set_f64_round_down();  // the FMAs are the only rounding f64 ops of the loop
     for (int cb = 0; cb < cnt; cb += FIT_CHUNK_GROUPS) {
       const int ce = cb + FIT_CHUNK_GROUPS < cnt ? cb + FIT_CHUNK_GROUPS : cnt;
       int32_t acc32 = 0;
@@ -577,26 +601,29 @@ __global__ __launch_bounds__(256) void fit_kernel(
         const i32x4 c1 = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, so + 16, 0));
         const i32x16 fcv = *reinterpret_cast<const i32x16*>(g->fc);
         const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
-        const i32x8 Pv = *reinterpret_cast<const i32x8*>(g->P);
+        const i32x16 Pv = *reinterpret_cast<const i32x16*>(g->Pb);
         const int32_t cl[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        auto f64_at = [](const i32x16& v, int k) {
+          return __longlong_as_double(((int64_t)(uint32_t)v[2 * k + 1] << 32) | (uint32_t)v[2 * k]);
+        };
 #pragma unroll
         for (int u = 0; u < FIT_GROUP / 2; ++u) {
           int32_t x[2];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int k = 2 * u + h;
-            const double fck = __longlong_as_double(((int64_t)(uint32_t)fcv[2 * k + 1] << 32) |
-                                                    (uint32_t)fcv[2 * k]);
-            const double fmk = __longlong_as_double(((int64_t)(uint32_t)fmv[2 * k + 1] << 32) |
-                                                    (uint32_t)fmv[2 * k]);
-            const int32_t xm = cvt_i32_sat(__builtin_fmin(fck * rc, fmk * rm));
-            x[h] = xm >= Pv[k] ? cl[k] : xm;
+            const double qc = fma_f64_s(f64_at(fcv, k), rc, bias);  // 2^52 + floor(fc/c)
+            const double qm = fma_f64_s(f64_at(fmv, k), rm, bias);  // 2^52 + floor(fm/m)
+            const double xb = min_f64(qc, qm);
+            const int32_t lo = (int32_t)(uint32_t)__double_as_longlong(xb);
+            x[h] = xb >= f64_at(Pv, k) ? cl[k] : lo;
           }
           acc32 += x[0] + x[1];
         }
       }
       acc += (uint64_t)(int64_t)acc32;
     }
+    set_f64_round_nearest();
     // rows outside the fast bounds, shared out over the node-chunk waves
     const int64_t n_slow = (int64_t)counters[1];
     for (int64_t j = (int64_t)by * FIT_SPLIT + wv; j < n_slow; j += (int64_t)gy * FIT_SPLIT)

@@ -1,16 +1,19 @@
 """CPU model of the fit kernel's fast path (kcc_kernels.hip `fit_kernel`).
 
 The kernel computes floor(fc / c) and floor(fm / m) (CC:123, CC:129) without any
-integer division or correction step:
+integer division, conversion or correction step: one fused multiply-add per quotient
+with the f64 rounding mode set to round toward -inf,
 
-    qc = trunc(RN64(fc * rc)),  rc = smallest f64 >= 1/c     (fc < 2^50, 1 <= c < 2^51)
-    qm = trunc(RN64(fm * rm)),  rm = smallest f64 >= 1/m     (fm < 2^50, 1 <= m < 2^51)
+    qc' = RD64(fc * rc + 2^52) = 2^52 + floor(fc * rc),  rc = smallest f64 >= 1/c
+    qm' = RD64(fm * rm + 2^52) = 2^52 + floor(fm * rm),  rm = smallest f64 >= 1/m
+    (fc, fm < 2^50; 1 <= c, m < 2^51)
 
-numpy's float64 products are IEEE round-to-nearest-even, exactly what v_mul_f64
-does, so these tests replay the kernel's arithmetic on the
-CPU and compare it with exact integer floor division — on the quotients where the
-argument is tightest: exact multiples, +-1 around them, the largest operands allowed
-on the fast path, powers of two and their neighbours.
+where fc * rc is the EXACT real product (the FMA rounds once, after the add, and in
+[2^52, 2^53) the ulp is 1, so rounding down is floor).  `floor_prod` replays that on
+the CPU — floor of the exact product from Dekker's error-free two-product, checked
+against Python's exact rationals — and the tests compare it with exact integer floor
+division where the argument is tightest: exact multiples, +-1 around them, the
+largest operands allowed on the fast path, powers of two and their neighbours.
 """
 import numpy as np
 import pytest
@@ -40,12 +43,60 @@ def _exact_prod_minus_one_negative(r, md):
     return (p < 1.0) | ((p == 1.0) & (e < 0.0))
 
 
+def _two_prod(a, b):
+    """p = RN(a*b) and e with a*b = p + e exactly (Dekker; no fma in numpy)."""
+    def split(x):
+        t = x * 134217729.0  # 2^27 + 1
+        hi = t - (t - x)
+        return hi, x - hi
+    p = a * b
+    ah, al = split(a)
+    bh, bl = split(b)
+    e = ((ah * bh - p) + ah * bl + al * bh) + al * bl
+    return p, e
+
+
+def floor_prod(a, r):
+    """floor(a * r) of the exact real product = RD64(a * r + 2^52) - 2^52, the kernel's
+    v_fma_f64 in round-toward--inf mode (a < 2^50 integer-valued, r > 0)."""
+    a = np.asarray(a).astype(np.float64)
+    p, e = _two_prod(a, np.asarray(r, np.float64))
+    fp = np.floor(p)
+    # p < 2^51: a non-integer p is >= ulp(p) away from every integer and |e| <= ulp/2
+    return np.where((p == fp) & (e < 0.0), fp - 1.0, fp).astype(np.int64)
+
+
 def fast_qc(fc, c):
-    return np.trunc(np.asarray(fc).astype(np.float64) * recip_up_f64(c)).astype(np.int64)
+    return floor_prod(fc, recip_up_f64(c))
 
 
 def fast_qm(fm, m):
-    return np.trunc(np.asarray(fm).astype(np.float64) * recip_up_f64(m)).astype(np.int64)
+    return floor_prod(fm, recip_up_f64(m))
+
+
+def test_floor_prod_model_vs_rationals():
+    """The numpy model of the RD FMA against exact rational arithmetic."""
+    from fractions import Fraction
+    rng = np.random.default_rng(5)
+    a = np.concatenate([rng.integers(0, FC_MAX, 3000), rng.integers(0, 1 << 20, 3000)])
+    b = np.concatenate([rng.integers(1, C_MAX, 3000), rng.integers(1, 1 << 12, 3000)])
+    a = np.concatenate([a, (a[:2000] // b[:2000]) * b[:2000]])  # exact multiples
+    b = np.concatenate([b, b[:2000]])
+    r = recip_up_f64(b)
+    got = floor_prod(a, r)
+    want = [int(Fraction(int(x)) * Fraction(float(y)) // 1) for x, y in zip(a, r)]
+    np.testing.assert_array_equal(got, np.array(want, np.int64))
+
+
+def test_round_mode_matters():
+    """With the default round-to-nearest the same biased FMA rounds the quotient to the
+    NEAREST integer: the kernel's s_setreg to round-toward--inf is load-bearing."""
+    fc = np.arange(1, 1 << 14, dtype=np.int64)
+    c = 3
+    p, e = _two_prod(fc.astype(np.float64), recip_up_f64(np.full(fc.size, c)))
+    nearest = np.rint(p + e).astype(np.int64)
+    assert np.count_nonzero(nearest != fc // c) > fc.size // 4
+    np.testing.assert_array_equal(fast_qc(fc, np.full(fc.size, c)), fc // c)
 
 
 def _cpu_pairs(rng):
@@ -146,10 +197,11 @@ def test_fast_contribution_matches_oracle(seed):
     fm = np.minimum(k * sm[j] + rng.integers(-1, 2, n), FM_MAX - 1).clip(0)
     P = k + rng.integers(-2, 3, n)
     pc = rng.integers(0, 300, n)
-    qc = fast_qc(fc[:, None], sc[None, :])
-    qm = np.minimum(fast_qm(fm[:, None], sm[None, :]), 2**31 - 1)
-    x = np.minimum(qc, qm)
-    contrib = np.where(x >= P[:, None], (P - pc)[:, None], x)
+    qc = fast_qc(fc[:, None], sc[None, :])          # x' - 2^52 of the kernel, exact
+    qm = fast_qm(fm[:, None], sm[None, :])
+    x = np.minimum(qc, qm)                          # v_min_f64 of the biased values
+    low32 = (x & 0xFFFFFFFF).astype(np.uint32).view(np.int32).astype(np.int64)
+    contrib = np.where(x >= P[:, None], (P - pc)[:, None], low32)  # v_cmp_f64 + v_cndmask
     tot = contrib.sum(axis=0)
     zero = np.zeros(n, np.int64)
     ot, oe = coracle.fit(fc.astype(np.uint64), fm, P, pc, zero.astype(np.uint64), zero,

@@ -1,9 +1,11 @@
 """Static ISA checks of the gfx950 kernels (CPU: hipcc cross-compiles).
 
-  - the fit kernel's fast loop, one 8-node FitGroup per iteration: 40 dwords of scalar
-    loads (fc, fm, P), two uniform 16-B buffer loads (cl), no 64-bit integer division,
-    no correction multiply, and exactly bench.FIT_VALU_PER_NODE_WAVE VALU instructions
-    per node (the VALU-roofline accounting of bench.py);
+  - the fit kernel's fast loop, one 8-node FitGroup per iteration: 48 dwords of scalar
+    loads (fc, fm, Pb), two uniform 16-B buffer loads (cl), no 64-bit integer division,
+    no conversion, and exactly bench.FIT_VALU_PER_NODE_WAVE VALU instructions per node
+    (the VALU-roofline accounting of bench.py);
+  - the loop runs inside the round-toward--inf window of the f64 mode (our two
+    s_setreg writes), and the compiler inserts no mode switch of its own;
   - no kernel spills to scratch.
 """
 import os
@@ -38,7 +40,7 @@ def kernel_body(asm, name):
 def test_fit_fast_loop(asm):
     import bench
     body = kernel_body(asm, "fit_kernel")
-    i = body.index(";;#ASMSTART")
+    i = body.index("v_fma_f64")
     loop = body[body.rfind(".LBB", 0, i):body.index("s_cbranch", i)]
     lines = [ln.strip() for ln in loop.splitlines()
              if ln.strip() and not ln.strip().startswith(";")]
@@ -47,16 +49,28 @@ def test_fit_fast_loop(asm):
     width = {"s_load_dword": 1, "s_load_dwordx2": 2, "s_load_dwordx4": 4, "s_load_dwordx8": 8,
              "s_load_dwordx16": 16}
     dwords = sum(width[ln.split()[0]] for ln in lines if ln.startswith("s_load_dword"))
-    assert dwords == group * 5  # fc (f64), fm (f64), P (i32) of each node
+    assert dwords == group * 6  # fc, fm, Pb (f64) of each node
     vmem = [ln for ln in lines if ln.startswith(("global_load", "flat_load", "buffer_load"))]
     assert len(vmem) == 2 and all(ln.startswith("buffer_load_dwordx4") and ", off," in ln
                                   for ln in vmem)  # cl: uniform address, no VGPR offset
     assert len(valu) / group == pytest.approx(bench.FIT_VALU_PER_NODE_WAVE, abs=1e-9), \
         f"{len(valu)} VALU / {group} nodes: update bench.FIT_VALU_PER_NODE_WAVE"
     ops = [ln.split()[0] for ln in valu]
-    assert ops.count("v_mul_f64") == 2 * group and ops.count("v_min_f64") == group
-    assert ops.count("v_cvt_i32_f64") == group and ops.count("v_add3_u32") == group // 2
-    assert not any(o.startswith(("v_mad", "v_fma", "v_mul_lo", "v_mul_hi")) for o in ops)
+    assert ops.count("v_fma_f64") == 2 * group and ops.count("v_min_f64") == group
+    assert sum(o.startswith("v_cmp_") and "_f64" in o for o in ops) == group
+    assert sum(o.startswith("v_cndmask_b32") for o in ops) == group
+    assert ops.count("v_add3_u32") == group // 2
+    assert not any(o.startswith(("v_mad", "v_cvt", "v_mul", "v_max")) for o in ops)
+
+
+def test_fit_round_mode_window(asm):
+    body = kernel_body(asm, "fit_kernel")
+    sets = [(m.start(), m.group(1)) for m in
+            re.finditer(r"s_setreg\w*\s+hwreg\(HW_REG_MODE[^)]*\),\s*(\S+)", body)]
+    assert [v for _, v in sets] == ["2", "0"], sets  # round down, then back to nearest
+    fmas = [m.start() for m in re.finditer(r"v_fma_f64", body)]
+    assert fmas and all(sets[0][0] < f < sets[1][0] for f in fmas)
+    assert "hwreg(HW_REG_MODE, 2, 2)" in body
 
 
 def test_no_scratch(asm):
