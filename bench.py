@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 #    kernel's ISA (pinned by tests/test_isa.py);
 #  - issue peak: one wave64 VALU instruction per SIMD per 4 cycles (PMC: every
 #    SQ_INSTS_VALU costs one SQ_ACTIVE_INST_VALU quad-cycle), 256 CUs x 4 SIMDs x 2.4 GHz.
-FIT_VALU_PER_NODE_WAVE = 5.5
+FIT_VALU_PER_NODE_WAVE = 5.0
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions / s
 METRIC = "node×spec fit evals/sec at 1M nodes × 4K specs; % of HBM roofline"
 # per-launch HBM traffic of each kernel from rocprofv3 PMC passes of this same bench
@@ -166,7 +166,7 @@ def main():
         value = n * S * args.emulate_world / (elapsed / args.steps)
 
     # algorithmic bytes per launch (DESIGN.md "Roofline accounting")
-    fit_bytes = n * 28 + S * 32 + S * 8            # FitGroup fields + spec records in, totals out
+    fit_bytes = n * 20 + S * 48 + S * 8            # FitGroupA fields + spec records in, totals out
     red_bytes = C * 16 + (n + 1) * 8 + n * 16      # requests + CSR offsets in, sums out
     fit_gbs = fit_bytes / (fit_ms * 1e-3) / 1e9
     fit_valu = n * ((S + 63) // 64) * FIT_VALU_PER_NODE_WAVE / (fit_ms * 1e-3)

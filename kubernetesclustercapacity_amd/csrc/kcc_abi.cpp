@@ -41,7 +41,7 @@ struct Dev {
   int device = 0;
   hipStream_t stream = nullptr;
   // workspace of the *_async entry points
-  DevBuf wave_node, fast, slow, slow_list, srec, sperm, counters;
+  DevBuf wave_node, fast_a, fast_b, slow, slow_list, srec, sperm, counters;
   int64_t last_pairs = 0;  // node x spec pairs of the last fit_prepare on this device
   int64_t prep_nodes = -1, prep_specs = -1;  // sizes the workspace was last prepared for
   // staging of the host-array entry points
@@ -158,12 +158,13 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   const size_t S = (size_t)(n_specs > 0 ? n_specs : 1);
   const int64_t waves = kcc::reduce_max_waves(n_cont > 0 ? n_cont : 1);
   KCC_HIP(ctx, ensure(dv.wave_node, sizeof(int64_t) * (size_t)waves));
-  KCC_HIP(ctx, ensure(dv.fast, sizeof(kcc::FitGroup) * (size_t)kcc::fit_groups((int64_t)N)));
+  KCC_HIP(ctx, ensure(dv.fast_a, sizeof(kcc::FitGroupA) * (size_t)kcc::fit_groups((int64_t)N)));
+  KCC_HIP(ctx, ensure(dv.fast_b, sizeof(kcc::FitGroup) * (size_t)kcc::fit_groups((int64_t)N)));
   KCC_HIP(ctx, ensure(dv.slow, sizeof(kcc::SlowNode) * N));
   KCC_HIP(ctx, ensure(dv.slow_list, sizeof(int64_t) * N));
   KCC_HIP(ctx, ensure(dv.srec, sizeof(kcc::SpecRec) * S));
   KCC_HIP(ctx, ensure(dv.sperm, 4 * S));
-  KCC_HIP(ctx, ensure(dv.counters, 64));
+  KCC_HIP(ctx, ensure(dv.counters, sizeof(unsigned long long) * kcc::CNT_N));
   return KCC_OK;
 }
 
@@ -189,8 +190,9 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
                                      as<unsigned long long>(dv.counters), s));
   if (n_nodes == 0) return KCC_OK;
   KCC_HIP(ctx, kcc::launch_node_prep(n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count,
-                                     used_cpu, used_mem, as<kcc::FitGroup>(dv.fast),
-                                     as<kcc::SlowNode>(dv.slow), as<int64_t>(dv.slow_list),
+                                     used_cpu, used_mem, as<kcc::FitGroupA>(dv.fast_a),
+                                     as<kcc::FitGroup>(dv.fast_b), as<kcc::SlowNode>(dv.slow),
+                                     as<int64_t>(dv.slow_list),
                                      as<unsigned long long>(dv.counters), s));
   return KCC_OK;
 }
@@ -201,7 +203,8 @@ int fit_run_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_specs, int64_t
     return fail(ctx, KCC_EINVAL, "fit_run sizes differ from the preceding fit_prepare");
   if (n_nodes == 0 || n_specs == 0) return KCC_OK;
   if (!partial) return fail(ctx, KCC_EINVAL, "NULL partial");
-  KCC_HIP(ctx, kcc::launch_fit(n_nodes, as<kcc::FitGroup>(dv.fast), as<kcc::SlowNode>(dv.slow),
+  KCC_HIP(ctx, kcc::launch_fit(n_nodes, as<kcc::FitGroupA>(dv.fast_a), as<kcc::FitGroup>(dv.fast_b),
+                               as<kcc::SlowNode>(dv.slow),
                                as<int64_t>(dv.slow_list), n_specs, spec_prep_of(dv), partial,
                                as<unsigned long long>(dv.counters), s));
   return KCC_OK;
@@ -401,7 +404,7 @@ void kcc_destroy(kcc_ctx* ctx) {
   for (Dev& dv : ctx->devs) {
     (void)hipSetDevice(dv.device);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
-    DevBuf* bufs[] = {&dv.wave_node, &dv.slow_list, &dv.fast,      &dv.slow,      &dv.srec,
+    DevBuf* bufs[] = {&dv.wave_node, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
                       &dv.sperm,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
                       &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,

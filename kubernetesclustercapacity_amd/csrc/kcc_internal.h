@@ -55,17 +55,30 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t n_containers, const int64_t* n
                          uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s);
 
 // ---- (b) fit -----------------------------------------------------------------
-// Node stream of the fit kernel: groups of FIT_GROUP nodes, field-major inside the
-// group (224 B).  fc/fm/Pb arrive through the scalar cache (SGPR operands of the VALU),
+// Node streams of the fit kernel: groups of FIT_GROUP nodes, field-major inside the
+// group.  Per-node values arrive through the scalar cache (SGPR operands of the VALU),
 // cl by one uniform-address vector load (it is a v_cndmask operand, and gfx9 allows a
-// single SGPR/VCC read per VALU instruction).  Rows outside the fast-path bounds, and
-// the padding of the last group, hold all-zero fields (contribute exactly 0: x' = 2^52
-// >= Pb = 0 selects cl = 0) and are listed in slow_list for the exact path.
+// single SGPR read per VALU instruction besides the lane mask).  Rows outside the
+// fast-path bounds, and the padding of the last group, hold all-zero fields (they
+// contribute exactly 0) and are listed in slow_list for the exact path.
+//
+// FitGroupA — class-A spec waves: the integers themselves, which the
+// VALU reads as IEEE denormals (an integer k < 2^23 is the f32 bit pattern of
+// k * 2^-149, k < 2^52 the f64 pattern of k * 2^-1074).
 constexpr int FIT_GROUP = 8;
+struct __attribute__((aligned(32))) FitGroupA {
+  uint64_t fm[FIT_GROUP];  // free memory (bytes), < 2^50
+  uint32_t fc[FIT_GROUP];  // free CPU (millicores), < 2^23
+  uint32_t P[FIT_GROUP];   // max(allocatable pods, 0), <= 2^20
+  int32_t cl[FIT_GROUP];   // clamp value allocatable pods - podCount (CC:135)
+};
+static_assert(sizeof(FitGroupA) == 160, "FitGroupA must be 160 B");
+// FitGroup — class-B spec waves (memory request < 2^18): f64 values for the biased
+// FMA path; written by node_prep only when such specs exist.
 constexpr double FIT_BIAS = 4503599627370496.0;  // 2^52: integers in [2^52, 2^53) have ulp 1
 struct __attribute__((aligned(32))) FitGroup {
-  double fc[FIT_GROUP];   // free CPU (millicores), exact in f64 on the fast path (< 2^50)
-  double fm[FIT_GROUP];   // free memory (bytes), exact in f64 on the fast path (< 2^50)
+  double fc[FIT_GROUP];   // free CPU (millicores), exact in f64
+  double fm[FIT_GROUP];   // free memory (bytes), exact in f64
   double Pb[FIT_GROUP];   // 2^52 + allocatable pods (|P| <= 2^20: exact), the biased compare operand
   int32_t cl[FIT_GROUP];  // clamp value allocatable pods - podCount (CC:135)
 };
@@ -82,24 +95,29 @@ struct __attribute__((aligned(32))) SlowNode {
 };
 static_assert(sizeof(SlowNode) == 32, "SlowNode must be 32 B");
 
-// One 32-B record per spec, in the kernel's internal (partitioned) order: specs that
-// satisfy the fast-path bounds first, the rest after (so at most one wavefront mixes
-// both).  rc == 0 marks a spec for the exact path (a fast-path rc is > 0).
-struct __attribute__((aligned(32))) SpecRec {
+// One 48-B record per spec, in the kernel's internal (partitioned) order: class A
+// first, then B, then the exact-path specs (so at most two wavefronts mix classes;
+// a wave runs the most general class among its lanes).
+enum SpecClass : int32_t { SPEC_A = 0, SPEC_B = 1, SPEC_EXACT = 2 };
+struct __attribute__((aligned(16))) SpecRec {
   uint64_t c;    // cpu request (millicores)
   int64_t m;     // memory request (bytes)
-  double rc;     // smallest f64 >= 1/c (see fit_kernel); 0 marks a spec off the fast path
-  double rm;     // smallest f64 >= 1/m
+  double rc;     // smallest f64 >= 1/c (classes A, B)
+  double rm;     // smallest f64 >= 1/m (classes A, B)
+  float rcf;     // smallest f32 >= 1/c (class A)
+  int32_t cls;   // SpecClass
+  int64_t pad;
 };
-static_assert(sizeof(SpecRec) == 32, "SpecRec must be 32 B");
+static_assert(sizeof(SpecRec) == 48, "SpecRec must be 48 B");
 
 struct SpecPrep {
   SpecRec* rec;
   int32_t* perm;  // internal index -> caller index
 };
 
-// counters: [0] (node, spec) pairs on the exact path, [1] rows in slow_list.
-// spec_prep zeroes partial[0..2S) and counters[0..1]; node_prep appends to slow_list.
+// counters (CNT_*): exact-path (node, spec) pairs, rows in slow_list, class-B specs.
+// spec_prep zeroes partial[0..2S) and the counters; node_prep appends to slow_list.
+enum { CNT_SLOW_PAIRS = 0, CNT_SLOW_ROWS = 1, CNT_SPECS_B = 2, CNT_N = 4 };
 hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
                             const int64_t* spec_mem, SpecPrep sp, int64_t* partial,
                             unsigned long long* counters, hipStream_t s);
@@ -107,11 +125,13 @@ hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
 hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
-                            const int64_t* used_mem, FitGroup* fast, SlowNode* slow,
-                            int64_t* slow_list, unsigned long long* counters, hipStream_t s);
+                            const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
+                            SlowNode* slow, int64_t* slow_list, unsigned long long* counters,
+                            hipStream_t s);
 
 // partial[0..S) += Σ_i q(i,s), partial[S..2S) += #div-by-zero rows (internal order).
-hipError_t launch_fit(int64_t n_nodes, const FitGroup* fast, const SlowNode* slow,
+hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,
+                      const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, hipStream_t s);
 

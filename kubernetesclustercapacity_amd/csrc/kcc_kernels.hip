@@ -290,37 +290,42 @@ __global__ __launch_bounds__(256) void reduce_kernel(
 // ----------------------------------------------------------------------------
 
 // Fast-path bounds (see DESIGN.md "Fit fast path: exactness argument").
-constexpr uint64_t FAST_FC_MAX = 1ull << 50;    // free CPU < 2^50 (f64 quotient exact)
+constexpr uint64_t FAST_FC_MAX = 1ull << 23;    // free CPU < 2^23 (f32 quotient exact)
 constexpr int64_t FAST_FM_MAX = 1ll << 50;      // 0 <= free mem < 2^50 (f64 quotient exact)
 constexpr int64_t FAST_P_ABS = 1ll << 20;       // |allocatable pods| <= 2^20
 constexpr int64_t FAST_CL_ABS = 1ll << 20;      // |allocPods - podCount| <= 2^20
 constexpr uint64_t FAST_C_MAX = 1ull << 51;     // 1 <= spec cpu < 2^51
 constexpr int64_t FAST_M_MAX = 1ll << 51;       // 1 <= spec mem < 2^51
+constexpr int64_t CLASS_A_M_MIN = 1ll << 18;    // class A: spec mem >= 2^18, so fm/m < 2^32
 
-__device__ __forceinline__ bool spec_is_normal(uint64_t c, int64_t m) {
-  return c >= 1 && c < FAST_C_MAX && m >= 1 && m < FAST_M_MAX;
+__device__ __forceinline__ int32_t spec_class(uint64_t c, int64_t m) {
+  if (c < 1 || c >= FAST_C_MAX || m < 1 || m >= FAST_M_MAX) return SPEC_EXACT;
+  return m >= CLASS_A_M_MIN ? SPEC_A : SPEC_B;
 }
 
 // Per-node free capacity (CC:119-135 operands).  Rows that fit the fast-path
-// bounds get exact FitGroup fields; the others get all-zero fields (contribute
-// exactly 0 on the fast path) and are appended to slow_list for the exact 64-bit
-// path.  Covers the padding of the last group too (zero fields, not listed).
+// bounds get exact FitGroupA fields (and FitGroup fields when class-B specs exist);
+// the others get all-zero fields (contribute exactly 0 on the fast paths) and are
+// appended to slow_list for the exact 64-bit path.  Covers the padding of the last
+// group too (zero fields, not listed).
 __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_cpu,
                                  const int64_t* __restrict__ alloc_mem,
                                  const int64_t* __restrict__ alloc_pods,
                                  const int64_t* __restrict__ pod_count,
                                  const uint64_t* __restrict__ used_cpu,
                                  const int64_t* __restrict__ used_mem,
-                                 FitGroup* __restrict__ fast, SlowNode* __restrict__ slow,
-                                 int64_t* __restrict__ slow_list,
+                                 FitGroupA* __restrict__ fast_a, FitGroup* __restrict__ fast_b,
+                                 SlowNode* __restrict__ slow, int64_t* __restrict__ slow_list,
                                  unsigned long long* __restrict__ counters) {
   const int lane = threadIdx.x & 63;
   const int64_t n_pad = fit_groups(n) * FIT_GROUP;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const bool want_b = counters[CNT_SPECS_B] != 0;  // written by spec_prep (same stream)
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i - lane < n_pad; i += stride) {
     const bool valid = i < n;
     bool ok = false;
-    double fc_d = 0.0, fm_d = 0.0, Pb_d = 0.0;
+    uint64_t fc_ok = 0;
+    int64_t fm_ok = 0, P_ok = 0;
     int32_t cl_i = 0;
     if (valid) {
       const uint64_t ac = alloc_cpu[i], uc = used_cpu[i];
@@ -332,9 +337,9 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
       ok = fc < FAST_FC_MAX && fm >= 0 && fm < FAST_FM_MAX && P >= -FAST_P_ABS &&
            P <= FAST_P_ABS && cl >= -FAST_CL_ABS && cl <= FAST_CL_ABS;
       if (ok) {
-        fc_d = (double)fc;  // exact (< 2^50)
-        fm_d = (double)fm;  // exact (< 2^50)
-        Pb_d = FIT_BIAS + (double)P;  // exact (|P| <= 2^20)
+        fc_ok = fc;
+        fm_ok = fm;
+        P_ok = P;
         cl_i = (int32_t)cl;
       }
       SlowNode sn;
@@ -345,17 +350,24 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
       slow[i] = sn;
     }
     if (i < n_pad) {
-      FitGroup& g = fast[i / FIT_GROUP];
       const int k = (int)(i % FIT_GROUP);
-      g.fc[k] = fc_d;
-      g.Pb[k] = Pb_d;
-      g.fm[k] = fm_d;
-      g.cl[k] = cl_i;
+      FitGroupA& a = fast_a[i / FIT_GROUP];
+      a.fm[k] = (uint64_t)fm_ok;
+      a.fc[k] = (uint32_t)fc_ok;
+      a.P[k] = (uint32_t)(P_ok > 0 ? P_ok : 0);  // P <= 0: x >= P always (clamp), as for P = 0
+      a.cl[k] = cl_i;
+      if (want_b) {
+        FitGroup& g = fast_b[i / FIT_GROUP];
+        g.fc[k] = (double)fc_ok;                          // exact
+        g.fm[k] = (double)fm_ok;                          // exact (< 2^50)
+        g.Pb[k] = ok ? FIT_BIAS + (double)P_ok : 0.0;     // exact (|P| <= 2^20)
+        g.cl[k] = cl_i;
+      }
     }
     const unsigned long long b = __ballot(valid && !ok);
     if (b) {
       unsigned long long base = 0;
-      if (lane == 0) base = atomicAdd(&counters[1], (unsigned long long)__popcll(b));
+      if (lane == 0) base = atomicAdd(&counters[CNT_SLOW_ROWS], (unsigned long long)__popcll(b));
       base = __shfl(base, 0);
       if (valid && !ok) slow_list[base + __popcll(b & ((1ull << lane) - 1ull))] = i;
     }
@@ -371,14 +383,26 @@ __device__ __forceinline__ double recip_up_f64(uint64_t v) {
   return r;
 }
 
-// Single-workgroup stable partition of the specs (fast-path specs first), in two
-// passes over contiguous per-thread chunks with one block-wide exclusive scan in
-// between.  Also zeroes partial[0..2S) and counters[0..1] (no memset launches).
+// Smallest f32 >= 1/v (1 <= v < 2^51, exact in f64).  1/v is first rounded to f64,
+// then to f32 (a double rounding can only land on the upper neighbour when that one is
+// already the smallest upper bound); the exact sign of r*v - 1 (fma, one rounding of a
+// value that is either 0 or >= 2^-75 in magnitude) fixes an undershoot.
+__device__ __forceinline__ float recip_up_f32(uint64_t v) {
+  const double vd = (double)v;
+  float r = (float)(1.0 / vd);
+  if (fma((double)r, vd, -1.0) < 0.0) r = __uint_as_float(__float_as_uint(r) + 1u);  // next up
+  return r;
+}
+
+// Single-workgroup stable 3-way partition of the specs (class A, then B, then the
+// exact-path specs), in two passes over contiguous per-thread chunks with one
+// block-wide exclusive scan of the per-class counts in between.  Also zeroes
+// partial[0..2S) and sets the counters (no memset launches).
 __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64_t* __restrict__ c_in,
                                                          const int64_t* __restrict__ m_in,
                                                          SpecPrep sp, int64_t* __restrict__ partial,
                                                          unsigned long long* __restrict__ counters) {
-  __shared__ int64_t wsum[16];
+  __shared__ int64_t wsum[16][2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t per = (S + 1023) / 1024;
   const int64_t b0 = tid * per < S ? tid * per : S;
@@ -414,95 +438,124 @@ __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64
     }
     return m_in[i];
   };
-  int64_t cnt = 0;
-  for (int64_t i = b0; i < b1; ++i) cnt += spec_is_normal(spec_c(i), spec_m(i)) ? 1 : 0;
-  // block exclusive scan of cnt (wave shuffles + 16 wave totals in LDS)
-  int64_t incl = cnt;
+  int64_t cnt[2] = {0, 0};  // class A, class B
+  for (int64_t i = b0; i < b1; ++i) {
+    const int32_t k = spec_class(spec_c(i), spec_m(i));
+    cnt[0] += k == SPEC_A ? 1 : 0;
+    cnt[1] += k == SPEC_B ? 1 : 0;
+  }
+  // block exclusive scans of both counts (wave shuffles + 16 wave totals in LDS)
+  int64_t incl[2] = {cnt[0], cnt[1]};
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    const int64_t u = __shfl_up(incl, d);
-    if (lane >= d) incl += u;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t u = __shfl_up(incl[q], d);
+      if (lane >= d) incl[q] += u;
+    }
   }
-  if (lane == 63) wsum[wv] = incl;
+  if (lane == 63) {
+    wsum[wv][0] = incl[0];
+    wsum[wv][1] = incl[1];
+  }
   __syncthreads();
-  int64_t wbase = 0, tot_n = 0;
+  int64_t wbase[2] = {0, 0}, tot[2] = {0, 0};
   for (int k = 0; k < 16; ++k) {
-    if (k < wv) wbase += wsum[k];
-    tot_n += wsum[k];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (k < wv) wbase[q] += wsum[k][q];
+      tot[q] += wsum[k][q];
+    }
   }
-  int64_t pn = wbase + incl - cnt;  // my first fast-path slot
-  int64_t pa = tot_n + (b0 - (wbase + incl - cnt));  // my first exact-path slot
+  const int64_t ea = wbase[0] + incl[0] - cnt[0], eb = wbase[1] + incl[1] - cnt[1];
+  int64_t pa = ea;                         // my first class-A slot
+  int64_t pb = tot[0] + eb;                // my first class-B slot
+  int64_t px = tot[0] + tot[1] + (b0 - ea - eb);  // my first exact-path slot
   for (int64_t i = b0; i < b1; ++i) {
     const uint64_t c = spec_c(i);
     const int64_t m = spec_m(i);
-    const bool nm = spec_is_normal(c, m);
-    const int64_t pos = nm ? pn++ : pa++;
+    const int32_t k = spec_class(c, m);
+    const int64_t pos = k == SPEC_A ? pa++ : (k == SPEC_B ? pb++ : px++);
     SpecRec r;
     r.c = c;
     r.m = m;
-    r.rc = nm ? recip_up_f64(c) : 0.0;
-    r.rm = nm ? recip_up_f64((uint64_t)m) : 0.0;
+    r.rc = k != SPEC_EXACT ? recip_up_f64(c) : 0.0;
+    r.rm = k != SPEC_EXACT ? recip_up_f64((uint64_t)m) : 0.0;
+    r.rcf = k == SPEC_A ? recip_up_f32(c) : 0.0f;
+    r.cls = k;
+    r.pad = 0;
     sp.rec[pos] = r;
     sp.perm[pos] = (int32_t)i;
   }
   for (int64_t i = tid; i < 2 * S; i += 1024) partial[i] = 0;
-  if (tid == 0) {
-    counters[0] = 0;
-    counters[1] = 0;
-  }
+  if (tid < CNT_N) counters[tid] = tid == CNT_SPECS_B ? (unsigned long long)tot[1] : 0ull;
 }
 
 // Lane = spec (its request, reciprocals and running total live in VGPRs); the node
-// stream is wave-uniform: fc/P/fm of a FitGroup arrive by scalar loads and feed the
-// VALU as SGPR operands, cl by one uniform-address buffer load.  The main loop is
+// stream is wave-uniform: the fields of a FitGroup arrive by scalar loads and feed the
+// VALU as SGPR operands, cl by one uniform-address buffer load.  The main loops are
 // branch-free: rows outside the fast bounds carry zero fields and are re-done exactly
 // from slow_list.  No cross-lane reduction until the block's end (one 64-bit atomic
-// per spec).
+// per spec).  Everything below is exact ("Fit fast path: exactness").
 //
-// Fast path per (node, spec), exact (DESIGN.md "Fit fast path: exactness argument"):
-//   rc = smallest f64 >= 1/c, rm = smallest f64 >= 1/m (spec_prep); fc, fm < 2^50
-//   are exact in f64.  The loop runs with the f64 rounding mode set to round toward
-//   -inf, and one fused multiply-add per quotient does floor AND the conversion:
-//     qc' = RD(fc * rc + 2^52) = 2^52 + floor(fc / c)
-//     qm' = RD(fm * rm + 2^52) = 2^52 + floor(fm / m)
-//   (the fused product is exact; an integer quotient is never below it since the
-//   reciprocal is rounded up, a non-integer one lies >= 1/c below the next integer,
-//   more than the relative error (< 2^-52) can cover while fc < 2^52; in [2^52, 2^53)
-//   the ulp is 1, so rounding down IS floor).  Then
-//     x' = min(qc', qm') = 2^52 + findMin(qc, qm)                      (CC:159-164)
-//     contribution = x' >= 2^52 + P ? P - podCount : low32(x')          (CC:133-136)
-//   low32(x') = x exactly whenever it is used (x < P <= 2^20).
-// Per node and 64-spec wavefront: 2x v_fma_f64, v_min_f64, v_cmp_ge_f64, v_cndmask,
-// v_add3_u32 (two nodes) = 5.5 VALU instructions.
+// Class A (1 <= c < 2^51, 2^18 <= m < 2^51; fc < 2^23, fm < 2^50), the loop runs in
+// round-toward--inf (f32 and f64) on integers read as denormals:
+//   qc = bits(RD32(fc*2^-149 * rcf)) = floor(fc * rcf) = floor(fc / c)   (rcf = RU32(1/c))
+//     — one v_pk_mul_f32 for two nodes (an SGPR pair of free CPUs);
+//   qm = low32(bits(RD64(fm*2^-1074 * rm))) = floor(fm / m)             (rm = RU64(1/m))
+//     — one v_mul_f64 (qm < 2^50 / 2^18 = 2^32, so the low dword is all of it);
+//   m3 = min3(qc, qm, P) = min(findMin(qc, qm), P)                       (CC:159-164)
+//   contribution = m3 == P ? P - podCount : m3  (x >= P <=> m3 == P)     (CC:133-136)
+// The products are exact reals rounded once onto the 2^-149 / 2^-1074 grid, so the
+// rounding down IS floor; a quotient that is an integer is never undershot (the
+// reciprocal is rounded up), a non-integer one lies >= 1/c below the next integer,
+// more than the relative error (< 2^-23 resp. 2^-52) covers while fc < 2^23, fm < 2^52.
+// Per node and 64-spec wavefront: v_pk_mul_f32 (half), v_mul_f64, v_min3_u32,
+// v_cmp_eq_u32, v_cndmask_b32, v_add3_u32 (half) = 5 VALU instructions.
+//
+// Class B (memory requests below 2^18, where fm/m may exceed 32 bits): f64 values, the
+// loop in round-toward--inf, one fused multiply-add per quotient doing floor AND the
+// conversion: qc' = RD(fc * rc + 2^52) = 2^52 + floor(fc / c), likewise qm';
+// x' = min(qc', qm'); contribution = x' >= 2^52 + P ? P - podCount : low32(x').
+// 5.5 VALU instructions per node and wavefront.
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef int32_t i32x8 __attribute__((ext_vector_type(8)));
 typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// MODE register FP_ROUND[3:2] (f64/f16 rounding): 0 nearest-even, 2 toward -inf.  The
-// fit's fast loop runs in round-toward--inf; f32 rounding (FP_ROUND[1:0], used by the
-// compiler's 64-bit integer division expansion on the exact path) stays nearest-even.
-// Both the mode switch and the rounding-sensitive FMA are inline asm: LLVM's
-// SIModeRegister pass assumes the function's default FP mode for every FP instruction
-// it emits and would re-insert a switch back to nearest-even in front of a compiler-
-// generated v_fma_f64.  (v_min_f64 and v_cmp_*_f64 do not round.)
-__device__ __forceinline__ void set_f64_round_down() {
-  asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 2\n\ts_nop 1" ::: "memory");
+// MODE register FP_ROUND[3:0]: [1:0] f32, [3:2] f64/f16; 0 nearest-even, 2 toward -inf.
+// The fast loops run in round-toward--inf; the exact path (whose 64-bit integer
+// division the compiler expands with f32 reciprocal steps) runs in the default mode.
+// The switch is inline asm on purpose: LLVM's SIModeRegister pass would otherwise
+// re-insert a switch back to the function's default mode in front of every FP
+// instruction it emits.  Invisible to it, the compiler-generated v_mul/v_fma in the
+// loops run in the mode set here (tests/test_isa.py pins the window and checks the
+// compiler adds no switch of its own).
+__device__ __forceinline__ void set_round_down() {
+  asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 4), 10\n\ts_nop 1" ::: "memory");
 }
-__device__ __forceinline__ void set_f64_round_nearest() {
-  asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 0\n\ts_nop 1" ::: "memory");
+__device__ __forceinline__ void set_round_nearest() {
+  asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 4), 0\n\ts_nop 1" ::: "memory");
 }
-// a * r + b rounded by the current f64 mode; a is wave-uniform (SGPR operand)
-__device__ __forceinline__ double fma_f64_s(double a, double r, double b) {
-  double d;
-  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "s"(a), "v"(r), "v"(b));
-  return d;
+// m3 == P ? cl : m3, with the compare mask in an SGPR pair: a v_cndmask reading VCC
+// issues at ~23 cycles per wave64 instruction per SIMD on gfx950 against ~4 with an
+// SGPR-pair mask (scripts/probe/valu_probe.hip), and the compiler picks VCC when free.
+__device__ __forceinline__ int32_t clamp_select(uint32_t m3, uint32_t P, int32_t cl) {
+  int32_t r;
+  uint64_t mask;
+  asm("v_cmp_eq_u32_e64 %1, %2, %3\n\tv_cndmask_b32_e64 %0, %2, %4, %1"
+      : "=v"(r), "=&s"(mask)
+      : "v"(m3), "s"(P), "v"(cl));
+  return r;
 }
-// min of two FMA results (asm: the compiler cannot see they are canonical and would
-// quiet them with a v_max_f64 each first)
-__device__ __forceinline__ double min_f64(double a, double b) {
-  double d;
-  asm("v_min_f64 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
-  return d;
+// x' >= Pb ? cl : low32(x') (class B), mask in an SGPR pair likewise
+__device__ __forceinline__ int32_t clamp_select_f64(double xb, double Pb, int32_t cl) {
+  int32_t r;
+  uint64_t mask;
+  asm("v_cmp_ge_f64_e64 %1, %2, %3\n\tv_cndmask_b32_e64 %0, %4, %5, %1"
+      : "=v"(r), "=&s"(mask)
+      : "v"(xb), "s"(Pb), "v"((uint32_t)__double_as_longlong(xb)), "v"(cl));
+  return r;
 }
 
 #ifndef KCC_FIT_SPECS_PER_WG
@@ -516,11 +569,16 @@ constexpr int FIT_CHUNK_GROUPS = 128;  // 1024 nodes: |sum of contributions| <= 
 #define KCC_FIT_TARGET_BLOCKS 32768
 #endif
 
+__device__ __forceinline__ double f64_at(const i32x16& v, int k) {
+  return __longlong_as_double(((int64_t)(uint32_t)v[2 * k + 1] << 32) | (uint32_t)v[2 * k]);
+}
+
 __global__ __launch_bounds__(256) void fit_kernel(
-    int64_t n_nodes, int64_t groups_per_block, const FitGroup* __restrict__ fast,
-    const SlowNode* __restrict__ slow, const int64_t* __restrict__ slow_list, int64_t S,
-    const SpecRec* __restrict__ specs, int64_t* __restrict__ partial,
-    unsigned long long* __restrict__ counters, int32_t gx, int32_t gy) {
+    int64_t n_nodes, int64_t groups_per_block, const FitGroupA* __restrict__ fast_a,
+    const FitGroup* __restrict__ fast_b, const SlowNode* __restrict__ slow,
+    const int64_t* __restrict__ slow_list, int64_t S, const SpecRec* __restrict__ specs,
+    int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t gx,
+    int32_t gy) {
   // XCD-aware order (speed only, never correctness): workgroups are dealt round-robin
   // over the 8 XCDs, so give every spec group of one node chunk the same b % 8 — the
   // chunk's FitGroup records then stay in that XCD's L2 for all of them.
@@ -531,21 +589,22 @@ __global__ __launch_bounds__(256) void fit_kernel(
   const int32_t wv = __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6) / (FIT_SPW / 64));
   const int64_t s = (int64_t)bx * FIT_SPW + (threadIdx.x % FIT_SPW);
   const bool active = s < S;
-  SpecRec sr;  // one 32-B record per lane (two 16-B loads)
+  SpecRec sr;  // one 48-B record per lane
   if (active) {
     sr = specs[s];
-  } else {
+  } else {  // a class-A placeholder (its sums are never stored)
     sr.c = 1;
-    sr.m = 1;
-    sr.rm = 1.0;
+    sr.m = CLASS_A_M_MIN;
     sr.rc = 1.0;
+    sr.rm = 1.0 / (double)CLASS_A_M_MIN;
+    sr.rcf = 1.0f;
+    sr.cls = SPEC_A;
   }
   const uint64_t c = sr.c;
   const int64_t m = sr.m;
   const double rm = sr.rm, rc = sr.rc;
-  const double bias = FIT_BIAS;
-  const bool normal = rc > 0.0;
-  const bool wave_fast = __all(normal);
+  const bool wave_exact = __any(sr.cls == SPEC_EXACT);
+  const bool wave_b = __any(sr.cls == SPEC_B);
 
   const int64_t n_groups = fit_groups(n_nodes);
   int64_t g0 = (int64_t)by * groups_per_block;
@@ -580,19 +639,61 @@ __global__ __launch_bounds__(256) void fit_kernel(
     acc += z ? 0ull : (uint64_t)q;
   };
 
-  if (wave_fast) {
-    // cl through a buffer descriptor over this block's groups: uniform offsets, no VGPR
-    // address (every lane reads the same 16 B)
-    const FitGroup* gbase = fast + g0;
-    const int cnt = (int)(g1 - g0);
+  const int cnt = (int)(g1 - g0);
+  if (!wave_exact && !wave_b) {
+    // class A: cl through a buffer descriptor over this block's groups: uniform
+    // offsets, no VGPR address (every lane reads the same 16 B)
+    const FitGroupA* gbase = fast_a + g0;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)gbase, (short)0, cnt * (int)sizeof(FitGroup), 0x00020000);
-    set_f64_round_down();  // the FMAs are the only rounding f64 ops of the loop
+        (void*)gbase, (short)0, cnt * (int)sizeof(FitGroupA), 0x00020000);
+    const f32x2 rcf2 = {sr.rcf, sr.rcf};
+    set_round_down();
     for (int cb = 0; cb < cnt; cb += FIT_CHUNK_GROUPS) {
       const int ce = cb + FIT_CHUNK_GROUPS < cnt ? cb + FIT_CHUNK_GROUPS : cnt;
       int32_t acc32 = 0;
       for (int gi = cb; gi < ce; ++gi) {
         // index opaque to loop-strength reduction: one base per group, immediate offsets
+        int io = gi;
+        asm volatile("" : "+s"(io));
+        const FitGroupA* g = gbase + io;
+        const int so = io * (int)sizeof(FitGroupA) + (int)offsetof(FitGroupA, cl);
+        const i32x4 c0 = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, so, 0));
+        const i32x4 c1 = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, so + 16, 0));
+        const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
+        const i32x8 fcv = *reinterpret_cast<const i32x8*>(g->fc);
+        const i32x8 Pv = *reinterpret_cast<const i32x8*>(g->P);
+        const int32_t cl[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+        for (int u = 0; u < FIT_GROUP / 2; ++u) {
+          const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
+          const f32x2 q = fcp * rcf2;  // two nodes' floor(fc / c), as integers
+          int32_t x[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int k = 2 * u + h;
+            const uint32_t qm = (uint32_t)__double_as_longlong(f64_at(fmv, k) * rm);
+            const uint32_t qc = __float_as_uint(h ? q.y : q.x);
+            const uint32_t Pk = (uint32_t)Pv[k];
+            const uint32_t m3 = min(min(qc, qm), Pk);
+            x[h] = clamp_select(m3, Pk, cl[k]);
+          }
+          acc32 += x[0] + x[1];
+        }
+      }
+      acc += (uint64_t)(int64_t)acc32;
+    }
+    set_round_nearest();
+  } else if (!wave_exact) {
+    // class B (and class-A lanes sharing its wave)
+    const FitGroup* gbase = fast_b + g0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)gbase, (short)0, cnt * (int)sizeof(FitGroup), 0x00020000);
+    const double bias = FIT_BIAS;
+    set_round_down();
+    for (int cb = 0; cb < cnt; cb += FIT_CHUNK_GROUPS) {
+      const int ce = cb + FIT_CHUNK_GROUPS < cnt ? cb + FIT_CHUNK_GROUPS : cnt;
+      int32_t acc32 = 0;
+      for (int gi = cb; gi < ce; ++gi) {
         int io = gi;
         asm volatile("" : "+s"(io));
         const FitGroup* g = gbase + io;
@@ -603,40 +704,36 @@ __global__ __launch_bounds__(256) void fit_kernel(
         const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
         const i32x16 Pv = *reinterpret_cast<const i32x16*>(g->Pb);
         const int32_t cl[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-        auto f64_at = [](const i32x16& v, int k) {
-          return __longlong_as_double(((int64_t)(uint32_t)v[2 * k + 1] << 32) | (uint32_t)v[2 * k]);
-        };
 #pragma unroll
         for (int u = 0; u < FIT_GROUP / 2; ++u) {
           int32_t x[2];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int k = 2 * u + h;
-            const double qc = fma_f64_s(f64_at(fcv, k), rc, bias);  // 2^52 + floor(fc/c)
-            const double qm = fma_f64_s(f64_at(fmv, k), rm, bias);  // 2^52 + floor(fm/m)
-            const double xb = min_f64(qc, qm);
-            const int32_t lo = (int32_t)(uint32_t)__double_as_longlong(xb);
-            x[h] = xb >= f64_at(Pv, k) ? cl[k] : lo;
+            const double qc = __builtin_fma(f64_at(fcv, k), rc, bias);  // 2^52 + floor(fc/c)
+            const double qm = __builtin_fma(f64_at(fmv, k), rm, bias);  // 2^52 + floor(fm/m)
+            x[h] = clamp_select_f64(__builtin_fmin(qc, qm), f64_at(Pv, k), cl[k]);
           }
           acc32 += x[0] + x[1];
         }
       }
       acc += (uint64_t)(int64_t)acc32;
     }
-    set_f64_round_nearest();
-    // rows outside the fast bounds, shared out over the node-chunk waves
-    const int64_t n_slow = (int64_t)counters[1];
-    for (int64_t j = (int64_t)by * FIT_SPLIT + wv; j < n_slow; j += (int64_t)gy * FIT_SPLIT)
-      eval_slow(slow_list[j]);
+    set_round_nearest();
   } else {
     const int64_t i1 = g1 * FIT_GROUP < n_nodes ? g1 * FIT_GROUP : n_nodes;
     for (int64_t i = g0 * FIT_GROUP; i < i1; ++i) eval_slow(i);
+  }
+  if (!wave_exact) {  // rows outside the fast bounds, shared out over the node-chunk waves
+    const int64_t n_slow = (int64_t)counters[CNT_SLOW_ROWS];
+    for (int64_t j = (int64_t)by * FIT_SPLIT + wv; j < n_slow; j += (int64_t)gy * FIT_SPLIT)
+      eval_slow(slow_list[j]);
   }
 
   {  // (node, spec) pairs evaluated on the exact path (statistics)
     const unsigned long long act = __ballot(active);
     if (slow_iters && (threadIdx.x & 63) == 0)
-      atomicAdd(counters, (unsigned long long)slow_iters * (unsigned long long)__popcll(act));
+      atomicAdd(&counters[CNT_SLOW_PAIRS], (unsigned long long)slow_iters * (unsigned long long)__popcll(act));
   }
   if (FIT_SPLIT > 1) {  // the waves of one spec group meet in LDS: one atomic per spec
     __shared__ uint64_t red_s[2][FIT_SPLIT][FIT_SPW];
@@ -720,12 +817,13 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t n_containers, const int64_t* n
 hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
-                            const int64_t* used_mem, FitGroup* fast, SlowNode* slow,
-                            int64_t* slow_list, unsigned long long* counters, hipStream_t s) {
+                            const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
+                            SlowNode* slow, int64_t* slow_list, unsigned long long* counters,
+                            hipStream_t s) {
   if (n_nodes <= 0) return hipSuccess;
   hipLaunchKernelGGL(node_prep_kernel, dim3(grid_for(fit_groups(n_nodes) * FIT_GROUP, 256, 8192)), dim3(256), 0, s,
                      n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu, used_mem,
-                     fast, slow, slow_list, counters);
+                     fast_a, fast_b, slow, slow_list, counters);
   return hipGetLastError();
 }
 
@@ -738,7 +836,8 @@ hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu, const int
   return hipGetLastError();
 }
 
-hipError_t launch_fit(int64_t n_nodes, const FitGroup* fast, const SlowNode* slow,
+hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,
+                      const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, hipStream_t s) {
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
@@ -760,8 +859,9 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroup* fast, const SlowNode* slo
   }
   if (gpb * (int64_t)sizeof(FitGroup) >= 0x7fffffffLL) return hipErrorInvalidValue;
   const int64_t blocks = gx * ((gy + 7) / 8 * 8);
-  hipLaunchKernelGGL(fit_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, gpb, fast,
-                     slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)gx, (int32_t)gy);
+  hipLaunchKernelGGL(fit_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, gpb, fast_a,
+                     fast_b, slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)gx,
+                     (int32_t)gy);
   return hipGetLastError();
 }
 

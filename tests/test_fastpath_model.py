@@ -1,4 +1,10 @@
-"""CPU model of the fit kernel's fast path (kcc_kernels.hip `fit_kernel`).
+"""CPU model of the fit kernel's fast paths (kcc_kernels.hip `fit_kernel`).
+
+Class A (the bench's specs) reads the node integers as IEEE denormals in
+round-toward--inf: qc = floor(fc * rcf) with rcf = smallest f32 >= 1/c (fc < 2^23),
+qm = floor(fm * rm) (fm < 2^50), both from ONE rounding of the exact product onto the
+denormal grid; `fast_qc_a` / `fast_qm` replay that and `test_class_a_*` check them.
+Class B (below) uses biased FMAs.
 
 The kernel computes floor(fc / c) and floor(fm / m) (CC:123, CC:129) without any
 integer division, conversion or correction step: one fused multiply-add per quotient
@@ -99,6 +105,70 @@ def test_round_mode_matters():
     np.testing.assert_array_equal(fast_qc(fc, np.full(fc.size, c)), fc // c)
 
 
+FC_A_MAX = 1 << 23
+
+
+def recip_up_f32(c):
+    """Smallest f32 >= 1/c, as spec_prep computes it (via f64, then one fix-up)."""
+    from fractions import Fraction
+    c = np.asarray(c, np.int64)
+    shape = c.shape
+    c = c.ravel()
+    r = (1.0 / c.astype(np.float64)).astype(np.float32)
+    # exact test r*c >= 1 (c < 2^29: the f64 product is exact; above, rationals)
+    small = c < (1 << 29)
+    low = np.zeros(c.size, bool)
+    low[small] = r[small].astype(np.float64) * c[small] < 1.0
+    big = np.flatnonzero(~small)
+    low[big] = [Fraction(float(r[i])) * int(c[i]) < 1 for i in big]
+    return np.where(low, np.nextafter(r, np.float32(np.inf)), r).reshape(shape)
+
+
+def fast_qc_a(fc, c):
+    """Class A CPU quotient: RD32(fc * 2^-149 * rcf) read as an integer = floor(fc * rcf)
+    (fc < 2^23 and rcf have 23 + 24 significant bits: the product is exact in f64)."""
+    rcf = recip_up_f32(c).astype(np.float64)
+    return np.floor(np.asarray(fc).astype(np.float64) * rcf).astype(np.int64)
+
+
+def test_class_a_recip_is_smallest_upper_bound():
+    from fractions import Fraction
+    rng = np.random.default_rng(8)
+    c = np.concatenate([np.arange(1, 3000), rng.integers(1, C_MAX, 3000),
+                        [C_MAX - 1, (1 << 24) + 1, (1 << 23) - 1, 3, 6, 12]]).astype(np.int64)
+    r = recip_up_f32(c)
+    for x, y in zip(r, c):
+        assert Fraction(float(x)) * int(y) >= 1
+        assert Fraction(float(np.nextafter(x, np.float32(0)))) * int(y) < 1
+
+
+def test_class_a_cpu_quotient_exact():
+    rng = np.random.default_rng(11)
+    cs = np.concatenate([np.arange(1, 1025), rng.integers(1, 8001, 2000),
+                         rng.integers(1, C_MAX, 500),
+                         np.array([(1 << k) + d for k in range(1, 24) for d in (-1, 0, 1)])])
+    fcs, cc = [], []
+    for c in cs:
+        nmax = (FC_A_MAX - 1) // c
+        n = np.unique(np.concatenate([[0, 1, nmax], rng.integers(0, nmax + 1, 16)]))
+        for d in (-1, 0, 1):
+            fcs.append(n * c + d)
+            cc.append(np.full(n.size, c))
+    fc = np.concatenate(fcs + [np.arange(FC_A_MAX - 4096, FC_A_MAX)])
+    c = np.concatenate(cc + [np.full(4096, 3)])
+    ok = (fc >= 0) & (fc < FC_A_MAX)
+    fc, c = fc[ok], c[ok]
+    assert fc.size > 100_000
+    np.testing.assert_array_equal(fast_qc_a(fc, c), fc // c)
+
+
+def test_class_a_bound_is_tight():
+    """Past fc < 2^23 the f32 quotient fails: the node bound is load-bearing."""
+    fc = np.arange(1 << 26, (1 << 26) + 20_000, dtype=np.int64)
+    c = np.full(fc.size, 3)
+    assert np.any(fast_qc_a(fc, c) != fc // c)
+
+
 def _cpu_pairs(rng):
     cs = np.concatenate([
         np.arange(1, 4097),
@@ -181,6 +251,33 @@ def test_recips_are_smallest_upper_bounds():
     rm = recip_up_f64(m)
     assert not np.any(_exact_prod_minus_one_negative(rm, m.astype(np.float64)))
     assert np.all(_exact_prod_minus_one_negative(np.nextafter(rm, 0.0), m.astype(np.float64)))
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_class_a_contribution_matches_oracle(seed):
+    """Class A: min3(qc, qm, P), m3 == P ? cl : m3, summed — vs the C oracle."""
+    from oracle import coracle
+    rng = np.random.default_rng(100 + seed)
+    n, s = 3_000, 40
+    sc = np.concatenate([rng.integers(1, 9000, s // 2), rng.integers(1, 1 << 20, s // 2)])
+    sm = np.concatenate([rng.integers(1 << 18, 1 << 37, s // 2), rng.integers(1 << 18, M_MAX, s // 2)])
+    k = rng.integers(0, 300, n)
+    j = rng.integers(0, s, n)
+    fc = np.minimum(k * sc[j] + rng.integers(-1, 2, n), FC_A_MAX - 1).clip(0)
+    fm = np.minimum(k * sm[j] + rng.integers(-1, 2, n), FM_MAX - 1).clip(0)
+    P = k + rng.integers(-2, 3, n)
+    pc = rng.integers(0, 300, n)
+    qc = fast_qc_a(fc[:, None], sc[None, :])
+    qm = fast_qm(fm[:, None], sm[None, :])
+    assert qm.max() < 2**32                                  # the low dword is all of qm
+    Penc = np.maximum(P, 0)[:, None]                         # node_prep: P <= 0 -> 0
+    m3 = np.minimum(np.minimum(qc, qm), Penc)               # v_min3_u32
+    contrib = np.where(m3 == Penc, (P - pc)[:, None], m3)   # v_cmp_eq + v_cndmask
+    zero = np.zeros(n, np.int64)
+    ot, oe = coracle.fit(fc.astype(np.uint64), fm, P, pc, zero.astype(np.uint64), zero,
+                         sc.astype(np.uint64), sm.astype(np.int64))
+    assert not oe.any()
+    np.testing.assert_array_equal(contrib.sum(axis=0), ot)
 
 
 @pytest.mark.parametrize("seed", [0, 1])

@@ -154,6 +154,56 @@ def test_fast_path_boundaries(engine):
     np.testing.assert_array_equal(e, oe)
 
 
+def _rows_near_bounds(rng, n, sc, sm):
+    """Rows whose quotients sit on / next to integers for the given specs, free CPU on
+    both sides of 2^23 (class-A node bound) and free memory up to 2^50."""
+    k = rng.integers(0, 300, n)
+    j = rng.integers(0, len(sc), n)
+    fc = (k * sc[j].astype(np.int64) + rng.integers(-1, 2, n)).clip(0)
+    fc[: n // 8] = (1 << 23) + rng.integers(-3, 3, n // 8)           # around the f32 bound
+    fm = (k * sm[j] + rng.integers(-1, 2, n)).clip(0)
+    fm[n // 8: n // 4] = (1 << 50) - rng.integers(1, 1 << 20, n // 8)  # top of the fm range
+    alloc_pods = k + rng.integers(-1, 2, n)
+    alloc_pods[-50:] = rng.integers(-3, 1, 50)                        # P <= 0: always clamped
+    pod_count = rng.integers(0, 300, n)
+    return (fc.astype(np.uint64), fm, alloc_pods, pod_count, np.zeros(n, np.uint64),
+            np.zeros(n, np.int64))
+
+
+def test_class_a_wave_boundaries(engine):
+    """Whole class-A waves (memory requests >= 2^18): quotients on/next to integers,
+    free CPU around 2^23, free memory near 2^50, P <= 0, memory requests at 2^18."""
+    rng = np.random.default_rng(23)
+    sc = np.concatenate([[1, 2, 3, 7, 100, 250, 8000, (1 << 23) - 1, 1 << 23, 2**51 - 1],
+                         rng.integers(1, 9000, 118)]).astype(np.uint64)
+    sm = np.concatenate([[1 << 18, (1 << 18) + 1, 104_857_600, 2**51 - 1, 1 << 30, 3 << 30,
+                          999_999_937, 2**37 - 1, (1 << 18) + 3, 1 << 32],
+                         rng.integers(1 << 18, 1 << 36, 118)]).astype(np.int64)
+    args = _rows_near_bounds(rng, 8_000, sc, sm)
+    t, e = engine.total_possible_max_replicas(*args, sc, sm)
+    ot, oe = coracle.fit(*args, sc, sm, NT)
+    np.testing.assert_array_equal(e, oe)
+    np.testing.assert_array_equal(t, ot)
+
+
+def test_mixed_class_waves(engine):
+    """64 class-A, 64 class-B (memory < 2^18) and 64 exact-path specs, shuffled: the
+    partition regroups them and every class matches the oracle."""
+    rng = np.random.default_rng(29)
+    sc = rng.integers(1, 9000, 192).astype(np.uint64)
+    sm = np.concatenate([rng.integers(1 << 18, 1 << 36, 64), rng.integers(1, 1 << 18, 64),
+                         rng.integers(1, 1 << 36, 64)]).astype(np.int64)
+    sm[128:160] = 0                                      # exact path: div-by-zero flags
+    sc[160:] = (1 << 51) + rng.integers(0, 1 << 40, 32).astype(np.uint64)  # exact path
+    perm = rng.permutation(192)
+    sc, sm = sc[perm], sm[perm]
+    args = _rows_near_bounds(rng, 5_000, sc, sm)
+    t, e = engine.total_possible_max_replicas(*args, sc, sm)
+    ot, oe = coracle.fit(*args, sc, sm, NT)
+    np.testing.assert_array_equal(e, oe)
+    np.testing.assert_array_equal(t, ot)
+
+
 # ---- CSR edge cases of the segmented reduce ----------------------------------------
 def _reduce_check(engine, sizes, seed=0):
     sizes = np.asarray(sizes, np.int64)

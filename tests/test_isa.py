@@ -1,11 +1,15 @@
 """Static ISA checks of the gfx950 kernels (CPU: hipcc cross-compiles).
 
-  - the fit kernel's fast loop, one 8-node FitGroup per iteration: 48 dwords of scalar
-    loads (fc, fm, Pb), two uniform 16-B buffer loads (cl), no 64-bit integer division,
-    no conversion, and exactly bench.FIT_VALU_PER_NODE_WAVE VALU instructions per node
-    (the VALU-roofline accounting of bench.py);
-  - the loop runs inside the round-toward--inf window of the f64 mode (our two
-    s_setreg writes), and the compiler inserts no mode switch of its own;
+  - the fit kernel's class-A loop, one 8-node FitGroupA per iteration: 32 dwords of
+    scalar loads (fm, fc, P), two uniform 16-B buffer loads (cl), exactly
+    bench.FIT_VALU_PER_NODE_WAVE VALU instructions per node (the VALU-roofline
+    accounting of bench.py): packed f32 and f64 multiplies, min3, compare, select, add
+    — no division, no conversion, no correction step, and no select reading VCC;
+  - the class-B loop: biased f64 FMAs, 5.5 VALU instructions per node;
+  - both loops run inside a round-toward--inf window of the MODE register (our two
+    s_setreg writes each), and the compiler inserts no mode switch of its own;
+  - f32 and f64 denormals are enabled in the kernel descriptor (class A reads
+    integers as denormals);
   - no kernel spills to scratch.
 """
 import os
@@ -37,40 +41,70 @@ def kernel_body(asm, name):
     return asm[start:asm.index("s_endpgm", start)]
 
 
-def test_fit_fast_loop(asm):
-    import bench
-    body = kernel_body(asm, "fit_kernel")
-    i = body.index("v_fma_f64")
+def loop_of(body, marker):
+    i = body.index(marker)
     loop = body[body.rfind(".LBB", 0, i):body.index("s_cbranch", i)]
-    lines = [ln.strip() for ln in loop.splitlines()
-             if ln.strip() and not ln.strip().startswith(";")]
-    valu = [ln for ln in lines if ln.startswith("v_")]
-    group = 8  # nodes per FitGroup = per loop iteration
-    width = {"s_load_dword": 1, "s_load_dwordx2": 2, "s_load_dwordx4": 4, "s_load_dwordx8": 8,
-             "s_load_dwordx16": 16}
-    dwords = sum(width[ln.split()[0]] for ln in lines if ln.startswith("s_load_dword"))
-    assert dwords == group * 6  # fc, fm, Pb (f64) of each node
+    return [ln.strip() for ln in loop.splitlines() if ln.strip() and not ln.strip().startswith(";")]
+
+
+WIDTH = {"s_load_dword": 1, "s_load_dwordx2": 2, "s_load_dwordx4": 4, "s_load_dwordx8": 8,
+         "s_load_dwordx16": 16}
+GROUP = 8  # nodes per FitGroup = per loop iteration
+
+
+def check_loads(lines, dwords):
+    assert sum(WIDTH[ln.split()[0]] for ln in lines if ln.startswith("s_load_dword")) == dwords
     vmem = [ln for ln in lines if ln.startswith(("global_load", "flat_load", "buffer_load"))]
     assert len(vmem) == 2 and all(ln.startswith("buffer_load_dwordx4") and ", off," in ln
                                   for ln in vmem)  # cl: uniform address, no VGPR offset
-    assert len(valu) / group == pytest.approx(bench.FIT_VALU_PER_NODE_WAVE, abs=1e-9), \
-        f"{len(valu)} VALU / {group} nodes: update bench.FIT_VALU_PER_NODE_WAVE"
+
+
+def test_fit_class_a_loop(asm):
+    import bench
+    lines = loop_of(kernel_body(asm, "fit_kernel"), "v_pk_mul_f32")
+    check_loads(lines, GROUP * 4)  # fm (2 dwords), fc, P per node
+    valu = [ln for ln in lines if ln.startswith("v_")]
+    assert len(valu) / GROUP == pytest.approx(bench.FIT_VALU_PER_NODE_WAVE, abs=1e-9), \
+        f"{len(valu)} VALU / {GROUP} nodes: update bench.FIT_VALU_PER_NODE_WAVE"
     ops = [ln.split()[0] for ln in valu]
-    assert ops.count("v_fma_f64") == 2 * group and ops.count("v_min_f64") == group
-    assert sum(o.startswith("v_cmp_") and "_f64" in o for o in ops) == group
-    assert sum(o.startswith("v_cndmask_b32") for o in ops) == group
-    assert ops.count("v_add3_u32") == group // 2
-    assert not any(o.startswith(("v_mad", "v_cvt", "v_mul", "v_max")) for o in ops)
+    assert ops.count("v_pk_mul_f32") == GROUP // 2 and ops.count("v_mul_f64") == GROUP
+    assert ops.count("v_min3_u32") == GROUP and ops.count("v_add3_u32") == GROUP // 2
+    assert ops.count("v_cmp_eq_u32_e64") == GROUP and ops.count("v_cndmask_b32_e64") == GROUP
+    assert not any("vcc" in ln for ln in valu)
+    assert not any(o.startswith(("v_mad", "v_cvt", "v_fma", "v_rcp", "v_div")) for o in ops)
 
 
-def test_fit_round_mode_window(asm):
+def test_fit_class_b_loop(asm):
+    lines = loop_of(kernel_body(asm, "fit_kernel"), "v_fma_f64")
+    check_loads(lines, GROUP * 6)  # fc, fm, Pb (f64) per node
+    valu = [ln for ln in lines if ln.startswith("v_")]
+    assert len(valu) / GROUP == 5.5
+    ops = [ln.split()[0] for ln in valu]
+    assert ops.count("v_fma_f64") == 2 * GROUP and ops.count("v_min_f64") == GROUP
+    assert ops.count("v_cmp_ge_f64_e64") == GROUP and ops.count("v_cndmask_b32_e64") == GROUP
+    assert not any("vcc" in ln for ln in valu)
+    assert not any(o.startswith(("v_cvt", "v_max", "v_mul")) for o in ops)
+
+
+def test_fit_round_mode_windows(asm):
     body = kernel_body(asm, "fit_kernel")
     sets = [(m.start(), m.group(1)) for m in
             re.finditer(r"s_setreg\w*\s+hwreg\(HW_REG_MODE[^)]*\),\s*(\S+)", body)]
-    assert [v for _, v in sets] == ["2", "0"], sets  # round down, then back to nearest
-    fmas = [m.start() for m in re.finditer(r"v_fma_f64", body)]
-    assert fmas and all(sets[0][0] < f < sets[1][0] for f in fmas)
-    assert "hwreg(HW_REG_MODE, 2, 2)" in body
+    # (round down, back to nearest) around each of the two fast loops, nothing else
+    assert [v for _, v in sets] == ["10", "0", "10", "0"], sets
+    assert all("hwreg(HW_REG_MODE, 0, 4)" in body[p:p + 60] for p, _ in sets)
+    windows = [(sets[0][0], sets[1][0]), (sets[2][0], sets[3][0])]
+    for op in ("v_pk_mul_f32", "v_mul_f64", "v_fma_f64"):
+        pos = [m.start() for m in re.finditer(op, body)]
+        assert pos and all(any(a < p < b for a, b in windows) for p in pos), op
+
+
+def test_denormals_enabled(asm):
+    m = re.search(r"^(_ZN3kcc12_GLOBAL__N_1\d+fit_kernel\w*):", asm, re.M)
+    desc = asm[asm.index(".amdhsa_kernel " + m.group(1)):]
+    desc = desc[:desc.index(".end_amdhsa_kernel")]
+    assert re.search(r"\.amdhsa_float_denorm_mode_32 3", desc)
+    assert re.search(r"\.amdhsa_float_denorm_mode_16_64 3", desc)
 
 
 def test_no_scratch(asm):
