@@ -548,6 +548,20 @@ __device__ __forceinline__ int32_t clamp_select(uint32_t m3, uint32_t P, int32_t
       : "v"(m3), "s"(P), "v"(cl));
   return r;
 }
+// acc += (a == Pa ? cla : a) + (b == Pb ? clb : b) in one block: one hazard wait
+// between blocks instead of one per select
+__device__ __forceinline__ void clamp_select2_acc(int32_t& acc, uint32_t a, uint32_t Pa, int32_t cla,
+                                                  uint32_t b, uint32_t Pb, int32_t clb) {
+  int32_t ta, tb;
+  uint64_t ma, mb;
+  asm("v_cmp_eq_u32_e64 %1, %5, %6\n\t"
+      "v_cmp_eq_u32_e64 %2, %7, %8\n\t"
+      "v_cndmask_b32_e64 %3, %5, %9, %1\n\t"
+      "v_cndmask_b32_e64 %4, %7, %10, %2\n\t"
+      "v_add3_u32 %0, %3, %4, %0"
+      : "+v"(acc), "=&s"(ma), "=&s"(mb), "=&v"(ta), "=&v"(tb)
+      : "v"(a), "s"(Pa), "v"(b), "s"(Pb), "v"(cla), "v"(clb));
+}
 // x' >= Pb ? cl : low32(x') (class B), mask in an SGPR pair likewise
 __device__ __forceinline__ int32_t clamp_select_f64(double xb, double Pb, int32_t cl) {
   int32_t r;
@@ -565,6 +579,9 @@ constexpr int FIT_SPW = KCC_FIT_SPECS_PER_WG;  // specs per 256-thread workgroup
 constexpr int FIT_SPLIT = 256 / FIT_SPW;       // waves per spec group (node chunk split)
 static_assert(FIT_SPW == 64 || FIT_SPW == 128 || FIT_SPW == 256, "FIT_SPW");
 constexpr int FIT_CHUNK_GROUPS = 128;  // 1024 nodes: |sum of contributions| <= 2^30 in i32
+#ifndef KCC_FIT_PAIR_ASM
+#define KCC_FIT_PAIR_ASM 1  // compare/select/add of two nodes in one asm block (0: one per node; same speed, 8 s_nop waits per 8 nodes)
+#endif
 #ifndef KCC_FIT_TARGET_BLOCKS
 #define KCC_FIT_TARGET_BLOCKS 32768
 #endif
@@ -667,17 +684,21 @@ __global__ __launch_bounds__(256) void fit_kernel(
         for (int u = 0; u < FIT_GROUP / 2; ++u) {
           const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
           const f32x2 q = fcp * rcf2;  // two nodes' floor(fc / c), as integers
-          int32_t x[2];
+          uint32_t m3[2];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int k = 2 * u + h;
             const uint32_t qm = (uint32_t)__double_as_longlong(f64_at(fmv, k) * rm);
             const uint32_t qc = __float_as_uint(h ? q.y : q.x);
-            const uint32_t Pk = (uint32_t)Pv[k];
-            const uint32_t m3 = min(min(qc, qm), Pk);
-            x[h] = clamp_select(m3, Pk, cl[k]);
+            m3[h] = min(min(qc, qm), (uint32_t)Pv[k]);
           }
-          acc32 += x[0] + x[1];
+#if KCC_FIT_PAIR_ASM
+          clamp_select2_acc(acc32, m3[0], (uint32_t)Pv[2 * u], cl[2 * u], m3[1],
+                            (uint32_t)Pv[2 * u + 1], cl[2 * u + 1]);
+#else
+          acc32 += clamp_select(m3[0], (uint32_t)Pv[2 * u], cl[2 * u]) +
+                   clamp_select(m3[1], (uint32_t)Pv[2 * u + 1], cl[2 * u + 1]);
+#endif
         }
       }
       acc += (uint64_t)(int64_t)acc32;
