@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C5"])
     ap.add_argument("--scaling", default="weak", choices=["strong", "weak"],
                     help="weak: a C4-sized node partition per rank; strong: C4 split over ranks")
+    ap.add_argument("--chunks", type=int, default=1,
+                    help="node chunks of the pipelined step (reduce of chunk k overlaps the fit "
+                         "of chunk k-1); 1 = reduce, then fit")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU time of the oracle's fit sample")
@@ -119,19 +122,13 @@ def main():
     eng.reserve(n, C, S)
     stream = torch.cuda.Stream(dev)
 
-    def step(ev=None):
-        if ev:
-            ev[0].record(stream)
-        eng.reduce_requests_async(ptr, cpu, mem, used_cpu, used_mem, stream=stream)
-        if ev:
-            ev[1].record(stream)
-        eng.fit_prepare_async(a_cpu, a_mem, a_pods, p_cnt, used_cpu, used_mem, s_cpu, s_mem,
-                              partial, stream=stream)
-        if ev:
-            ev[2].record(stream)
-        eng.fit_run_async(n, S, partial, stream=stream)
-        if ev:
-            ev[3].record(stream)
+    h_ptr = np.ascontiguousarray(cl.node_ptr, np.int64)
+
+    def step():
+        # reduce (side stream, node chunk k) overlapped with the fit of chunk k-1
+        eng.capacity_partial_async(h_ptr, ptr, cpu, mem, a_cpu, a_mem, a_pods, p_cnt, used_cpu,
+                                   used_mem, s_cpu, s_mem, partial, n_chunks=args.chunks,
+                                   stream=stream)
         if world > 1:
             dist.all_reduce(partial, op=dist.ReduceOp.SUM)
         eng.fit_finalize_async(S, partial, totals, err, stream=stream)
@@ -140,36 +137,41 @@ def main():
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+        # per-launch kernel durations from HIP events the library records on the stream
+        # each kernel runs on, over exactly the timed steps
+        eng.profile_enable(True)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t_start = time.perf_counter()
-        for k in range(args.steps):
-            step(evs[k])
+        for _ in range(args.steps):
+            step()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t_end = time.perf_counter()
+    red_ms_tot, red_launches, fit_ms_tot, fit_launches = eng.profile_read()
+    eng.profile_enable(False)
     elapsed = t_end - t_start
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_step = elapsed / args.steps * 1e3
-    red_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    prep_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
-    fit_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+    chunks = fit_launches // args.steps
+    red_ms = red_ms_tot / max(red_launches, 1)   # per launch
+    fit_ms = fit_ms_tot / max(fit_launches, 1)
     slow_pairs, pairs = eng.fit_slow_pairs()
     value = n_total * S / (elapsed / args.steps)
     if args.emulate_world > 1:  # per-rank rate x world (no all-reduce): an upper bound
         value = n * S * args.emulate_world / (elapsed / args.steps)
 
-    # algorithmic bytes per launch (DESIGN.md "Roofline accounting")
-    fit_bytes = n * 20 + S * 48 + S * 8            # FitGroupA fields + spec records in, totals out
-    red_bytes = C * 16 + (n + 1) * 8 + n * 16      # requests + CSR offsets in, sums out
+    # algorithmic bytes per launch (DESIGN.md "Roofline accounting"): a step runs
+    # `chunks` reduce launches and `chunks` fit launches over node ranges of ~n/chunks
+    fit_bytes = (n * 20 + chunks * (S * 48 + S * 8)) / chunks  # FitGroupA + spec records in, totals out
+    red_bytes = (C * 16 + (n + 1) * 8 + n * 16) / chunks       # requests + CSR offsets in, sums out
     fit_gbs = fit_bytes / (fit_ms * 1e-3) / 1e9
-    fit_valu = n * ((S + 63) // 64) * FIT_VALU_PER_NODE_WAVE / (fit_ms * 1e-3)
+    fit_valu = n / chunks * ((S + 63) // 64) * FIT_VALU_PER_NODE_WAVE / (fit_ms * 1e-3)
     red_gbs = red_bytes / (red_ms * 1e-3) / 1e9
     fit_traffic, tsrc = pmc_traffic("fit_kernel") if args.config == "C4" and world == 1 else (None, None)
     red_traffic, _ = pmc_traffic("reduce_kernel<2>") if tsrc else (None, None)
@@ -207,7 +209,7 @@ def main():
             "peak": VALU_ISSUE_PEAK / 1e9, "unit": "G wave-instr/s",
             "frac": fit_valu / VALU_ISSUE_PEAK,
             "valu_per_node_wave": FIT_VALU_PER_NODE_WAVE,
-            "fit_evals_per_s": n * S / (fit_ms * 1e-3),
+            "fit_evals_per_s": n / chunks * S / (fit_ms * 1e-3),
         },
         "roofline_reduce": {
             "bound": "hbm", "kernel": "reduce_mark_kernel+reduce_kernel<2>",
@@ -215,7 +217,10 @@ def main():
             "frac": red_gbs / HBM_PEAK_GBS, "bytes_per_launch": red_bytes, "ms_per_launch": red_ms,
             "traffic": red_traffic,
         },
-        "fit_prepare_ms": prep_ms,
+        "pipeline": {"chunks": chunks, "reduce_ms_per_step": red_ms_tot / args.steps,
+                     "fit_ms_per_step": fit_ms_tot / args.steps,
+                     "note": "reduce launches run on a side stream under the fit launches; "
+                             "their durations include that overlap"},
         "fast_path_fraction": 1.0 - (slow_pairs / pairs if pairs else 0.0),
         "gen_seconds": gen_s,
     }

@@ -157,6 +157,36 @@ int kcc_fit_async(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* d_alloc_cpu,
                   const int64_t* d_spec_mem, int64_t* d_totals, int32_t* d_spec_err,
                   void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Pipelined (a)+(b) on one device: reduce + fit partial of the whole hot path in one
+ * call, d_partial as kcc_fit_partial_async (follow with an optional all-reduce and
+ * kcc_fit_finalize_async).  n_chunks > 1 cuts the nodes into that many contiguous
+ * ranges (fewer when chunks would be small) and runs the reduce of range k on a
+ * library-owned side stream while `stream` fits range k-1; 0 = library default (1:
+ * the overlap measured slower on MI355X).  h_node_ptr is a HOST copy
+ * of the CSR offsets in d_node_ptr (used only to place the chunk boundaries; NULL =
+ * one chunk).  The
+ * per-node request sums land in d_used_cpu / d_used_mem (CC:290-293).  Everything is
+ * ordered after the work already queued on `stream`, and `stream` waits for the side
+ * stream before the call's last kernel: capturable into a hipGraph.
+ * ------------------------------------------------------------------------- */
+int kcc_capacity_partial_async(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containers,
+                               const int64_t* h_node_ptr, const int64_t* d_node_ptr,
+                               const uint64_t* d_cpu_req, const int64_t* d_mem_req,
+                               const uint64_t* d_alloc_cpu, const int64_t* d_alloc_mem,
+                               const int64_t* d_alloc_pods, const int64_t* d_pod_count,
+                               uint64_t* d_used_cpu, int64_t* d_used_mem, int64_t n_specs,
+                               const uint64_t* d_spec_cpu, const int64_t* d_spec_mem,
+                               int64_t* d_partial, int n_chunks, void* stream);
+
+/* Per-launch timing of kcc_capacity_partial_async (HIP events recorded on the stream
+ * each kernel runs on): enable (1) / disable (0) resets the sums; read synchronises
+ * and returns the summed durations and launch counts of the reduces (mark + reduce,
+ * one per chunk) and of the fit kernel (one per chunk). */
+int kcc_profile_enable(kcc_ctx* ctx, int on);
+int kcc_profile_read(kcc_ctx* ctx, double* reduce_ms, int64_t* reduce_launches, double* fit_ms,
+                     int64_t* fit_launches);
+
 /* Fraction of (node, spec) pairs of the last kcc_fit* call that took the exact
  * 64-bit path instead of the saturating fast path (diagnostic; host-computed from
  * the class counters the fit kernel keeps).  -1 if unknown. */

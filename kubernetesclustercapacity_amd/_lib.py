@@ -43,6 +43,10 @@ SIGNATURES = {
     "kcc_fit_run_async": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "kcc_fit_finalize_async": (_int, [_vp, _i64, _vp, _vp, _vp, _vp]),
     "kcc_fit_async": (_int, [_vp, _i64] + [_vp] * 6 + [_i64] + [_vp] * 5),
+    "kcc_capacity_partial_async": (_int, [_vp, _i64, _i64] + [_vp] * 10 + [_i64] + [_vp] * 3
+                                   + [_int, _vp]),
+    "kcc_profile_enable": (_int, [_vp, _int]),
+    "kcc_profile_read": (_int, [_vp] + [C.POINTER(_dbl), C.POINTER(_i64)] * 2),
     "kcc_last_slow_fraction": (_dbl, [_vp]),
     "kcc_fit_slow_pairs": (_int, [_vp, C.POINTER(_i64), C.POINTER(_i64)]),
 }
@@ -53,6 +57,16 @@ def header_symbols(path: str = HEADER_PATH) -> list[str]:
     text = open(path).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(kcc_[a-z0-9_]+)\s*\(", text)))
+
+
+def header_arities(path: str = HEADER_PATH) -> dict[str, int]:
+    """Number of parameters of every function the C-ABI header declares."""
+    text = re.sub(r"/\*.*?\*/", "", open(path).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(kcc_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", text, flags=re.S):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
 
 
 def load(path: str = LIB_PATH) -> C.CDLL:

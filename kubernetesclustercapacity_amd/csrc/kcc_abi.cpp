@@ -37,9 +37,26 @@ T* as(DevBuf& b) {
   return static_cast<T*>(b.p);
 }
 
+// Timing of the pipelined entry point (kcc_profile_*): event pairs recorded around each
+// reduce (side stream) and each fit launch (caller stream), read back on demand.
+struct ProfPair {
+  hipEvent_t a, b;
+  int kind;  // 0 reduce (mark + reduce), 1 fit
+};
+
 struct Dev {
   int device = 0;
   hipStream_t stream = nullptr;
+  // pipelined capacity (kcc_capacity_partial_async): node chunk k's reduce runs on `side`
+  // while the caller's stream fits chunk k-1
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr;
+  hipEvent_t ev_red[kcc::FIT_MAX_CHUNKS] = {};
+  bool prof_on = false;
+  std::vector<ProfPair> prof_pending;
+  std::vector<hipEvent_t> prof_free;
+  double prof_ms[2] = {0.0, 0.0};
+  int64_t prof_n[2] = {0, 0};
   // workspace of the *_async entry points
   DevBuf wave_node, fast_a, fast_b, slow, slow_list, srec, sperm, counters;
   int64_t last_pairs = 0;  // node x spec pairs of the last fit_prepare on this device
@@ -136,10 +153,10 @@ int reduce_async_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, con
     return fail(ctx, KCC_EINVAL, "container arrays must be 16-byte aligned");
   const int64_t waves = kcc::reduce_max_waves(n_cont);
   KCC_HIP(ctx, ensure(dv.wave_node, sizeof(int64_t) * (size_t)(waves > 0 ? waves : 1)));
-  KCC_HIP(ctx, kcc::launch_reduce_mark(n_nodes, n_cont, ptr, as<int64_t>(dv.wave_node), used_cpu,
+  KCC_HIP(ctx, kcc::launch_reduce_mark(n_nodes, 0, n_cont, ptr, as<int64_t>(dv.wave_node), used_cpu,
                                        used_mem, lim ? lim_cpu : nullptr,
                                        lim ? lim_mem : nullptr, s));
-  KCC_HIP(ctx, kcc::launch_reduce(n_nodes, n_cont, ptr, cpu, mem, lim ? cpul : nullptr,
+  KCC_HIP(ctx, kcc::launch_reduce(n_nodes, 0, n_cont, ptr, cpu, mem, lim ? cpul : nullptr,
                                   lim ? meml : nullptr, as<int64_t>(dv.wave_node), used_cpu,
                                   used_mem, lim ? lim_cpu : nullptr, lim ? lim_mem : nullptr, s));
   return KCC_OK;
@@ -193,7 +210,7 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
                                      used_cpu, used_mem, as<kcc::FitGroupA>(dv.fast_a),
                                      as<kcc::FitGroup>(dv.fast_b), as<kcc::SlowNode>(dv.slow),
                                      as<int64_t>(dv.slow_list),
-                                     as<unsigned long long>(dv.counters), s));
+                                     as<unsigned long long>(dv.counters), 0, s));
   return KCC_OK;
 }
 
@@ -206,7 +223,7 @@ int fit_run_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_specs, int64_t
   KCC_HIP(ctx, kcc::launch_fit(n_nodes, as<kcc::FitGroupA>(dv.fast_a), as<kcc::FitGroup>(dv.fast_b),
                                as<kcc::SlowNode>(dv.slow),
                                as<int64_t>(dv.slow_list), n_specs, spec_prep_of(dv), partial,
-                               as<unsigned long long>(dv.counters), s));
+                               as<unsigned long long>(dv.counters), 0, n_nodes, s));
   return KCC_OK;
 }
 
@@ -230,6 +247,145 @@ int fit_finalize_dev(kcc_ctx* ctx, Dev& dv, int64_t n_specs, const int64_t* part
     return fail(ctx, KCC_EINVAL, "finalize without a matching fit_partial");
   KCC_HIP(ctx, kcc::launch_fit_finalize(n_specs, partial, as<int32_t>(dv.sperm), totals,
                                         spec_err, s));
+  return KCC_OK;
+}
+
+
+// ---- pipelined reduce + fit (kcc_capacity_partial_async) ---------------------------
+
+hipError_t prof_event(Dev& dv, hipEvent_t* ev) {
+  if (!dv.prof_free.empty()) {
+    *ev = dv.prof_free.back();
+    dv.prof_free.pop_back();
+    return hipSuccess;
+  }
+  return hipEventCreate(ev);
+}
+
+// Chunk boundaries: node ranges of ~equal node count, multiples of FIT_GROUP (the fit's
+// node groups never straddle two chunks); at least `min_nodes` nodes per chunk.
+int plan_chunks(int64_t n_nodes, int want, int64_t min_nodes, std::vector<int64_t>& lo,
+                std::vector<int64_t>& hi) {
+  int k = want;
+  if (k > kcc::FIT_MAX_CHUNKS) k = kcc::FIT_MAX_CHUNKS;
+  while (k > 1 && n_nodes / k < min_nodes) --k;
+  if (k < 1) k = 1;
+  lo.assign(k, 0);
+  hi.assign(k, 0);
+  for (int c = 0; c < k; ++c) {
+    lo[c] = c == 0 ? 0 : hi[c - 1];
+    hi[c] = c == k - 1 ? n_nodes : (n_nodes * (c + 1) / k) / kcc::FIT_GROUP * kcc::FIT_GROUP;
+    if (hi[c] < lo[c]) hi[c] = lo[c];
+  }
+  return k;
+}
+
+// Overlapping the reduce of chunk k with the fit of chunk k-1 measured SLOWER at C4
+// (0.80 / 0.85 / 0.88 ms per step at 1 / 2 / 4 chunks): the fit keeps every SIMD's
+// VALU issue ~90 % busy and the concurrent reduce's waves slow it by more than the
+// reduce's own time.  Default: one chunk, everything on the caller's stream.
+constexpr int KCC_DEFAULT_CHUNKS = 1;
+constexpr int64_t KCC_MIN_CHUNK_NODES = 32768;
+
+int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
+                         const int64_t* h_ptr, const int64_t* ptr, const uint64_t* cpu,
+                         const int64_t* mem, const uint64_t* alloc_cpu, const int64_t* alloc_mem,
+                         const int64_t* alloc_pods, const int64_t* pod_count, uint64_t* used_cpu,
+                         int64_t* used_mem, int64_t n_specs, const uint64_t* spec_cpu,
+                         const int64_t* spec_mem, int64_t* partial, int n_chunks, hipStream_t s) {
+  if (n_nodes < 0 || n_cont < 0 || n_specs < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (n_specs > 0x7fffffffLL) return fail(ctx, KCC_EINVAL, "too many specs (max 2^31-1)");
+  if (n_nodes == 0 && n_cont != 0) return fail(ctx, KCC_EINVAL, "containers without nodes");
+  if (n_nodes > 0 && (!ptr || !used_cpu || !used_mem || !alloc_cpu || !alloc_mem || !alloc_pods ||
+                      !pod_count))
+    return fail(ctx, KCC_EINVAL, "NULL node array");
+  if (n_cont > 0 && (!cpu || !mem)) return fail(ctx, KCC_EINVAL, "NULL cpu_req/mem_req");
+  if (!aligned16(cpu) || !aligned16(mem))
+    return fail(ctx, KCC_EINVAL, "container arrays must be 16-byte aligned");
+  if (n_specs > 0 && (!spec_cpu || !spec_mem || !partial))
+    return fail(ctx, KCC_EINVAL, "NULL spec array / partial");
+  std::vector<int64_t> lo, hi;
+  const int k = plan_chunks(n_nodes, h_ptr ? (n_chunks > 0 ? n_chunks : KCC_DEFAULT_CHUNKS) : 1,
+                            KCC_MIN_CHUNK_NODES, lo, hi);
+  std::vector<int64_t> c0(k), c1(k);
+  for (int c = 0; c < k; ++c) {
+    if (k == 1) {
+      c0[c] = 0;
+      c1[c] = n_cont;
+    } else {
+      c0[c] = h_ptr[lo[c]];
+      c1[c] = h_ptr[hi[c]];
+      if (c0[c] < 0 || c1[c] < c0[c] || c1[c] > n_cont)
+        return fail(ctx, KCC_EINVAL, "h_node_ptr is not a CSR of n_containers");
+    }
+  }
+  int rc = reserve_dev(ctx, dv, n_nodes, n_cont, n_specs);
+  if (rc) return rc;
+  for (int c = 0; c < k; ++c)
+    if (!dv.ev_red[c]) KCC_HIP(ctx, hipEventCreateWithFlags(&dv.ev_red[c], hipEventDisableTiming));
+  dv.last_pairs = n_nodes * n_specs;
+  dv.prep_nodes = -1;  // the split fit_run API must not reuse this call's workspace state
+  dv.prep_specs = -1;
+  // k > 1: the reduces run on the side stream, forked from s (they wait for everything
+  // already queued on s: the previous call's fits still read used_* and the node
+  // streams); k == 1: everything on s
+  hipStream_t rs = k > 1 ? dv.side : s;
+  if (k > 1) {
+    KCC_HIP(ctx, hipEventRecord(dv.ev_fork, s));
+    KCC_HIP(ctx, hipStreamWaitEvent(dv.side, dv.ev_fork, 0));
+  }
+  if (n_specs > 0)  // spec partition on s (concurrent with the first reduce when k > 1)
+    KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv), partial,
+                                       as<unsigned long long>(dv.counters), s));
+  for (int c = 0; c < k; ++c) {
+    const int64_t n = hi[c] - lo[c];
+    ProfPair pp{};
+    if (dv.prof_on) {
+      KCC_HIP(ctx, prof_event(dv, &pp.a));
+      KCC_HIP(ctx, prof_event(dv, &pp.b));
+      KCC_HIP(ctx, hipEventRecord(pp.a, rs));
+    }
+    KCC_HIP(ctx, kcc::launch_reduce_mark(n, c0[c], c1[c] - c0[c], ptr + lo[c],
+                                         as<int64_t>(dv.wave_node), used_cpu + lo[c],
+                                         used_mem + lo[c], nullptr, nullptr, rs));
+    KCC_HIP(ctx, kcc::launch_reduce(n, c0[c], c1[c] - c0[c], ptr + lo[c], cpu, mem, nullptr,
+                                    nullptr, as<int64_t>(dv.wave_node), used_cpu + lo[c],
+                                    used_mem + lo[c], nullptr, nullptr, rs));
+    if (dv.prof_on) {
+      KCC_HIP(ctx, hipEventRecord(pp.b, rs));
+      pp.kind = 0;
+      dv.prof_pending.push_back(pp);
+    }
+    if (k > 1) KCC_HIP(ctx, hipEventRecord(dv.ev_red[c], dv.side));
+  }
+  for (int c = 0; c < k; ++c) {
+    if (k > 1) KCC_HIP(ctx, hipStreamWaitEvent(s, dv.ev_red[c], 0));  // also joins the side stream
+    const int64_t n = hi[c] - lo[c];
+    if (n_specs == 0 || n == 0) continue;
+    KCC_HIP(ctx, kcc::launch_node_prep(n, alloc_cpu + lo[c], alloc_mem + lo[c], alloc_pods + lo[c],
+                                       pod_count + lo[c], used_cpu + lo[c], used_mem + lo[c],
+                                       as<kcc::FitGroupA>(dv.fast_a) + lo[c] / kcc::FIT_GROUP,
+                                       as<kcc::FitGroup>(dv.fast_b) + lo[c] / kcc::FIT_GROUP,
+                                       as<kcc::SlowNode>(dv.slow) + lo[c],
+                                       as<int64_t>(dv.slow_list) + lo[c],
+                                       as<unsigned long long>(dv.counters), c, s));
+    ProfPair pp{};
+    if (dv.prof_on) {
+      KCC_HIP(ctx, prof_event(dv, &pp.a));
+      KCC_HIP(ctx, prof_event(dv, &pp.b));
+      KCC_HIP(ctx, hipEventRecord(pp.a, s));
+    }
+    KCC_HIP(ctx, kcc::launch_fit(n, as<kcc::FitGroupA>(dv.fast_a) + lo[c] / kcc::FIT_GROUP,
+                                 as<kcc::FitGroup>(dv.fast_b) + lo[c] / kcc::FIT_GROUP,
+                                 as<kcc::SlowNode>(dv.slow) + lo[c],
+                                 as<int64_t>(dv.slow_list) + lo[c], n_specs, spec_prep_of(dv),
+                                 partial, as<unsigned long long>(dv.counters), c, n_nodes, s));
+    if (dv.prof_on) {
+      KCC_HIP(ctx, hipEventRecord(pp.b, s));
+      pp.kind = 1;
+      dv.prof_pending.push_back(pp);
+    }
+  }
   return KCC_OK;
 }
 
@@ -378,7 +534,9 @@ int kcc_create(kcc_ctx** out, int first_device, int n_gpus) {
       return KCC_ENODEV;
     }
     if ((e = hipSetDevice(dv.device)) != hipSuccess ||
-        (e = hipStreamCreateWithFlags(&dv.stream, hipStreamNonBlocking)) != hipSuccess) {
+        (e = hipStreamCreateWithFlags(&dv.stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&dv.side, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&dv.ev_fork, hipEventDisableTiming)) != hipSuccess) {
       g_create_error = std::string("stream creation failed: ") + hipGetErrorString(e);
       kcc_destroy(ctx);
       return KCC_EHIP;
@@ -413,6 +571,18 @@ void kcc_destroy(kcc_ctx* ctx) {
     for (DevBuf* b : bufs)
       if (b->p) (void)hipFree(b->p);
     if (dv.stream) (void)hipStreamDestroy(dv.stream);
+    if (dv.side) {
+      (void)hipStreamSynchronize(dv.side);
+      (void)hipStreamDestroy(dv.side);
+    }
+    if (dv.ev_fork) (void)hipEventDestroy(dv.ev_fork);
+    for (hipEvent_t ev : dv.ev_red)
+      if (ev) (void)hipEventDestroy(ev);
+    for (const ProfPair& pp : dv.prof_pending) {
+      (void)hipEventDestroy(pp.a);
+      (void)hipEventDestroy(pp.b);
+    }
+    for (hipEvent_t ev : dv.prof_free) (void)hipEventDestroy(ev);
   }
   delete ctx;
 }
@@ -567,6 +737,63 @@ int kcc_fit_async(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* d_alloc_cpu,
                            as<int64_t>(dv.partial), s);
   if (rc) return rc;
   return fit_finalize_dev(ctx, dv, n_specs, as<int64_t>(dv.partial), d_totals, d_spec_err, s);
+}
+
+int kcc_capacity_partial_async(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containers,
+                               const int64_t* h_node_ptr, const int64_t* d_node_ptr,
+                               const uint64_t* d_cpu_req, const int64_t* d_mem_req,
+                               const uint64_t* d_alloc_cpu, const int64_t* d_alloc_mem,
+                               const int64_t* d_alloc_pods, const int64_t* d_pod_count,
+                               uint64_t* d_used_cpu, int64_t* d_used_mem, int64_t n_specs,
+                               const uint64_t* d_spec_cpu, const int64_t* d_spec_mem,
+                               int64_t* d_partial, int n_chunks, void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  return capacity_partial_dev(ctx, dv, n_nodes, n_containers, h_node_ptr, d_node_ptr, d_cpu_req,
+                              d_mem_req, d_alloc_cpu, d_alloc_mem, d_alloc_pods, d_pod_count,
+                              d_used_cpu, d_used_mem, n_specs, d_spec_cpu, d_spec_mem, d_partial,
+                              n_chunks, static_cast<hipStream_t>(stream));
+}
+
+int kcc_profile_enable(kcc_ctx* ctx, int on) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  KCC_HIP(ctx, hipDeviceSynchronize());
+  for (const ProfPair& pp : dv.prof_pending) {
+    dv.prof_free.push_back(pp.a);
+    dv.prof_free.push_back(pp.b);
+  }
+  dv.prof_pending.clear();
+  dv.prof_on = on != 0;
+  dv.prof_ms[0] = dv.prof_ms[1] = 0.0;
+  dv.prof_n[0] = dv.prof_n[1] = 0;
+  return KCC_OK;
+}
+
+int kcc_profile_read(kcc_ctx* ctx, double* reduce_ms, int64_t* reduce_launches, double* fit_ms,
+                     int64_t* fit_launches) {
+  if (!ctx) return KCC_EINVAL;
+  if (!reduce_ms || !reduce_launches || !fit_ms || !fit_launches)
+    return fail(ctx, KCC_EINVAL, "NULL output");
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  for (const ProfPair& pp : dv.prof_pending) {
+    KCC_HIP(ctx, hipEventSynchronize(pp.b));
+    float ms = 0.0f;
+    KCC_HIP(ctx, hipEventElapsedTime(&ms, pp.a, pp.b));
+    dv.prof_ms[pp.kind] += ms;
+    dv.prof_n[pp.kind] += 1;
+    dv.prof_free.push_back(pp.a);
+    dv.prof_free.push_back(pp.b);
+  }
+  dv.prof_pending.clear();
+  *reduce_ms = dv.prof_ms[0];
+  *reduce_launches = dv.prof_n[0];
+  *fit_ms = dv.prof_ms[1];
+  *fit_launches = dv.prof_n[1];
+  return KCC_OK;
 }
 
 double kcc_last_slow_fraction(const kcc_ctx* ctx) { return ctx ? ctx->slow_frac : -1.0; }

@@ -42,13 +42,17 @@ inline int64_t reduce_max_waves(int64_t n_containers) {
   return (n_containers + RED_TILE - 1) / RED_TILE + 1;
 }
 
+// Both reduce launches cover nodes [0, n_nodes) of `node_ptr` (the caller offsets
+// node_ptr and the per-node outputs for a node range) and containers [c0, c0 +
+// n_containers): the offsets in node_ptr and the container arrays stay absolute, so a
+// node range of one CSR is reduced without rebasing anything.
 // Zeroes the per-node outputs and records, for every wave range, the node that owns
 // the range's first container (wave_node[n_waves]).
-hipError_t launch_reduce_mark(int64_t n_nodes, int64_t n_containers, const int64_t* node_ptr,
-                              int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem,
-                              uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s);
+hipError_t launch_reduce_mark(int64_t n_nodes, int64_t c0, int64_t n_containers,
+                              const int64_t* node_ptr, int64_t* wave_node, uint64_t* used_cpu,
+                              int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s);
 
-hipError_t launch_reduce(int64_t n_nodes, int64_t n_containers, const int64_t* node_ptr,
+hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, const int64_t* node_ptr,
                          const uint64_t* cpu_req, const int64_t* mem_req,
                          const uint64_t* cpu_lim, const int64_t* mem_lim,
                          const int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem,
@@ -115,9 +119,11 @@ struct SpecPrep {
   int32_t* perm;  // internal index -> caller index
 };
 
-// counters (CNT_*): exact-path (node, spec) pairs, rows in slow_list, class-B specs.
+// counters (CNT_*): exact-path (node, spec) pairs, class-B specs, and per node chunk
+// of a pipelined call (kcc_capacity_partial_async) the rows in that chunk's slow_list.
 // spec_prep zeroes partial[0..2S) and the counters; node_prep appends to slow_list.
-enum { CNT_SLOW_PAIRS = 0, CNT_SLOW_ROWS = 1, CNT_SPECS_B = 2, CNT_N = 4 };
+constexpr int FIT_MAX_CHUNKS = 16;
+enum { CNT_SLOW_PAIRS = 0, CNT_SPECS_B = 1, CNT_SLOW_ROWS = 2, CNT_N = 2 + FIT_MAX_CHUNKS };
 hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
                             const int64_t* spec_mem, SpecPrep sp, int64_t* partial,
                             unsigned long long* counters, hipStream_t s);
@@ -127,13 +133,13 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
                             SlowNode* slow, int64_t* slow_list, unsigned long long* counters,
-                            hipStream_t s);
+                            int chunk, hipStream_t s);
 
 // partial[0..S) += Σ_i q(i,s), partial[S..2S) += #div-by-zero rows (internal order).
 hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,
                       const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
-                      unsigned long long* counters, hipStream_t s);
+                      unsigned long long* counters, int chunk, int64_t grid_nodes, hipStream_t s);
 
 hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial,
                                const int32_t* perm, int64_t* totals, int32_t* spec_err,

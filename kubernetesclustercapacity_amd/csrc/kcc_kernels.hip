@@ -27,8 +27,11 @@ __device__ __forceinline__ unsigned long long atomic_add_u64(uint64_t* p, uint64
 // (a) segmented reduce
 // ----------------------------------------------------------------------------
 
-// Zero the outputs; for every wave range x*range record the node owning it.
-__global__ void reduce_mark_kernel(int64_t n_nodes, int64_t n_cont, int32_t range,
+// Zero the outputs; for every wave range [c0 + x*range, ...) record the node owning
+// its first container.  Node indices are local to the launch (ptr and the outputs are
+// offset by the caller); the container offsets in ptr are absolute and the launch
+// covers containers [c0, c_end).
+__global__ void reduce_mark_kernel(int64_t n_nodes, int64_t c0, int64_t c_end, int32_t range,
                                    const int64_t* __restrict__ ptr,
                                    int64_t* __restrict__ wave_node, uint64_t* __restrict__ o0,
                                    uint64_t* __restrict__ o1, uint64_t* __restrict__ o2,
@@ -39,9 +42,9 @@ __global__ void reduce_mark_kernel(int64_t n_nodes, int64_t n_cont, int32_t rang
     o1[j] = 0;
     if (o2) o2[j] = 0;
     if (o3) o3[j] = 0;
-    int64_t b = ptr[j], e = ptr[j + 1];
+    int64_t b = ptr[j] - c0, e = ptr[j + 1] - c0;  // relative to the launch's first container
     b = b < 0 ? 0 : b;
-    e = e > n_cont ? n_cont : e;
+    e = e > c_end - c0 ? c_end - c0 : e;
     if (e > b) {
       for (int64_t x = (b + range - 1) / range * range; x < e; x += range)
         wave_node[x / range] = j;
@@ -127,7 +130,7 @@ __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff
 // Empty nodes are never visited (zeroed by reduce_mark_kernel).
 template <int NA>
 __global__ __launch_bounds__(256) void reduce_kernel(
-    int64_t n_nodes, int64_t n_cont, int32_t range, const int64_t* __restrict__ ptr,
+    int64_t n_nodes, int64_t c0, int64_t n_cont, int32_t range, const int64_t* __restrict__ ptr,
     const uint64_t* __restrict__ in0, const uint64_t* __restrict__ in1,
     const uint64_t* __restrict__ in2, const uint64_t* __restrict__ in3,
     const int64_t* __restrict__ wave_node, uint64_t* __restrict__ out0,
@@ -137,7 +140,9 @@ __global__ __launch_bounds__(256) void reduce_kernel(
   // wave index made provably uniform (T20: no waterfall loops around the buffer ops)
   const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)(blockIdx.x * RED_WAVES_PER_BLOCK +
                                                              (threadIdx.x >> 6)));
-  const int64_t wb = (int64_t)w * range;
+  // containers [c0, n_cont): absolute indices, like the offsets in ptr (node indices
+  // are local to the launch)
+  const int64_t wb = c0 + (int64_t)w * range;
   if (wb >= n_cont) return;  // wave-uniform; no block-level barrier in this kernel
   const int32_t len = (int32_t)(n_cont - wb < range ? n_cont - wb : range);
   uint64_t (*pre)[RED_TILE] = pre_s[threadIdx.x >> 6];
@@ -316,7 +321,7 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
                                  const int64_t* __restrict__ used_mem,
                                  FitGroupA* __restrict__ fast_a, FitGroup* __restrict__ fast_b,
                                  SlowNode* __restrict__ slow, int64_t* __restrict__ slow_list,
-                                 unsigned long long* __restrict__ counters) {
+                                 unsigned long long* __restrict__ counters, int32_t chunk) {
   const int lane = threadIdx.x & 63;
   const int64_t n_pad = fit_groups(n) * FIT_GROUP;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -367,7 +372,8 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
     const unsigned long long b = __ballot(valid && !ok);
     if (b) {
       unsigned long long base = 0;
-      if (lane == 0) base = atomicAdd(&counters[CNT_SLOW_ROWS], (unsigned long long)__popcll(b));
+      if (lane == 0)
+        base = atomicAdd(&counters[CNT_SLOW_ROWS + chunk], (unsigned long long)__popcll(b));
       base = __shfl(base, 0);
       if (valid && !ok) slow_list[base + __popcll(b & ((1ull << lane) - 1ull))] = i;
     }
@@ -540,7 +546,8 @@ __device__ __forceinline__ void set_round_nearest() {
 // m3 == P ? cl : m3, with the compare mask in an SGPR pair: a v_cndmask reading VCC
 // issues at ~23 cycles per wave64 instruction per SIMD on gfx950 against ~4 with an
 // SGPR-pair mask (scripts/probe/valu_probe.hip), and the compiler picks VCC when free.
-__device__ __forceinline__ int32_t clamp_select(uint32_t m3, uint32_t P, int32_t cl) {
+__device__ __forceinline__ __attribute__((unused)) int32_t clamp_select(uint32_t m3, uint32_t P,
+                                                                     int32_t cl) {
   int32_t r;
   uint64_t mask;
   asm("v_cmp_eq_u32_e64 %1, %2, %3\n\tv_cndmask_b32_e64 %0, %2, %4, %1"
@@ -594,8 +601,8 @@ __global__ __launch_bounds__(256) void fit_kernel(
     int64_t n_nodes, int64_t groups_per_block, const FitGroupA* __restrict__ fast_a,
     const FitGroup* __restrict__ fast_b, const SlowNode* __restrict__ slow,
     const int64_t* __restrict__ slow_list, int64_t S, const SpecRec* __restrict__ specs,
-    int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t gx,
-    int32_t gy) {
+    int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t chunk,
+    int32_t gx, int32_t gy) {
   // XCD-aware order (speed only, never correctness): workgroups are dealt round-robin
   // over the 8 XCDs, so give every spec group of one node chunk the same b % 8 — the
   // chunk's FitGroup records then stay in that XCD's L2 for all of them.
@@ -746,7 +753,7 @@ __global__ __launch_bounds__(256) void fit_kernel(
     for (int64_t i = g0 * FIT_GROUP; i < i1; ++i) eval_slow(i);
   }
   if (!wave_exact) {  // rows outside the fast bounds, shared out over the node-chunk waves
-    const int64_t n_slow = (int64_t)counters[CNT_SLOW_ROWS];
+    const int64_t n_slow = (int64_t)counters[CNT_SLOW_ROWS + chunk];
     for (int64_t j = (int64_t)by * FIT_SPLIT + wv; j < n_slow; j += (int64_t)gy * FIT_SPLIT)
       eval_slow(slow_list[j]);
   }
@@ -798,18 +805,19 @@ inline unsigned grid_for(int64_t n, int block, int64_t cap) {
 
 }  // namespace
 
-hipError_t launch_reduce_mark(int64_t n_nodes, int64_t n_containers, const int64_t* node_ptr,
-                              int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem,
-                              uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s) {
+hipError_t launch_reduce_mark(int64_t n_nodes, int64_t c0, int64_t n_containers,
+                              const int64_t* node_ptr, int64_t* wave_node, uint64_t* used_cpu,
+                              int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s) {
   if (n_nodes <= 0) return hipSuccess;
   hipLaunchKernelGGL(reduce_mark_kernel, dim3(grid_for(n_nodes, 256, 8192)), dim3(256), 0, s,
-                     n_nodes, n_containers, reduce_range(n_containers), node_ptr, wave_node, used_cpu,
+                     n_nodes, c0, c0 + n_containers, reduce_range(n_containers), node_ptr, wave_node,
+                     used_cpu,
                      reinterpret_cast<uint64_t*>(used_mem), lim_cpu,
                      reinterpret_cast<uint64_t*>(lim_mem));
   return hipGetLastError();
 }
 
-hipError_t launch_reduce(int64_t n_nodes, int64_t n_containers, const int64_t* node_ptr,
+hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, const int64_t* node_ptr,
                          const uint64_t* cpu_req, const int64_t* mem_req,
                          const uint64_t* cpu_lim, const int64_t* mem_lim,
                          const int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem,
@@ -820,14 +828,14 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t n_containers, const int64_t* n
   const unsigned blocks = (unsigned)((waves + RED_WAVES_PER_BLOCK - 1) / RED_WAVES_PER_BLOCK);
   const bool lim = cpu_lim && mem_lim && lim_cpu && lim_mem;
   if (lim) {
-    hipLaunchKernelGGL(reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, n_nodes, n_containers,
-                       range, node_ptr, cpu_req, reinterpret_cast<const uint64_t*>(mem_req), cpu_lim,
+    hipLaunchKernelGGL(reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, n_nodes, c0,
+                       c0 + n_containers, range, node_ptr, cpu_req, reinterpret_cast<const uint64_t*>(mem_req), cpu_lim,
                        reinterpret_cast<const uint64_t*>(mem_lim), wave_node, used_cpu,
                        reinterpret_cast<uint64_t*>(used_mem), lim_cpu,
                        reinterpret_cast<uint64_t*>(lim_mem));
   } else {
-    hipLaunchKernelGGL(reduce_kernel<2>, dim3(blocks), dim3(256), 0, s, n_nodes, n_containers,
-                       range, node_ptr, cpu_req, reinterpret_cast<const uint64_t*>(mem_req),
+    hipLaunchKernelGGL(reduce_kernel<2>, dim3(blocks), dim3(256), 0, s, n_nodes, c0,
+                       c0 + n_containers, range, node_ptr, cpu_req, reinterpret_cast<const uint64_t*>(mem_req),
                        (const uint64_t*)nullptr, (const uint64_t*)nullptr, wave_node, used_cpu,
                        reinterpret_cast<uint64_t*>(used_mem), (uint64_t*)nullptr,
                        (uint64_t*)nullptr);
@@ -840,11 +848,11 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
                             SlowNode* slow, int64_t* slow_list, unsigned long long* counters,
-                            hipStream_t s) {
+                            int chunk, hipStream_t s) {
   if (n_nodes <= 0) return hipSuccess;
   hipLaunchKernelGGL(node_prep_kernel, dim3(grid_for(fit_groups(n_nodes) * FIT_GROUP, 256, 8192)), dim3(256), 0, s,
                      n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu, used_mem,
-                     fast_a, fast_b, slow, slow_list, counters);
+                     fast_a, fast_b, slow, slow_list, counters, (int32_t)chunk);
   return hipGetLastError();
 }
 
@@ -860,16 +868,19 @@ hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu, const int
 hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,
                       const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
-                      unsigned long long* counters, hipStream_t s) {
+                      unsigned long long* counters, int chunk, int64_t grid_nodes,
+                      hipStream_t s) {
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
   const int64_t gx = (n_specs + FIT_SPW - 1) / FIT_SPW;
   const int64_t n_groups = fit_groups(n_nodes);
-  // aim for KCC_FIT_TARGET_BLOCKS workgroups (2048 = one round at 8 per CU; 16 rounds keep
-  // the ragged end of the last round short; measured best of 4k..128k at C4); >= 8
-  // groups (64 nodes) each
+  // aim for KCC_FIT_TARGET_BLOCKS workgroups over `grid_nodes` nodes (the whole call's
+  // node count: a chunk of a pipelined call gets its share, not a full grid); 2048 =
+  // one round at 8 per CU, 16 rounds keep the ragged end of the last round short
+  // (measured best of 4k..128k at C4); >= 8 groups (64 nodes) each
   int64_t gy_target = KCC_FIT_TARGET_BLOCKS / gx;
   if (gy_target < 1) gy_target = 1;
-  int64_t gpb = (n_groups + gy_target - 1) / gy_target;
+  const int64_t grid_groups = fit_groups(grid_nodes > n_nodes ? grid_nodes : n_nodes);
+  int64_t gpb = (grid_groups + gy_target - 1) / gy_target;
   if (gpb < 8) gpb = 8;
   int64_t gy = (n_groups + gpb - 1) / gpb;
   // 1-D grid of gx * roundup(gy, 8) workgroups, remapped XCD-aware in the kernel; the
@@ -881,8 +892,8 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
   if (gpb * (int64_t)sizeof(FitGroup) >= 0x7fffffffLL) return hipErrorInvalidValue;
   const int64_t blocks = gx * ((gy + 7) / 8 * 8);
   hipLaunchKernelGGL(fit_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, gpb, fast_a,
-                     fast_b, slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)gx,
-                     (int32_t)gy);
+                     fast_b, slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)chunk,
+                     (int32_t)gx, (int32_t)gy);
   return hipGetLastError();
 }
 

@@ -183,6 +183,31 @@ class CapacityEngine:
                                                      _dp(totals), _dp(spec_err),
                                                      _stream(stream)))
 
+    def capacity_partial_async(self, h_node_ptr, node_ptr, cpu_req, mem_req, alloc_cpu,
+                               alloc_mem, alloc_pods, pod_count, used_cpu, used_mem, spec_cpu,
+                               spec_mem, partial, n_chunks=0, stream=None):
+        """Pipelined reduce + fit partial (kcc_capacity_partial_async): h_node_ptr is the
+        host copy (numpy int64) of node_ptr, used only to place the chunk boundaries."""
+        h = None if h_node_ptr is None else np.ascontiguousarray(h_node_ptr, np.int64)
+        if h is not None and h.size != node_ptr.numel():
+            raise ValueError("h_node_ptr and node_ptr differ in length")
+        self._check(self._lib.kcc_capacity_partial_async(
+            self._h, node_ptr.numel() - 1, cpu_req.numel(), _p(h), _dp(node_ptr), _dp(cpu_req),
+            _dp(mem_req), _dp(alloc_cpu), _dp(alloc_mem), _dp(alloc_pods), _dp(pod_count),
+            _dp(used_cpu), _dp(used_mem), spec_cpu.numel(), _dp(spec_cpu), _dp(spec_mem),
+            _dp(partial), int(n_chunks), _stream(stream)))
+
+    def profile_enable(self, on: bool = True):
+        self._check(self._lib.kcc_profile_enable(self._h, 1 if on else 0))
+
+    def profile_read(self):
+        """(reduce_ms_total, reduce_launches, fit_ms_total, fit_launches) of the pipelined
+        calls since profile_enable (synchronises)."""
+        rm, rn, fm, fn = C.c_double(), C.c_int64(), C.c_double(), C.c_int64()
+        self._check(self._lib.kcc_profile_read(self._h, C.byref(rm), C.byref(rn), C.byref(fm),
+                                               C.byref(fn)))
+        return rm.value, rn.value, fm.value, fn.value
+
     def fit_slow_pairs(self):
         a, b = C.c_int64(), C.c_int64()
         self._check(self._lib.kcc_fit_slow_pairs(self._h, C.byref(a), C.byref(b)))

@@ -34,6 +34,13 @@ def test_binding_covers_every_header_symbol():
     assert set(_lib.header_symbols()) == set(_lib.SIGNATURES)
 
 
+def test_binding_arities_match_header():
+    arity = _lib.header_arities()
+    assert set(arity) == set(_lib.SIGNATURES)
+    wrong = {k: (arity[k], len(v[1])) for k, v in _lib.SIGNATURES.items() if arity[k] != len(v[1])}
+    assert not wrong, f"header vs ctypes parameter counts: {wrong}"
+
+
 def test_library_loads_and_reports_version():
     lib = _lib.load()
     assert lib.kcc_abi_version() == 1

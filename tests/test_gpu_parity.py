@@ -301,6 +301,54 @@ def test_device_api_matches_host(engine):
     assert pairs == n * s and 0 < slow < pairs
 
 
+# ---- pipelined reduce + fit (node chunks, side stream) == host API ------------------------
+@pytest.mark.parametrize("n_chunks", [1, 2, 3, 4, 16])
+def test_pipelined_capacity_matches_host(engine, n_chunks):
+    import torch
+    c = synth.make_cluster(300_001, 6_000_000, seed=31, chunk=4096, adversarial=True)
+    sc, sm = synth.make_specs(333, seed=31, adversarial=True)
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+    n, s = c.n_nodes, sc.size
+    used_cpu = torch.full((n,), 7, dtype=torch.int64, device=dev)   # garbage: must be overwritten
+    used_mem = torch.full((n,), 7, dtype=torch.int64, device=dev)
+    partial = torch.empty(2 * s, dtype=torch.int64, device=dev)
+    totals = torch.empty(s, dtype=torch.int64, device=dev)
+    err = torch.empty(s, dtype=torch.int32, device=dev)
+    args = [T(c.node_ptr), T(c.cpu_req), T(c.mem_req), T(c.alloc_cpu), T(c.alloc_mem),
+            T(c.alloc_pods), T(c.pod_count), used_cpu, used_mem, T(sc), T(sm), partial]
+    stream = torch.cuda.Stream(dev)
+    engine.profile_enable(True)
+    with torch.cuda.stream(stream):
+        for _ in range(2):  # back to back: the second call must wait for the first's fits
+            engine.capacity_partial_async(c.node_ptr, *args, n_chunks=n_chunks, stream=stream)
+            engine.fit_finalize_async(s, partial, totals, err, stream=stream)
+    stream.synchronize()
+    rms, rn, fms, fn = engine.profile_read()
+    engine.profile_enable(False)
+    assert rn == fn and rn >= 2 and rms > 0 and fms > 0
+    np.testing.assert_array_equal(used_cpu.cpu().numpy().view(np.uint64), seg_sums(c.node_ptr, c.cpu_req))
+    np.testing.assert_array_equal(used_mem.cpu().numpy().view(np.uint64), seg_sums(c.node_ptr, c.mem_req))
+    ht, he = engine.capacity(c.node_ptr, c.cpu_req, c.mem_req, c.alloc_cpu, c.alloc_mem,
+                             c.alloc_pods, c.pod_count, sc, sm)
+    np.testing.assert_array_equal(err.cpu().numpy(), he)
+    np.testing.assert_array_equal(totals.cpu().numpy(), ht)
+
+
+def test_pipelined_rejects_bad_host_csr(engine):
+    import torch
+    from kubernetesclustercapacity_amd import KccError
+    dev = torch.device("cuda", 0)
+    n = 100_000
+    ptr = np.arange(n + 1, dtype=np.int64)
+    bad = ptr.copy()
+    bad[n // 2:] = 10 * n  # the chunk boundaries past the middle point beyond n_containers
+    z = lambda k: torch.zeros(k, dtype=torch.int64, device=dev)  # noqa: E731
+    with pytest.raises(KccError):
+        engine.capacity_partial_async(bad, z(n + 1), z(n), z(n), z(n), z(n), z(n), z(n), z(n),
+                                      z(n), z(4), z(4), z(8), n_chunks=4)
+
+
 # ---- BASELINE config C4 at full size: size-independent properties ------------------------
 @pytest.fixture(scope="module")
 def c4():
