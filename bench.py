@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 #    kernel's ISA (pinned by tests/test_isa.py);
 #  - issue peak: one wave64 VALU instruction per SIMD per 4 cycles (PMC: every
 #    SQ_INSTS_VALU costs one SQ_ACTIVE_INST_VALU quad-cycle), 256 CUs x 4 SIMDs x 2.4 GHz.
-FIT_VALU_PER_NODE_WAVE = 5.0
+FIT_VALU_PER_NODE_WAVE = 3.0
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions / s
 METRIC = "node×spec fit evals/sec at 1M nodes × 4K specs; % of HBM roofline"
 # per-launch HBM traffic of each kernel from rocprofv3 PMC passes of this same bench
@@ -168,7 +168,7 @@ def main():
 
     # algorithmic bytes per launch (DESIGN.md "Roofline accounting"): a step runs
     # `chunks` reduce launches and `chunks` fit launches over node ranges of ~n/chunks
-    fit_bytes = (n * 20 + chunks * (S * 48 + S * 8)) / chunks  # FitGroupA + spec records in, totals out
+    fit_bytes = (n * 16 + chunks * (S * 48 + S * 8)) / chunks  # FitGroupA + spec records in, totals out
     red_bytes = (C * 16 + (n + 1) * 8 + n * 16) / chunks       # requests + CSR offsets in, sums out
     fit_gbs = fit_bytes / (fit_ms * 1e-3) / 1e9
     fit_valu = n / chunks * ((S + 63) // 64) * FIT_VALU_PER_NODE_WAVE / (fit_ms * 1e-3)

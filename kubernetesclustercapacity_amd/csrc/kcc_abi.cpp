@@ -59,6 +59,8 @@ struct Dev {
   int64_t prof_n[2] = {0, 0};
   // workspace of the *_async entry points
   DevBuf wave_node, fast_a, fast_b, slow, slow_list, srec, sperm, counters;
+  // clamp correction (kcc::ClampWork)
+  DevBuf c_rank, c_cs, c_ms, c_mless, c_dperm, c_H, c_pkey, c_pb, c_pw, c_dpart;
   int64_t last_pairs = 0;  // node x spec pairs of the last fit_prepare on this device
   int64_t prep_nodes = -1, prep_specs = -1;  // sizes the workspace was last prepared for
   // staging of the host-array entry points
@@ -182,7 +184,32 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.srec, sizeof(kcc::SpecRec) * S));
   KCC_HIP(ctx, ensure(dv.sperm, 4 * S));
   KCC_HIP(ctx, ensure(dv.counters, sizeof(unsigned long long) * kcc::CNT_N));
+  KCC_HIP(ctx, ensure(dv.c_rank, 3 * 4 * S));
+  KCC_HIP(ctx, ensure(dv.c_cs, 8 * S));
+  KCC_HIP(ctx, ensure(dv.c_ms, 8 * S));
+  KCC_HIP(ctx, ensure(dv.c_mless, 4 * S));
+  KCC_HIP(ctx, ensure(dv.c_dperm, 4 * S));
+  KCC_HIP(ctx, ensure(dv.c_H, 8 * (size_t)kcc::clamp_h_cells((int64_t)S)));
+  KCC_HIP(ctx, ensure(dv.c_pkey, 4 * N));
+  KCC_HIP(ctx, ensure(dv.c_pb, 4 * N));
+  KCC_HIP(ctx, ensure(dv.c_pw, 4 * N));
+  KCC_HIP(ctx, ensure(dv.c_dpart, 8 * (size_t)kcc::CLAMP_PARTIAL_ROWS * S));
   return KCC_OK;
+}
+
+kcc::ClampWork clamp_of(Dev& dv) {
+  kcc::ClampWork cw;
+  cw.rank = as<uint32_t>(dv.c_rank);
+  cw.cs = as<uint64_t>(dv.c_cs);
+  cw.ms = as<int64_t>(dv.c_ms);
+  cw.m_less = as<uint32_t>(dv.c_mless);
+  cw.dperm = as<int32_t>(dv.c_dperm);
+  cw.H = as<int64_t>(dv.c_H);
+  cw.pkey = as<uint32_t>(dv.c_pkey);
+  cw.pb = as<uint32_t>(dv.c_pb);
+  cw.pw = as<int32_t>(dv.c_pw);
+  cw.dpart = as<int64_t>(dv.c_dpart);
+  return cw;
 }
 
 int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* alloc_cpu,
@@ -203,14 +230,18 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
   dv.prep_specs = n_specs;
   if (n_specs == 0) return KCC_OK;
   // spec_prep also zeroes `partial` and the counters (no memset launches)
-  KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv), partial,
-                                     as<unsigned long long>(dv.counters), s));
+  KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv), clamp_of(dv),
+                                     partial, as<unsigned long long>(dv.counters), s));
   if (n_nodes == 0) return KCC_OK;
+  KCC_HIP(ctx, kcc::launch_clamp_specs(n_specs, spec_prep_of(dv), clamp_of(dv),
+                                       as<unsigned long long>(dv.counters), s));
   KCC_HIP(ctx, kcc::launch_node_prep(n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count,
                                      used_cpu, used_mem, as<kcc::FitGroupA>(dv.fast_a),
                                      as<kcc::FitGroup>(dv.fast_b), as<kcc::SlowNode>(dv.slow),
-                                     as<int64_t>(dv.slow_list),
+                                     as<int64_t>(dv.slow_list), clamp_of(dv),
                                      as<unsigned long long>(dv.counters), 0, s));
+  KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, n_nodes, clamp_of(dv),
+                                       as<unsigned long long>(dv.counters), partial, s));
   return KCC_OK;
 }
 
@@ -334,9 +365,14 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     KCC_HIP(ctx, hipEventRecord(dv.ev_fork, s));
     KCC_HIP(ctx, hipStreamWaitEvent(dv.side, dv.ev_fork, 0));
   }
-  if (n_specs > 0)  // spec partition on s (concurrent with the first reduce when k > 1)
-    KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv), partial,
-                                       as<unsigned long long>(dv.counters), s));
+  if (n_specs > 0) {  // spec partition on s (concurrent with the first reduce when k > 1)
+    KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv),
+                                       clamp_of(dv), partial, as<unsigned long long>(dv.counters),
+                                       s));
+    if (n_nodes > 0)
+      KCC_HIP(ctx, kcc::launch_clamp_specs(n_specs, spec_prep_of(dv), clamp_of(dv),
+                                           as<unsigned long long>(dv.counters), s));
+  }
   for (int c = 0; c < k; ++c) {
     const int64_t n = hi[c] - lo[c];
     ProfPair pp{};
@@ -367,7 +403,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                        as<kcc::FitGroupA>(dv.fast_a) + lo[c] / kcc::FIT_GROUP,
                                        as<kcc::FitGroup>(dv.fast_b) + lo[c] / kcc::FIT_GROUP,
                                        as<kcc::SlowNode>(dv.slow) + lo[c],
-                                       as<int64_t>(dv.slow_list) + lo[c],
+                                       as<int64_t>(dv.slow_list) + lo[c], clamp_of(dv),
                                        as<unsigned long long>(dv.counters), c, s));
     ProfPair pp{};
     if (dv.prof_on) {
@@ -386,6 +422,9 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
       dv.prof_pending.push_back(pp);
     }
   }
+  // the pod-slot clamp of every chunk's fast rows, added back per spec
+  KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, n_nodes, clamp_of(dv),
+                                       as<unsigned long long>(dv.counters), partial, s));
   return KCC_OK;
 }
 
@@ -562,7 +601,9 @@ void kcc_destroy(kcc_ctx* ctx) {
   for (Dev& dv : ctx->devs) {
     (void)hipSetDevice(dv.device);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
-    DevBuf* bufs[] = {&dv.wave_node, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
+    DevBuf* bufs[] = {&dv.c_rank, &dv.c_cs, &dv.c_ms, &dv.c_mless, &dv.c_dperm, &dv.c_H,
+                      &dv.c_pkey, &dv.c_pb, &dv.c_pw, &dv.c_dpart,
+                      &dv.wave_node, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
                       &dv.sperm,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
                       &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,

@@ -60,11 +60,11 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
 
 // ---- (b) fit -----------------------------------------------------------------
 // Node streams of the fit kernel: groups of FIT_GROUP nodes, field-major inside the
-// group.  Per-node values arrive through the scalar cache (SGPR operands of the VALU),
-// cl by one uniform-address vector load (it is a v_cndmask operand, and gfx9 allows a
-// single SGPR read per VALU instruction besides the lane mask).  Rows outside the
-// fast-path bounds, and the padding of the last group, hold all-zero fields (they
-// contribute exactly 0) and are listed in slow_list for the exact path.
+// group.  The per-node values arrive through the scalar cache and feed the VALU as
+// SGPR operands.  The fast loops sum min(findMin(qc, qm), P) — the pod-slot clamp
+// itself (CC:134-136) is added back per spec by the clamp correction (ClampWork).
+// Rows outside the fast-path bounds, and the padding of the last group, hold all-zero
+// fields (they contribute exactly 0) and are listed in slow_list for the exact path.
 //
 // FitGroupA — class-A spec waves: the integers themselves, which the
 // VALU reads as IEEE denormals (an integer k < 2^23 is the f32 bit pattern of
@@ -74,19 +74,17 @@ struct __attribute__((aligned(32))) FitGroupA {
   uint64_t fm[FIT_GROUP];  // free memory (bytes), < 2^50
   uint32_t fc[FIT_GROUP];  // free CPU (millicores), < 2^23
   uint32_t P[FIT_GROUP];   // max(allocatable pods, 0), <= 2^20
-  int32_t cl[FIT_GROUP];   // clamp value allocatable pods - podCount (CC:135)
 };
-static_assert(sizeof(FitGroupA) == 160, "FitGroupA must be 160 B");
+static_assert(sizeof(FitGroupA) == 128, "FitGroupA must be 128 B");
 // FitGroup — class-B spec waves (memory request < 2^18): f64 values for the biased
 // FMA path; written by node_prep only when such specs exist.
 constexpr double FIT_BIAS = 4503599627370496.0;  // 2^52: integers in [2^52, 2^53) have ulp 1
 struct __attribute__((aligned(32))) FitGroup {
-  double fc[FIT_GROUP];   // free CPU (millicores), exact in f64
-  double fm[FIT_GROUP];   // free memory (bytes), exact in f64
-  double Pb[FIT_GROUP];   // 2^52 + allocatable pods (|P| <= 2^20: exact), the biased compare operand
-  int32_t cl[FIT_GROUP];  // clamp value allocatable pods - podCount (CC:135)
+  double fc[FIT_GROUP];  // free CPU (millicores), exact in f64
+  double fm[FIT_GROUP];  // free memory (bytes), exact in f64
+  double Pb[FIT_GROUP];  // 2^52 + max(allocatable pods, 0) (<= 2^20: exact)
 };
-static_assert(sizeof(FitGroup) == 224, "FitGroup must be 224 B");
+static_assert(sizeof(FitGroup) == 192, "FitGroup must be 192 B");
 __host__ __device__ inline int64_t fit_groups(int64_t n_nodes) { return (n_nodes + FIT_GROUP - 1) / FIT_GROUP; }
 
 // Raw per-node values for the exact path (fc/fm are 0 where the reference's
@@ -119,21 +117,62 @@ struct SpecPrep {
   int32_t* perm;  // internal index -> caller index
 };
 
+// Clamp correction.  On the fast paths the fit kernel sums
+// min(findMin(qc, qm), P) and leaves out the pod-slot clamp of CC:134-136; the clamp is
+// added back per spec as  partial[s] -= D_s,  D_s = Σ_i w_i [x_is >= P_i],  w_i = P_i - cl_i
+// (the pod count; for P_i <= 0 rows, clamped for every spec, w_i = -cl_i).  For P_i >= 1,
+// x_is >= P_i  <=>  c_s <= U_i = fc_i / P_i  and  m_s <= V_i = fm_i / P_i  (integer
+// quotients): a 2-D dominance count.  The normal specs (classes A and B) are ranked by c
+// (groups of 64 consecutive c-ranks) and by m; a node covering L_i = #{s : c_s <= U_i}
+// c-ranks covers groups [0, G_i = L_i / 64) fully — one cell H[G_i][b_i] of a
+// (T+1) x (nN+1) table, b_i = #{s : m_s <= V_i}, read back through a 2-D suffix sum — and
+// the first r_i = L_i % 64 lanes of group G_i: one plist entry (key G_i<<6 | r_i, b_i, w_i).
+struct ClampWork {
+  uint32_t* rank;    // [3*S] per normal spec (internal position): c-rank, m-rank, #{smaller m}
+  uint64_t* cs;      // [S] normal specs' cpu requests in c-rank order
+  int64_t* ms;       // [S] normal specs' memory requests in m-rank order
+  uint32_t* m_less;  // [S] by c-rank: #normal specs with a smaller memory request
+  int32_t* dperm;    // [S] c-rank -> internal position
+  int64_t* H;        // [(S/64 + 2) * (S + 1)] (T+1) x (nN+1) clamp weights, then their 2-D suffix sums
+  uint32_t* pkey;    // [N] plist: G << 6 | r
+  uint32_t* pb;      // [N] plist: b (m-rank bound)
+  int32_t* pw;       // [N] plist: w
+  int64_t* dpart;    // [CLAMP_PARTIAL_ROWS * S] per-workgroup partial-group sums
+};
+inline int64_t clamp_h_cells(int64_t S) { return (S / 64 + 2) * (S + 1); }
+// up to this many normal specs the sorted requests / accumulators live in LDS
+constexpr int64_t CLAMP_LDS_SPECS = 4096;
+constexpr int64_t CLAMP_PARTIAL_ROWS = 64;
+
 // counters (CNT_*): exact-path (node, spec) pairs, class-B specs, and per node chunk
 // of a pipelined call (kcc_capacity_partial_async) the rows in that chunk's slow_list.
 // spec_prep zeroes partial[0..2S) and the counters; node_prep appends to slow_list.
 constexpr int FIT_MAX_CHUNKS = 16;
-enum { CNT_SLOW_PAIRS = 0, CNT_SPECS_B = 1, CNT_SLOW_ROWS = 2, CNT_N = 2 + FIT_MAX_CHUNKS };
+enum {
+  CNT_SLOW_PAIRS = 0,  // (node, spec) pairs evaluated on the exact path
+  CNT_SPECS_A = 1,     // class-A specs (internal positions [0, nA))
+  CNT_SPECS_B = 2,     // class-B specs (internal positions [nA, nA + nB))
+  CNT_PLIST = 3,       // clamp-correction plist entries
+  CNT_SLOW_ROWS = 4,   // + chunk: rows in that node chunk's slow_list
+  CNT_N = 4 + FIT_MAX_CHUNKS
+};
 hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
-                            const int64_t* spec_mem, SpecPrep sp, int64_t* partial,
+                            const int64_t* spec_mem, SpecPrep sp, ClampWork cw, int64_t* partial,
                             unsigned long long* counters, hipStream_t s);
+// c/m ranks of the normal specs, sorted arrays, zeroed H (after spec_prep)
+hipError_t launch_clamp_specs(int64_t n_specs, SpecPrep sp, ClampWork cw,
+                              const unsigned long long* counters, hipStream_t s);
+// H -> its 2-D suffix sums; partial[s] -= D_s for the normal specs of clamp-free waves
+// (after every node_prep of the call, before the all-reduce)
+hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
+                              const unsigned long long* counters, int64_t* partial, hipStream_t s);
 
 hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
-                            SlowNode* slow, int64_t* slow_list, unsigned long long* counters,
-                            int chunk, hipStream_t s);
+                            SlowNode* slow, int64_t* slow_list, ClampWork cw,
+                            unsigned long long* counters, int chunk, hipStream_t s);
 
 // partial[0..S) += Σ_i q(i,s), partial[S..2S) += #div-by-zero rows (internal order).
 hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,

@@ -308,12 +308,44 @@ __device__ __forceinline__ int32_t spec_class(uint64_t c, int64_t m) {
   return m >= CLASS_A_M_MIN ? SPEC_A : SPEC_B;
 }
 
+// Smallest f64 >= 1/v (1 <= v < 2^51, exact in f64): the fit's quotients never
+// undershoot.
+__device__ __forceinline__ double recip_up_f64(uint64_t v) {
+  const double vd = (double)v;
+  double r = 1.0 / vd;                                   // correctly rounded
+  if (fma(r, vd, -1.0) < 0.0) r = __longlong_as_double(__double_as_longlong(r) + 1);  // next up
+  return r;
+}
+
+// ---- clamp-correction helpers (see ClampWork in kcc_internal.h) ----
+
+__device__ __forceinline__ int64_t clamp_n_normal(const unsigned long long* counters) {
+  return (int64_t)(counters[CNT_SPECS_A] + counters[CNT_SPECS_B]);
+}
+// normal specs whose wavefront has no exact-path lane (the exact path applies the clamp
+// itself): all of them, or all but a last wave shared with exact-path specs
+__device__ __forceinline__ int64_t clamp_n_pure(int64_t nN, int64_t S) {
+  return (nN % 64 == 0 || nN == S) ? nN : nN / 64 * 64;
+}
+
+// #{k < n : a[k] <= v} for a sorted ascending (binary search, n <= 2^31)
+template <class T>
+__device__ __forceinline__ uint32_t upper_bound_count(const T* __restrict__ a, int64_t n, T v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] <= v) lo = mid + 1;
+    else hi = mid;
+  }
+  return (uint32_t)lo;
+}
+
 // Per-node free capacity (CC:119-135 operands).  Rows that fit the fast-path
 // bounds get exact FitGroupA fields (and FitGroup fields when class-B specs exist);
 // the others get all-zero fields (contribute exactly 0 on the fast paths) and are
 // appended to slow_list for the exact 64-bit path.  Covers the padding of the last
 // group too (zero fields, not listed).
-__global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_cpu,
+__global__ __launch_bounds__(1024) void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_cpu,
                                  const int64_t* __restrict__ alloc_mem,
                                  const int64_t* __restrict__ alloc_pods,
                                  const int64_t* __restrict__ pod_count,
@@ -321,12 +353,37 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
                                  const int64_t* __restrict__ used_mem,
                                  FitGroupA* __restrict__ fast_a, FitGroup* __restrict__ fast_b,
                                  SlowNode* __restrict__ slow, int64_t* __restrict__ slow_list,
-                                 unsigned long long* __restrict__ counters, int32_t chunk) {
+                                 ClampWork cw, unsigned long long* __restrict__ counters,
+                                 int32_t chunk) {
   const int lane = threadIdx.x & 63;
   const int64_t n_pad = fit_groups(n) * FIT_GROUP;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const bool want_b = counters[CNT_SPECS_B] != 0;  // written by spec_prep (same stream)
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i - lane < n_pad; i += stride) {
+  const int64_t nN = clamp_n_normal(counters);     // normal specs (clamp correction)
+  const int64_t T = (nN + 63) / 64, hw = nN + 1;
+  // the sorted spec requests of the binary searches, in LDS when they fit: c clamped
+  // to 2^23 (> every U = fc / P, fc < 2^23) as u32, m as i64
+  extern __shared__ __attribute__((aligned(16))) unsigned char np_lds[];
+  int64_t* ms_l = reinterpret_cast<int64_t*>(np_lds);
+  uint32_t* cs_l = reinterpret_cast<uint32_t*>(np_lds + 8 * CLAMP_LDS_SPECS);
+  const bool lds = nN <= CLAMP_LDS_SPECS;
+  // smallest normal requests (rows below either dominate no spec); cs[0] >= 1
+  const uint32_t cmin = nN > 0 ? (cw.cs[0] < FAST_FC_MAX ? (uint32_t)cw.cs[0] : (uint32_t)FAST_FC_MAX)
+                               : 0xffffffffu;
+  const int64_t mmin = nN > 0 ? cw.ms[0] : INT64_MAX;
+  if (lds) {
+    for (int64_t k = threadIdx.x; k < nN; k += blockDim.x) {
+      const uint64_t c = cw.cs[k];
+      cs_l[k] = c < FAST_FC_MAX ? (uint32_t)c : (uint32_t)FAST_FC_MAX;
+      ms_l[k] = cw.ms[k];
+    }
+  }
+  __syncthreads();
+  __shared__ unsigned long long wcount[16], wg_base;
+  const int wv = threadIdx.x >> 6;
+  // block-uniform trip count (the plist append below synchronises the workgroup)
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n_pad; i0 += stride) {
+    const int64_t i = i0 + threadIdx.x;
     const bool valid = i < n;
     bool ok = false;
     uint64_t fc_ok = 0;
@@ -360,14 +417,76 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
       a.fm[k] = (uint64_t)fm_ok;
       a.fc[k] = (uint32_t)fc_ok;
       a.P[k] = (uint32_t)(P_ok > 0 ? P_ok : 0);  // P <= 0: x >= P always (clamp), as for P = 0
-      a.cl[k] = cl_i;
       if (want_b) {
         FitGroup& g = fast_b[i / FIT_GROUP];
-        g.fc[k] = (double)fc_ok;                          // exact
-        g.fm[k] = (double)fm_ok;                          // exact (< 2^50)
-        g.Pb[k] = ok ? FIT_BIAS + (double)P_ok : 0.0;     // exact (|P| <= 2^20)
-        g.cl[k] = cl_i;
+        g.fc[k] = (double)fc_ok;                                         // exact
+        g.fm[k] = (double)fm_ok;                                         // exact (< 2^50)
+        g.Pb[k] = FIT_BIAS + (double)(P_ok > 0 ? P_ok : 0);              // exact (P <= 2^20)
       }
+    }
+    // clamp correction: where (and with which weight) this row's pod-slot clamp applies
+    bool always = false, in_plist = false;
+    int64_t w = 0;
+    uint32_t key = 0, bnd = 0;
+    if (ok && nN > 0) {
+      const int64_t P = P_ok, Penc = P > 0 ? P : 0;
+      w = Penc - (int64_t)cl_i;  // contribution = min(x, Penc) - w when clamped
+      if (P <= 0) {
+        always = true;  // x >= P for every spec
+      } else {
+        // c <= U  <=>  floor(fc / c) >= P  and  m <= V  <=>  floor(fm / m) >= P, with
+        // U = floor(fc / P), V = floor(fm / P) from the rounded-up reciprocal of P
+        // (exact: fc, fm < 2^50, P < 2^51)
+        const double rP = recip_up_f64((uint64_t)P);
+        const uint32_t U = (uint32_t)((double)fc_ok * rP);
+        const int64_t V = (int64_t)((double)fm_ok * rP);
+        uint32_t L = 0, b = 0;
+        if (U >= cmin && V >= mmin) {  // else no spec is dominated
+#ifdef KCC_DIAG_NO_SEARCH  // diagnostic timing build only: results are wrong
+          L = U % (uint32_t)(nN + 1);
+          b = (uint32_t)(V % (nN + 1));
+#else
+          L = lds ? upper_bound_count(cs_l, nN, U) : upper_bound_count(cw.cs, nN, (uint64_t)U);
+          b = lds ? upper_bound_count(ms_l, nN, V) : upper_bound_count(cw.ms, nN, V);
+#endif
+        }
+        if (L > 0 && b > 0 && w != 0) {
+          const uint32_t G = L >> 6, r = L & 63u;
+#ifndef KCC_DIAG_NO_H_ATOMIC  // diagnostic timing build only: results are wrong
+          if (G > 0) atomic_add_u64(reinterpret_cast<uint64_t*>(&cw.H[G * hw + b]), (uint64_t)w);
+#endif
+          in_plist = r != 0;
+          key = G << 6 | r;
+          bnd = b;
+        }
+      }
+    }
+    {  // rows clamped for every spec: one wave-summed atomic into H[T][nN]
+      uint64_t v = always ? (uint64_t)w : 0ull;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+      if (lane == 0 && v) atomic_add_u64(reinterpret_cast<uint64_t*>(&cw.H[T * hw + nN]), v);
+    }
+    {  // plist append: one atomic per workgroup (a per-wave atomic on one counter
+       // serialises ~15k waves at C4)
+      const unsigned long long pm = __ballot(in_plist);
+      if (lane == 0) wcount[wv] = __popcll(pm);
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        unsigned long long tot = 0;
+        for (int k = 0; k < (int)(blockDim.x >> 6); ++k) tot += wcount[k];
+        wg_base = tot ? atomicAdd(&counters[CNT_PLIST], tot) : 0ull;
+      }
+      __syncthreads();
+      if (in_plist) {
+        unsigned long long j = wg_base;
+        for (int k = 0; k < wv; ++k) j += wcount[k];
+        j += __popcll(pm & ((1ull << lane) - 1ull));
+        cw.pkey[j] = key;
+        cw.pb[j] = bnd;
+        cw.pw[j] = (int32_t)w;
+      }
+      __syncthreads();  // wcount / wg_base are reused by the next iteration
     }
     const unsigned long long b = __ballot(valid && !ok);
     if (b) {
@@ -378,15 +497,6 @@ __global__ void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_c
       if (valid && !ok) slow_list[base + __popcll(b & ((1ull << lane) - 1ull))] = i;
     }
   }
-}
-
-// Smallest f64 >= 1/v (1 <= v < 2^51, exact in f64): the fit's quotients never
-// undershoot.
-__device__ __forceinline__ double recip_up_f64(uint64_t v) {
-  const double vd = (double)v;
-  double r = 1.0 / vd;                                   // correctly rounded
-  if (fma(r, vd, -1.0) < 0.0) r = __longlong_as_double(__double_as_longlong(r) + 1);  // next up
-  return r;
 }
 
 // Smallest f32 >= 1/v (1 <= v < 2^51, exact in f64).  1/v is first rounded to f64,
@@ -406,7 +516,8 @@ __device__ __forceinline__ float recip_up_f32(uint64_t v) {
 // partial[0..2S) and sets the counters (no memset launches).
 __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64_t* __restrict__ c_in,
                                                          const int64_t* __restrict__ m_in,
-                                                         SpecPrep sp, int64_t* __restrict__ partial,
+                                                         SpecPrep sp, ClampWork cw,
+                                                         int64_t* __restrict__ partial,
                                                          unsigned long long* __restrict__ counters) {
   __shared__ int64_t wsum[16][2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -494,36 +605,256 @@ __global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64
     sp.perm[pos] = (int32_t)i;
   }
   for (int64_t i = tid; i < 2 * S; i += 1024) partial[i] = 0;
-  if (tid < CNT_N) counters[tid] = tid == CNT_SPECS_B ? (unsigned long long)tot[1] : 0ull;
+  for (int64_t i = tid; i < 3 * S; i += 1024) cw.rank[i] = 0;
+  if (tid < CNT_N)
+    counters[tid] = tid == CNT_SPECS_A ? (unsigned long long)tot[0]
+                  : tid == CNT_SPECS_B ? (unsigned long long)tot[1] : 0ull;
+}
+
+// ---- clamp correction (see ClampWork in kcc_internal.h) ----------
+
+// Ranks of the normal specs (internal positions [0, nN)) among themselves, by brute
+// force over a 2-D grid of 256 x CLAMP_RANK_TILE tiles (exact, order-free atomics):
+//   c-rank(p) = #{q : (c_q, q) < (c_p, p)},  m-rank(p) = #{q : (m_q, q) < (m_p, p)},
+//   m-less(p) = #{q : m_q < m_p}
+constexpr int CLAMP_RANK_TILE = 64;
+__global__ __launch_bounds__(256) void clamp_rank_kernel(const SpecRec* __restrict__ rec,
+                                                         ClampWork cw, int64_t S,
+                                                         const unsigned long long* __restrict__ counters) {
+  const int64_t nN = clamp_n_normal(counters);
+  const int64_t p0 = (int64_t)blockIdx.x * 256, q0 = (int64_t)blockIdx.y * CLAMP_RANK_TILE;
+  if (p0 >= nN || q0 >= nN) return;  // whole block
+  __shared__ uint64_t cq[CLAMP_RANK_TILE];
+  __shared__ int64_t mq[CLAMP_RANK_TILE];
+  const int t = threadIdx.x;
+  if (t < CLAMP_RANK_TILE) {
+    const int64_t q = q0 + t;
+    cq[t] = q < nN ? rec[q].c : ~0ull;
+    mq[t] = q < nN ? rec[q].m : INT64_MAX;
+  }
+  __syncthreads();
+  const int64_t p = p0 + t;
+  if (p >= nN) return;
+  const uint64_t c = rec[p].c;
+  const int64_t m = rec[p].m;
+  const int qn = (int)(nN - q0 < CLAMP_RANK_TILE ? nN - q0 : CLAMP_RANK_TILE);
+  uint32_t rc = 0, rm = 0, ml = 0;
+  for (int j = 0; j < qn; ++j) {
+    const bool before = q0 + j < p;
+    rc += (cq[j] < c || (cq[j] == c && before)) ? 1u : 0u;
+    rm += (mq[j] < m || (mq[j] == m && before)) ? 1u : 0u;
+    ml += mq[j] < m ? 1u : 0u;
+  }
+  if (rc) atomicAdd(&cw.rank[p], rc);
+  if (rm) atomicAdd(&cw.rank[S + p], rm);
+  if (ml) atomicAdd(&cw.rank[2 * S + p], ml);
+}
+
+// Sorted arrays from the ranks; zero the used part of H.
+__global__ void clamp_scatter_kernel(const SpecRec* __restrict__ rec, ClampWork cw, int64_t S,
+                                     const unsigned long long* __restrict__ counters) {
+  const int64_t nN = clamp_n_normal(counters);
+  const int64_t T = (nN + 63) / 64;
+  const int64_t cells = (T + 1) * (nN + 1);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells || i < nN; i += stride) {
+    if (i < nN) {
+      const uint32_t d = cw.rank[i];
+      cw.cs[d] = rec[i].c;
+      cw.dperm[d] = (int32_t)i;
+      cw.m_less[d] = cw.rank[2 * S + i];
+      cw.ms[cw.rank[S + i]] = rec[i].m;
+    }
+    if (i < cells) cw.H[i] = 0;
+  }
+}
+
+// 2-D suffix sums of H, step 1: down each column (G from T to 0), one thread per
+// column, eight rows' loads in flight at a time
+__global__ __launch_bounds__(64) void clamp_hcol_kernel(ClampWork cw,
+                                                        const unsigned long long* __restrict__ counters) {
+  const int64_t nN = clamp_n_normal(counters);
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (nN == 0 || b > nN) return;
+  const int64_t T = (nN + 63) / 64, w = nN + 1;
+  uint64_t run = 0;
+  for (int64_t G0 = T; G0 >= 0; G0 -= 8) {
+    uint64_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = G0 - k >= 0 ? (uint64_t)cw.H[(G0 - k) * w + b] : 0ull;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      run += v[k];
+      if (G0 - k >= 0) cw.H[(G0 - k) * w + b] = (int64_t)run;
+    }
+  }
+}
+
+// step 2: along each row (b from nN to 0), one 1024-thread workgroup per row, in tiles
+// of 1024 from the end (wave suffix scans + a carry)
+__global__ __launch_bounds__(1024) void clamp_hrow_kernel(ClampWork cw,
+                                                          const unsigned long long* __restrict__ counters) {
+  const int64_t nN = clamp_n_normal(counters);
+  const int64_t G = blockIdx.x;
+  const int64_t T = (nN + 63) / 64;
+  if (nN == 0 || G > T) return;  // whole block
+  __shared__ uint64_t wtot[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t w = nN + 1;
+  int64_t* row = cw.H + G * w;
+  uint64_t carry = 0;
+  for (int64_t end = w; end > 0; end -= 1024) {
+    const int64_t i = end - 1 - tid;  // thread tid walks the row backwards
+    uint64_t v = i >= 0 ? (uint64_t)row[i] : 0ull;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {  // inclusive scan in thread order = suffix in b
+      const uint64_t u = __shfl_up(v, d);
+      if (lane >= d) v += u;
+    }
+    if (lane == 63) wtot[wv] = v;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+    for (int k = 0; k < 16; ++k) {
+      if (k < wv) before += wtot[k];
+      all += wtot[k];
+    }
+    if (i >= 0) row[i] = (int64_t)(v + before + carry);
+    carry += all;
+    __syncthreads();
+  }
+}
+
+// D_partial: every plist entry (G, r, b, w) adds w to the specs with c-rank 64G + lane,
+// lane < r, and m_less < b.  CLAMP_PARTIAL_WGS workgroups share the entries; each
+// accumulates ALL nN specs in LDS (ds_add_u64; one entry per wave-iteration, lanes =
+// the entry's group) and writes its row of dpart[CLAMP_PARTIAL_WGS][nN]; clamp_full
+// sums the rows.  nN <= CLAMP_LDS_SPECS (else clamp_partial_big_kernel).
+constexpr int CLAMP_PARTIAL_WGS = (int)CLAMP_PARTIAL_ROWS;
+__global__ __launch_bounds__(1024) void clamp_partial_kernel(ClampWork cw,
+                                                             const unsigned long long* __restrict__ counters,
+                                                             int64_t* __restrict__ dpart) {
+  const int64_t nN = clamp_n_normal(counters);
+  if (nN == 0 || nN > CLAMP_LDS_SPECS) return;
+  __shared__ uint32_t ml_l[CLAMP_LDS_SPECS];
+  __shared__ unsigned long long acc_l[CLAMP_LDS_SPECS];
+  for (int64_t q = threadIdx.x; q < nN; q += blockDim.x) {
+    ml_l[q] = cw.m_less[q];
+    acc_l[q] = 0;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int32_t wv = __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6));
+  const int32_t nw = (int32_t)(blockDim.x >> 6);
+  const int64_t npl = (int64_t)counters[CNT_PLIST];
+  const int64_t j0 = npl * blockIdx.x / CLAMP_PARTIAL_WGS, j1 = npl * (blockIdx.x + 1) / CLAMP_PARTIAL_WGS;
+  // 64 entries per wave-iteration by one coalesced load each, then walked lane by lane
+  // from registers (v_readlane): no memory latency inside the inner loop
+  for (int64_t jb = j0 + (int64_t)wv * 64; jb < j1; jb += (int64_t)nw * 64) {
+    const int64_t j = jb + lane;
+    const bool in = j < j1;
+    const uint32_t key_v = in ? cw.pkey[j] : 0u, bnd_v = in ? cw.pb[j] : 0u;
+    const int32_t w_v = in ? cw.pw[j] : 0;
+    const int cnt = (int)(j1 - jb < 64 ? j1 - jb : 64);
+    for (int k = 0; k < cnt; ++k) {
+      const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)key_v, k);
+      const uint32_t bnd = (uint32_t)__builtin_amdgcn_readlane((int)bnd_v, k);
+      const int32_t w = __builtin_amdgcn_readlane(w_v, k);
+      const int64_t q = (int64_t)(key >> 6) * 64 + lane;
+      if ((uint32_t)lane < (key & 63u) && ml_l[q] < bnd)
+        atomicAdd(&acc_l[q], (unsigned long long)(int64_t)w);
+    }
+  }
+  __syncthreads();
+  for (int64_t q = threadIdx.x; q < nN; q += blockDim.x)
+    dpart[(int64_t)blockIdx.x * nN + q] = (int64_t)acc_l[q];
+}
+
+// the same for nN > CLAMP_LDS_SPECS: one wavefront per (group, slice of the plist),
+// lanes = the group's 64 c-ranks; scans the 4-B keys, reads b / w only for matches,
+// and subtracts straight from partial
+constexpr int CLAMP_SLICES = 512;
+__global__ __launch_bounds__(64) void clamp_partial_big_kernel(ClampWork cw,
+                                                               const unsigned long long* __restrict__ counters,
+                                                               int64_t S, int64_t* __restrict__ partial) {
+  const int64_t nN = clamp_n_normal(counters);
+  if (nN <= CLAMP_LDS_SPECS) return;
+  const int64_t T = (nN + 63) / 64;
+  const int64_t g = blockIdx.x;
+  if (g >= T) return;
+  const int lane = threadIdx.x;
+  const int64_t q = g * 64 + lane;
+  const bool valid = q < nN;
+  const uint32_t ml = valid ? cw.m_less[q] : 0xffffffffu;
+  const int64_t npl = (int64_t)counters[CNT_PLIST];
+  const int64_t j0 = npl * blockIdx.y / CLAMP_SLICES, j1 = npl * (blockIdx.y + 1) / CLAMP_SLICES;
+  uint64_t acc = 0;
+  for (int64_t jb = j0; jb < j1; jb += 64) {
+    const int64_t j = jb + lane;
+    const uint32_t key = j < j1 ? cw.pkey[j] : 0xffffffffu;
+    uint64_t mask = __ballot((int64_t)(key >> 6) == g);
+    while (mask) {
+      const int k = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)key, k) & 63u;
+      const int64_t jj = jb + k;
+      const uint32_t bnd = cw.pb[jj];
+      const int32_t w = cw.pw[jj];
+      acc += ((uint32_t)lane < r && ml < bnd) ? (uint64_t)(int64_t)w : 0ull;
+    }
+  }
+  if (valid && acc) {
+    const int32_t p = cw.dperm[q];
+    if (p < clamp_n_pure(nN, S)) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[p]), 0ull - acc);
+  }
+}
+
+// partial[p] -= D(p) = HS[g + 1][m_less + 1] + Σ_k dpart[k][q] for the normal specs of
+// clamp-free waves (q = the spec's c-rank, g = q / 64)
+__global__ void clamp_full_kernel(ClampWork cw, const unsigned long long* __restrict__ counters,
+                                  int64_t S, const int64_t* __restrict__ dpart,
+                                  int64_t* __restrict__ partial) {
+  const int64_t nN = clamp_n_normal(counters);
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // c-rank
+  if (q >= nN) return;
+  const int64_t T = (nN + 63) / 64, w = nN + 1;
+  const int64_t g1 = (q >> 6) + 1, b1 = (int64_t)cw.m_less[q] + 1;
+  const int32_t p = cw.dperm[q];
+  if (p >= clamp_n_pure(nN, S)) return;
+  uint64_t d = (g1 <= T && b1 <= nN) ? (uint64_t)cw.H[g1 * w + b1] : 0ull;
+  if (nN <= CLAMP_LDS_SPECS)
+    for (int k = 0; k < CLAMP_PARTIAL_WGS; ++k) d += (uint64_t)dpart[(int64_t)k * nN + q];
+  if (d) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[p]), 0ull - d);
 }
 
 // Lane = spec (its request, reciprocals and running total live in VGPRs); the node
 // stream is wave-uniform: the fields of a FitGroup arrive by scalar loads and feed the
-// VALU as SGPR operands, cl by one uniform-address buffer load.  The main loops are
-// branch-free: rows outside the fast bounds carry zero fields and are re-done exactly
-// from slow_list.  No cross-lane reduction until the block's end (one 64-bit atomic
-// per spec).  Everything below is exact ("Fit fast path: exactness").
+// VALU as SGPR operands.  The main loops are branch-free: rows outside the fast bounds
+// carry zero fields and are re-done exactly from slow_list.  No cross-lane reduction
+// until the block's end (one 64-bit atomic per spec).  Everything is exact (DESIGN.md
+// §5, "Fit fast path: exactness").
 //
-// Class A (1 <= c < 2^51, 2^18 <= m < 2^51; fc < 2^23, fm < 2^50), the loop runs in
-// round-toward--inf (f32 and f64) on integers read as denormals:
+// The fast loops (normal specs: 1 <= c, m < 2^51) sum  min(findMin(qc, qm), P)  per
+// node, which equals the reference's contribution `x >= P ? P - podCount : x`
+// (CC:133-136) except where the clamp applies — there it is larger by w = podCount;
+// the clamp correction (ClampWork, clamp_*_kernel) subtracts  Σ w  over those nodes
+// from each spec's total.  The per-pair work is the two quotients and one min:
+//
+// Class A (m >= 2^18; fc < 2^23, fm < 2^50), round-toward--inf, integers read as denormals:
 //   qc = bits(RD32(fc*2^-149 * rcf)) = floor(fc * rcf) = floor(fc / c)   (rcf = RU32(1/c))
 //     — one v_pk_mul_f32 for two nodes (an SGPR pair of free CPUs);
 //   qm = low32(bits(RD64(fm*2^-1074 * rm))) = floor(fm / m)             (rm = RU64(1/m))
 //     — one v_mul_f64 (qm < 2^50 / 2^18 = 2^32, so the low dword is all of it);
-//   m3 = min3(qc, qm, P) = min(findMin(qc, qm), P)                       (CC:159-164)
-//   contribution = m3 == P ? P - podCount : m3  (x >= P <=> m3 == P)     (CC:133-136)
+//   min3(qc, qm, P) — one v_min3_u32; two nodes per v_add3_u32.
 // The products are exact reals rounded once onto the 2^-149 / 2^-1074 grid, so the
 // rounding down IS floor; a quotient that is an integer is never undershot (the
 // reciprocal is rounded up), a non-integer one lies >= 1/c below the next integer,
 // more than the relative error (< 2^-23 resp. 2^-52) covers while fc < 2^23, fm < 2^52.
-// Per node and 64-spec wavefront: v_pk_mul_f32 (half), v_mul_f64, v_min3_u32,
-// v_cmp_eq_u32, v_cndmask_b32, v_add3_u32 (half) = 5 VALU instructions.
+// Per node and 64-spec wavefront: 3 VALU instructions.
 //
-// Class B (memory requests below 2^18, where fm/m may exceed 32 bits): f64 values, the
-// loop in round-toward--inf, one fused multiply-add per quotient doing floor AND the
+// Class B (memory requests below 2^18, where fm/m may exceed 32 bits): f64 values,
+// round-toward--inf, one fused multiply-add per quotient doing floor AND the
 // conversion: qc' = RD(fc * rc + 2^52) = 2^52 + floor(fc / c), likewise qm';
-// x' = min(qc', qm'); contribution = x' >= 2^52 + P ? P - podCount : low32(x').
-// 5.5 VALU instructions per node and wavefront.
+// min(qc', qm', 2^52 + P) and its low dword.  4.5 VALU instructions per node and wave.
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef int32_t i32x8 __attribute__((ext_vector_type(8)));
 typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
@@ -543,40 +874,12 @@ __device__ __forceinline__ void set_round_down() {
 __device__ __forceinline__ void set_round_nearest() {
   asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 4), 0\n\ts_nop 1" ::: "memory");
 }
-// m3 == P ? cl : m3, with the compare mask in an SGPR pair: a v_cndmask reading VCC
-// issues at ~23 cycles per wave64 instruction per SIMD on gfx950 against ~4 with an
-// SGPR-pair mask (scripts/probe/valu_probe.hip), and the compiler picks VCC when free.
-__device__ __forceinline__ __attribute__((unused)) int32_t clamp_select(uint32_t m3, uint32_t P,
-                                                                     int32_t cl) {
-  int32_t r;
-  uint64_t mask;
-  asm("v_cmp_eq_u32_e64 %1, %2, %3\n\tv_cndmask_b32_e64 %0, %2, %4, %1"
-      : "=v"(r), "=&s"(mask)
-      : "v"(m3), "s"(P), "v"(cl));
-  return r;
-}
-// acc += (a == Pa ? cla : a) + (b == Pb ? clb : b) in one block: one hazard wait
-// between blocks instead of one per select
-__device__ __forceinline__ void clamp_select2_acc(int32_t& acc, uint32_t a, uint32_t Pa, int32_t cla,
-                                                  uint32_t b, uint32_t Pb, int32_t clb) {
-  int32_t ta, tb;
-  uint64_t ma, mb;
-  asm("v_cmp_eq_u32_e64 %1, %5, %6\n\t"
-      "v_cmp_eq_u32_e64 %2, %7, %8\n\t"
-      "v_cndmask_b32_e64 %3, %5, %9, %1\n\t"
-      "v_cndmask_b32_e64 %4, %7, %10, %2\n\t"
-      "v_add3_u32 %0, %3, %4, %0"
-      : "+v"(acc), "=&s"(ma), "=&s"(mb), "=&v"(ta), "=&v"(tb)
-      : "v"(a), "s"(Pa), "v"(b), "s"(Pb), "v"(cla), "v"(clb));
-}
-// x' >= Pb ? cl : low32(x') (class B), mask in an SGPR pair likewise
-__device__ __forceinline__ int32_t clamp_select_f64(double xb, double Pb, int32_t cl) {
-  int32_t r;
-  uint64_t mask;
-  asm("v_cmp_ge_f64_e64 %1, %2, %3\n\tv_cndmask_b32_e64 %0, %4, %5, %1"
-      : "=v"(r), "=&s"(mask)
-      : "v"(xb), "s"(Pb), "v"((uint32_t)__double_as_longlong(xb)), "v"(cl));
-  return r;
+// min(x, p) with p a loaded (wave-uniform) double: asm, because the compiler would first
+// quiet p with a v_max_f64 (it cannot see that 2^52 + P is no signalling NaN)
+__device__ __forceinline__ double min_f64_s(double x, double p) {
+  double d;
+  asm("v_min_f64 %0, %1, %2" : "=v"(d) : "v"(x), "s"(p));
+  return d;
 }
 
 #ifndef KCC_FIT_SPECS_PER_WG
@@ -586,9 +889,6 @@ constexpr int FIT_SPW = KCC_FIT_SPECS_PER_WG;  // specs per 256-thread workgroup
 constexpr int FIT_SPLIT = 256 / FIT_SPW;       // waves per spec group (node chunk split)
 static_assert(FIT_SPW == 64 || FIT_SPW == 128 || FIT_SPW == 256, "FIT_SPW");
 constexpr int FIT_CHUNK_GROUPS = 128;  // 1024 nodes: |sum of contributions| <= 2^30 in i32
-#ifndef KCC_FIT_PAIR_ASM
-#define KCC_FIT_PAIR_ASM 1  // compare/select/add of two nodes in one asm block (0: one per node; same speed, 8 s_nop waits per 8 nodes)
-#endif
 #ifndef KCC_FIT_TARGET_BLOCKS
 #define KCC_FIT_TARGET_BLOCKS 32768
 #endif
@@ -665,11 +965,8 @@ __global__ __launch_bounds__(256) void fit_kernel(
 
   const int cnt = (int)(g1 - g0);
   if (!wave_exact && !wave_b) {
-    // class A: cl through a buffer descriptor over this block's groups: uniform
-    // offsets, no VGPR address (every lane reads the same 16 B)
+    // class A
     const FitGroupA* gbase = fast_a + g0;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)gbase, (short)0, cnt * (int)sizeof(FitGroupA), 0x00020000);
     const f32x2 rcf2 = {sr.rcf, sr.rcf};
     set_round_down();
     for (int cb = 0; cb < cnt; cb += FIT_CHUNK_GROUPS) {
@@ -680,13 +977,9 @@ __global__ __launch_bounds__(256) void fit_kernel(
         int io = gi;
         asm volatile("" : "+s"(io));
         const FitGroupA* g = gbase + io;
-        const int so = io * (int)sizeof(FitGroupA) + (int)offsetof(FitGroupA, cl);
-        const i32x4 c0 = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, so, 0));
-        const i32x4 c1 = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, so + 16, 0));
         const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
         const i32x8 fcv = *reinterpret_cast<const i32x8*>(g->fc);
         const i32x8 Pv = *reinterpret_cast<const i32x8*>(g->P);
-        const int32_t cl[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
         for (int u = 0; u < FIT_GROUP / 2; ++u) {
           const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
@@ -697,15 +990,9 @@ __global__ __launch_bounds__(256) void fit_kernel(
             const int k = 2 * u + h;
             const uint32_t qm = (uint32_t)__double_as_longlong(f64_at(fmv, k) * rm);
             const uint32_t qc = __float_as_uint(h ? q.y : q.x);
-            m3[h] = min(min(qc, qm), (uint32_t)Pv[k]);
+            m3[h] = min(min(qc, qm), (uint32_t)Pv[k]);  // min(findMin(qc, qm), P)
           }
-#if KCC_FIT_PAIR_ASM
-          clamp_select2_acc(acc32, m3[0], (uint32_t)Pv[2 * u], cl[2 * u], m3[1],
-                            (uint32_t)Pv[2 * u + 1], cl[2 * u + 1]);
-#else
-          acc32 += clamp_select(m3[0], (uint32_t)Pv[2 * u], cl[2 * u]) +
-                   clamp_select(m3[1], (uint32_t)Pv[2 * u + 1], cl[2 * u + 1]);
-#endif
+          acc32 += (int32_t)(m3[0] + m3[1]);
         }
       }
       acc += (uint64_t)(int64_t)acc32;
@@ -714,8 +1001,6 @@ __global__ __launch_bounds__(256) void fit_kernel(
   } else if (!wave_exact) {
     // class B (and class-A lanes sharing its wave)
     const FitGroup* gbase = fast_b + g0;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)gbase, (short)0, cnt * (int)sizeof(FitGroup), 0x00020000);
     const double bias = FIT_BIAS;
     set_round_down();
     for (int cb = 0; cb < cnt; cb += FIT_CHUNK_GROUPS) {
@@ -725,13 +1010,9 @@ __global__ __launch_bounds__(256) void fit_kernel(
         int io = gi;
         asm volatile("" : "+s"(io));
         const FitGroup* g = gbase + io;
-        const int so = io * (int)sizeof(FitGroup) + (int)offsetof(FitGroup, cl);
-        const i32x4 c0 = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, so, 0));
-        const i32x4 c1 = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, so + 16, 0));
         const i32x16 fcv = *reinterpret_cast<const i32x16*>(g->fc);
         const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
         const i32x16 Pv = *reinterpret_cast<const i32x16*>(g->Pb);
-        const int32_t cl[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
         for (int u = 0; u < FIT_GROUP / 2; ++u) {
           int32_t x[2];
@@ -740,7 +1021,8 @@ __global__ __launch_bounds__(256) void fit_kernel(
             const int k = 2 * u + h;
             const double qc = __builtin_fma(f64_at(fcv, k), rc, bias);  // 2^52 + floor(fc/c)
             const double qm = __builtin_fma(f64_at(fmv, k), rm, bias);  // 2^52 + floor(fm/m)
-            x[h] = clamp_select_f64(__builtin_fmin(qc, qm), f64_at(Pv, k), cl[k]);
+            const double xb = min_f64_s(__builtin_fmin(qc, qm), f64_at(Pv, k));
+            x[h] = (int32_t)(uint32_t)__double_as_longlong(xb);  // min(findMin(qc, qm), P)
           }
           acc32 += x[0] + x[1];
         }
@@ -847,21 +1129,54 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
-                            SlowNode* slow, int64_t* slow_list, unsigned long long* counters,
-                            int chunk, hipStream_t s) {
+                            SlowNode* slow, int64_t* slow_list, ClampWork cw,
+                            unsigned long long* counters, int chunk, hipStream_t s) {
   if (n_nodes <= 0) return hipSuccess;
-  hipLaunchKernelGGL(node_prep_kernel, dim3(grid_for(fit_groups(n_nodes) * FIT_GROUP, 256, 8192)), dim3(256), 0, s,
+  hipLaunchKernelGGL(node_prep_kernel, dim3(grid_for(fit_groups(n_nodes) * FIT_GROUP, 1024, 2048)),
+                     dim3(1024), (size_t)(12 * CLAMP_LDS_SPECS), s,
                      n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu, used_mem,
-                     fast_a, fast_b, slow, slow_list, counters, (int32_t)chunk);
+                     fast_a, fast_b, slow, slow_list, cw, counters, (int32_t)chunk);
   return hipGetLastError();
 }
 
 hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
-                            SpecPrep sp, int64_t* partial, unsigned long long* counters,
-                            hipStream_t s) {
+                            SpecPrep sp, ClampWork cw, int64_t* partial,
+                            unsigned long long* counters, hipStream_t s) {
   if (n_specs <= 0) return hipSuccess;
   hipLaunchKernelGGL(spec_prep_kernel, dim3(1), dim3(1024), 0, s, n_specs, spec_cpu, spec_mem,
-                     sp, partial, counters);
+                     sp, cw, partial, counters);
+  return hipGetLastError();
+}
+
+hipError_t launch_clamp_specs(int64_t n_specs, SpecPrep sp, ClampWork cw,
+                              const unsigned long long* counters, hipStream_t s) {
+  if (n_specs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(clamp_rank_kernel,
+                     dim3((unsigned)((n_specs + 255) / 256),
+                          (unsigned)((n_specs + CLAMP_RANK_TILE - 1) / CLAMP_RANK_TILE)),
+                     dim3(256), 0, s, sp.rec, cw, n_specs, counters);
+  hipLaunchKernelGGL(clamp_scatter_kernel, dim3(grid_for(clamp_h_cells(n_specs), 256, 2048)),
+                     dim3(256), 0, s, sp.rec, cw, n_specs, counters);
+  return hipGetLastError();
+}
+
+hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
+                              const unsigned long long* counters, int64_t* partial, hipStream_t s) {
+  if (n_specs <= 0 || n_nodes <= 0) return hipSuccess;
+  const int64_t t_max = (n_specs + 63) / 64;
+  hipLaunchKernelGGL(clamp_hcol_kernel, dim3(grid_for(n_specs + 1, 64, 1 << 30)), dim3(64), 0, s,
+                     cw, counters);
+  hipLaunchKernelGGL(clamp_hrow_kernel, dim3((unsigned)(t_max + 1)), dim3(1024), 0, s, cw,
+                     counters);
+  if (n_specs <= CLAMP_LDS_SPECS) {
+    hipLaunchKernelGGL(clamp_partial_kernel, dim3(CLAMP_PARTIAL_WGS), dim3(1024), 0, s, cw,
+                       counters, cw.dpart);
+  } else {
+    hipLaunchKernelGGL(clamp_partial_big_kernel, dim3((unsigned)t_max, CLAMP_SLICES), dim3(64), 0,
+                       s, cw, counters, n_specs, partial);
+  }
+  hipLaunchKernelGGL(clamp_full_kernel, dim3(grid_for(n_specs, 256, 1 << 30)), dim3(256), 0, s, cw,
+                     counters, n_specs, cw.dpart, partial);
   return hipGetLastError();
 }
 

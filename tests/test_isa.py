@@ -1,11 +1,12 @@
 """Static ISA checks of the gfx950 kernels (CPU: hipcc cross-compiles).
 
   - the fit kernel's class-A loop, one 8-node FitGroupA per iteration: 32 dwords of
-    scalar loads (fm, fc, P), two uniform 16-B buffer loads (cl), exactly
+    scalar loads (fm, fc, P) and no vector memory access, exactly
     bench.FIT_VALU_PER_NODE_WAVE VALU instructions per node (the VALU-roofline
-    accounting of bench.py): packed f32 and f64 multiplies, min3, compare, select, add
-    — no division, no conversion, no correction step, and no select reading VCC;
-  - the class-B loop: biased f64 FMAs, 5.5 VALU instructions per node;
+    accounting of bench.py): packed f32 and f64 multiplies, min3, add — no division,
+    no conversion, no correction step, no compare/select (the clamp is the clamp
+    correction's job);
+  - the class-B loop: biased f64 FMAs, 4.5 VALU instructions per node;
   - both loops run inside a round-toward--inf window of the MODE register (our two
     s_setreg writes each), and the compiler inserts no mode switch of its own;
   - f32 and f64 denormals are enabled in the kernel descriptor (class A reads
@@ -54,9 +55,7 @@ GROUP = 8  # nodes per FitGroup = per loop iteration
 
 def check_loads(lines, dwords):
     assert sum(WIDTH[ln.split()[0]] for ln in lines if ln.startswith("s_load_dword")) == dwords
-    vmem = [ln for ln in lines if ln.startswith(("global_load", "flat_load", "buffer_load"))]
-    assert len(vmem) == 2 and all(ln.startswith("buffer_load_dwordx4") and ", off," in ln
-                                  for ln in vmem)  # cl: uniform address, no VGPR offset
+    assert not [ln for ln in lines if ln.startswith(("global_", "flat_", "buffer_", "ds_"))]
 
 
 def test_fit_class_a_loop(asm):
@@ -69,21 +68,19 @@ def test_fit_class_a_loop(asm):
     ops = [ln.split()[0] for ln in valu]
     assert ops.count("v_pk_mul_f32") == GROUP // 2 and ops.count("v_mul_f64") == GROUP
     assert ops.count("v_min3_u32") == GROUP and ops.count("v_add3_u32") == GROUP // 2
-    assert ops.count("v_cmp_eq_u32_e64") == GROUP and ops.count("v_cndmask_b32_e64") == GROUP
-    assert not any("vcc" in ln for ln in valu)
-    assert not any(o.startswith(("v_mad", "v_cvt", "v_fma", "v_rcp", "v_div")) for o in ops)
+    assert not any(o.startswith(("v_mad", "v_cvt", "v_fma", "v_rcp", "v_div", "v_cmp",
+                                 "v_cndmask")) for o in ops)
 
 
 def test_fit_class_b_loop(asm):
     lines = loop_of(kernel_body(asm, "fit_kernel"), "v_fma_f64")
     check_loads(lines, GROUP * 6)  # fc, fm, Pb (f64) per node
     valu = [ln for ln in lines if ln.startswith("v_")]
-    assert len(valu) / GROUP == 5.5
+    assert len(valu) / GROUP == 4.5
     ops = [ln.split()[0] for ln in valu]
-    assert ops.count("v_fma_f64") == 2 * GROUP and ops.count("v_min_f64") == GROUP
-    assert ops.count("v_cmp_ge_f64_e64") == GROUP and ops.count("v_cndmask_b32_e64") == GROUP
-    assert not any("vcc" in ln for ln in valu)
-    assert not any(o.startswith(("v_cvt", "v_max", "v_mul")) for o in ops)
+    assert ops.count("v_fma_f64") == 2 * GROUP and ops.count("v_min_f64") == 2 * GROUP
+    assert ops.count("v_add3_u32") == GROUP // 2
+    assert not any(o.startswith(("v_cvt", "v_max", "v_mul", "v_cmp", "v_cndmask")) for o in ops)
 
 
 def test_fit_round_mode_windows(asm):
