@@ -141,8 +141,14 @@ struct ClampWork {
 };
 inline int64_t clamp_h_cells(int64_t S) { return (S / 64 + 2) * (S + 1); }
 // up to this many normal specs the sorted requests / accumulators live in LDS
-constexpr int64_t CLAMP_LDS_SPECS = 4096;
-constexpr int64_t CLAMP_PARTIAL_ROWS = 64;
+#ifndef KCC_CLAMP_LDS_SPECS
+#define KCC_CLAMP_LDS_SPECS 4096
+#endif
+#ifndef KCC_CLAMP_PARTIAL_ROWS
+#define KCC_CLAMP_PARTIAL_ROWS 256
+#endif
+constexpr int64_t CLAMP_LDS_SPECS = KCC_CLAMP_LDS_SPECS;
+constexpr int64_t CLAMP_PARTIAL_ROWS = KCC_CLAMP_PARTIAL_ROWS;
 
 // counters (CNT_*): exact-path (node, spec) pairs, class-B specs, and per node chunk
 // of a pipelined call (kcc_capacity_partial_async) the rows in that chunk's slow_list.

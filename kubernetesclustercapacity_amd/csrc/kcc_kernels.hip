@@ -345,7 +345,13 @@ __device__ __forceinline__ uint32_t upper_bound_count(const T* __restrict__ a, i
 // the others get all-zero fields (contribute exactly 0 on the fast paths) and are
 // appended to slow_list for the exact 64-bit path.  Covers the padding of the last
 // group too (zero fields, not listed).
-__global__ __launch_bounds__(1024) void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_cpu,
+#ifndef KCC_NODE_PREP_BLOCK
+#define KCC_NODE_PREP_BLOCK 1024
+#endif
+#ifndef KCC_NODE_PREP_GRID
+#define KCC_NODE_PREP_GRID 2048  // workgroups at most (each fills its LDS search tables once)
+#endif
+__global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_cpu,
                                  const int64_t* __restrict__ alloc_mem,
                                  const int64_t* __restrict__ alloc_pods,
                                  const int64_t* __restrict__ pod_count,
@@ -730,6 +736,7 @@ __global__ __launch_bounds__(1024) void clamp_hrow_kernel(ClampWork cw,
 // the entry's group) and writes its row of dpart[CLAMP_PARTIAL_WGS][nN]; clamp_full
 // sums the rows.  nN <= CLAMP_LDS_SPECS (else clamp_partial_big_kernel).
 constexpr int CLAMP_PARTIAL_WGS = (int)CLAMP_PARTIAL_ROWS;
+static_assert(CLAMP_PARTIAL_WGS % 64 == 0, "clamp_full sums the rows in 8 splits, 8 at a time");
 __global__ __launch_bounds__(1024) void clamp_partial_kernel(ClampWork cw,
                                                              const unsigned long long* __restrict__ counters,
                                                              int64_t* __restrict__ dpart) {
@@ -754,8 +761,10 @@ __global__ __launch_bounds__(1024) void clamp_partial_kernel(ClampWork cw,
     const bool in = j < j1;
     const uint32_t key_v = in ? cw.pkey[j] : 0u, bnd_v = in ? cw.pb[j] : 0u;
     const int32_t w_v = in ? cw.pw[j] : 0;
-    const int cnt = (int)(j1 - jb < 64 ? j1 - jb : 64);
-    for (int k = 0; k < cnt; ++k) {
+    const int cnt = (int)(j1 - jb < 64 ? j1 - jb : 64);  // entries past cnt are r = 0 no-ops
+#pragma unroll 4
+    for (int k = 0; k < 64; ++k) {
+      if (k >= cnt) break;
       const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)key_v, k);
       const uint32_t bnd = (uint32_t)__builtin_amdgcn_readlane((int)bnd_v, k);
       const int32_t w = __builtin_amdgcn_readlane(w_v, k);
@@ -809,20 +818,34 @@ __global__ __launch_bounds__(64) void clamp_partial_big_kernel(ClampWork cw,
 }
 
 // partial[p] -= D(p) = HS[g + 1][m_less + 1] + Σ_k dpart[k][q] for the normal specs of
-// clamp-free waves (q = the spec's c-rank, g = q / 64)
-__global__ void clamp_full_kernel(ClampWork cw, const unsigned long long* __restrict__ counters,
-                                  int64_t S, const int64_t* __restrict__ dpart,
-                                  int64_t* __restrict__ partial) {
+// clamp-free waves (q = the spec's c-rank, g = q / 64).  Grid (nN / 64, CLAMP_FULL_SPLIT):
+// split y sums dpart rows [y * R, (y + 1) * R), split 0 also the H term; one atomic each.
+constexpr int CLAMP_FULL_SPLIT = 8;
+__global__ __launch_bounds__(64) void clamp_full_kernel(ClampWork cw,
+                                                        const unsigned long long* __restrict__ counters,
+                                                        int64_t S, const int64_t* __restrict__ dpart,
+                                                        int64_t* __restrict__ partial) {
   const int64_t nN = clamp_n_normal(counters);
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // c-rank
   if (q >= nN) return;
-  const int64_t T = (nN + 63) / 64, w = nN + 1;
-  const int64_t g1 = (q >> 6) + 1, b1 = (int64_t)cw.m_less[q] + 1;
   const int32_t p = cw.dperm[q];
   if (p >= clamp_n_pure(nN, S)) return;
-  uint64_t d = (g1 <= T && b1 <= nN) ? (uint64_t)cw.H[g1 * w + b1] : 0ull;
-  if (nN <= CLAMP_LDS_SPECS)
-    for (int k = 0; k < CLAMP_PARTIAL_WGS; ++k) d += (uint64_t)dpart[(int64_t)k * nN + q];
+  uint64_t d = 0;
+  if (blockIdx.y == 0) {
+    const int64_t T = (nN + 63) / 64, w = nN + 1;
+    const int64_t g1 = (q >> 6) + 1, b1 = (int64_t)cw.m_less[q] + 1;
+    if (g1 <= T && b1 <= nN) d = (uint64_t)cw.H[g1 * w + b1];
+  }
+  if (nN <= CLAMP_LDS_SPECS) {  // the partial kernel's per-workgroup rows, 8 loads in flight
+    constexpr int R = CLAMP_PARTIAL_WGS / CLAMP_FULL_SPLIT;
+    uint64_t part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = (int)blockIdx.y * R; k < ((int)blockIdx.y + 1) * R; k += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) part[u] += (uint64_t)dpart[(int64_t)(k + u) * nN + q];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) d += part[u];
+  }
   if (d) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[p]), 0ull - d);
 }
 
@@ -1132,8 +1155,10 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             SlowNode* slow, int64_t* slow_list, ClampWork cw,
                             unsigned long long* counters, int chunk, hipStream_t s) {
   if (n_nodes <= 0) return hipSuccess;
-  hipLaunchKernelGGL(node_prep_kernel, dim3(grid_for(fit_groups(n_nodes) * FIT_GROUP, 1024, 2048)),
-                     dim3(1024), (size_t)(12 * CLAMP_LDS_SPECS), s,
+  hipLaunchKernelGGL(node_prep_kernel,
+                     dim3(grid_for(fit_groups(n_nodes) * FIT_GROUP, KCC_NODE_PREP_BLOCK,
+                                   KCC_NODE_PREP_GRID)),
+                     dim3(KCC_NODE_PREP_BLOCK), (size_t)(12 * CLAMP_LDS_SPECS), s,
                      n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu, used_mem,
                      fast_a, fast_b, slow, slow_list, cw, counters, (int32_t)chunk);
   return hipGetLastError();
@@ -1175,8 +1200,8 @@ hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
     hipLaunchKernelGGL(clamp_partial_big_kernel, dim3((unsigned)t_max, CLAMP_SLICES), dim3(64), 0,
                        s, cw, counters, n_specs, partial);
   }
-  hipLaunchKernelGGL(clamp_full_kernel, dim3(grid_for(n_specs, 256, 1 << 30)), dim3(256), 0, s, cw,
-                     counters, n_specs, cw.dpart, partial);
+  hipLaunchKernelGGL(clamp_full_kernel, dim3(grid_for(n_specs, 64, 1 << 30), CLAMP_FULL_SPLIT),
+                     dim3(64), 0, s, cw, counters, n_specs, cw.dpart, partial);
   return hipGetLastError();
 }
 
