@@ -60,8 +60,9 @@ struct Dev {
   // workspace of the *_async entry points
   DevBuf wave_node, fast_a, fast_b, slow, slow_list, srec, sperm, counters;
   // clamp correction (kcc::ClampWork)
-  DevBuf c_rank, c_cs, c_ms, c_mless, c_dperm, c_H, c_pkey, c_pb, c_pw, c_dpart;
+  DevBuf c_rank, c_cs, c_ms, c_mless, c_dperm, c_H, c_pcount, c_pkey, c_pb, c_pw, c_dpart;
   int64_t last_pairs = 0;  // node x spec pairs of the last fit_prepare on this device
+  int64_t h_stride = 0;    // cells per copy of the clamp table H in c_H
   int64_t prep_nodes = -1, prep_specs = -1;  // sizes the workspace was last prepared for
   // staging of the host-array entry points
   DevBuf ptr, cpu, mem, cpul, meml, used_cpu, used_mem, lim_cpu, lim_mem;
@@ -189,12 +190,27 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.c_ms, 8 * S));
   KCC_HIP(ctx, ensure(dv.c_mless, 4 * S));
   KCC_HIP(ctx, ensure(dv.c_dperm, 4 * S));
-  KCC_HIP(ctx, ensure(dv.c_H, 8 * (size_t)kcc::clamp_h_cells((int64_t)S)));
-  KCC_HIP(ctx, ensure(dv.c_pkey, 4 * N));
-  KCC_HIP(ctx, ensure(dv.c_pb, 4 * N));
-  KCC_HIP(ctx, ensure(dv.c_pw, 4 * N));
+  KCC_HIP(ctx, ensure(dv.c_H, 8 * (size_t)kcc::H_COPIES * (size_t)kcc::clamp_h_cells((int64_t)S)));
+  dv.h_stride = kcc::clamp_h_cells((int64_t)S);
+  const size_t NS = (N + kcc::PLIST_SLOT - 1) / kcc::PLIST_SLOT * kcc::PLIST_SLOT;  // whole slots
+  KCC_HIP(ctx, ensure(dv.c_pcount, 4 * (NS / kcc::PLIST_SLOT + 1)));
+  KCC_HIP(ctx, ensure(dv.c_pkey, 4 * NS));
+  KCC_HIP(ctx, ensure(dv.c_pb, 4 * NS));
+  KCC_HIP(ctx, ensure(dv.c_pw, 4 * NS));
   KCC_HIP(ctx, ensure(dv.c_dpart, 8 * (size_t)kcc::CLAMP_PARTIAL_ROWS * S));
   return KCC_OK;
+}
+
+kcc::ClampWork clamp_of(Dev& dv);
+// the clamp workspace seen by the node_prep of a node range starting at `lo` (a
+// multiple of PLIST_SLOT): its plist slots are the range's own
+kcc::ClampWork clamp_at(Dev& dv, int64_t lo) {
+  kcc::ClampWork cw = clamp_of(dv);
+  cw.pcount += lo / kcc::PLIST_SLOT;
+  cw.pkey += lo;
+  cw.pb += lo;
+  cw.pw += lo;
+  return cw;
 }
 
 kcc::ClampWork clamp_of(Dev& dv) {
@@ -205,10 +221,12 @@ kcc::ClampWork clamp_of(Dev& dv) {
   cw.m_less = as<uint32_t>(dv.c_mless);
   cw.dperm = as<int32_t>(dv.c_dperm);
   cw.H = as<int64_t>(dv.c_H);
+  cw.pcount = as<uint32_t>(dv.c_pcount);
   cw.pkey = as<uint32_t>(dv.c_pkey);
   cw.pb = as<uint32_t>(dv.c_pb);
   cw.pw = as<int32_t>(dv.c_pw);
   cw.dpart = as<int64_t>(dv.c_dpart);
+  cw.h_stride = dv.h_stride;
   return cw;
 }
 
@@ -293,8 +311,9 @@ hipError_t prof_event(Dev& dv, hipEvent_t* ev) {
   return hipEventCreate(ev);
 }
 
-// Chunk boundaries: node ranges of ~equal node count, multiples of FIT_GROUP (the fit's
-// node groups never straddle two chunks); at least `min_nodes` nodes per chunk.
+// Chunk boundaries: node ranges of ~equal node count, multiples of PLIST_SLOT (a multiple
+// of FIT_GROUP: neither the fit's node groups nor the clamp correction's plist slots
+// straddle two chunks); at least `min_nodes` nodes per chunk.
 int plan_chunks(int64_t n_nodes, int want, int64_t min_nodes, std::vector<int64_t>& lo,
                 std::vector<int64_t>& hi) {
   int k = want;
@@ -305,7 +324,7 @@ int plan_chunks(int64_t n_nodes, int want, int64_t min_nodes, std::vector<int64_
   hi.assign(k, 0);
   for (int c = 0; c < k; ++c) {
     lo[c] = c == 0 ? 0 : hi[c - 1];
-    hi[c] = c == k - 1 ? n_nodes : (n_nodes * (c + 1) / k) / kcc::FIT_GROUP * kcc::FIT_GROUP;
+    hi[c] = c == k - 1 ? n_nodes : (n_nodes * (c + 1) / k) / kcc::PLIST_SLOT * kcc::PLIST_SLOT;
     if (hi[c] < lo[c]) hi[c] = lo[c];
   }
   return k;
@@ -403,7 +422,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                        as<kcc::FitGroupA>(dv.fast_a) + lo[c] / kcc::FIT_GROUP,
                                        as<kcc::FitGroup>(dv.fast_b) + lo[c] / kcc::FIT_GROUP,
                                        as<kcc::SlowNode>(dv.slow) + lo[c],
-                                       as<int64_t>(dv.slow_list) + lo[c], clamp_of(dv),
+                                       as<int64_t>(dv.slow_list) + lo[c], clamp_at(dv, lo[c]),
                                        as<unsigned long long>(dv.counters), c, s));
     ProfPair pp{};
     if (dv.prof_on) {
@@ -602,7 +621,7 @@ void kcc_destroy(kcc_ctx* ctx) {
     (void)hipSetDevice(dv.device);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
     DevBuf* bufs[] = {&dv.c_rank, &dv.c_cs, &dv.c_ms, &dv.c_mless, &dv.c_dperm, &dv.c_H,
-                      &dv.c_pkey, &dv.c_pb, &dv.c_pw, &dv.c_dpart,
+                      &dv.c_pcount, &dv.c_pkey, &dv.c_pb, &dv.c_pw, &dv.c_dpart,
                       &dv.wave_node, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
                       &dv.sperm,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,

@@ -133,13 +133,20 @@ struct ClampWork {
   int64_t* ms;       // [S] normal specs' memory requests in m-rank order
   uint32_t* m_less;  // [S] by c-rank: #normal specs with a smaller memory request
   int32_t* dperm;    // [S] c-rank -> internal position
-  int64_t* H;        // [(S/64 + 2) * (S + 1)] (T+1) x (nN+1) clamp weights, then their 2-D suffix sums
+  int64_t* H;        // [H_COPIES][clamp_h_cells(S)]: (T+1) x (nN+1) clamp weights, one copy
+                     // per XCD (node_prep's atomics spread over 8x the cache lines); copy 0
+                     // then holds the 2-D suffix sums of their total
+  // plist: one slot of PLIST_SLOT entries per PLIST_SLOT consecutive nodes (node_prep
+  // fills a slot's first pcount[slot] entries: no shared counter)
+  uint32_t* pcount;  // [N / PLIST_SLOT + 1]
   uint32_t* pkey;    // [N] plist: G << 6 | r
   uint32_t* pb;      // [N] plist: b (m-rank bound)
   int32_t* pw;       // [N] plist: w
   int64_t* dpart;    // [CLAMP_PARTIAL_ROWS * S] per-workgroup partial-group sums
+  int64_t h_stride;  // cells per H copy (clamp_h_cells(S) of the workspace)
 };
 inline int64_t clamp_h_cells(int64_t S) { return (S / 64 + 2) * (S + 1); }
+constexpr int H_COPIES = 8;
 // up to this many normal specs the sorted requests / accumulators live in LDS
 #ifndef KCC_CLAMP_LDS_SPECS
 #define KCC_CLAMP_LDS_SPECS 4096
@@ -148,6 +155,7 @@ inline int64_t clamp_h_cells(int64_t S) { return (S / 64 + 2) * (S + 1); }
 #define KCC_CLAMP_PARTIAL_ROWS 256
 #endif
 constexpr int64_t CLAMP_LDS_SPECS = KCC_CLAMP_LDS_SPECS;
+constexpr int64_t PLIST_SLOT = 1024;  // = node_prep's workgroup size
 constexpr int64_t CLAMP_PARTIAL_ROWS = KCC_CLAMP_PARTIAL_ROWS;
 
 // counters (CNT_*): exact-path (node, spec) pairs, class-B specs, and per node chunk
@@ -170,6 +178,7 @@ hipError_t launch_clamp_specs(int64_t n_specs, SpecPrep sp, ClampWork cw,
                               const unsigned long long* counters, hipStream_t s);
 // H -> its 2-D suffix sums; partial[s] -= D_s for the normal specs of clamp-free waves
 // (after every node_prep of the call, before the all-reduce)
+// n_nodes: all nodes of the call (the plist slots of every node_prep launch)
 hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
                               const unsigned long long* counters, int64_t* partial, hipStream_t s);
 

@@ -329,6 +329,22 @@ __device__ __forceinline__ int64_t clamp_n_pure(int64_t nN, int64_t S) {
 }
 
 // #{k < n : a[k] <= v} for a sorted ascending (binary search, n <= 2^31)
+// #{k < 4096 : a[k] <= v} for a sorted ascending (8-ary: after the step of width s the
+// answer lies in [lo, lo + s])
+template <class T>
+__device__ __forceinline__ uint32_t search8_4096(const T* a, T v) {
+  static_assert(CLAMP_LDS_SPECS == 4096, "search8_4096 covers 8^4 entries");
+  uint32_t lo = 0;
+#pragma unroll
+  for (uint32_t s = 512; s >= 1; s /= 8) {
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t j = 1; j < 8; ++j) cnt += a[lo + j * s - 1] <= v ? 1u : 0u;
+    lo += cnt * s;
+  }
+  return lo;
+}
+
 template <class T>
 __device__ __forceinline__ uint32_t upper_bound_count(const T* __restrict__ a, int64_t n, T v) {
   int64_t lo = 0, hi = n;
@@ -345,9 +361,7 @@ __device__ __forceinline__ uint32_t upper_bound_count(const T* __restrict__ a, i
 // the others get all-zero fields (contribute exactly 0 on the fast paths) and are
 // appended to slow_list for the exact 64-bit path.  Covers the padding of the last
 // group too (zero fields, not listed).
-#ifndef KCC_NODE_PREP_BLOCK
-#define KCC_NODE_PREP_BLOCK 1024
-#endif
+#define KCC_NODE_PREP_BLOCK 1024  // = PLIST_SLOT
 #ifndef KCC_NODE_PREP_GRID
 #define KCC_NODE_PREP_GRID 2048  // workgroups at most (each fills its LDS search tables once)
 #endif
@@ -367,6 +381,8 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   const bool want_b = counters[CNT_SPECS_B] != 0;  // written by spec_prep (same stream)
   const int64_t nN = clamp_n_normal(counters);     // normal specs (clamp correction)
   const int64_t T = (nN + 63) / 64, hw = nN + 1;
+  // this workgroup's copy of H: workgroups are dealt round-robin over the 8 XCDs
+  int64_t* Hc = cw.H + (int64_t)(blockIdx.x % H_COPIES) * cw.h_stride;
   // the sorted spec requests of the binary searches, in LDS when they fit: c clamped
   // to 2^23 (> every U = fc / P, fc < 2^23) as u32, m as i64
   extern __shared__ __attribute__((aligned(16))) unsigned char np_lds[];
@@ -377,15 +393,20 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   const uint32_t cmin = nN > 0 ? (cw.cs[0] < FAST_FC_MAX ? (uint32_t)cw.cs[0] : (uint32_t)FAST_FC_MAX)
                                : 0xffffffffu;
   const int64_t mmin = nN > 0 ? cw.ms[0] : INT64_MAX;
+#ifndef KCC_DIAG_NO_FILL  // diagnostic timing build only: results are wrong
   if (lds) {
-    for (int64_t k = threadIdx.x; k < nN; k += blockDim.x) {
-      const uint64_t c = cw.cs[k];
-      cs_l[k] = c < FAST_FC_MAX ? (uint32_t)c : (uint32_t)FAST_FC_MAX;
-      ms_l[k] = cw.ms[k];
+#else
+  if (false) {
+#endif
+    for (int64_t k = threadIdx.x; k < CLAMP_LDS_SPECS; k += blockDim.x) {  // padded: +inf
+      const uint64_t c = k < nN ? cw.cs[k] : ~0ull;
+      cs_l[k] = c < FAST_FC_MAX ? (uint32_t)c : 0xffffffffu;
+      ms_l[k] = k < nN ? cw.ms[k] : INT64_MAX;
     }
   }
   __syncthreads();
-  __shared__ unsigned long long wcount[16], wg_base;
+  __shared__ unsigned long long wcount[16];
+  static_assert(KCC_NODE_PREP_BLOCK == PLIST_SLOT, "one plist slot per workgroup iteration");
   const int wv = threadIdx.x >> 6;
   // block-uniform trip count (the plist append below synchronises the workgroup)
   for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n_pad; i0 += stride) {
@@ -452,14 +473,20 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
           L = U % (uint32_t)(nN + 1);
           b = (uint32_t)(V % (nN + 1));
 #else
-          L = lds ? upper_bound_count(cs_l, nN, U) : upper_bound_count(cw.cs, nN, (uint64_t)U);
-          b = lds ? upper_bound_count(ms_l, nN, V) : upper_bound_count(cw.ms, nN, V);
+          if (lds) {  // 8-ary searches over the +inf-padded 4096-entry tables: 4 steps of
+                      // 7 independent LDS reads each (a binary search chains 12)
+            L = search8_4096(cs_l, U);
+            b = search8_4096(ms_l, V);
+          } else {
+            L = upper_bound_count(cw.cs, nN, (uint64_t)U);
+            b = upper_bound_count(cw.ms, nN, V);
+          }
 #endif
         }
         if (L > 0 && b > 0 && w != 0) {
           const uint32_t G = L >> 6, r = L & 63u;
 #ifndef KCC_DIAG_NO_H_ATOMIC  // diagnostic timing build only: results are wrong
-          if (G > 0) atomic_add_u64(reinterpret_cast<uint64_t*>(&cw.H[G * hw + b]), (uint64_t)w);
+          if (G > 0) atomic_add_u64(reinterpret_cast<uint64_t*>(&Hc[G * hw + b]), (uint64_t)w);
 #endif
           in_plist = r != 0;
           key = G << 6 | r;
@@ -471,28 +498,29 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       uint64_t v = always ? (uint64_t)w : 0ull;
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-      if (lane == 0 && v) atomic_add_u64(reinterpret_cast<uint64_t*>(&cw.H[T * hw + nN]), v);
+      if (lane == 0 && v) atomic_add_u64(reinterpret_cast<uint64_t*>(&Hc[T * hw + nN]), v);
     }
-    {  // plist append: one atomic per workgroup (a per-wave atomic on one counter
-       // serialises ~15k waves at C4)
+#ifdef KCC_DIAG_NO_PLIST  // diagnostic timing build only: results are wrong
+    in_plist = false;
+#endif
+    {  // plist: this workgroup's rows own slot i0 / PLIST_SLOT (no shared counter)
       const unsigned long long pm = __ballot(in_plist);
       if (lane == 0) wcount[wv] = __popcll(pm);
       __syncthreads();
       if (threadIdx.x == 0) {
         unsigned long long tot = 0;
         for (int k = 0; k < (int)(blockDim.x >> 6); ++k) tot += wcount[k];
-        wg_base = tot ? atomicAdd(&counters[CNT_PLIST], tot) : 0ull;
+        cw.pcount[i0 / PLIST_SLOT] = (uint32_t)tot;
       }
-      __syncthreads();
       if (in_plist) {
-        unsigned long long j = wg_base;
-        for (int k = 0; k < wv; ++k) j += wcount[k];
+        int64_t j = i0;  // the slot's first entry (i0 is a multiple of PLIST_SLOT)
+        for (int k = 0; k < wv; ++k) j += (int64_t)wcount[k];
         j += __popcll(pm & ((1ull << lane) - 1ull));
         cw.pkey[j] = key;
         cw.pb[j] = bnd;
         cw.pw[j] = (int32_t)w;
       }
-      __syncthreads();  // wcount / wg_base are reused by the next iteration
+      __syncthreads();  // wcount is reused by the next iteration
     }
     const unsigned long long b = __ballot(valid && !ok);
     if (b) {
@@ -664,6 +692,10 @@ __global__ void clamp_scatter_kernel(const SpecRec* __restrict__ rec, ClampWork 
   const int64_t cells = (T + 1) * (nN + 1);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells || i < nN; i += stride) {
+    if (i < cells) {
+#pragma unroll
+      for (int k = 1; k < H_COPIES; ++k) cw.H[k * cw.h_stride + i] = 0;
+    }
     if (i < nN) {
       const uint32_t d = cw.rank[i];
       cw.cs[d] = rec[i].c;
@@ -675,8 +707,21 @@ __global__ void clamp_scatter_kernel(const SpecRec* __restrict__ rec, ClampWork 
   }
 }
 
-// 2-D suffix sums of H, step 1: down each column (G from T to 0), one thread per
-// column, eight rows' loads in flight at a time
+// 2-D suffix sums of H, step 0: the XCD copies summed into copy 0 (all cells in parallel)
+__global__ void clamp_hsum_kernel(ClampWork cw, const unsigned long long* __restrict__ counters) {
+  const int64_t nN = clamp_n_normal(counters);
+  const int64_t cells = ((nN + 63) / 64 + 1) * (nN + 1);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells; i += stride) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int c = 0; c < H_COPIES; ++c) v += (uint64_t)cw.H[c * cw.h_stride + i];
+    cw.H[i] = (int64_t)v;
+  }
+}
+
+// step 1: down each column (G from T to 0), one thread per column, eight rows' loads
+// in flight at a time
 __global__ __launch_bounds__(64) void clamp_hcol_kernel(ClampWork cw,
                                                         const unsigned long long* __restrict__ counters) {
   const int64_t nN = clamp_n_normal(counters);
@@ -736,10 +781,11 @@ __global__ __launch_bounds__(1024) void clamp_hrow_kernel(ClampWork cw,
 // the entry's group) and writes its row of dpart[CLAMP_PARTIAL_WGS][nN]; clamp_full
 // sums the rows.  nN <= CLAMP_LDS_SPECS (else clamp_partial_big_kernel).
 constexpr int CLAMP_PARTIAL_WGS = (int)CLAMP_PARTIAL_ROWS;
+constexpr int CLAMP_PARTIAL_MAX_SLOTS = 1024;  // per workgroup (n_nodes <= 256 x 1024 x 1024)
 static_assert(CLAMP_PARTIAL_WGS % 64 == 0, "clamp_full sums the rows in 8 splits, 8 at a time");
 __global__ __launch_bounds__(1024) void clamp_partial_kernel(ClampWork cw,
                                                              const unsigned long long* __restrict__ counters,
-                                                             int64_t* __restrict__ dpart) {
+                                                             int64_t n_nodes, int64_t* __restrict__ dpart) {
   const int64_t nN = clamp_n_normal(counters);
   if (nN == 0 || nN > CLAMP_LDS_SPECS) return;
   __shared__ uint32_t ml_l[CLAMP_LDS_SPECS];
@@ -752,22 +798,36 @@ __global__ __launch_bounds__(1024) void clamp_partial_kernel(ClampWork cw,
   const int lane = threadIdx.x & 63;
   const int32_t wv = __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6));
   const int32_t nw = (int32_t)(blockDim.x >> 6);
-  const int64_t npl = (int64_t)counters[CNT_PLIST];
-  const int64_t j0 = npl * blockIdx.x / CLAMP_PARTIAL_WGS, j1 = npl * (blockIdx.x + 1) / CLAMP_PARTIAL_WGS;
-  // 64 entries per wave-iteration by one coalesced load each, then walked lane by lane
-  // from registers (v_readlane): no memory latency inside the inner loop
-  for (int64_t jb = j0 + (int64_t)wv * 64; jb < j1; jb += (int64_t)nw * 64) {
-    const int64_t j = jb + lane;
-    const bool in = j < j1;
+  // this workgroup's plist slots [s0, s1), their entries taken as one sequence in
+  // 64-entry batches by the workgroup's waves (slot counts prefix-summed in LDS)
+  __shared__ uint32_t spre[CLAMP_PARTIAL_MAX_SLOTS + 1];
+  const int64_t n_slots = (n_nodes + PLIST_SLOT - 1) / PLIST_SLOT;
+  const int64_t s0 = n_slots * blockIdx.x / CLAMP_PARTIAL_WGS, s1 = n_slots * (blockIdx.x + 1) / CLAMP_PARTIAL_WGS;
+  const int ns = (int)(s1 - s0);  // <= CLAMP_PARTIAL_MAX_SLOTS (host-checked)
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (int k = 0; k < ns; ++k) {
+      spre[k] = run;
+      run += cw.pcount[s0 + k];
+    }
+    spre[ns] = run;
+  }
+  __syncthreads();
+  const int64_t n_ent = spre[ns];
+  for (int64_t e0 = (int64_t)wv * 64; e0 < n_ent; e0 += (int64_t)nw * 64) {
+    const int64_t e = e0 + lane;
+    int k = 0;  // slot of entry e (lanes of one batch span at most a few slots)
+    while (k + 1 < ns && (int64_t)spre[k + 1] <= e) ++k;
+    const bool in = e < n_ent;
+    const int64_t j = (s0 + k) * PLIST_SLOT + (e - (int64_t)spre[k]);
     const uint32_t key_v = in ? cw.pkey[j] : 0u, bnd_v = in ? cw.pb[j] : 0u;
     const int32_t w_v = in ? cw.pw[j] : 0;
-    const int cnt = (int)(j1 - jb < 64 ? j1 - jb : 64);  // entries past cnt are r = 0 no-ops
-#pragma unroll 4
-    for (int k = 0; k < 64; ++k) {
-      if (k >= cnt) break;
-      const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)key_v, k);
-      const uint32_t bnd = (uint32_t)__builtin_amdgcn_readlane((int)bnd_v, k);
-      const int32_t w = __builtin_amdgcn_readlane(w_v, k);
+    const int cnt = (int)(n_ent - e0 < 64 ? n_ent - e0 : 64);
+    // 64 entries by one coalesced load each, walked lane by lane from registers
+    for (int kk = 0; kk < cnt; ++kk) {
+      const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)key_v, kk);
+      const uint32_t bnd = (uint32_t)__builtin_amdgcn_readlane((int)bnd_v, kk);
+      const int32_t w = __builtin_amdgcn_readlane(w_v, kk);
       const int64_t q = (int64_t)(key >> 6) * 64 + lane;
       if ((uint32_t)lane < (key & 63u) && ml_l[q] < bnd)
         atomicAdd(&acc_l[q], (unsigned long long)(int64_t)w);
@@ -784,7 +844,8 @@ __global__ __launch_bounds__(1024) void clamp_partial_kernel(ClampWork cw,
 constexpr int CLAMP_SLICES = 512;
 __global__ __launch_bounds__(64) void clamp_partial_big_kernel(ClampWork cw,
                                                                const unsigned long long* __restrict__ counters,
-                                                               int64_t S, int64_t* __restrict__ partial) {
+                                                               int64_t S, int64_t n_nodes,
+                                                               int64_t* __restrict__ partial) {
   const int64_t nN = clamp_n_normal(counters);
   if (nN <= CLAMP_LDS_SPECS) return;
   const int64_t T = (nN + 63) / 64;
@@ -794,21 +855,24 @@ __global__ __launch_bounds__(64) void clamp_partial_big_kernel(ClampWork cw,
   const int64_t q = g * 64 + lane;
   const bool valid = q < nN;
   const uint32_t ml = valid ? cw.m_less[q] : 0xffffffffu;
-  const int64_t npl = (int64_t)counters[CNT_PLIST];
-  const int64_t j0 = npl * blockIdx.y / CLAMP_SLICES, j1 = npl * (blockIdx.y + 1) / CLAMP_SLICES;
+  const int64_t n_slots = (n_nodes + PLIST_SLOT - 1) / PLIST_SLOT;
+  const int64_t s0 = n_slots * blockIdx.y / CLAMP_SLICES, s1 = n_slots * (blockIdx.y + 1) / CLAMP_SLICES;
   uint64_t acc = 0;
-  for (int64_t jb = j0; jb < j1; jb += 64) {
-    const int64_t j = jb + lane;
-    const uint32_t key = j < j1 ? cw.pkey[j] : 0xffffffffu;
-    uint64_t mask = __ballot((int64_t)(key >> 6) == g);
-    while (mask) {
-      const int k = __builtin_ctzll(mask);
-      mask &= mask - 1;
-      const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)key, k) & 63u;
-      const int64_t jj = jb + k;
-      const uint32_t bnd = cw.pb[jj];
-      const int32_t w = cw.pw[jj];
-      acc += ((uint32_t)lane < r && ml < bnd) ? (uint64_t)(int64_t)w : 0ull;
+  for (int64_t sl = s0; sl < s1; ++sl) {
+    const int64_t j1 = sl * PLIST_SLOT + (int64_t)cw.pcount[sl];
+    for (int64_t jb = sl * PLIST_SLOT; jb < j1; jb += 64) {
+      const int64_t j = jb + lane;
+      const uint32_t key = j < j1 ? cw.pkey[j] : 0xffffffffu;
+      uint64_t mask = __ballot((int64_t)(key >> 6) == g);
+      while (mask) {
+        const int k = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)key, k) & 63u;
+        const int64_t jj = jb + k;
+        const uint32_t bnd = cw.pb[jj];
+        const int32_t w = cw.pw[jj];
+        acc += ((uint32_t)lane < r && ml < bnd) ? (uint64_t)(int64_t)w : 0ull;
+      }
     }
   }
   if (valid && acc) {
@@ -1188,17 +1252,21 @@ hipError_t launch_clamp_specs(int64_t n_specs, SpecPrep sp, ClampWork cw,
 hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
                               const unsigned long long* counters, int64_t* partial, hipStream_t s) {
   if (n_specs <= 0 || n_nodes <= 0) return hipSuccess;
+  if ((n_nodes + PLIST_SLOT - 1) / PLIST_SLOT > (int64_t)CLAMP_PARTIAL_WGS * CLAMP_PARTIAL_MAX_SLOTS)
+    return hipErrorInvalidValue;  // > 2^28 nodes on one device
   const int64_t t_max = (n_specs + 63) / 64;
+  hipLaunchKernelGGL(clamp_hsum_kernel, dim3(grid_for(clamp_h_cells(n_specs), 256, 2048)),
+                     dim3(256), 0, s, cw, counters);
   hipLaunchKernelGGL(clamp_hcol_kernel, dim3(grid_for(n_specs + 1, 64, 1 << 30)), dim3(64), 0, s,
                      cw, counters);
   hipLaunchKernelGGL(clamp_hrow_kernel, dim3((unsigned)(t_max + 1)), dim3(1024), 0, s, cw,
                      counters);
   if (n_specs <= CLAMP_LDS_SPECS) {
     hipLaunchKernelGGL(clamp_partial_kernel, dim3(CLAMP_PARTIAL_WGS), dim3(1024), 0, s, cw,
-                       counters, cw.dpart);
+                       counters, n_nodes, cw.dpart);
   } else {
     hipLaunchKernelGGL(clamp_partial_big_kernel, dim3((unsigned)t_max, CLAMP_SLICES), dim3(64), 0,
-                       s, cw, counters, n_specs, partial);
+                       s, cw, counters, n_specs, n_nodes, partial);
   }
   hipLaunchKernelGGL(clamp_full_kernel, dim3(grid_for(n_specs, 64, 1 << 30), CLAMP_FULL_SPLIT),
                      dim3(64), 0, s, cw, counters, n_specs, cw.dpart, partial);
