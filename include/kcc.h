@@ -76,6 +76,7 @@ int kcc_reserve(kcc_ctx* ctx, int64_t max_nodes, int64_t max_containers, int64_t
  *   Containers are grouped by node in CSR form: node i owns containers
  *   [node_ptr[i], node_ptr[i+1]); node_ptr[0] == 0, non-decreasing,
  *   node_ptr[n_nodes] == n_containers.  Empty nodes get 0 sums.
+ *   At most 2^28 - 1 nodes per device (per call, or per shard for a multi-GPU ctx).
  *   cpu_lim/mem_lim may both be NULL (then lim_cpu/lim_mem are ignored): the limit
  *   sums are only printed by the reference (CC:110, CC:115-117).
  * ------------------------------------------------------------------------- */

@@ -147,6 +147,8 @@ int reduce_async_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, con
                      uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s) {
   if (n_nodes < 0 || n_cont < 0) return fail(ctx, KCC_EINVAL, "negative size");
   if (n_nodes == 0) return n_cont == 0 ? KCC_OK : fail(ctx, KCC_EINVAL, "containers without nodes");
+  if (n_nodes >= kcc::RED_MAX_NODES)
+    return fail(ctx, KCC_EINVAL, "too many nodes per device (max 2^28 - 1)");
   if (!ptr || !used_cpu || !used_mem) return fail(ctx, KCC_EINVAL, "NULL node_ptr/output");
   if (n_cont > 0 && (!cpu || !mem)) return fail(ctx, KCC_EINVAL, "NULL cpu_req/mem_req");
   const bool lim = cpul != nullptr || meml != nullptr;
@@ -344,6 +346,8 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                          int64_t* used_mem, int64_t n_specs, const uint64_t* spec_cpu,
                          const int64_t* spec_mem, int64_t* partial, int n_chunks, hipStream_t s) {
   if (n_nodes < 0 || n_cont < 0 || n_specs < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (n_nodes >= kcc::RED_MAX_NODES)
+    return fail(ctx, KCC_EINVAL, "too many nodes per device (max 2^28 - 1)");
   if (n_specs > 0x7fffffffLL) return fail(ctx, KCC_EINVAL, "too many specs (max 2^31-1)");
   if (n_nodes == 0 && n_cont != 0) return fail(ctx, KCC_EINVAL, "containers without nodes");
   if (n_nodes > 0 && (!ptr || !used_cpu || !used_mem || !alloc_cpu || !alloc_mem || !alloc_pods ||

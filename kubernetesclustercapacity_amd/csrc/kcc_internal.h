@@ -9,32 +9,27 @@ namespace kcc {
 // ---- (a) segmented request reduce -------------------------------------------
 // One wavefront owns a contiguous range of reduce_range() containers and walks it in
 // tiles of RED_TILE (RED_IPL containers per lane: two 16-B loads per lane per array).
-#ifndef KCC_RED_TILES_PER_WAVE
-#define KCC_RED_TILES_PER_WAVE 16  // longest wave range (tiles)
-#endif
-#ifndef KCC_RED_TARGET_WAVES
-#define KCC_RED_TARGET_WAVES 8192  // shorten ranges until this many waves exist
+#ifndef KCC_RED_ROUNDS
+#define KCC_RED_ROUNDS 1  // waves = this many rounds of the resident wave capacity
 #endif
 #ifndef KCC_RED_PREFETCH
 #define KCC_RED_PREFETCH 1  // tiles in flight ahead of the one being reduced (1 or 2)
 #endif
 constexpr int RED_IPL = 4;
 constexpr int RED_TILE = 64 * RED_IPL;  // 256
-constexpr int RED_TILES_PER_WAVE = KCC_RED_TILES_PER_WAVE;
 constexpr int RED_WAVES_PER_BLOCK = 4;
+// the reduce stores through 32-bit buffer offsets (8 B per node, < 2^31)
+constexpr int64_t RED_MAX_NODES = (int64_t)1 << 28;
 
-// Containers per wave range: whole tiles, long (<= 16 tiles) for big inputs, short
-// enough for small ones (a node shard of an 8-GPU run) that ~KCC_RED_TARGET_WAVES
-// waves exist and every SIMD has several in flight.
-inline int32_t reduce_range(int64_t n_containers) {
-  int64_t t = (n_containers + (int64_t)RED_TILE * KCC_RED_TARGET_WAVES - 1) /
-              ((int64_t)RED_TILE * KCC_RED_TARGET_WAVES);
-  if (t < 1) t = 1;
-  if (t > RED_TILES_PER_WAVE) t = RED_TILES_PER_WAVE;
-  return (int32_t)(t * RED_TILE);
-}
-inline int64_t reduce_n_waves(int64_t n_containers) {
-  const int64_t r = reduce_range(n_containers);
+// Containers per wave range: whole tiles, sized so the waves fill the device's resident
+// wave slots (occupancy API) in KCC_RED_ROUNDS rounds: one round of equal, long ranges
+// leaves no half-empty second round (9672 waves of 4096 containers at C4 ran 1.6 rounds
+// of 6144 resident waves).  Small inputs get one tile per wave.  `limits` selects the
+// 4-array kernel (more registers, fewer resident waves).  Both reduce launches of a call
+// use the same range.
+int32_t reduce_range(int64_t n_containers, bool limits);
+inline int64_t reduce_n_waves(int64_t n_containers, bool limits) {
+  const int64_t r = reduce_range(n_containers, limits);
   return (n_containers + r - 1) / r;
 }
 // workspace bound for wave_node (shortest range)

@@ -80,8 +80,8 @@ __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
 
 // CSR offset of node j relative to the wave range start, clamped into int32.
 __device__ __forceinline__ int32_t rel_clamp(int64_t raw, int64_t wb) {
-  const int64_t v = raw - wb;  // any range is <= RED_TILE * RED_TILES_PER_WAVE
-  constexpr int64_t HI = (int64_t)RED_TILE * RED_TILES_PER_WAVE + 2;
+  const int64_t v = raw - wb;  // any range is < 2^28 (reduce_range)
+  constexpr int64_t HI = (int64_t)1 << 30;
   return (int32_t)(v < -1 ? -1 : (v > HI ? HI : v));
 }
 __device__ __forceinline__ int64_t ptr_at(const int64_t* __restrict__ ptr, int64_t j,
@@ -118,18 +118,34 @@ __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff
 //   1. the tile-local inclusive prefix sum of the 256 values: a 4-item running sum per
 //      lane, one DPP inclusive scan (64-bit, all VALU) of the lane totals, written to
 //      a per-wave LDS strip pre[0..255];
-//   2. lane k takes node cur + k (cur = the node holding the tile's first item): its
-//      end offset comes from a sliding register window of CSR offsets (3 x 64, the
-//      third prefetched), its start is lane k-1's end (DPP shift).  A node ending in
-//      this tile gets sum = pre[end-1] - pre[start-1], or pre[end-1] + carry when it
-//      began in an earlier tile (carry = its running sum so far, wave-uniform), all
-//      in wrapping uint64 arithmetic, so the differences are exact;
-//   3. the node's sum is stored by its lane — a plain store when the node lies
-//      inside this wave's range, a 64-bit atomic add only for the (at most two) nodes
-//      crossing the range boundaries.
-// Empty nodes are never visited (zeroed by reduce_mark_kernel).
+//   2. nodes are visited in aligned blocks of 64 (lane l <-> node 64*blk + l), so the
+//      block's CSR end offsets are one coalesced 512-B load, held in a register (eA),
+//      with the next block's reloaded at every tile end (eNr; L2 hits, but at a fixed
+//      distance from its use, so no tile drains the data prefetch); a node's start is the previous lane's end
+//      (DPP shift; lane 0 takes the previous block's last end).  The nodes ending in
+//      this tile are a contiguous run of lanes starting at node cur (the node holding
+//      the tile's first item); each gets sum = pre[end-1] - pre[start-1], or
+//      pre[end-1] + carry when it began in an earlier tile (carry = its running sum so
+//      far, wave-uniform), in wrapping uint64 arithmetic, so the differences are exact;
+//      when the run reaches lane 63 the block is complete and the pass continues with
+//      the next block in the same tile;
+//   3. the sums stay in registers (res, one per lane = per node of the block) and a
+//      completed block is written with ONE coalesced 512-B store per array: stores
+//      count in vmcnt like loads, so a store per tile would put its completion latency
+//      in front of the next tile's data wait.  Only the (at most two) nodes crossing
+//      the range boundaries use 64-bit atomics.
+// Nodes before the wave's first owned node and the empty nodes ahead of node0 are
+// zeroed by reduce_mark_kernel; every other node of the wave's run, empty ones
+// included, is written by its flush.
+constexpr uint32_t RED_OOB_OFFSET = 0x7ffffff0u;  // > any output's range (n_nodes < 2^28)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
 template <int NA>
-__global__ __launch_bounds__(256) void reduce_kernel(
+__global__ __launch_bounds__(256)
+#ifdef KCC_RED_WAVES_PER_EU
+__attribute__((amdgpu_waves_per_eu(KCC_RED_WAVES_PER_EU)))
+#endif
+void reduce_kernel(
     int64_t n_nodes, int64_t c0, int64_t n_cont, int32_t range, const int64_t* __restrict__ ptr,
     const uint64_t* __restrict__ in0, const uint64_t* __restrict__ in1,
     const uint64_t* __restrict__ in2, const uint64_t* __restrict__ in3,
@@ -155,20 +171,52 @@ __global__ __launch_bounds__(256) void reduce_kernel(
                                               (int)((len & ~1) * 8), 0x00020000);
 
   const int64_t node0 = wave_node[w];
-  const int64_t start0 = ptr[node0];
-  const bool first_open = start0 < wb;  // node0 began in an earlier range
-  int64_t cur = node0;                  // node holding the current tile's first item
-  int32_t cur_start = rel_clamp(start0, wb);
-  uint64_t carry[NA];                   // node cur's running sum over [cur_start, tb)
+  const bool first_open = ptr[node0] < wb;           // node0 began in an earlier range
+  const int64_t own_lo = node0 + (first_open ? 1 : 0);  // first node stored plainly
+  int64_t cur = node0;  // node holding the current tile's first item
+  uint64_t carry[NA];   // node cur's running sum over the earlier tiles of this range
+  uint64_t res[NA];     // sums of block blk's nodes (lane l <-> node 64*blk + l)
 #pragma unroll
-  for (int k = 0; k < NA; ++k) carry[k] = 0;
+  for (int k = 0; k < NA; ++k) carry[k] = res[k] = 0;
 
-  // sliding window of CSR end offsets: win0/win1 (relative, clamped) hold the ends
-  // of nodes [wbase-1, wbase+63), [wbase+63, +127); win2r (raw, in flight) the next 64
-  int64_t wbase = cur + 1;
-  int32_t win0 = rel_ptr(ptr, wbase + lane, n_nodes, wb);
-  int32_t win1 = rel_ptr(ptr, wbase + 64 + lane, n_nodes, wb);
-  int64_t win2r = ptr_at(ptr, wbase + 128 + lane, n_nodes);
+  int64_t blk = node0 >> 6;
+  int32_t eA = rel_ptr(ptr, 64 * blk + 1 + lane, n_nodes, wb);  // end of node 64*blk + l
+  int32_t sA0 = rel_ptr(ptr, 64 * blk, n_nodes, wb);            // end of node 64*blk - 1
+  int64_t eNr = ptr_at(ptr, 64 * blk + 65 + lane, n_nodes);     // next block (raw, in flight)
+  bool have_next = true;  // eNr holds block blk + 1's ends
+  // a completed block's sums awaiting their store (lane l <-> node 64*pend_blk + l)
+  uint64_t resF[NA];
+  bool pend = false;
+  int64_t pend_blk = 0;  // wave-uniform
+  auto flush_pending = [&]() {  // rare path only (see issue_pending)
+    const int64_t pend_j = 64 * pend_blk + lane;
+    if (pend_j >= own_lo) {
+#pragma unroll
+      for (int k = 0; k < NA; ++k) out[k][pend_j] = resF[k];
+    }
+    pend = false;
+  };
+  // Output descriptors: a store at an offset past the end is dropped by the hardware,
+  // which lets every tile issue its pending-block stores unconditionally.
+  __amdgpu_buffer_rsrc_t ro[NA];
+#pragma unroll
+  for (int k = 0; k < NA; ++k)
+    ro[k] = __builtin_amdgcn_make_buffer_rsrc((void*)out[k], (short)0, (int)(n_nodes * 8),
+                                              0x00020000);
+  // The pending block's stores, issued right before a tile's prefetch loads: vmcnt is
+  // an in-order count, so a store makes every later load's wait include its
+  // acknowledgement; issued alongside the prefetch it completes with it.  A fixed
+  // number of them every tile (out of range when nothing is pending) keeps the count
+  // static, so the compiler's waits do not assume the stores absent.
+  auto issue_pending = [&]() {
+    const int64_t pend_j = 64 * pend_blk + lane;
+    const uint32_t voff = (pend && pend_j >= own_lo) ? (uint32_t)(pend_j * 8) : RED_OOB_OFFSET;
+#pragma unroll
+    for (int k = 0; k < NA; ++k)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, resF[k]), ro[k],
+                                            (int)voff, 0, 0);
+    pend = false;
+  };
 
   uint64_t xa[NA][4], xb[NA][4];
 #if KCC_RED_PREFETCH == 2
@@ -183,9 +231,17 @@ __global__ __launch_bounds__(256) void reduce_kernel(
   }
 
   auto tile = [&](uint64_t (&x)[NA][4], uint64_t (&nx)[NA][4], const int32_t tb) {
+#ifndef KCC_DIAG_RED_NOSTORE
+    issue_pending();
+#endif
 #pragma unroll
     for (int k = 0; k < NA; ++k)
       load_quad(rs[k], lane * 32, (tb + KCC_RED_PREFETCH * RED_TILE) * 8, nx[k]);
+#ifdef KCC_DIAG_RED_LOADONLY
+#pragma unroll
+    for (int k = 0; k < NA; ++k) carry[k] += x[k][0] + x[k][1] + x[k][2] + x[k][3];
+    return;
+#endif
     const int32_t p0 = tb + 4 * lane;  // relative position of this lane's first item
     if ((len & 1) && p0 <= len - 1 && len - 1 < p0 + 4) {  // odd tail: last item alone
 #pragma unroll
@@ -213,56 +269,54 @@ __global__ __launch_bounds__(256) void reduce_kernel(
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 
-    // --- 2./3. nodes ending in this tile ------------------------------------------
+    // --- 2./3. nodes ending in this tile, block by block ----------------------------
+    const int32_t eN_rel = rel_clamp(eNr, wb);  // next block's ends (previous tile's load)
     const int32_t lim = tb + RED_TILE < len ? tb + RED_TILE : len;
-    while (cur + 1 - wbase >= 64) {  // slide the window (rarely more than once)
-      win0 = win1;
-      win1 = rel_clamp(win2r, wb);
-      wbase += 64;
-      win2r = ptr_at(ptr, wbase + 128 + lane, n_nodes);
-    }
-    const int off = (int)(cur + 1 - wbase);  // 0..63
-    const int idx = off + lane;               // 0..126
-    const int32_t g0 = __shfl(win0, idx & 63), g1 = __shfl(win1, idx & 63);
-    const int32_t e = idx < 64 ? g0 : g1;    // end of node cur + lane
-    int32_t s = __builtin_amdgcn_update_dpp(0, e, DPP_WAVE_SHR1, 0xf, 0xf, false);
-    if (lane == 0) s = cur_start;
-    const int64_t j = cur + lane;
-    bool ends = (j < n_nodes) && (e <= lim);
-    if (ends && e > s) {
+    int32_t last_end = -1;  // end of the last node that ended in this tile (-1: none)
+    for (;;) {
+      const int64_t j = 64 * blk + lane;
+      int32_t s = __builtin_amdgcn_update_dpp(0, eA, DPP_WAVE_SHR1, 0xf, 0xf, false);
+      if (lane == 0) s = sA0;
+      const bool act = (j >= cur) && (j < n_nodes) && (eA <= lim);
+      if (act) {
 #pragma unroll
-      for (int k = 0; k < NA; ++k) {
-        const uint64_t endp = pre[k][e - 1 - tb];
-        const uint64_t startp = s > tb ? pre[k][s - 1 - tb] : (0ull - carry[k]);
-        const uint64_t sum = endp - startp;
-        if (j == node0 && first_open) atomic_add_u64(&out[k][j], sum);
-        else out[k][j] = sum;
+        for (int k = 0; k < NA; ++k) {
+          uint64_t sum = 0;
+          if (eA > s) {  // s <= tb only for node cur, which began in an earlier tile
+            const uint64_t startp = s > tb ? pre[k][s - 1 - tb] : (0ull - carry[k]);
+            sum = pre[k][eA - 1 - tb] - startp;
+          }
+          if (j == node0 && first_open) atomic_add_u64(&out[k][j], sum);
+          res[k] = sum;
+        }
       }
-    }
-    unsigned long long bal = __ballot(ends);
-    int64_t cnt = __popcll(bal);
-    int32_t last_end = 0;  // end of the last node that ended in this tile
-    if (cnt) last_end = __builtin_amdgcn_readlane(e, (int)cnt - 1);
-    // more than 64 nodes end in this tile (runs of tiny or empty nodes): direct loads
-    for (int64_t r = 64; (bal >> 63) & 1ull; r += 64) {
-      const int64_t j2 = cur + r + lane;
-      const int32_t s2 = rel_ptr(ptr, j2, n_nodes, wb);
-      const int32_t e2 = rel_ptr(ptr, j2 + 1, n_nodes, wb);
-      const bool ends2 = (j2 < n_nodes) && (e2 <= lim);
-      if (ends2 && e2 > s2) {  // s2 > tb: these nodes start after node cur's end
+      const unsigned long long bal = __ballot(act);
+      if (!bal) break;
+      const int hi = 63 - __builtin_clzll(bal);  // the run is lanes [cur - 64*blk, hi]
+      last_end = __builtin_amdgcn_readlane(eA, hi);
+      cur = 64 * blk + hi + 1;
+      if (hi != 63) break;
+      // block complete.  The next block's ends were loaded at the end of the previous
+      // tile (a second block completing in the same tile loads its ends here).  This
+      // block's sums move to the pending buffer, stored at the top of the next tile.
+      const int32_t e_next =
+          have_next ? eN_rel : rel_ptr(ptr, 64 * blk + 65 + lane, n_nodes, wb);
+      have_next = false;
+      if (pend) flush_pending();  // two blocks in one tile (runs of tiny nodes): now
 #pragma unroll
-        for (int k = 0; k < NA; ++k) out[k][j2] = pre[k][e2 - 1 - tb] - pre[k][s2 - 1 - tb];
-      }
-      bal = __ballot(ends2);
-      const int c2 = __popcll(bal);
-      if (c2) last_end = __builtin_amdgcn_readlane(e2, c2 - 1);
-      cnt += c2;
+      for (int k = 0; k < NA; ++k) resF[k] = res[k];
+      pend = true;
+      pend_blk = blk;
+      sA0 = last_end;
+      eA = e_next;
+      ++blk;
     }
-    if (cnt) {  // a new node is open at the tile end: its sum so far
-      cur += cnt;
-      cur_start = last_end;  // > tb
+    eNr = ptr_at(ptr, 64 * blk + 65 + lane, n_nodes);  // next block's ends (usually L2 hits)
+    have_next = true;
+    if (last_end >= 0) {  // node cur is open at the tile end: its sum so far
 #pragma unroll
-      for (int k = 0; k < NA; ++k) carry[k] = tot[k] - pre[k][last_end - 1 - tb];
+      for (int k = 0; k < NA; ++k)
+        carry[k] = tot[k] - pre[k][last_end - 1 - tb];
     } else {
 #pragma unroll
       for (int k = 0; k < NA; ++k) carry[k] += tot[k];
@@ -282,6 +336,22 @@ __global__ __launch_bounds__(256) void reduce_kernel(
     if (tb + RED_TILE < len) tile(xb, xa, tb + RED_TILE);
   }
 #endif
+#if defined(KCC_DIAG_RED_LOADONLY) || defined(KCC_DIAG_RED_NOSTORE)
+  if (carry[0] == 0x123456789ull) out[0][0] = carry[NA - 1] ^ res[0];
+#endif
+#ifndef KCC_DIAG_RED_NOSTORE
+  issue_pending();
+#endif
+  // the partly finished block: nodes [max(own_lo, 64*blk), cur)
+  {
+    const int64_t j = 64 * blk + lane;
+    if (j >= own_lo && j < cur) {
+#ifndef KCC_DIAG_RED_NOSTORE
+#pragma unroll
+      for (int k = 0; k < NA; ++k) out[k][j] = res[k];
+#endif
+    }
+  }
   // the node open at the end of the range continues into the next wave's range
   if (wb + len < n_cont && lane == 0 && cur < n_nodes) {
 #pragma unroll
@@ -1174,12 +1244,40 @@ inline unsigned grid_for(int64_t n, int block, int64_t cap) {
 
 }  // namespace
 
+namespace {
+int64_t reduce_resident_waves(bool limits) {
+  static int64_t cache[2] = {0, 0};
+  int64_t& w = cache[limits ? 1 : 0];
+  if (w == 0) {
+    int dev = 0, cus = 0, blocks = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &blocks, limits ? reduce_kernel<4> : reduce_kernel<2>, 256, 0) == hipSuccess &&
+        cus > 0 && blocks > 0)
+      w = (int64_t)cus * blocks * RED_WAVES_PER_BLOCK;
+    else
+      w = 8192;
+  }
+  return w;
+}
+}  // namespace
+
+int32_t reduce_range(int64_t n_containers, bool limits) {
+  const int64_t r = reduce_resident_waves(limits) * KCC_RED_ROUNDS * RED_TILE;
+  int64_t t = (n_containers + r - 1) / r;
+  if (t < 1) t = 1;
+  if (t > ((int64_t)1 << 20)) t = (int64_t)1 << 20;  // range < 2^28 (int32 relative offsets)
+  return (int32_t)(t * RED_TILE);
+}
+
 hipError_t launch_reduce_mark(int64_t n_nodes, int64_t c0, int64_t n_containers,
                               const int64_t* node_ptr, int64_t* wave_node, uint64_t* used_cpu,
                               int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s) {
   if (n_nodes <= 0) return hipSuccess;
   hipLaunchKernelGGL(reduce_mark_kernel, dim3(grid_for(n_nodes, 256, 8192)), dim3(256), 0, s,
-                     n_nodes, c0, c0 + n_containers, reduce_range(n_containers), node_ptr, wave_node,
+                     n_nodes, c0, c0 + n_containers, reduce_range(n_containers, lim_cpu != nullptr),
+                     node_ptr, wave_node,
                      used_cpu,
                      reinterpret_cast<uint64_t*>(used_mem), lim_cpu,
                      reinterpret_cast<uint64_t*>(lim_mem));
@@ -1192,8 +1290,10 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
                          const int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem,
                          uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s) {
   if (n_nodes <= 0 || n_containers <= 0) return hipSuccess;
-  const int32_t range = reduce_range(n_containers);
-  const int64_t waves = reduce_n_waves(n_containers);
+  if (n_nodes >= RED_MAX_NODES) return hipErrorInvalidValue;
+  const bool limits = cpu_lim && mem_lim && lim_cpu && lim_mem;
+  const int32_t range = reduce_range(n_containers, limits);
+  const int64_t waves = reduce_n_waves(n_containers, limits);
   const unsigned blocks = (unsigned)((waves + RED_WAVES_PER_BLOCK - 1) / RED_WAVES_PER_BLOCK);
   const bool lim = cpu_lim && mem_lim && lim_cpu && lim_mem;
   if (lim) {
