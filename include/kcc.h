@@ -105,6 +105,7 @@ int kcc_reduce_requests_async(kcc_ctx* ctx, int64_t n_nodes, int64_t n_container
  *   (spec_cpu[s] == 0 reached on a row with free CPU, or spec_mem[s] == 0 on a row
  *   with free memory); totals[s] is then 0.  pod_count = len(pods) (CC:106, CC:135).
  *   The verdict (CC:144) is totals[s] >= replicas[s], left to the caller.
+ *   At most 2^26 - 1 specs per call.
  * ------------------------------------------------------------------------- */
 int kcc_fit(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* alloc_cpu,
             const int64_t* alloc_mem, const int64_t* alloc_pods,

@@ -58,11 +58,16 @@ struct Dev {
   double prof_ms[2] = {0.0, 0.0};
   int64_t prof_n[2] = {0, 0};
   // workspace of the *_async entry points
-  DevBuf wave_node, fast_a, fast_b, slow, slow_list, srec, sperm, counters;
+  DevBuf wave_node, fast_a, fast_b, slow, slow_list, srec, sperm, srec_o, counters;
   // clamp correction (kcc::ClampWork)
-  DevBuf c_rank, c_cs, c_ms, c_mless, c_dperm, c_H, c_pcount, c_pkey, c_pb, c_pw, c_dpart;
+  DevBuf c_rank, c_sync, c_cs, c_ms, c_mless, c_dperm, c_gml, c_kpos, c_H, c_H2, c_R;
+  // H, H2, rank and the completion counter not known to be all zero (fresh allocation
+  // or an interrupted call)
+  bool clamp_dirty = true;
   int64_t last_pairs = 0;  // node x spec pairs of the last fit_prepare on this device
   int64_t h_stride = 0;    // cells per copy of the clamp table H in c_H
+  int64_t h2_stride = 0;   // cells per copy of the clamp table H2 in c_H2
+  int64_t rt_stride = 0;   // tiles per row of the clamp table's row sums
   int64_t prep_nodes = -1, prep_specs = -1;  // sizes the workspace was last prepared for
   // staging of the host-array entry points
   DevBuf ptr, cpu, mem, cpul, meml, used_cpu, used_mem, lim_cpu, lim_mem;
@@ -171,6 +176,7 @@ kcc::SpecPrep spec_prep_of(Dev& dv) {
   kcc::SpecPrep sp;
   sp.rec = as<kcc::SpecRec>(dv.srec);
   sp.perm = as<int32_t>(dv.sperm);
+  sp.rec_o = as<kcc::SpecRec>(dv.srec_o);
   return sp;
 }
 
@@ -186,49 +192,62 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.slow_list, sizeof(int64_t) * N));
   KCC_HIP(ctx, ensure(dv.srec, sizeof(kcc::SpecRec) * S));
   KCC_HIP(ctx, ensure(dv.sperm, 4 * S));
+  KCC_HIP(ctx, ensure(dv.srec_o, sizeof(kcc::SpecRec) * S));
   KCC_HIP(ctx, ensure(dv.counters, sizeof(unsigned long long) * kcc::CNT_N));
-  KCC_HIP(ctx, ensure(dv.c_rank, 3 * 4 * S));
+  KCC_HIP(ctx, ensure(dv.c_sync, 64));
   KCC_HIP(ctx, ensure(dv.c_cs, 8 * S));
   KCC_HIP(ctx, ensure(dv.c_ms, 8 * S));
   KCC_HIP(ctx, ensure(dv.c_mless, 4 * S));
   KCC_HIP(ctx, ensure(dv.c_dperm, 4 * S));
-  KCC_HIP(ctx, ensure(dv.c_H, 8 * (size_t)kcc::H_COPIES * (size_t)kcc::clamp_h_cells((int64_t)S)));
-  dv.h_stride = kcc::clamp_h_cells((int64_t)S);
-  const size_t NS = (N + kcc::PLIST_SLOT - 1) / kcc::PLIST_SLOT * kcc::PLIST_SLOT;  // whole slots
-  KCC_HIP(ctx, ensure(dv.c_pcount, 4 * (NS / kcc::PLIST_SLOT + 1)));
-  KCC_HIP(ctx, ensure(dv.c_pkey, 4 * NS));
-  KCC_HIP(ctx, ensure(dv.c_pb, 4 * NS));
-  KCC_HIP(ctx, ensure(dv.c_pw, 4 * NS));
-  KCC_HIP(ctx, ensure(dv.c_dpart, 8 * (size_t)kcc::CLAMP_PARTIAL_ROWS * S));
+  KCC_HIP(ctx, ensure(dv.c_gml, 4 * (S / 64 + 1) * 64));
+  KCC_HIP(ctx, ensure(dv.c_kpos, S));
+  // H, H2, rank and the completion counter stay all-zero between calls (their consumers
+  // zero what they read); a new or grown allocation, or a layout change, is zeroed
+  // before its first use
+  const int64_t hs = kcc::clamp_h_cells((int64_t)S), h2s = kcc::clamp_h2_cells((int64_t)S);
+  const int64_t rts = kcc::clamp_rtiles((int64_t)S);
+  void* const before[3] = {dv.c_H.p, dv.c_H2.p, dv.c_rank.p};
+  KCC_HIP(ctx, ensure(dv.c_rank, 4 * 4 * S));
+  KCC_HIP(ctx, ensure(dv.c_H, 8 * (size_t)kcc::H_COPIES * (size_t)hs));
+  KCC_HIP(ctx, ensure(dv.c_H2, 8 * (size_t)kcc::H_COPIES * (size_t)h2s));
+  KCC_HIP(ctx, ensure(dv.c_R, 8 * ((size_t)hs + (size_t)kcc::clamp_rows_max((int64_t)S) * (size_t)rts)));
+  if (dv.c_H.p != before[0] || dv.c_H2.p != before[1] || dv.c_rank.p != before[2] ||
+      dv.h_stride != hs || dv.h2_stride != h2s)
+    dv.clamp_dirty = true;
+  dv.h_stride = hs;
+  dv.h2_stride = h2s;
+  dv.rt_stride = rts;
   return KCC_OK;
 }
 
-kcc::ClampWork clamp_of(Dev& dv);
-// the clamp workspace seen by the node_prep of a node range starting at `lo` (a
-// multiple of PLIST_SLOT): its plist slots are the range's own
-kcc::ClampWork clamp_at(Dev& dv, int64_t lo) {
-  kcc::ClampWork cw = clamp_of(dv);
-  cw.pcount += lo / kcc::PLIST_SLOT;
-  cw.pkey += lo;
-  cw.pb += lo;
-  cw.pw += lo;
-  return cw;
+// Zero H / H2 when they are not known to be zero (before node_prep adds to them).
+int clamp_clean(kcc_ctx* ctx, Dev& dv, hipStream_t s) {
+  if (!dv.clamp_dirty) return KCC_OK;
+  KCC_HIP(ctx, hipMemsetAsync(dv.c_H.p, 0, dv.c_H.bytes, s));
+  KCC_HIP(ctx, hipMemsetAsync(dv.c_H2.p, 0, dv.c_H2.bytes, s));
+  KCC_HIP(ctx, hipMemsetAsync(dv.c_rank.p, 0, dv.c_rank.bytes, s));
+  KCC_HIP(ctx, hipMemsetAsync(dv.c_sync.p, 0, dv.c_sync.bytes, s));
+  dv.clamp_dirty = false;
+  return KCC_OK;
 }
 
 kcc::ClampWork clamp_of(Dev& dv) {
   kcc::ClampWork cw;
   cw.rank = as<uint32_t>(dv.c_rank);
+  cw.sync = as<uint32_t>(dv.c_sync);
   cw.cs = as<uint64_t>(dv.c_cs);
   cw.ms = as<int64_t>(dv.c_ms);
   cw.m_less = as<uint32_t>(dv.c_mless);
   cw.dperm = as<int32_t>(dv.c_dperm);
+  cw.gml = as<uint32_t>(dv.c_gml);
+  cw.kpos = as<uint8_t>(dv.c_kpos);
   cw.H = as<int64_t>(dv.c_H);
-  cw.pcount = as<uint32_t>(dv.c_pcount);
-  cw.pkey = as<uint32_t>(dv.c_pkey);
-  cw.pb = as<uint32_t>(dv.c_pb);
-  cw.pw = as<int32_t>(dv.c_pw);
-  cw.dpart = as<int64_t>(dv.c_dpart);
+  cw.H2 = as<int64_t>(dv.c_H2);
+  cw.R = as<int64_t>(dv.c_R);
+  cw.Rtot = as<int64_t>(dv.c_R) + dv.h_stride;
   cw.h_stride = dv.h_stride;
+  cw.h2_stride = dv.h2_stride;
+  cw.rt_stride = dv.rt_stride;
   return cw;
 }
 
@@ -238,7 +257,7 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
                     const int64_t* used_mem, int64_t n_specs, const uint64_t* spec_cpu,
                     const int64_t* spec_mem, int64_t* partial, hipStream_t s) {
   if (n_nodes < 0 || n_specs < 0) return fail(ctx, KCC_EINVAL, "negative size");
-  if (n_specs > 0x7fffffffLL) return fail(ctx, KCC_EINVAL, "too many specs (max 2^31-1)");
+  if (n_specs >= kcc::MAX_SPECS) return fail(ctx, KCC_EINVAL, "too many specs (max 2^26 - 1)");
   if (n_specs > 0 && (!spec_cpu || !spec_mem || !partial))
     return fail(ctx, KCC_EINVAL, "NULL spec array / partial");
   if (n_nodes > 0 && (!alloc_cpu || !alloc_mem || !alloc_pods || !pod_count || !used_cpu || !used_mem))
@@ -249,19 +268,24 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
   dv.prep_nodes = n_nodes;
   dv.prep_specs = n_specs;
   if (n_specs == 0) return KCC_OK;
+  rc = clamp_clean(ctx, dv, s);
+  if (rc) return rc;
+  dv.clamp_dirty = true;  // until every kernel that leaves the tables zero is queued
   // spec_prep also zeroes `partial` and the counters (no memset launches)
   KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv), clamp_of(dv),
                                      partial, as<unsigned long long>(dv.counters), s));
-  if (n_nodes == 0) return KCC_OK;
-  KCC_HIP(ctx, kcc::launch_clamp_specs(n_specs, spec_prep_of(dv), clamp_of(dv),
-                                       as<unsigned long long>(dv.counters), s));
+  if (n_nodes == 0) {
+    dv.clamp_dirty = false;
+    return KCC_OK;
+  }
   KCC_HIP(ctx, kcc::launch_node_prep(n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count,
                                      used_cpu, used_mem, as<kcc::FitGroupA>(dv.fast_a),
                                      as<kcc::FitGroup>(dv.fast_b), as<kcc::SlowNode>(dv.slow),
-                                     as<int64_t>(dv.slow_list), clamp_of(dv),
+                                     as<int64_t>(dv.slow_list), n_specs, clamp_of(dv),
                                      as<unsigned long long>(dv.counters), 0, s));
-  KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, n_nodes, clamp_of(dv),
+  KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, clamp_of(dv),
                                        as<unsigned long long>(dv.counters), partial, s));
+  dv.clamp_dirty = false;
   return KCC_OK;
 }
 
@@ -313,9 +337,10 @@ hipError_t prof_event(Dev& dv, hipEvent_t* ev) {
   return hipEventCreate(ev);
 }
 
-// Chunk boundaries: node ranges of ~equal node count, multiples of PLIST_SLOT (a multiple
-// of FIT_GROUP: neither the fit's node groups nor the clamp correction's plist slots
-// straddle two chunks); at least `min_nodes` nodes per chunk.
+// Chunk boundaries: node ranges of ~equal node count, multiples of CHUNK_ALIGN (a
+// multiple of FIT_GROUP: the fit's node groups do not straddle two chunks); at least
+// `min_nodes` nodes per chunk.
+constexpr int64_t CHUNK_ALIGN = 1024;
 int plan_chunks(int64_t n_nodes, int want, int64_t min_nodes, std::vector<int64_t>& lo,
                 std::vector<int64_t>& hi) {
   int k = want;
@@ -326,7 +351,7 @@ int plan_chunks(int64_t n_nodes, int want, int64_t min_nodes, std::vector<int64_
   hi.assign(k, 0);
   for (int c = 0; c < k; ++c) {
     lo[c] = c == 0 ? 0 : hi[c - 1];
-    hi[c] = c == k - 1 ? n_nodes : (n_nodes * (c + 1) / k) / kcc::PLIST_SLOT * kcc::PLIST_SLOT;
+    hi[c] = c == k - 1 ? n_nodes : (n_nodes * (c + 1) / k) / CHUNK_ALIGN * CHUNK_ALIGN;
     if (hi[c] < lo[c]) hi[c] = lo[c];
   }
   return k;
@@ -348,7 +373,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   if (n_nodes < 0 || n_cont < 0 || n_specs < 0) return fail(ctx, KCC_EINVAL, "negative size");
   if (n_nodes >= kcc::RED_MAX_NODES)
     return fail(ctx, KCC_EINVAL, "too many nodes per device (max 2^28 - 1)");
-  if (n_specs > 0x7fffffffLL) return fail(ctx, KCC_EINVAL, "too many specs (max 2^31-1)");
+  if (n_specs >= kcc::MAX_SPECS) return fail(ctx, KCC_EINVAL, "too many specs (max 2^26 - 1)");
   if (n_nodes == 0 && n_cont != 0) return fail(ctx, KCC_EINVAL, "containers without nodes");
   if (n_nodes > 0 && (!ptr || !used_cpu || !used_mem || !alloc_cpu || !alloc_mem || !alloc_pods ||
                       !pod_count))
@@ -389,12 +414,12 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     KCC_HIP(ctx, hipStreamWaitEvent(dv.side, dv.ev_fork, 0));
   }
   if (n_specs > 0) {  // spec partition on s (concurrent with the first reduce when k > 1)
+    rc = clamp_clean(ctx, dv, s);
+    if (rc) return rc;
+    dv.clamp_dirty = true;  // until every kernel that leaves the tables zero is queued
     KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv),
                                        clamp_of(dv), partial, as<unsigned long long>(dv.counters),
                                        s));
-    if (n_nodes > 0)
-      KCC_HIP(ctx, kcc::launch_clamp_specs(n_specs, spec_prep_of(dv), clamp_of(dv),
-                                           as<unsigned long long>(dv.counters), s));
   }
   for (int c = 0; c < k; ++c) {
     const int64_t n = hi[c] - lo[c];
@@ -426,7 +451,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                        as<kcc::FitGroupA>(dv.fast_a) + lo[c] / kcc::FIT_GROUP,
                                        as<kcc::FitGroup>(dv.fast_b) + lo[c] / kcc::FIT_GROUP,
                                        as<kcc::SlowNode>(dv.slow) + lo[c],
-                                       as<int64_t>(dv.slow_list) + lo[c], clamp_at(dv, lo[c]),
+                                       as<int64_t>(dv.slow_list) + lo[c], n_specs, clamp_of(dv),
                                        as<unsigned long long>(dv.counters), c, s));
     ProfPair pp{};
     if (dv.prof_on) {
@@ -446,8 +471,12 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     }
   }
   // the pod-slot clamp of every chunk's fast rows, added back per spec
-  KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, n_nodes, clamp_of(dv),
-                                       as<unsigned long long>(dv.counters), partial, s));
+  if (n_specs > 0) {
+    if (n_nodes > 0)
+      KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, clamp_of(dv),
+                                           as<unsigned long long>(dv.counters), partial, s));
+    dv.clamp_dirty = false;
+  }
   return KCC_OK;
 }
 
@@ -624,10 +653,10 @@ void kcc_destroy(kcc_ctx* ctx) {
   for (Dev& dv : ctx->devs) {
     (void)hipSetDevice(dv.device);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
-    DevBuf* bufs[] = {&dv.c_rank, &dv.c_cs, &dv.c_ms, &dv.c_mless, &dv.c_dperm, &dv.c_H,
-                      &dv.c_pcount, &dv.c_pkey, &dv.c_pb, &dv.c_pw, &dv.c_dpart,
+    DevBuf* bufs[] = {&dv.c_rank, &dv.c_sync, &dv.c_cs, &dv.c_ms, &dv.c_mless,
+                      &dv.c_dperm, &dv.c_gml, &dv.c_kpos, &dv.c_H, &dv.c_H2, &dv.c_R,
                       &dv.wave_node, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
-                      &dv.sperm,
+                      &dv.sperm, &dv.srec_o,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
                       &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,
                       &dv.alloc_cpu, &dv.alloc_mem, &dv.alloc_pods, &dv.pod_count, &dv.spec_cpu,

@@ -108,8 +108,9 @@ struct __attribute__((aligned(16))) SpecRec {
 static_assert(sizeof(SpecRec) == 48, "SpecRec must be 48 B");
 
 struct SpecPrep {
-  SpecRec* rec;
-  int32_t* perm;  // internal index -> caller index
+  SpecRec* rec;    // by internal position
+  int32_t* perm;   // internal index -> caller index
+  SpecRec* rec_o;  // by caller index (spec setup's staging)
 };
 
 // Clamp correction.  On the fast paths the fit kernel sums
@@ -117,41 +118,55 @@ struct SpecPrep {
 // added back per spec as  partial[s] -= D_s,  D_s = Σ_i w_i [x_is >= P_i],  w_i = P_i - cl_i
 // (the pod count; for P_i <= 0 rows, clamped for every spec, w_i = -cl_i).  For P_i >= 1,
 // x_is >= P_i  <=>  c_s <= U_i = fc_i / P_i  and  m_s <= V_i = fm_i / P_i  (integer
-// quotients): a 2-D dominance count.  The normal specs (classes A and B) are ranked by c
-// (groups of 64 consecutive c-ranks) and by m; a node covering L_i = #{s : c_s <= U_i}
-// c-ranks covers groups [0, G_i = L_i / 64) fully — one cell H[G_i][b_i] of a
-// (T+1) x (nN+1) table, b_i = #{s : m_s <= V_i}, read back through a 2-D suffix sum — and
-// the first r_i = L_i % 64 lanes of group G_i: one plist entry (key G_i<<6 | r_i, b_i, w_i).
+// quotients): a 2-D dominance count.  The nN normal specs (classes A and B) are ranked by
+// c — groups of 64 consecutive c-ranks, T = ceil(nN / 64) — and by m.  Node i covers
+// L_i = #{s : c_s <= U_i} c-ranks, G_i = L_i / 64 full groups and the first r_i = L_i % 64
+// lanes of group G_i, and b_i = #{s : m_s <= V_i} m-ranks:
+//   - full groups: one cell H[G_i][b_i] of a (T+1) x (nN+1) table; spec s (c-rank q,
+//     group g = q / 64) collects  Σ_{G > g, b > m_less_s} H[G][b];
+//   - group G_i's first r_i lanes: one cell H2[G_i][r_i][k_i] of a 64 x 65 table per
+//     group, k_i = #{specs of group G_i with m_less < b_i}; spec s collects
+//     Σ_{r > q % 64, k > kpos_s} H2[g][r][k], kpos_s = its position in the group's
+//     m_less order (m_s <= V_i  <=>  m_less_s < b_i  <=>  kpos_s < k_i).
+// H and H2 have one copy per XCD (node_prep's atomics spread over 8x the cache lines) and
+// are zero between calls: clamp_rows / clamp_groups zero every cell they read.
 struct ClampWork {
-  uint32_t* rank;    // [3*S] per normal spec (internal position): c-rank, m-rank, #{smaller m}
+  uint32_t* rank;    // [4*S] by caller index: c-rank, m-rank, #{smaller m}, rank within
+                     // the class (zero between calls)
+  uint32_t* sync;    // spec setup: [1] [2] class A / B counts (zero between calls)
   uint64_t* cs;      // [S] normal specs' cpu requests in c-rank order
-  int64_t* ms;       // [S] normal specs' memory requests in m-rank order
+  int64_t* ms;       // [S] normal specs' memory requests in m order
   uint32_t* m_less;  // [S] by c-rank: #normal specs with a smaller memory request
   int32_t* dperm;    // [S] c-rank -> internal position
-  int64_t* H;        // [H_COPIES][clamp_h_cells(S)]: (T+1) x (nN+1) clamp weights, one copy
-                     // per XCD (node_prep's atomics spread over 8x the cache lines); copy 0
-                     // then holds the 2-D suffix sums of their total
-  // plist: one slot of PLIST_SLOT entries per PLIST_SLOT consecutive nodes (node_prep
-  // fills a slot's first pcount[slot] entries: no shared counter)
-  uint32_t* pcount;  // [N / PLIST_SLOT + 1]
-  uint32_t* pkey;    // [N] plist: G << 6 | r
-  uint32_t* pb;      // [N] plist: b (m-rank bound)
-  int32_t* pw;       // [N] plist: w
-  int64_t* dpart;    // [CLAMP_PARTIAL_ROWS * S] per-workgroup partial-group sums
+  uint32_t* gml;     // [64*T] per group of 64 c-ranks: its m_less values ascending
+  uint8_t* kpos;     // [S] by c-rank: the spec's position in its group's gml order
+  int64_t* H;        // [H_COPIES][h_stride]: (T+1) x (nN+1)
+  int64_t* H2;       // [H_COPIES][h2_stride]: T x 64 x 65, cell (G*64 + r)*65 + k
+  int64_t* R;        // [h_stride]: H's rows summed over the copies, suffix sums over b
+                     // within tiles of CLAMP_RTILE (clamp_rows)
+  int64_t* Rtot;     // [(T+1) x rt_stride]: the tiles' totals
   int64_t h_stride;  // cells per H copy (clamp_h_cells(S) of the workspace)
+  int64_t h2_stride; // cells per H2 copy (clamp_h2_cells(S))
+  int64_t rt_stride; // tiles per row (clamp_rtiles(S))
 };
+constexpr int64_t CLAMP_RTILE = 1024;
+// specs per call: the group orders use 32-bit keys m_less << 6 | lane
+constexpr int64_t MAX_SPECS = (int64_t)1 << 26;
+inline int64_t clamp_rtiles(int64_t S) { return (S + 1 + CLAMP_RTILE - 1) / CLAMP_RTILE; }
+inline int64_t clamp_rows_max(int64_t S) { return S / 64 + 2; }
 inline int64_t clamp_h_cells(int64_t S) { return (S / 64 + 2) * (S + 1); }
-constexpr int H_COPIES = 8;
-// up to this many normal specs the sorted requests / accumulators live in LDS
+inline int64_t clamp_h2_cells(int64_t S) { return (S / 64 + 1) * 64 * 65; }
+#ifndef KCC_H_COPIES
+#define KCC_H_COPIES 8
+#endif
+constexpr int H_COPIES = KCC_H_COPIES;
+// up to this many specs the spec setup sorts in LDS (one workgroup) and node_prep's
+// search tables live in LDS; larger S takes the brute-force rank kernels and global
+// searches
 #ifndef KCC_CLAMP_LDS_SPECS
 #define KCC_CLAMP_LDS_SPECS 4096
 #endif
-#ifndef KCC_CLAMP_PARTIAL_ROWS
-#define KCC_CLAMP_PARTIAL_ROWS 256
-#endif
 constexpr int64_t CLAMP_LDS_SPECS = KCC_CLAMP_LDS_SPECS;
-constexpr int64_t PLIST_SLOT = 1024;  // = node_prep's workgroup size
-constexpr int64_t CLAMP_PARTIAL_ROWS = KCC_CLAMP_PARTIAL_ROWS;
 
 // counters (CNT_*): exact-path (node, spec) pairs, class-B specs, and per node chunk
 // of a pipelined call (kcc_capacity_partial_async) the rows in that chunk's slow_list.
@@ -161,27 +176,29 @@ enum {
   CNT_SLOW_PAIRS = 0,  // (node, spec) pairs evaluated on the exact path
   CNT_SPECS_A = 1,     // class-A specs (internal positions [0, nA))
   CNT_SPECS_B = 2,     // class-B specs (internal positions [nA, nA + nB))
-  CNT_PLIST = 3,       // clamp-correction plist entries
+  CNT_SPARE = 3,
   CNT_SLOW_ROWS = 4,   // + chunk: rows in that node chunk's slow_list
   CNT_N = 4 + FIT_MAX_CHUNKS
 };
+// Spec setup, three launches: brute-force ranks of every spec (64 queries per workgroup,
+// the candidates split over workgroups and waves) — by request for the clamp correction
+// and within its class for the stable 3-way partition; then one thread per spec places
+// SpecRec / perm and the sorted arrays (cs, ms, dperm, m_less); then one workgroup per
+// group of 64 c-ranks orders it by m_less (gml, kpos).  Zeroes partial[0..2S) and sets
+// the counters.
 hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
                             const int64_t* spec_mem, SpecPrep sp, ClampWork cw, int64_t* partial,
                             unsigned long long* counters, hipStream_t s);
-// c/m ranks of the normal specs, sorted arrays, zeroed H (after spec_prep)
-hipError_t launch_clamp_specs(int64_t n_specs, SpecPrep sp, ClampWork cw,
-                              const unsigned long long* counters, hipStream_t s);
-// H -> its 2-D suffix sums; partial[s] -= D_s for the normal specs of clamp-free waves
-// (after every node_prep of the call, before the all-reduce)
-// n_nodes: all nodes of the call (the plist slots of every node_prep launch)
-hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
+// H, H2 -> D_s;  partial[s] -= D_s for the normal specs of clamp-free waves (after every
+// node_prep of the call, before the all-reduce); leaves H and H2 zero
+hipError_t launch_clamp_apply(int64_t n_specs, ClampWork cw,
                               const unsigned long long* counters, int64_t* partial, hipStream_t s);
 
 hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
-                            SlowNode* slow, int64_t* slow_list, ClampWork cw,
+                            SlowNode* slow, int64_t* slow_list, int64_t n_specs, ClampWork cw,
                             unsigned long long* counters, int chunk, hipStream_t s);
 
 // partial[0..S) += Σ_i q(i,s), partial[S..2S) += #div-by-zero rows (internal order).

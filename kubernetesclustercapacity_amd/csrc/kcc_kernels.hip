@@ -18,6 +18,16 @@ namespace kcc {
 
 namespace {
 
+// Diagnostic timeline (KCC_TIMELINE builds only): per-workgroup wall-clock stamps
+// (s_memrealtime, 100 MHz) of the small kernels' phases, read by kcc_debug_timeline.
+#ifdef KCC_TIMELINE
+__device__ uint64_t kcc_tl[4096][4];
+#define KCC_TL(slot, k) \
+  do { if (threadIdx.x == 0) kcc_tl[(slot)][(k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define KCC_TL(slot, k) do { } while (0)
+#endif
+
 __device__ __forceinline__ unsigned long long atomic_add_u64(uint64_t* p, uint64_t v) {
   return atomicAdd(reinterpret_cast<unsigned long long*>(p),
                    static_cast<unsigned long long>(v));
@@ -426,14 +436,27 @@ __device__ __forceinline__ uint32_t upper_bound_count(const T* __restrict__ a, i
   return (uint32_t)lo;
 }
 
+// #{j < 64 : a[j] < b} for one group's ascending gml entries (0xffff / 0xffffffff pad)
+template <class T>
+__device__ __forceinline__ uint32_t group_count64(const T* a, uint32_t b) {
+  if ((uint32_t)a[63] < b) return 64;
+  uint32_t lo = 0;
+#pragma unroll
+  for (uint32_t s = 32; s >= 1; s >>= 1) lo += (uint32_t)a[lo + s - 1] < b ? s : 0u;
+  return lo;
+}
+
 // Per-node free capacity (CC:119-135 operands).  Rows that fit the fast-path
 // bounds get exact FitGroupA fields (and FitGroup fields when class-B specs exist);
 // the others get all-zero fields (contribute exactly 0 on the fast paths) and are
-// appended to slow_list for the exact 64-bit path.  Covers the padding of the last
-// group too (zero fields, not listed).
-#define KCC_NODE_PREP_BLOCK 1024  // = PLIST_SLOT
+// appended to slow_list for the exact path.  Covers the padding of the last group too
+// (zero fields, not listed).  SlowNode records are written for the slow rows, and for
+// every row when exact-path specs exist (their waves walk all rows).  Clamp correction:
+// each fast row with P >= 1 adds its weight to one cell of H (full c-rank groups) and
+// one of H2 (its partial group), rows with P <= 0 to H[T][nN] (ClampWork).
+#define KCC_NODE_PREP_BLOCK 1024
 #ifndef KCC_NODE_PREP_GRID
-#define KCC_NODE_PREP_GRID 2048  // workgroups at most (each fills its LDS search tables once)
+#define KCC_NODE_PREP_GRID 512  // workgroups at most (2 per CU, one round; each fills its LDS tables once)
 #endif
 __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_cpu,
                                  const int64_t* __restrict__ alloc_mem,
@@ -443,22 +466,27 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
                                  const int64_t* __restrict__ used_mem,
                                  FitGroupA* __restrict__ fast_a, FitGroup* __restrict__ fast_b,
                                  SlowNode* __restrict__ slow, int64_t* __restrict__ slow_list,
-                                 ClampWork cw, unsigned long long* __restrict__ counters,
+                                 int64_t S, ClampWork cw, unsigned long long* __restrict__ counters,
                                  int32_t chunk) {
   const int lane = threadIdx.x & 63;
   const int64_t n_pad = fit_groups(n) * FIT_GROUP;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const bool want_b = counters[CNT_SPECS_B] != 0;  // written by spec_prep (same stream)
   const int64_t nN = clamp_n_normal(counters);     // normal specs (clamp correction)
+  const bool slow_all = nN < S;                    // exact-path specs exist
   const int64_t T = (nN + 63) / 64, hw = nN + 1;
-  // this workgroup's copy of H: workgroups are dealt round-robin over the 8 XCDs
-  int64_t* Hc = cw.H + (int64_t)(blockIdx.x % H_COPIES) * cw.h_stride;
-  // the sorted spec requests of the binary searches, in LDS when they fit: c clamped
-  // to 2^23 (> every U = fc / P, fc < 2^23) as u32, m as i64
+  // this workgroup's copies of H and H2: workgroups are dealt round-robin over the XCDs
+  const int64_t copy = (int64_t)(blockIdx.x % H_COPIES);
+  int64_t* Hc = cw.H + copy * cw.h_stride;
+  int64_t* H2c = cw.H2 + copy * cw.h2_stride;
+  // the sorted spec requests of the searches and the groups' m_less orders, in LDS when
+  // they fit: c clamped to 2^23 (> every U = fc / P, fc < 2^23) as u32, m as i64, the
+  // gml entries as u16 (< 4096, padding 0xffff)
   extern __shared__ __attribute__((aligned(16))) unsigned char np_lds[];
   int64_t* ms_l = reinterpret_cast<int64_t*>(np_lds);
   uint32_t* cs_l = reinterpret_cast<uint32_t*>(np_lds + 8 * CLAMP_LDS_SPECS);
-  const bool lds = nN <= CLAMP_LDS_SPECS;
+  uint16_t* gml_l = reinterpret_cast<uint16_t*>(np_lds + 12 * CLAMP_LDS_SPECS);
+  const bool lds = S <= CLAMP_LDS_SPECS;
   // smallest normal requests (rows below either dominate no spec); cs[0] >= 1
   const uint32_t cmin = nN > 0 ? (cw.cs[0] < FAST_FC_MAX ? (uint32_t)cw.cs[0] : (uint32_t)FAST_FC_MAX)
                                : 0xffffffffu;
@@ -473,14 +501,16 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       cs_l[k] = c < FAST_FC_MAX ? (uint32_t)c : 0xffffffffu;
       ms_l[k] = k < nN ? cw.ms[k] : INT64_MAX;
     }
+    for (int64_t k = threadIdx.x; k < 64 * T; k += blockDim.x) {
+      const uint32_t v = cw.gml[k];
+      gml_l[k] = v < 0xffffu ? (uint16_t)v : (uint16_t)0xffffu;
+    }
   }
   __syncthreads();
-  __shared__ unsigned long long wcount[16];
-  static_assert(KCC_NODE_PREP_BLOCK == PLIST_SLOT, "one plist slot per workgroup iteration");
-  const int wv = threadIdx.x >> 6;
-  // block-uniform trip count (the plist append below synchronises the workgroup)
-  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n_pad; i0 += stride) {
-    const int64_t i = i0 + threadIdx.x;
+  KCC_TL(3072 + blockIdx.x % 1024, 0);
+  // wave-uniform trip count (wave-wide sums and ballots below)
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < n_pad; i0 += stride) {
+    const int64_t i = i0 + lane;
     const bool valid = i < n;
     bool ok = false;
     uint64_t fc_ok = 0;
@@ -501,12 +531,14 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
         P_ok = P;
         cl_i = (int32_t)cl;
       }
-      SlowNode sn;
-      sn.fc = fc;
-      sn.fm = fm;
-      sn.P = P;
-      sn.cl = cl;
-      slow[i] = sn;
+      if (slow_all || !ok) {
+        SlowNode sn;
+        sn.fc = fc;
+        sn.fm = fm;
+        sn.P = P;
+        sn.cl = cl;
+        slow[i] = sn;
+      }
     }
     if (i < n_pad) {
       const int k = (int)(i % FIT_GROUP);
@@ -522,23 +554,22 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       }
     }
     // clamp correction: where (and with which weight) this row's pod-slot clamp applies
-    bool always = false, in_plist = false;
+    bool always = false;
     int64_t w = 0;
-    uint32_t key = 0, bnd = 0;
     if (ok && nN > 0) {
       const int64_t P = P_ok, Penc = P > 0 ? P : 0;
       w = Penc - (int64_t)cl_i;  // contribution = min(x, Penc) - w when clamped
       if (P <= 0) {
         always = true;  // x >= P for every spec
-      } else {
+      } else if (w != 0) {
         // c <= U  <=>  floor(fc / c) >= P  and  m <= V  <=>  floor(fm / m) >= P, with
         // U = floor(fc / P), V = floor(fm / P) from the rounded-up reciprocal of P
         // (exact: fc, fm < 2^50, P < 2^51)
         const double rP = recip_up_f64((uint64_t)P);
         const uint32_t U = (uint32_t)((double)fc_ok * rP);
         const int64_t V = (int64_t)((double)fm_ok * rP);
-        uint32_t L = 0, b = 0;
         if (U >= cmin && V >= mmin) {  // else no spec is dominated
+          uint32_t L, b;
 #ifdef KCC_DIAG_NO_SEARCH  // diagnostic timing build only: results are wrong
           L = U % (uint32_t)(nN + 1);
           b = (uint32_t)(V % (nN + 1));
@@ -552,15 +583,17 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
             b = upper_bound_count(cw.ms, nN, V);
           }
 #endif
-        }
-        if (L > 0 && b > 0 && w != 0) {
-          const uint32_t G = L >> 6, r = L & 63u;
+          const uint32_t G = L >> 6, r = L & 63u;  // L >= 1, b >= 1 (U >= cmin, V >= mmin)
 #ifndef KCC_DIAG_NO_H_ATOMIC  // diagnostic timing build only: results are wrong
           if (G > 0) atomic_add_u64(reinterpret_cast<uint64_t*>(&Hc[G * hw + b]), (uint64_t)w);
+          if (r > 0) {
+            const uint32_t kq = lds ? group_count64(gml_l + 64 * G, b)
+                                    : group_count64(cw.gml + 64 * G, b);
+            if (kq > 0)
+              atomic_add_u64(reinterpret_cast<uint64_t*>(&H2c[((int64_t)G * 64 + r) * 65 + kq]),
+                             (uint64_t)w);
+          }
 #endif
-          in_plist = r != 0;
-          key = G << 6 | r;
-          bnd = b;
         }
       }
     }
@@ -570,37 +603,16 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
       if (lane == 0 && v) atomic_add_u64(reinterpret_cast<uint64_t*>(&Hc[T * hw + nN]), v);
     }
-#ifdef KCC_DIAG_NO_PLIST  // diagnostic timing build only: results are wrong
-    in_plist = false;
-#endif
-    {  // plist: this workgroup's rows own slot i0 / PLIST_SLOT (no shared counter)
-      const unsigned long long pm = __ballot(in_plist);
-      if (lane == 0) wcount[wv] = __popcll(pm);
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        unsigned long long tot = 0;
-        for (int k = 0; k < (int)(blockDim.x >> 6); ++k) tot += wcount[k];
-        cw.pcount[i0 / PLIST_SLOT] = (uint32_t)tot;
-      }
-      if (in_plist) {
-        int64_t j = i0;  // the slot's first entry (i0 is a multiple of PLIST_SLOT)
-        for (int k = 0; k < wv; ++k) j += (int64_t)wcount[k];
-        j += __popcll(pm & ((1ull << lane) - 1ull));
-        cw.pkey[j] = key;
-        cw.pb[j] = bnd;
-        cw.pw[j] = (int32_t)w;
-      }
-      __syncthreads();  // wcount is reused by the next iteration
-    }
-    const unsigned long long b = __ballot(valid && !ok);
-    if (b) {
+    const unsigned long long bl = __ballot(valid && !ok);
+    if (bl) {
       unsigned long long base = 0;
       if (lane == 0)
-        base = atomicAdd(&counters[CNT_SLOW_ROWS + chunk], (unsigned long long)__popcll(b));
+        base = atomicAdd(&counters[CNT_SLOW_ROWS + chunk], (unsigned long long)__popcll(bl));
       base = __shfl(base, 0);
-      if (valid && !ok) slow_list[base + __popcll(b & ((1ull << lane) - 1ull))] = i;
+      if (valid && !ok) slow_list[base + __popcll(bl & ((1ull << lane) - 1ull))] = i;
     }
   }
+  KCC_TL(3072 + blockIdx.x % 1024, 1);
 }
 
 // Smallest f32 >= 1/v (1 <= v < 2^51, exact in f64).  1/v is first rounded to f64,
@@ -614,373 +626,367 @@ __device__ __forceinline__ float recip_up_f32(uint64_t v) {
   return r;
 }
 
-// Single-workgroup stable 3-way partition of the specs (class A, then B, then the
-// exact-path specs), in two passes over contiguous per-thread chunks with one
-// block-wide exclusive scan of the per-class counts in between.  Also zeroes
-// partial[0..2S) and sets the counters (no memset launches).
-__global__ __launch_bounds__(1024) void spec_prep_kernel(int64_t S, const uint64_t* __restrict__ c_in,
-                                                         const int64_t* __restrict__ m_in,
-                                                         SpecPrep sp, ClampWork cw,
-                                                         int64_t* __restrict__ partial,
-                                                         unsigned long long* __restrict__ counters) {
-  __shared__ int64_t wsum[16][2];
+// ---- spec setup: partition + ranks + sorted arrays, one launch --------------------
+constexpr int SPEC_BLOCK = 1024;
+constexpr int SPEC_NW = SPEC_BLOCK / 64;
+constexpr int RANK_SLICES = 4;  // workgroups per block of 64 queries
+
+// Spec setup, three launches (the work is tiny: what costs is dependent memory round
+// trips and device-scope fences, so every thread does one step of one spec and the
+// kernel boundaries carry the results).
+//
+// spec_rank_kernel: (S/64) x RANK_SLICES workgroups of 1024 threads; lane = query spec i
+// (64 per workgroup), the candidates j split over the RANK_SLICES workgroups of a query
+// block, staged in LDS (S <= 8192: 64-bit keys request << 13 | index, one compare per
+// rank) and walked by the 16 waves with broadcast reads.  Per normal query (ties by
+// index):
+//   c-rank(i) = #{normal j : (c_j, j) < (c_i, i)},  m-rank(i) = #{normal j : (m_j, j) < (m_i, i)},
+//   m-less(i) = #{normal j : m_j < m_i},
+// and per query its rank within its class, #{j < i : class(j) == class(i)} (the stable
+// 3-way partition: class A, then B, then the exact-path specs); the waves' counts meet
+// in LDS, then one atomic per query and count into rank[] (zero between calls).  The
+// query block's first workgroup also writes the query's SpecRec by caller index (rec_o)
+// and zeroes its partial[] entries; the first query block counts the classes.
+__global__ __launch_bounds__(SPEC_BLOCK) void spec_rank_kernel(int64_t S, const uint64_t* __restrict__ c_in,
+                                                               const int64_t* __restrict__ m_in,
+                                                               SpecPrep sp, ClampWork cw,
+                                                               int64_t* __restrict__ partial) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t per = (S + 1023) / 1024;
-  const int64_t b0 = tid * per < S ? tid * per : S;
-  const int64_t b1 = b0 + per < S ? b0 + per : S;
-  // up to 8 specs per thread (S <= 8192) stay in registers: all loads issue at once
-  constexpr int REG = 8;
-  const bool in_regs = per <= REG;
-  uint64_t rc_[REG];
-  int64_t rm_[REG];
-  if (in_regs) {
+  KCC_TL(blockIdx.x, 0);
+  constexpr int SLICE_LDS = (int)(8192 / RANK_SLICES);  // staged candidates (S <= 8192)
+  __shared__ uint64_t kc_l[SLICE_LDS], km_l[SLICE_LDS];
+  __shared__ uint8_t cls_l[SLICE_LDS];
+  __shared__ uint32_t part[SPEC_NW][4][64];
+  const int64_t qb = blockIdx.x / RANK_SLICES, sl = blockIdx.x % RANK_SLICES;
+  const int64_t i = qb * 64 + lane;  // this lane's query
+  const bool qv = i < S;
+  const uint64_t c = qv ? c_in[i] : 0;
+  const int64_t m = qv ? m_in[i] : 0;
+  const int32_t ci = qv ? spec_class(c, m) : SPEC_EXACT;
+  const bool qn = qv && ci != SPEC_EXACT;
+  const int64_t j0 = S * sl / RANK_SLICES, j1 = S * (sl + 1) / RANK_SLICES;  // this slice
+  uint32_t rc = 0, rm = 0, ml = 0, cp = 0;
+  if (S <= 8192) {
+    uint32_t na = 0, nb = 0;
+    for (int64_t j = j0 + tid; j < j1; j += SPEC_BLOCK) {  // stage the slice's keys
+      const uint64_t cj = c_in[j];
+      const int64_t mj = m_in[j];
+      const int32_t kj = spec_class(cj, mj);
+      const bool nj = kj != SPEC_EXACT;
+      kc_l[j - j0] = nj ? cj << 13 | (uint64_t)j : ~0ull;
+      km_l[j - j0] = nj ? (uint64_t)mj << 13 | (uint64_t)j : ~0ull;
+      cls_l[j - j0] = (uint8_t)kj;
+      na += kj == SPEC_A ? 1u : 0u;
+      nb += kj == SPEC_B ? 1u : 0u;
+    }
+    if (qb == 0) {  // class totals, one atomic per wave and class
+      uint32_t ta = na, tb = nb;
 #pragma unroll
-    for (int u = 0; u < REG; ++u) {
-      const bool v = b0 + u < b1;
-      rc_[u] = v ? c_in[b0 + u] : 0;
-      rm_[u] = v ? m_in[b0 + u] : 0;
+      for (int d = 32; d >= 1; d >>= 1) {
+        ta += __shfl_xor(ta, d);
+        tb += __shfl_xor(tb, d);
+      }
+      if (lane == 0 && ta) atomicAdd(&cw.sync[1], ta);
+      if (lane == 0 && tb) atomicAdd(&cw.sync[2], tb);
+    }
+    __syncthreads();
+    const uint64_t kc = c << 13 | (uint64_t)i, km = (uint64_t)m << 13 | (uint64_t)i;
+    const uint64_t km0 = (uint64_t)m << 13;
+    const int n = (int)(j1 - j0);
+    const int w0 = n * wv / SPEC_NW, w1 = n * (wv + 1) / SPEC_NW;  // this wave's part
+#pragma unroll 4
+    for (int j = w0; j < w1; ++j) {
+      const uint64_t kcj = kc_l[j], kmj = km_l[j];  // broadcast reads
+      const int32_t kj = cls_l[j];
+      rc += kcj < kc ? 1u : 0u;
+      rm += kmj < km ? 1u : 0u;
+      ml += kmj < km0 ? 1u : 0u;
+      cp += (kj == ci && j0 + j < i) ? 1u : 0u;
+    }
+  } else {  // straight from memory (large S)
+    const int64_t n = j1 - j0;
+    uint32_t na = 0, nb = 0;
+    for (int64_t j = j0 + n * wv / SPEC_NW; j < j0 + n * (wv + 1) / SPEC_NW; ++j) {
+      const uint64_t cj = c_in[j];
+      const int64_t mj = m_in[j];
+      const int32_t kj = spec_class(cj, mj);
+      na += kj == SPEC_A ? 1u : 0u;
+      nb += kj == SPEC_B ? 1u : 0u;
+      cp += (kj == ci && j < i) ? 1u : 0u;
+      if (kj == SPEC_EXACT) continue;  // wave-uniform
+      rc += (cj < c || (cj == c && j < i)) ? 1u : 0u;
+      rm += (mj < m || (mj == m && j < i)) ? 1u : 0u;
+      ml += mj < m ? 1u : 0u;
+    }
+    if (qb == 0 && lane == 0) {  // wave-uniform counts
+      if (na) atomicAdd(&cw.sync[1], na);
+      if (nb) atomicAdd(&cw.sync[2], nb);
     }
   }
-  auto spec_c = [&](int64_t i) -> uint64_t {
-    if (in_regs) {
-      uint64_t r = 0;
-#pragma unroll
-      for (int u = 0; u < REG; ++u) r = (i - b0 == u) ? rc_[u] : r;  // static indices only
-      return r;
-    }
-    return c_in[i];
-  };
-  auto spec_m = [&](int64_t i) -> int64_t {
-    if (in_regs) {
-      int64_t r = 0;
-#pragma unroll
-      for (int u = 0; u < REG; ++u) r = (i - b0 == u) ? rm_[u] : r;
-      return r;
-    }
-    return m_in[i];
-  };
-  int64_t cnt[2] = {0, 0};  // class A, class B
-  for (int64_t i = b0; i < b1; ++i) {
-    const int32_t k = spec_class(spec_c(i), spec_m(i));
-    cnt[0] += k == SPEC_A ? 1 : 0;
-    cnt[1] += k == SPEC_B ? 1 : 0;
-  }
-  // block exclusive scans of both counts (wave shuffles + 16 wave totals in LDS)
-  int64_t incl[2] = {cnt[0], cnt[1]};
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int64_t u = __shfl_up(incl[q], d);
-      if (lane >= d) incl[q] += u;
-    }
-  }
-  if (lane == 63) {
-    wsum[wv][0] = incl[0];
-    wsum[wv][1] = incl[1];
-  }
+  part[wv][0][lane] = rc;
+  part[wv][1][lane] = rm;
+  part[wv][2][lane] = ml;
+  part[wv][3][lane] = cp;
   __syncthreads();
-  int64_t wbase[2] = {0, 0}, tot[2] = {0, 0};
-  for (int k = 0; k < 16; ++k) {
+  if (wv < 4 && qv && (qn || wv == 3)) {  // wave r adds count r (the class rank for all)
+    uint32_t t = 0;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (k < wv) wbase[q] += wsum[k][q];
-      tot[q] += wsum[k][q];
-    }
+    for (int k = 0; k < SPEC_NW; ++k) t += part[k][wv][lane];
+    if (t) atomicAdd(&cw.rank[(int64_t)wv * S + i], t);
   }
-  const int64_t ea = wbase[0] + incl[0] - cnt[0], eb = wbase[1] + incl[1] - cnt[1];
-  int64_t pa = ea;                         // my first class-A slot
-  int64_t pb = tot[0] + eb;                // my first class-B slot
-  int64_t px = tot[0] + tot[1] + (b0 - ea - eb);  // my first exact-path slot
-  for (int64_t i = b0; i < b1; ++i) {
-    const uint64_t c = spec_c(i);
-    const int64_t m = spec_m(i);
-    const int32_t k = spec_class(c, m);
-    const int64_t pos = k == SPEC_A ? pa++ : (k == SPEC_B ? pb++ : px++);
+  if (sl == 0 && wv == 4 && qv) {  // the query's SpecRec fields, by caller index
     SpecRec r;
     r.c = c;
     r.m = m;
-    r.rc = k != SPEC_EXACT ? recip_up_f64(c) : 0.0;
-    r.rm = k != SPEC_EXACT ? recip_up_f64((uint64_t)m) : 0.0;
-    r.rcf = k == SPEC_A ? recip_up_f32(c) : 0.0f;
-    r.cls = k;
+    r.rc = qn ? recip_up_f64(c) : 0.0;
+    r.rm = qn ? recip_up_f64((uint64_t)m) : 0.0;
+    r.rcf = ci == SPEC_A ? recip_up_f32(c) : 0.0f;
+    r.cls = ci;
     r.pad = 0;
-    sp.rec[pos] = r;
-    sp.perm[pos] = (int32_t)i;
+    sp.rec_o[i] = r;
   }
-  for (int64_t i = tid; i < 2 * S; i += 1024) partial[i] = 0;
-  for (int64_t i = tid; i < 3 * S; i += 1024) cw.rank[i] = 0;
-  if (tid < CNT_N)
-    counters[tid] = tid == CNT_SPECS_A ? (unsigned long long)tot[0]
-                  : tid == CNT_SPECS_B ? (unsigned long long)tot[1] : 0ull;
+  if (sl == 0 && wv == 5 && qv) {
+    partial[i] = 0;
+    partial[S + i] = 0;
+  }
+  KCC_TL(blockIdx.x, 1);
 }
 
-// ---- clamp correction (see ClampWork in kcc_internal.h) ----------
+// spec_place_kernel: one thread per spec (caller index i): SpecRec / perm at the
+// partitioned position, and for the normal specs cs, dperm, m_less (by c-rank) and ms;
+// zeroes the spec's rank[] entries; thread 0 sets the counters.
+__global__ __launch_bounds__(256) void spec_place_kernel(int64_t S, SpecPrep sp, ClampWork cw,
+                                                         unsigned long long* __restrict__ counters) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nA = cw.sync[1], nB = cw.sync[2];
+  if (i == 0) {
+    for (int k = 0; k < CNT_N; ++k)
+      counters[k] = k == CNT_SPECS_A ? (unsigned long long)nA
+                  : k == CNT_SPECS_B ? (unsigned long long)nB : 0ull;
+  }
+  if (i >= S) return;
+  typedef uint64_t u64x2_t __attribute__((ext_vector_type(2)));
+  const u64x2_t* rec_o = reinterpret_cast<const u64x2_t*>(sp.rec_o);
+  // a SpecRec moves as three 16-B words (c, m | rc, rm | rcf, cls, pad)
+  const u64x2_t w0 = rec_o[3 * i], w1 = rec_o[3 * i + 1], w2 = rec_o[3 * i + 2];
+  const uint32_t q = cw.rank[i], mr = cw.rank[S + i], ml = cw.rank[2 * S + i];
+  const uint32_t cp = cw.rank[3 * S + i];
+  const int32_t k = (int32_t)(w2.x >> 32);
+  const int64_t pos = k == SPEC_A ? cp : (k == SPEC_B ? nA + cp : (int64_t)nA + nB + cp);
+  u64x2_t* dst = reinterpret_cast<u64x2_t*>(sp.rec + pos);
+  dst[0] = w0;
+  dst[1] = w1;
+  dst[2] = w2;
+  sp.perm[pos] = (int32_t)i;
+  if (k != SPEC_EXACT) {
+    cw.cs[q] = w0.x;
+    cw.dperm[q] = (int32_t)pos;
+    cw.m_less[q] = ml;
+    cw.ms[mr] = (int64_t)w0.y;
+  }
+#pragma unroll
+  for (int r4 = 0; r4 < 4; ++r4) cw.rank[(int64_t)r4 * S + i] = 0;
+}
 
-// Ranks of the normal specs (internal positions [0, nN)) among themselves, by brute
-// force over a 2-D grid of 256 x CLAMP_RANK_TILE tiles (exact, order-free atomics):
-//   c-rank(p) = #{q : (c_q, q) < (c_p, p)},  m-rank(p) = #{q : (m_q, q) < (m_p, p)},
-//   m-less(p) = #{q : m_q < m_p}
-constexpr int CLAMP_RANK_TILE = 64;
-__global__ __launch_bounds__(256) void clamp_rank_kernel(const SpecRec* __restrict__ rec,
-                                                         ClampWork cw, int64_t S,
-                                                         const unsigned long long* __restrict__ counters) {
+// spec_groups_kernel: one 1024-thread workgroup per group g of 64 c-ranks: each spec's
+// position in the group's m_less order (keys m_less << 6 | lane), counted by 16 threads
+// over 4 candidates each: kpos by c-rank, gml (the group's m_less ascending, 0xffffffff
+// padding).  Workgroup 0 zeroes the class counts of spec_rank (read by spec_place).
+__global__ __launch_bounds__(1024) void spec_groups_kernel(ClampWork cw,
+                                                           const unsigned long long* __restrict__ counters) {
   const int64_t nN = clamp_n_normal(counters);
-  const int64_t p0 = (int64_t)blockIdx.x * 256, q0 = (int64_t)blockIdx.y * CLAMP_RANK_TILE;
-  if (p0 >= nN || q0 >= nN) return;  // whole block
-  __shared__ uint64_t cq[CLAMP_RANK_TILE];
-  __shared__ int64_t mq[CLAMP_RANK_TILE];
-  const int t = threadIdx.x;
-  if (t < CLAMP_RANK_TILE) {
-    const int64_t q = q0 + t;
-    cq[t] = q < nN ? rec[q].c : ~0ull;
-    mq[t] = q < nN ? rec[q].m : INT64_MAX;
+  const int64_t g = blockIdx.x;
+  if (g == 0 && threadIdx.x < 2) cw.sync[1 + threadIdx.x] = 0u;
+  if (g * 64 >= nN) return;  // whole block
+  __shared__ uint32_t key_l[64];
+  __shared__ uint32_t cnt_l[16][64];
+  const int tid = threadIdx.x, l = tid & 63, p = tid >> 6;
+  const uint32_t pad = (1u << 26) - 1;  // sorts last
+  if (tid < 64) {
+    const int64_t q = 64 * g + tid;
+    key_l[tid] = (q < nN ? cw.m_less[q] : pad) << 6 | (uint32_t)tid;
   }
   __syncthreads();
-  const int64_t p = p0 + t;
-  if (p >= nN) return;
-  const uint64_t c = rec[p].c;
-  const int64_t m = rec[p].m;
-  const int qn = (int)(nN - q0 < CLAMP_RANK_TILE ? nN - q0 : CLAMP_RANK_TILE);
-  uint32_t rc = 0, rm = 0, ml = 0;
-  for (int j = 0; j < qn; ++j) {
-    const bool before = q0 + j < p;
-    rc += (cq[j] < c || (cq[j] == c && before)) ? 1u : 0u;
-    rm += (mq[j] < m || (mq[j] == m && before)) ? 1u : 0u;
-    ml += mq[j] < m ? 1u : 0u;
-  }
-  if (rc) atomicAdd(&cw.rank[p], rc);
-  if (rm) atomicAdd(&cw.rank[S + p], rm);
-  if (ml) atomicAdd(&cw.rank[2 * S + p], ml);
-}
-
-// Sorted arrays from the ranks; zero the used part of H.
-__global__ void clamp_scatter_kernel(const SpecRec* __restrict__ rec, ClampWork cw, int64_t S,
-                                     const unsigned long long* __restrict__ counters) {
-  const int64_t nN = clamp_n_normal(counters);
-  const int64_t T = (nN + 63) / 64;
-  const int64_t cells = (T + 1) * (nN + 1);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells || i < nN; i += stride) {
-    if (i < cells) {
+  const uint32_t key = key_l[l];
+  uint32_t c = 0;
 #pragma unroll
-      for (int k = 1; k < H_COPIES; ++k) cw.H[k * cw.h_stride + i] = 0;
-    }
-    if (i < nN) {
-      const uint32_t d = cw.rank[i];
-      cw.cs[d] = rec[i].c;
-      cw.dperm[d] = (int32_t)i;
-      cw.m_less[d] = cw.rank[2 * S + i];
-      cw.ms[cw.rank[S + i]] = rec[i].m;
-    }
-    if (i < cells) cw.H[i] = 0;
+  for (int u = 0; u < 4; ++u) c += key_l[4 * p + u] < key ? 1u : 0u;
+  cnt_l[p][l] = c;
+  __syncthreads();
+  if (tid < 64) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) pos += cnt_l[k][tid];
+    const int64_t q = 64 * g + tid;
+    if (q < nN) cw.kpos[q] = (uint8_t)pos;
+    cw.gml[64 * g + pos] = q < nN ? (key >> 6) : 0xffffffffu;
   }
 }
 
-// 2-D suffix sums of H, step 0: the XCD copies summed into copy 0 (all cells in parallel)
-__global__ void clamp_hsum_kernel(ClampWork cw, const unsigned long long* __restrict__ counters) {
-  const int64_t nN = clamp_n_normal(counters);
-  const int64_t cells = ((nN + 63) / 64 + 1) * (nN + 1);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cells; i += stride) {
-    uint64_t v = 0;
-#pragma unroll
-    for (int c = 0; c < H_COPIES; ++c) v += (uint64_t)cw.H[c * cw.h_stride + i];
-    cw.H[i] = (int64_t)v;
-  }
-}
+// ---- clamp correction: D_s and partial[s] -= D_s ------------------------------------
 
-// step 1: down each column (G from T to 0), one thread per column, eight rows' loads
-// in flight at a time
-__global__ __launch_bounds__(64) void clamp_hcol_kernel(ClampWork cw,
-                                                        const unsigned long long* __restrict__ counters) {
-  const int64_t nN = clamp_n_normal(counters);
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (nN == 0 || b > nN) return;
-  const int64_t T = (nN + 63) / 64, w = nN + 1;
-  uint64_t run = 0;
-  for (int64_t G0 = T; G0 >= 0; G0 -= 8) {
-    uint64_t v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = G0 - k >= 0 ? (uint64_t)cw.H[(G0 - k) * w + b] : 0ull;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      run += v[k];
-      if (G0 - k >= 0) cw.H[(G0 - k) * w + b] = (int64_t)run;
-    }
-  }
-}
-
-// step 2: along each row (b from nN to 0), one 1024-thread workgroup per row, in tiles
-// of 1024 from the end (wave suffix scans + a carry)
-__global__ __launch_bounds__(1024) void clamp_hrow_kernel(ClampWork cw,
+// Tile (G, t) of H (every copy summed, then zeroed) -> R[G][b] = Σ_{b' >= b in the tile}
+// H[G][b'] and Rtot[G][t] = the tile's total; grid (T+1, rtiles), 1024 threads.
+__global__ __launch_bounds__(1024) void clamp_rows_kernel(ClampWork cw,
                                                           const unsigned long long* __restrict__ counters) {
   const int64_t nN = clamp_n_normal(counters);
-  const int64_t G = blockIdx.x;
-  const int64_t T = (nN + 63) / 64;
-  if (nN == 0 || G > T) return;  // whole block
+  const int64_t G = blockIdx.x, t = blockIdx.y;
+  const int64_t T = (nN + 63) / 64, w = nN + 1;
+  if (nN == 0 || G > T || t * CLAMP_RTILE >= w) return;  // whole block
   __shared__ uint64_t wtot[16];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t w = nN + 1;
-  int64_t* row = cw.H + G * w;
-  uint64_t carry = 0;
-  for (int64_t end = w; end > 0; end -= 1024) {
-    const int64_t i = end - 1 - tid;  // thread tid walks the row backwards
-    uint64_t v = i >= 0 ? (uint64_t)row[i] : 0ull;
+  KCC_TL(2048 + (G * 8 + t) % 1024, 0);
+  const int64_t end = (t + 1) * CLAMP_RTILE < w ? (t + 1) * CLAMP_RTILE : w;
+  const int64_t i = end - 1 - tid;  // thread tid walks the tile backwards
+  const bool in = i >= t * CLAMP_RTILE;
+  uint64_t v = 0;
+  if (in) {
+    uint64_t h[H_COPIES];
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {  // inclusive scan in thread order = suffix in b
-      const uint64_t u = __shfl_up(v, d);
-      if (lane >= d) v += u;
+    for (int c = 0; c < H_COPIES; ++c) h[c] = (uint64_t)cw.H[c * cw.h_stride + G * w + i];
+#pragma unroll
+    for (int c = 0; c < H_COPIES; ++c) {
+      v += h[c];
+      cw.H[c * cw.h_stride + G * w + i] = 0;  // zero between calls
     }
-    if (lane == 63) wtot[wv] = v;
-    __syncthreads();
-    uint64_t before = 0, all = 0;
-    for (int k = 0; k < 16; ++k) {
-      if (k < wv) before += wtot[k];
-      all += wtot[k];
-    }
-    if (i >= 0) row[i] = (int64_t)(v + before + carry);
-    carry += all;
-    __syncthreads();
   }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {  // inclusive scan in thread order = suffix in b
+    const uint64_t u = __shfl_up(v, d);
+    if (lane >= d) v += u;
+  }
+  if (lane == 63) wtot[wv] = v;
+  __syncthreads();
+  uint64_t before = 0, all = 0;
+  for (int k = 0; k < 16; ++k) {
+    if (k < wv) before += wtot[k];
+    all += wtot[k];
+  }
+  if (in) cw.R[G * w + i] = (int64_t)(v + before);
+  if (tid == 0) cw.Rtot[G * cw.rt_stride + t] = (int64_t)all;
+  KCC_TL(2048 + (G * 8 + t) % 1024, 1);
 }
 
-// D_partial: every plist entry (G, r, b, w) adds w to the specs with c-rank 64G + lane,
-// lane < r, and m_less < b.  CLAMP_PARTIAL_WGS workgroups share the entries; each
-// accumulates ALL nN specs in LDS (ds_add_u64; one entry per wave-iteration, lanes =
-// the entry's group) and writes its row of dpart[CLAMP_PARTIAL_WGS][nN]; clamp_full
-// sums the rows.  nN <= CLAMP_LDS_SPECS (else clamp_partial_big_kernel).
-constexpr int CLAMP_PARTIAL_WGS = (int)CLAMP_PARTIAL_ROWS;
-constexpr int CLAMP_PARTIAL_MAX_SLOTS = 1024;  // per workgroup (n_nodes <= 256 x 1024 x 1024)
-static_assert(CLAMP_PARTIAL_WGS % 64 == 0, "clamp_full sums the rows in 8 splits, 8 at a time");
-__global__ __launch_bounds__(1024) void clamp_partial_kernel(ClampWork cw,
-                                                             const unsigned long long* __restrict__ counters,
-                                                             int64_t n_nodes, int64_t* __restrict__ dpart) {
-  const int64_t nN = clamp_n_normal(counters);
-  if (nN == 0 || nN > CLAMP_LDS_SPECS) return;
-  __shared__ uint32_t ml_l[CLAMP_LDS_SPECS];
-  __shared__ unsigned long long acc_l[CLAMP_LDS_SPECS];
-  for (int64_t q = threadIdx.x; q < nN; q += blockDim.x) {
-    ml_l[q] = cw.m_less[q];
-    acc_l[q] = 0;
+// inclusive suffix sum over the 64 lanes (lane k: Σ_{k' >= k})
+__device__ __forceinline__ uint64_t wave_suffix_u64(uint64_t v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t u = __shfl_down(v, d);
+    if (lane + d < 64) v += u;
   }
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int32_t wv = __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6));
-  const int32_t nw = (int32_t)(blockDim.x >> 6);
-  // this workgroup's plist slots [s0, s1), their entries taken as one sequence in
-  // 64-entry batches by the workgroup's waves (slot counts prefix-summed in LDS)
-  __shared__ uint32_t spre[CLAMP_PARTIAL_MAX_SLOTS + 1];
-  const int64_t n_slots = (n_nodes + PLIST_SLOT - 1) / PLIST_SLOT;
-  const int64_t s0 = n_slots * blockIdx.x / CLAMP_PARTIAL_WGS, s1 = n_slots * (blockIdx.x + 1) / CLAMP_PARTIAL_WGS;
-  const int ns = (int)(s1 - s0);  // <= CLAMP_PARTIAL_MAX_SLOTS (host-checked)
-  if (threadIdx.x == 0) {
-    uint32_t run = 0;
-    for (int k = 0; k < ns; ++k) {
-      spre[k] = run;
-      run += cw.pcount[s0 + k];
-    }
-    spre[ns] = run;
-  }
-  __syncthreads();
-  const int64_t n_ent = spre[ns];
-  for (int64_t e0 = (int64_t)wv * 64; e0 < n_ent; e0 += (int64_t)nw * 64) {
-    const int64_t e = e0 + lane;
-    int k = 0;  // slot of entry e (lanes of one batch span at most a few slots)
-    while (k + 1 < ns && (int64_t)spre[k + 1] <= e) ++k;
-    const bool in = e < n_ent;
-    const int64_t j = (s0 + k) * PLIST_SLOT + (e - (int64_t)spre[k]);
-    const uint32_t key_v = in ? cw.pkey[j] : 0u, bnd_v = in ? cw.pb[j] : 0u;
-    const int32_t w_v = in ? cw.pw[j] : 0;
-    const int cnt = (int)(n_ent - e0 < 64 ? n_ent - e0 : 64);
-    // 64 entries by one coalesced load each, walked lane by lane from registers
-    for (int kk = 0; kk < cnt; ++kk) {
-      const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)key_v, kk);
-      const uint32_t bnd = (uint32_t)__builtin_amdgcn_readlane((int)bnd_v, kk);
-      const int32_t w = __builtin_amdgcn_readlane(w_v, kk);
-      const int64_t q = (int64_t)(key >> 6) * 64 + lane;
-      if ((uint32_t)lane < (key & 63u) && ml_l[q] < bnd)
-        atomicAdd(&acc_l[q], (unsigned long long)(int64_t)w);
-    }
-  }
-  __syncthreads();
-  for (int64_t q = threadIdx.x; q < nN; q += blockDim.x)
-    dpart[(int64_t)blockIdx.x * nN + q] = (int64_t)acc_l[q];
+  return v;
 }
 
-// the same for nN > CLAMP_LDS_SPECS: one wavefront per (group, slice of the plist),
-// lanes = the group's 64 c-ranks; scans the 4-B keys, reads b / w only for matches,
-// and subtracts straight from partial
-constexpr int CLAMP_SLICES = 512;
-__global__ __launch_bounds__(64) void clamp_partial_big_kernel(ClampWork cw,
-                                                               const unsigned long long* __restrict__ counters,
-                                                               int64_t S, int64_t n_nodes,
-                                                               int64_t* __restrict__ partial) {
+// One workgroup per group g of 64 c-ranks: the group's H2 table (copies summed, then
+// zeroed) -> its 2-D suffix sums S2 in LDS; for each spec of the group (c-rank
+// q = 64g + l, kpos = its position in the group's m_less order)
+//   D = Σ_{G > g} R[G][m_less + 1]  +  S2[l + 1][kpos + 1],
+// R read as the in-tile suffix plus the totals of the later tiles; partial[p] -= D for
+// the normal specs of clamp-free waves.
+constexpr int CG_CELLS = 63 * 65;  // H2 rows r = 1..63
+constexpr int CG_PER = (CG_CELLS + 1023) / 1024;
+__global__ __launch_bounds__(1024) void clamp_groups_kernel(ClampWork cw,
+                                                            const unsigned long long* __restrict__ counters,
+                                                            int64_t S, int64_t* __restrict__ partial) {
   const int64_t nN = clamp_n_normal(counters);
-  if (nN <= CLAMP_LDS_SPECS) return;
-  const int64_t T = (nN + 63) / 64;
+  const int64_t T = (nN + 63) / 64, w = nN + 1;
   const int64_t g = blockIdx.x;
-  if (g >= T) return;
-  const int lane = threadIdx.x;
-  const int64_t q = g * 64 + lane;
-  const bool valid = q < nN;
-  const uint32_t ml = valid ? cw.m_less[q] : 0xffffffffu;
-  const int64_t n_slots = (n_nodes + PLIST_SLOT - 1) / PLIST_SLOT;
-  const int64_t s0 = n_slots * blockIdx.y / CLAMP_SLICES, s1 = n_slots * (blockIdx.y + 1) / CLAMP_SLICES;
-  uint64_t acc = 0;
-  for (int64_t sl = s0; sl < s1; ++sl) {
-    const int64_t j1 = sl * PLIST_SLOT + (int64_t)cw.pcount[sl];
-    for (int64_t jb = sl * PLIST_SLOT; jb < j1; jb += 64) {
-      const int64_t j = jb + lane;
-      const uint32_t key = j < j1 ? cw.pkey[j] : 0xffffffffu;
-      uint64_t mask = __ballot((int64_t)(key >> 6) == g);
-      while (mask) {
-        const int k = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)key, k) & 63u;
-        const int64_t jj = jb + k;
-        const uint32_t bnd = cw.pb[jj];
-        const int32_t w = cw.pw[jj];
-        acc += ((uint32_t)lane < r && ml < bnd) ? (uint64_t)(int64_t)w : 0ull;
+  if (g >= T) return;  // whole block
+  constexpr int NW = 16;
+  constexpr int MAX_RT = 64;  // tiles per row held in LDS (nN < 64 * CLAMP_RTILE)
+  __shared__ uint64_t t2[65][65];  // [r][k]; rows 0 and 64 stay 0
+  __shared__ uint64_t d1p[NW][64];
+  __shared__ uint64_t rts[65][MAX_RT + 1];  // per G <= T (of this call, G > g): Σ tiles > t
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  KCC_TL(1024 + g, 0);
+  const int64_t nt = (w + CLAMP_RTILE - 1) / CLAMP_RTILE;
+  {  // all copies of all this thread's cells first (independent loads), then the zeros
+    uint64_t v[CG_PER] = {};
+#pragma unroll
+    for (int u = 0; u < CG_PER; ++u) {
+      const int cell = tid + 1024 * u;
+      if (cell < CG_CELLS) {
+        const int64_t at = g * 64 * 65 + 65 + cell;  // row r = 1 + cell / 65
+#pragma unroll
+        for (int c = 0; c < H_COPIES; ++c) v[u] += (uint64_t)cw.H2[c * cw.h2_stride + at];
       }
     }
-  }
-  if (valid && acc) {
-    const int32_t p = cw.dperm[q];
-    if (p < clamp_n_pure(nN, S)) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[p]), 0ull - acc);
-  }
-}
-
-// partial[p] -= D(p) = HS[g + 1][m_less + 1] + Σ_k dpart[k][q] for the normal specs of
-// clamp-free waves (q = the spec's c-rank, g = q / 64).  Grid (nN / 64, CLAMP_FULL_SPLIT):
-// split y sums dpart rows [y * R, (y + 1) * R), split 0 also the H term; one atomic each.
-constexpr int CLAMP_FULL_SPLIT = 8;
-__global__ __launch_bounds__(64) void clamp_full_kernel(ClampWork cw,
-                                                        const unsigned long long* __restrict__ counters,
-                                                        int64_t S, const int64_t* __restrict__ dpart,
-                                                        int64_t* __restrict__ partial) {
-  const int64_t nN = clamp_n_normal(counters);
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // c-rank
-  if (q >= nN) return;
-  const int32_t p = cw.dperm[q];
-  if (p >= clamp_n_pure(nN, S)) return;
-  uint64_t d = 0;
-  if (blockIdx.y == 0) {
-    const int64_t T = (nN + 63) / 64, w = nN + 1;
-    const int64_t g1 = (q >> 6) + 1, b1 = (int64_t)cw.m_less[q] + 1;
-    if (g1 <= T && b1 <= nN) d = (uint64_t)cw.H[g1 * w + b1];
-  }
-  if (nN <= CLAMP_LDS_SPECS) {  // the partial kernel's per-workgroup rows, 8 loads in flight
-    constexpr int R = CLAMP_PARTIAL_WGS / CLAMP_FULL_SPLIT;
-    uint64_t part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int k = (int)blockIdx.y * R; k < ((int)blockIdx.y + 1) * R; k += 8) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) part[u] += (uint64_t)dpart[(int64_t)(k + u) * nN + q];
+    for (int u = 0; u < CG_PER; ++u) {
+      const int cell = tid + 1024 * u;
+      if (cell < CG_CELLS) {
+        const int64_t at = g * 64 * 65 + 65 + cell;
+#pragma unroll
+        for (int c = 0; c < H_COPIES; ++c) cw.H2[c * cw.h2_stride + at] = 0;  // zero between calls
+        t2[1 + cell / 65][cell % 65] = v[u];
+      }
     }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) d += part[u];
+    if (tid < 65) {
+      t2[0][tid] = 0;
+      t2[64][tid] = 0;
+    }
   }
-  if (d) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[p]), 0ull - d);
+  const bool rts_lds = nt <= MAX_RT && T < 65;
+  if (rts_lds) {  // the later tiles' totals: one load per thread, then a suffix per row
+    for (int64_t e = tid; e < (T - g) * nt; e += 1024) {
+      const int64_t G = g + 1 + e / nt, t = e % nt;
+      rts[G][t] = (uint64_t)cw.Rtot[G * cw.rt_stride + t];
+    }
+  }
+  // this lane's spec: its m_less, internal position and kpos, loaded up front
+  const int64_t q = 64 * g + lane;
+  const uint32_t ml = q < nN ? cw.m_less[q] : 0u;
+  const int32_t p_q = q < nN ? cw.dperm[q] : 0;
+  const uint32_t kp_q = q < nN ? cw.kpos[q] : 0u;
+  __syncthreads();
+  if (rts_lds && tid < 65 && tid > g && tid <= T) {  // rts[G][t] = Σ_{u > t} Rtot[G][u]
+    uint64_t run = 0;
+    for (int64_t t = nt - 1; t >= 0; --t) {
+      const uint64_t v = rts[tid][t];
+      rts[tid][t] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  KCC_TL(1024 + g, 1);
+  {  // full groups: Σ_{G > g} R[G][m_less + 1], the waves taking every NW-th G
+    uint64_t d = 0;
+    const int64_t b1 = (int64_t)ml + 1;
+    if (q < nN && b1 <= nN) {
+      const int64_t t1 = b1 / CLAMP_RTILE;
+      for (int64_t G = g + 1 + wv; G <= T; G += NW) {
+        d += (uint64_t)cw.R[G * w + b1];
+        if (rts_lds) {
+          d += rts[G][t1];
+        } else {
+          for (int64_t t = t1 + 1; t < nt; ++t) d += (uint64_t)cw.Rtot[G * cw.rt_stride + t];
+        }
+      }
+    }
+    d1p[wv][lane] = d;
+  }
+  for (int r = wv; r < 65; r += NW) {  // suffix over k within each row (k = 64 on top)
+    const uint64_t top = t2[r][64];
+    const uint64_t v = wave_suffix_u64(t2[r][lane], lane);
+    t2[r][lane] = v + top;
+  }
+  __syncthreads();
+  for (int k = wv; k < 65; k += NW) {  // suffix over r within each column (r = 64 on top)
+    const uint64_t top = t2[64][k];
+    const uint64_t v = wave_suffix_u64(t2[lane][k], lane);
+    t2[lane][k] = v + top;
+  }
+  __syncthreads();
+  KCC_TL(1024 + g, 2);
+  if (wv == 0 && q < nN) {
+    const int32_t p = p_q;
+    if (p < clamp_n_pure(nN, S)) {
+      uint64_t d = t2[lane + 1][kp_q + 1];
+#pragma unroll
+      for (int k = 0; k < NW; ++k) d += d1p[k][lane];
+      if (d) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[p]), 0ull - d);
+    }
+  }
 }
 
 // Lane = spec (its request, reciprocals and running total live in VGPRs); the node
@@ -1316,15 +1322,15 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
-                            SlowNode* slow, int64_t* slow_list, ClampWork cw,
+                            SlowNode* slow, int64_t* slow_list, int64_t n_specs, ClampWork cw,
                             unsigned long long* counters, int chunk, hipStream_t s) {
   if (n_nodes <= 0) return hipSuccess;
   hipLaunchKernelGGL(node_prep_kernel,
                      dim3(grid_for(fit_groups(n_nodes) * FIT_GROUP, KCC_NODE_PREP_BLOCK,
                                    KCC_NODE_PREP_GRID)),
-                     dim3(KCC_NODE_PREP_BLOCK), (size_t)(12 * CLAMP_LDS_SPECS), s,
+                     dim3(KCC_NODE_PREP_BLOCK), (size_t)(14 * CLAMP_LDS_SPECS), s,
                      n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu, used_mem,
-                     fast_a, fast_b, slow, slow_list, cw, counters, (int32_t)chunk);
+                     fast_a, fast_b, slow, slow_list, n_specs, cw, counters, (int32_t)chunk);
   return hipGetLastError();
 }
 
@@ -1332,44 +1338,25 @@ hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu, const int
                             SpecPrep sp, ClampWork cw, int64_t* partial,
                             unsigned long long* counters, hipStream_t s) {
   if (n_specs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(spec_prep_kernel, dim3(1), dim3(1024), 0, s, n_specs, spec_cpu, spec_mem,
-                     sp, cw, partial, counters);
-  return hipGetLastError();
-}
-
-hipError_t launch_clamp_specs(int64_t n_specs, SpecPrep sp, ClampWork cw,
-                              const unsigned long long* counters, hipStream_t s) {
-  if (n_specs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(clamp_rank_kernel,
-                     dim3((unsigned)((n_specs + 255) / 256),
-                          (unsigned)((n_specs + CLAMP_RANK_TILE - 1) / CLAMP_RANK_TILE)),
-                     dim3(256), 0, s, sp.rec, cw, n_specs, counters);
-  hipLaunchKernelGGL(clamp_scatter_kernel, dim3(grid_for(clamp_h_cells(n_specs), 256, 2048)),
-                     dim3(256), 0, s, sp.rec, cw, n_specs, counters);
-  return hipGetLastError();
-}
-
-hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
-                              const unsigned long long* counters, int64_t* partial, hipStream_t s) {
-  if (n_specs <= 0 || n_nodes <= 0) return hipSuccess;
-  if ((n_nodes + PLIST_SLOT - 1) / PLIST_SLOT > (int64_t)CLAMP_PARTIAL_WGS * CLAMP_PARTIAL_MAX_SLOTS)
-    return hipErrorInvalidValue;  // > 2^28 nodes on one device
-  const int64_t t_max = (n_specs + 63) / 64;
-  hipLaunchKernelGGL(clamp_hsum_kernel, dim3(grid_for(clamp_h_cells(n_specs), 256, 2048)),
-                     dim3(256), 0, s, cw, counters);
-  hipLaunchKernelGGL(clamp_hcol_kernel, dim3(grid_for(n_specs + 1, 64, 1 << 30)), dim3(64), 0, s,
+  const int64_t blocks = (n_specs + 63) / 64 * RANK_SLICES;
+  if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(spec_rank_kernel, dim3((unsigned)blocks), dim3(SPEC_BLOCK), 0, s, n_specs,
+                     spec_cpu, spec_mem, sp, cw, partial);
+  hipLaunchKernelGGL(spec_place_kernel, dim3(grid_for(n_specs, 256, 1 << 30)), dim3(256), 0, s,
+                     n_specs, sp, cw, counters);
+  hipLaunchKernelGGL(spec_groups_kernel, dim3((unsigned)((n_specs + 63) / 64)), dim3(1024), 0, s,
                      cw, counters);
-  hipLaunchKernelGGL(clamp_hrow_kernel, dim3((unsigned)(t_max + 1)), dim3(1024), 0, s, cw,
-                     counters);
-  if (n_specs <= CLAMP_LDS_SPECS) {
-    hipLaunchKernelGGL(clamp_partial_kernel, dim3(CLAMP_PARTIAL_WGS), dim3(1024), 0, s, cw,
-                       counters, n_nodes, cw.dpart);
-  } else {
-    hipLaunchKernelGGL(clamp_partial_big_kernel, dim3((unsigned)t_max, CLAMP_SLICES), dim3(64), 0,
-                       s, cw, counters, n_specs, n_nodes, partial);
-  }
-  hipLaunchKernelGGL(clamp_full_kernel, dim3(grid_for(n_specs, 64, 1 << 30), CLAMP_FULL_SPLIT),
-                     dim3(64), 0, s, cw, counters, n_specs, cw.dpart, partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_clamp_apply(int64_t n_specs, ClampWork cw,
+                              const unsigned long long* counters, int64_t* partial, hipStream_t s) {
+  if (n_specs <= 0) return hipSuccess;
+  const int64_t t_max = (n_specs + 63) / 64;
+  hipLaunchKernelGGL(clamp_rows_kernel, dim3((unsigned)(t_max + 1), (unsigned)clamp_rtiles(n_specs)),
+                     dim3(1024), 0, s, cw, counters);
+  hipLaunchKernelGGL(clamp_groups_kernel, dim3((unsigned)t_max), dim3(1024), 0, s, cw, counters,
+                     n_specs, partial);
   return hipGetLastError();
 }
 
@@ -1414,3 +1401,14 @@ hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial, const in
 }
 
 }  // namespace kcc
+
+#ifdef KCC_TIMELINE
+// diagnostic builds only: copy the timeline stamps (4096 x 4 u64) to `host`, then zero them
+extern "C" int kcc_debug_timeline(void* host) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(kcc::kcc_tl), sizeof(uint64_t) * 4096 * 4) != hipSuccess)
+    return -2;
+  static uint64_t zero[4096][4];
+  return hipMemcpyToSymbol(HIP_SYMBOL(kcc::kcc_tl), zero, sizeof(zero)) == hipSuccess ? 0 : -3;
+}
+#endif

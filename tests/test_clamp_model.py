@@ -9,15 +9,42 @@ w = P - cl (= podCount) wherever x >= P.  The correction subtracts, per spec,
 computed as a 2-D dominance count: x >= P <=> c_s <= U_i = fc_i // P_i and
 m_s <= V_i = fm_i // P_i (P_i >= 1; P_i <= 0 rows are clamped for every spec).  This
 module restates the kernels' algorithm in numpy — c-ranks in groups of 64, the
-(T+1) x (nN+1) table H of fully covered groups with its 2-D suffix sums, and the plist
-of partially covered groups — and checks it against the direct definition, then the
-whole per-spec total against the C oracle.
+(T+1) x (nN+1) table H of fully covered groups read through its row suffix sums R
+(clamp_rows_kernel), and per group the 64 x 65 table H2 of partially covered groups
+indexed by (r, k), k = #{group specs with m_less < b}, read through its 2-D suffix sums
+(clamp_groups_kernel) — and checks it against the direct definition, then the whole
+per-spec total against the C oracle.
 """
 import numpy as np
 import pytest
 
 # uint64 sums wrap on purpose (Go's int64 arithmetic)
 pytestmark = pytest.mark.filterwarnings("ignore:overflow encountered:RuntimeWarning")
+
+INF32 = 0xFFFFFFFF
+
+
+def group_orders(mlq, nN):
+    """spec_prep_kernel / clamp_group_kernel: per group of 64 c-ranks, each spec's
+    position in the group's m_less order (ties by lane) and the ascending m_less list."""
+    T = (nN + 63) // 64
+    kpos = np.zeros(nN, np.int64)
+    gml = np.full(64 * T, INF32, np.int64)
+    for g in range(T):
+        v = np.full(64, INF32, np.int64)
+        n = min(64, nN - 64 * g)
+        v[:n] = mlq[64 * g: 64 * g + n]
+        pos = np.empty(64, np.int64)
+        pos[np.lexsort((np.arange(64), v))] = np.arange(64)
+        kpos[64 * g: 64 * g + n] = pos[:n]
+        gml[64 * g + pos] = v
+    return kpos, gml
+
+
+def suffix2(a):
+    """2-D suffix sums over the last two axes (wrapping uint64)."""
+    a = a[..., ::-1, :].cumsum(axis=-2, dtype=np.uint64)[..., ::-1, :]
+    return a[..., ::-1].cumsum(axis=-1, dtype=np.uint64)[..., ::-1]
 
 
 def clamp_correction(U, V, w, always, c, m):
@@ -27,9 +54,10 @@ def clamp_correction(U, V, w, always, c, m):
     order_c = np.lexsort((np.arange(nN), c))          # c-rank -> spec (ties by position)
     cs = c[order_c]
     ms = np.sort(m, kind="stable")
-    m_less = np.searchsorted(ms, m, side="left")      # #specs with a smaller m
+    mlq = np.searchsorted(ms, m, side="left")[order_c]  # by c-rank: #specs with a smaller m
+    kpos, gml = group_orders(mlq, nN)
     H = np.zeros((T + 1, nN + 1), np.uint64)
-    plist = []
+    H2 = np.zeros((T, 65, 65), np.uint64)             # [G][r][k], rows r = 0 and 64 empty
     for Ui, Vi, wi, al in zip(U, V, w, always):
         wi = np.uint64(np.int64(wi).view(np.uint64))
         if al:
@@ -43,20 +71,21 @@ def clamp_correction(U, V, w, always, c, m):
         if G:
             H[G, b] += wi
         if r:
-            plist.append((G, r, b, wi))
-    HS = H[::-1].cumsum(axis=0, dtype=np.uint64)[::-1]            # suffix over G
-    HS = HS[:, ::-1].cumsum(axis=1, dtype=np.uint64)[:, ::-1]     # suffix over b
+            k = int((gml[64 * G: 64 * G + 64] < b).sum())
+            if k:
+                H2[G, r, k] += wi
+    R = H[:, ::-1].cumsum(axis=1, dtype=np.uint64)[:, ::-1]   # clamp_rows_kernel
+    S2 = suffix2(H2)                                          # clamp_groups_kernel
     D = np.zeros(nN, np.uint64)
-    for q in range(nN):                                            # full groups
+    for q in range(nN):
         s = order_c[q]
-        g1, b1 = (q >> 6) + 1, m_less[s] + 1
-        if g1 <= T and b1 <= nN:
-            D[s] += HS[g1, b1]
-    for G, r, b, wi in plist:                                      # partial groups
-        for lane in range(r):
-            s = order_c[64 * G + lane]
-            if m_less[s] < b:
-                D[s] += wi
+        g, lane = q >> 6, q & 63
+        b1 = mlq[q] + 1
+        d = np.uint64(0)
+        if b1 <= nN:
+            d += R[g + 1:, b1].sum(dtype=np.uint64)
+        d += S2[g, lane + 1, kpos[q] + 1]
+        D[s] = d
     return D.view(np.int64)
 
 

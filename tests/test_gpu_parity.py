@@ -99,6 +99,24 @@ def test_capacity_vs_oracle(engine, cfg):
     np.testing.assert_array_equal(t, ot)
 
 
+@pytest.mark.parametrize("s,adv", [(64, False), (4095, False), (4096, False), (4097, False),
+                                   (6000, False), (4100, True), (6000, True)])
+def test_spec_count_clamp_paths(engine, s, adv):
+    """Spec counts around the LDS sort / search tables (<= 4096 normal specs: one-workgroup
+    bitonic sort; more: the rank kernels and global searches), with heavy ties."""
+    c = synth.make_cluster(2_500, 50_000, seed=11, chunk=1024)
+    sc, sm = synth.make_specs(s, seed=11, adversarial=adv)
+    sc[::3] = sc[0]
+    sm[::5] = sm[1]
+    sc[1::7] = sc[2]
+    t, e = engine.capacity(c.node_ptr, c.cpu_req, c.mem_req, c.alloc_cpu, c.alloc_mem,
+                           c.alloc_pods, c.pod_count, sc, sm)
+    uc, um, _, _ = coracle.reduce_requests(c.node_ptr, c.cpu_req, c.mem_req, c.cpu_lim, c.mem_lim)
+    ot, oe = coracle.fit(c.alloc_cpu, c.alloc_mem, c.alloc_pods, c.pod_count, uc, um, sc, sm, NT)
+    np.testing.assert_array_equal(e, oe)
+    np.testing.assert_array_equal(t, ot)
+
+
 def test_fit_random_raw_rows(engine):
     """Arbitrary 64-bit rows (not derived from a cluster) against the oracle."""
     rng = np.random.default_rng(99)
