@@ -209,7 +209,7 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   void* const before[3] = {dv.c_H.p, dv.c_H2.p, dv.c_rank.p};
   KCC_HIP(ctx, ensure(dv.c_rank, 4 * 4 * S));
   KCC_HIP(ctx, ensure(dv.c_H, 8 * (size_t)kcc::H_COPIES * (size_t)hs));
-  KCC_HIP(ctx, ensure(dv.c_H2, 8 * (size_t)kcc::H_COPIES * (size_t)h2s));
+  KCC_HIP(ctx, ensure(dv.c_H2, 8 * (size_t)kcc::H2_COPIES * (size_t)h2s));
   KCC_HIP(ctx, ensure(dv.c_R, 8 * ((size_t)hs + (size_t)kcc::clamp_rows_max((int64_t)S) * (size_t)rts)));
   if (dv.c_H.p != before[0] || dv.c_H2.p != before[1] || dv.c_rank.p != before[2] ||
       dv.h_stride != hs || dv.h2_stride != h2s)

@@ -141,7 +141,7 @@ struct ClampWork {
   uint32_t* gml;     // [64*T] per group of 64 c-ranks: its m_less values ascending
   uint8_t* kpos;     // [S] by c-rank: the spec's position in its group's gml order
   int64_t* H;        // [H_COPIES][h_stride]: (T+1) x (nN+1)
-  int64_t* H2;       // [H_COPIES][h2_stride]: T x 64 x 65, cell (G*64 + r)*65 + k
+  int64_t* H2;       // [H2_COPIES][h2_stride]: T x 64 x 65, cell (G*64 + r)*65 + k
   int64_t* R;        // [h_stride]: H's rows summed over the copies, suffix sums over b
                      // within tiles of CLAMP_RTILE (clamp_rows)
   int64_t* Rtot;     // [(T+1) x rt_stride]: the tiles' totals
@@ -160,6 +160,10 @@ inline int64_t clamp_h2_cells(int64_t S) { return (S / 64 + 1) * 64 * 65; }
 #define KCC_H_COPIES 8
 #endif
 constexpr int H_COPIES = KCC_H_COPIES;
+#ifndef KCC_H2_COPIES
+#define KCC_H2_COPIES 2
+#endif
+constexpr int H2_COPIES = KCC_H2_COPIES;
 // up to this many specs the spec setup sorts in LDS (one workgroup) and node_prep's
 // search tables live in LDS; larger S takes the brute-force rank kernels and global
 // searches

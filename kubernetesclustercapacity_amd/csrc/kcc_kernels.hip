@@ -455,6 +455,7 @@ __device__ __forceinline__ uint32_t group_count64(const T* a, uint32_t b) {
 // each fast row with P >= 1 adds its weight to one cell of H (full c-rank groups) and
 // one of H2 (its partial group), rows with P <= 0 to H[T][nN] (ClampWork).
 #define KCC_NODE_PREP_BLOCK 1024
+static_assert(CLAMP_LDS_SPECS % KCC_NODE_PREP_BLOCK == 0, "node_prep table fill");
 #ifndef KCC_NODE_PREP_GRID
 #define KCC_NODE_PREP_GRID 512  // workgroups at most (2 per CU, one round; each fills its LDS tables once)
 #endif
@@ -476,9 +477,8 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   const bool slow_all = nN < S;                    // exact-path specs exist
   const int64_t T = (nN + 63) / 64, hw = nN + 1;
   // this workgroup's copies of H and H2: workgroups are dealt round-robin over the XCDs
-  const int64_t copy = (int64_t)(blockIdx.x % H_COPIES);
-  int64_t* Hc = cw.H + copy * cw.h_stride;
-  int64_t* H2c = cw.H2 + copy * cw.h2_stride;
+  int64_t* Hc = cw.H + (int64_t)(blockIdx.x % H_COPIES) * cw.h_stride;
+  int64_t* H2c = cw.H2 + (int64_t)(blockIdx.x % H2_COPIES) * cw.h2_stride;
   // the sorted spec requests of the searches and the groups' m_less orders, in LDS when
   // they fit: c clamped to 2^23 (> every U = fc / P, fc < 2^23) as u32, m as i64, the
   // gml entries as u16 (< 4096, padding 0xffff)
@@ -496,14 +496,23 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
 #else
   if (false) {
 #endif
-    for (int64_t k = threadIdx.x; k < CLAMP_LDS_SPECS; k += blockDim.x) {  // padded: +inf
-      const uint64_t c = k < nN ? cw.cs[k] : ~0ull;
-      cs_l[k] = c < FAST_FC_MAX ? (uint32_t)c : 0xffffffffu;
-      ms_l[k] = k < nN ? cw.ms[k] : INT64_MAX;
+    // every load first (one memory round trip), then the LDS writes
+    constexpr int PER = (int)(CLAMP_LDS_SPECS / KCC_NODE_PREP_BLOCK);
+    uint64_t cv[PER], mv[PER];
+    uint32_t gv[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int64_t k = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
+      cv[u] = k < nN ? cw.cs[k] : ~0ull;  // padded: +inf
+      mv[u] = k < nN ? (uint64_t)cw.ms[k] : (uint64_t)INT64_MAX;
+      gv[u] = k < 64 * T ? cw.gml[k] : 0xffffffffu;
     }
-    for (int64_t k = threadIdx.x; k < 64 * T; k += blockDim.x) {
-      const uint32_t v = cw.gml[k];
-      gml_l[k] = v < 0xffffu ? (uint16_t)v : (uint16_t)0xffffu;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int64_t k = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
+      cs_l[k] = cv[u] < FAST_FC_MAX ? (uint32_t)cv[u] : 0xffffffffu;
+      ms_l[k] = (int64_t)mv[u];
+      gml_l[k] = gv[u] < 0xffffu ? (uint16_t)gv[u] : (uint16_t)0xffffu;
     }
   }
   __syncthreads();
@@ -908,7 +917,7 @@ __global__ __launch_bounds__(1024) void clamp_groups_kernel(ClampWork cw,
       if (cell < CG_CELLS) {
         const int64_t at = g * 64 * 65 + 65 + cell;  // row r = 1 + cell / 65
 #pragma unroll
-        for (int c = 0; c < H_COPIES; ++c) v[u] += (uint64_t)cw.H2[c * cw.h2_stride + at];
+        for (int c = 0; c < H2_COPIES; ++c) v[u] += (uint64_t)cw.H2[c * cw.h2_stride + at];
       }
     }
 #pragma unroll
@@ -917,7 +926,7 @@ __global__ __launch_bounds__(1024) void clamp_groups_kernel(ClampWork cw,
       if (cell < CG_CELLS) {
         const int64_t at = g * 64 * 65 + 65 + cell;
 #pragma unroll
-        for (int c = 0; c < H_COPIES; ++c) cw.H2[c * cw.h2_stride + at] = 0;  // zero between calls
+        for (int c = 0; c < H2_COPIES; ++c) cw.H2[c * cw.h2_stride + at] = 0;  // zero between calls
         t2[1 + cell / 65][cell % 65] = v[u];
       }
     }
