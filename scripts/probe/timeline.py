@@ -66,7 +66,10 @@ def show(label, rows, k0, k1):
 sp = t[0:257]
 sp = t[0:300]
 show("spec_rank wgs", sp, 0, 1)
+show("node_prep entry -> after prologue", t[3072:4096], 2, 0)
 show("node_prep (after prologue -> end)", t[3072:4096], 0, 1)
-show("clamp_rows", t[2048:3072], 0, 1)
-show("clamp_groups H2 load + rts", t[1024:2048], 0, 1)
-show("clamp_groups D1 + suffixes", t[1024:2048], 1, 2)
+show("clamp_agg accumulate", t[2048:3072], 0, 1)
+show("clamp_agg suffixes+write", t[2048:3072], 1, 2)
+
+np_rows = t[3072:3072 + 512]
+np.save(os.path.join(ROOT, "gpurun_out", "tl_node_prep.npy"), np.stack([us(np_rows[:, 2]), us(np_rows[:, 0]), us(np_rows[:, 1])], 1))
