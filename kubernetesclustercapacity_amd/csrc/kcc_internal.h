@@ -13,7 +13,7 @@ namespace kcc {
 #define KCC_RED_ROUNDS 1  // waves = this many rounds of the resident wave capacity
 #endif
 #ifndef KCC_RED_PREFETCH
-#define KCC_RED_PREFETCH 1  // tiles in flight ahead of the one being reduced (1 or 2)
+#define KCC_RED_PREFETCH 1  // tiles in flight ahead of the one being reduced
 #endif
 constexpr int RED_IPL = 4;
 constexpr int RED_TILE = 64 * RED_IPL;  // 256

@@ -37,10 +37,13 @@ __device__ __forceinline__ unsigned long long atomic_add_u64(uint64_t* p, uint64
 // (a) segmented reduce
 // ----------------------------------------------------------------------------
 
-// Zero the outputs; for every wave range [c0 + x*range, ...) record the node owning
-// its first container.  Node indices are local to the launch (ptr and the outputs are
-// offset by the caller); the container offsets in ptr are absolute and the launch
-// covers containers [c0, c_end).
+// For every wave range [c0 + x*range, ...) record the node owning its first container,
+// and zero the outputs of the nodes the reduce does not store plainly: those a range
+// boundary cuts (each wave adds its part with an atomic) and the empty nodes ahead of the
+// launch's first container.  Every other node is stored whole by the wave where it ends
+// (block flushes of reduce_kernel).  Node indices are local to the launch (ptr and the
+// outputs are offset by the caller); the container offsets in ptr are absolute and the
+// launch covers containers [c0, c_end).
 __global__ void reduce_mark_kernel(int64_t n_nodes, int64_t c0, int64_t c_end, int32_t range,
                                    const int64_t* __restrict__ ptr,
                                    int64_t* __restrict__ wave_node, uint64_t* __restrict__ o0,
@@ -48,16 +51,20 @@ __global__ void reduce_mark_kernel(int64_t n_nodes, int64_t c0, int64_t c_end, i
                                    uint64_t* __restrict__ o3) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n_nodes; j += stride) {
-    o0[j] = 0;
-    o1[j] = 0;
-    if (o2) o2[j] = 0;
-    if (o3) o3[j] = 0;
     int64_t b = ptr[j] - c0, e = ptr[j + 1] - c0;  // relative to the launch's first container
     b = b < 0 ? 0 : b;
     e = e > c_end - c0 ? c_end - c0 : e;
+    bool zero = e <= 0;  // empty and ahead of every container (all nodes, when none)
     if (e > b) {
       for (int64_t x = (b + range - 1) / range * range; x < e; x += range)
         wave_node[x / range] = j;
+      zero = (b / range + 1) * range < e;  // a range boundary strictly inside (b, e)
+    }
+    if (zero) {
+      o0[j] = 0;
+      o1[j] = 0;
+      if (o2) o2[j] = 0;
+      if (o3) o3[j] = 0;
     }
   }
 }
@@ -228,17 +235,14 @@ void reduce_kernel(
     pend = false;
   };
 
-  uint64_t xa[NA][4], xb[NA][4];
-#if KCC_RED_PREFETCH == 2
-  uint64_t xc[NA][4];
-#endif
+  // a ring of KCC_RED_PREFETCH + 1 tiles in registers: KCC_RED_PREFETCH in flight while
+  // one is reduced (static ring indices: the tile loop below is unrolled over the ring)
+  constexpr int RING = KCC_RED_PREFETCH + 1;
+  uint64_t xs[RING][NA][4];
 #pragma unroll
-  for (int k = 0; k < NA; ++k) {
-    load_quad(rs[k], lane * 32, 0, xa[k]);
-#if KCC_RED_PREFETCH == 2
-    load_quad(rs[k], lane * 32, RED_TILE * 8, xb[k]);
-#endif
-  }
+  for (int u = 0; u < KCC_RED_PREFETCH; ++u)
+#pragma unroll
+    for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 32, u * RED_TILE * 8, xs[u][k]);
 
   auto tile = [&](uint64_t (&x)[NA][4], uint64_t (&nx)[NA][4], const int32_t tb) {
 #ifndef KCC_DIAG_RED_NOSTORE
@@ -334,18 +338,11 @@ void reduce_kernel(
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   };
-#if KCC_RED_PREFETCH == 2
-  for (int32_t tb = 0; tb < len; tb += 3 * RED_TILE) {
-    tile(xa, xc, tb);
-    if (tb + RED_TILE < len) tile(xb, xa, tb + RED_TILE);
-    if (tb + 2 * RED_TILE < len) tile(xc, xb, tb + 2 * RED_TILE);
+  for (int32_t tb = 0; tb < len; tb += RING * RED_TILE) {
+#pragma unroll
+    for (int u = 0; u < RING; ++u)
+      if (tb + u * RED_TILE < len) tile(xs[u], xs[(u + KCC_RED_PREFETCH) % RING], tb + u * RED_TILE);
   }
-#else
-  for (int32_t tb = 0; tb < len; tb += 2 * RED_TILE) {
-    tile(xa, xb, tb);
-    if (tb + RED_TILE < len) tile(xb, xa, tb + RED_TILE);
-  }
-#endif
 #if defined(KCC_DIAG_RED_LOADONLY) || defined(KCC_DIAG_RED_NOSTORE)
   if (carry[0] == 0x123456789ull) out[0][0] = carry[NA - 1] ^ res[0];
 #endif
