@@ -62,6 +62,8 @@ def parse():
                     help="node chunks of the pipelined step (reduce of chunk k overlaps the fit "
                          "of chunk k-1); 1 = reduce, then fit")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parse", action="store_true",
+                    help="skip the quantity-string parse leg (SURVEY §8f row 2)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU time of the oracle's fit sample")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -235,11 +237,74 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cl, sc, sm, totals.cpu().numpy(), err.cpu().numpy(),
                                            args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_parse:
+        del ptr, cpu, mem
+        out["parse"] = parse_leg(eng, cl, dev, stream, args.steps, args.warmup,
+                                 not args.no_cpu_baseline)
     eng.close()
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+def parse_leg(eng, cl, dev, stream, steps, warmup, with_cpu):
+    """SURVEY §8f row 2, measured beside the step (not part of `value`): every container's
+    canonical cpu request string (Quantity.String(), CC:280) -> convertCPUToMilis
+    (CC:301-319) on the device, inputs resident in HBM.  Algorithmic bytes per launch:
+    (n+1) x 8 offsets + the characters in, n x 8 values + n x 1 status out."""
+    import torch
+
+    from kubernetesclustercapacity_amd import quantity
+
+    t0 = time.time()
+    buf, off = quantity.cpu_quantity_strings(cl.cpu_req)
+    fmt_s = time.time() - t0
+    n = off.size - 1
+    d_buf = torch.from_numpy(buf).to(dev)
+    d_off = torch.from_numpy(off).to(dev)
+    d_out = torch.empty(n, dtype=torch.int64, device=dev)
+    d_st = torch.empty(n, dtype=torch.int8, device=dev)
+    with torch.cuda.stream(stream):
+        for _ in range(warmup):
+            eng.parse_cpu_millis_async(d_buf, d_off, d_out, d_st, stream=stream)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        ev0.record(stream)
+        for _ in range(steps):
+            eng.parse_cpu_millis_async(d_buf, d_off, d_out, d_st, stream=stream)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / steps
+    got = d_out.cpu().numpy().view(np.uint64)
+    ok = bool((d_st.cpu().numpy() == 1).all() and np.array_equal(got, cl.cpu_req))
+    nbytes = int(off[-1])
+    alg = (n + 1) * 8 + nbytes + n * 9
+    gbs = alg / (ms * 1e-3) / 1e9
+    res = {
+        "op": "convertCPUToMilis (CC:301-319) over every container's cpu request string",
+        "kernel": "parse_kernel<0>", "strings": n, "chars": nbytes,
+        "ms_per_launch": ms, "strings_per_s": n / (ms * 1e-3),
+        "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": alg},
+        "round_trip_exact": ok, "format_seconds": fmt_s,
+    }
+    del d_buf, d_off, d_out, d_st
+    if with_cpu:
+        from oracle import coracle
+        threads = min(16, os.cpu_count() or 1)
+        t0 = time.perf_counter()
+        ov, os_ = coracle.parse_cpu_millis(buf, off, 1)
+        t1 = time.perf_counter()
+        coracle.parse_cpu_millis(buf, off, threads)
+        t2 = time.perf_counter()
+        res["cpu_baseline"] = {
+            "value": n / (t2 - t1), "unit": "strings/s", "cores": threads, "kind": "port",
+            "value_1thread": n / (t1 - t0),
+            "sample": f"C oracle (oracle/kcc_oracle.c) kcco_parse_cpu_millis over all {n} strings",
+            "match": bool(np.array_equal(ov, got) and (os_ == 1).all()),
+        }
+    return res
 
 
 def cpu_baseline(cl, sc, sm, gpu_totals, gpu_err, target_s):

@@ -199,6 +199,44 @@ double kcc_last_slow_fraction(const kcc_ctx* ctx);
  * the device. */
 int kcc_fit_slow_pairs(kcc_ctx* ctx, int64_t* slow_pairs, int64_t* pairs);
 
+/* ---------------------------------------------------------------------------
+ * Quantity strings -> int64 (the caller side of (a)).
+ * Strings are packed Arrow-style: string i = bytes[offsets[i], offsets[i+1]),
+ * offsets non-decreasing, 0 <= offsets[i] <= n_bytes (n + 1 offsets).  Per string,
+ * out[i] is the reference's value and status[i] one of KCC_PARSE_*; the call itself
+ * returns KCC_OK unless an argument is invalid (the reference prints per-string errors
+ * and carries on with 0, CC:315-316, CC:203-206).
+ *
+ *   kcc_parse_cpu_millis: convertCPUToMilis (CC:301-319) — one trailing 'm' means
+ *     millicores, else cores x 1000 (Go int multiply, wraps); strconv.Atoi failure ->
+ *     KCC_PARSE_ERR, value 0.  Replaces the per-container calls at CC:280 and CC:283
+ *     (on cpuRequests.String() / cpuLimits.String()) and the node's at CC:197.
+ *   kcc_parse_bytes: bytefmt.ToBytes (BF:75-105) — base-2 multiples for K/M/G/T with
+ *     the reference's accepted spellings (KI and MI but not GI/TI), ParseFloat > 0,
+ *     int64(float64 * multiple) with amd64 overflow (0x8000000000000000).  Replaces
+ *     the node allocatable-memory conversion at CC:203 (and the flag parse, CC:78-81).
+ *     KCC_PARSE_UNSUPPORTED marks the rare inputs outside the device's exact
+ *     ParseFloat domain (more than 19 significant digits below 10^19, or a value at
+ *     the float64 overflow / underflow edge); never a silently different value.
+ * The *_async forms take device pointers (bytes 4-byte aligned) and a stream.
+ * ------------------------------------------------------------------------- */
+enum {
+  KCC_PARSE_OK = 1,
+  KCC_PARSE_ERR = 0,          /* the reference reports an error and uses 0 */
+  KCC_PARSE_UNSUPPORTED = -1, /* outside the exact device domain; value 0  */
+  KCC_PARSE_BADOFF = -2       /* malformed offsets (async forms only)      */
+};
+int kcc_parse_cpu_millis(kcc_ctx* ctx, int64_t n, const char* bytes, int64_t n_bytes,
+                         const int64_t* offsets, uint64_t* out, int8_t* status);
+int kcc_parse_bytes(kcc_ctx* ctx, int64_t n, const char* bytes, int64_t n_bytes,
+                    const int64_t* offsets, int64_t* out, int8_t* status);
+int kcc_parse_cpu_millis_async(kcc_ctx* ctx, int64_t n, const char* d_bytes, int64_t n_bytes,
+                               const int64_t* d_offsets, uint64_t* d_out, int8_t* d_status,
+                               void* stream);
+int kcc_parse_bytes_async(kcc_ctx* ctx, int64_t n, const char* d_bytes, int64_t n_bytes,
+                          const int64_t* d_offsets, int64_t* d_out, int8_t* d_status,
+                          void* stream);
+
 #ifdef __cplusplus
 }
 #endif

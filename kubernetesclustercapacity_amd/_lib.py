@@ -49,7 +49,17 @@ SIGNATURES = {
     "kcc_profile_read": (_int, [_vp] + [C.POINTER(_dbl), C.POINTER(_i64)] * 2),
     "kcc_last_slow_fraction": (_dbl, [_vp]),
     "kcc_fit_slow_pairs": (_int, [_vp, C.POINTER(_i64), C.POINTER(_i64)]),
+    "kcc_parse_cpu_millis": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp]),
+    "kcc_parse_bytes": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp]),
+    "kcc_parse_cpu_millis_async": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp]),
+    "kcc_parse_bytes_async": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp]),
 }
+
+# per-string status of kcc_parse_* (include/kcc.h)
+KCC_PARSE_OK = 1
+KCC_PARSE_ERR = 0
+KCC_PARSE_UNSUPPORTED = -1
+KCC_PARSE_BADOFF = -2
 
 
 def header_symbols(path: str = HEADER_PATH) -> list[str]:

@@ -72,6 +72,7 @@ struct Dev {
   // staging of the host-array entry points
   DevBuf ptr, cpu, mem, cpul, meml, used_cpu, used_mem, lim_cpu, lim_mem;
   DevBuf alloc_cpu, alloc_mem, alloc_pods, pod_count, spec_cpu, spec_mem, partial, totals, err;
+  DevBuf p_bytes, p_off, p_out, p_st;  // kcc_parse_* staging
 };
 
 }  // namespace
@@ -904,3 +905,82 @@ int kcc_fit_slow_pairs(kcc_ctx* ctx, int64_t* slow_pairs, int64_t* pairs) {
 }
 
 }  // extern "C"
+
+
+// ---- quantity-string parse --------------------------------------
+
+namespace {
+
+int parse_async_dev(kcc_ctx* ctx, int mode, int64_t n, const char* bytes, int64_t n_bytes,
+                    const int64_t* offsets, int64_t* out, int8_t* status, hipStream_t s) {
+  if (n < 0 || n_bytes < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (n == 0) return KCC_OK;
+  if (!offsets || !out || !status || (n_bytes > 0 && !bytes))
+    return fail(ctx, KCC_EINVAL, "NULL bytes/offsets/out/status");
+  if ((reinterpret_cast<uintptr_t>(bytes) & 3u) != 0)
+    return fail(ctx, KCC_EINVAL, "bytes must be 4-byte aligned");
+  KCC_HIP(ctx, kcc::launch_parse(mode, n, reinterpret_cast<const uint8_t*>(bytes), n_bytes,
+                                 offsets, out, status, s));
+  return KCC_OK;
+}
+
+int parse_host(kcc_ctx* ctx, int mode, int64_t n, const char* bytes, int64_t n_bytes,
+               const int64_t* offsets, int64_t* out, int8_t* status) {
+  if (!ctx) return KCC_EINVAL;
+  if (n < 0 || n_bytes < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (n == 0) return KCC_OK;
+  if (!offsets || !out || !status || (n_bytes > 0 && !bytes))
+    return fail(ctx, KCC_EINVAL, "NULL bytes/offsets/out/status");
+  if (offsets[0] < 0 || offsets[n] > n_bytes)
+    return fail(ctx, KCC_EINVAL, "offsets outside [0, n_bytes]");
+  for (int64_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) return fail(ctx, KCC_EINVAL, "offsets are not non-decreasing");
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  int rc;
+  if ((rc = h2d(ctx, dv, dv.p_bytes, bytes, n_bytes))) return rc;
+  if ((rc = h2d(ctx, dv, dv.p_off, offsets, n + 1))) return rc;
+  KCC_HIP(ctx, ensure(dv.p_out, 8 * (size_t)n));
+  KCC_HIP(ctx, ensure(dv.p_st, (size_t)n));
+  rc = parse_async_dev(ctx, mode, n, as<char>(dv.p_bytes), n_bytes, as<int64_t>(dv.p_off),
+                       as<int64_t>(dv.p_out), as<int8_t>(dv.p_st), dv.stream);
+  if (rc) return rc;
+  KCC_HIP(ctx, hipMemcpyAsync(out, dv.p_out.p, 8 * (size_t)n, hipMemcpyDeviceToHost, dv.stream));
+  KCC_HIP(ctx, hipMemcpyAsync(status, dv.p_st.p, (size_t)n, hipMemcpyDeviceToHost, dv.stream));
+  KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
+  return KCC_OK;
+}
+
+}  // namespace
+
+int kcc_parse_cpu_millis(kcc_ctx* ctx, int64_t n, const char* bytes, int64_t n_bytes,
+                         const int64_t* offsets, uint64_t* out, int8_t* status) {
+  return parse_host(ctx, kcc::PARSE_MODE_CPU_MILLIS, n, bytes, n_bytes, offsets,
+                    reinterpret_cast<int64_t*>(out), status);
+}
+
+int kcc_parse_bytes(kcc_ctx* ctx, int64_t n, const char* bytes, int64_t n_bytes,
+                    const int64_t* offsets, int64_t* out, int8_t* status) {
+  return parse_host(ctx, kcc::PARSE_MODE_BYTES, n, bytes, n_bytes, offsets, out, status);
+}
+
+int kcc_parse_cpu_millis_async(kcc_ctx* ctx, int64_t n, const char* d_bytes, int64_t n_bytes,
+                               const int64_t* d_offsets, uint64_t* d_out, int8_t* d_status,
+                               void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  return parse_async_dev(ctx, kcc::PARSE_MODE_CPU_MILLIS, n, d_bytes, n_bytes, d_offsets,
+                         reinterpret_cast<int64_t*>(d_out), d_status,
+                         static_cast<hipStream_t>(stream));
+}
+
+int kcc_parse_bytes_async(kcc_ctx* ctx, int64_t n, const char* d_bytes, int64_t n_bytes,
+                          const int64_t* d_offsets, int64_t* d_out, int8_t* d_status,
+                          void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  return parse_async_dev(ctx, kcc::PARSE_MODE_BYTES, n, d_bytes, n_bytes, d_offsets, d_out,
+                         d_status, static_cast<hipStream_t>(stream));
+}

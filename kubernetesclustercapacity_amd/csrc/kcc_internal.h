@@ -215,4 +215,18 @@ hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial,
                                const int32_t* perm, int64_t* totals, int32_t* spec_err,
                                hipStream_t s);
 
+// ---- quantity-string parse (kcc_parse.hip) ------------------------
+enum ParseMode : int { PARSE_MODE_CPU_MILLIS = 0, PARSE_MODE_BYTES = 1 };
+// per-string status (include/kcc.h KCC_PARSE_*)
+enum ParseStatus : int8_t {
+  PARSE_OK = 1,           // value as the reference computes it
+  PARSE_ERR = 0,          // the reference reports an error and uses 0
+  PARSE_UNSUPPORTED = -1, // outside the device parser's exact domain (value 0)
+  PARSE_BADOFF = -2       // offsets outside [0, n_bytes] or decreasing (value 0)
+};
+int64_t parse_grid(int64_t n);
+// string i = bytes[offsets[i], offsets[i+1]); bytes 4-byte aligned
+hipError_t launch_parse(int mode, int64_t n, const uint8_t* bytes, int64_t n_bytes,
+                        const int64_t* offsets, int64_t* out, int8_t* status, hipStream_t s);
+
 }  // namespace kcc

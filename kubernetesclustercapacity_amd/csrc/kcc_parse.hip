@@ -1,0 +1,341 @@
+// kcc_parse.hip — batch conversion of resource-quantity strings to the int64s the hot
+// path consumes (the caller side of the reduce):
+//
+//   MODE_CPU_MILLIS  convertCPUToMilis   CC:301-319  (container cpu request / limit
+//                    strings, CC:279-283; node allocatable cpu, CC:196-197)
+//   MODE_BYTES       bytefmt.ToBytes     BF:75-105   (node allocatable memory, CC:199-206)
+//
+// Input: Arrow-style packed strings, string i = bytes[offsets[i], offsets[i+1]).
+// Output: value[i] and status[i] (PARSE_OK; PARSE_ERR where the reference reports an
+// error and uses 0; PARSE_UNSUPPORTED outside the exact domain of MODE_BYTES, see
+// bytes_value(); PARSE_BADOFF for offsets outside [0, n_bytes] or decreasing).
+//
+// Byte work, HBM-bound: a workgroup owns PS_BLOCK consecutive strings,
+// stages their offsets and their character span in LDS with coalesced dword loads, and
+// each lane parses PS_PER_THREAD strings out of LDS (strided by the workgroup size, so a
+// wave's lanes read neighbouring strings).  A span too long for the LDS buffer is read
+// straight from global memory by the same parser (same results, slower).
+#include "kcc_internal.h"
+
+namespace kcc {
+namespace {
+
+constexpr int PS_THREADS = 256;
+constexpr int PS_PER_THREAD = 4;
+constexpr int PS_BLOCK = PS_THREADS * PS_PER_THREAD;  // strings per workgroup
+constexpr int PS_LDS_WORDS = 6144;                    // 24 KiB of staged characters
+
+__device__ __forceinline__ bool go_space(uint32_t c) {
+  // strings.TrimSpace on ASCII input: '\t', '\n', '\v', '\f', '\r', ' '
+  return c == ' ' || (c >= 9 && c <= 13);
+}
+__device__ __forceinline__ bool go_letter(uint32_t c) {
+  // unicode.IsLetter on ASCII; a byte >= 0x80 starts a non-ASCII rune and is taken as a
+  // letter (as in oracle/kcc_oracle.c; Quantity.String() emits ASCII only)
+  return ((c | 0x20u) - 'a') < 26u || c >= 0x80u;
+}
+__device__ __forceinline__ uint32_t up(uint32_t c) { return (c - 'a') < 26u ? c - 32u : c; }
+
+// Go strconv.Atoi (64-bit int) on s[0, n): ParseInt base 10 — optional sign, at least
+// one digit, no underscores (base given), range error beyond int64.
+template <class P>
+__device__ __forceinline__ bool go_atoi(P s, int n, int64_t& out) {
+  int i = 0;
+  bool neg = false;
+  if (n <= 0) return false;
+  const uint32_t c0 = s[0];
+  if (c0 == '+' || c0 == '-') {
+    neg = c0 == '-';
+    i = 1;
+  }
+  if (i == n) return false;
+  // v * 10 + d <= lim  with lim = 2^63 - 1 (or 2^63 negative): lim / 10 = 922337203685477580
+  const uint64_t q = 922337203685477580ull;
+  const uint32_t r = neg ? 8u : 7u;
+  uint64_t v = 0;
+  for (; i < n; ++i) {
+    const uint32_t d = (uint32_t)s[i] - '0';
+    if (d > 9u) return false;
+    if (v > q || (v == q && d > r)) return false;  // ErrRange
+    v = v * 10u + d;
+  }
+  out = neg ? (int64_t)(0ull - v) : (int64_t)v;
+  return true;
+}
+
+// convertCPUToMilis (CC:301-319): one trailing 'm' means millicores, otherwise cores
+// times 1000 (Go int multiply: wraps); an Atoi failure prints and yields 0.
+template <class P>
+__device__ __forceinline__ uint64_t cpu_millis_value(P s, int n, int8_t& st) {
+  bool cores = true;
+  if (n > 0 && (uint32_t)s[n - 1] == 'm') {  // HasSuffix / TrimSuffix: one 'm'
+    --n;
+    cores = false;
+  }
+  int64_t v;
+  if (!go_atoi(s, n, v)) {
+    st = PARSE_ERR;
+    return 0;
+  }
+  st = PARSE_OK;
+  return cores ? (uint64_t)v * 1000ull : (uint64_t)v;
+}
+
+// amd64 CVTTSD2SQ (Go's float64 -> int64 on amd64): truncation, 0x8000000000000000 when
+// out of range.  v is finite and >= 0 here.
+__device__ __forceinline__ int64_t f2i_amd64(double v) {
+  return v >= 9223372036854775808.0 ? (int64_t)0x8000000000000000ull : (int64_t)v;
+}
+
+__device__ __forceinline__ double p10(int k) {  // exact for k <= 22
+  double r = 1.0;
+  double b = 10.0;
+  while (k) {
+    if (k & 1) r *= b;
+    b *= b;
+    k >>= 1;
+  }
+  return r;
+}
+
+// Correctly rounded D / 10^k for 1 <= k <= 38 (D >= 1): restoring division until the
+// quotient holds 57 bits, then round-half-even to 53 bits with the remainder as sticky.
+__device__ __noinline__ double div_pow10_rn(uint64_t D, int k) {
+  unsigned __int128 V = 1;
+  for (int t = 0; t < k; ++t) V *= 10u;  // < 2^127
+  unsigned __int128 R = 0;
+  uint64_t q = 0;
+  int bit = 63;   // next bit of D to bring down
+  int extra = 0;  // zero bits brought down after D's last bit
+  while (q < (1ull << 56)) {
+    uint32_t b = 0;
+    if (bit >= 0) {
+      b = (uint32_t)(D >> bit) & 1u;
+      --bit;
+    } else {
+      ++extra;
+    }
+    R = (R << 1) | b;
+    q <<= 1;
+    if (R >= V) {
+      R -= V;
+      q |= 1u;
+    }
+  }
+  // x = (q + f) * 2^e2,  f in [0, 1),  f > 0 iff sticky
+  bool sticky = R != 0;
+  int e2;
+  if (bit >= 0) {
+    sticky |= (D & ((2ull << bit) - 1u)) != 0;
+    e2 = bit + 1;
+  } else {
+    e2 = -extra;
+  }
+  // q in [2^56, 2^57): drop 4 bits
+  const uint32_t low = (uint32_t)(q & 15u);
+  q >>= 4;
+  e2 += 4;
+  const bool guard = (low & 8u) != 0;
+  const bool rest = (low & 7u) != 0 || sticky;
+  if (guard && (rest || (q & 1u))) {
+    ++q;
+    if (q == (1ull << 53)) {
+      q >>= 1;
+      ++e2;
+    }
+  }
+  return ldexp((double)q, e2);
+}
+
+// D / 10^k correctly rounded, 1 <= k <= 38
+__device__ __forceinline__ double frac_rn(uint64_t D, int k) {
+  if (D < (1ull << 53) && k <= 22) return (double)D / p10(k);  // exact operands: one rounding
+  return div_pow10_rn(D, k);
+}
+
+// bytefmt.ToBytes (BF:75-105): TrimSpace, ToUpper, split at the first letter,
+// ParseFloat(number, 64) > 0, multiple in {T,TB,TIB | G,GB,GIB | M,MB,MIB,MI |
+// K,KB,KIB,KI | B}, int64(bytes * multiple).
+//
+// The number is [sign] digits [. digits] (no letters: the split is at the first one).
+// Exact domain on the device: values >= 10^19 (int64() overflows to 0x8000000000000000
+// whatever the rounding), < 10^-19 (the product truncates to 0), and in between any
+// digit string whose first 19 significant digits D decide the rounding (all of them
+// when there are at most 19; otherwise when D and D+1 round alike).  Outside it (a value
+// at the float64 overflow or underflow edge, 10^308 <= x < 10^309 or 10^-324 <= x <
+// 10^-323, or > 19 significant digits straddling a rounding boundary) the status is
+// PARSE_UNSUPPORTED — never a silently different value.
+template <class P>
+__device__ __forceinline__ int64_t bytes_value(P s, int n, int8_t& st) {
+  int b = 0, e = n;
+  while (b < e && go_space((uint32_t)s[b])) ++b;
+  while (e > b && go_space((uint32_t)s[e - 1])) --e;
+  int i = b;
+  while (i < e && !go_letter((uint32_t)s[i])) ++i;
+  st = PARSE_ERR;
+  if (i == e) return 0;  // no letter: invalidByteQuantityError (BF:81-83)
+  // the multiple (BF:91-104), upper-cased
+  const int ml = e - i;
+  const uint32_t m0 = up(s[i]);
+  const uint32_t m1 = ml > 1 ? up(s[i + 1]) : 0u;
+  const uint32_t m2 = ml > 2 ? up(s[i + 2]) : 0u;
+  int shift = -1;
+  if (ml <= 3) {
+    if (m0 == 'B') {
+      shift = ml == 1 ? 0 : -1;
+    } else if (m0 == 'T' || m0 == 'G' || m0 == 'M' || m0 == 'K') {
+      const int sh = m0 == 'T' ? 40 : m0 == 'G' ? 30 : m0 == 'M' ? 20 : 10;
+      const bool ok1 = ml == 1 || (ml == 2 && m1 == 'B') || (ml == 3 && m1 == 'I' && m2 == 'B') ||
+                       (ml == 2 && m1 == 'I' && (m0 == 'M' || m0 == 'K'));
+      shift = ok1 ? sh : -1;
+    }
+  }
+  // ParseFloat(s[b:i])
+  int j = b;
+  bool neg = false;
+  if (j < i && ((uint32_t)s[j] == '+' || (uint32_t)s[j] == '-')) {
+    neg = (uint32_t)s[j] == '-';
+    ++j;
+  }
+  bool dot = false, trunc_nz = false;
+  int digits = 0, sig = 0, e10 = 0;
+  uint64_t D = 0;
+  for (; j < i; ++j) {
+    const uint32_t c = s[j];
+    const uint32_t d = c - '0';
+    if (d <= 9u) {
+      ++digits;
+      if (sig == 0 && d == 0) {  // leading zero
+        if (dot) --e10;
+        continue;
+      }
+      if (sig < 19) {
+        D = D * 10u + d;
+        ++sig;
+        if (dot) --e10;
+      } else {  // beyond 19 significant digits
+        trunc_nz |= d != 0;
+        if (!dot) ++e10;
+      }
+    } else if (c == '.' && !dot) {
+      dot = true;
+    } else {
+      return 0;  // syntax error
+    }
+  }
+  if (digits == 0 || D == 0 || neg || shift < 0) return 0;  // error, or bytes <= 0
+  const int mag = sig + e10;  // x in [10^(mag-1), 10^mag)
+  if (mag >= 310) return 0;   // ParseFloat ErrRange (rounds to +Inf)
+  if (mag == 309) {
+    st = PARSE_UNSUPPORTED;
+    return 0;
+  }
+  if (mag >= 20) {  // x >= 10^19 > 2^63: int64() overflows
+    st = PARSE_OK;
+    return (int64_t)0x8000000000000000ull;
+  }
+  double x;
+  if (e10 >= 0) {
+    uint64_t v = D;  // mag <= 19: the integer fits 64 bits
+    for (int t = 0; t < e10; ++t) v *= 10u;
+    x = (double)v;  // u64 -> f64, correctly rounded
+  } else {
+    const int k = -e10;
+    if (k > 38) {  // x < 10^-19: the product truncates to 0; only the status depends on x
+      if (mag >= -322) {
+        st = PARSE_OK;  // x > 2^-1075: rounds to a positive double
+      } else if (mag == -323) {
+        st = PARSE_UNSUPPORTED;
+      }  // mag <= -324: rounds to 0, bytes <= 0 -> error
+      return 0;
+    }
+    x = frac_rn(D, k);
+    // more than 19 significant digits: x lies in [D, D+1) x 10^-k; when both ends round
+    // to the same double so does x (Go's own test for a truncated mantissa, atof.go)
+    if (trunc_nz && frac_rn(D + 1u, k) != x) {
+      st = PARSE_UNSUPPORTED;
+      return 0;
+    }
+  }
+  st = PARSE_OK;
+  return f2i_amd64(ldexp(x, shift));  // times a power of two: exact
+}
+
+template <int MODE, class P>
+__device__ __forceinline__ void parse_one(P s, int n, int64_t& v, int8_t& st) {
+  if (MODE == PARSE_MODE_CPU_MILLIS)
+    v = (int64_t)cpu_millis_value(s, n, st);
+  else
+    v = bytes_value(s, n, st);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(PS_THREADS) void parse_kernel(int64_t n, const uint8_t* __restrict__ bytes,
+                                                           int64_t n_bytes,
+                                                           const int64_t* __restrict__ off,
+                                                           int64_t* __restrict__ out,
+                                                           int8_t* __restrict__ status) {
+  __shared__ int64_t s_off[PS_BLOCK + 1];
+  __shared__ uint32_t s_chr[PS_LDS_WORDS];
+  const int64_t base = (int64_t)blockIdx.x * PS_BLOCK;
+  const int cnt = (int)min((int64_t)PS_BLOCK, n - base);
+  for (int t = threadIdx.x; t <= cnt; t += PS_THREADS) s_off[t] = off[base + t];
+  __syncthreads();
+  const int64_t b0 = max(s_off[0], (int64_t)0);
+  const int64_t b1 = min(max(s_off[cnt], b0), n_bytes);
+  const int64_t w0 = b0 >> 2, w1 = (b1 + 3) >> 2;
+  const bool staged = w1 - w0 <= PS_LDS_WORDS;  // uniform over the workgroup
+  if (staged) {
+    const uint32_t* __restrict__ wp = reinterpret_cast<const uint32_t*>(bytes);
+    const int64_t full = n_bytes >> 2;  // words entirely inside the buffer
+    for (int64_t t = threadIdx.x; t < w1 - w0; t += PS_THREADS) {
+      const int64_t w = w0 + t;
+      uint32_t v = 0;
+      if (w < full) {
+        v = __builtin_nontemporal_load(wp + w);
+      } else {
+        for (int k = 0; k < 4; ++k)
+          if (w * 4 + k < n_bytes) v |= (uint32_t)bytes[w * 4 + k] << (8 * k);
+      }
+      s_chr[t] = v;
+    }
+  }
+  __syncthreads();
+  const uint8_t* lds = reinterpret_cast<const uint8_t*>(s_chr);
+#pragma unroll
+  for (int r = 0; r < PS_PER_THREAD; ++r) {
+    const int li = r * PS_THREADS + (int)threadIdx.x;
+    if (li >= cnt) break;
+    const int64_t sb = s_off[li], se = s_off[li + 1];
+    int64_t v = 0;
+    int8_t st = PARSE_BADOFF;
+    if (sb >= 0 && se >= sb && se <= n_bytes && se - sb < ((int64_t)1 << 31)) {
+      if (staged && sb >= b0 && se <= b1)
+        parse_one<MODE>(lds + (sb - w0 * 4), (int)(se - sb), v, st);
+      else
+        parse_one<MODE>(bytes + sb, (int)(se - sb), v, st);
+    }
+    out[base + li] = v;
+    status[base + li] = st;
+  }
+}
+
+}  // namespace
+
+int64_t parse_grid(int64_t n) { return (n + PS_BLOCK - 1) / PS_BLOCK; }
+
+hipError_t launch_parse(int mode, int64_t n, const uint8_t* bytes, int64_t n_bytes,
+                        const int64_t* offsets, int64_t* out, int8_t* status, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t grid = parse_grid(n);
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  if (mode == PARSE_MODE_CPU_MILLIS)
+    hipLaunchKernelGGL(parse_kernel<PARSE_MODE_CPU_MILLIS>, dim3((unsigned)grid), dim3(PS_THREADS), 0,
+                       s, n, bytes, n_bytes, offsets, out, status);
+  else
+    hipLaunchKernelGGL(parse_kernel<PARSE_MODE_BYTES>, dim3((unsigned)grid), dim3(PS_THREADS), 0, s,
+                       n, bytes, n_bytes, offsets, out, status);
+  return hipGetLastError();
+}
+
+}  // namespace kcc

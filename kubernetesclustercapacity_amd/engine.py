@@ -5,6 +5,8 @@ src/KubeAPI/ClusterCapacity.go = CC):
 
   get_pod_cpu_memory_requests_limits  <- getPodCPUMemoryRequestsLimits (CC:255-299)
   total_possible_max_replicas          <- main's node loop (CC:101-140)
+  convert_cpu_to_milis                 <- convertCPUToMilis (CC:301-319), batched
+  to_bytes                             <- bytefmt.ToBytes (BF:75-105), batched
 
 Every call goes through the C-ABI into the gfx950 kernels; nothing is computed here.
 """
@@ -154,6 +156,35 @@ class CapacityEngine:
             *[_p(x) for x in a], sc.size, _p(sc), _p(sm), _p(totals), _p(err)))
         return totals, err
 
+    # -- quantity strings -------------------------------------
+    def _parse(self, fn, strings, dtype):
+        if isinstance(strings, tuple):
+            buf, off = strings
+        else:
+            from .quantity import pack_strings
+            buf, off = pack_strings(strings)
+        buf = _arr(buf, np.uint8)
+        off = _arr(off, np.int64)
+        n = off.size - 1
+        if n < 0:
+            raise ValueError("offsets must hold n + 1 entries")
+        out = np.zeros(n, dtype)
+        st = np.zeros(n, np.int8)
+        self._check(fn(self._h, n, _p(buf), buf.size, _p(off), _p(out), _p(st)))
+        return out, st
+
+    def convert_cpu_to_milis(self, strings):
+        """convertCPUToMilis (CC:301-319) over a batch: `strings` is a sequence of str or
+        a packed (bytes uint8, offsets int64) pair.  Returns (uint64 values, int8
+        status: 1 ok, 0 where the reference prints an error and uses 0)."""
+        return self._parse(self._lib.kcc_parse_cpu_millis, strings, np.uint64)
+
+    def to_bytes(self, strings):
+        """bytefmt.ToBytes (BF:75-105) over a batch.  Returns (int64 values, int8
+        status: 1 ok, 0 error (value 0), -1 outside the device's exact ParseFloat
+        domain — see include/kcc.h)."""
+        return self._parse(self._lib.kcc_parse_bytes, strings, np.int64)
+
     def last_slow_fraction(self) -> float:
         return float(self._lib.kcc_last_slow_fraction(self._h))
 
@@ -196,6 +227,16 @@ class CapacityEngine:
             _dp(mem_req), _dp(alloc_cpu), _dp(alloc_mem), _dp(alloc_pods), _dp(pod_count),
             _dp(used_cpu), _dp(used_mem), spec_cpu.numel(), _dp(spec_cpu), _dp(spec_mem),
             _dp(partial), int(n_chunks), _stream(stream)))
+
+    def parse_cpu_millis_async(self, buf, off, out, status, stream=None):
+        self._check(self._lib.kcc_parse_cpu_millis_async(
+            self._h, off.numel() - 1, _dp(buf), buf.numel(), _dp(off), _dp(out), _dp(status),
+            _stream(stream)))
+
+    def parse_bytes_async(self, buf, off, out, status, stream=None):
+        self._check(self._lib.kcc_parse_bytes_async(
+            self._h, off.numel() - 1, _dp(buf), buf.numel(), _dp(off), _dp(out), _dp(status),
+            _stream(stream)))
 
     def profile_enable(self, on: bool = True):
         self._check(self._lib.kcc_profile_enable(self._h, 1 if on else 0))

@@ -40,6 +40,10 @@ def lib():
         L.kcco_convert_cpu_to_milis.restype = C.c_uint64
         L.kcco_to_bytes.argtypes = [C.c_char_p, C.POINTER(i64)]
         L.kcco_to_bytes.restype = C.c_int
+        L.kcco_parse_cpu_millis.argtypes = [i64, vp, vp, vp, vp, C.c_int]
+        L.kcco_parse_cpu_millis.restype = None
+        L.kcco_parse_bytes.argtypes = [i64, vp, vp, vp, vp, C.c_int]
+        L.kcco_parse_bytes.restype = None
         _LIB = L
     return _LIB
 
@@ -95,3 +99,23 @@ def to_bytes(s: str):
     out = C.c_int64(0)
     rc = lib().kcco_to_bytes(s.encode(), C.byref(out))
     return out.value, rc == 0
+
+
+def parse_cpu_millis(buf, off, n_threads=1):
+    """Batch convertCPUToMilis over packed strings -> (uint64 values, int8 status)."""
+    buf = np.ascontiguousarray(buf, np.uint8)
+    off = np.ascontiguousarray(off, np.int64)
+    n = off.size - 1
+    out, st = np.zeros(n, np.uint64), np.zeros(n, np.int8)
+    lib().kcco_parse_cpu_millis(n, _p(buf), _p(off), _p(out), _p(st), int(n_threads))
+    return out, st
+
+
+def parse_bytes(buf, off, n_threads=1):
+    """Batch bytefmt.ToBytes over packed strings -> (int64 values, int8 status)."""
+    buf = np.ascontiguousarray(buf, np.uint8)
+    off = np.ascontiguousarray(off, np.int64)
+    n = off.size - 1
+    out, st = np.zeros(n, np.int64), np.zeros(n, np.int8)
+    lib().kcco_parse_bytes(n, _p(buf), _p(off), _p(out), _p(st), int(n_threads))
+    return out, st

@@ -154,8 +154,7 @@ static int go_atoi(const char* s, size_t n, int64_t* out) {
 }
 
 /* CC:301-319 */
-uint64_t kcco_convert_cpu_to_milis(const char* cpu, int* ok) {
-  size_t n = strlen(cpu);
+static uint64_t cpu_to_milis_n(const char* cpu, size_t n, int* ok) {
   int flag = 1;
   if (n > 0 && cpu[n - 1] == 'm') { /* strings.HasSuffix / TrimSuffix (one 'm') */
     n -= 1;
@@ -170,6 +169,10 @@ uint64_t kcco_convert_cpu_to_milis(const char* cpu, int* ok) {
     if (ok) *ok = 0; /* CC:315-316 prints an error */
   }
   return (uint64_t)cpuMili; /* CC:318 */
+}
+
+uint64_t kcco_convert_cpu_to_milis(const char* cpu, int* ok) {
+  return cpu_to_milis_n(cpu, strlen(cpu), ok);
 }
 
 /* Go unicode.IsLetter restricted to the bytes a Quantity/flag string can carry:
@@ -212,9 +215,8 @@ static int64_t go_f64_to_i64_amd64(double v) {
 }
 
 /* BF:75-105 */
-int kcco_to_bytes(const char* s_in, int64_t* out) {
+static int to_bytes_n(const char* s_in, size_t n, int64_t* out) {
   /* strings.TrimSpace + strings.ToUpper (ASCII subset) */
-  size_t n = strlen(s_in);
   size_t b = 0, e = n;
   while (b < e && isspace((unsigned char)s_in[b])) ++b;
   while (e > b && isspace((unsigned char)s_in[e - 1])) --e;
@@ -229,6 +231,7 @@ int kcco_to_bytes(const char* s_in, int64_t* out) {
   double bytes = 0;
   if (!go_parse_float_noletters(s, i, &bytes) || bytes <= 0) { free(s); return -1; } /* BF:86-89 */
   const char* m = s + i;
+  if (strlen(m) != len - i) { free(s); return -1; } /* an embedded NUL is no multiple */
   double mult;
   if (!strcmp(m, "T") || !strcmp(m, "TB") || !strcmp(m, "TIB")) mult = 1099511627776.0;
   else if (!strcmp(m, "G") || !strcmp(m, "GB") || !strcmp(m, "GIB")) mult = 1073741824.0;
@@ -239,4 +242,63 @@ int kcco_to_bytes(const char* s_in, int64_t* out) {
   free(s);
   *out = go_f64_to_i64_amd64(bytes * mult);
   return 0;
+}
+
+int kcco_to_bytes(const char* s_in, int64_t* out) { return to_bytes_n(s_in, strlen(s_in), out); }
+
+/* Batch forms over Arrow-style packed strings (string i = bytes[offsets[i],
+ * offsets[i+1])): the checker of kcc_parse_* and the CPU baseline of its bench leg.
+ * status[i] = 1 ok, 0 error (the reference prints and uses 0). */
+typedef struct {
+  int mode;
+  const char* bytes;
+  const int64_t* off;
+  int64_t* out;
+  int8_t* st;
+  int64_t b, e;
+} parse_job;
+
+static void* parse_worker(void* arg) {
+  parse_job* j = (parse_job*)arg;
+  for (int64_t i = j->b; i < j->e; ++i) {
+    const char* s = j->bytes + j->off[i];
+    const size_t n = (size_t)(j->off[i + 1] - j->off[i]);
+    if (j->mode == 0) {
+      int ok = 0;
+      j->out[i] = (int64_t)cpu_to_milis_n(s, n, &ok);
+      j->st[i] = (int8_t)ok;
+    } else {
+      int64_t v = 0;
+      j->st[i] = (int8_t)(to_bytes_n(s, n, &v) == 0);
+      j->out[i] = v;
+    }
+  }
+  return NULL;
+}
+
+static void parse_batch(int mode, int64_t n, const char* bytes, const int64_t* off, int64_t* out,
+                        int8_t* st, int n_threads) {
+  parse_job jobs[256];
+  pthread_t tids[256];
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > 256) n_threads = 256;
+  for (int t = 0; t < n_threads; ++t) {
+    parse_job* j = &jobs[t];
+    j->mode = mode; j->bytes = bytes; j->off = off; j->out = out; j->st = st;
+    j->b = n * t / n_threads;
+    j->e = n * (t + 1) / n_threads;
+  }
+  if (n_threads == 1) { parse_worker(&jobs[0]); return; }
+  for (int t = 0; t < n_threads; ++t) pthread_create(&tids[t], NULL, parse_worker, &jobs[t]);
+  for (int t = 0; t < n_threads; ++t) pthread_join(tids[t], NULL);
+}
+
+void kcco_parse_cpu_millis(int64_t n, const char* bytes, const int64_t* offsets, uint64_t* out,
+                           int8_t* status, int n_threads) {
+  parse_batch(0, n, bytes, offsets, (int64_t*)out, status, n_threads);
+}
+
+void kcco_parse_bytes(int64_t n, const char* bytes, const int64_t* offsets, int64_t* out,
+                      int8_t* status, int n_threads) {
+  parse_batch(1, n, bytes, offsets, out, status, n_threads);
 }

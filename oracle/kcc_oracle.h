@@ -50,6 +50,14 @@ uint64_t kcco_convert_cpu_to_milis(const char* s, int* ok);
 /* BF:75-105 — returns 0 on success, -1 on error (value then 0). */
 int kcco_to_bytes(const char* s, int64_t* out);
 
+/* Batch forms of the two conversions over Arrow-style packed strings (string i =
+ * bytes[offsets[i], offsets[i+1])); status[i] = 1 ok, 0 error.  n_threads > 1 splits
+ * the strings over pthreads (CPU baseline timing only). */
+void kcco_parse_cpu_millis(int64_t n, const char* bytes, const int64_t* offsets, uint64_t* out,
+                           int8_t* status, int n_threads);
+void kcco_parse_bytes(int64_t n, const char* bytes, const int64_t* offsets, int64_t* out,
+                      int8_t* status, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

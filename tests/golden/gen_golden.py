@@ -110,7 +110,29 @@ CASES = {
 }
 
 
+def parse_case():
+    """tests/golden/parse.npz: the hand KAT strings and seeded corpora of
+    tests/test_parse.py, packed; expected values/statuses from oracle/pyoracle.py."""
+    from kubernetesclustercapacity_amd import quantity
+    from tests import test_parse as tp
+    d = {}
+    for key, strs, fn in (("cpu", tp.CPU_KATS + tp.fuzz_corpus(600, 31), pyoracle.convert_cpu_to_milis),
+                          ("mem", tp.BYTES_KATS + tp.fuzz_corpus(600, 32) + tp.decimal_corpus(1200, 33),
+                           pyoracle.to_bytes)):
+        buf, off = quantity.pack_strings(strs)
+        res = [fn(x.decode("latin-1")) for x in strs]
+        d[f"{key}_buf"], d[f"{key}_off"] = buf, off
+        d[f"{key}_val"] = np.array([r[0] for r in res], np.uint64 if key == "cpu" else np.int64)
+        d[f"{key}_st"] = np.array([1 if r[1] else 0 for r in res], np.int8)
+    return d
+
+
 def main():
+    path = os.path.join(HERE, "parse.npz")
+    np.savez_compressed(path, **parse_case())
+    print(f"{path}")
+    if len(sys.argv) > 1 and sys.argv[1] == "parse":
+        return
     for name, fn in CASES.items():
         d = fn()
         d.update(expected(d))

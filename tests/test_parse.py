@@ -1,0 +1,287 @@
+"""Quantity-string conversion: convertCPUToMilis (CC:301-319) and
+bytefmt.ToBytes (BF:75-105) over packed string batches.
+
+CPU tests pin the device algorithm (tests/parse_model.py, a step-by-step restatement of
+kcc_parse.hip) to the C oracle and to exact rational rounding; GPU tests call the
+kernels through the C-ABI (kcc_parse_*) and require bit-exact values and statuses.
+"""
+import os
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+from kubernetesclustercapacity_amd import quantity
+from oracle import coracle
+from tests import parse_model as pm
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "parse.npz")
+
+CPU_KATS = [b"200m", b"2", b"250m", b"0", b"+3", b"0.5", b"2k", b"500u", b"", b"m", b"-100m",
+            b"9223372036854775807m", b"9223372036854775808m", b"-9223372036854775808m",
+            b"-9223372036854775809m", b"9223372036854775807", b"9223372036854776", b"1mm",
+            b"1 m", b" 1", b"00000000000000000000000000000250m", b"-0", b"+", b"-m", b"1_000",
+            b"12345678901234567890", b"\x00", b"1\x00m"]
+BYTES_KATS = [b"250mb", b"500mb", b"100mb", b"16331524Ki", b"16Gi", b"1Ti", b"1", b"1.5G",
+              b"1GIB", b"  2 KB ", b"  2KB ", b"0.5B", b"0mb", b"-1mb", b"1e3MB", b"100M",
+              b"7b", b"1.0000000001K", b".5K", b"5.K", b"99999999999T", b".", b"+.5k",
+              b"1.2.3k", b"\t64Mi\n", b"1kib", b"1KIB ", b"3mi", b"3gi", b"1BB", b"1Mx",
+              b"0.000000000000000000001T", b"1" + b"0" * 308 + b"B", b"1" + b"0" * 309 + b"B",
+              b"1" + b"0" * 307 + b"B", b"0." + b"0" * 322 + b"1B", b"0." + b"0" * 323 + b"1B",
+              b"0." + b"0" * 321 + b"1B", b"1234567890123456789012345B",
+              b"1.234567890123456789012345B", b"12345678901234567890000000.000B",
+              b"9007199254740993B", b"9007199254740993.5B", b"0.1B", b"0.3K",
+              b"18446744073709551615B", b"9223372036854775807B", b"9223372036854775808B",
+              b"8589934591.9999999999K", b"1.00000000000000000000000000000000000000001K",
+              b"123456789012345678.9K", b"0.00000000000000000000000000000000000001T",
+              b"0.000000000000000000000000000000000000001T"]
+
+
+def fuzz_corpus(n, seed):
+    rng = np.random.default_rng(seed)
+    alpha = np.frombuffer(b"0123456789012345678901234567890123456789..+-mMkKgGiIbBtTeE  \t_x",
+                          np.uint8)
+    out = []
+    for _ in range(n):
+        L = int(rng.integers(0, 24))
+        out.append(bytes(rng.choice(alpha, L)))
+    return out
+
+
+def decimal_corpus(n, seed):
+    """Structured decimals: 0-25 integer digits, optional point and 0-45 fraction digits,
+    leading zeros, a valid or near-valid multiple."""
+    rng = np.random.default_rng(seed)
+    sufs = [b"B", b"K", b"KB", b"KI", b"KIB", b"M", b"MB", b"MI", b"MIB", b"G", b"GB", b"GIB",
+            b"T", b"TB", b"TIB", b"m", b"mb", b"ki", b"Mi", b"Gi", b"k"]
+    out = []
+    for _ in range(n):
+        ni = int(rng.integers(0, 26))
+        nf = int(rng.integers(0, 46)) if rng.random() < 0.7 else 0
+        ip = "".join(str(int(d)) for d in rng.integers(0, 10, ni))
+        if rng.random() < 0.2:
+            ip = "0" * int(rng.integers(1, 5)) + ip
+        fp = "".join(str(int(d)) for d in rng.integers(0, 10, nf))
+        if rng.random() < 0.3 and nf:
+            fp = "0" * int(rng.integers(1, 30)) + fp
+        s = ip + ("." + fp if nf or rng.random() < 0.1 else "")
+        if rng.random() < 0.05:
+            s = "-" + s
+        out.append(s.encode() + sufs[int(rng.integers(0, len(sufs)))])
+    return out
+
+
+def cpu_corpus():
+    rng = np.random.default_rng(5)
+    vals = rng.integers(0, 1 << 63, 2000, dtype=np.int64)
+    extra = [str(int(v)).encode() + (b"m" if i % 2 else b"") for i, v in enumerate(vals)]
+    return CPU_KATS + fuzz_corpus(3000, 11) + extra
+
+
+def bytes_corpus():
+    return BYTES_KATS + fuzz_corpus(3000, 12) + decimal_corpus(6000, 13)
+
+
+# ---- CPU: the algorithm against the oracle ---------------------------------------
+def test_model_cpu_millis_matches_oracle():
+    strs = cpu_corpus()
+    buf, off = quantity.pack_strings(strs)
+    ov, os_ = coracle.parse_cpu_millis(buf, off)
+    for s, v, st in zip(strs, ov, os_):
+        mv, mst = pm.cpu_millis(s)
+        assert (mv, mst) == (int(v), int(st)), s
+
+
+def test_model_to_bytes_matches_oracle():
+    strs = bytes_corpus()
+    buf, off = quantity.pack_strings(strs)
+    ov, os_ = coracle.parse_bytes(buf, off)
+    unsupported = 0
+    for s, v, st in zip(strs, ov, os_):
+        mv, mst = pm.to_bytes(s)
+        if mst == pm.UNSUPPORTED:
+            unsupported += 1
+            continue
+        assert (mv, mst) == (int(v), int(st)), s
+    # the exact device domain covers all but the designed edge cases
+    assert unsupported < 0.01 * len(strs)
+
+
+def test_model_unsupported_only_at_designed_edges():
+    assert pm.to_bytes(b"1" + b"0" * 308 + b"B")[1] == pm.UNSUPPORTED      # 10^308: < MaxFloat64?
+    assert pm.to_bytes(b"0." + b"0" * 323 + b"1B")[1] == pm.UNSUPPORTED    # 1e-324 vs 2^-1075
+    assert pm.to_bytes(b"0." + b"0" * 322 + b"1B") == (0, pm.OK)           # 1e-323 > 2^-1075
+    assert pm.to_bytes(b"1.234567890123456789012345B") == (1, pm.OK)  # > 19 digits, decided
+    # > 19 significant digits straddling a rounding boundary: 2^-1 + 2^-54 (a tie) + 1e-30
+    tie = Fraction(1, 2) + Fraction(1, 2 ** 54)
+    digits = str(tie.numerator * 10 ** 60 // tie.denominator)  # 0.5000...0555 x 10^60
+    assert pm.to_bytes(("0." + digits + "1B").encode())[1] == pm.UNSUPPORTED
+    assert pm.to_bytes(b"1234567890123456789012345B") == (pm.I64_MIN, pm.OK)
+    assert pm.to_bytes(b"1.00000000000000000000B") == (1, pm.OK)  # trailing zeros are exact
+
+
+def test_div_pow10_correctly_rounded():
+    rng = np.random.default_rng(3)
+    for _ in range(4000):
+        D = int(rng.integers(1, 10 ** 18)) * int(rng.integers(1, 10))
+        k = int(rng.integers(1, 39))
+        assert pm.div_pow10_rn(D, k) == float(Fraction(D, 10 ** k)), (D, k)
+    # halfway-adjacent cases: D / 10^k within a few ulp of a tie
+    for k in (23, 25, 30, 38):
+        for m in range(1, 200):
+            x = Fraction(m * 2 + 1, 2 ** 60)  # exact binary ties scaled
+            D = int(x * 10 ** k)
+            if 0 < D < 10 ** 19:
+                assert pm.div_pow10_rn(D, k) == float(Fraction(D, 10 ** k))
+
+
+def test_oracle_batch_equals_single():
+    strs = [s for s in BYTES_KATS if b"\x00" not in s]
+    buf, off = quantity.pack_strings(strs)
+    ov, os_ = coracle.parse_bytes(buf, off)
+    for s, v, st in zip(strs, ov, os_):
+        assert coracle.to_bytes(s.decode("latin-1")) == (int(v), bool(st))
+    strs = [s for s in CPU_KATS if b"\x00" not in s]
+    buf, off = quantity.pack_strings(strs)
+    cv, cs = coracle.parse_cpu_millis(buf, off)
+    for s, v, st in zip(strs, cv, cs):
+        assert coracle.convert_cpu_to_milis(s.decode("latin-1")) == (int(v), bool(st))
+
+
+def test_quantity_string_format():
+    rng = np.random.default_rng(8)
+    m = np.concatenate([rng.integers(0, 10 ** 7, 5000), [0, 1000, 1500, 2000, 999, 10 ** 18]])
+    buf, off = quantity.cpu_quantity_strings(m.astype(np.uint64))
+    got = quantity.unpack_strings(buf, off)
+    want = [(str(v // 1000) if v % 1000 == 0 else f"{v}m").encode() for v in m.tolist()]
+    assert got == want
+    b = np.concatenate([rng.integers(0, 1 << 45, 3000) * 1024, rng.integers(0, 1 << 40, 3000),
+                        [0, 1024, 1 << 30, 16 << 30, 5 << 40, 3 << 60]]).astype(np.uint64)
+    buf, off = quantity.memory_quantity_strings(b)
+    got = quantity.unpack_strings(buf, off)
+    sufs = ["", "Ki", "Mi", "Gi", "Ti", "Pi", "Ei"]
+    for v, g in zip(b.tolist(), got):
+        k = 0
+        while v and k < 6 and v % (1 << (10 * (k + 1))) == 0:
+            k += 1
+        assert g == f"{v >> (10 * k)}{sufs[k]}".encode()
+
+
+def test_golden_parse_fixture():
+    """tests/golden/parse.npz (made by tests/golden/gen_golden.py from the hand KATs and
+    seeded corpora) against the oracle."""
+    z = np.load(GOLDEN)
+    v, s = coracle.parse_cpu_millis(z["cpu_buf"], z["cpu_off"])
+    assert np.array_equal(v, z["cpu_val"]) and np.array_equal(s, z["cpu_st"])
+    v, s = coracle.parse_bytes(z["mem_buf"], z["mem_off"])
+    assert np.array_equal(v, z["mem_val"]) and np.array_equal(s, z["mem_st"])
+
+
+# ---- GPU: the kernels through the C-ABI ---------------------------------------------
+@pytest.fixture(scope="module")
+def eng():
+    from kubernetesclustercapacity_amd import CapacityEngine
+    with CapacityEngine(0, 1) as e:
+        yield e
+
+
+@pytest.mark.gpu
+def test_gpu_cpu_millis_bit_exact(eng):
+    strs = cpu_corpus()
+    buf, off = quantity.pack_strings(strs)
+    gv, gs = eng.convert_cpu_to_milis((buf, off))
+    ov, os_ = coracle.parse_cpu_millis(buf, off)
+    assert np.array_equal(gs, os_)
+    assert np.array_equal(gv, ov)
+
+
+@pytest.mark.gpu
+def test_gpu_to_bytes_bit_exact(eng):
+    strs = bytes_corpus()
+    buf, off = quantity.pack_strings(strs)
+    gv, gs = eng.to_bytes((buf, off))
+    ov, os_ = coracle.parse_bytes(buf, off)
+    model = [pm.to_bytes(s) for s in strs]
+    assert [int(x) for x in gs] == [m[1] for m in model]
+    assert [int(x) for x in gv] == [m[0] for m in model]
+    sup = gs != pm.UNSUPPORTED
+    assert np.array_equal(gs[sup], os_[sup]) and np.array_equal(gv[sup], ov[sup])
+
+
+@pytest.mark.gpu
+def test_gpu_golden_fixture(eng):
+    z = np.load(GOLDEN)
+    v, s = eng.convert_cpu_to_milis((z["cpu_buf"], z["cpu_off"]))
+    assert np.array_equal(v, z["cpu_val"]) and np.array_equal(s, z["cpu_st"])
+    v, s = eng.to_bytes((z["mem_buf"], z["mem_off"]))
+    sup = s != pm.UNSUPPORTED
+    assert np.array_equal(v[sup], z["mem_val"][sup]) and np.array_equal(s[sup], z["mem_st"][sup])
+
+
+@pytest.mark.gpu
+def test_gpu_long_strings_global_path(eng):
+    """Workgroups whose character span exceeds the LDS stage read global memory."""
+    rng = np.random.default_rng(21)
+    strs = []
+    for i in range(5000):
+        if i % 7 == 0:
+            strs.append(b"0" * int(rng.integers(100, 3000)) + b"250m")
+        else:
+            strs.append(str(int(rng.integers(0, 10 ** 6))).encode() + b"m")
+    buf, off = quantity.pack_strings(strs)
+    gv, gs = eng.convert_cpu_to_milis((buf, off))
+    ov, os_ = coracle.parse_cpu_millis(buf, off)
+    assert np.array_equal(gs, os_) and np.array_equal(gv, ov)
+    mstrs = [b" " * int(rng.integers(0, 4000)) + b"16331524Ki" if i % 5 == 0 else b"64Mi"
+             for i in range(3000)]
+    buf, off = quantity.pack_strings(mstrs)
+    gv, gs = eng.to_bytes((buf, off))
+    ov, os_ = coracle.parse_bytes(buf, off)
+    assert np.array_equal(gs, os_) and np.array_equal(gv, ov)
+
+
+@pytest.mark.gpu
+def test_gpu_edge_sizes(eng):
+    for n in (0, 1, 1023, 1024, 1025, 4097):
+        strs = [f"{i}m".encode() for i in range(n)]
+        buf, off = quantity.pack_strings(strs)
+        gv, gs = eng.convert_cpu_to_milis((buf, off))
+        assert gv.size == n and np.array_equal(gv, np.arange(n, dtype=np.uint64))
+        assert (gs == 1).all()
+    # unaligned tail: total bytes not a multiple of 4, no padding handed over
+    buf, off = quantity.pack_strings([b"1", b"22", b"333m"])
+    gv, gs = eng.convert_cpu_to_milis((buf[:int(off[-1])].copy(), off))
+    assert gv.tolist() == [1000, 22000, 333] and (gs == 1).all()
+
+
+@pytest.mark.gpu
+def test_gpu_async_bad_offsets(eng):
+    import torch
+    buf, off = quantity.pack_strings([b"1", b"2", b"3"])
+    off = off.copy()
+    off[2] = 1000  # past n_bytes
+    d_buf = torch.from_numpy(buf).cuda()
+    d_off = torch.from_numpy(off).cuda()
+    out = torch.zeros(3, dtype=torch.int64, device="cuda")
+    st = torch.zeros(3, dtype=torch.int8, device="cuda")
+    eng.parse_cpu_millis_async(d_buf, d_off, out, st)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [1, -2, -2]
+    assert out.cpu().tolist() == [1000, 0, 0]
+
+
+@pytest.mark.gpu
+def test_gpu_c4_round_trip():
+    """C4 scale (1M nodes, 20M pods): every container's canonical cpu string parses back
+    to its request (size-independent property), node memory strings to ToBytes'
+    values (Ki/Mi multiples exact, Gi/Ti multiples 0 — the reference's quirk)."""
+    from kubernetesclustercapacity_amd import CapacityEngine, synth
+    c = synth.make_cluster(1_000_000, 20_000_000, seed=20261019)
+    buf, off = quantity.cpu_quantity_strings(c.cpu_req)
+    with CapacityEngine(0, 1) as e:
+        v, s = e.convert_cpu_to_milis((buf, off))
+        assert (s == 1).all() and np.array_equal(v, c.cpu_req)
+        mb, mo = quantity.memory_quantity_strings(c.alloc_mem.astype(np.uint64))
+        v, s = e.to_bytes((mb, mo))
+    ov, os_ = coracle.parse_bytes(mb, mo)
+    assert np.array_equal(v, ov) and np.array_equal(s, os_)
