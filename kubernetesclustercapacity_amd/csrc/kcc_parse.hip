@@ -320,6 +320,99 @@ __global__ __launch_bounds__(PS_THREADS) void parse_kernel(int64_t n, const uint
   }
 }
 
+// Eight ASCII characters (the first in the low byte) -> their decimal value, when all
+// eight are digits: nibble tests, then three multiply-shift steps that combine digit
+// pairs, quads and the two halves (SWAR).
+__device__ __forceinline__ bool swar8(uint64_t c, uint64_t& v) {
+  const uint64_t hi = 0xF0F0F0F0F0F0F0F0ull, z = 0x3030303030303030ull;
+  if ((c & hi) != z || ((c + 0x0606060606060606ull) & hi) != z) return false;
+  c = ((c & 0x0F0F0F0F0F0F0F0Full) * 2561u) >> 8;
+  c = ((c & 0x00FF00FF00FF00FFull) * 6553601u) >> 16;
+  v = ((c & 0x0000FFFF0000FFFFull) * 42949672960001ull) >> 32;
+  return true;
+}
+
+// convertCPUToMilis without LDS: one lane per string.  Strings of <= 9 characters (all
+// canonical cpu quantities up to 99999999m / 99999999 cores) come from one aligned
+// 12-byte load per lane — neighbouring lanes read neighbouring bytes, so a wave's loads
+// coalesce into the few cache lines its strings span — and are parsed in registers
+// (swar8); anything else takes the byte loop over global memory.  PS_PER_THREAD strings
+// per lane, strided by the workgroup size, all loads issued before the first parse.
+__global__ __launch_bounds__(PS_THREADS) void parse_cpu_kernel(int64_t n, const uint8_t* __restrict__ bytes,
+                                                               int64_t n_bytes,
+                                                               const int64_t* __restrict__ off,
+                                                               int64_t* __restrict__ out,
+                                                               int8_t* __restrict__ status) {
+  const int64_t b0 = (int64_t)blockIdx.x * PS_BLOCK;
+  const int64_t base = b0 + threadIdx.x;
+  // the workgroup's character span, for one range-checked buffer descriptor: loads past
+  // it (or past n_bytes) read 0 instead of faulting, so every load is unconditional
+  const int64_t cnt = min((int64_t)PS_BLOCK, n - b0);
+  const int64_t lo_b = max(off[b0], (int64_t)0) & ~(int64_t)3;
+  const int64_t hi_b = min(off[b0 + cnt], n_bytes);
+  const bool span_ok = hi_b > lo_b && hi_b - lo_b < ((int64_t)1 << 31);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(bytes + (span_ok ? lo_b : 0)), (short)0, span_ok ? (int)(hi_b - lo_b) : 0,
+      0x00020000);
+  int64_t sb[PS_PER_THREAD], se[PS_PER_THREAD];
+  uint32_t w[PS_PER_THREAD][3];
+  bool fast[PS_PER_THREAD];
+#pragma unroll
+  for (int r = 0; r < PS_PER_THREAD; ++r) {
+    const int64_t i = min(base + r * PS_THREADS, n - 1);
+    sb[r] = off[i];
+    se[r] = off[i + 1];
+  }
+#pragma unroll
+  for (int r = 0; r < PS_PER_THREAD; ++r) {
+    const int64_t a = sb[r] & ~(int64_t)3;
+    const int64_t L = se[r] - sb[r];
+    fast[r] = span_ok && sb[r] >= lo_b && L >= 1 && L <= 9 && a + 12 <= hi_b;
+    typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+    const u32x3 x = __builtin_bit_cast(
+        u32x3, __builtin_amdgcn_raw_buffer_load_b96(rs, fast[r] ? (int)(a - lo_b) : 0x7ffffff0, 0, 0));
+    w[r][0] = x.x;
+    w[r][1] = x.y;
+    w[r][2] = x.z;
+  }
+#pragma unroll
+  for (int r = 0; r < PS_PER_THREAD; ++r) {
+    const int64_t i = base + r * PS_THREADS;
+    if (i >= n) break;
+    int64_t v = 0;
+    int8_t st = PARSE_BADOFF;
+    bool done = false;
+    if (fast[r]) {
+      const int L = (int)(se[r] - sb[r]);
+      const int sh = (int)(sb[r] & 3) * 8;
+      const uint64_t lo = ((uint64_t)w[r][1] << 32) | w[r][0];
+      const uint64_t hi = w[r][2];
+      const uint64_t c = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;  // characters 0..7
+      const uint32_t last = L == 9 ? (uint32_t)(hi >> sh) & 0xffu : (uint32_t)(c >> (8 * (L - 1))) & 0xffu;
+      const bool milli = last == 'm';
+      const int d = L - (milli ? 1 : 0);
+      const uint32_t c0 = (uint32_t)c & 0xffu;
+      if (d >= 1 && d <= 8 && c0 != '+' && c0 != '-') {
+        // d digits, left-padded with '0' to eight
+        const uint64_t cp =
+            d == 8 ? c : (c << (8 * (8 - d))) | (0x3030303030303030ull >> (8 * d));
+        uint64_t x;
+        if (swar8(cp, x)) {
+          v = (int64_t)(milli ? x : x * 1000u);
+          st = PARSE_OK;
+        } else {
+          st = PARSE_ERR;  // unsigned, non-digit inside: strconv.Atoi fails
+        }
+        done = true;
+      }
+    }
+    if (!done && sb[r] >= 0 && se[r] >= sb[r] && se[r] <= n_bytes && se[r] - sb[r] < ((int64_t)1 << 31))
+      v = (int64_t)cpu_millis_value(bytes + sb[r], (int)(se[r] - sb[r]), st);
+    out[i] = v;
+    status[i] = st;
+  }
+}
+
 }  // namespace
 
 int64_t parse_grid(int64_t n) { return (n + PS_BLOCK - 1) / PS_BLOCK; }
@@ -330,8 +423,8 @@ hipError_t launch_parse(int mode, int64_t n, const uint8_t* bytes, int64_t n_byt
   const int64_t grid = parse_grid(n);
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   if (mode == PARSE_MODE_CPU_MILLIS)
-    hipLaunchKernelGGL(parse_kernel<PARSE_MODE_CPU_MILLIS>, dim3((unsigned)grid), dim3(PS_THREADS), 0,
-                       s, n, bytes, n_bytes, offsets, out, status);
+    hipLaunchKernelGGL(parse_cpu_kernel, dim3((unsigned)grid), dim3(PS_THREADS), 0, s, n, bytes,
+                       n_bytes, offsets, out, status);
   else
     hipLaunchKernelGGL(parse_kernel<PARSE_MODE_BYTES>, dim3((unsigned)grid), dim3(PS_THREADS), 0, s,
                        n, bytes, n_bytes, offsets, out, status);

@@ -19,9 +19,17 @@ def have_gpu() -> bool:
         return False
 
 
+def init_torch_first():
+    """Initialise torch's HIP runtime (bundled with the wheel) before libkcc's (/opt/rocm):
+    torch's fails to come up in a process where the other one initialised first."""
+    import torch
+    torch.cuda.init()
+
+
 @pytest.fixture(scope="session")
 def engine():
     """One libkcc context for the whole GPU session (device 0)."""
+    init_torch_first()
     from kubernetesclustercapacity_amd import CapacityEngine
     eng = CapacityEngine(0, 1)
     yield eng

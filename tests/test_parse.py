@@ -180,6 +180,8 @@ def test_golden_parse_fixture():
 # ---- GPU: the kernels through the C-ABI ---------------------------------------------
 @pytest.fixture(scope="module")
 def eng():
+    from tests.conftest import init_torch_first
+    init_torch_first()
     from kubernetesclustercapacity_amd import CapacityEngine
     with CapacityEngine(0, 1) as e:
         yield e
