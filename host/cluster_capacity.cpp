@@ -165,12 +165,13 @@ int main(int argc, char** argv) {
     return 2;
   }
   const std::vector<node> rows = getHealthyNodes(cl);
-  const EngineInputs in = buildInputs(cl, rows);
-  const int64_t n = (int64_t)rows.size(), nc = (int64_t)in.cpu_req.size();
-
   kcc_ctx* ctx = nullptr;
   int rc = kcc_create(&ctx, std::atoi(f.v["device"].c_str()), std::atoi(f.v["gpus"].c_str()));
   if (rc) return fail(nullptr, rc);
+  EngineInputs in;
+  rc = buildInputs(ctx, cl, rows, in);  // container cpu strings parsed on the device
+  if (rc) return fail(ctx, rc);
+  const int64_t n = (int64_t)rows.size(), nc = (int64_t)in.cpu_req.size();
 
   if (verbose) {  // CC:107-117, 137 — per-node sums and fit, one row at a time
     std::vector<uint64_t> uc(n), lc(n);

@@ -180,27 +180,50 @@ std::vector<size_t> getNonTerminatedPodsForNode(const Cluster& c, const std::str
   return out;
 }
 
-EngineInputs buildInputs(const Cluster& c, const std::vector<node>& rows) {
-  EngineInputs in;
+int buildInputs(kcc_ctx* ctx, const Cluster& c, const std::vector<node>& rows, EngineInputs& in) {
+  in = EngineInputs{};
+  std::string chars;          // limit, request, limit, request, ... (CC:279-283 order)
+  std::vector<int64_t> off{0};
   for (const node& r : rows) {  // CC:105: every row, zero rows included (name "")
     const std::vector<size_t> pods = getNonTerminatedPodsForNode(c, r.name);
     for (size_t pi : pods) {
       const Pod& p = c.pods[pi];
       if (p.getFails) continue;  // NotFound: skipped by the sum (CC:267-268), still counted
       for (const Container& ct : p.containers) {  // CC:277-293
-        in.cpu_req.push_back(convertCPUToMilis(ct.cpuRequest, nullptr, false));
-        in.cpu_lim.push_back(convertCPUToMilis(ct.cpuLimit, nullptr, false));
+        chars += ct.cpuLimit;
+        off.push_back((int64_t)chars.size());
+        chars += ct.cpuRequest;
+        off.push_back((int64_t)chars.size());
         in.mem_req.push_back(ct.memRequest);
         in.mem_lim.push_back(ct.memLimit);
       }
     }
-    in.node_ptr.push_back((int64_t)in.cpu_req.size());
+    in.node_ptr.push_back((int64_t)in.mem_req.size());
     in.alloc_cpu.push_back(r.allocatableCPU);
     in.alloc_mem.push_back(r.allocatableMemory);
     in.alloc_pods.push_back(r.allocatablePods);
     in.pod_count.push_back((int64_t)pods.size());  // len(pods), CC:106/135
   }
-  return in;
+  const int64_t ns = (int64_t)off.size() - 1;
+  std::vector<uint64_t> millis((size_t)ns);
+  std::vector<int8_t> st((size_t)ns);
+  chars.resize((chars.size() + 4) & ~(size_t)3, '\0');  // 4-byte padded buffer
+  if (ns > 0) {
+    const int rc = kcc_parse_cpu_millis(ctx, ns, chars.data(), off[ns], off.data(), millis.data(),
+                                        st.data());
+    if (rc) return rc;
+  }
+  in.cpu_lim.resize((size_t)ns / 2);
+  in.cpu_req.resize((size_t)ns / 2);
+  for (int64_t k = 0; k < ns; ++k) {
+    if (st[k] != KCC_PARSE_OK) {  // CC:315-316 prints the string without its 'm'
+      std::string s = chars.substr((size_t)off[k], (size_t)(off[k + 1] - off[k]));
+      if (!s.empty() && s.back() == 'm') s.pop_back();
+      std::printf("\nError converting string to int for %s\n", s.c_str());
+    }
+    (k & 1 ? in.cpu_req : in.cpu_lim)[(size_t)k / 2] = millis[k];
+  }
+  return KCC_OK;
 }
 
 }  // namespace kcchost

@@ -14,6 +14,8 @@
 #include <utility>
 #include <vector>
 
+#include "kcc.h"
+
 namespace kcchost {
 
 // CC:301-319.  Prints "\nError converting string to int for <s>\n" and returns 0 on an
@@ -79,6 +81,10 @@ struct EngineInputs {
   std::vector<uint64_t> alloc_cpu;
   std::vector<int64_t> alloc_mem, alloc_pods, pod_count;
 };
-EngineInputs buildInputs(const Cluster& c, const std::vector<node>& rows);
+// The container cpu strings (limits and requests, CC:279-283) are converted on the device
+// in one kcc_parse_cpu_millis batch on `ctx`; each failed string prints
+// the reference's "Error converting string to int" line, in the reference's order
+// (per container: limit, then request).  Returns a KCC_E* code (0 on success).
+int buildInputs(kcc_ctx* ctx, const Cluster& c, const std::vector<node>& rows, EngineInputs& in);
 
 }  // namespace kcchost

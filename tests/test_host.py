@@ -197,3 +197,23 @@ def test_cli_end_to_end(cli, tmp_path):
     assert r.returncode == 2 and "integer divide by zero" in r.stderr
     r = _run(["-cluster", path, "-v"])
     assert r.returncode == 0 and r.stdout.count("Max replicas :") == 60
+
+
+@pytest.mark.gpu
+def test_cli_container_cpu_strings_on_device(cli, tmp_path):
+    """Container cpu strings go through kcc_parse_cpu_millis; failures print the
+    reference's line (CC:315-316, without the trailing 'm') in limit, request order."""
+    path = tmp_path / "c.txt"
+    path.write_text("node n0 4 16331524Ki 110 False False False False\n"
+                    "pod n0 ns p0 Running\n"
+                    "container 250m 0.5 0 0\n"
+                    "container 1500m 2km 0 0\n"
+                    "container 1 1 0 0\n")
+    r = _run(["-cluster", str(path), "-cpuRequests=100m", "-memRequests=100mb", "-v"])
+    assert r.returncode == 0, r.stderr
+    errs = [ln for ln in r.stdout.splitlines() if ln.startswith("Error converting")]
+    # container lines are "<cpuRequest> <cpuLimit> ...": limits 0.5 and 2km fail
+    assert errs == ["Error converting string to int for 0.5", "Error converting string to int for 2k"]
+    # limits 0 + 0 + 1000, requests 250 + 1500 + 1000
+    assert "Sum of CPU Limits, Requests and Memory Limits, Requests for all pods : 1000 2750 0 0" \
+        in r.stdout
