@@ -286,7 +286,9 @@ def parse_leg(eng, cl, dev, stream, steps, warmup, with_cpu):
         "kernel": "parse_kernel<0>", "strings": n, "chars": nbytes,
         "ms_per_launch": ms, "strings_per_s": n / (ms * 1e-3),
         "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": alg},
+                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": alg,
+                     "traffic": pmc_traffic("parse_cpu_kernel")[0],
+                     "traffic_source": pmc_traffic("parse_cpu_kernel")[1]},
         "round_trip_exact": ok, "format_seconds": fmt_s,
     }
     del d_buf, d_off, d_out, d_st

@@ -9,6 +9,7 @@
 #include <cctype>
 #include <cerrno>
 #include <cinttypes>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -91,6 +92,16 @@ bool goAtoiStrict(const std::string& s, int64_t& out) {
 }
 
 // CC:64-83: parse one spec exactly like the flags; exits like the reference on error.
+// Go fmt "%.2f" (CC:117): NaN prints "NaN" and infinities "+Inf" / "-Inf" (an
+// unhealthy node's zero row divides 0 by 0, CC:112-115); finite values format like C's.
+std::string goF2(double x) {
+  if (std::isnan(x)) return "NaN";
+  if (std::isinf(x)) return x > 0 ? "+Inf" : "-Inf";
+  char b[64];
+  std::snprintf(b, sizeof b, "%.2f", x);
+  return b;
+}
+
 void parseSpec(Spec& s, bool verbose_errors) {
   s.cpu = convertCPUToMilis(s.cpuStr);
   const auto mem = ToBytes(s.memStr);
@@ -195,8 +206,9 @@ int main(int argc, char** argv) {
                   rows[i].allocatableMemory);
       const double ac = (double)rows[i].allocatableCPU, am = (double)rows[i].allocatableMemory;
       std::printf("\nCPU Limits, Requests and Memory Limits, Requests used percentage till now : "
-                  "%.2f %.2f %.2f %.2f", (double)lc[i] * 100 / ac, (double)uc[i] * 100 / ac,
-                  (double)lm[i] * 100 / am, (double)um[i] * 100 / am);
+                  "%s %s %s %s", goF2((double)lc[i] * 100 / ac).c_str(),
+                  goF2((double)uc[i] * 100 / ac).c_str(), goF2((double)lm[i] * 100 / am).c_str(),
+                  goF2((double)um[i] * 100 / am).c_str());
       if (e) {
         std::fprintf(stderr, "panic: runtime error: integer divide by zero\n");
         kcc_destroy(ctx);

@@ -217,3 +217,25 @@ def test_cli_container_cpu_strings_on_device(cli, tmp_path):
     # limits 0 + 0 + 1000, requests 250 + 1500 + 1000
     assert "Sum of CPU Limits, Requests and Memory Limits, Requests for all pods : 1000 2750 0 0" \
         in r.stdout
+
+
+@pytest.mark.gpu
+def test_cli_verbose_rows_go_format(cli, tmp_path):
+    """-v per-node report (CC:107-117): an unhealthy node's zero row prints Go's NaN /
+    +Inf for the percentages (0*100/0, x*100/0), the struct as {name cpu mem pods}."""
+    path = tmp_path / "c.txt"
+    path.write_text("node a 4 16331524Ki 110 False False False False\n"
+                    "node b 8 32Gi 110 False True False False\n"
+                    "pod a ns p0 Running\n"
+                    "container 250m 500m 1073741824 0\n"
+                    "pod - ns p1 Running\n"
+                    "container 100m 0 0 0\n")
+    r = _run(["-cluster", str(path), "-cpuRequests=100m", "-memRequests=100mb", "-v"])
+    assert r.returncode == 0, r.stderr
+    out = r.stdout
+    assert "{a 4000 16723480576 110} - Current non-terminated pods : 1" in out
+    assert "used percentage till now : 12.50 6.25 0.00 6.42" in out
+    # node b is unhealthy: zero row named "", which lists the unscheduled pod (nodeName "")
+    assert "{ 0 0 0} - Current non-terminated pods : 1" in out
+    assert "used percentage till now : NaN +Inf NaN NaN" in out
+    assert "Max replicas : -1" in out  # findMin(0, 0) >= 0 pods -> 0 - 1
