@@ -167,6 +167,18 @@ std::vector<node> getHealthyNodes(const Cluster& c, bool print) {
   return healthy;
 }
 
+std::map<std::string, std::vector<size_t>> nonTerminatedPodsByNode(const Cluster& c) {
+  std::map<std::string, std::vector<size_t>> out;
+  for (size_t i = 0; i < c.pods.size(); ++i) {  // pods in list order within each node
+    const Pod& p = c.pods[i];
+    if (p.phase == "Pending" || p.phase == "Succeeded" || p.phase == "Failed" ||
+        p.phase == "Unknown")
+      continue;
+    out[p.nodeName].push_back(i);
+  }
+  return out;
+}
+
 std::vector<size_t> getNonTerminatedPodsForNode(const Cluster& c, const std::string& nodeName) {
   std::vector<size_t> out;
   for (size_t i = 0; i < c.pods.size(); ++i) {  // field selector of CC:236
@@ -184,8 +196,14 @@ int buildInputs(kcc_ctx* ctx, const Cluster& c, const std::vector<node>& rows, E
   in = EngineInputs{};
   std::string chars;          // limit, request, limit, request, ... (CC:279-283 order)
   std::vector<int64_t> off{0};
+  // one cluster-wide pass (the List of CC:236 with the phase selector)
+  // grouped by spec.nodeName, instead of one List per node row; a zero row (name "")
+  // gets the pods whose nodeName is "", like the reference's per-row List
+  const std::map<std::string, std::vector<size_t>> by_node = nonTerminatedPodsByNode(c);
+  const std::vector<size_t> none;
   for (const node& r : rows) {  // CC:105: every row, zero rows included (name "")
-    const std::vector<size_t> pods = getNonTerminatedPodsForNode(c, r.name);
+    const auto it = by_node.find(r.name);
+    const std::vector<size_t>& pods = it == by_node.end() ? none : it->second;
     for (size_t pi : pods) {
       const Pod& p = c.pods[pi];
       if (p.getFails) continue;  // NotFound: skipped by the sum (CC:267-268), still counted

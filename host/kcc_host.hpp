@@ -10,6 +10,7 @@
 #pragma once
 
 #include <cstdint>
+#include <map>
 #include <string>
 #include <utility>
 #include <vector>
@@ -72,6 +73,10 @@ std::vector<node> getHealthyNodes(const Cluster& c, bool print = true);
 // CC:232-253 — indices of the pods on `nodeName` whose phase is not Pending,
 // Succeeded, Failed or Unknown.
 std::vector<size_t> getNonTerminatedPodsForNode(const Cluster& c, const std::string& nodeName);
+
+// The same selection for every node at once (one cluster-wide pass, grouped by
+// spec.nodeName): nodeName -> pod indices in list order.
+std::map<std::string, std::vector<size_t>> nonTerminatedPodsByNode(const Cluster& c);
 
 // Per-row inputs of the engine: CSR containers (requests), podCount = len(pods).
 struct EngineInputs {
