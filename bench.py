@@ -62,6 +62,8 @@ def parse():
                     help="node chunks of the pipelined step (reduce of chunk k overlaps the fit "
                          "of chunk k-1); 1 = reduce, then fit")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-keyed", action="store_true",
+                    help="skip the list-order (keyed) reduce leg (SURVEY §8f row 1)")
     ap.add_argument("--no-parse", action="store_true",
                     help="skip the quantity-string parse leg (SURVEY §8f row 2)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -237,6 +239,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cl, sc, sm, totals.cpu().numpy(), err.cpu().numpy(),
                                            args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_keyed:
+        out["keyed"] = keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream,
+                                 args.steps, args.warmup)
     if rank == 0 and world == 1 and not args.no_parse:
         del ptr, cpu, mem
         out["parse"] = parse_leg(eng, cl, dev, stream, args.steps, args.warmup,
@@ -246,6 +251,52 @@ def main():
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+def keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream, steps, warmup):
+    """SURVEY §8f row 1, measured beside the step (not part of `value`): the C4 containers
+    in a random order (a cluster-wide pod List, without even a pod's containers kept
+    together: every container is its own run, the atomic worst case), each keyed by its
+    node's row -> per-row sums (kcc_reduce_requests_keyed), checked equal to the CSR
+    reduce of the step.  Algorithmic bytes per launch: C x (4 key + 16 requests) in,
+    n x 16 sums out."""
+    import torch
+
+    C = cpu.numel()
+    g = torch.Generator(device=dev)
+    g.manual_seed(20261016)
+    perm = torch.randperm(C, device=dev, generator=g)
+    node_of = torch.repeat_interleave(torch.arange(n, device=dev, dtype=torch.int32),
+                                      torch.diff(ptr))
+    key = node_of[perm].contiguous()
+    kc, km = cpu[perm].contiguous(), mem[perm].contiguous()
+    del perm, node_of
+    oc = torch.empty(n, dtype=torch.int64, device=dev)
+    om = torch.empty(n, dtype=torch.int64, device=dev)
+    with torch.cuda.stream(stream):
+        for _ in range(warmup):
+            eng.reduce_requests_keyed_async(n, key, kc, km, oc, om, stream=stream)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        ev0.record(stream)
+        for _ in range(steps):
+            eng.reduce_requests_keyed_async(n, key, kc, km, oc, om, stream=stream)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / steps
+    ok = bool(torch.equal(oc, used_cpu) and torch.equal(om, used_mem))
+    alg = C * 20 + n * 16
+    gbs = alg / (ms * 1e-3) / 1e9
+    del key, kc, km, oc, om
+    return {
+        "op": "per-row request sums of CC:290-293 from containers in list order (random)",
+        "kernel": "reduce_keyed_kernel<2> (+2 memsets)", "containers": C, "rows": n,
+        "ms_per_launch": ms, "containers_per_s": C / (ms * 1e-3),
+        "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": alg,
+                     "note": "2 x 64-bit device atomics per container (random rows)"},
+        "equals_csr_reduce": ok,
+    }
 
 
 def parse_leg(eng, cl, dev, stream, steps, warmup, with_cpu):

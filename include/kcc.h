@@ -237,6 +237,29 @@ int kcc_parse_bytes_async(kcc_ctx* ctx, int64_t n, const char* d_bytes, int64_t 
                           const int64_t* d_offsets, int64_t* d_out, int8_t* d_status,
                           void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Per-node sums from containers in LIST order.  A cluster-wide
+ * Pods("").List (one call instead of the per-node List of CC:236) returns pods in
+ * namespace/name order; key[i] is the row of container i's node (<0 or >= n_keys:
+ * skipped).  Same sums as kcc_reduce_requests on the grouped (CSR) containers, bit for
+ * bit (wrapping addition does not depend on order).  kcc_count_by_key gives
+ * len(pods) per row (CC:106, CC:135) from the pods' keys.  Arrays 16-byte aligned.
+ * ------------------------------------------------------------------------- */
+int kcc_reduce_requests_keyed(kcc_ctx* ctx, int64_t n_keys, int64_t n_containers,
+                              const int32_t* key, const uint64_t* cpu_req, const int64_t* mem_req,
+                              const uint64_t* cpu_lim, const int64_t* mem_lim,
+                              uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu,
+                              int64_t* lim_mem);
+int kcc_reduce_requests_keyed_async(kcc_ctx* ctx, int64_t n_keys, int64_t n_containers,
+                                    const int32_t* d_key, const uint64_t* d_cpu_req,
+                                    const int64_t* d_mem_req, const uint64_t* d_cpu_lim,
+                                    const int64_t* d_mem_lim, uint64_t* d_used_cpu,
+                                    int64_t* d_used_mem, uint64_t* d_lim_cpu, int64_t* d_lim_mem,
+                                    void* stream);
+int kcc_count_by_key(kcc_ctx* ctx, int64_t n_keys, int64_t n, const int32_t* key, int64_t* count);
+int kcc_count_by_key_async(kcc_ctx* ctx, int64_t n_keys, int64_t n, const int32_t* d_key,
+                           int64_t* d_count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -53,6 +53,10 @@ SIGNATURES = {
     "kcc_parse_bytes": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp]),
     "kcc_parse_cpu_millis_async": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp]),
     "kcc_parse_bytes_async": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp]),
+    "kcc_reduce_requests_keyed": (_int, [_vp, _i64, _i64] + [_vp] * 9),
+    "kcc_reduce_requests_keyed_async": (_int, [_vp, _i64, _i64] + [_vp] * 10),
+    "kcc_count_by_key": (_int, [_vp, _i64, _i64, _vp, _vp]),
+    "kcc_count_by_key_async": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
 }
 
 # per-string status of kcc_parse_* (include/kcc.h)

@@ -73,6 +73,7 @@ struct Dev {
   DevBuf ptr, cpu, mem, cpul, meml, used_cpu, used_mem, lim_cpu, lim_mem;
   DevBuf alloc_cpu, alloc_mem, alloc_pods, pod_count, spec_cpu, spec_mem, partial, totals, err;
   DevBuf p_bytes, p_off, p_out, p_st;  // kcc_parse_* staging
+  DevBuf k_key;                        // kcc_*_keyed staging
 };
 
 }  // namespace
@@ -984,3 +985,126 @@ int kcc_parse_bytes_async(kcc_ctx* ctx, int64_t n, const char* d_bytes, int64_t 
   return parse_async_dev(ctx, kcc::PARSE_MODE_BYTES, n, d_bytes, n_bytes, d_offsets, d_out,
                          d_status, static_cast<hipStream_t>(stream));
 }
+
+
+// ---- list-order (keyed) reduce ------------------------------------
+
+namespace {
+
+int keyed_async_dev(kcc_ctx* ctx, int64_t n_keys, int64_t n, const int32_t* key,
+                    const uint64_t* cpu, const int64_t* mem, const uint64_t* cpul,
+                    const int64_t* meml, uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu,
+                    int64_t* lim_mem, hipStream_t s) {
+  if (n_keys < 0 || n < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (n_keys > 0x7fffffff) return fail(ctx, KCC_EINVAL, "more than 2^31 - 1 keys");
+  if (n_keys > 0 && (!used_cpu || !used_mem)) return fail(ctx, KCC_EINVAL, "NULL output");
+  if (n > 0 && (!key || !cpu || !mem)) return fail(ctx, KCC_EINVAL, "NULL key/cpu_req/mem_req");
+  const bool lim = cpul != nullptr || meml != nullptr;
+  if (lim && (!cpul || !meml || (n_keys > 0 && (!lim_cpu || !lim_mem))))
+    return fail(ctx, KCC_EINVAL, "limits need cpu_lim, mem_lim, lim_cpu and lim_mem");
+  if (!aligned16(key) || !aligned16(cpu) || !aligned16(mem) ||
+      (lim && (!aligned16(cpul) || !aligned16(meml))))
+    return fail(ctx, KCC_EINVAL, "key and container arrays must be 16-byte aligned");
+  KCC_HIP(ctx, kcc::launch_reduce_keyed(n_keys, n, key, cpu, mem, lim ? cpul : nullptr,
+                                        lim ? meml : nullptr, used_cpu, used_mem,
+                                        lim ? lim_cpu : nullptr, lim ? lim_mem : nullptr, s));
+  return KCC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kcc_reduce_requests_keyed_async(kcc_ctx* ctx, int64_t n_keys, int64_t n_containers,
+                                    const int32_t* d_key, const uint64_t* d_cpu_req,
+                                    const int64_t* d_mem_req, const uint64_t* d_cpu_lim,
+                                    const int64_t* d_mem_lim, uint64_t* d_used_cpu,
+                                    int64_t* d_used_mem, uint64_t* d_lim_cpu, int64_t* d_lim_mem,
+                                    void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  return keyed_async_dev(ctx, n_keys, n_containers, d_key, d_cpu_req, d_mem_req, d_cpu_lim,
+                         d_mem_lim, d_used_cpu, d_used_mem, d_lim_cpu, d_lim_mem,
+                         static_cast<hipStream_t>(stream));
+}
+
+int kcc_reduce_requests_keyed(kcc_ctx* ctx, int64_t n_keys, int64_t n_containers,
+                              const int32_t* key, const uint64_t* cpu_req, const int64_t* mem_req,
+                              const uint64_t* cpu_lim, const int64_t* mem_lim,
+                              uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu,
+                              int64_t* lim_mem) {
+  if (!ctx) return KCC_EINVAL;
+  if (n_keys < 0 || n_containers < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (n_keys > 0 && (!used_cpu || !used_mem)) return fail(ctx, KCC_EINVAL, "NULL output");
+  if (n_containers > 0 && (!key || !cpu_req || !mem_req))
+    return fail(ctx, KCC_EINVAL, "NULL key/cpu_req/mem_req");
+  const bool lim = cpu_lim != nullptr || mem_lim != nullptr;
+  if (lim && (!cpu_lim || !mem_lim || (n_keys > 0 && (!lim_cpu || !lim_mem))))
+    return fail(ctx, KCC_EINVAL, "limits need cpu_lim, mem_lim, lim_cpu and lim_mem");
+  if (n_keys == 0) return KCC_OK;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  int rc;
+  if ((rc = h2d(ctx, dv, dv.k_key, key, n_containers))) return rc;
+  if ((rc = h2d(ctx, dv, dv.cpu, cpu_req, n_containers))) return rc;
+  if ((rc = h2d(ctx, dv, dv.mem, mem_req, n_containers))) return rc;
+  if (lim) {
+    if ((rc = h2d(ctx, dv, dv.cpul, cpu_lim, n_containers))) return rc;
+    if ((rc = h2d(ctx, dv, dv.meml, mem_lim, n_containers))) return rc;
+    KCC_HIP(ctx, ensure(dv.lim_cpu, 8 * (size_t)n_keys));
+    KCC_HIP(ctx, ensure(dv.lim_mem, 8 * (size_t)n_keys));
+  }
+  KCC_HIP(ctx, ensure(dv.used_cpu, 8 * (size_t)n_keys));
+  KCC_HIP(ctx, ensure(dv.used_mem, 8 * (size_t)n_keys));
+  rc = keyed_async_dev(ctx, n_keys, n_containers, as<int32_t>(dv.k_key), as<uint64_t>(dv.cpu),
+                       as<int64_t>(dv.mem), lim ? as<uint64_t>(dv.cpul) : nullptr,
+                       lim ? as<int64_t>(dv.meml) : nullptr, as<uint64_t>(dv.used_cpu),
+                       as<int64_t>(dv.used_mem), lim ? as<uint64_t>(dv.lim_cpu) : nullptr,
+                       lim ? as<int64_t>(dv.lim_mem) : nullptr, dv.stream);
+  if (rc) return rc;
+  KCC_HIP(ctx, hipMemcpyAsync(used_cpu, dv.used_cpu.p, 8 * (size_t)n_keys, hipMemcpyDeviceToHost,
+                              dv.stream));
+  KCC_HIP(ctx, hipMemcpyAsync(used_mem, dv.used_mem.p, 8 * (size_t)n_keys, hipMemcpyDeviceToHost,
+                              dv.stream));
+  if (lim) {
+    KCC_HIP(ctx, hipMemcpyAsync(lim_cpu, dv.lim_cpu.p, 8 * (size_t)n_keys,
+                                hipMemcpyDeviceToHost, dv.stream));
+    KCC_HIP(ctx, hipMemcpyAsync(lim_mem, dv.lim_mem.p, 8 * (size_t)n_keys,
+                                hipMemcpyDeviceToHost, dv.stream));
+  }
+  KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
+  return KCC_OK;
+}
+
+int kcc_count_by_key_async(kcc_ctx* ctx, int64_t n_keys, int64_t n, const int32_t* d_key,
+                           int64_t* d_count, void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  if (n_keys < 0 || n < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (n_keys > 0x7fffffff) return fail(ctx, KCC_EINVAL, "more than 2^31 - 1 keys");
+  if ((n_keys > 0 && !d_count) || (n > 0 && !d_key)) return fail(ctx, KCC_EINVAL, "NULL key/count");
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  KCC_HIP(ctx, kcc::launch_count_keyed(n_keys, n, d_key, d_count, static_cast<hipStream_t>(stream)));
+  return KCC_OK;
+}
+
+int kcc_count_by_key(kcc_ctx* ctx, int64_t n_keys, int64_t n, const int32_t* key, int64_t* count) {
+  if (!ctx) return KCC_EINVAL;
+  if (n_keys < 0 || n < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if ((n_keys > 0 && !count) || (n > 0 && !key)) return fail(ctx, KCC_EINVAL, "NULL key/count");
+  if (n_keys == 0) return KCC_OK;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  int rc;
+  if ((rc = h2d(ctx, dv, dv.k_key, key, n))) return rc;
+  KCC_HIP(ctx, ensure(dv.pod_count, 8 * (size_t)n_keys));
+  KCC_HIP(ctx, kcc::launch_count_keyed(n_keys, n, as<int32_t>(dv.k_key), as<int64_t>(dv.pod_count),
+                                       dv.stream));
+  KCC_HIP(ctx, hipMemcpyAsync(count, dv.pod_count.p, 8 * (size_t)n_keys, hipMemcpyDeviceToHost,
+                              dv.stream));
+  KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
+  return KCC_OK;
+}
+
+}  // extern "C"

@@ -229,4 +229,15 @@ int64_t parse_grid(int64_t n);
 hipError_t launch_parse(int mode, int64_t n, const uint8_t* bytes, int64_t n_bytes,
                         const int64_t* offsets, int64_t* out, int8_t* status, hipStream_t s);
 
+// ---- keyed (list-order) reduce (kcc_keyed.hip) --------------------
+// Zeroes the per-key outputs, then adds every container with 0 <= key < n_keys into its
+// key's sums (atomics; wrapping sums are order-independent).  key/value arrays 16-B aligned.
+hipError_t launch_reduce_keyed(int64_t n_keys, int64_t n, const int32_t* key, const uint64_t* cpu,
+                               const int64_t* mem, const uint64_t* cpul, const int64_t* meml,
+                               uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu,
+                               int64_t* lim_mem, hipStream_t s);
+// count[k] = #{i : key[i] == k}
+hipError_t launch_count_keyed(int64_t n_keys, int64_t n, const int32_t* key, int64_t* count,
+                              hipStream_t s);
+
 }  // namespace kcc

@@ -7,6 +7,7 @@ src/KubeAPI/ClusterCapacity.go = CC):
   total_possible_max_replicas          <- main's node loop (CC:101-140)
   convert_cpu_to_milis                 <- convertCPUToMilis (CC:301-319), batched
   to_bytes                             <- bytefmt.ToBytes (BF:75-105), batched
+  get_pod_cpu_memory_requests_limits_keyed  <- CC:255-299 over one cluster-wide pod List
 
 Every call goes through the C-ABI into the gfx950 kernels; nothing is computed here.
 """
@@ -155,6 +156,43 @@ class CapacityEngine:
             self._h, n, cpu_req.size, _p(node_ptr), _p(cpu_req), _p(mem_req),
             *[_p(x) for x in a], sc.size, _p(sc), _p(sm), _p(totals), _p(err)))
         return totals, err
+
+    # -- list-order containers ---------------------------------
+    def get_pod_cpu_memory_requests_limits_keyed(self, n_keys, key, cpu_req, mem_req,
+                                                 cpu_lim=None, mem_lim=None) -> RequestSums:
+        """CC:255-299 for every row at once from containers in list order: key[i] is the
+        row of container i's node (<0 or >= n_keys: not on a listed row)."""
+        key = _arr(key, np.int32)
+        cpu_req, mem_req = _arr(cpu_req, np.uint64), _arr(mem_req, np.int64)
+        lim = cpu_lim is not None or mem_lim is not None
+        if lim and (cpu_lim is None or mem_lim is None):
+            raise ValueError("pass both cpu_lim and mem_lim, or neither")
+        cpu_lim = _arr(cpu_lim, np.uint64) if lim else None
+        mem_lim = _arr(mem_lim, np.int64) if lim else None
+        nc = key.size
+        if cpu_req.size != nc or mem_req.size != nc or (lim and (cpu_lim.size != nc or
+                                                                 mem_lim.size != nc)):
+            raise ValueError("container arrays differ in length")
+        used_cpu, used_mem = np.zeros(n_keys, np.uint64), np.zeros(n_keys, np.int64)
+        lim_cpu = np.zeros(n_keys, np.uint64) if lim else None
+        lim_mem = np.zeros(n_keys, np.int64) if lim else None
+        self._check(self._lib.kcc_reduce_requests_keyed(
+            self._h, n_keys, nc, _p(key), _p(cpu_req), _p(mem_req), _p(cpu_lim), _p(mem_lim),
+            _p(used_cpu), _p(used_mem), _p(lim_cpu), _p(lim_mem)))
+        return RequestSums(lim_cpu, used_cpu, lim_mem, used_mem)
+
+    def count_by_key(self, n_keys, key):
+        """len(pods) per row (CC:106, CC:135) from the pods' row keys."""
+        key = _arr(key, np.int32)
+        count = np.zeros(n_keys, np.int64)
+        self._check(self._lib.kcc_count_by_key(self._h, n_keys, key.size, _p(key), _p(count)))
+        return count
+
+    def reduce_requests_keyed_async(self, n_keys, key, cpu_req, mem_req, used_cpu, used_mem,
+                                    stream=None):
+        self._check(self._lib.kcc_reduce_requests_keyed_async(
+            self._h, n_keys, key.numel(), _dp(key), _dp(cpu_req), _dp(mem_req), None, None,
+            _dp(used_cpu), _dp(used_mem), None, None, _stream(stream)))
 
     # -- quantity strings (SURVEY §8f row 2) -------------------------------------
     def _parse(self, fn, strings, dtype):

@@ -1,0 +1,112 @@
+"""List-order (keyed) request sums: containers of a cluster-wide
+Pods("").List in namespace/name order, each tagged with its node's row, must give the
+sums of getPodCPUMemoryRequestsLimits (CC:255-299) per row bit for bit — checked
+against the C oracle on the same containers grouped into CSR (stable by key)."""
+import numpy as np
+import pytest
+
+from kubernetesclustercapacity_amd import synth
+from oracle import coracle
+
+
+def list_order(c, seed, skip_frac=0.0):
+    """Shuffle a CSR cluster into pod-list order: pods permuted, a pod's containers kept
+    together (as the API returns them); some pods keyed off the rows (skipped)."""
+    rng = np.random.default_rng(seed)
+    n = c.n_nodes
+    node_of = np.repeat(np.arange(n, dtype=np.int32), np.diff(c.node_ptr))
+    # pods: runs of 1-3 containers within a node
+    starts = np.flatnonzero(np.r_[True, (rng.random(node_of.size - 1) < 0.5) |
+                                  (node_of[1:] != node_of[:-1])])
+    mark = np.zeros(node_of.size, bool)
+    mark[starts] = True
+    pod_of = np.cumsum(mark) - 1
+    perm_pods = rng.permutation(starts.size)
+    order = np.argsort(perm_pods[pod_of], kind="stable")
+    key = node_of[order].copy()
+    if skip_frac:
+        bad = rng.random(key.size) < skip_frac
+        key[bad] = rng.choice(np.array([-1, n, n + 7, -(2 ** 31)], np.int32), bad.sum())
+    return key, c.cpu_req[order], c.mem_req[order], order, pod_of[order], key
+
+
+def oracle_keyed(n, key, cpu, mem, cl=None, ml=None):
+    ok = (key >= 0) & (key < n)
+    srt = np.argsort(key[ok], kind="stable")
+    k = key[ok][srt]
+    ptr = np.searchsorted(k, np.arange(n + 1)).astype(np.int64)
+    sel = lambda a: None if a is None else a[ok][srt]  # noqa: E731
+    return coracle.reduce_requests(ptr, sel(cpu), sel(mem), sel(cl), sel(ml))
+
+
+def test_list_order_model_matches_csr():
+    """The host-side model (oracle over the regrouped list) equals the CSR sums."""
+    c = synth.make_cluster(2_000, 30_000, seed=3, chunk=512)
+    key, cpu, mem, *_ = list_order(c, 1)
+    a = oracle_keyed(c.n_nodes, key, cpu, mem)
+    b = coracle.reduce_requests(c.node_ptr, c.cpu_req, c.mem_req)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from tests.conftest import init_torch_first
+    init_torch_first()
+    from kubernetesclustercapacity_amd import CapacityEngine
+    with CapacityEngine(0, 1) as e:
+        yield e
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,pods,skip,adv", [(1, 10, 0.0, False), (3_000, 60_000, 0.0, True),
+                                             (20_000, 400_000, 0.05, True),
+                                             (50_000, 200_000, 0.3, False)])
+def test_gpu_keyed_matches_oracle(eng, n, pods, skip, adv):
+    c = synth.make_cluster(n, pods, seed=n, chunk=1024, adversarial=adv)
+    key, cpu, mem, *_ = list_order(c, n + 1, skip)
+    rng = np.random.default_rng(n)
+    cl = rng.integers(0, 1 << 63, key.size, dtype=np.int64).view(np.uint64) * np.uint64(3)
+    ml = rng.integers(-(1 << 62), 1 << 62, key.size, dtype=np.int64)
+    r = eng.get_pod_cpu_memory_requests_limits_keyed(n, key, cpu, mem, cl, ml)
+    o = oracle_keyed(n, key, cpu, mem, cl, ml)
+    assert np.array_equal(r.cpu_requests, o[0]) and np.array_equal(r.memory_requests, o[1])
+    assert np.array_equal(r.cpu_limits, o[2]) and np.array_equal(r.memory_limits, o[3])
+    r2 = eng.get_pod_cpu_memory_requests_limits_keyed(n, key, cpu, mem)
+    assert np.array_equal(r2.cpu_requests, o[0]) and np.array_equal(r2.memory_requests, o[1])
+
+
+@pytest.mark.gpu
+def test_gpu_keyed_edges(eng):
+    r = eng.get_pod_cpu_memory_requests_limits_keyed(5, np.zeros(0, np.int32), [], [])
+    assert (r.cpu_requests == 0).all() and r.cpu_requests.size == 5
+    # tails (n % 4 != 0), one key everywhere, runs crossing lane quads
+    for nc in (1, 2, 3, 5, 7, 1025):
+        key = np.zeros(nc, np.int32)
+        v = np.arange(1, nc + 1, dtype=np.uint64)
+        r = eng.get_pod_cpu_memory_requests_limits_keyed(1, key, v, v.astype(np.int64))
+        assert int(r.cpu_requests[0]) == nc * (nc + 1) // 2
+    # wrapping: 2^63 + 2^63 == 0 mod 2^64
+    r = eng.get_pod_cpu_memory_requests_limits_keyed(
+        2, np.array([1, 1, 0], np.int32), np.array([1 << 63, 1 << 63, 5], np.uint64),
+        np.array([-(1 << 63), -(1 << 63), 7], np.int64))
+    assert r.cpu_requests.tolist() == [5, 0] and r.memory_requests.tolist() == [7, 0]
+
+
+@pytest.mark.gpu
+def test_gpu_count_by_key(eng):
+    rng = np.random.default_rng(4)
+    key = rng.integers(-3, 1003, 100_003).astype(np.int32)
+    got = eng.count_by_key(1000, key)
+    ok = key[(key >= 0) & (key < 1000)]
+    assert np.array_equal(got, np.bincount(ok, minlength=1000).astype(np.int64))
+
+
+@pytest.mark.gpu
+def test_gpu_keyed_c4_equals_csr(eng):
+    """C4 scale: 1M rows, 39.6M containers in list order == the CSR reduce, bit for bit."""
+    c = synth.config_cluster("C4")
+    key, cpu, mem, *_ = list_order(c, 9)
+    r = eng.get_pod_cpu_memory_requests_limits_keyed(c.n_nodes, key, cpu, mem)
+    s = eng.get_pod_cpu_memory_requests_limits(c.node_ptr, c.cpu_req, c.mem_req)
+    assert np.array_equal(r.cpu_requests, s.cpu_requests)
+    assert np.array_equal(r.memory_requests, s.memory_requests)
