@@ -74,6 +74,7 @@ struct Dev {
   DevBuf alloc_cpu, alloc_mem, alloc_pods, pod_count, spec_cpu, spec_mem, partial, totals, err;
   DevBuf p_bytes, p_off, p_out, p_st;  // kcc_parse_* staging
   DevBuf k_key;                        // kcc_*_keyed staging
+  DevBuf kb_counts, kb_tot, kb_sk, kb_sv;  // kcc::KeyedWork (bucketed keyed reduce)
 };
 
 }  // namespace
@@ -991,6 +992,25 @@ int kcc_parse_bytes_async(kcc_ctx* ctx, int64_t n, const char* d_bytes, int64_t 
 
 namespace {
 
+// Workspace of the bucketed keyed reduce (grows on demand); nullptr when the keys do not
+// fit the bucketed path (the kernels then fall back to device atomics).
+int keyed_work(kcc_ctx* ctx, Dev& dv, int64_t n_keys, int64_t n, int na, kcc::KeyedWork& kw,
+               const kcc::KeyedWork** out) {
+  *out = nullptr;
+  if (!kcc::keyed_bucketed(n_keys, n)) return KCC_OK;
+  const size_t nb = (size_t)kcc::keyed_buckets(n_keys), G = (size_t)kcc::keyed_tiles(n);
+  KCC_HIP(ctx, ensure(dv.kb_counts, 4 * nb * (G > 0 ? G : 1)));
+  KCC_HIP(ctx, ensure(dv.kb_tot, 4 * nb));
+  KCC_HIP(ctx, ensure(dv.kb_sk, 2 * (size_t)(n > 0 ? n : 1)));
+  if (na > 0) KCC_HIP(ctx, ensure(dv.kb_sv, 8 * (size_t)na * (size_t)(n > 0 ? n : 1)));
+  kw.counts = as<uint32_t>(dv.kb_counts);
+  kw.tot = as<uint32_t>(dv.kb_tot);
+  kw.sk = as<uint16_t>(dv.kb_sk);
+  kw.sv = na > 0 ? as<uint64_t>(dv.kb_sv) : nullptr;
+  *out = &kw;
+  return KCC_OK;
+}
+
 int keyed_async_dev(kcc_ctx* ctx, int64_t n_keys, int64_t n, const int32_t* key,
                     const uint64_t* cpu, const int64_t* mem, const uint64_t* cpul,
                     const int64_t* meml, uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu,
@@ -1005,9 +1025,14 @@ int keyed_async_dev(kcc_ctx* ctx, int64_t n_keys, int64_t n, const int32_t* key,
   if (!aligned16(key) || !aligned16(cpu) || !aligned16(mem) ||
       (lim && (!aligned16(cpul) || !aligned16(meml))))
     return fail(ctx, KCC_EINVAL, "key and container arrays must be 16-byte aligned");
+  Dev& dv = ctx->devs[0];
+  kcc::KeyedWork kw{};
+  const kcc::KeyedWork* kwp = nullptr;
+  int rc = keyed_work(ctx, dv, n_keys, n, lim ? 4 : 2, kw, &kwp);
+  if (rc) return rc;
   KCC_HIP(ctx, kcc::launch_reduce_keyed(n_keys, n, key, cpu, mem, lim ? cpul : nullptr,
                                         lim ? meml : nullptr, used_cpu, used_mem,
-                                        lim ? lim_cpu : nullptr, lim ? lim_mem : nullptr, s));
+                                        lim ? lim_cpu : nullptr, lim ? lim_mem : nullptr, kwp, s));
   return KCC_OK;
 }
 
@@ -1085,7 +1110,12 @@ int kcc_count_by_key_async(kcc_ctx* ctx, int64_t n_keys, int64_t n, const int32_
   if ((n_keys > 0 && !d_count) || (n > 0 && !d_key)) return fail(ctx, KCC_EINVAL, "NULL key/count");
   Dev& dv = ctx->devs[0];
   KCC_HIP(ctx, hipSetDevice(dv.device));
-  KCC_HIP(ctx, kcc::launch_count_keyed(n_keys, n, d_key, d_count, static_cast<hipStream_t>(stream)));
+  kcc::KeyedWork kw{};
+  const kcc::KeyedWork* kwp = nullptr;
+  int rc = keyed_work(ctx, dv, n_keys, n, 0, kw, &kwp);
+  if (rc) return rc;
+  KCC_HIP(ctx, kcc::launch_count_keyed(n_keys, n, d_key, d_count, kwp,
+                                       static_cast<hipStream_t>(stream)));
   return KCC_OK;
 }
 
@@ -1099,8 +1129,11 @@ int kcc_count_by_key(kcc_ctx* ctx, int64_t n_keys, int64_t n, const int32_t* key
   int rc;
   if ((rc = h2d(ctx, dv, dv.k_key, key, n))) return rc;
   KCC_HIP(ctx, ensure(dv.pod_count, 8 * (size_t)n_keys));
+  kcc::KeyedWork kw{};
+  const kcc::KeyedWork* kwp = nullptr;
+  if ((rc = keyed_work(ctx, dv, n_keys, n, 0, kw, &kwp))) return rc;
   KCC_HIP(ctx, kcc::launch_count_keyed(n_keys, n, as<int32_t>(dv.k_key), as<int64_t>(dv.pod_count),
-                                       dv.stream));
+                                       kwp, dv.stream));
   KCC_HIP(ctx, hipMemcpyAsync(count, dv.pod_count.p, 8 * (size_t)n_keys, hipMemcpyDeviceToHost,
                               dv.stream));
   KCC_HIP(ctx, hipStreamSynchronize(dv.stream));

@@ -230,14 +230,29 @@ hipError_t launch_parse(int mode, int64_t n, const uint8_t* bytes, int64_t n_byt
                         const int64_t* offsets, int64_t* out, int8_t* status, hipStream_t s);
 
 // ---- keyed (list-order) reduce (kcc_keyed.hip) --------------------
-// Zeroes the per-key outputs, then adds every container with 0 <= key < n_keys into its
-// key's sums (atomics; wrapping sums are order-independent).  key/value arrays 16-B aligned.
+// Bucketed path: rows in buckets of KB_ROWS, containers in tiles of KB_TILE.
+constexpr int KB_SHIFT = 12;  // 4096 rows per bucket: ~1 KB runs per tile and array
+constexpr int KB_ROWS = 1 << KB_SHIFT;
+constexpr int KB_TILE = 32768;
+constexpr int64_t KB_NB_MAX = 4096;  // buckets (LDS cursors): n_keys <= 16M rows
+struct KeyedWork {
+  uint32_t* counts;  // [keyed_tiles(n) * keyed_buckets(n_keys)]
+  uint32_t* tot;     // [keyed_buckets(n_keys)]
+  uint16_t* sk;      // [n] scattered rows within the bucket
+  uint64_t* sv;      // [NA * n] scattered values (NA = 2 requests, 4 with limits, 0 counts)
+};
+int64_t keyed_tiles(int64_t n);
+int64_t keyed_buckets(int64_t n_keys);
+bool keyed_bucketed(int64_t n_keys, int64_t n);
+// Writes every per-key output (zero where no container), adding every container with
+// 0 <= key < n_keys (wrapping sums are order-independent).  kw == nullptr or too many keys:
+// memsets + device atomics.  key/value arrays 16-B aligned.
 hipError_t launch_reduce_keyed(int64_t n_keys, int64_t n, const int32_t* key, const uint64_t* cpu,
                                const int64_t* mem, const uint64_t* cpul, const int64_t* meml,
                                uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu,
-                               int64_t* lim_mem, hipStream_t s);
+                               int64_t* lim_mem, const KeyedWork* kw, hipStream_t s);
 // count[k] = #{i : key[i] == k}
 hipError_t launch_count_keyed(int64_t n_keys, int64_t n, const int32_t* key, int64_t* count,
-                              hipStream_t s);
+                              const KeyedWork* kw, hipStream_t s);
 
 }  // namespace kcc

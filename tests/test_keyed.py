@@ -93,6 +93,23 @@ def test_gpu_keyed_edges(eng):
 
 
 @pytest.mark.gpu
+def test_gpu_keyed_atomic_fallback(eng):
+    """More rows than the bucketed path holds (4096 buckets x 4096 rows): the device-atomic
+    kernels."""
+    nk = 4096 * 4096 + 5
+    rng = np.random.default_rng(6)
+    key = rng.integers(-2, nk + 2, 50_001).astype(np.int32)
+    key[:7] = [nk - 1, nk - 1, 0, 0, 5, nk, -1]
+    v = rng.integers(0, 1 << 62, key.size).astype(np.uint64)
+    r = eng.get_pod_cpu_memory_requests_limits_keyed(nk, key, v, v.astype(np.int64))
+    o = oracle_keyed(nk, key, v, v.astype(np.int64))
+    assert np.array_equal(r.cpu_requests, o[0]) and np.array_equal(r.memory_requests, o[1])
+    got = eng.count_by_key(nk, key)
+    ok = key[(key >= 0) & (key < nk)]
+    assert np.array_equal(got, np.bincount(ok, minlength=nk).astype(np.int64))
+
+
+@pytest.mark.gpu
 def test_gpu_count_by_key(eng):
     rng = np.random.default_rng(4)
     key = rng.integers(-3, 1003, 100_003).astype(np.int32)
