@@ -291,11 +291,12 @@ def keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream, steps, war
     del key, kc, km, oc, om
     return {
         "op": "per-row request sums of CC:290-293 from containers in list order (random)",
-        "kernel": "reduce_keyed_kernel<2> (+2 memsets)", "containers": C, "rows": n,
+        "kernel": "kb_hist + kb_scan + kb_scatter<2> + kb_accum<2>", "containers": C, "rows": n,
         "ms_per_launch": ms, "containers_per_s": C / (ms * 1e-3),
         "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": alg,
-                     "note": "2 x 64-bit device atomics per container (random rows)"},
+                     "note": "bucketed: LDS histograms, staged scatter, LDS accumulation; "
+                             "no global atomics"},
         "equals_csr_reduce": diff_rows == 0, "rows_differing": diff_rows,
     }
 
