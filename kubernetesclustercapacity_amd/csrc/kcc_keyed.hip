@@ -226,17 +226,30 @@ __global__ __launch_bounds__(KB_HIST_THREADS) void kb_scatter(
   __syncthreads();
   const int64_t t0 = (int64_t)blockIdx.x * KB_TILE;
   const int64_t t1 = min(t0 + (int64_t)KB_TILE, n);
+  // sub-chunk loads run one sub-chunk ahead: issued before this one's scan, stage and
+  // writes, consumed at the top of the next iteration
+  int32_t kn[KB_SUB_PER];
+  uint64_t vn[NS][KB_SUB_PER];
+  auto load_sub = [&](int64_t c0) {
+#pragma unroll
+    for (int u = 0; u < KB_SUB_PER; ++u) {
+      const int64_t c = c0 + (int64_t)u * KB_HIST_THREADS + threadIdx.x;
+      const bool ok = c < t1;
+      kn[u] = ok ? __builtin_nontemporal_load(key + c) : -1;
+#pragma unroll
+      for (int a = 0; a < NA; ++a) vn[a][u] = ok ? __builtin_nontemporal_load(in[a] + c) : 0;
+    }
+  };
+  load_sub(t0);
   for (int64_t c0 = t0; c0 < t1; c0 += KB_SUB) {
     int32_t k[KB_SUB_PER];
     uint32_t rk[KB_SUB_PER];
     uint64_t v[NS][KB_SUB_PER];
 #pragma unroll
     for (int u = 0; u < KB_SUB_PER; ++u) {
-      const int64_t c = c0 + (int64_t)u * KB_HIST_THREADS + threadIdx.x;
-      const bool ok = c < t1;
-      k[u] = ok ? __builtin_nontemporal_load(key + c) : -1;
+      k[u] = kn[u];
 #pragma unroll
-      for (int a = 0; a < NA; ++a) v[a][u] = ok ? __builtin_nontemporal_load(in[a] + c) : 0;
+      for (int a = 0; a < NA; ++a) v[a][u] = vn[a][u];
     }
 #pragma unroll
     for (int u = 0; u < KB_SUB_PER; ++u) {
@@ -244,15 +257,27 @@ __global__ __launch_bounds__(KB_HIST_THREADS) void kb_scatter(
       if (!valid) k[u] = -1;
       rk[u] = valid ? atomicAdd(&lcnt[k[u] >> KB_SHIFT], 1u) : 0u;
     }
+    load_sub(c0 + KB_SUB);  // past t1: every lane reads nothing
     __syncthreads();
-    // lstart = exclusive scan of lcnt (per-thread runs of buckets)
-    uint32_t ls = 0;
-    for (int b = b0; b < b1; ++b) ls += lcnt[b];
-    const uint32_t li = block_incl_scan<KB_HIST_THREADS>(ls, sh);
-    uint32_t lr = li - ls;
-    for (int b = b0; b < b1; ++b) {
-      lstart[b] = lr;
-      lr += lcnt[b];
+    // lstart = exclusive scan of lcnt: the first wave alone (runs of wb buckets per lane,
+    // a shuffle scan of the run totals), no workgroup-wide scan barriers
+    if (threadIdx.x < 64) {
+      const int wb = (nb + 63) / 64;
+      const int w0 = threadIdx.x * wb, w1 = min(w0 + wb, nb);
+      uint32_t ls = 0;
+      for (int b = w0; b < w1; ++b) ls += lcnt[b];
+      uint32_t li = ls;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(li, d, 64);
+        if ((int)threadIdx.x >= d) li += t;
+      }
+      uint32_t lr = li - ls;
+      for (int b = w0; b < w1; ++b) {
+        lstart[b] = lr;
+        lr += lcnt[b];
+      }
+      if (threadIdx.x == 63) sh[KB_HIST_THREADS - 1] = li;  // valid elements of the sub-chunk
     }
     __syncthreads();
 #pragma unroll
@@ -273,6 +298,7 @@ __global__ __launch_bounds__(KB_HIST_THREADS) void kb_scatter(
 #pragma unroll
       for (int a = 0; a < NA; ++a) sv[(int64_t)a * n + pos] = st_v[a][j];
     }
+    __syncthreads();  // nvalid read, stage drained before the counters change
     for (int b = b0; b < b1; ++b) {  // advance the cursors, clear the sub-chunk counts
       cur[b] += lcnt[b];
       lcnt[b] = 0;
