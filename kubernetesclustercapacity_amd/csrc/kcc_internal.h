@@ -43,6 +43,16 @@ inline int64_t reduce_max_waves(int64_t n_containers) {
 // node range of one CSR is reduced without rebasing anything.
 // Zeroes the per-node outputs and records, for every wave range, the node that owns
 // the range's first container (wave_node[n_waves]).
+struct MarkArgs {
+  int64_t n_nodes, c0, c_end;
+  int32_t range;
+  const int64_t* ptr;
+  int64_t* wave_node;
+  uint64_t *o0, *o1, *o2, *o3;
+};
+MarkArgs mark_args(int64_t n_nodes, int64_t c0, int64_t n_containers, const int64_t* node_ptr,
+                   int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu,
+                   int64_t* lim_mem);
 hipError_t launch_reduce_mark(int64_t n_nodes, int64_t c0, int64_t n_containers,
                               const int64_t* node_ptr, int64_t* wave_node, uint64_t* used_cpu,
                               int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s);
@@ -190,9 +200,12 @@ enum {
 // SpecRec / perm and the sorted arrays (cs, ms, dperm, m_less); then one workgroup per
 // group of 64 c-ranks orders it by m_less (gml, kpos).  Zeroes partial[0..2S) and sets
 // the counters.
+// mark != nullptr: the first launch also runs launch_reduce_mark's work for those args
+// (extra workgroups), so the caller skips launch_reduce_mark.
 hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
                             const int64_t* spec_mem, SpecPrep sp, ClampWork cw, int64_t* partial,
-                            unsigned long long* counters, hipStream_t s);
+                            unsigned long long* counters, hipStream_t s,
+                            const MarkArgs* mark = nullptr);
 // H, H2 -> D_s;  partial[s] -= D_s for the normal specs of clamp-free waves (after every
 // node_prep of the call, before the all-reduce); leaves H and H2 zero
 hipError_t launch_clamp_apply(int64_t n_specs, ClampWork cw,

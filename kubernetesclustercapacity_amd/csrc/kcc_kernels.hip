@@ -44,30 +44,30 @@ __device__ __forceinline__ unsigned long long atomic_add_u64(uint64_t* p, uint64
 // (block flushes of reduce_kernel).  Node indices are local to the launch (ptr and the
 // outputs are offset by the caller); the container offsets in ptr are absolute and the
 // launch covers containers [c0, c_end).
-__global__ void reduce_mark_kernel(int64_t n_nodes, int64_t c0, int64_t c_end, int32_t range,
-                                   const int64_t* __restrict__ ptr,
-                                   int64_t* __restrict__ wave_node, uint64_t* __restrict__ o0,
-                                   uint64_t* __restrict__ o1, uint64_t* __restrict__ o2,
-                                   uint64_t* __restrict__ o3) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n_nodes; j += stride) {
-    int64_t b = ptr[j] - c0, e = ptr[j + 1] - c0;  // relative to the launch's first container
+__device__ __forceinline__ void reduce_mark_body(int64_t blk, int64_t nblk, const MarkArgs& a) {
+  const int64_t n_nodes = a.n_nodes, c0 = a.c0, c_end = a.c_end;
+  const int32_t range = a.range;
+  const int64_t stride = nblk * blockDim.x;
+  for (int64_t j = blk * blockDim.x + threadIdx.x; j < n_nodes; j += stride) {
+    int64_t b = a.ptr[j] - c0, e = a.ptr[j + 1] - c0;  // relative to the launch's first container
     b = b < 0 ? 0 : b;
     e = e > c_end - c0 ? c_end - c0 : e;
     bool zero = e <= 0;  // empty and ahead of every container (all nodes, when none)
     if (e > b) {
       for (int64_t x = (b + range - 1) / range * range; x < e; x += range)
-        wave_node[x / range] = j;
+        a.wave_node[x / range] = j;
       zero = (b / range + 1) * range < e;  // a range boundary strictly inside (b, e)
     }
     if (zero) {
-      o0[j] = 0;
-      o1[j] = 0;
-      if (o2) o2[j] = 0;
-      if (o3) o3[j] = 0;
+      a.o0[j] = 0;
+      a.o1[j] = 0;
+      if (a.o2) a.o2[j] = 0;
+      if (a.o3) a.o3[j] = 0;
     }
   }
 }
+
+__global__ void reduce_mark_kernel(MarkArgs a) { reduce_mark_body(blockIdx.x, gridDim.x, a); }
 
 // DPP controls (gfx9 family): row_shr:n, row_bcast:15/31, wave_shr:1.
 constexpr int DPP_ROW_SHR = 0x110;
@@ -653,10 +653,17 @@ constexpr int RANK_SLICES = 4;  // workgroups per block of 64 queries
 // in LDS, then one atomic per query and count into rank[] (zero between calls).  The
 // query block's first workgroup also writes the query's SpecRec by caller index (rec_o)
 // and zeroes its partial[] entries; the first query block counts the classes.
+// Workgroups from rank_blocks on run reduce_mark_body instead (the reduce's mark fused
+// into this launch: the two are independent, and one launch fewer sits on the step).
 __global__ __launch_bounds__(SPEC_BLOCK) void spec_rank_kernel(int64_t S, const uint64_t* __restrict__ c_in,
                                                                const int64_t* __restrict__ m_in,
                                                                SpecPrep sp, ClampWork cw,
-                                                               int64_t* __restrict__ partial) {
+                                                               int64_t* __restrict__ partial,
+                                                               int64_t rank_blocks, MarkArgs mark) {
+  if ((int64_t)blockIdx.x >= rank_blocks) {  // workgroup-uniform, before any barrier
+    reduce_mark_body((int64_t)blockIdx.x - rank_blocks, (int64_t)gridDim.x - rank_blocks, mark);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   KCC_TL(blockIdx.x, 0);
   constexpr int SLICE_LDS = (int)(8192 / RANK_SLICES);  // staged candidates (S <= 8192)
@@ -1287,13 +1294,27 @@ hipError_t launch_reduce_mark(int64_t n_nodes, int64_t c0, int64_t n_containers,
                               const int64_t* node_ptr, int64_t* wave_node, uint64_t* used_cpu,
                               int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s) {
   if (n_nodes <= 0) return hipSuccess;
-  hipLaunchKernelGGL(reduce_mark_kernel, dim3(grid_for(n_nodes, 256, 8192)), dim3(256), 0, s,
-                     n_nodes, c0, c0 + n_containers, reduce_range(n_containers, lim_cpu != nullptr),
-                     node_ptr, wave_node,
-                     used_cpu,
-                     reinterpret_cast<uint64_t*>(used_mem), lim_cpu,
-                     reinterpret_cast<uint64_t*>(lim_mem));
+  const MarkArgs a = mark_args(n_nodes, c0, n_containers, node_ptr, wave_node, used_cpu, used_mem,
+                               lim_cpu, lim_mem);
+  hipLaunchKernelGGL(reduce_mark_kernel, dim3(grid_for(n_nodes, 256, 8192)), dim3(256), 0, s, a);
   return hipGetLastError();
+}
+
+MarkArgs mark_args(int64_t n_nodes, int64_t c0, int64_t n_containers, const int64_t* node_ptr,
+                   int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu,
+                   int64_t* lim_mem) {
+  MarkArgs a;
+  a.n_nodes = n_nodes;
+  a.c0 = c0;
+  a.c_end = c0 + n_containers;
+  a.range = reduce_range(n_containers, lim_cpu != nullptr);
+  a.ptr = node_ptr;
+  a.wave_node = wave_node;
+  a.o0 = used_cpu;
+  a.o1 = reinterpret_cast<uint64_t*>(used_mem);
+  a.o2 = lim_cpu;
+  a.o3 = reinterpret_cast<uint64_t*>(lim_mem);
+  return a;
 }
 
 hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, const int64_t* node_ptr,
@@ -1342,12 +1363,14 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
 
 hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
                             SpecPrep sp, ClampWork cw, int64_t* partial,
-                            unsigned long long* counters, hipStream_t s) {
+                            unsigned long long* counters, hipStream_t s, const MarkArgs* mark) {
   if (n_specs <= 0) return hipSuccess;
   const int64_t blocks = (n_specs + 63) / 64 * RANK_SLICES;
-  if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(spec_rank_kernel, dim3((unsigned)blocks), dim3(SPEC_BLOCK), 0, s, n_specs,
-                     spec_cpu, spec_mem, sp, cw, partial);
+  const int64_t mblocks = mark && mark->n_nodes > 0 ? grid_for(mark->n_nodes, SPEC_BLOCK, 2048) : 0;
+  if (blocks + mblocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  MarkArgs none{};
+  hipLaunchKernelGGL(spec_rank_kernel, dim3((unsigned)(blocks + mblocks)), dim3(SPEC_BLOCK), 0, s,
+                     n_specs, spec_cpu, spec_mem, sp, cw, partial, blocks, mblocks ? *mark : none);
   hipLaunchKernelGGL(spec_place_kernel, dim3(grid_for(n_specs, 256, 1 << 30)), dim3(256), 0, s,
                      n_specs, sp, cw, counters);
   hipLaunchKernelGGL(spec_groups_kernel, dim3((unsigned)((n_specs + 63) / 64)), dim3(1024), 0, s,
