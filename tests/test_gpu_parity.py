@@ -101,10 +101,12 @@ def test_capacity_vs_oracle(engine, cfg):
 
 
 @pytest.mark.parametrize("s,adv", [(64, False), (4095, False), (4096, False), (4097, False),
-                                   (6000, False), (4100, True), (6000, True)])
+                                   (6000, False), (4100, True), (6000, True), (8193, False),
+                                   (16384, False), (9000, True)])
 def test_spec_count_clamp_paths(engine, s, adv):
-    """Spec counts around the LDS sort / search tables (<= 4096 normal specs: one-workgroup
-    bitonic sort; more: the rank kernels and global searches), with heavy ties."""
+    """Spec counts around the LDS search tables (<= 4096 specs: LDS tables in node_prep;
+    more: global searches) and the rank kernel's staging (<= 8192: candidates staged in
+    LDS; more, e.g. C5's 16384: straight from memory), with heavy ties."""
     c = synth.make_cluster(2_500, 50_000, seed=11, chunk=1024)
     sc, sm = synth.make_specs(s, seed=11, adversarial=adv)
     sc[::3] = sc[0]
