@@ -328,12 +328,13 @@ __global__ __launch_bounds__(KB_ACC_THREADS) void kb_accum(
   const uint32_t start = sh[KB_ACC_THREADS - 1];
   (void)base;
   const uint32_t end = start + tot[b];
-  for (uint32_t i0 = start + threadIdx.x; i0 < end; i0 += KB_ACC_THREADS * KB_UNROLL) {
+  for (int64_t i0 = (int64_t)start + threadIdx.x; i0 < (int64_t)end;
+       i0 += KB_ACC_THREADS * KB_UNROLL) {  // 64-bit: end may be close to 2^32
     uint32_t r[KB_UNROLL];
     uint64_t v[NACC][KB_UNROLL];
 #pragma unroll
     for (int u = 0; u < KB_UNROLL; ++u) {
-      const uint32_t i = i0 + u * KB_ACC_THREADS;
+      const int64_t i = i0 + (int64_t)u * KB_ACC_THREADS;
       const bool ok = i < end;
       r[u] = ok ? (uint32_t)__builtin_nontemporal_load(sk + i) : 0xffffffffu;
 #pragma unroll

@@ -162,7 +162,7 @@ class CapacityEngine:
                                                  cpu_lim=None, mem_lim=None) -> RequestSums:
         """CC:255-299 for every row at once from containers in list order: key[i] is the
         row of container i's node (<0 or >= n_keys: not on a listed row)."""
-        key = _arr(key, np.int32)
+        key = _key32(key)
         cpu_req, mem_req = _arr(cpu_req, np.uint64), _arr(mem_req, np.int64)
         lim = cpu_lim is not None or mem_lim is not None
         if lim and (cpu_lim is None or mem_lim is None):
@@ -183,7 +183,7 @@ class CapacityEngine:
 
     def count_by_key(self, n_keys, key):
         """len(pods) per row (CC:106, CC:135) from the pods' row keys."""
-        key = _arr(key, np.int32)
+        key = _key32(key)
         count = np.zeros(n_keys, np.int64)
         self._check(self._lib.kcc_count_by_key(self._h, n_keys, key.size, _p(key), _p(count)))
         return count
@@ -291,6 +291,15 @@ class CapacityEngine:
         a, b = C.c_int64(), C.c_int64()
         self._check(self._lib.kcc_fit_slow_pairs(self._h, C.byref(a), C.byref(b)))
         return a.value, b.value
+
+
+def _key32(key) -> np.ndarray:
+    """Row keys as int32 (the C-ABI's type); wider keys must fit, never wrap silently."""
+    k = np.asarray(key)
+    if k.dtype != np.int32 and k.size and (k.max() > np.iinfo(np.int32).max or
+                                           k.min() < np.iinfo(np.int32).min):
+        raise ValueError("row keys must fit int32")
+    return np.ascontiguousarray(k, np.int32)
 
 
 def _stream(stream):
