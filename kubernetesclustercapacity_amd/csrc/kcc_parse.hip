@@ -23,6 +23,11 @@ namespace {
 constexpr int PS_THREADS = 256;
 constexpr int PS_PER_THREAD = 4;
 constexpr int PS_BLOCK = PS_THREADS * PS_PER_THREAD;  // strings per workgroup
+#ifndef KCC_PC_PER_THREAD
+#define KCC_PC_PER_THREAD 4  // 8 measured equal or slower (86 VGPRs)
+#endif
+constexpr int PC_PER_THREAD = KCC_PC_PER_THREAD;      // parse_cpu_kernel: strings per lane
+constexpr int PC_BLOCK = PS_THREADS * PC_PER_THREAD;
 constexpr int PS_LDS_WORDS = 6144;                    // 24 KiB of staged characters
 
 __device__ __forceinline__ bool go_space(uint32_t c) {
@@ -336,35 +341,35 @@ __device__ __forceinline__ bool swar8(uint64_t c, uint64_t& v) {
 // canonical cpu quantities up to 99999999m / 99999999 cores) come from one aligned
 // 12-byte load per lane — neighbouring lanes read neighbouring bytes, so a wave's loads
 // coalesce into the few cache lines its strings span — and are parsed in registers
-// (swar8); anything else takes the byte loop over global memory.  PS_PER_THREAD strings
+// (swar8); anything else takes the byte loop over global memory.  PC_PER_THREAD strings
 // per lane, strided by the workgroup size, all loads issued before the first parse.
 __global__ __launch_bounds__(PS_THREADS) void parse_cpu_kernel(int64_t n, const uint8_t* __restrict__ bytes,
                                                                int64_t n_bytes,
                                                                const int64_t* __restrict__ off,
                                                                int64_t* __restrict__ out,
                                                                int8_t* __restrict__ status) {
-  const int64_t b0 = (int64_t)blockIdx.x * PS_BLOCK;
+  const int64_t b0 = (int64_t)blockIdx.x * PC_BLOCK;
   const int64_t base = b0 + threadIdx.x;
   // the workgroup's character span, for one range-checked buffer descriptor: loads past
   // it (or past n_bytes) read 0 instead of faulting, so every load is unconditional
-  const int64_t cnt = min((int64_t)PS_BLOCK, n - b0);
+  const int64_t cnt = min((int64_t)PC_BLOCK, n - b0);
   const int64_t lo_b = max(off[b0], (int64_t)0) & ~(int64_t)3;
   const int64_t hi_b = min(off[b0 + cnt], n_bytes);
   const bool span_ok = hi_b > lo_b && hi_b - lo_b < ((int64_t)1 << 31);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(bytes + (span_ok ? lo_b : 0)), (short)0, span_ok ? (int)(hi_b - lo_b) : 0,
       0x00020000);
-  int64_t sb[PS_PER_THREAD], se[PS_PER_THREAD];
-  uint32_t w[PS_PER_THREAD][3];
-  bool fast[PS_PER_THREAD];
+  int64_t sb[PC_PER_THREAD], se[PC_PER_THREAD];
+  uint32_t w[PC_PER_THREAD][3];
+  bool fast[PC_PER_THREAD];
 #pragma unroll
-  for (int r = 0; r < PS_PER_THREAD; ++r) {
+  for (int r = 0; r < PC_PER_THREAD; ++r) {
     const int64_t i = min(base + r * PS_THREADS, n - 1);
     sb[r] = off[i];
     se[r] = off[i + 1];
   }
 #pragma unroll
-  for (int r = 0; r < PS_PER_THREAD; ++r) {
+  for (int r = 0; r < PC_PER_THREAD; ++r) {
     const int64_t a = sb[r] & ~(int64_t)3;
     const int64_t L = se[r] - sb[r];
     fast[r] = span_ok && sb[r] >= lo_b && L >= 1 && L <= 9 && a + 12 <= hi_b;
@@ -376,7 +381,7 @@ __global__ __launch_bounds__(PS_THREADS) void parse_cpu_kernel(int64_t n, const 
     w[r][2] = x.z;
   }
 #pragma unroll
-  for (int r = 0; r < PS_PER_THREAD; ++r) {
+  for (int r = 0; r < PC_PER_THREAD; ++r) {
     const int64_t i = base + r * PS_THREADS;
     if (i >= n) break;
     int64_t v = 0;
@@ -416,6 +421,7 @@ __global__ __launch_bounds__(PS_THREADS) void parse_cpu_kernel(int64_t n, const 
 }  // namespace
 
 int64_t parse_grid(int64_t n) { return (n + PS_BLOCK - 1) / PS_BLOCK; }
+static int64_t parse_cpu_grid(int64_t n) { return (n + PC_BLOCK - 1) / PC_BLOCK; }
 
 hipError_t launch_parse(int mode, int64_t n, const uint8_t* bytes, int64_t n_bytes,
                         const int64_t* offsets, int64_t* out, int8_t* status, hipStream_t s) {
@@ -423,8 +429,8 @@ hipError_t launch_parse(int mode, int64_t n, const uint8_t* bytes, int64_t n_byt
   const int64_t grid = parse_grid(n);
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   if (mode == PARSE_MODE_CPU_MILLIS)
-    hipLaunchKernelGGL(parse_cpu_kernel, dim3((unsigned)grid), dim3(PS_THREADS), 0, s, n, bytes,
-                       n_bytes, offsets, out, status);
+    hipLaunchKernelGGL(parse_cpu_kernel, dim3((unsigned)parse_cpu_grid(n)), dim3(PS_THREADS), 0, s,
+                       n, bytes, n_bytes, offsets, out, status);
   else
     hipLaunchKernelGGL(parse_kernel<PARSE_MODE_BYTES>, dim3((unsigned)grid), dim3(PS_THREADS), 0, s,
                        n, bytes, n_bytes, offsets, out, status);
