@@ -191,12 +191,16 @@ int main(int argc, char** argv) {
                              in.cpu_lim.data(), in.mem_lim.data(), uc.data(), um.data(), lc.data(),
                              lm.data());
     if (rc) return fail(ctx, rc);
+    // every row's "Max replicas" (CC:137) for the first spec in one device call
+    std::vector<int64_t> qs(n);
+    std::vector<int32_t> es(n);
+    rc = kcc_fit_rows(ctx, n, in.alloc_cpu.data(), in.alloc_mem.data(), in.alloc_pods.data(),
+                      in.pod_count.data(), uc.data(), um.data(), specs[0].cpu, specs[0].mem,
+                      qs.data(), es.data());
+    if (rc) return fail(ctx, rc);
     for (int64_t i = 0; i < n; ++i) {
-      int64_t q = 0;
-      int32_t e = 0;
-      rc = kcc_fit(ctx, 1, &in.alloc_cpu[i], &in.alloc_mem[i], &in.alloc_pods[i],
-                   &in.pod_count[i], &uc[i], &um[i], 1, &specs[0].cpu, &specs[0].mem, &q, &e);
-      if (rc) return fail(ctx, rc);
+      const int64_t q = qs[i];
+      const int32_t e = es[i];
       std::printf("\n{%s %" PRIu64 " %" PRId64 " %" PRId64 "} - Current non-terminated pods : %" PRId64,
                   rows[i].name.c_str(), rows[i].allocatableCPU, rows[i].allocatableMemory,
                   rows[i].allocatablePods, in.pod_count[i]);

@@ -260,6 +260,17 @@ int kcc_count_by_key(kcc_ctx* ctx, int64_t n_keys, int64_t n, const int32_t* key
 int kcc_count_by_key_async(kcc_ctx* ctx, int64_t n_keys, int64_t n, const int32_t* d_key,
                            int64_t* d_count, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Per-row "Max replicas" of one spec (the verbose report's
+ * CC:137 line for every node row, CC:119-136): q[i] = row i's contribution to the total,
+ * row_err[i] = 1 where Go would panic with an integer divide by zero at that row (q[i]
+ * is then 0; the reference stops at the first such row).
+ * ------------------------------------------------------------------------- */
+int kcc_fit_rows(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* alloc_cpu,
+                 const int64_t* alloc_mem, const int64_t* alloc_pods, const int64_t* pod_count,
+                 const uint64_t* used_cpu, const int64_t* used_mem, uint64_t spec_cpu,
+                 int64_t spec_mem, int64_t* q, int32_t* row_err);
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,6 +57,7 @@ SIGNATURES = {
     "kcc_reduce_requests_keyed_async": (_int, [_vp, _i64, _i64] + [_vp] * 10),
     "kcc_count_by_key": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "kcc_count_by_key_async": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
+    "kcc_fit_rows": (_int, [_vp, _i64] + [_vp] * 6 + [C.c_uint64, _i64, _vp, _vp]),
 }
 
 # per-string status of kcc_parse_* (include/kcc.h)

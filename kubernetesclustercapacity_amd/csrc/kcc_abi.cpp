@@ -1147,3 +1147,41 @@ int kcc_count_by_key(kcc_ctx* ctx, int64_t n_keys, int64_t n, const int32_t* key
 }
 
 }  // extern "C"
+
+
+// ---- per-row q of one spec -----------------------------------------
+
+extern "C" int kcc_fit_rows(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* alloc_cpu,
+                            const int64_t* alloc_mem, const int64_t* alloc_pods,
+                            const int64_t* pod_count, const uint64_t* used_cpu,
+                            const int64_t* used_mem, uint64_t spec_cpu, int64_t spec_mem,
+                            int64_t* q, int32_t* row_err) {
+  if (!ctx) return KCC_EINVAL;
+  if (n_nodes < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (n_nodes == 0) return KCC_OK;
+  if (!alloc_cpu || !alloc_mem || !alloc_pods || !pod_count || !used_cpu || !used_mem || !q ||
+      !row_err)
+    return fail(ctx, KCC_EINVAL, "NULL node array / output");
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  int rc;
+  if ((rc = h2d(ctx, dv, dv.alloc_cpu, alloc_cpu, n_nodes))) return rc;
+  if ((rc = h2d(ctx, dv, dv.alloc_mem, alloc_mem, n_nodes))) return rc;
+  if ((rc = h2d(ctx, dv, dv.alloc_pods, alloc_pods, n_nodes))) return rc;
+  if ((rc = h2d(ctx, dv, dv.pod_count, pod_count, n_nodes))) return rc;
+  if ((rc = h2d(ctx, dv, dv.used_cpu, used_cpu, n_nodes))) return rc;
+  if ((rc = h2d(ctx, dv, dv.used_mem, used_mem, n_nodes))) return rc;
+  KCC_HIP(ctx, ensure(dv.totals, 8 * (size_t)n_nodes));
+  KCC_HIP(ctx, ensure(dv.err, 4 * (size_t)n_nodes));
+  KCC_HIP(ctx, kcc::launch_fit_rows(n_nodes, as<uint64_t>(dv.alloc_cpu), as<int64_t>(dv.alloc_mem),
+                                    as<int64_t>(dv.alloc_pods), as<int64_t>(dv.pod_count),
+                                    as<uint64_t>(dv.used_cpu), as<int64_t>(dv.used_mem), spec_cpu,
+                                    spec_mem, as<int64_t>(dv.totals), as<int32_t>(dv.err),
+                                    dv.stream));
+  KCC_HIP(ctx, hipMemcpyAsync(q, dv.totals.p, 8 * (size_t)n_nodes, hipMemcpyDeviceToHost,
+                              dv.stream));
+  KCC_HIP(ctx, hipMemcpyAsync(row_err, dv.err.p, 4 * (size_t)n_nodes, hipMemcpyDeviceToHost,
+                              dv.stream));
+  KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
+  return KCC_OK;
+}

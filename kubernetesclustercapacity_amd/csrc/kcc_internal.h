@@ -268,4 +268,10 @@ hipError_t launch_reduce_keyed(int64_t n_keys, int64_t n, const int32_t* key, co
 hipError_t launch_count_keyed(int64_t n_keys, int64_t n, const int32_t* key, int64_t* count,
                               const KeyedWork* kw, hipStream_t s);
 
+// ---- per-row q of one spec (kcc_rows.hip) -------------------------
+hipError_t launch_fit_rows(int64_t n, const uint64_t* alloc_cpu, const int64_t* alloc_mem,
+                           const int64_t* alloc_pods, const int64_t* pod_count,
+                           const uint64_t* used_cpu, const int64_t* used_mem, uint64_t spec_cpu,
+                           int64_t spec_mem, int64_t* q, int32_t* err, hipStream_t s);
+
 }  // namespace kcc

@@ -223,6 +223,22 @@ class CapacityEngine:
         domain — see include/kcc.h)."""
         return self._parse(self._lib.kcc_parse_bytes, strings, np.int64)
 
+    def max_replicas_per_row(self, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu,
+                             used_mem, spec_cpu: int, spec_mem: int):
+        """CC:119-137 per node row for one spec ("Max replicas" of the verbose report).
+        Returns (q int64[N], row_err int32[N]: 1 where Go would panic at that row)."""
+        a = [_arr(alloc_cpu, np.uint64), _arr(alloc_mem, np.int64), _arr(alloc_pods, np.int64),
+             _arr(pod_count, np.int64), _arr(used_cpu, np.uint64), _arr(used_mem, np.int64)]
+        n = a[0].size
+        if any(x.size != n for x in a):
+            raise ValueError("node arrays differ in length")
+        q = np.zeros(n, np.int64)
+        err = np.zeros(n, np.int32)
+        self._check(self._lib.kcc_fit_rows(self._h, n, *[_p(x) for x in a],
+                                           int(spec_cpu) % (1 << 64), int(spec_mem), _p(q),
+                                           _p(err)))
+        return q, err
+
     def last_slow_fraction(self) -> float:
         return float(self._lib.kcc_last_slow_fraction(self._h))
 
