@@ -252,7 +252,8 @@ struct KeyedWork {
   uint32_t* counts;  // [keyed_tiles(n) * keyed_buckets(n_keys)]
   uint32_t* tot;     // [keyed_buckets(n_keys)]
   uint16_t* sk;      // [n] scattered rows within the bucket
-  uint64_t* sv;      // [NA * n] scattered values (NA = 2 requests, 4 with limits, 0 counts)
+  uint64_t* sv;      // [n][NA] scattered values, element-major (NA = 2 requests, 4 with
+                     // limits, 0 counts): one 16-B (32-B) store per element
 };
 int64_t keyed_tiles(int64_t n);
 int64_t keyed_buckets(int64_t n_keys);

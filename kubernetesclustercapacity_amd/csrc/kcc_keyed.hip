@@ -296,7 +296,7 @@ __global__ __launch_bounds__(KB_HIST_THREADS) void kb_scatter(
       const uint32_t pos = st_pos[j];
       sk[pos] = st_k[j];
 #pragma unroll
-      for (int a = 0; a < NA; ++a) sv[(int64_t)a * n + pos] = st_v[a][j];
+      for (int a = 0; a < NA; ++a) sv[(int64_t)pos * NA + a] = st_v[a][j];  // element-major
     }
     __syncthreads();  // nvalid read, stage drained before the counters change
     for (int b = b0; b < b1; ++b) {  // advance the cursors, clear the sub-chunk counts
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(KB_ACC_THREADS) void kb_accum(
       r[u] = ok ? (uint32_t)__builtin_nontemporal_load(sk + i) : 0xffffffffu;
 #pragma unroll
       for (int a = 0; a < NACC; ++a)
-        v[a][u] = NA == 0 ? 1ull : (ok ? __builtin_nontemporal_load(sv + (int64_t)a * n + i) : 0ull);
+        v[a][u] = NA == 0 ? 1ull : (ok ? __builtin_nontemporal_load(sv + i * NA + a) : 0ull);
     }
 #pragma unroll
     for (int u = 0; u < KB_UNROLL; ++u)
