@@ -110,6 +110,22 @@ def test_gpu_keyed_atomic_fallback(eng):
 
 
 @pytest.mark.gpu
+def test_gpu_keyed_max_buckets_with_limits(eng):
+    """The largest bucketed key space (4096 buckets x 4096 rows) with limits: the scatter's
+    LDS (cursors for 4096 buckets + the 4-value stage) at its maximum."""
+    nk = 4096 * 4096
+    rng = np.random.default_rng(8)
+    key = rng.integers(0, nk, 300_000).astype(np.int32)
+    key[:4] = [nk - 1, nk - 1, 0, 4095]
+    v = rng.integers(0, 1 << 62, (4, key.size)).astype(np.uint64)
+    r = eng.get_pod_cpu_memory_requests_limits_keyed(nk, key, v[0], v[1].astype(np.int64),
+                                                      v[2], v[3].astype(np.int64))
+    o = oracle_keyed(nk, key, v[0], v[1].astype(np.int64), v[2], v[3].astype(np.int64))
+    for got, want in zip((r.cpu_requests, r.memory_requests, r.cpu_limits, r.memory_limits), o):
+        assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
 def test_gpu_count_by_key(eng):
     rng = np.random.default_rng(4)
     key = rng.integers(-3, 1003, 100_003).astype(np.int32)
