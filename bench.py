@@ -337,7 +337,7 @@ def parse_leg(eng, cl, dev, stream, steps, warmup, with_cpu):
     gbs = alg / (ms * 1e-3) / 1e9
     res = {
         "op": "convertCPUToMilis (CC:301-319) over every container's cpu request string",
-        "kernel": "parse_kernel<0>", "strings": n, "chars": nbytes,
+        "kernel": "parse_cpu_kernel", "strings": n, "chars": nbytes,
         "ms_per_launch": ms, "strings_per_s": n / (ms * 1e-3),
         "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": alg,
