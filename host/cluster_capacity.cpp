@@ -175,10 +175,12 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "panic: %s\n", err.c_str());
     return 2;
   }
-  const std::vector<node> rows = getHealthyNodes(cl);
   kcc_ctx* ctx = nullptr;
   int rc = kcc_create(&ctx, std::atoi(f.v["device"].c_str()), std::atoi(f.v["gpus"].c_str()));
   if (rc) return fail(nullptr, rc);
+  std::vector<node> rows;
+  rc = getHealthyNodes(ctx, cl, rows);  // node cpu / memory strings parsed on the device
+  if (rc) return fail(ctx, rc);
   EngineInputs in;
   rc = buildInputs(ctx, cl, rows, in);  // container cpu strings parsed on the device
   if (rc) return fail(ctx, rc);

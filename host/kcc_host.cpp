@@ -140,15 +140,57 @@ bool loadCluster(const std::string& path, Cluster& out, std::string& err) {
   return true;
 }
 
-std::vector<node> getHealthyNodes(const Cluster& c, bool print) {
+namespace {
+// One packed batch (Arrow layout, 4-byte padded) of strings for kcc_parse_*.
+void pack(const std::vector<const std::string*>& strs, std::string& chars,
+          std::vector<int64_t>& off) {
+  chars.clear();
+  off.assign(1, 0);
+  for (const std::string* s : strs) {
+    chars += *s;
+    off.push_back((int64_t)chars.size());
+  }
+  chars.resize((chars.size() + 4) & ~(size_t)3, '\0');
+}
+}  // namespace
+
+int getHealthyNodes(kcc_ctx* ctx, const Cluster& c, std::vector<node>& healthy, bool print) {
   const size_t noOfNodes = c.nodes.size();
   if (print) std::printf("\nThere are total %zu nodes in the cluster\n\n", noOfNodes);
-  std::vector<node> healthy(noOfNodes);  // zero rows stay for unhealthy nodes (CC:221-226)
+  healthy.assign(noOfNodes, node{});  // zero rows stay for unhealthy nodes (CC:221-226)
+  // both conversions of every node in one device batch each (CC:196-197, CC:202-206);
+  // the prints below keep the reference's per-node order
+  std::vector<uint64_t> cpu(noOfNodes);
+  std::vector<int64_t> mem(noOfNodes);
+  std::vector<int8_t> cst(noOfNodes), mst(noOfNodes);
+  if (noOfNodes > 0) {
+    std::vector<const std::string*> cs, ms;
+    for (const NodeObj& n : c.nodes) {
+      cs.push_back(&n.cpu);
+      ms.push_back(&n.memory);
+    }
+    std::string chars;
+    std::vector<int64_t> off;
+    pack(cs, chars, off);
+    int rc = kcc_parse_cpu_millis(ctx, (int64_t)noOfNodes, chars.data(), off.back(), off.data(),
+                                  cpu.data(), cst.data());
+    if (rc) return rc;
+    pack(ms, chars, off);
+    rc = kcc_parse_bytes(ctx, (int64_t)noOfNodes, chars.data(), off.back(), off.data(), mem.data(),
+                         mst.data());
+    if (rc) return rc;
+  }
   for (size_t i = 0; i < noOfNodes; ++i) {
     const NodeObj& n = c.nodes[i];
-    const uint64_t cpu = convertCPUToMilis(n.cpu, nullptr, print);  // CC:196-197
-    auto mem = ToBytes(n.memory);                                    // CC:202-206
-    const int64_t memAlloc = mem.second ? mem.first : 0;
+    if (cst[i] != KCC_PARSE_OK && print) {  // CC:315-316, the string without its 'm'
+      std::string s = n.cpu;
+      if (!s.empty() && s.back() == 'm') s.pop_back();
+      std::printf("\nError converting string to int for %s\n", s.c_str());
+    }
+    const int64_t memAlloc = mst[i] == KCC_PARSE_OK ? mem[i] : 0;  // CC:203-206
+    if (mst[i] == KCC_PARSE_UNSUPPORTED)  // a float64-edge literal Quantity never prints
+      std::fprintf(stderr, "node %s: memory %s is outside the device parser's exact domain; "
+                   "using 0\n", n.name.c_str(), n.memory.c_str());
     bool flagHealthy = true;
     for (int j = 0; j < 4; ++j) {  // CC:212-219
       if (n.conditions[j] != "False") {
@@ -159,12 +201,12 @@ std::vector<node> getHealthyNodes(const Cluster& c, bool print) {
     }
     if (flagHealthy) {
       healthy[i].name = n.name;
-      healthy[i].allocatableCPU = cpu;
+      healthy[i].allocatableCPU = cpu[i];
       healthy[i].allocatableMemory = memAlloc;
       healthy[i].allocatablePods = n.pods;
     }
   }
-  return healthy;
+  return KCC_OK;
 }
 
 std::map<std::string, std::vector<size_t>> nonTerminatedPodsByNode(const Cluster& c) {

@@ -68,7 +68,10 @@ bool loadCluster(const std::string& path, Cluster& out, std::string& err);
 
 // CC:166-230 — rows in node order; an unhealthy node keeps a zero row (CC:221-226).
 // (The reference's make([]node, n, 3) panics for n > 3, CC:176: not reproduced.)
-std::vector<node> getHealthyNodes(const Cluster& c, bool print = true);
+// The nodes' cpu and memory strings are converted on the device (kcc_parse_cpu_millis,
+// kcc_parse_bytes on `ctx`, one batch each).  Returns a KCC_E* code (0 on success).
+int getHealthyNodes(kcc_ctx* ctx, const Cluster& c, std::vector<node>& healthy,
+                    bool print = true);
 
 // CC:232-253 — indices of the pods on `nodeName` whose phase is not Pending,
 // Succeeded, Failed or Unknown.

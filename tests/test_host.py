@@ -239,3 +239,22 @@ def test_cli_verbose_rows_go_format(cli, tmp_path):
     assert "{ 0 0 0} - Current non-terminated pods : 1" in out
     assert "used percentage till now : NaN +Inf NaN NaN" in out
     assert "Max replicas : -1" in out  # findMin(0, 0) >= 0 pods -> 0 - 1
+
+
+@pytest.mark.gpu
+def test_cli_node_strings_on_device_keep_print_order(cli, tmp_path):
+    """Node cpu / memory strings go through kcc_parse_* in one batch each; the reference's
+    per-node prints (CC:196-219: cpu conversion errors, "Skipping node") keep their order,
+    and a "16Gi" allocatable memory (ToBytes rejects GI) is 0."""
+    path = tmp_path / "c.txt"
+    path.write_text("node n0 2k 16331524Ki 110 False False False False\n"
+                    "node n1 4 16331524Ki 110 True False False False\n"
+                    "node n2 500m 16Gi 110 False False False False\n"
+                    "node n3 0.5 1Mi 110 False False False True\n")
+    r = _run(["-cluster", str(path), "-cpuRequests=100m", "-memRequests=100mb", "-v"])
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines()
+             if ln.startswith("Error converting") or ln.startswith("Skipping node")]
+    assert lines == ["Error converting string to int for 2k", "Skipping node n1 as it is not healthy",
+                     "Error converting string to int for 0.5", "Skipping node n3 as it is not healthy"]
+    assert "{n0 0 16723480576 110}" in r.stdout and "{n2 500 0 110}" in r.stdout
