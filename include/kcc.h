@@ -230,6 +230,18 @@ int kcc_parse_cpu_millis(kcc_ctx* ctx, int64_t n, const char* bytes, int64_t n_b
                          const int64_t* offsets, uint64_t* out, int8_t* status);
 int kcc_parse_bytes(kcc_ctx* ctx, int64_t n, const char* bytes, int64_t n_bytes,
                     const int64_t* offsets, int64_t* out, int8_t* status);
+/* resource.Quantity.Value() of ParseQuantity(s) (CC:285-286, the containers' memory
+ * requests): [+-] digits [. digits] + "", Ki..Ei, n u m k M G T P E or e<int> suffix;
+ * magnitude capped at 2^63 - 1 and rounded up away from zero.  Restated from
+ * k8s.io/apimachinery's published algorithm, which is not vendored in the reference
+ * (version unpinned): parity unpinned.  KCC_PARSE_ERR for strings
+ * ParseQuantity rejects; KCC_PARSE_UNSUPPORTED for binary-suffixed fractions with more
+ * than 19 significant digits. */
+int kcc_parse_quantity(kcc_ctx* ctx, int64_t n, const char* bytes, int64_t n_bytes,
+                       const int64_t* offsets, int64_t* out, int8_t* status);
+int kcc_parse_quantity_async(kcc_ctx* ctx, int64_t n, const char* d_bytes, int64_t n_bytes,
+                             const int64_t* d_offsets, int64_t* d_out, int8_t* d_status,
+                             void* stream);
 int kcc_parse_cpu_millis_async(kcc_ctx* ctx, int64_t n, const char* d_bytes, int64_t n_bytes,
                                const int64_t* d_offsets, uint64_t* d_out, int8_t* d_status,
                                void* stream);

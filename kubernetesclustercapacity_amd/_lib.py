@@ -51,6 +51,8 @@ SIGNATURES = {
     "kcc_fit_slow_pairs": (_int, [_vp, C.POINTER(_i64), C.POINTER(_i64)]),
     "kcc_parse_cpu_millis": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp]),
     "kcc_parse_bytes": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp]),
+    "kcc_parse_quantity": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp]),
+    "kcc_parse_quantity_async": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp]),
     "kcc_parse_cpu_millis_async": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp]),
     "kcc_parse_bytes_async": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp]),
     "kcc_reduce_requests_keyed": (_int, [_vp, _i64, _i64] + [_vp] * 9),

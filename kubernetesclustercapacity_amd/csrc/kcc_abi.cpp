@@ -972,6 +972,21 @@ int kcc_parse_bytes(kcc_ctx* ctx, int64_t n, const char* bytes, int64_t n_bytes,
   return parse_host(ctx, kcc::PARSE_MODE_BYTES, n, bytes, n_bytes, offsets, out, status);
 }
 
+int kcc_parse_quantity(kcc_ctx* ctx, int64_t n, const char* bytes, int64_t n_bytes,
+                       const int64_t* offsets, int64_t* out, int8_t* status) {
+  return parse_host(ctx, kcc::PARSE_MODE_QUANTITY, n, bytes, n_bytes, offsets, out, status);
+}
+
+int kcc_parse_quantity_async(kcc_ctx* ctx, int64_t n, const char* d_bytes, int64_t n_bytes,
+                             const int64_t* d_offsets, int64_t* d_out, int8_t* d_status,
+                             void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  return parse_async_dev(ctx, kcc::PARSE_MODE_QUANTITY, n, d_bytes, n_bytes, d_offsets, d_out,
+                         d_status, static_cast<hipStream_t>(stream));
+}
+
 int kcc_parse_cpu_millis_async(kcc_ctx* ctx, int64_t n, const char* d_bytes, int64_t n_bytes,
                                const int64_t* d_offsets, uint64_t* d_out, int8_t* d_status,
                                void* stream) {

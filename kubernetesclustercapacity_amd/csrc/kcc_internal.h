@@ -229,7 +229,7 @@ hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial,
                                hipStream_t s);
 
 // ---- quantity-string parse (kcc_parse.hip) ------------------------
-enum ParseMode : int { PARSE_MODE_CPU_MILLIS = 0, PARSE_MODE_BYTES = 1 };
+enum ParseMode : int { PARSE_MODE_CPU_MILLIS = 0, PARSE_MODE_BYTES = 1, PARSE_MODE_QUANTITY = 2 };
 // per-string status (include/kcc.h KCC_PARSE_*)
 enum ParseStatus : int8_t {
   PARSE_OK = 1,           // value as the reference computes it

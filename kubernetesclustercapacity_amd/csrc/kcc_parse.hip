@@ -266,12 +266,179 @@ __device__ __forceinline__ int64_t bytes_value(P s, int n, int8_t& st) {
   return f2i_amd64(ldexp(x, shift));  // times a power of two: exact
 }
 
+// resource.Quantity.Value() of ParseQuantity(s) (k8s.io/apimachinery resource/quantity.go;
+// the reference's per-container memory, CC:285-286).  Restated from the published
+// algorithm — apimachinery is not vendored and its version is unpinned (DESIGN.md §4.6:
+// parity unpinned): [+-] digits [. digits] then a suffix — "", Ki..Ei (2^10k), n u m k M
+// G T P E (10^3k), or e/E<int64> (10^int32(exp)); parse errors (ErrFormatWrong /
+// ErrSuffix) -> PARSE_ERR.  The amount is capped at 2^63 - 1 in magnitude and Value()
+// rounds up away from zero: v = sign * min(ceil(|x|), 2^63 - 1).  Binary suffixes with a
+// fraction are exact for <= 19 significant digits (else PARSE_UNSUPPORTED).
+__device__ __forceinline__ bool mul10_sat(uint64_t& v, uint32_t d) {  // v = v*10 + d, false on > 2^63-1
+  const uint64_t lim = 0x7fffffffffffffffull;
+  if (v > (lim - d) / 10u) return false;
+  v = v * 10u + d;
+  return true;
+}
+
+template <class P>
+__device__ __forceinline__ int64_t quantity_value(P s, int n, int8_t& st) {
+  const uint64_t MAXV = 0x7fffffffffffffffull;
+  st = PARSE_ERR;
+  if (n == 0) return 0;  // ErrFormatWrong
+  int i = 0;
+  bool neg = false;
+  if ((uint32_t)s[0] == '-' || (uint32_t)s[0] == '+') {
+    neg = (uint32_t)s[0] == '-';
+    i = 1;
+  }
+  while (i < n && (uint32_t)s[i] == '0') ++i;  // leading zeros
+  if (i >= n) {  // all zeros (or a bare sign): 0
+    st = PARSE_OK;
+    return 0;
+  }
+  const int num0 = i;
+  while (i < n && (uint32_t)s[i] - '0' <= 9u) ++i;
+  const int num1 = i;  // numerator digits [num0, num1)
+  int den0 = i, den1 = i;
+  if (i < n && (uint32_t)s[i] == '.') {
+    ++i;
+    den0 = i;
+    while (i < n && (uint32_t)s[i] - '0' <= 9u) ++i;
+    den1 = i;
+  }
+  // suffix: letters of "eEinumkKMGTP", then an optional sign, then digits, to the end
+  const int suf0 = i;
+  auto suffix_letter = [](uint32_t c) {
+    return c == 'e' || c == 'E' || c == 'i' || c == 'n' || c == 'u' || c == 'm' || c == 'k' ||
+           c == 'K' || c == 'M' || c == 'G' || c == 'T' || c == 'P';
+  };
+  while (i < n && suffix_letter((uint32_t)s[i])) ++i;
+  if (i < n && ((uint32_t)s[i] == '+' || (uint32_t)s[i] == '-')) ++i;
+  while (i < n && (uint32_t)s[i] - '0' <= 9u) ++i;
+  if (i < n) return 0;  // ErrFormatWrong
+  // interpret the suffix
+  const int sl = n - suf0;
+  const uint32_t a0 = sl > 0 ? (uint32_t)s[suf0] : 0u, a1 = sl > 1 ? (uint32_t)s[suf0 + 1] : 0u;
+  bool binary = false;
+  int64_t e10 = 0;
+  int bexp = 0;
+  if (sl == 0) {
+  } else if (sl == 2 && a1 == 'i' &&
+             (a0 == 'K' || a0 == 'M' || a0 == 'G' || a0 == 'T' || a0 == 'P' || a0 == 'E')) {
+    binary = true;
+    bexp = a0 == 'K' ? 10 : a0 == 'M' ? 20 : a0 == 'G' ? 30 : a0 == 'T' ? 40 : a0 == 'P' ? 50 : 60;
+  } else if (sl == 1 && (a0 == 'n' || a0 == 'u' || a0 == 'm' || a0 == 'k' || a0 == 'M' ||
+                         a0 == 'G' || a0 == 'T' || a0 == 'P' || a0 == 'E')) {
+    e10 = a0 == 'n' ? -9 : a0 == 'u' ? -6 : a0 == 'm' ? -3 : a0 == 'k' ? 3 : a0 == 'M' ? 6
+        : a0 == 'G' ? 9 : a0 == 'T' ? 12 : a0 == 'P' ? 15 : 18;
+  } else if (sl > 1 && (a0 == 'e' || a0 == 'E')) {  // strconv.ParseInt(suffix[1:], 10, 64)
+    int64_t x;
+    if (!go_atoi(s + suf0 + 1, sl - 1, x)) return 0;  // ErrSuffix
+    e10 = (int64_t)(int32_t)(uint32_t)(uint64_t)x;     // int32(parsed)
+  } else {
+    return 0;  // ErrSuffix
+  }
+  const int nd = (num1 - num0) + (den1 - den0);  // significant-or-not digits after the zeros
+  uint64_t I = 0;
+  bool over = false, frac = false;
+  if (!binary) {
+    // x = digits x 10^(e10 - |denom|): the first (|num| + e10) digits are the integer part
+    const int64_t intlen = (int64_t)(num1 - num0) + e10;
+    int64_t k = 0;
+    for (int j = num0; j < den1; ++j) {
+      if (j == num1) continue;  // the point
+      const uint32_t d = (uint32_t)s[j] - '0';
+      if (k < intlen) {
+        if (!over && !mul10_sat(I, d)) over = true;
+      } else {
+        frac |= d != 0;
+      }
+      ++k;
+    }
+    if (!over && intlen > nd && I != 0) {  // the exponent's trailing zeros (0 stays 0)
+      if (intlen - nd > 19) {
+        over = true;
+      } else {
+        for (int64_t t = nd; t < intlen; ++t)
+          if (!mul10_sat(I, 0)) {
+            over = true;
+            break;
+          }
+      }
+    }
+  } else {
+    // x = D x 2^bexp / 10^f exactly, D the digits (<= 19 significant)
+    uint64_t D = 0;
+    int sig = 0, f = den1 - den0;
+    bool trunc = false;
+    for (int j = num0; j < den1; ++j) {
+      if (j == num1) continue;
+      const uint32_t d = (uint32_t)s[j] - '0';
+      if (sig == 0 && d == 0) continue;
+      if (sig < 19) {
+        D = D * 10u + d;
+        ++sig;
+      } else {
+        trunc |= d != 0;
+        if (j < num1) {  // an integer digit beyond 19: the value is >= 10^19 > cap
+          over = true;
+        } else {
+          --f;  // fractional zero digits past the 19th are dropped exactly
+        }
+      }
+    }
+    if (trunc && !over) {
+      st = PARSE_UNSUPPORTED;
+      return 0;
+    }
+    // (f counts fraction digits kept in D: f - (dropped zeros))
+    if (!over) {
+      unsigned __int128 N = (unsigned __int128)D << bexp;  // < 2^124
+      unsigned __int128 Q = N;
+      if (f > 0) {
+        if (f > 38) {
+          st = PARSE_UNSUPPORTED;
+          return 0;
+        }
+        unsigned __int128 V = 1;
+        for (int t = 0; t < f; ++t) V *= 10u;
+        // restoring division N / V
+        unsigned __int128 R = 0;
+        Q = 0;
+        for (int b = 127; b >= 0; --b) {
+          R = (R << 1) | (unsigned __int128)((N >> b) & 1u);
+          Q <<= 1;
+          if (R >= V) {
+            R -= V;
+            Q |= 1u;
+          }
+        }
+        frac = R != 0;
+      }
+      if (Q > (unsigned __int128)MAXV) over = true;
+      else I = (uint64_t)Q;
+    }
+  }
+  uint64_t mag;
+  if (over) {
+    mag = MAXV;  // capped at maxAllowed
+  } else {
+    mag = I + (frac ? 1u : 0u);  // rounded up away from zero
+    if (mag > MAXV) mag = MAXV;
+  }
+  st = PARSE_OK;
+  return neg ? -(int64_t)mag : (int64_t)mag;
+}
+
 template <int MODE, class P>
 __device__ __forceinline__ void parse_one(P s, int n, int64_t& v, int8_t& st) {
   if (MODE == PARSE_MODE_CPU_MILLIS)
     v = (int64_t)cpu_millis_value(s, n, st);
-  else
+  else if (MODE == PARSE_MODE_BYTES)
     v = bytes_value(s, n, st);
+  else
+    v = quantity_value(s, n, st);
 }
 
 template <int MODE>
@@ -431,9 +598,12 @@ hipError_t launch_parse(int mode, int64_t n, const uint8_t* bytes, int64_t n_byt
   if (mode == PARSE_MODE_CPU_MILLIS)
     hipLaunchKernelGGL(parse_cpu_kernel, dim3((unsigned)parse_cpu_grid(n)), dim3(PS_THREADS), 0, s,
                        n, bytes, n_bytes, offsets, out, status);
-  else
+  else if (mode == PARSE_MODE_BYTES)
     hipLaunchKernelGGL(parse_kernel<PARSE_MODE_BYTES>, dim3((unsigned)grid), dim3(PS_THREADS), 0, s,
                        n, bytes, n_bytes, offsets, out, status);
+  else
+    hipLaunchKernelGGL(parse_kernel<PARSE_MODE_QUANTITY>, dim3((unsigned)grid), dim3(PS_THREADS), 0,
+                       s, n, bytes, n_bytes, offsets, out, status);
   return hipGetLastError();
 }
 

@@ -239,6 +239,11 @@ class CapacityEngine:
                                            _p(err)))
         return q, err
 
+    def quantity_value(self, strings):
+        """resource.Quantity.Value() of ParseQuantity (CC:285-286, parity unpinned: see
+        include/kcc.h) over a batch.  Returns (int64 values, int8 status)."""
+        return self._parse(self._lib.kcc_parse_quantity, strings, np.int64)
+
     def last_slow_fraction(self) -> float:
         return float(self._lib.kcc_last_slow_fraction(self._h))
 

@@ -287,3 +287,54 @@ def test_gpu_c4_round_trip():
         v, s = e.to_bytes((mb, mo))
     ov, os_ = coracle.parse_bytes(mb, mo)
     assert np.array_equal(v, ov) and np.array_equal(s, os_)
+
+
+# ---- resource.Quantity.Value() (CC:285-286; parity unpinned) --------------------------
+from tests import quantity_model as qm  # noqa: E402
+
+QTY_KATS = [("128Mi", 134217728), ("1G", 10 ** 9), ("1.5Gi", 1610612736), ("100m", 1),
+            ("0.1Ki", 103), ("-100m", -1), ("1e3", 1000), ("1E3", 1000), ("1E", 10 ** 18),
+            ("0", 0), ("-", 0), ("000", 0), ("9223372036854775807", (1 << 63) - 1),
+            ("9223372036854775808", (1 << 63) - 1), ("1e19", (1 << 63) - 1),
+            ("-1e19", -((1 << 63) - 1)), ("1.G", 10 ** 9), (".5", 1), ("1.5", 2), ("+1", 1),
+            ("1e-3", 1), ("12Ti", 12 << 40), ("0.5E", 5 * 10 ** 17), ("1e4294967296", 1),
+            ("16331524Ki", 16723480576), ("250M", 250_000_000), ("1n", 1), ("2u", 1),
+            ("3Ei", 3 << 60), ("8Ei", (1 << 63) - 1), ("0.0001Ki", 1), ("1.0e+2", 100)]
+QTY_ERRS = ["", "5e", "1ki", "1mi", "1Gib", "abc", "1.2.3", "1 Mi", "1e99999999999999999999",
+            "1e", "--1", "1Mi2", "0x10"]
+
+
+def qty_corpus():
+    rng = np.random.default_rng(17)
+    sufs = ["", "Ki", "Mi", "Gi", "Ti", "Pi", "Ei", "n", "u", "m", "k", "M", "G", "T", "P", "E",
+            "e3", "E-2", "e+5", "e0", "e-12", "e18", "x", "ki", "iB"]
+    out = [k for k, _ in QTY_KATS] + QTY_ERRS
+    for _ in range(6000):
+        ni = int(rng.integers(0, 22))
+        nf = int(rng.integers(0, 25)) if rng.random() < 0.5 else 0
+        ip = "".join(str(int(d)) for d in rng.integers(0, 10, ni))
+        fp = "".join(str(int(d)) for d in rng.integers(0, 10, nf))
+        sgn = rng.choice(["", "", "", "-", "+"])
+        out.append(sgn + ip + ("." + fp if nf else "") + sufs[int(rng.integers(0, len(sufs)))])
+    return out
+
+
+def test_quantity_model_kats():
+    for s, want in QTY_KATS:
+        assert qm.value(s) == (want, qm.OK), s
+    for s in QTY_ERRS:
+        assert qm.value(s)[1] == qm.ERR, s
+
+
+@pytest.mark.gpu
+def test_gpu_quantity_value(eng):
+    strs = qty_corpus()
+    gv, gs = eng.quantity_value(strs)
+    unsupported = 0
+    for s, v, st in zip(strs, gv, gs):
+        if st == -1:  # binary-suffixed fraction beyond 19 significant digits
+            unsupported += 1
+            assert s.endswith("i") and "." in s, s
+            continue
+        assert (int(v), int(st)) == qm.value(s), s
+    assert unsupported < 0.1 * len(strs)  # the corpus is rich in 20+ digit binary fractions
