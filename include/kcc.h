@@ -283,6 +283,47 @@ int kcc_fit_rows(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* alloc_cpu,
                  const uint64_t* used_cpu, const int64_t* used_mem, uint64_t spec_cpu,
                  int64_t spec_mem, int64_t* q, int32_t* row_err);
 
+/* ---------------------------------------------------------------------------
+ * OPT-IN scheduler request model — explicitly NOT the
+ * reference's semantics: the reference sums only the app containers of a node's pods
+ * (CC:276-294, kcc_reduce_requests above; that stays the default).  This gives the
+ * kube-scheduler's effective pod request instead (k8s pkg/api/v1/resource PodRequests,
+ * sidecar-aware form; that dependency is absent here, parity unpinned beyond the
+ * hand-derived cases of tests/test_pods.py), per resource, in the engine's 64-bit
+ * wrapping domain (cpu uint64 with unsigned max, memory int64 with signed max):
+ *   app = sum of the pod's app containers; side = 0; init = identity of max
+ *   for each init container k of the pod, in order:
+ *     restartable[k] (a sidecar): app += r_k; side += r_k; init = max(init, side)
+ *     otherwise:                  init = max(init, r_k + side)
+ *   req(p) = max(app, init) + overhead(p)
+ * pod_ptr[P+1] / init_ptr[P+1]: CSR offsets of each pod's app / init containers.
+ * init_ptr (with init_cpu, init_mem), restartable and the overhead pair are nullable
+ * (absent = no init containers / none restartable / no overhead).
+ * kcc_pod_requests: req(p) per pod.  kcc_reduce_requests_pods: also sums the pods of each
+ * node (node_pod_ptr[N+1], pods grouped by node) into used_cpu / used_mem, the inputs
+ * kcc_fit takes.  The *_async forms take device pointers (offsets must be in range;
+ * the kernel clamps them, so a malformed CSR gives wrong sums, never a fault).
+ * ------------------------------------------------------------------------- */
+int kcc_pod_requests(kcc_ctx* ctx, int64_t n_pods, int64_t n_containers, int64_t n_init,
+                     const int64_t* pod_ptr, const uint64_t* cpu_req, const int64_t* mem_req,
+                     const int64_t* init_ptr, const uint64_t* init_cpu, const int64_t* init_mem,
+                     const uint8_t* restartable, const uint64_t* ovh_cpu,
+                     const int64_t* ovh_mem, uint64_t* pod_cpu, int64_t* pod_mem);
+int kcc_pod_requests_async(kcc_ctx* ctx, int64_t n_pods, int64_t n_containers, int64_t n_init,
+                           const int64_t* d_pod_ptr, const uint64_t* d_cpu_req,
+                           const int64_t* d_mem_req, const int64_t* d_init_ptr,
+                           const uint64_t* d_init_cpu, const int64_t* d_init_mem,
+                           const uint8_t* d_restartable, const uint64_t* d_ovh_cpu,
+                           const int64_t* d_ovh_mem, uint64_t* d_pod_cpu, int64_t* d_pod_mem,
+                           void* stream);
+int kcc_reduce_requests_pods(kcc_ctx* ctx, int64_t n_nodes, int64_t n_pods,
+                             int64_t n_containers, int64_t n_init, const int64_t* node_pod_ptr,
+                             const int64_t* pod_ptr, const uint64_t* cpu_req,
+                             const int64_t* mem_req, const int64_t* init_ptr,
+                             const uint64_t* init_cpu, const int64_t* init_mem,
+                             const uint8_t* restartable, const uint64_t* ovh_cpu,
+                             const int64_t* ovh_mem, uint64_t* used_cpu, int64_t* used_mem);
+
 #ifdef __cplusplus
 }
 #endif

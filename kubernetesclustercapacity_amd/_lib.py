@@ -60,6 +60,9 @@ SIGNATURES = {
     "kcc_count_by_key": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "kcc_count_by_key_async": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "kcc_fit_rows": (_int, [_vp, _i64] + [_vp] * 6 + [C.c_uint64, _i64, _vp, _vp]),
+    "kcc_pod_requests": (_int, [_vp, _i64, _i64, _i64] + [_vp] * 11),
+    "kcc_pod_requests_async": (_int, [_vp, _i64, _i64, _i64] + [_vp] * 12),
+    "kcc_reduce_requests_pods": (_int, [_vp, _i64, _i64, _i64, _i64] + [_vp] * 12),
 }
 
 # per-string status of kcc_parse_* (include/kcc.h)

@@ -75,6 +75,8 @@ struct Dev {
   DevBuf p_bytes, p_off, p_out, p_st;  // kcc_parse_* staging
   DevBuf k_key;                        // kcc_*_keyed staging
   DevBuf kb_counts, kb_tot, kb_sk, kb_sv;  // kcc::KeyedWork (bucketed keyed reduce)
+  // kcc_pod_requests / kcc_reduce_requests_pods staging (app containers in cpu / mem)
+  DevBuf q_ptr, q_iptr, q_icpu, q_imem, q_rst, q_ocpu, q_omem, q_pcpu, q_pmem;
 };
 
 }  // namespace
@@ -669,7 +671,11 @@ void kcc_destroy(kcc_ctx* ctx) {
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
                       &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,
                       &dv.alloc_cpu, &dv.alloc_mem, &dv.alloc_pods, &dv.pod_count, &dv.spec_cpu,
-                      &dv.spec_mem,  &dv.partial,   &dv.totals,    &dv.err};
+                      &dv.spec_mem,  &dv.partial,   &dv.totals,    &dv.err,
+                      &dv.p_bytes,   &dv.p_off,     &dv.p_out,     &dv.p_st,      &dv.k_key,
+                      &dv.kb_counts, &dv.kb_tot,    &dv.kb_sk,     &dv.kb_sv,     &dv.q_ptr,
+                      &dv.q_iptr,    &dv.q_icpu,    &dv.q_imem,    &dv.q_rst,     &dv.q_ocpu,
+                      &dv.q_omem,    &dv.q_pcpu,    &dv.q_pmem};
     for (DevBuf* b : bufs)
       if (b->p) (void)hipFree(b->p);
     if (dv.stream) (void)hipStreamDestroy(dv.stream);
@@ -1200,3 +1206,154 @@ extern "C" int kcc_fit_rows(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* alloc
   KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
   return KCC_OK;
 }
+
+
+// ---- opt-in scheduler request model (kcc_pods.hip) ------------------
+
+namespace {
+
+// Host-side checks shared by the two host-array entry points.
+int check_pods(kcc_ctx* ctx, int64_t n_pods, int64_t n_cont, int64_t n_init,
+               const int64_t* pod_ptr, const uint64_t* cpu_req, const int64_t* mem_req,
+               const int64_t* init_ptr, const uint64_t* init_cpu, const int64_t* init_mem,
+               const uint8_t* restartable) {
+  int rc = check_csr(ctx, n_pods, n_cont, pod_ptr);
+  if (rc) return rc;
+  if (n_cont > 0 && (!cpu_req || !mem_req)) return fail(ctx, KCC_EINVAL, "NULL cpu_req/mem_req");
+  if (!init_ptr) {
+    if (n_init != 0 || init_cpu || init_mem || restartable)
+      return fail(ctx, KCC_EINVAL, "init container arrays without init_ptr");
+    return KCC_OK;
+  }
+  if ((rc = check_csr(ctx, n_pods, n_init, init_ptr))) return rc;
+  if (n_init > 0 && (!init_cpu || !init_mem)) return fail(ctx, KCC_EINVAL, "NULL init_cpu/init_mem");
+  return KCC_OK;
+}
+
+// Stages the pod-level inputs and enqueues the per-pod kernel; pod outputs in q_pcpu/q_pmem.
+int pods_stage_run(kcc_ctx* ctx, Dev& dv, int64_t n_pods, int64_t n_cont, int64_t n_init,
+                   const int64_t* pod_ptr, const uint64_t* cpu_req, const int64_t* mem_req,
+                   const int64_t* init_ptr, const uint64_t* init_cpu, const int64_t* init_mem,
+                   const uint8_t* restartable, const uint64_t* ovh_cpu, const int64_t* ovh_mem) {
+  int rc;
+  if ((rc = h2d(ctx, dv, dv.q_ptr, pod_ptr, n_pods + 1))) return rc;
+  if ((rc = h2d(ctx, dv, dv.cpu, cpu_req, n_cont))) return rc;
+  if ((rc = h2d(ctx, dv, dv.mem, mem_req, n_cont))) return rc;
+  if (init_ptr) {
+    if ((rc = h2d(ctx, dv, dv.q_iptr, init_ptr, n_pods + 1))) return rc;
+    if ((rc = h2d(ctx, dv, dv.q_icpu, init_cpu, n_init))) return rc;
+    if ((rc = h2d(ctx, dv, dv.q_imem, init_mem, n_init))) return rc;
+    if (restartable && (rc = h2d(ctx, dv, dv.q_rst, restartable, n_init))) return rc;
+  }
+  if (ovh_cpu && (rc = h2d(ctx, dv, dv.q_ocpu, ovh_cpu, n_pods))) return rc;
+  if (ovh_mem && (rc = h2d(ctx, dv, dv.q_omem, ovh_mem, n_pods))) return rc;
+  KCC_HIP(ctx, ensure(dv.q_pcpu, 8 * (size_t)n_pods));
+  KCC_HIP(ctx, ensure(dv.q_pmem, 8 * (size_t)n_pods));
+  KCC_HIP(ctx, kcc::launch_pod_requests(
+                   n_pods, n_cont, init_ptr ? n_init : 0, as<int64_t>(dv.q_ptr),
+                   as<uint64_t>(dv.cpu), as<int64_t>(dv.mem),
+                   init_ptr ? as<int64_t>(dv.q_iptr) : nullptr,
+                   init_ptr ? as<uint64_t>(dv.q_icpu) : nullptr,
+                   init_ptr ? as<int64_t>(dv.q_imem) : nullptr,
+                   init_ptr && restartable ? as<uint8_t>(dv.q_rst) : nullptr,
+                   ovh_cpu ? as<uint64_t>(dv.q_ocpu) : nullptr,
+                   ovh_mem ? as<int64_t>(dv.q_omem) : nullptr, as<uint64_t>(dv.q_pcpu),
+                   as<int64_t>(dv.q_pmem), dv.stream));
+  return KCC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kcc_pod_requests_async(kcc_ctx* ctx, int64_t n_pods, int64_t n_containers, int64_t n_init,
+                           const int64_t* d_pod_ptr, const uint64_t* d_cpu_req,
+                           const int64_t* d_mem_req, const int64_t* d_init_ptr,
+                           const uint64_t* d_init_cpu, const int64_t* d_init_mem,
+                           const uint8_t* d_restartable, const uint64_t* d_ovh_cpu,
+                           const int64_t* d_ovh_mem, uint64_t* d_pod_cpu, int64_t* d_pod_mem,
+                           void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  if (n_pods < 0 || n_containers < 0 || n_init < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (n_pods == 0) return KCC_OK;
+  if (!d_pod_ptr || !d_pod_cpu || !d_pod_mem) return fail(ctx, KCC_EINVAL, "NULL pod_ptr/output");
+  if (n_containers > 0 && (!d_cpu_req || !d_mem_req))
+    return fail(ctx, KCC_EINVAL, "NULL cpu_req/mem_req");
+  if (d_init_ptr && n_init > 0 && (!d_init_cpu || !d_init_mem))
+    return fail(ctx, KCC_EINVAL, "NULL init_cpu/init_mem");
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  KCC_HIP(ctx, kcc::launch_pod_requests(n_pods, n_containers, d_init_ptr ? n_init : 0, d_pod_ptr,
+                                        d_cpu_req, d_mem_req, d_init_ptr, d_init_cpu, d_init_mem,
+                                        d_init_ptr ? d_restartable : nullptr, d_ovh_cpu,
+                                        d_ovh_mem, d_pod_cpu, d_pod_mem,
+                                        static_cast<hipStream_t>(stream)));
+  return KCC_OK;
+}
+
+int kcc_pod_requests(kcc_ctx* ctx, int64_t n_pods, int64_t n_containers, int64_t n_init,
+                     const int64_t* pod_ptr, const uint64_t* cpu_req, const int64_t* mem_req,
+                     const int64_t* init_ptr, const uint64_t* init_cpu, const int64_t* init_mem,
+                     const uint8_t* restartable, const uint64_t* ovh_cpu,
+                     const int64_t* ovh_mem, uint64_t* pod_cpu, int64_t* pod_mem) {
+  if (!ctx) return KCC_EINVAL;
+  if (n_init < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  int rc = check_pods(ctx, n_pods, n_containers, n_init, pod_ptr, cpu_req, mem_req, init_ptr,
+                      init_cpu, init_mem, restartable);
+  if (rc) return rc;
+  if (n_pods == 0) return KCC_OK;
+  if (!pod_cpu || !pod_mem) return fail(ctx, KCC_EINVAL, "NULL output");
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  if ((rc = pods_stage_run(ctx, dv, n_pods, n_containers, n_init, pod_ptr, cpu_req, mem_req,
+                           init_ptr, init_cpu, init_mem, restartable, ovh_cpu, ovh_mem)))
+    return rc;
+  KCC_HIP(ctx, hipMemcpyAsync(pod_cpu, dv.q_pcpu.p, 8 * (size_t)n_pods, hipMemcpyDeviceToHost,
+                              dv.stream));
+  KCC_HIP(ctx, hipMemcpyAsync(pod_mem, dv.q_pmem.p, 8 * (size_t)n_pods, hipMemcpyDeviceToHost,
+                              dv.stream));
+  KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
+  return KCC_OK;
+}
+
+int kcc_reduce_requests_pods(kcc_ctx* ctx, int64_t n_nodes, int64_t n_pods,
+                             int64_t n_containers, int64_t n_init, const int64_t* node_pod_ptr,
+                             const int64_t* pod_ptr, const uint64_t* cpu_req,
+                             const int64_t* mem_req, const int64_t* init_ptr,
+                             const uint64_t* init_cpu, const int64_t* init_mem,
+                             const uint8_t* restartable, const uint64_t* ovh_cpu,
+                             const int64_t* ovh_mem, uint64_t* used_cpu, int64_t* used_mem) {
+  if (!ctx) return KCC_EINVAL;
+  if (n_init < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  int rc = check_csr(ctx, n_nodes, n_pods, node_pod_ptr);
+  if (rc) return rc;
+  if ((rc = check_pods(ctx, n_pods, n_containers, n_init, pod_ptr, cpu_req, mem_req, init_ptr,
+                       init_cpu, init_mem, restartable)))
+    return rc;
+  if (n_nodes == 0) return KCC_OK;
+  if (!used_cpu || !used_mem) return fail(ctx, KCC_EINVAL, "NULL output");
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  if ((rc = h2d(ctx, dv, dv.ptr, node_pod_ptr, n_nodes + 1))) return rc;
+  if (n_pods > 0 &&
+      (rc = pods_stage_run(ctx, dv, n_pods, n_containers, n_init, pod_ptr, cpu_req, mem_req,
+                           init_ptr, init_cpu, init_mem, restartable, ovh_cpu, ovh_mem)))
+    return rc;
+  KCC_HIP(ctx, ensure(dv.q_pcpu, 8 * (size_t)(n_pods > 0 ? n_pods : 1)));
+  KCC_HIP(ctx, ensure(dv.q_pmem, 8 * (size_t)(n_pods > 0 ? n_pods : 1)));
+  KCC_HIP(ctx, ensure(dv.used_cpu, 8 * (size_t)n_nodes));
+  KCC_HIP(ctx, ensure(dv.used_mem, 8 * (size_t)n_nodes));
+  // the pods of each node are the "containers" of the ordinary segmented reduce
+  rc = reduce_async_dev(ctx, dv, n_nodes, n_pods, as<int64_t>(dv.ptr), as<uint64_t>(dv.q_pcpu),
+                        as<int64_t>(dv.q_pmem), nullptr, nullptr, as<uint64_t>(dv.used_cpu),
+                        as<int64_t>(dv.used_mem), nullptr, nullptr, dv.stream);
+  if (rc) return rc;
+  KCC_HIP(ctx, hipMemcpyAsync(used_cpu, dv.used_cpu.p, 8 * (size_t)n_nodes,
+                              hipMemcpyDeviceToHost, dv.stream));
+  KCC_HIP(ctx, hipMemcpyAsync(used_mem, dv.used_mem.p, 8 * (size_t)n_nodes,
+                              hipMemcpyDeviceToHost, dv.stream));
+  KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
+  return KCC_OK;
+}
+
+}  // extern "C"

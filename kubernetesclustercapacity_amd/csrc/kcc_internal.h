@@ -275,4 +275,13 @@ hipError_t launch_fit_rows(int64_t n, const uint64_t* alloc_cpu, const int64_t* 
                            const uint64_t* used_cpu, const int64_t* used_mem, uint64_t spec_cpu,
                            int64_t spec_mem, int64_t* q, int32_t* err, hipStream_t s);
 
+// ---- opt-in scheduler request model (kcc_pods.hip) ---------------
+hipError_t launch_pod_requests(int64_t n_pods, int64_t n_cont, int64_t n_init,
+                               const int64_t* pod_ptr, const uint64_t* cpu_req,
+                               const int64_t* mem_req, const int64_t* init_ptr,
+                               const uint64_t* init_cpu, const int64_t* init_mem,
+                               const uint8_t* restartable, const uint64_t* ovh_cpu,
+                               const int64_t* ovh_mem, uint64_t* pod_cpu, int64_t* pod_mem,
+                               hipStream_t s);
+
 }  // namespace kcc

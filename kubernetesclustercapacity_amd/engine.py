@@ -239,6 +239,67 @@ class CapacityEngine:
                                            _p(err)))
         return q, err
 
+    @staticmethod
+    def _pod_args(pod_ptr, cpu_req, mem_req, init_ptr, init_cpu, init_mem, restartable,
+                  ovh_cpu, ovh_mem):
+        pp = _arr(pod_ptr, np.int64)
+        if pp.size < 1:
+            raise ValueError("pod_ptr needs n_pods + 1 entries")
+        n_pods = pp.size - 1
+        cr, mr = _arr(cpu_req, np.uint64), _arr(mem_req, np.int64)
+        if cr.size != mr.size:
+            raise ValueError("container arrays differ in length")
+        ip = ic = im = rs = None
+        n_init = 0
+        if init_ptr is not None:
+            ip, ic, im = _arr(init_ptr, np.int64), _arr(init_cpu, np.uint64), _arr(init_mem, np.int64)
+            if ip.size != n_pods + 1 or ic.size != im.size:
+                raise ValueError("init arrays do not match pod_ptr")
+            n_init = ic.size
+            if restartable is not None:
+                rs = _arr(restartable, np.uint8)
+                if rs.size != n_init:
+                    raise ValueError("restartable differs in length from the init arrays")
+        elif restartable is not None or init_cpu is not None or init_mem is not None:
+            raise ValueError("init container arrays without init_ptr")
+        oc = None if ovh_cpu is None else _arr(ovh_cpu, np.uint64)
+        om = None if ovh_mem is None else _arr(ovh_mem, np.int64)
+        for o in (oc, om):
+            if o is not None and o.size != n_pods:
+                raise ValueError("overhead arrays need one entry per pod")
+        return n_pods, cr.size, n_init, [pp, cr, mr, ip, ic, im, rs, oc, om]
+
+    def pod_requests(self, pod_ptr, cpu_req, mem_req, init_ptr=None, init_cpu=None,
+                     init_mem=None, restartable=None, ovh_cpu=None, ovh_mem=None):
+        """OPT-IN scheduler request model (NOT the reference, which sums
+        app containers only, CC:276-294): per pod max(app sum, init max incl. sidecars) +
+        overhead — see include/kcc.h.  Returns (uint64 cpu[P], int64 mem[P])."""
+        n_pods, n_cont, n_init, a = self._pod_args(pod_ptr, cpu_req, mem_req, init_ptr,
+                                                   init_cpu, init_mem, restartable, ovh_cpu,
+                                                   ovh_mem)
+        pc, pm = np.zeros(n_pods, np.uint64), np.zeros(n_pods, np.int64)
+        self._check(self._lib.kcc_pod_requests(self._h, n_pods, n_cont, n_init,
+                                               *[_p(x) for x in a], _p(pc), _p(pm)))
+        return pc, pm
+
+    def reduce_requests_pods(self, node_pod_ptr, pod_ptr, cpu_req, mem_req, init_ptr=None,
+                             init_cpu=None, init_mem=None, restartable=None, ovh_cpu=None,
+                             ovh_mem=None):
+        """Per-node sums of the opt-in pod requests (pods grouped by node, CSR
+        node_pod_ptr[N+1]): the used_cpu / used_mem kcc_fit takes."""
+        npp = _arr(node_pod_ptr, np.int64)
+        if npp.size < 1:
+            raise ValueError("node_pod_ptr needs n_nodes + 1 entries")
+        n_nodes = npp.size - 1
+        n_pods, n_cont, n_init, a = self._pod_args(pod_ptr, cpu_req, mem_req, init_ptr,
+                                                   init_cpu, init_mem, restartable, ovh_cpu,
+                                                   ovh_mem)
+        uc, um = np.zeros(n_nodes, np.uint64), np.zeros(n_nodes, np.int64)
+        self._check(self._lib.kcc_reduce_requests_pods(self._h, n_nodes, n_pods, n_cont, n_init,
+                                                       _p(npp), *[_p(x) for x in a], _p(uc),
+                                                       _p(um)))
+        return uc, um
+
     def quantity_value(self, strings):
         """resource.Quantity.Value() of ParseQuantity (CC:285-286, parity unpinned: see
         include/kcc.h) over a batch.  Returns (int64 values, int8 status)."""

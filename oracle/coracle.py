@@ -44,6 +44,8 @@ def lib():
         L.kcco_parse_cpu_millis.restype = None
         L.kcco_parse_bytes.argtypes = [i64, vp, vp, vp, vp, C.c_int]
         L.kcco_parse_bytes.restype = None
+        L.kcco_pod_requests.argtypes = [i64] + [vp] * 11
+        L.kcco_pod_requests.restype = None
         _LIB = L
     return _LIB
 
@@ -119,3 +121,19 @@ def parse_bytes(buf, off, n_threads=1):
     out, st = np.zeros(n, np.int64), np.zeros(n, np.int8)
     lib().kcco_parse_bytes(n, _p(buf), _p(off), _p(out), _p(st), int(n_threads))
     return out, st
+
+
+def pod_requests(pod_ptr, cpu_req, mem_req, init_ptr=None, init_cpu=None, init_mem=None,
+                 restartable=None, ovh_cpu=None, ovh_mem=None):
+    """SURVEY §8f row 4 (opt-in scheduler request model, not the reference): per-pod
+    effective requests, see kcc_oracle.h kcco_pod_requests."""
+    pod_ptr = np.ascontiguousarray(pod_ptr, np.int64)
+    n = pod_ptr.size - 1
+    a = [np.ascontiguousarray(cpu_req, np.uint64), np.ascontiguousarray(mem_req, np.int64)]
+    opt = [(init_ptr, np.int64), (init_cpu, np.uint64), (init_mem, np.int64),
+           (restartable, np.uint8), (ovh_cpu, np.uint64), (ovh_mem, np.int64)]
+    b = [None if x is None else np.ascontiguousarray(x, t) for x, t in opt]
+    pc, pm = np.zeros(n, np.uint64), np.zeros(n, np.int64)
+    lib().kcco_pod_requests(n, _p(pod_ptr), *[_p(x) for x in a], *[_p(x) for x in b],
+                            _p(pc), _p(pm))
+    return pc, pm

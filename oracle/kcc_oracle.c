@@ -41,6 +41,48 @@ void kcco_reduce_requests(int64_t n_nodes, const int64_t* node_ptr,
   }
 }
 
+/* SURVEY §8f row 4 (opt-in, not the reference): see kcc_oracle.h. */
+void kcco_pod_requests(int64_t n_pods, const int64_t* pod_ptr, const uint64_t* cpu_req,
+                       const int64_t* mem_req, const int64_t* init_ptr,
+                       const uint64_t* init_cpu, const int64_t* init_mem,
+                       const uint8_t* restartable, const uint64_t* ovh_cpu,
+                       const int64_t* ovh_mem, uint64_t* pod_cpu, int64_t* pod_mem) {
+  for (int64_t p = 0; p < n_pods; ++p) {
+    uint64_t ac = 0, am = 0; /* app sums (memory kept as bits) */
+    for (int64_t c = pod_ptr[p]; c < pod_ptr[p + 1]; ++c) {
+      ac += cpu_req[c];
+      am += (uint64_t)mem_req[c];
+    }
+    /* sidecar sums; init max, starting at the identity of max (no init container:
+     * req = app, as k8s' maxResourceList over an empty list) */
+    uint64_t sc = 0, sm = 0, ic = 0;
+    int64_t im = INT64_MIN;
+    if (init_ptr) {
+      for (int64_t k = init_ptr[p]; k < init_ptr[p + 1]; ++k) {
+        if (restartable && restartable[k]) {
+          ac += init_cpu[k];
+          am += (uint64_t)init_mem[k];
+          sc += init_cpu[k];
+          sm += (uint64_t)init_mem[k];
+          if (sc > ic) ic = sc;
+          if ((int64_t)sm > im) im = (int64_t)sm;
+        } else {
+          const uint64_t tc = init_cpu[k] + sc;
+          const int64_t tm = (int64_t)((uint64_t)init_mem[k] + sm);
+          if (tc > ic) ic = tc;
+          if (tm > im) im = tm;
+        }
+      }
+    }
+    uint64_t rc = ac > ic ? ac : ic;
+    uint64_t rm = (int64_t)am > im ? am : (uint64_t)im;
+    if (ovh_cpu) rc += ovh_cpu[p];
+    if (ovh_mem) rm += (uint64_t)ovh_mem[p];
+    pod_cpu[p] = rc;
+    pod_mem[p] = (int64_t)rm;
+  }
+}
+
 /* CC:159-164 */
 int64_t kcco_find_min(int64_t x, int64_t y) { return x <= y ? x : y; }
 

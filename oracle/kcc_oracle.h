@@ -58,6 +58,24 @@ void kcco_parse_cpu_millis(int64_t n, const char* bytes, const int64_t* offsets,
 void kcco_parse_bytes(int64_t n, const char* bytes, const int64_t* offsets, int64_t* out,
                       int8_t* status, int n_threads);
 
+/* SURVEY §8f row 4 — OPT-IN scheduler request model, NOT the reference's semantics
+ * (the reference sums app containers only, CC:276-294).  Restates the published
+ * kube-scheduler pod request (k8s.io/kubernetes pkg/api/v1/resource PodRequests, the
+ * sidecar-aware form of k8s >= 1.28; that dependency is absent here, so parity is
+ * unpinned beyond hand-derived cases), per resource, over 64-bit wrapping sums:
+ *   app = sum of app containers; side = 0; init = 0
+ *   for each init container k in order:
+ *     restartable: app += r_k; side += r_k; init = max(init, side)
+ *     otherwise:   init = max(init, r_k + side)
+ *   req(p) = max(app, init) + overhead(p)
+ * cpu unsigned (uint64 max), memory signed (int64 max).  init_ptr / init arrays /
+ * restartable / overhead may be NULL (none / false / 0). */
+void kcco_pod_requests(int64_t n_pods, const int64_t* pod_ptr, const uint64_t* cpu_req,
+                       const int64_t* mem_req, const int64_t* init_ptr,
+                       const uint64_t* init_cpu, const int64_t* init_mem,
+                       const uint8_t* restartable, const uint64_t* ovh_cpu,
+                       const int64_t* ovh_mem, uint64_t* pod_cpu, int64_t* pod_mem);
+
 #ifdef __cplusplus
 }
 #endif

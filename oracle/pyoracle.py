@@ -157,3 +157,40 @@ def to_bytes(s: str):
     if math.isnan(v) or v >= 2.0 ** 63 or v < -(2.0 ** 63):
         return I64_MIN, True  # amd64 CVTTSD2SQ overflow value
     return int(v), True
+
+
+def pod_requests(pod_ptr, cpu_req, mem_req, init_ptr=None, init_cpu=None, init_mem=None,
+                 restartable=None, ovh_cpu=None, ovh_mem=None):
+    """SURVEY §8f row 4 — OPT-IN scheduler request model, NOT the reference's semantics
+    (the reference sums app containers only, CC:276-294).  The kube-scheduler's pod
+    request (pkg/api/v1/resource PodRequests, sidecar-aware form; absent here, parity
+    unpinned beyond hand-derived cases), restated with k8s' "absent resource" rule for
+    max: an empty init list leaves the app sum unchanged.  Returns [(cpu, mem)]."""
+    out = []
+    for p in range(len(pod_ptr) - 1):
+        app = [0, 0]
+        for c in range(pod_ptr[p], pod_ptr[p + 1]):
+            app = [app[0] + int(cpu_req[c]), app[1] + int(mem_req[c])]
+        side = [0, 0]
+        init = [None, None]
+        if init_ptr is not None:
+            for k in range(init_ptr[p], init_ptr[p + 1]):
+                r = [int(init_cpu[k]), int(init_mem[k])]
+                if restartable is not None and restartable[k]:
+                    app = [app[0] + r[0], app[1] + r[1]]
+                    side = [side[0] + r[0], side[1] + r[1]]
+                    cand = side
+                else:
+                    cand = [r[0] + side[0], r[1] + side[1]]
+                # compare in the wrapped domain (cpu unsigned, memory signed)
+                cand = [u64(cand[0]), i64(cand[1])]
+                init = [cand[j] if init[j] is None or cand[j] > init[j] else init[j]
+                        for j in range(2)]
+        app = [u64(app[0]), i64(app[1])]
+        req = [app[j] if init[j] is None or app[j] >= init[j] else init[j] for j in range(2)]
+        if ovh_cpu is not None:
+            req[0] += int(ovh_cpu[p])
+        if ovh_mem is not None:
+            req[1] += int(ovh_mem[p])
+        out.append((u64(req[0]), i64(req[1])))
+    return out
