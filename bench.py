@@ -62,6 +62,8 @@ def parse():
                     help="node chunks of the pipelined step (reduce of chunk k overlaps the fit "
                          "of chunk k-1); 1 = reduce, then fit")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pods", action="store_true",
+                    help="skip the opt-in scheduler pod-request leg (SURVEY §8f row 4)")
     ap.add_argument("--no-keyed", action="store_true",
                     help="skip the list-order (keyed) reduce leg (SURVEY §8f row 1)")
     ap.add_argument("--no-parse", action="store_true",
@@ -242,6 +244,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_keyed:
         out["keyed"] = keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream,
                                  args.steps, args.warmup)
+    if rank == 0 and world == 1 and not args.no_pods:
+        out["pods"] = pods_leg(eng, ptr, cpu, mem, n, dev, stream, args.steps, args.warmup)
     if rank == 0 and world == 1 and not args.no_parse:
         del ptr, cpu, mem
         out["parse"] = parse_leg(eng, cl, dev, stream, args.steps, args.warmup,
@@ -298,6 +302,78 @@ def keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream, steps, war
                      "note": "bucketed: LDS histograms, staged scatter, LDS accumulation; "
                              "no global atomics"},
         "equals_csr_reduce": diff_rows == 0, "rows_differing": diff_rows,
+    }
+
+
+def pods_leg(eng, ptr, cpu, mem, n, dev, stream, steps, warmup):
+    """SURVEY §8f row 4 (opt-in scheduler request model, NOT the reference's semantics),
+    measured beside the step: the C4 containers cut into pods (a pod starts at every node
+    start and with probability 1/2 at any other container: ~2 containers per pod), one
+    init container on every third pod (30 % of them restartable sidecars), overhead on
+    every fifth pod -> per-pod effective requests (pod_requests_kernel).  Algorithmic bytes
+    per launch: P x 16 (app + init offsets) + C x 16 + I x 17 + P x 16 (overhead) in,
+    P x 16 out.  Checked: with the init containers and overhead dropped, the per-node sums
+    of the pod requests equal the step's CSR reduce."""
+    import torch
+
+    C = cpu.numel()
+    g = torch.Generator(device=dev)
+    g.manual_seed(20261017)
+    start = torch.rand(C, device=dev, generator=g) < 0.5
+    start[ptr[:-1][torch.diff(ptr) > 0]] = True
+    pod_ptr = torch.cat([torch.nonzero(start).flatten(),
+                         torch.tensor([C], device=dev, dtype=torch.int64)])
+    P = pod_ptr.numel() - 1
+    node_pod_ptr = torch.cat([torch.zeros(1, device=dev, dtype=torch.int64),
+                              torch.cumsum(start.to(torch.int64), 0)])[ptr]
+    has_init = (torch.arange(P, device=dev) % 3) == 0
+    init_ptr = torch.cat([torch.zeros(1, device=dev, dtype=torch.int64),
+                          torch.cumsum(has_init.to(torch.int64), 0)])
+    I = int(init_ptr[-1].item())
+    init_cpu = torch.randint(0, 40, (I,), device=dev, generator=g, dtype=torch.int64) * 50
+    init_mem = torch.randint(0, 256, (I,), device=dev, generator=g, dtype=torch.int64) << 26
+    rst = (torch.rand(I, device=dev, generator=g) < 0.3).to(torch.uint8)
+    sel = (torch.arange(P, device=dev) % 5) == 0
+    ovh_cpu = torch.where(sel, 100, 0).to(torch.int64)
+    ovh_mem = torch.where(sel, 1 << 27, 0).to(torch.int64)
+    pc = torch.empty(P, dtype=torch.int64, device=dev)
+    pm = torch.empty(P, dtype=torch.int64, device=dev)
+    del start, has_init, sel
+    torch.cuda.synchronize()
+    with torch.cuda.stream(stream):
+        run = lambda: eng.pod_requests_async(pod_ptr, cpu, mem, pc, pm, init_ptr, init_cpu,
+                                             init_mem, rst, ovh_cpu, ovh_mem, stream=stream)
+        for _ in range(warmup):
+            run()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        ev0.record(stream)
+        for _ in range(steps):
+            run()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        ms = ev0.elapsed_time(ev1) / steps
+        # default semantics (no init, no overhead): node sums == the step's reduce
+        eng.pod_requests_async(pod_ptr, cpu, mem, pc, pm, stream=stream)
+        uc = torch.empty(n, dtype=torch.int64, device=dev)
+        um = torch.empty(n, dtype=torch.int64, device=dev)
+        eng.reduce_requests_async(node_pod_ptr, pc, pm, uc, um, stream=stream)
+        rc = torch.empty(n, dtype=torch.int64, device=dev)
+        rm = torch.empty(n, dtype=torch.int64, device=dev)
+        eng.reduce_requests_async(ptr, cpu, mem, rc, rm, stream=stream)
+        torch.cuda.synchronize()
+    diff_rows = int(((uc != rc) | (um != rm)).sum().item())
+    alg = P * 16 + C * 16 + I * 17 + P * 16 + P * 16
+    gbs = alg / (ms * 1e-3) / 1e9
+    del pod_ptr, node_pod_ptr, init_ptr, init_cpu, init_mem, rst, ovh_cpu, ovh_mem, pc, pm
+    return {
+        "op": "opt-in scheduler pod requests: max(app sum, init max incl. sidecars) + overhead "
+              "(NOT the reference's semantics)",
+        "kernel": "pod_requests_kernel", "pods": P, "containers": C, "init_containers": I,
+        "ms_per_launch": ms, "pods_per_s": P / (ms * 1e-3),
+        "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": alg},
+        "default_semantics_equals_csr_reduce": diff_rows == 0, "rows_differing": diff_rows,
     }
 
 

@@ -23,6 +23,9 @@
 namespace kcc {
 namespace {
 
+constexpr int POD_BATCH = 4;   // app containers loaded per round trip
+constexpr int INIT_BATCH = 2;  // init containers loaded per round trip
+
 __global__ __launch_bounds__(256) void pod_requests_kernel(
     int64_t n_pods, int64_t n_cont, int64_t n_init, const int64_t* __restrict__ pod_ptr,
     const uint64_t* __restrict__ cpu_req, const int64_t* __restrict__ mem_req,
@@ -36,10 +39,25 @@ __global__ __launch_bounds__(256) void pod_requests_kernel(
   int64_t lo = pod_ptr[p], hi = pod_ptr[p + 1];
   lo = lo < 0 ? 0 : (lo > n_cont ? n_cont : lo);
   hi = hi < lo ? lo : (hi > n_cont ? n_cont : hi);
+  // the overhead loads go out first (independent of everything else), then the
+  // containers in batches whose loads are all issued before their sums (a pod's loop
+  // is 1-3 iterations: one memory round trip per batch, not per container)
+  const uint64_t oc = ovh_cpu ? ovh_cpu[p] : 0;
+  const uint64_t om = ovh_mem ? (uint64_t)ovh_mem[p] : 0;
   uint64_t ac = 0, am = 0;
-  for (int64_t c = lo; c < hi; ++c) {
-    ac += cpu_req[c];
-    am += (uint64_t)mem_req[c];
+  for (int64_t c = lo; c < hi; c += POD_BATCH) {
+    uint64_t vc[POD_BATCH], vm[POD_BATCH];
+#pragma unroll
+    for (int u = 0; u < POD_BATCH; ++u) {
+      const bool in = c + u < hi;
+      vc[u] = in ? cpu_req[c + u] : 0;
+      vm[u] = in ? (uint64_t)mem_req[c + u] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < POD_BATCH; ++u) {
+      ac += vc[u];
+      am += vm[u];
+    }
   }
   uint64_t sc = 0, sm = 0, ic = 0;
   int64_t im = INT64_MIN;
@@ -47,27 +65,38 @@ __global__ __launch_bounds__(256) void pod_requests_kernel(
     int64_t a = init_ptr[p], b = init_ptr[p + 1];
     a = a < 0 ? 0 : (a > n_init ? n_init : a);
     b = b < a ? a : (b > n_init ? n_init : b);
-    for (int64_t k = a; k < b; ++k) {
-      const uint64_t rc = init_cpu[k], rm = (uint64_t)init_mem[k];
-      if (restartable && restartable[k]) {
-        ac += rc;
-        am += rm;
-        sc += rc;
-        sm += rm;
-        ic = sc > ic ? sc : ic;
-        im = (int64_t)sm > im ? (int64_t)sm : im;
-      } else {
-        const uint64_t tc = rc + sc;
-        const int64_t tm = (int64_t)(rm + sm);
-        ic = tc > ic ? tc : ic;
-        im = tm > im ? tm : im;
+    for (int64_t k0 = a; k0 < b; k0 += INIT_BATCH) {
+      uint64_t rcv[INIT_BATCH], rmv[INIT_BATCH];
+      bool rs[INIT_BATCH];
+#pragma unroll
+      for (int u = 0; u < INIT_BATCH; ++u) {
+        const bool in = k0 + u < b;
+        rcv[u] = in ? init_cpu[k0 + u] : 0;
+        rmv[u] = in ? (uint64_t)init_mem[k0 + u] : 0;
+        rs[u] = in && restartable ? restartable[k0 + u] != 0 : false;
+      }
+#pragma unroll
+      for (int u = 0; u < INIT_BATCH; ++u) {
+        if (k0 + u >= b) break;
+        const uint64_t rc = rcv[u], rm = rmv[u];
+        if (rs[u]) {  // a sidecar: runs for the pod's life
+          ac += rc;
+          am += rm;
+          sc += rc;
+          sm += rm;
+          ic = sc > ic ? sc : ic;
+          im = (int64_t)sm > im ? (int64_t)sm : im;
+        } else {
+          const uint64_t tc = rc + sc;
+          const int64_t tm = (int64_t)(rm + sm);
+          ic = tc > ic ? tc : ic;
+          im = tm > im ? tm : im;
+        }
       }
     }
   }
-  uint64_t rc = ac > ic ? ac : ic;
-  uint64_t rm = (int64_t)am > im ? am : (uint64_t)im;
-  if (ovh_cpu) rc += ovh_cpu[p];
-  if (ovh_mem) rm += (uint64_t)ovh_mem[p];
+  const uint64_t rc = (ac > ic ? ac : ic) + oc;
+  const uint64_t rm = ((int64_t)am > im ? am : (uint64_t)im) + om;
   pod_cpu[p] = rc;
   pod_mem[p] = (int64_t)rm;
 }

@@ -194,6 +194,16 @@ class CapacityEngine:
             self._h, n_keys, key.numel(), _dp(key), _dp(cpu_req), _dp(mem_req), None, None,
             _dp(used_cpu), _dp(used_mem), None, None, _stream(stream)))
 
+    def pod_requests_async(self, pod_ptr, cpu_req, mem_req, pod_cpu, pod_mem, init_ptr=None,
+                           init_cpu=None, init_mem=None, restartable=None, ovh_cpu=None,
+                           ovh_mem=None, stream=None):
+        """Device form of pod_requests (torch tensors; SURVEY §8f row 4, opt-in)."""
+        n_init = 0 if init_cpu is None else init_cpu.numel()
+        self._check(self._lib.kcc_pod_requests_async(
+            self._h, pod_ptr.numel() - 1, cpu_req.numel(), n_init, _dp(pod_ptr), _dp(cpu_req),
+            _dp(mem_req), _dp(init_ptr), _dp(init_cpu), _dp(init_mem), _dp(restartable),
+            _dp(ovh_cpu), _dp(ovh_mem), _dp(pod_cpu), _dp(pod_mem), _stream(stream)))
+
     # -- quantity strings (SURVEY §8f row 2) -------------------------------------
     def _parse(self, fn, strings, dtype):
         if isinstance(strings, tuple):
