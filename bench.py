@@ -365,6 +365,7 @@ def pods_leg(eng, ptr, cpu, mem, n, dev, stream, steps, warmup):
     diff_rows = int(((uc != rc) | (um != rm)).sum().item())
     alg = P * 16 + C * 16 + I * 17 + P * 16 + P * 16
     gbs = alg / (ms * 1e-3) / 1e9
+    traffic, tsrc = pmc_traffic("pod_requests_kernel")
     del pod_ptr, node_pod_ptr, init_ptr, init_cpu, init_mem, rst, ovh_cpu, ovh_mem, pc, pm
     return {
         "op": "opt-in scheduler pod requests: max(app sum, init max incl. sidecars) + overhead "
@@ -372,7 +373,8 @@ def pods_leg(eng, ptr, cpu, mem, n, dev, stream, steps, warmup):
         "kernel": "pod_requests_kernel", "pods": P, "containers": C, "init_containers": I,
         "ms_per_launch": ms, "pods_per_s": P / (ms * 1e-3),
         "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": alg},
+                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": alg, "traffic": traffic,
+                     "traffic_source": tsrc},
         "default_semantics_equals_csr_reduce": diff_rows == 0, "rows_differing": diff_rows,
     }
 
