@@ -14,10 +14,10 @@
 // The per-node sums are then the ordinary segmented reduce (reduce_kernel) over the
 // pods of each node, so used_cpu / used_mem feed kcc_fit unchanged.
 //
-// One lane per pod: pods hold 1-3 containers, so a lane's loop is short
-// and the lanes of a wave read consecutive runs of the container arrays (the CSR keeps
-// a pod's containers contiguous).  HBM-bound: 16 B per pod of offsets (app + init),
-// 16 B per container, 16 B per pod of overhead in, 16 B per pod out.
+// One lane per pod (pods hold 1-3 containers): the lanes of a wave read
+// consecutive runs of the container arrays (the CSR keeps a pod's containers contiguous),
+// in batches whose loads are all issued before their sums.  HBM-bound: 16 B per pod of offsets (app + init), 16 B per
+// container, 17 B per init container, 16 B per pod of overhead in, 16 B per pod out.
 #include "kcc_internal.h"
 
 namespace kcc {
@@ -26,32 +26,36 @@ namespace {
 constexpr int POD_BATCH = 4;   // app containers loaded per round trip
 constexpr int INIT_BATCH = 2;  // init containers loaded per round trip
 
-__global__ __launch_bounds__(256) void pod_requests_kernel(
-    int64_t n_pods, int64_t n_cont, int64_t n_init, const int64_t* __restrict__ pod_ptr,
-    const uint64_t* __restrict__ cpu_req, const int64_t* __restrict__ mem_req,
-    const int64_t* __restrict__ init_ptr, const uint64_t* __restrict__ init_cpu,
-    const int64_t* __restrict__ init_mem, const uint8_t* __restrict__ restartable,
-    const uint64_t* __restrict__ ovh_cpu, const int64_t* __restrict__ ovh_mem,
-    uint64_t* __restrict__ pod_cpu, int64_t* __restrict__ pod_mem) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n_pods) return;
-  // offsets clamped into the arrays: a malformed CSR gives wrong sums, never a fault
-  int64_t lo = pod_ptr[p], hi = pod_ptr[p + 1];
-  lo = lo < 0 ? 0 : (lo > n_cont ? n_cont : lo);
-  hi = hi < lo ? lo : (hi > n_cont ? n_cont : hi);
-  // the overhead loads go out first (independent of everything else), then the
-  // containers in batches whose loads are all issued before their sums (a pod's loop
-  // is 1-3 iterations: one memory round trip per batch, not per container)
-  const uint64_t oc = ovh_cpu ? ovh_cpu[p] : 0;
-  const uint64_t om = ovh_mem ? (uint64_t)ovh_mem[p] : 0;
+#ifndef KCC_POD_LDS
+// 1: stage each workgroup's container ranges in LDS by coalesced loads first.  Measured
+// slower at C4 (scripts/ab_pods.py: 0.359 vs 0.347 ms; the per-lane loads already move
+// only the algorithmic bytes, PMC 1.69 GB vs 1.72 GB), so off by default.
+#define KCC_POD_LDS 0
+#endif
+constexpr int POD_WG = 256;
+[[maybe_unused]] constexpr int POD_CAP_C = 1024;  // app containers staged per workgroup (16 KB)
+[[maybe_unused]] constexpr int POD_CAP_I = 512;   // init containers staged per workgroup (8.5 KB)
+
+// Clamp [lo, hi) into [0, n).
+__device__ __forceinline__ void clamp_range(int64_t& lo, int64_t& hi, int64_t n) {
+  lo = lo < 0 ? 0 : (lo > n ? n : lo);
+  hi = hi < lo ? lo : (hi > n ? n : hi);
+}
+
+// One pod's request from loaders for its app / init containers (staged or global).
+template <class AppAt, class InitAt>
+__device__ __forceinline__ void pod_request(int64_t lo, int64_t hi, int64_t a, int64_t b,
+                                            bool has_init, uint64_t oc, uint64_t om,
+                                            AppAt app_at, InitAt init_at, uint64_t& out_c,
+                                            uint64_t& out_m) {
   uint64_t ac = 0, am = 0;
   for (int64_t c = lo; c < hi; c += POD_BATCH) {
     uint64_t vc[POD_BATCH], vm[POD_BATCH];
 #pragma unroll
     for (int u = 0; u < POD_BATCH; ++u) {
-      const bool in = c + u < hi;
-      vc[u] = in ? cpu_req[c + u] : 0;
-      vm[u] = in ? (uint64_t)mem_req[c + u] : 0;
+      vc[u] = 0;
+      vm[u] = 0;
+      if (c + u < hi) app_at(c + u, vc[u], vm[u]);
     }
 #pragma unroll
     for (int u = 0; u < POD_BATCH; ++u) {
@@ -61,19 +65,16 @@ __global__ __launch_bounds__(256) void pod_requests_kernel(
   }
   uint64_t sc = 0, sm = 0, ic = 0;
   int64_t im = INT64_MIN;
-  if (init_ptr) {
-    int64_t a = init_ptr[p], b = init_ptr[p + 1];
-    a = a < 0 ? 0 : (a > n_init ? n_init : a);
-    b = b < a ? a : (b > n_init ? n_init : b);
+  if (has_init) {
     for (int64_t k0 = a; k0 < b; k0 += INIT_BATCH) {
       uint64_t rcv[INIT_BATCH], rmv[INIT_BATCH];
       bool rs[INIT_BATCH];
 #pragma unroll
       for (int u = 0; u < INIT_BATCH; ++u) {
-        const bool in = k0 + u < b;
-        rcv[u] = in ? init_cpu[k0 + u] : 0;
-        rmv[u] = in ? (uint64_t)init_mem[k0 + u] : 0;
-        rs[u] = in && restartable ? restartable[k0 + u] != 0 : false;
+        rcv[u] = 0;
+        rmv[u] = 0;
+        rs[u] = false;
+        if (k0 + u < b) init_at(k0 + u, rcv[u], rmv[u], rs[u]);
       }
 #pragma unroll
       for (int u = 0; u < INIT_BATCH; ++u) {
@@ -95,8 +96,108 @@ __global__ __launch_bounds__(256) void pod_requests_kernel(
       }
     }
   }
-  const uint64_t rc = (ac > ic ? ac : ic) + oc;
-  const uint64_t rm = ((int64_t)am > im ? am : (uint64_t)im) + om;
+  out_c = (ac > ic ? ac : ic) + oc;
+  out_m = ((int64_t)am > im ? am : (uint64_t)im) + om;
+}
+
+// One lane per pod.  The workgroup's pods [p0, p0 + 256) hold one contiguous range of
+// app containers and one of init containers (CSR): with KCC_POD_LDS the first POD_CAP_C / POD_CAP_I of them
+// are loaded by all lanes together (coalesced) into LDS, and each lane then walks its
+// pods' containers there; containers past the caps (a workgroup of unusually large
+// pods) are read from global memory by the lane itself.
+__global__ __launch_bounds__(POD_WG) void pod_requests_kernel(
+    int64_t n_pods, int64_t n_cont, int64_t n_init, const int64_t* __restrict__ pod_ptr,
+    const uint64_t* __restrict__ cpu_req, const int64_t* __restrict__ mem_req,
+    const int64_t* __restrict__ init_ptr, const uint64_t* __restrict__ init_cpu,
+    const int64_t* __restrict__ init_mem, const uint8_t* __restrict__ restartable,
+    const uint64_t* __restrict__ ovh_cpu, const int64_t* __restrict__ ovh_mem,
+    uint64_t* __restrict__ pod_cpu, int64_t* __restrict__ pod_mem) {
+  const int64_t p0 = (int64_t)blockIdx.x * POD_WG;
+  const int64_t p = p0 + threadIdx.x;
+  const bool live = p < n_pods;
+  const bool has_init = init_ptr != nullptr;
+  // offsets clamped into the arrays: a malformed CSR gives wrong sums, never a fault
+  int64_t lo = 0, hi = 0, a = 0, b = 0;
+  uint64_t oc = 0, om = 0;
+  if (live) {
+    lo = pod_ptr[p];
+    hi = pod_ptr[p + 1];
+    clamp_range(lo, hi, n_cont);
+    if (has_init) {
+      a = init_ptr[p];
+      b = init_ptr[p + 1];
+      clamp_range(a, b, n_init);
+    }
+    oc = ovh_cpu ? ovh_cpu[p] : 0;
+    om = ovh_mem ? (uint64_t)ovh_mem[p] : 0;
+  }
+#if KCC_POD_LDS
+  __shared__ uint64_t s_c[POD_CAP_C], s_m[POD_CAP_C], s_ic[POD_CAP_I], s_im[POD_CAP_I];
+  __shared__ uint8_t s_rs[POD_CAP_I];
+  const int64_t pe = p0 + POD_WG < n_pods ? p0 + POD_WG : n_pods;
+  int64_t cb = pod_ptr[p0], ce = pod_ptr[pe];  // wave-uniform
+  clamp_range(cb, ce, n_cont);
+  const int64_t wc = ce - cb < POD_CAP_C ? ce - cb : POD_CAP_C;
+  int64_t ib = 0, ie = 0;
+  if (has_init) {
+    ib = init_ptr[p0];
+    ie = init_ptr[pe];
+    clamp_range(ib, ie, n_init);
+  }
+  const int64_t wi = ie - ib < POD_CAP_I ? ie - ib : POD_CAP_I;
+  for (int64_t i = threadIdx.x; i < wc; i += POD_WG) {
+    s_c[i] = cpu_req[cb + i];
+    s_m[i] = (uint64_t)mem_req[cb + i];
+  }
+  for (int64_t i = threadIdx.x; i < wi; i += POD_WG) {
+    s_ic[i] = init_cpu[ib + i];
+    s_im[i] = (uint64_t)init_mem[ib + i];
+    s_rs[i] = restartable ? restartable[ib + i] : 0;
+  }
+  __syncthreads();
+  if (!live) return;
+  uint64_t rc, rm;
+  pod_request(
+      lo, hi, a, b, has_init, oc, om,
+      [&](int64_t c, uint64_t& vc, uint64_t& vm) {
+        const int64_t j = c - cb;  // in [0, wc) unless past the cap (or a malformed CSR)
+        if (j >= 0 && j < wc) {
+          vc = s_c[j];
+          vm = s_m[j];
+        } else {
+          vc = cpu_req[c];
+          vm = (uint64_t)mem_req[c];
+        }
+      },
+      [&](int64_t k, uint64_t& vc, uint64_t& vm, bool& rs) {
+        const int64_t j = k - ib;
+        if (j >= 0 && j < wi) {
+          vc = s_ic[j];
+          vm = s_im[j];
+          rs = s_rs[j] != 0;
+        } else {
+          vc = init_cpu[k];
+          vm = (uint64_t)init_mem[k];
+          rs = restartable ? restartable[k] != 0 : false;
+        }
+      },
+      rc, rm);
+#else
+  if (!live) return;
+  uint64_t rc, rm;
+  pod_request(
+      lo, hi, a, b, has_init, oc, om,
+      [&](int64_t c, uint64_t& vc, uint64_t& vm) {
+        vc = cpu_req[c];
+        vm = (uint64_t)mem_req[c];
+      },
+      [&](int64_t k, uint64_t& vc, uint64_t& vm, bool& rs) {
+        vc = init_cpu[k];
+        vm = (uint64_t)init_mem[k];
+        rs = restartable ? restartable[k] != 0 : false;
+      },
+      rc, rm);
+#endif
   pod_cpu[p] = rc;
   pod_mem[p] = (int64_t)rm;
 }
@@ -111,9 +212,9 @@ hipError_t launch_pod_requests(int64_t n_pods, int64_t n_cont, int64_t n_init,
                                const int64_t* ovh_mem, uint64_t* pod_cpu, int64_t* pod_mem,
                                hipStream_t s) {
   if (n_pods <= 0) return hipSuccess;
-  const int64_t grid = (n_pods + 255) / 256;
+  const int64_t grid = (n_pods + POD_WG - 1) / POD_WG;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pod_requests_kernel, dim3((unsigned)grid), dim3(256), 0, s, n_pods, n_cont,
+  hipLaunchKernelGGL(pod_requests_kernel, dim3((unsigned)grid), dim3(POD_WG), 0, s, n_pods, n_cont,
                      n_init, pod_ptr, cpu_req, mem_req, init_ptr, init_cpu, init_mem, restartable,
                      ovh_cpu, ovh_mem, pod_cpu, pod_mem);
   return hipGetLastError();
