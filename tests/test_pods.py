@@ -186,3 +186,23 @@ def test_gpu_rejects_malformed_input(eng):
                          init_mem=[1, 1])
     with pytest.raises(ValueError):
         eng.pod_requests([0, 1], [1], [1], restartable=[1])
+
+
+@pytest.mark.gpu
+def test_gpu_device_api_matches_host_api(eng):
+    """kcc_pod_requests_async on device tensors (the bench's path) == the host entry."""
+    import torch
+    c = pods_case(10, n_nodes=3000, extremes=True)
+    dev = torch.device("cuda", 0)
+    t = {k: torch.from_numpy(v.view(np.int64) if v.dtype == np.uint64 else v).to(dev)
+         for k, v in c.items()}
+    P = c["pod_ptr"].size - 1
+    pc = torch.empty(P, dtype=torch.int64, device=dev)
+    pm = torch.empty(P, dtype=torch.int64, device=dev)
+    eng.pod_requests_async(t["pod_ptr"], t["cpu_req"], t["mem_req"], pc, pm, t["init_ptr"],
+                           t["init_cpu"], t["init_mem"], t["restartable"], t["ovh_cpu"],
+                           t["ovh_mem"])
+    torch.cuda.synchronize()
+    oc, om = coracle.pod_requests(**_pod_kw(c))
+    assert np.array_equal(pc.cpu().numpy().view(np.uint64), oc)
+    assert np.array_equal(pm.cpu().numpy(), om)
