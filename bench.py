@@ -424,6 +424,7 @@ def parse_leg(eng, cl, dev, stream, steps, warmup, with_cpu):
         "round_trip_exact": ok, "format_seconds": fmt_s,
     }
     del d_buf, d_off, d_out, d_st
+    res["quantity"] = quantity_leg(eng, cl, dev, stream, steps, warmup)
     if with_cpu:
         from oracle import coracle
         threads = min(16, os.cpu_count() or 1)
@@ -439,6 +440,50 @@ def parse_leg(eng, cl, dev, stream, steps, warmup, with_cpu):
             "match": bool(np.array_equal(ov, got) and (os_ == 1).all()),
         }
     return res
+
+
+def quantity_leg(eng, cl, dev, stream, steps, warmup):
+    """SURVEY §8f row 2, the memory side: every container's canonical memory request
+    string (Quantity.String()) -> Quantity.Value() (CC:285-286; apimachinery, parity
+    unpinned) on the device.  Algorithmic bytes per launch: (n+1) x 8
+    offsets + the characters in, n x 8 values + n x 1 status out."""
+    import torch
+
+    from kubernetesclustercapacity_amd import quantity
+
+    buf, off = quantity.memory_quantity_strings(cl.mem_req)
+    n = off.size - 1
+    d_buf = torch.from_numpy(buf).to(dev)
+    d_off = torch.from_numpy(off).to(dev)
+    d_out = torch.empty(n, dtype=torch.int64, device=dev)
+    d_st = torch.empty(n, dtype=torch.int8, device=dev)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(stream):
+        for _ in range(warmup):
+            eng.parse_quantity_async(d_buf, d_off, d_out, d_st, stream=stream)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        ev0.record(stream)
+        for _ in range(steps):
+            eng.parse_quantity_async(d_buf, d_off, d_out, d_st, stream=stream)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / steps
+    ok = bool((d_st.cpu().numpy() == 1).all() and np.array_equal(d_out.cpu().numpy(), cl.mem_req))
+    nbytes = int(off[-1])
+    alg = (n + 1) * 8 + nbytes + n * 9
+    gbs = alg / (ms * 1e-3) / 1e9
+    del d_buf, d_off, d_out, d_st
+    return {
+        "op": "Quantity.Value() (CC:285-286) over every container's memory request string",
+        "kernel": "parse_quantity_kernel", "strings": n, "chars": nbytes,
+        "ms_per_launch": ms, "strings_per_s": n / (ms * 1e-3),
+        "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": alg,
+                     "traffic": pmc_traffic("parse_quantity_kernel")[0],
+                     "traffic_source": pmc_traffic("parse_quantity_kernel")[1]},
+        "round_trip_exact": ok,
+    }
 
 
 def cpu_baseline(cl, sc, sm, gpu_totals, gpu_err, target_s):

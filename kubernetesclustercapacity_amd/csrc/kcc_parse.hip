@@ -585,6 +585,119 @@ __global__ __launch_bounds__(PS_THREADS) void parse_cpu_kernel(int64_t n, const 
   }
 }
 
+// '0'-padded to eight: the first d (1..8) characters of c (first in the low byte) as the
+// low-order digits of an eight-digit string, for swar8.
+__device__ __forceinline__ uint64_t pad_digits8(uint64_t c, int d) {
+  return d == 8 ? c : (c << (8 * (8 - d))) | (0x3030303030303030ull >> (8 * d));
+}
+
+// Quantity.Value() without LDS, as parse_cpu_kernel: one lane per string, strings of
+// <= 13 characters from one aligned 16-byte buffer load per lane, parsed in registers
+// when they are plain digits (<= 13, two swar8) and an optional integral suffix — k M G
+// T P E (10^3k) or Ki Mi Gi Ti Pi Ei (2^10k) — which covers every canonical memory
+// quantity of a container (Quantity.String() of a BinarySI or DecimalSI integer amount);
+// the value is capped at 2^63 - 1 exactly as quantity_value does.  Anything else (a sign,
+// a fraction, an exponent, m/u/n, a malformed string) takes quantity_value over global
+// memory, so the results are identical by construction.
+__global__ __launch_bounds__(PS_THREADS) void parse_quantity_kernel(int64_t n, const uint8_t* __restrict__ bytes,
+                                                                    int64_t n_bytes,
+                                                                    const int64_t* __restrict__ off,
+                                                                    int64_t* __restrict__ out,
+                                                                    int8_t* __restrict__ status) {
+  const uint64_t MAXV = 0x7fffffffffffffffull;
+  const int64_t b0 = (int64_t)blockIdx.x * PC_BLOCK;
+  const int64_t base = b0 + threadIdx.x;
+  const int64_t cnt = min((int64_t)PC_BLOCK, n - b0);
+  const int64_t lo_b = max(off[b0], (int64_t)0) & ~(int64_t)3;
+  const int64_t hi_b = min(off[b0 + cnt], n_bytes);
+  const bool span_ok = hi_b > lo_b && hi_b - lo_b < ((int64_t)1 << 31);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(bytes + (span_ok ? lo_b : 0)), (short)0, span_ok ? (int)(hi_b - lo_b) : 0,
+      0x00020000);
+  int64_t sb[PC_PER_THREAD], se[PC_PER_THREAD];
+  uint32_t w[PC_PER_THREAD][4];
+  bool fast[PC_PER_THREAD];
+#pragma unroll
+  for (int r = 0; r < PC_PER_THREAD; ++r) {
+    const int64_t i = min(base + r * PS_THREADS, n - 1);
+    sb[r] = off[i];
+    se[r] = off[i + 1];
+  }
+#pragma unroll
+  for (int r = 0; r < PC_PER_THREAD; ++r) {
+    const int64_t a = sb[r] & ~(int64_t)3;
+    const int64_t L = se[r] - sb[r];
+    fast[r] = span_ok && sb[r] >= lo_b && L >= 1 && L <= 13 && a + 16 <= hi_b;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 x = __builtin_bit_cast(
+        u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, fast[r] ? (int)(a - lo_b) : 0x7ffffff0, 0, 0));
+    w[r][0] = x.x;
+    w[r][1] = x.y;
+    w[r][2] = x.z;
+    w[r][3] = x.w;
+  }
+#pragma unroll
+  for (int r = 0; r < PC_PER_THREAD; ++r) {
+    const int64_t i = base + r * PS_THREADS;
+    if (i >= n) break;
+    int64_t v = 0;
+    int8_t st = PARSE_BADOFF;
+    bool done = false;
+    if (fast[r]) {
+      const int L = (int)(se[r] - sb[r]);
+      const int sh = (int)(sb[r] & 3) * 8;
+      unsigned __int128 X = ((unsigned __int128)(((uint64_t)w[r][3] << 32) | w[r][2]) << 64) |
+                            (((uint64_t)w[r][1] << 32) | w[r][0]);
+      X >>= sh;  // characters 0..12 (at least) from the low byte up
+      const uint64_t c = (uint64_t)X;
+      const uint32_t z = (uint32_t)(X >> (8 * (L - 1))) & 0xffu;                 // last
+      const uint32_t y = L >= 2 ? (uint32_t)(X >> (8 * (L - 2))) & 0xffu : 0u;  // second last
+      auto pre = [](uint32_t ch) {  // k M G T P E (also the Ki..Ei prefixes, with K for k)
+        return ch == 'k' || ch == 'M' || ch == 'G' || ch == 'T' || ch == 'P' || ch == 'E';
+      };
+      int sl = 0, bexp = 0, e10 = 0;
+      if (z == 'i' && (y == 'K' || (y != 'k' && pre(y)))) {
+        sl = 2;
+        bexp = y == 'K' ? 10 : y == 'M' ? 20 : y == 'G' ? 30 : y == 'T' ? 40 : y == 'P' ? 50 : 60;
+      } else if (pre(z)) {
+        sl = 1;
+        e10 = z == 'k' ? 3 : z == 'M' ? 6 : z == 'G' ? 9 : z == 'T' ? 12 : z == 'P' ? 15 : 18;
+      } else if (z - '0' > 9u) {
+        sl = -1;  // anything else: the general parser
+      }
+      const int d = L - sl;
+      if (sl >= 0 && d >= 1) {
+        uint64_t hiv = 0, lov = 0;
+        bool ok;
+        if (d <= 8) {
+          ok = swar8(pad_digits8(c, d), lov);
+        } else {
+          const int hd = d - 8;  // 1..5 leading digits, then eight
+          ok = swar8(pad_digits8(c, hd), hiv) && swar8((uint64_t)(X >> (8 * hd)), lov);
+        }
+        if (ok) {
+          const uint64_t D = hiv * 100000000ull + lov;  // < 10^13
+          uint64_t mag;
+          if (bexp) {
+            mag = D > (MAXV >> bexp) ? MAXV : D << bexp;
+          } else {
+            uint64_t m = 1;
+            for (int t = 0; t < e10; ++t) m *= 10u;  // <= 10^18
+            mag = D > MAXV / m ? MAXV : D * m;
+          }
+          v = (int64_t)mag;
+          st = PARSE_OK;
+          done = true;
+        }
+      }
+    }
+    if (!done && sb[r] >= 0 && se[r] >= sb[r] && se[r] <= n_bytes && se[r] - sb[r] < ((int64_t)1 << 31))
+      v = quantity_value(bytes + sb[r], (int)(se[r] - sb[r]), st);
+    out[i] = v;
+    status[i] = st;
+  }
+}
+
 }  // namespace
 
 int64_t parse_grid(int64_t n) { return (n + PS_BLOCK - 1) / PS_BLOCK; }
@@ -602,7 +715,7 @@ hipError_t launch_parse(int mode, int64_t n, const uint8_t* bytes, int64_t n_byt
     hipLaunchKernelGGL(parse_kernel<PARSE_MODE_BYTES>, dim3((unsigned)grid), dim3(PS_THREADS), 0, s,
                        n, bytes, n_bytes, offsets, out, status);
   else
-    hipLaunchKernelGGL(parse_kernel<PARSE_MODE_QUANTITY>, dim3((unsigned)grid), dim3(PS_THREADS), 0,
+    hipLaunchKernelGGL(parse_quantity_kernel, dim3((unsigned)parse_cpu_grid(n)), dim3(PS_THREADS), 0,
                        s, n, bytes, n_bytes, offsets, out, status);
   return hipGetLastError();
 }

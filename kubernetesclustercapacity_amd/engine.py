@@ -368,6 +368,11 @@ class CapacityEngine:
             self._h, off.numel() - 1, _dp(buf), buf.numel(), _dp(off), _dp(out), _dp(status),
             _stream(stream)))
 
+    def parse_quantity_async(self, buf, off, out, status, stream=None):
+        self._check(self._lib.kcc_parse_quantity_async(
+            self._h, off.numel() - 1, _dp(buf), buf.numel(), _dp(off), _dp(out), _dp(status),
+            _stream(stream)))
+
     def profile_enable(self, on: bool = True):
         self._check(self._lib.kcc_profile_enable(self._h, 1 if on else 0))
 

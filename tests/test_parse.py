@@ -338,3 +338,33 @@ def test_gpu_quantity_value(eng):
             continue
         assert (int(v), int(st)) == qm.value(s), s
     assert unsupported < 0.1 * len(strs)  # the corpus is rich in 20+ digit binary fractions
+
+
+def qty_fast_corpus():
+    """The register fast path of parse_quantity_kernel: 1-14 plain digits (leading zeros
+    included) with no suffix or an integral one, at every byte alignment, the 2^63 - 1 cap
+    boundaries, and near-misses that must fall back to the general parser."""
+    rng = np.random.default_rng(23)
+    sufs = ["", "k", "M", "G", "T", "P", "E", "Ki", "Mi", "Gi", "Ti", "Pi", "Ei"]
+    out = []
+    for d in range(1, 15):
+        for s in sufs:
+            for _ in range(6):
+                digs = "".join(str(int(x)) for x in rng.integers(0, 10, d))
+                out.append(digs + s)
+            out.append("9" * d + s)
+            out.append("0" * d + s)
+    out += ["7Ei", "8Ei", "8191Pi", "8192Pi", "9223372036854", "9223372036854k",
+            "9223372E", "9223373T", "1K", "1ki", "1Ei0", "Ki", "k", "1.5Gi", "+1Gi", "-1Gi",
+            "1e3", "1m", "1 ", " 1", "1Kib", "12345678901234"]
+    return out
+
+
+@pytest.mark.gpu
+def test_gpu_quantity_fast_path(eng):
+    strs = qty_fast_corpus()
+    for shift in range(4):  # every start alignment of the first string
+        batch = ["x" * shift] + strs
+        gv, gs = eng.quantity_value(batch)
+        for s, v, st in zip(batch[1:], gv[1:], gs[1:]):
+            assert (int(v), int(st)) == qm.value(s), (shift, s)
