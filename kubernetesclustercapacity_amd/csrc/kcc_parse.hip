@@ -585,6 +585,18 @@ __global__ __launch_bounds__(PS_THREADS) void parse_cpu_kernel(int64_t n, const 
   }
 }
 
+// The general parser for the strings the register path does not take, out of line (one
+// copy instead of one per unrolled string; the result comes back in registers).
+struct QtyResult {
+  int64_t v;
+  int32_t st;
+};
+__device__ __noinline__ QtyResult quantity_value_global(const uint8_t* s, int n) {
+  int8_t st;
+  const int64_t v = quantity_value(s, n, st);
+  return QtyResult{v, st};
+}
+
 // '0'-padded to eight: the first d (1..8) characters of c (first in the low byte) as the
 // low-order digits of an eight-digit string, for swar8.
 __device__ __forceinline__ uint64_t pad_digits8(uint64_t c, int d) {
@@ -655,44 +667,52 @@ __global__ __launch_bounds__(PS_THREADS) void parse_quantity_kernel(int64_t n, c
       auto pre = [](uint32_t ch) {  // k M G T P E (also the Ki..Ei prefixes, with K for k)
         return ch == 'k' || ch == 'M' || ch == 'G' || ch == 'T' || ch == 'P' || ch == 'E';
       };
-      int sl = 0, bexp = 0, e10 = 0;
+      // suffix -> multiplier: a shift (binary) or 10^3k with its overflow threshold
+      // (2^63 - 1) / 10^3k as constants (no 64-bit division in the loop)
+      int sl = 0, bexp = 0;
+      uint64_t m10 = 1, lim10 = MAXV;
       if (z == 'i' && (y == 'K' || (y != 'k' && pre(y)))) {
         sl = 2;
         bexp = y == 'K' ? 10 : y == 'M' ? 20 : y == 'G' ? 30 : y == 'T' ? 40 : y == 'P' ? 50 : 60;
       } else if (pre(z)) {
         sl = 1;
-        e10 = z == 'k' ? 3 : z == 'M' ? 6 : z == 'G' ? 9 : z == 'T' ? 12 : z == 'P' ? 15 : 18;
+        m10 = z == 'k' ? 1000ull : z == 'M' ? 1000000ull : z == 'G' ? 1000000000ull
+            : z == 'T' ? 1000000000000ull : z == 'P' ? 1000000000000000ull : 1000000000000000000ull;
+        lim10 = MAXV / 1000000000000000000ull;  // 'E'
+        lim10 = z == 'k' ? MAXV / 1000ull : z == 'M' ? MAXV / 1000000ull
+              : z == 'G' ? MAXV / 1000000000ull : z == 'T' ? MAXV / 1000000000000ull
+              : z == 'P' ? MAXV / 1000000000000000ull : lim10;
       } else if (z - '0' > 9u) {
         sl = -1;  // anything else: the general parser
       }
       const int d = L - sl;
       if (sl >= 0 && d >= 1) {
+        // branch-free over the wave: the digits right-aligned in sixteen, '0'-padded —
+        // the last eight (or all d <= 8) and the 1..5 before them (or eight zeros)
         uint64_t hiv = 0, lov = 0;
-        bool ok;
-        if (d <= 8) {
-          ok = swar8(pad_digits8(c, d), lov);
-        } else {
-          const int hd = d - 8;  // 1..5 leading digits, then eight
-          ok = swar8(pad_digits8(c, hd), hiv) && swar8((uint64_t)(X >> (8 * hd)), lov);
-        }
+        const int hd = d > 8 ? d - 8 : 0;
+        const uint64_t lo8 = d > 8 ? (uint64_t)(X >> (8 * hd)) : pad_digits8(c, d);
+        const uint64_t hi8 = d > 8 ? pad_digits8(c, hd) : 0x3030303030303030ull;
+        const bool okh = swar8(hi8, hiv), okl = swar8(lo8, lov);
+        const bool ok = okh && okl;
         if (ok) {
           const uint64_t D = hiv * 100000000ull + lov;  // < 10^13
           uint64_t mag;
-          if (bexp) {
+          if (bexp)
             mag = D > (MAXV >> bexp) ? MAXV : D << bexp;
-          } else {
-            uint64_t m = 1;
-            for (int t = 0; t < e10; ++t) m *= 10u;  // <= 10^18
-            mag = D > MAXV / m ? MAXV : D * m;
-          }
+          else
+            mag = D > lim10 ? MAXV : D * m10;
           v = (int64_t)mag;
           st = PARSE_OK;
           done = true;
         }
       }
     }
-    if (!done && sb[r] >= 0 && se[r] >= sb[r] && se[r] <= n_bytes && se[r] - sb[r] < ((int64_t)1 << 31))
-      v = quantity_value(bytes + sb[r], (int)(se[r] - sb[r]), st);
+    if (!done && sb[r] >= 0 && se[r] >= sb[r] && se[r] <= n_bytes && se[r] - sb[r] < ((int64_t)1 << 31)) {
+      const QtyResult q = quantity_value_global(bytes + sb[r], (int)(se[r] - sb[r]));
+      v = q.v;
+      st = (int8_t)q.st;
+    }
     out[i] = v;
     status[i] = st;
   }
