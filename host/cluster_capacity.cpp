@@ -37,7 +37,7 @@ struct Flags {
       {"kubeconfig", ""},         {"cluster", ""},          {"cpuRequests", "100m"},
       {"cpuLimits", "200m"},      {"memRequests", "100mb"}, {"memLimits", "200mb"},
       {"replicas", "1"},          {"specs", ""},            {"device", "0"},
-      {"gpus", "1"},              {"v", "false"}};
+      {"gpus", "1"},              {"v", "false"},           {"schedulerRequests", "false"}};
 };
 
 // Go flag package syntax: -name=value, -name value, --name=value; bool -v.
@@ -61,7 +61,7 @@ bool parseFlags(int argc, char** argv, Flags& f) {
       std::fprintf(stderr, "flag provided but not defined: -%s\n", name.c_str());
       return false;
     }
-    if (name == "v" && !has) {
+    if ((name == "v" || name == "schedulerRequests") && !has) {
       val = "true";
     } else if (!has) {
       if (i + 1 >= argc) {
@@ -130,6 +130,9 @@ int main(int argc, char** argv) {
   Flags f;
   if (!parseFlags(argc, argv, f)) return 2;
   const bool verbose = f.v["v"] == "true";
+  // opt-in (NOT the reference's semantics): pod requests as the
+  // scheduler counts them — init containers, sidecars, overhead
+  const bool schedReq = f.v["schedulerRequests"] == "true";
 
   Spec one{f.v["cpuRequests"], f.v["memRequests"], f.v["replicas"]};
   const uint64_t cpuLimits = convertCPUToMilis(f.v["cpuLimits"]);            // CC:65
@@ -186,6 +189,23 @@ int main(int argc, char** argv) {
   if (rc) return fail(ctx, rc);
   const int64_t n = (int64_t)rows.size(), nc = (int64_t)in.cpu_req.size();
 
+  // -schedulerRequests: the per-node request sums of the opt-in model, fed to the fit
+  std::vector<uint64_t> suc;
+  std::vector<int64_t> sum_;
+  if (schedReq) {
+    suc.resize((size_t)n);
+    sum_.resize((size_t)n);
+    const int64_t np = (int64_t)in.ovh_cpu.size(), ni = (int64_t)in.init_mem.size();
+    rc = kcc_reduce_requests_pods(ctx, n, np, nc, ni, in.node_pod_ptr.data(), in.pod_ptr.data(),
+                                  in.cpu_req.data(), in.mem_req.data(), in.init_ptr.data(),
+                                  ni ? in.init_cpu.data() : nullptr,
+                                  ni ? in.init_mem.data() : nullptr,
+                                  ni ? in.init_rst.data() : nullptr,
+                                  np ? in.ovh_cpu.data() : nullptr,
+                                  np ? in.ovh_mem.data() : nullptr, suc.data(), sum_.data());
+    if (rc) return fail(ctx, rc);
+  }
+
   if (verbose) {  // CC:107-117, 137 — per-node sums and fit, one row at a time
     std::vector<uint64_t> uc(n), lc(n);
     std::vector<int64_t> um(n), lm(n);
@@ -193,6 +213,10 @@ int main(int argc, char** argv) {
                              in.cpu_lim.data(), in.mem_lim.data(), uc.data(), um.data(), lc.data(),
                              lm.data());
     if (rc) return fail(ctx, rc);
+    if (schedReq) {
+      uc = suc;
+      um = sum_;
+    }
     // every row's "Max replicas" (CC:137) for the first spec in one device call
     std::vector<int64_t> qs(n);
     std::vector<int32_t> es(n);
@@ -231,10 +255,15 @@ int main(int argc, char** argv) {
     sc[s] = specs[s].cpu;
     sm[s] = specs[s].mem;
   }
-  rc = kcc_capacity(ctx, n, nc, in.node_ptr.data(), in.cpu_req.data(), in.mem_req.data(),
-                    in.alloc_cpu.data(), in.alloc_mem.data(), in.alloc_pods.data(),
-                    in.pod_count.data(), (int64_t)specs.size(), sc.data(), sm.data(), totals.data(),
-                    serr.data());
+  if (schedReq)
+    rc = kcc_fit(ctx, n, in.alloc_cpu.data(), in.alloc_mem.data(), in.alloc_pods.data(),
+                 in.pod_count.data(), suc.data(), sum_.data(), (int64_t)specs.size(), sc.data(),
+                 sm.data(), totals.data(), serr.data());
+  else
+    rc = kcc_capacity(ctx, n, nc, in.node_ptr.data(), in.cpu_req.data(), in.mem_req.data(),
+                      in.alloc_cpu.data(), in.alloc_mem.data(), in.alloc_pods.data(),
+                      in.pod_count.data(), (int64_t)specs.size(), sc.data(), sm.data(),
+                      totals.data(), serr.data());
   if (rc) return fail(ctx, rc);
   kcc_destroy(ctx);
 

@@ -133,6 +133,19 @@ bool loadCluster(const std::string& path, Cluster& out, std::string& err) {
       if (!(is >> c.cpuRequest >> c.cpuLimit >> c.memRequest >> c.memLimit))
         return bad("container <cpuReq> <cpuLim> <memReqBytes> <memLimBytes>");
       out.pods.back().containers.push_back(c);
+    } else if (kind == "initcontainer") {
+      if (out.pods.empty()) return bad("initcontainer before any pod");
+      Container c;
+      c.init = true;
+      if (!(is >> c.cpuRequest >> c.cpuLimit >> c.memRequest >> c.memLimit))
+        return bad("initcontainer <cpuReq> <cpuLim> <memReqBytes> <memLimBytes> [always]");
+      std::string pol;
+      if (is >> pol) c.restartable = pol == "always";
+      out.pods.back().containers.push_back(c);
+    } else if (kind == "overhead") {
+      if (out.pods.empty()) return bad("overhead before any pod");
+      if (!(is >> out.pods.back().overheadCPU >> out.pods.back().overheadMem))
+        return bad("overhead <cpuMillis> <memBytes>");
     } else {
       return bad("unknown record");
     }
@@ -243,13 +256,15 @@ int buildInputs(kcc_ctx* ctx, const Cluster& c, const std::vector<node>& rows, E
   // gets the pods whose nodeName is "", like the reference's per-row List
   const std::map<std::string, std::vector<size_t>> by_node = nonTerminatedPodsByNode(c);
   const std::vector<size_t> none;
+  std::vector<const std::string*> init_cpu_str;  // after the app strings: same error order
   for (const node& r : rows) {  // CC:105: every row, zero rows included (name "")
     const auto it = by_node.find(r.name);
     const std::vector<size_t>& pods = it == by_node.end() ? none : it->second;
     for (size_t pi : pods) {
       const Pod& p = c.pods[pi];
       if (p.getFails) continue;  // NotFound: skipped by the sum (CC:267-268), still counted
-      for (const Container& ct : p.containers) {  // CC:277-293
+      for (const Container& ct : p.containers) {  // CC:277-293 (app containers only)
+        if (ct.init) continue;
         chars += ct.cpuLimit;
         off.push_back((int64_t)chars.size());
         chars += ct.cpuRequest;
@@ -257,8 +272,19 @@ int buildInputs(kcc_ctx* ctx, const Cluster& c, const std::vector<node>& rows, E
         in.mem_req.push_back(ct.memRequest);
         in.mem_lim.push_back(ct.memLimit);
       }
+      for (const Container& ct : p.containers) {  // opt-in model: init containers
+        if (!ct.init) continue;
+        init_cpu_str.push_back(&ct.cpuRequest);
+        in.init_mem.push_back(ct.memRequest);
+        in.init_rst.push_back(ct.restartable ? 1 : 0);
+      }
+      in.pod_ptr.push_back((int64_t)in.mem_req.size());
+      in.init_ptr.push_back((int64_t)in.init_mem.size());
+      in.ovh_cpu.push_back(p.overheadCPU);
+      in.ovh_mem.push_back(p.overheadMem);
     }
     in.node_ptr.push_back((int64_t)in.mem_req.size());
+    in.node_pod_ptr.push_back((int64_t)in.ovh_cpu.size());
     in.alloc_cpu.push_back(r.allocatableCPU);
     in.alloc_mem.push_back(r.allocatableMemory);
     in.alloc_pods.push_back(r.allocatablePods);
@@ -282,6 +308,24 @@ int buildInputs(kcc_ctx* ctx, const Cluster& c, const std::vector<node>& rows, E
       std::printf("\nError converting string to int for %s\n", s.c_str());
     }
     (k & 1 ? in.cpu_req : in.cpu_lim)[(size_t)k / 2] = millis[k];
+  }
+  if (!init_cpu_str.empty()) {  // opt-in model only; the reference never reads them
+    std::string ichars;
+    std::vector<int64_t> ioff;
+    pack(init_cpu_str, ichars, ioff);
+    const int64_t ni = (int64_t)init_cpu_str.size();
+    in.init_cpu.resize((size_t)ni);
+    std::vector<int8_t> ist((size_t)ni);
+    const int rc = kcc_parse_cpu_millis(ctx, ni, ichars.data(), ioff[ni], ioff.data(),
+                                        in.init_cpu.data(), ist.data());
+    if (rc) return rc;
+    for (int64_t k = 0; k < ni; ++k)
+      if (ist[k] != KCC_PARSE_OK) {  // as convertCPUToMilis reports it (CC:315-316)
+        std::string s = *init_cpu_str[(size_t)k];
+        if (!s.empty() && s.back() == 'm') s.pop_back();
+        std::printf("\nError converting string to int for %s\n", s.c_str());
+        in.init_cpu[(size_t)k] = 0;
+      }
   }
   return KCC_OK;
 }

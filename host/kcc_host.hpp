@@ -40,12 +40,15 @@ struct node {
 struct Container {
   std::string cpuRequest = "0", cpuLimit = "0";  // Quantity.String() (canonical)
   int64_t memRequest = 0, memLimit = 0;          // Quantity.Value()
+  bool init = false, restartable = false;        // an init container (restartPolicy Always)
 };
 
 struct Pod {
   std::string nodeName, ns, name, phase;
   std::vector<Container> containers;
   bool getFails = false;  // the per-pod Get of CC:264 returns NotFound (CC:267-271)
+  uint64_t overheadCPU = 0;  // spec.overhead (millicores, bytes): opt-in model only
+  int64_t overheadMem = 0;
 };
 
 struct NodeObj {
@@ -63,6 +66,10 @@ struct Cluster {
 //   node <name> <cpu> <memory> <pods> <cond0> <cond1> <cond2> <cond3>
 //   pod <nodeName|-> <namespace> <name> <phase> [missing]
 //   container <cpuRequest> <cpuLimit> <memRequestBytes> <memLimitBytes>   (of the last pod)
+//   initcontainer <cpuRequest> <cpuLimit> <memRequestBytes> <memLimitBytes> [always]
+//   overhead <cpuMillis> <memBytes>                                         (of the last pod)
+// (init containers and overhead are read only by -schedulerRequests; the
+// reference's sums ignore them, CC:277.)
 // "-" as nodeName means "" (an unscheduled pod).  Returns false with a message on error.
 bool loadCluster(const std::string& path, Cluster& out, std::string& err);
 
@@ -88,6 +95,11 @@ struct EngineInputs {
   std::vector<int64_t> mem_req, mem_lim;
   std::vector<uint64_t> alloc_cpu;
   std::vector<int64_t> alloc_mem, alloc_pods, pod_count;
+  // opt-in scheduler request model: the summed pods in CSR form
+  std::vector<int64_t> node_pod_ptr{0}, pod_ptr{0}, init_ptr{0};
+  std::vector<uint64_t> init_cpu, ovh_cpu;
+  std::vector<int64_t> init_mem, ovh_mem;
+  std::vector<uint8_t> init_rst;
 };
 // The container cpu strings (limits and requests, CC:279-283) are converted on the device
 // in one kcc_parse_cpu_millis batch on `ctx`; each failed string prints

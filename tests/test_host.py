@@ -258,3 +258,37 @@ def test_cli_node_strings_on_device_keep_print_order(cli, tmp_path):
     assert lines == ["Error converting string to int for 2k", "Skipping node n1 as it is not healthy",
                      "Error converting string to int for 0.5", "Skipping node n3 as it is not healthy"]
     assert "{n0 0 16723480576 110}" in r.stdout and "{n2 500 0 110}" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cli_scheduler_requests_opt_in(cli, tmp_path):
+    """-schedulerRequests (NOT the reference's semantics): init
+    containers, sidecars and pod overhead count toward a node's requests; without the
+    flag they are ignored, as by the reference (CC:277 walks Spec.Containers only)."""
+    lines = [
+        "node n0 64 65840760Ki 110 False False False False",   # 64000 m, 67420938240 B
+        "pod n0 ns a Running",
+        "container 500m 500m 1073741824 0",
+        "initcontainer 2 2 2147483648 0",                       # init max: 2000 m, 2 GiB
+        "pod n0 ns b Running",
+        "container 250m 250m 536870912 0",
+        "initcontainer 100m 100m 104857600 0 always",           # sidecar: adds to the app sum
+        "overhead 50 10485760",
+    ]
+    path = tmp_path / "c.txt"
+    path.write_text("\n".join(lines) + "\n")
+    # pod a: max(500, 2000) = 2000 m, max(1 GiB, 2 GiB) = 2 GiB
+    # pod b: 250 + 100 + 50 = 400 m, 512 MiB + 100 MiB + 10 MiB
+    want_c = [(500, 1 << 30), (250, 512 << 20)]                 # reference sums
+    sched = pyoracle.pod_requests([0, 1, 2], [500, 250], [1 << 30, 512 << 20], [0, 1, 2],
+                                  [2000, 100], [2 << 30, 100 << 20], [0, 1], [0, 50],
+                                  [0, 10 << 20])
+    assert sched == [(2000, 2 << 30), (400, (512 + 110) << 20)]
+    node = [[64000], [67420938240], [110], [2]]
+    for flag, used in (([], want_c), (["-schedulerRequests"], sched)):
+        uc = [sum(c for c, _ in used)]
+        um = [sum(m for _, m in used)]
+        t, e = pyoracle.fit(*node[:3], node[3], uc, um, [200], [262_144_000])
+        r = _run(["-cluster", str(path), "-cpuRequests=200m", "-memRequests=250mb"] + flag)
+        assert r.returncode == 0, r.stderr
+        assert f"Total possible replicas for the pod with required input specs : {t[0]}" in r.stdout, flag
