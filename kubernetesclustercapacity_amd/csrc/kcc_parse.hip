@@ -617,6 +617,14 @@ __global__ __launch_bounds__(PS_THREADS) void parse_quantity_kernel(int64_t n, c
                                                                     int64_t* __restrict__ out,
                                                                     int8_t* __restrict__ status) {
   const uint64_t MAXV = 0x7fffffffffffffffull;
+  __shared__ uint64_t s_p10[8], s_lim[8];  // 10^3k and (2^63 - 1) / 10^3k, k = 0..6
+  if (threadIdx.x < 8) {
+    uint64_t p = 1;
+    for (unsigned k = 0; k < threadIdx.x && k < 6; ++k) p *= 1000u;
+    s_p10[threadIdx.x] = p;
+    s_lim[threadIdx.x] = MAXV / p;
+  }
+  __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * PC_BLOCK;
   const int64_t base = b0 + threadIdx.x;
   const int64_t cnt = min((int64_t)PC_BLOCK, n - b0);
@@ -664,24 +672,26 @@ __global__ __launch_bounds__(PS_THREADS) void parse_quantity_kernel(int64_t n, c
       const uint64_t c = (uint64_t)X;
       const uint32_t z = (uint32_t)(X >> (8 * (L - 1))) & 0xffu;                 // last
       const uint32_t y = L >= 2 ? (uint32_t)(X >> (8 * (L - 2))) & 0xffu : 0u;  // second last
-      auto pre = [](uint32_t ch) {  // k M G T P E (also the Ki..Ei prefixes, with K for k)
-        return ch == 'k' || ch == 'M' || ch == 'G' || ch == 'T' || ch == 'P' || ch == 'E';
+      // suffix decode by table: 3-bit index per character 'E'..'Y' (offset ch - 'E' <=
+      // 20) — E 6, G 3, K 1, M 2, P 5, T 4 — then 10^3k and its overflow threshold from
+      // two LDS tables (no compare chains)
+      constexpr uint64_t SFX = (6ull << 0) | (3ull << 6) | (1ull << 18) | (2ull << 24) |
+                               (5ull << 33) | (4ull << 45);
+      auto sfx = [](uint32_t ch) -> uint32_t {
+        const uint32_t o = ch - 'E';
+        return o <= 20u ? (uint32_t)(SFX >> (3u * o)) & 7u : 0u;
       };
-      // suffix -> multiplier: a shift (binary) or 10^3k with its overflow threshold
-      // (2^63 - 1) / 10^3k as constants (no 64-bit division in the loop)
+      const uint32_t yb = sfx(y);                                    // Ki..Ei ('k' -> 0)
+      const uint32_t zd = z == 'k' ? 1u : (z == 'K' ? 0u : sfx(z));  // k M G T P E
       int sl = 0, bexp = 0;
       uint64_t m10 = 1, lim10 = MAXV;
-      if (z == 'i' && (y == 'K' || (y != 'k' && pre(y)))) {
+      if (z == 'i' && yb) {
         sl = 2;
-        bexp = y == 'K' ? 10 : y == 'M' ? 20 : y == 'G' ? 30 : y == 'T' ? 40 : y == 'P' ? 50 : 60;
-      } else if (pre(z)) {
+        bexp = 10 * (int)yb;
+      } else if (zd) {
         sl = 1;
-        m10 = z == 'k' ? 1000ull : z == 'M' ? 1000000ull : z == 'G' ? 1000000000ull
-            : z == 'T' ? 1000000000000ull : z == 'P' ? 1000000000000000ull : 1000000000000000000ull;
-        lim10 = MAXV / 1000000000000000000ull;  // 'E'
-        lim10 = z == 'k' ? MAXV / 1000ull : z == 'M' ? MAXV / 1000000ull
-              : z == 'G' ? MAXV / 1000000000ull : z == 'T' ? MAXV / 1000000000000ull
-              : z == 'P' ? MAXV / 1000000000000000ull : lim10;
+        m10 = s_p10[zd];
+        lim10 = s_lim[zd];
       } else if (z - '0' > 9u) {
         sl = -1;  // anything else: the general parser
       }
