@@ -8,11 +8,14 @@ Inputs are resident in HBM before the timed region; value = nodes x specs of the
 whole job / step time (max over ranks).
 
 Default workload = BASELINE config C4 (1M nodes, ~20M pods / ~40M containers, 4096
-specs), which fits one MI355X.  --gpus N (one process per GPU, torch.distributed.run):
-the cluster is partitioned by nodes; by default each rank owns one C4-sized partition
-of an N x 1M-node cluster (weak scaling: N=1 is exactly C4) and the only exchange is
-the RCCL all-reduce of the per-spec partials.  --scaling strong shards the same 1M
-nodes over the N ranks instead.
+specs), which fits one MI355X.  --gpus N: one process per GPU; the SAME 1M-node
+cluster is split into N contiguous node ranges (strong scaling, BASELINE configs[3]:
+"1M nodes x 20M pods, 4096 specs, nodes sharded over 2/4/8 MI355X") and the only
+exchange is the RCCL all-reduce of the per-spec partials, issued by libkcc on the
+kernels' own stream (kcc_allreduce_partial_async).  Launched without torchrun
+(`python bench.py --gpus N`), the script re-launches itself under
+torch.distributed.run with N ranks before anything touches the GPU.  --scaling weak
+(one C4-sized partition per rank, an N x 1M-node cluster) is a secondary mode.
 """
 from __future__ import annotations
 
@@ -56,8 +59,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C4", choices=["C2", "C3", "C4", "C5"])
-    ap.add_argument("--scaling", default="weak", choices=["strong", "weak"],
-                    help="weak: a C4-sized node partition per rank; strong: C4 split over ranks")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong (default): the config's cluster split over the ranks; "
+                         "weak: a config-sized node partition per rank")
+    ap.add_argument("--exchange", default="kcc", choices=["kcc", "torch"],
+                    help="N > 1: all-reduce of the partials by libkcc's own RCCL communicator "
+                         "on the kernel stream (kcc), or torch.distributed.all_reduce (torch)")
     ap.add_argument("--chunks", type=int, default=1,
                     help="node chunks of the pipelined step (reduce of chunk k overlaps the fit "
                          "of chunk k-1); 1 = reduce, then fit")
@@ -75,26 +82,79 @@ def parse():
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="diagnostic: run only rank 0's node shard of a world of this size "
                          "(no all-reduce) to estimate per-rank step time at N GPUs")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: start the ranks, exchange one gloo "
+                         "all-reduce, print the rank count (no measurement)")
     return ap.parse_args()
+
+
+def relaunch(args) -> int:
+    """`python bench.py --gpus N` (N > 1) outside torchrun: run the N ranks under
+    torch.distributed.run as a CHILD process and return its exit code.  This process
+    never initialises the GPU (no exec from a GPU-initialised process)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def dry_run(args, rank, world):
+    """The launcher path without a GPU: every rank joins a gloo group and all-reduces
+    its rank id; rank 0 reports how many ranks answered."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.tensor([1, rank], dtype=torch.int64)
+        dist.all_reduce(t)
+        seen, rank_sum = int(t[0]), int(t[1])
+        dist.destroy_process_group()
+    else:
+        seen, rank_sum = 1, 0
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": seen, "gpus_requested": args.gpus,
+                          "rank_sum": rank_sum, "scaling": args.scaling, "config": args.config}))
+    return 0 if seen == args.gpus else 2
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(args))
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but {world} rank(s) were launched (WORLD_SIZE): "
+              "refusing to report a line for a different GPU count", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        sys.exit(dry_run(args, rank, world))
+
     import torch
     import torch.distributed as dist
 
     from kubernetesclustercapacity_amd import CapacityEngine, synth
     from kubernetesclustercapacity_amd.shard import node_range
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and rank == 0:
-        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: running {world} rank(s)",
-              file=sys.stderr)
-    local = local % max(torch.cuda.device_count(), 1)  # rehearsal: several ranks, one GPU
+    n_dev = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if args.dist_backend == "nccl" and world > 1 and n_dev < int(os.environ.get(
+            "LOCAL_WORLD_SIZE", world)):
+        print(f"[bench] {world} ranks but {n_dev} visible GPU(s): RCCL needs one GPU per rank "
+              "(use --dist-backend gloo only to rehearse ranks sharing a GPU)", file=sys.stderr)
+        sys.exit(2)
+    local = local % max(n_dev, 1)  # gloo rehearsal: several ranks, one GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    exchange = args.exchange if args.dist_backend == "nccl" else "torch"
     if world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -127,16 +187,33 @@ def main():
     eng = CapacityEngine(local, 1)
     eng.reserve(n, C, S)
     stream = torch.cuda.Stream(dev)
+    exchange_note = None
+    if world > 1 and exchange == "kcc":
+        # libkcc's own RCCL communicator: rank 0's id travels over the process group
+        try:
+            obj = [CapacityEngine.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            eng.comm_init(obj[0], world, rank)
+        except Exception as e:  # noqa: BLE001 - every rank falls back the same way below
+            exchange_note = f"kcc communicator failed ({e}); torch.distributed all-reduce used"
+        ok = torch.tensor([0 if exchange_note else 1], dtype=torch.int64, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            exchange = "torch"
+            exchange_note = exchange_note or "a peer's kcc communicator failed; torch all-reduce used"
 
     h_ptr = np.ascontiguousarray(cl.node_ptr, np.int64)
 
     def step():
-        # reduce (side stream, node chunk k) overlapped with the fit of chunk k-1
+        # reduce -> spec setup -> node prep -> fit -> clamp correction, one stream
         eng.capacity_partial_async(h_ptr, ptr, cpu, mem, a_cpu, a_mem, a_pods, p_cnt, used_cpu,
                                    used_mem, s_cpu, s_mem, partial, n_chunks=args.chunks,
                                    stream=stream)
         if world > 1:
-            dist.all_reduce(partial, op=dist.ReduceOp.SUM)
+            if exchange == "kcc":  # RCCL on the same stream: no cross-stream event
+                eng.allreduce_partial_async(S, partial, stream=stream)
+            else:
+                dist.all_reduce(partial, op=dist.ReduceOp.SUM)
         eng.fit_finalize_async(S, partial, totals, err, stream=stream)
 
     with torch.cuda.stream(stream):
@@ -199,8 +276,17 @@ def main():
             "workload": f"{args.config}: {n_total} nodes x {pods_total} pods x {S} specs; "
                         "reduce + fit prepare + fit + finalize"
                         + (" + RCCL all-reduce" if world > 1 else ""),
-            "nodes": n_total, "pods": pods_total, "containers_rank0": C, "specs": S,
-            "parallelism": f"node-sharded x{world}",
+            "nodes": n_total, "pods": pods_total, "containers_rank0": C, "nodes_rank0": n,
+            "specs": S, "parallelism": f"node-sharded x{world}",
+        },
+        "world": {
+            "ranks": world, "process_group_size": dist.get_world_size() if world > 1 else 1,
+            "backend": args.dist_backend if world > 1 else None,
+            "exchange": (("libkcc RCCL (kcc_allreduce_partial_async, kernel stream)"
+                          if exchange == "kcc" else f"torch.distributed.all_reduce ({args.dist_backend})")
+                         if world > 1 else None),
+            "exchange_note": exchange_note,
+            "visible_gpus": n_dev,
         },
         "roofline": {
             "bound": "hbm", "kernel": "fit_kernel", "achieved": fit_gbs, "peak": HBM_PEAK_GBS,
@@ -238,6 +324,9 @@ def main():
     out["totals_checksum"] = int(((tot_np * np.uint64(0x9E3779B97F4A7C15)) ^ (tot_np >> np.uint64(29)))
                                  .sum(dtype=np.uint64))
     out["spec_errors"] = int(err.cpu().numpy().sum())
+    if rank == 0 and world == 1 and args.emulate_world <= 1:
+        out["h2d"] = h2d_leg([cl.node_ptr, cl.cpu_req, cl.mem_req, cl.alloc_cpu, cl.alloc_mem,
+                              cl.alloc_pods, cl.pod_count, sc, sm], dev, ms_step, n_total * S)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cl, sc, sm, totals.cpu().numpy(), err.cpu().numpy(),
                                            args.cpu_seconds)
@@ -427,7 +516,7 @@ def parse_leg(eng, cl, dev, stream, steps, warmup, with_cpu):
     res["quantity"] = quantity_leg(eng, cl, dev, stream, steps, warmup)
     if with_cpu:
         from oracle import coracle
-        threads = min(16, os.cpu_count() or 1)
+        threads = host_cpus()["threads"]
         t0 = time.perf_counter()
         ov, os_ = coracle.parse_cpu_millis(buf, off, 1)
         t1 = time.perf_counter()
@@ -493,7 +582,8 @@ def cpu_baseline(cl, sc, sm, gpu_totals, gpu_err, target_s):
     totals for the sampled specs are also compared with the GPU's."""
     from oracle import coracle
 
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    host = host_cpus()
+    threads = host["threads"]
     t = time.perf_counter()
     uc, um, _, _ = coracle.reduce_requests(cl.node_ptr, cl.cpu_req, cl.mem_req)
     t_red = time.perf_counter() - t
@@ -508,16 +598,78 @@ def cpu_baseline(cl, sc, sm, gpu_totals, gpu_err, target_s):
     ot, oe = coracle.fit(*args, sc[:k], sm[:k], threads)
     t_fit = time.perf_counter() - t
     step_s = t_red + t_fit * sc.size / k
+    # one thread, like the reference's single goroutine (CC:105): a smaller spec sample
+    k1 = int(min(sc.size, max(2, target_s / 3 / max(per_spec * threads, 1e-9))))
+    t = time.perf_counter()
+    o1, e1 = coracle.fit(*args, sc[:k1], sm[:k1], 1)
+    t_fit1 = time.perf_counter() - t
+    step1_s = t_red + t_fit1 * sc.size / k1
     return {
         "value": cl.n_nodes * sc.size / step_s,
         "unit": "evals/s",
         "cores": threads,
         "kind": "port",
+        "value_1thread": cl.n_nodes * sc.size / step1_s,
+        "host": host,
         "sample": f"C oracle (oracle/kcc_oracle.c, -O3): full reduce over {cl.n_containers} "
                   f"containers (1 thread, {t_red:.3f}s) + fit of all {cl.n_nodes} nodes x first "
-                  f"{k} of {sc.size} specs ({threads} threads, {t_fit:.2f}s), extrapolated "
-                  f"linearly to {sc.size} specs",
-        "match": bool(np.array_equal(ot, gpu_totals[:k]) and np.array_equal(oe, gpu_err[:k])),
+                  f"{k} of {sc.size} specs ({threads} threads, {t_fit:.2f}s; 1 thread: first "
+                  f"{k1} specs, {t_fit1:.2f}s), extrapolated linearly to {sc.size} specs",
+        "match": bool(np.array_equal(ot, gpu_totals[:k]) and np.array_equal(oe, gpu_err[:k])
+                      and np.array_equal(o1, gpu_totals[:k1]) and np.array_equal(e1, gpu_err[:k1])),
+    }
+
+
+def host_cpus():
+    """The host cores the CPU baseline may use: this process's CPU share (affinity,
+    capped by OMP_NUM_THREADS, which the GPU box sets to the slot's 16 CPUs — nproc
+    there counts the whole machine), the CPU model, and what nproc reports."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    threads = max(1, min(aff, int(omp))) if omp.isdigit() and int(omp) > 0 else aff
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"threads": threads, "nproc": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads": omp or None, "cpu_model": model}
+
+
+def h2d_leg(arrays, dev, step_ms, evals):
+    """the host->device upload of the step's inputs, reported beside the
+    device-resident rate (never `value`): pageable numpy arrays as a caller hands them
+    over (torch .to(device)), and the same bytes from pinned buffers."""
+    import torch
+
+    host = [torch.from_numpy(np.ascontiguousarray(a).view(np.int64)) for a in arrays]
+    nbytes = sum(h.numel() * 8 for h in host)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    outs = [h.to(dev) for h in host]
+    torch.cuda.synchronize()
+    t_page = time.perf_counter() - t
+    del outs
+    pinned = [h.pin_memory() for h in host]
+    dst = [torch.empty_like(h, device=dev) for h in host]
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for d, h in zip(dst, pinned):
+        d.copy_(h, non_blocking=True)
+    torch.cuda.synchronize()
+    t_pin = time.perf_counter() - t
+    del pinned, dst
+    return {
+        "bytes": nbytes,
+        "ms_pageable": t_page * 1e3, "gbs_pageable": nbytes / t_page / 1e9,
+        "ms_pinned": t_pin * 1e3, "gbs_pinned": nbytes / t_pin / 1e9,
+        "evals_per_s_incl_pinned_h2d": evals / (step_ms * 1e-3 + t_pin),
+        "note": "inputs of one step (CSR offsets, container requests, node SoA, specs) "
+                "host->device; not part of `value` (inputs resident in HBM)",
     }
 
 

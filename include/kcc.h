@@ -181,6 +181,32 @@ int kcc_capacity_partial_async(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containe
                                const uint64_t* d_spec_cpu, const int64_t* d_spec_mem,
                                int64_t* d_partial, int n_chunks, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Node sharding.  Nodes are independent and each per-spec total is a
+ * wrapping int64 sum, so a cluster splits into contiguous node ranges whose partial
+ * vectors (kcc_fit_partial_async / kcc_capacity_partial_async) add up to the whole.
+ *
+ * kcc_set_node_shards: the host-array entry points (kcc_fit, kcc_capacity) cut the
+ *   nodes into max(n_shards, devices) contiguous ranges (balanced by node count),
+ *   dealt round-robin over the context's devices; a device's shards run one after the
+ *   other and their partials are summed on it before the RCCL all-reduce over devices.
+ *   0 (default) = one shard per device.  Same results for every shard count; more
+ *   shards than devices rehearse a multi-GPU split on fewer GPUs.
+ *
+ * One process per GPU (the Go host as one process per device, or torchrun): every
+ *   rank owns one node range and a single-device context; rank 0 creates an id with
+ *   kcc_comm_unique_id and hands it to the other ranks (any channel: the bytes are
+ *   opaque), every rank calls kcc_comm_init (collective: blocks until all joined), and
+ *   each step runs kcc_capacity_partial_async -> kcc_allreduce_partial_async ->
+ *   kcc_fit_finalize_async on one stream: an RCCL all-reduce (sum, int64) of the 2*S
+ *   partial vector over xGMI, the only exchange.  Every rank must pass the same specs.
+ * ------------------------------------------------------------------------- */
+#define KCC_COMM_ID_BYTES 128
+int kcc_set_node_shards(kcc_ctx* ctx, int n_shards);
+int kcc_comm_unique_id(uint8_t* id /* [KCC_COMM_ID_BYTES] */);
+int kcc_comm_init(kcc_ctx* ctx, const uint8_t* id, int n_ranks, int rank);
+int kcc_allreduce_partial_async(kcc_ctx* ctx, int64_t n_specs, int64_t* d_partial, void* stream);
+
 /* Per-launch timing of kcc_capacity_partial_async (HIP events recorded on the stream
  * each kernel runs on): enable (1) / disable (0) resets the sums; read synchronises
  * and returns the summed durations and launch counts of the reduces (mark + reduce,

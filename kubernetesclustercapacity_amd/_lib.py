@@ -45,6 +45,10 @@ SIGNATURES = {
     "kcc_fit_async": (_int, [_vp, _i64] + [_vp] * 6 + [_i64] + [_vp] * 5),
     "kcc_capacity_partial_async": (_int, [_vp, _i64, _i64] + [_vp] * 10 + [_i64] + [_vp] * 3
                                    + [_int, _vp]),
+    "kcc_set_node_shards": (_int, [_vp, _int]),
+    "kcc_comm_unique_id": (_int, [_vp]),
+    "kcc_comm_init": (_int, [_vp, _vp, _int, _int]),
+    "kcc_allreduce_partial_async": (_int, [_vp, _i64, _vp, _vp]),
     "kcc_profile_enable": (_int, [_vp, _int]),
     "kcc_profile_read": (_int, [_vp] + [C.POINTER(_dbl), C.POINTER(_i64)] * 2),
     "kcc_last_slow_fraction": (_dbl, [_vp]),

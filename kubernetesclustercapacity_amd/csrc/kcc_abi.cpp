@@ -83,7 +83,10 @@ struct Dev {
 
 struct kcc_ctx {
   std::vector<Dev> devs;
-  std::vector<ncclComm_t> comms;
+  std::vector<ncclComm_t> comms;  // in-process devices (kcc_create with n_gpus > 1)
+  ncclComm_t proc_comm = nullptr;  // one rank of a multi-process run (kcc_comm_init)
+  int proc_ranks = 0, proc_rank = 0;
+  int node_shards = 0;  // host-array entry points: node shards (0 = one per device)
   std::string err;
   double slow_frac = -1.0;
 };
@@ -514,26 +517,39 @@ int run_host(kcc_ctx* ctx, bool with_reduce, int64_t n_nodes, int64_t n_cont,
   }
   if (n_specs == 0) return KCC_OK;
   const int nd = (int)ctx->devs.size();
+  // node shards: one per device, or ctx->node_shards (kcc_set_node_shards) dealt
+  // round-robin over the devices; a device's shards run one after the other on its
+  // stream, each into its own slot of the device's partial buffer, and the slots are
+  // summed on the device before the RCCL all-reduce over devices
+  const int ns = ctx->node_shards > nd ? ctx->node_shards : nd;
+  const int slots = (ns + nd - 1) / nd;
   std::vector<int64_t> lo, hi;
-  shard_nodes(n_nodes, nd, lo, hi);
-  std::vector<std::vector<int64_t>> rebased(nd);  // per device: copies may still be in flight
+  shard_nodes(n_nodes, ns, lo, hi);
+  std::vector<std::vector<int64_t>> rebased(ns);  // per shard: copies may still be in flight
+  std::vector<unsigned long long> shard_slow(ns, 0ull);
   for (int d = 0; d < nd; ++d) {
     Dev& dv = ctx->devs[d];
     KCC_HIP(ctx, hipSetDevice(dv.device));
-    const int64_t n = hi[d] - lo[d];
+    KCC_HIP(ctx, ensure(dv.partial, sizeof(int64_t) * 2 * (size_t)n_specs * (size_t)slots));
+  }
+  for (int sh = 0; sh < ns; ++sh) {
+    Dev& dv = ctx->devs[sh % nd];
+    int64_t* part = as<int64_t>(dv.partial) + (size_t)(sh / nd) * 2 * (size_t)n_specs;
+    KCC_HIP(ctx, hipSetDevice(dv.device));
+    const int64_t n = hi[sh] - lo[sh];
     int rc;
-    if ((rc = h2d(ctx, dv, dv.alloc_cpu, alloc_cpu + lo[d], n))) return rc;
-    if ((rc = h2d(ctx, dv, dv.alloc_mem, alloc_mem + lo[d], n))) return rc;
-    if ((rc = h2d(ctx, dv, dv.alloc_pods, alloc_pods + lo[d], n))) return rc;
-    if ((rc = h2d(ctx, dv, dv.pod_count, pod_count + lo[d], n))) return rc;
+    if ((rc = h2d(ctx, dv, dv.alloc_cpu, alloc_cpu + lo[sh], n))) return rc;
+    if ((rc = h2d(ctx, dv, dv.alloc_mem, alloc_mem + lo[sh], n))) return rc;
+    if ((rc = h2d(ctx, dv, dv.alloc_pods, alloc_pods + lo[sh], n))) return rc;
+    if ((rc = h2d(ctx, dv, dv.pod_count, pod_count + lo[sh], n))) return rc;
     if ((rc = h2d(ctx, dv, dv.spec_cpu, spec_cpu, n_specs))) return rc;
     if ((rc = h2d(ctx, dv, dv.spec_mem, spec_mem, n_specs))) return rc;
-    KCC_HIP(ctx, ensure(dv.partial, sizeof(int64_t) * 2 * (size_t)n_specs));
     if (with_reduce) {
-      const int64_t c0 = n > 0 ? node_ptr[lo[d]] : 0, c1 = n > 0 ? node_ptr[hi[d]] : 0;
-      std::vector<int64_t>& rb = rebased[d];
+      // the shard's containers [c0, c1) with its CSR offsets rebased to 0
+      const int64_t c0 = n > 0 ? node_ptr[lo[sh]] : 0, c1 = n > 0 ? node_ptr[hi[sh]] : 0;
+      std::vector<int64_t>& rb = rebased[sh];
       rb.resize((size_t)n + 1);
-      for (int64_t k = 0; k <= n; ++k) rb[k] = n > 0 ? node_ptr[lo[d] + k] - c0 : 0;
+      for (int64_t k = 0; k <= n; ++k) rb[k] = n > 0 ? node_ptr[lo[sh] + k] - c0 : 0;
       if ((rc = h2d(ctx, dv, dv.ptr, rb.data(), n + 1))) return rc;
       if ((rc = h2d(ctx, dv, dv.cpu, cpu_req + c0, c1 - c0))) return rc;
       if ((rc = h2d(ctx, dv, dv.mem, mem_req + c0, c1 - c0))) return rc;
@@ -546,15 +562,19 @@ int run_host(kcc_ctx* ctx, bool with_reduce, int64_t n_nodes, int64_t n_cont,
         if (rc) return rc;
       }
     } else {
-      if ((rc = h2d(ctx, dv, dv.used_cpu, used_cpu_in + lo[d], n))) return rc;
-      if ((rc = h2d(ctx, dv, dv.used_mem, used_mem_in + lo[d], n))) return rc;
+      if ((rc = h2d(ctx, dv, dv.used_cpu, used_cpu_in + lo[sh], n))) return rc;
+      if ((rc = h2d(ctx, dv, dv.used_mem, used_mem_in + lo[sh], n))) return rc;
     }
     rc = fit_partial_dev(ctx, dv, n, as<uint64_t>(dv.alloc_cpu), as<int64_t>(dv.alloc_mem),
                          as<int64_t>(dv.alloc_pods), as<int64_t>(dv.pod_count),
                          as<uint64_t>(dv.used_cpu), as<int64_t>(dv.used_mem), n_specs,
-                         as<uint64_t>(dv.spec_cpu), as<int64_t>(dv.spec_mem),
-                         as<int64_t>(dv.partial), dv.stream);
+                         as<uint64_t>(dv.spec_cpu), as<int64_t>(dv.spec_mem), part, dv.stream);
     if (rc) return rc;
+    // exact-path pair count of this shard (the next shard's spec setup zeroes it)
+    KCC_HIP(ctx, hipMemcpyAsync(&shard_slow[sh], dv.counters.p, sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost, dv.stream));
+    if (sh >= nd)  // fold this slot into the device's slot 0 (wrapping int64 adds)
+      KCC_HIP(ctx, kcc::launch_partial_add(2 * n_specs, as<int64_t>(dv.partial), part, dv.stream));
   }
   if (nd > 1) {
     KCC_NCCL(ctx, ncclGroupStart());
@@ -580,11 +600,9 @@ int run_host(kcc_ctx* ctx, bool with_reduce, int64_t n_nodes, int64_t n_cont,
   for (int d = 0; d < nd; ++d) {
     Dev& dv = ctx->devs[d];
     KCC_HIP(ctx, hipSetDevice(dv.device));
-    unsigned long long c = 0;
-    KCC_HIP(ctx, hipMemcpyAsync(&c, dv.counters.p, sizeof(c), hipMemcpyDeviceToHost, dv.stream));
     KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
-    slow_pairs += c;
   }
+  for (int sh = 0; sh < ns; ++sh) slow_pairs += shard_slow[sh];
   const double pairs = (double)n_nodes * (double)n_specs;
   ctx->slow_frac = pairs > 0 ? (double)slow_pairs / pairs : 0.0;
   return KCC_OK;
@@ -661,6 +679,11 @@ int kcc_create(kcc_ctx** out, int first_device, int n_gpus) {
 void kcc_destroy(kcc_ctx* ctx) {
   if (!ctx) return;
   for (auto& c : ctx->comms) ncclCommDestroy(c);
+  if (ctx->proc_comm) {
+    (void)hipSetDevice(ctx->devs[0].device);
+    (void)hipDeviceSynchronize();  // its all-reduces ran on caller streams
+    ncclCommDestroy(ctx->proc_comm);
+  }
   for (Dev& dv : ctx->devs) {
     (void)hipSetDevice(dv.device);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
@@ -915,6 +938,52 @@ int kcc_fit_slow_pairs(kcc_ctx* ctx, int64_t* slow_pairs, int64_t* pairs) {
   if (dv.counters.p) KCC_HIP(ctx, hipMemcpy(&c, dv.counters.p, sizeof(c), hipMemcpyDeviceToHost));
   *slow_pairs = (int64_t)c;
   *pairs = dv.last_pairs;
+  return KCC_OK;
+}
+
+int kcc_set_node_shards(kcc_ctx* ctx, int n_shards) {
+  if (!ctx) return KCC_EINVAL;
+  if (n_shards < 0) return fail(ctx, KCC_EINVAL, "n_shards must be >= 0");
+  ctx->node_shards = n_shards;
+  return KCC_OK;
+}
+
+// ---- one rank of a multi-process run (one process per GPU) --------------------------
+
+int kcc_comm_unique_id(uint8_t* id) {
+  if (!id) return KCC_EINVAL;
+  static_assert(sizeof(ncclUniqueId) == KCC_COMM_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return KCC_ERCCL;
+  std::memcpy(id, &u, sizeof(u));
+  return KCC_OK;
+}
+
+int kcc_comm_init(kcc_ctx* ctx, const uint8_t* id, int n_ranks, int rank) {
+  if (!ctx) return KCC_EINVAL;
+  if (!id || n_ranks < 1 || rank < 0 || rank >= n_ranks)
+    return fail(ctx, KCC_EINVAL, "need an id, n_ranks >= 1 and 0 <= rank < n_ranks");
+  if (ctx->devs.size() != 1)
+    return fail(ctx, KCC_EINVAL, "a multi-process rank drives exactly one device");
+  if (ctx->proc_comm) return fail(ctx, KCC_EINVAL, "communicator already initialised");
+  KCC_HIP(ctx, hipSetDevice(ctx->devs[0].device));
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  KCC_NCCL(ctx, ncclCommInitRank(&ctx->proc_comm, n_ranks, u, rank));
+  ctx->proc_ranks = n_ranks;
+  ctx->proc_rank = rank;
+  return KCC_OK;
+}
+
+int kcc_allreduce_partial_async(kcc_ctx* ctx, int64_t n_specs, int64_t* d_partial, void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  if (n_specs < 0) return fail(ctx, KCC_EINVAL, "negative size");
+  if (!ctx->proc_comm) return fail(ctx, KCC_EINVAL, "no communicator (kcc_comm_init)");
+  if (n_specs == 0) return KCC_OK;
+  if (!d_partial) return fail(ctx, KCC_EINVAL, "NULL partial");
+  KCC_HIP(ctx, hipSetDevice(ctx->devs[0].device));
+  KCC_NCCL(ctx, ncclAllReduce(d_partial, d_partial, 2 * (size_t)n_specs, ncclInt64, ncclSum,
+                              ctx->proc_comm, static_cast<hipStream_t>(stream)));
   return KCC_OK;
 }
 

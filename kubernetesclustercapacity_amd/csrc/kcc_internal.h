@@ -227,6 +227,9 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
 hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial,
                                const int32_t* perm, int64_t* totals, int32_t* spec_err,
                                hipStream_t s);
+// dst[k] += src[k] (wrapping int64), k < n: folds one node shard's partial vector into
+// another on the same device (the host-array entry points with more shards than devices)
+hipError_t launch_partial_add(int64_t n, int64_t* dst, const int64_t* src, hipStream_t s);
 
 // ---- quantity-string parse (kcc_parse.hip) ------------------------
 enum ParseMode : int { PARSE_MODE_CPU_MILLIS = 0, PARSE_MODE_BYTES = 1, PARSE_MODE_QUANTITY = 2 };

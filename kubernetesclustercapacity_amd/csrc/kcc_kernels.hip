@@ -1254,6 +1254,12 @@ __global__ void fit_finalize_kernel(int64_t S, const int64_t* __restrict__ parti
   spec_err[dst] = err ? 1 : 0;
 }
 
+__global__ void partial_add_kernel(int64_t n, int64_t* __restrict__ dst,
+                                   const int64_t* __restrict__ src) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (int64_t)((uint64_t)dst[i] + (uint64_t)src[i]);
+}
+
 inline unsigned grid_for(int64_t n, int block, int64_t cap) {
   int64_t g = (n + block - 1) / block;
   if (g < 1) g = 1;
@@ -1426,6 +1432,13 @@ hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial, const in
   if (n_specs <= 0) return hipSuccess;
   hipLaunchKernelGGL(fit_finalize_kernel, dim3(grid_for(n_specs, 256, 1 << 30)), dim3(256), 0, s,
                      n_specs, partial, perm, totals, spec_err);
+  return hipGetLastError();
+}
+
+hipError_t launch_partial_add(int64_t n, int64_t* dst, const int64_t* src, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(partial_add_kernel, dim3(grid_for(n, 256, 1 << 30)), dim3(256), 0, s, n, dst,
+                     src);
   return hipGetLastError();
 }
 

@@ -20,6 +20,8 @@ import numpy as np
 
 from . import _lib
 
+COMM_ID_BYTES = 128  # KCC_COMM_ID_BYTES
+
 
 class KccError(RuntimeError):
     def __init__(self, code: int, msg: str):
@@ -372,6 +374,34 @@ class CapacityEngine:
         self._check(self._lib.kcc_parse_quantity_async(
             self._h, off.numel() - 1, _dp(buf), buf.numel(), _dp(off), _dp(out), _dp(status),
             _stream(stream)))
+
+    # -- node sharding ------------------------------------------------
+    def set_node_shards(self, n_shards: int):
+        """Host-array entry points: cut the nodes into this many contiguous shards
+        (round-robin over the context's devices; 0 = one per device)."""
+        self._check(self._lib.kcc_set_node_shards(self._h, int(n_shards)))
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """Rank 0 of a one-process-per-GPU run: the RCCL id every rank passes to
+        comm_init (opaque bytes, distributed by the caller)."""
+        buf = C.create_string_buffer(COMM_ID_BYTES)
+        rc = _lib.lib().kcc_comm_unique_id(C.cast(buf, C.c_void_p))
+        if rc != 0:
+            raise KccError(rc, "ncclGetUniqueId failed")
+        return buf.raw
+
+    def comm_init(self, uid: bytes, n_ranks: int, rank: int):
+        """Join the ranks' RCCL communicator (collective: blocks until every rank joined)."""
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError(f"the id holds {COMM_ID_BYTES} bytes")
+        buf = C.create_string_buffer(uid, COMM_ID_BYTES)
+        self._check(self._lib.kcc_comm_init(self._h, C.cast(buf, C.c_void_p), n_ranks, rank))
+
+    def allreduce_partial_async(self, n_specs, partial, stream=None):
+        """RCCL all-reduce (sum, int64) of the 2*S partial vector, on `stream`."""
+        self._check(self._lib.kcc_allreduce_partial_async(self._h, n_specs, _dp(partial),
+                                                          _stream(stream)))
 
     def profile_enable(self, on: bool = True):
         self._check(self._lib.kcc_profile_enable(self._h, 1 if on else 0))

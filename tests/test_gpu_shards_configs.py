@@ -1,0 +1,225 @@
+"""GPU: node sharding and the BASELINE configs at their own sizes.
+
+Sharding — the per-spec totals of CC:105-140 are wrapping int64 sums over node rows,
+so any split of the rows into contiguous shards must give the same totals bit for bit:
+  - the library's own split (kcc_set_node_shards: k shards on one device, the
+    shard/rebase logic of the host-array path, partials folded on the device);
+  - the split bench.py runs per rank (kcc_capacity_partial_async on a node range of the
+    resident arrays, partials summed as the RCCL all-reduce would, then finalize);
+  - the library's RCCL communicator with a single rank (the all-reduce entry point);
+  - bench.py itself with 2 ranks sharing GPU 0 over gloo (the launcher + exchange path)
+    against its own 1-rank run.
+Configs (BASELINE.json `configs`) against the C oracle, every spec, at full size:
+C2 (10k x 200k pods x 1 spec), C3 (100k x 2M x 256), C4 (1M x 20M x 4096), and the C5
+rank-0 shard of an 8-way split (625k of 5M Zipf-skewed nodes x 16384 specs).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from kubernetesclustercapacity_amd import synth
+from kubernetesclustercapacity_amd.shard import node_range
+from oracle import coracle
+
+pytestmark = pytest.mark.gpu
+NT = min(16, len(os.sched_getaffinity(0)))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def seg_sums(node_ptr, vals):
+    v = np.asarray(vals).view(np.uint64)
+    cs = np.zeros(v.size + 1, np.uint64)
+    np.cumsum(v, out=cs[1:])
+    return cs[node_ptr[1:]] - cs[node_ptr[:-1]]
+
+
+def oracle_totals(c, sc, sm):
+    uc = seg_sums(c.node_ptr, c.cpu_req)
+    um = seg_sums(c.node_ptr, c.mem_req).view(np.int64)
+    return coracle.fit(c.alloc_cpu, c.alloc_mem, c.alloc_pods, c.pod_count, uc, um, sc, sm, NT)
+
+
+def capacity(engine, c, sc, sm):
+    return engine.capacity(c.node_ptr, c.cpu_req, c.mem_req, c.alloc_cpu, c.alloc_mem,
+                           c.alloc_pods, c.pod_count, sc, sm)
+
+
+def device_shards(c, sc, sm, k):
+    """bench.py's per-rank step for each of k node ranges of the resident arrays."""
+    import torch
+
+    from kubernetesclustercapacity_amd import CapacityEngine
+    torch.cuda.init()  # torch's HIP runtime before libkcc's (tests/conftest.py)
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+    S = sc.size
+    acc = torch.zeros(2 * S, dtype=torch.int64, device=dev)
+    with CapacityEngine(0, 1) as eng:
+        stream = torch.cuda.Stream(dev)
+        s_cpu, s_mem = T(sc), T(sm)
+        for r in range(k):
+            lo, hi = node_range(c.n_nodes, r, k)
+            c0, c1 = int(c.node_ptr[lo]), int(c.node_ptr[hi])
+            hp = c.node_ptr[lo:hi + 1] - c0           # the rank's own CSR, rebased
+            n = hi - lo
+            used = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(2)]
+            partial = torch.empty(2 * S, dtype=torch.int64, device=dev)
+            with torch.cuda.stream(stream):
+                eng.capacity_partial_async(hp, T(hp), T(c.cpu_req[c0:c1]), T(c.mem_req[c0:c1]),
+                                           T(c.alloc_cpu[lo:hi]), T(c.alloc_mem[lo:hi]),
+                                           T(c.alloc_pods[lo:hi]), T(c.pod_count[lo:hi]),
+                                           used[0], used[1], s_cpu, s_mem, partial, stream=stream)
+            stream.synchronize()
+            acc += partial                            # the all-reduce (int64 adds wrap)
+        totals = torch.empty(S, dtype=torch.int64, device=dev)
+        err = torch.empty(S, dtype=torch.int32, device=dev)
+        with torch.cuda.stream(stream):
+            eng.fit_finalize_async(S, acc, totals, err, stream=stream)
+        stream.synchronize()
+    return totals.cpu().numpy(), err.cpu().numpy()
+
+
+# ---- BASELINE C4 at full size: every spec vs the oracle, and its shards --------------------
+@pytest.fixture(scope="module")
+def c4():
+    return synth.config_cluster("C4"), synth.config_specs("C4")
+
+
+@pytest.fixture(scope="module")
+def c4_oracle(c4):
+    c, (sc, sm) = c4
+    return oracle_totals(c, sc, sm)
+
+
+def test_c4_every_spec_vs_oracle(engine, c4, c4_oracle):
+    c, (sc, sm) = c4
+    t, e = capacity(engine, c, sc, sm)
+    np.testing.assert_array_equal(e, c4_oracle[1])
+    np.testing.assert_array_equal(t, c4_oracle[0])
+
+
+@pytest.mark.parametrize("k", [2, 3, 8])
+def test_c4_library_node_shards(engine, c4, c4_oracle, k):
+    c, (sc, sm) = c4
+    engine.set_node_shards(k)
+    try:
+        t, e = capacity(engine, c, sc, sm)
+    finally:
+        engine.set_node_shards(0)
+    np.testing.assert_array_equal(e, c4_oracle[1])
+    np.testing.assert_array_equal(t, c4_oracle[0])
+
+
+@pytest.mark.parametrize("k", [2, 8])
+def test_c4_rank_shards_like_bench(c4, c4_oracle, k):
+    c, (sc, sm) = c4
+    t, e = device_shards(c, sc, sm, k)
+    np.testing.assert_array_equal(e, c4_oracle[1])
+    np.testing.assert_array_equal(t, c4_oracle[0])
+
+
+# ---- skewed (Zipf) cluster with the adversarial slice, sharded -----------------------------
+@pytest.mark.parametrize("k", [1, 2, 5, 8])
+def test_zipf_adversarial_shards(engine, k):
+    c = synth.make_cluster(200_003, 4_000_000, seed=55, skew=True, adversarial=True, chunk=4096)
+    sc, sm = synth.make_specs(1000, seed=55, adversarial=True)
+    ot, oe = oracle_totals(c, sc, sm)
+    engine.set_node_shards(k)
+    try:
+        t, e = capacity(engine, c, sc, sm)
+    finally:
+        engine.set_node_shards(0)
+    np.testing.assert_array_equal(e, oe)
+    np.testing.assert_array_equal(t, ot)
+    t2, e2 = device_shards(c, sc, sm, k)
+    np.testing.assert_array_equal(e2, oe)
+    np.testing.assert_array_equal(t2, ot)
+
+
+def test_single_rank_communicator():
+    """kcc_comm_unique_id / kcc_comm_init / kcc_allreduce_partial_async with one rank:
+    the all-reduce of one partial is the identity, on the kernel stream."""
+    import torch
+
+    from kubernetesclustercapacity_amd import CapacityEngine
+    torch.cuda.init()
+    c = synth.make_cluster(20_000, 400_000, seed=9, chunk=4096)
+    sc, sm = synth.make_specs(300, seed=9, adversarial=True)
+    ot, oe = oracle_totals(c, sc, sm)
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+    S, n = sc.size, c.n_nodes
+    with CapacityEngine(0, 1) as eng:
+        eng.comm_init(CapacityEngine.comm_unique_id(), 1, 0)
+        used = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(2)]
+        partial = torch.empty(2 * S, dtype=torch.int64, device=dev)
+        totals = torch.empty(S, dtype=torch.int64, device=dev)
+        err = torch.empty(S, dtype=torch.int32, device=dev)
+        stream = torch.cuda.Stream(dev)
+        with torch.cuda.stream(stream):
+            eng.capacity_partial_async(c.node_ptr, T(c.node_ptr), T(c.cpu_req), T(c.mem_req),
+                                       T(c.alloc_cpu), T(c.alloc_mem), T(c.alloc_pods),
+                                       T(c.pod_count), used[0], used[1], T(sc), T(sm), partial,
+                                       stream=stream)
+            eng.allreduce_partial_async(S, partial, stream=stream)
+            eng.fit_finalize_async(S, partial, totals, err, stream=stream)
+        stream.synchronize()
+    np.testing.assert_array_equal(err.cpu().numpy(), oe)
+    np.testing.assert_array_equal(totals.cpu().numpy(), ot)
+
+
+# ---- the other BASELINE configs at their own sizes -----------------------------------------
+@pytest.mark.parametrize("name", ["C2", "C3"])
+def test_config_every_spec_vs_oracle(engine, name):
+    c, (sc, sm) = synth.config_cluster(name), synth.config_specs(name)
+    assert c.n_nodes == synth.CONFIGS[name]["n_nodes"] and sc.size == synth.CONFIGS[name]["n_specs"]
+    r = engine.get_pod_cpu_memory_requests_limits(c.node_ptr, c.cpu_req, c.mem_req)
+    np.testing.assert_array_equal(r.cpu_requests, seg_sums(c.node_ptr, c.cpu_req))
+    np.testing.assert_array_equal(r.memory_requests.view(np.uint64), seg_sums(c.node_ptr, c.mem_req))
+    ot, oe = oracle_totals(c, sc, sm)
+    t, e = capacity(engine, c, sc, sm)
+    np.testing.assert_array_equal(e, oe)
+    np.testing.assert_array_equal(t, ot)
+
+
+def test_c5_rank0_shard_every_spec_vs_oracle(engine):
+    """C5 = 5M Zipf-skewed nodes x 16384 specs over 8 GPUs: rank 0's node range."""
+    lo, hi = node_range(synth.CONFIGS["C5"]["n_nodes"], 0, 8)
+    c = synth.config_cluster("C5", node_lo=lo, node_hi=hi)
+    sc, sm = synth.config_specs("C5")
+    assert c.n_nodes == 625_000 and sc.size == 16384
+    r = engine.get_pod_cpu_memory_requests_limits(c.node_ptr, c.cpu_req, c.mem_req)
+    np.testing.assert_array_equal(r.cpu_requests, seg_sums(c.node_ptr, c.cpu_req))
+    np.testing.assert_array_equal(r.memory_requests.view(np.uint64), seg_sums(c.node_ptr, c.mem_req))
+    ot, oe = oracle_totals(c, sc, sm)
+    t, e = capacity(engine, c, sc, sm)
+    np.testing.assert_array_equal(e, oe)
+    np.testing.assert_array_equal(t, ot)
+
+
+# ---- bench.py: 2 ranks (gloo, sharing GPU 0) == 1 rank -------------------------------------
+def _bench(*extra):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+                        "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "C3",
+                        "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-keyed",
+                        "--no-pods", "--no-parse", *extra], capture_output=True, text=True,
+                       timeout=100, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+def test_bench_two_ranks_equal_one():
+    one = _bench("--gpus", "1")
+    two = _bench("--gpus", "2", "--dist-backend", "gloo")
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert two["world"]["process_group_size"] == 2 and two["scaling"] == "strong"
+    assert two["config"]["nodes"] == one["config"]["nodes"] == 100_000
+    assert two["config"]["nodes_rank0"] == 50_000
+    assert two["totals_checksum"] == one["totals_checksum"]
+    assert two["spec_errors"] == one["spec_errors"]
