@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="diagnostic: run only rank 0's node shard of a world of this size "
                          "(no all-reduce) to estimate per-rank step time at N GPUs")
+    ap.add_argument("--kernel-events", default="after", choices=["timed", "after"],
+                    help="per-kernel HIP events inside the timed steps (timed) or in as many "
+                         "extra steps after them (after)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: start the ranks, exchange one gloo "
                          "all-reduce, print the rank count (no measurement)")
@@ -221,8 +224,9 @@ def main():
             step()
         torch.cuda.synchronize()
         # per-launch kernel durations from HIP events the library records on the stream
-        # each kernel runs on, over exactly the timed steps
-        eng.profile_enable(True)
+        # each kernel runs on: over exactly the timed steps (--kernel-events timed), or
+        # over as many extra steps right after them (after: the timed region has no events)
+        eng.profile_enable(args.kernel_events == "timed")
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -233,6 +237,11 @@ def main():
         if world > 1:
             dist.barrier()
         t_end = time.perf_counter()
+        if args.kernel_events == "after":
+            eng.profile_enable(True)
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
     red_ms_tot, red_launches, fit_ms_tot, fit_launches = eng.profile_read()
     eng.profile_enable(False)
     elapsed = t_end - t_start

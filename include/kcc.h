@@ -258,11 +258,12 @@ int kcc_parse_bytes(kcc_ctx* ctx, int64_t n, const char* bytes, int64_t n_bytes,
                     const int64_t* offsets, int64_t* out, int8_t* status);
 /* resource.Quantity.Value() of ParseQuantity(s) (CC:285-286, the containers' memory
  * requests): [+-] digits [. digits] + "", Ki..Ei, n u m k M G T P E or e<int> suffix;
- * magnitude capped at 2^63 - 1 and rounded up away from zero.  Restated from
- * k8s.io/apimachinery's published algorithm, which is not vendored in the reference
+ * rounded up away from zero, binary (Ki..Ei) magnitudes capped at 2^63 - 1.  Restated
+ * from k8s.io/apimachinery's published algorithm, which is not vendored in the reference
  * (version unpinned): parity unpinned.  KCC_PARSE_ERR for strings
- * ParseQuantity rejects; KCC_PARSE_UNSUPPORTED for binary-suffixed fractions with more
- * than 19 significant digits. */
+ * ParseQuantity rejects; KCC_PARSE_UNSUPPORTED (value 0) for a decimal amount beyond
+ * 2^63 - 1 (k8s wraps it), a negative amount off ParseQuantity's int64 fast path and
+ * binary-suffixed fractions with more than 19 significant digits. */
 int kcc_parse_quantity(kcc_ctx* ctx, int64_t n, const char* bytes, int64_t n_bytes,
                        const int64_t* offsets, int64_t* out, int8_t* status);
 int kcc_parse_quantity_async(kcc_ctx* ctx, int64_t n, const char* d_bytes, int64_t n_bytes,

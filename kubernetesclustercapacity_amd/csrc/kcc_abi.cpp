@@ -58,16 +58,16 @@ struct Dev {
   double prof_ms[2] = {0.0, 0.0};
   int64_t prof_n[2] = {0, 0};
   // workspace of the *_async entry points
-  DevBuf wave_node, fast_a, fast_b, slow, slow_list, srec, sperm, srec_o, counters;
-  // clamp correction (kcc::ClampWork)
-  DevBuf c_rank, c_sync, c_cs, c_ms, c_mless, c_dperm, c_gml, c_kpos, c_H, c_H2, c_R;
-  // H, H2, rank and the completion counter not known to be all zero (fresh allocation
-  // or an interrupted call)
+  DevBuf wave_node, fast_a, fast_b, slow, slow_list, srec, sperm, counters;
+  // spec setup + clamp correction (kcc::ClampWork)
+  DevBuf c_rank, c_bcnt, c_cs, c_ms, c_mrc, c_crm, c_dperm;
+  DevBuf c_C, c_H2, c_H3, c_Crow, c_S2, c_S3;
+  // the table copies C / H2 / H3 not known to be all zero (fresh allocation or an
+  // interrupted call)
   bool clamp_dirty = true;
   int64_t last_pairs = 0;  // node x spec pairs of the last fit_prepare on this device
-  int64_t h_stride = 0;    // cells per copy of the clamp table H in c_H
-  int64_t h2_stride = 0;   // cells per copy of the clamp table H2 in c_H2
-  int64_t rt_stride = 0;   // tiles per row of the clamp table's row sums
+  int64_t c_stride = 0;    // cells per copy of the clamp table C
+  int64_t h_stride = 0;    // cells per copy of the clamp tables H2 / H3
   int64_t prep_nodes = -1, prep_specs = -1;  // sizes the workspace was last prepared for
   // staging of the host-array entry points
   DevBuf ptr, cpu, mem, cpul, meml, used_cpu, used_mem, lim_cpu, lim_mem;
@@ -184,7 +184,6 @@ kcc::SpecPrep spec_prep_of(Dev& dv) {
   kcc::SpecPrep sp;
   sp.rec = as<kcc::SpecRec>(dv.srec);
   sp.perm = as<int32_t>(dv.sperm);
-  sp.rec_o = as<kcc::SpecRec>(dv.srec_o);
   return sp;
 }
 
@@ -200,41 +199,41 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.slow_list, sizeof(int64_t) * N));
   KCC_HIP(ctx, ensure(dv.srec, sizeof(kcc::SpecRec) * S));
   KCC_HIP(ctx, ensure(dv.sperm, 4 * S));
-  KCC_HIP(ctx, ensure(dv.srec_o, sizeof(kcc::SpecRec) * S));
   KCC_HIP(ctx, ensure(dv.counters, sizeof(unsigned long long) * kcc::CNT_N));
-  KCC_HIP(ctx, ensure(dv.c_sync, 64));
+  const size_t S64 = (S + 63) / 64 * 64;
+  KCC_HIP(ctx, ensure(dv.c_bcnt, 8 * (S64 / 64)));
   KCC_HIP(ctx, ensure(dv.c_cs, 8 * S));
   KCC_HIP(ctx, ensure(dv.c_ms, 8 * S));
-  KCC_HIP(ctx, ensure(dv.c_mless, 4 * S));
+  KCC_HIP(ctx, ensure(dv.c_mrc, 4 * S64));
+  KCC_HIP(ctx, ensure(dv.c_crm, 4 * S64));
   KCC_HIP(ctx, ensure(dv.c_dperm, 4 * S));
-  KCC_HIP(ctx, ensure(dv.c_gml, 4 * (S / 64 + 1) * 64));
-  KCC_HIP(ctx, ensure(dv.c_kpos, S));
-  // H, H2, rank and the completion counter stay all-zero between calls (their consumers
-  // zero what they read); a new or grown allocation, or a layout change, is zeroed
-  // before its first use
-  const int64_t hs = kcc::clamp_h_cells((int64_t)S), h2s = kcc::clamp_h2_cells((int64_t)S);
-  const int64_t rts = kcc::clamp_rtiles((int64_t)S);
-  void* const before[3] = {dv.c_H.p, dv.c_H2.p, dv.c_rank.p};
-  KCC_HIP(ctx, ensure(dv.c_rank, 4 * 4 * S));
-  KCC_HIP(ctx, ensure(dv.c_H, 8 * (size_t)kcc::H_COPIES * (size_t)hs));
-  KCC_HIP(ctx, ensure(dv.c_H2, 8 * (size_t)kcc::H2_COPIES * (size_t)h2s));
-  KCC_HIP(ctx, ensure(dv.c_R, 8 * ((size_t)hs + (size_t)kcc::clamp_rows_max((int64_t)S) * (size_t)rts)));
-  if (dv.c_H.p != before[0] || dv.c_H2.p != before[1] || dv.c_rank.p != before[2] ||
-      dv.h_stride != hs || dv.h2_stride != h2s)
+  // the table copies stay all-zero between calls (clamp_prep zeroes what it reads); a
+  // new or grown allocation, or a layout change, is zeroed before its first use
+  const int64_t cs_ = kcc::clamp_c_cells((int64_t)S), hs = kcc::clamp_h_cells((int64_t)S);
+  void* const before[4] = {dv.c_C.p, dv.c_H2.p, dv.c_H3.p, dv.c_rank.p};
+  KCC_HIP(ctx, ensure(dv.c_rank, 4 * 2 * S));
+  KCC_HIP(ctx, ensure(dv.c_C, 8 * (size_t)kcc::C_COPIES * (size_t)cs_));
+  KCC_HIP(ctx, ensure(dv.c_H2, 8 * (size_t)kcc::H2_COPIES * (size_t)hs));
+  KCC_HIP(ctx, ensure(dv.c_H3, 8 * (size_t)kcc::H2_COPIES * (size_t)hs));
+  KCC_HIP(ctx, ensure(dv.c_Crow, 8 * (size_t)cs_));
+  KCC_HIP(ctx, ensure(dv.c_S2, 8 * (size_t)hs));
+  KCC_HIP(ctx, ensure(dv.c_S3, 8 * (size_t)hs));
+  if (dv.c_C.p != before[0] || dv.c_H2.p != before[1] || dv.c_H3.p != before[2] ||
+      dv.c_rank.p != before[3] ||
+      dv.c_stride != cs_ || dv.h_stride != hs)
     dv.clamp_dirty = true;
+  dv.c_stride = cs_;
   dv.h_stride = hs;
-  dv.h2_stride = h2s;
-  dv.rt_stride = rts;
   return KCC_OK;
 }
 
-// Zero H / H2 when they are not known to be zero (before node_prep adds to them).
+// Zero the table copies when they are not known to be zero (before node_prep adds to them).
 int clamp_clean(kcc_ctx* ctx, Dev& dv, hipStream_t s) {
   if (!dv.clamp_dirty) return KCC_OK;
-  KCC_HIP(ctx, hipMemsetAsync(dv.c_H.p, 0, dv.c_H.bytes, s));
+  KCC_HIP(ctx, hipMemsetAsync(dv.c_C.p, 0, dv.c_C.bytes, s));
   KCC_HIP(ctx, hipMemsetAsync(dv.c_H2.p, 0, dv.c_H2.bytes, s));
+  KCC_HIP(ctx, hipMemsetAsync(dv.c_H3.p, 0, dv.c_H3.bytes, s));
   KCC_HIP(ctx, hipMemsetAsync(dv.c_rank.p, 0, dv.c_rank.bytes, s));
-  KCC_HIP(ctx, hipMemsetAsync(dv.c_sync.p, 0, dv.c_sync.bytes, s));
   dv.clamp_dirty = false;
   return KCC_OK;
 }
@@ -242,20 +241,20 @@ int clamp_clean(kcc_ctx* ctx, Dev& dv, hipStream_t s) {
 kcc::ClampWork clamp_of(Dev& dv) {
   kcc::ClampWork cw;
   cw.rank = as<uint32_t>(dv.c_rank);
-  cw.sync = as<uint32_t>(dv.c_sync);
+  cw.bcnt = as<uint32_t>(dv.c_bcnt);
   cw.cs = as<uint64_t>(dv.c_cs);
   cw.ms = as<int64_t>(dv.c_ms);
-  cw.m_less = as<uint32_t>(dv.c_mless);
+  cw.mr_c = as<uint32_t>(dv.c_mrc);
+  cw.cr_m = as<uint32_t>(dv.c_crm);
   cw.dperm = as<int32_t>(dv.c_dperm);
-  cw.gml = as<uint32_t>(dv.c_gml);
-  cw.kpos = as<uint8_t>(dv.c_kpos);
-  cw.H = as<int64_t>(dv.c_H);
+  cw.C = as<int64_t>(dv.c_C);
   cw.H2 = as<int64_t>(dv.c_H2);
-  cw.R = as<int64_t>(dv.c_R);
-  cw.Rtot = as<int64_t>(dv.c_R) + dv.h_stride;
+  cw.H3 = as<int64_t>(dv.c_H3);
+  cw.Crow = as<int64_t>(dv.c_Crow);
+  cw.S2 = as<int64_t>(dv.c_S2);
+  cw.S3 = as<int64_t>(dv.c_S3);
+  cw.c_stride = dv.c_stride;
   cw.h_stride = dv.h_stride;
-  cw.h2_stride = dv.h2_stride;
-  cw.rt_stride = dv.rt_stride;
   return cw;
 }
 
@@ -342,7 +341,13 @@ hipError_t prof_event(Dev& dv, hipEvent_t* ev) {
     dv.prof_free.pop_back();
     return hipSuccess;
   }
+#ifdef KCC_PROF_SYSTEM_FENCE
   return hipEventCreate(ev);
+#else
+  // device-scope release only: a timing event between two kernels of one stream needs no
+  // system-scope fence (with it every record left a ~5.5 us gap on the stream)
+  return hipEventCreateWithFlags(ev, hipEventDisableSystemFence);
+#endif
 }
 
 // Chunk boundaries: node ranges of ~equal node count, multiples of CHUNK_ALIGN (a
@@ -687,10 +692,11 @@ void kcc_destroy(kcc_ctx* ctx) {
   for (Dev& dv : ctx->devs) {
     (void)hipSetDevice(dv.device);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
-    DevBuf* bufs[] = {&dv.c_rank, &dv.c_sync, &dv.c_cs, &dv.c_ms, &dv.c_mless,
-                      &dv.c_dperm, &dv.c_gml, &dv.c_kpos, &dv.c_H, &dv.c_H2, &dv.c_R,
+    DevBuf* bufs[] = {&dv.c_rank, &dv.c_bcnt, &dv.c_cs, &dv.c_ms,
+                      &dv.c_mrc, &dv.c_crm, &dv.c_dperm, &dv.c_C, &dv.c_H2, &dv.c_H3,
+                      &dv.c_Crow, &dv.c_S2, &dv.c_S3,
                       &dv.wave_node, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
-                      &dv.sperm, &dv.srec_o,
+                      &dv.sperm,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
                       &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,
                       &dv.alloc_cpu, &dv.alloc_mem, &dv.alloc_pods, &dv.pod_count, &dv.spec_cpu,

@@ -120,7 +120,6 @@ static_assert(sizeof(SpecRec) == 48, "SpecRec must be 48 B");
 struct SpecPrep {
   SpecRec* rec;    // by internal position
   int32_t* perm;   // internal index -> caller index
-  SpecRec* rec_o;  // by caller index (spec setup's staging)
 };
 
 // Clamp correction.  On the fast paths the fit kernel sums
@@ -128,55 +127,52 @@ struct SpecPrep {
 // added back per spec as  partial[s] -= D_s,  D_s = Σ_i w_i [x_is >= P_i],  w_i = P_i - cl_i
 // (the pod count; for P_i <= 0 rows, clamped for every spec, w_i = -cl_i).  For P_i >= 1,
 // x_is >= P_i  <=>  c_s <= U_i = fc_i / P_i  and  m_s <= V_i = fm_i / P_i  (integer
-// quotients): a 2-D dominance count.  The nN normal specs (classes A and B) are ranked by
-// c — groups of 64 consecutive c-ranks, T = ceil(nN / 64) — and by m.  Node i covers
-// L_i = #{s : c_s <= U_i} c-ranks, G_i = L_i / 64 full groups and the first r_i = L_i % 64
-// lanes of group G_i, and b_i = #{s : m_s <= V_i} m-ranks:
-//   - full groups: one cell H[G_i][b_i] of a (T+1) x (nN+1) table; spec s (c-rank q,
-//     group g = q / 64) collects  Σ_{G > g, b > m_less_s} H[G][b];
-//   - group G_i's first r_i lanes: one cell H2[G_i][r_i][k_i] of a 64 x 65 table per
-//     group, k_i = #{specs of group G_i with m_less < b_i}; spec s collects
-//     Σ_{r > q % 64, k > kpos_s} H2[g][r][k], kpos_s = its position in the group's
-//     m_less order (m_s <= V_i  <=>  m_less_s < b_i  <=>  kpos_s < k_i).
-// H and H2 have one copy per XCD (node_prep's atomics spread over 8x the cache lines) and
-// are zero between calls: clamp_rows / clamp_groups zero every cell they read.
+// quotients): a 2-D dominance sum.  The nN normal specs (classes A and B) get an x-rank by
+// (c, index) and a y-rank by (m, index) (permutations of 0..nN-1); row i dominates exactly
+// the specs with x < L_i = #{c <= U_i} and y < b_i = #{m <= V_i}.  Both axes are cut into
+// blocks of 64 ranks (T = ceil(nN / 64)):
+//   - coarse: C[L_i >> 6][b_i >> 6] += w_i, a (T+2) x (T+2) table (P <= 0 rows in cell
+//     [T+1][T+1]); spec s collects Σ_{GX > x_s>>6, GY > y_s>>6} C;
+//   - x-group: the rows with L_i >> 6 == g, r = L_i & 63 > 0, in H2[g][k][r] with
+//     k = #{specs of x-group g with y < b_i}; spec s (x-group g) collects
+//     Σ_{k > kpos_s, r > x_s & 63} H2[g][k][r], kpos_s = #{specs of x-group g, y < y_s};
+//   - y-block: the rows with b_i >> 6 == Y, r = b_i & 63 > 0, L_i >> 6 > 0, in H3[Y][j][r]
+//     with j = #{specs of y-block Y whose x-group < L_i >> 6}; spec s collects
+//     Σ_{j > jpos_s, r > y_s & 63} H3[Y][j][r], jpos_s = #{specs of y-block Y, x < x_s}.
+// All tables are O(S) (the tables of round 1 grew as S^2/64: 270 MB at S = 16384).  C has
+// one copy per XCD, H2/H3 two (node_prep's atomics spread over more cache lines); every
+// copy is zero between calls: clamp_prep zeroes what it reads.
 struct ClampWork {
-  uint32_t* rank;    // [4*S] by caller index: c-rank, m-rank, #{smaller m}, rank within
-                     // the class (zero between calls)
-  uint32_t* sync;    // spec setup: [1] [2] class A / B counts (zero between calls)
-  uint64_t* cs;      // [S] normal specs' cpu requests in c-rank order
-  int64_t* ms;       // [S] normal specs' memory requests in m order
-  uint32_t* m_less;  // [S] by c-rank: #normal specs with a smaller memory request
-  int32_t* dperm;    // [S] c-rank -> internal position
-  uint32_t* gml;     // [64*T] per group of 64 c-ranks: its m_less values ascending
-  uint8_t* kpos;     // [S] by c-rank: the spec's position in its group's gml order
-  int64_t* H;        // [H_COPIES][h_stride]: (T+1) x (nN+1)
-  int64_t* H2;       // [H2_COPIES][h2_stride]: T x 64 x 65, cell (G*64 + r)*65 + k
-  int64_t* R;        // [h_stride]: H's rows summed over the copies, suffix sums over b
-                     // within tiles of CLAMP_RTILE (clamp_rows)
-  int64_t* Rtot;     // [(T+1) x rt_stride]: the tiles' totals
-  int64_t h_stride;  // cells per H copy (clamp_h_cells(S) of the workspace)
-  int64_t h2_stride; // cells per H2 copy (clamp_h2_cells(S))
-  int64_t rt_stride; // tiles per row (clamp_rtiles(S))
+  uint32_t* rank;    // [2S] by caller index: x-rank, y-rank (zero between calls)
+  uint32_t* bcnt;    // [ceil(S/64)][2] class A / class B specs per block of 64 (caller order)
+  uint64_t* cs;      // [S] normal specs' cpu requests by x-rank (ascending)
+  int64_t* ms;       // [S] memory requests by y-rank (ascending)
+  uint32_t* mr_c;    // [64 * T] y-rank by x-rank (padding 0xffffffff)
+  uint32_t* cr_m;    // [64 * T] x-rank by y-rank (padding 0xffffffff)
+  int32_t* dperm;    // [S] x-rank -> internal position
+  int64_t* C;        // [C_COPIES][c_stride]: (T+2) x (T+2), cell GX * (T+2) + GY
+  int64_t* H2;       // [H2_COPIES][h_stride]: T x 65 x 64, cell (g * 65 + k) * 64 + r
+  int64_t* H3;       // [H2_COPIES][h_stride]: T x 65 x 64, cell (Y * 65 + j) * 64 + r
+  int64_t* Crow;     // [c_stride]: C summed over the copies, suffix sums along GY
+  int64_t* S2;       // [h_stride]: H2 summed over the copies, 2-D suffix sums (k, r)
+  int64_t* S3;       // [h_stride]: the same for H3
+  int64_t c_stride;  // cells per C copy (clamp_c_cells(S) of the workspace)
+  int64_t h_stride;  // cells per H2 / H3 copy (clamp_h_cells(S))
 };
-constexpr int64_t CLAMP_RTILE = 1024;
-// specs per call: the group orders use 32-bit keys m_less << 6 | lane
+// specs per call
 constexpr int64_t MAX_SPECS = (int64_t)1 << 26;
-inline int64_t clamp_rtiles(int64_t S) { return (S + 1 + CLAMP_RTILE - 1) / CLAMP_RTILE; }
-inline int64_t clamp_rows_max(int64_t S) { return S / 64 + 2; }
-inline int64_t clamp_h_cells(int64_t S) { return (S / 64 + 2) * (S + 1); }
-inline int64_t clamp_h2_cells(int64_t S) { return (S / 64 + 1) * 64 * 65; }
-#ifndef KCC_H_COPIES
-#define KCC_H_COPIES 8
+__host__ __device__ inline int64_t clamp_c_cells(int64_t S) { return (S / 64 + 3) * (S / 64 + 3); }
+inline int64_t clamp_h_cells(int64_t S) { return (S / 64 + 1) * 65 * 64; }
+#ifndef KCC_C_COPIES
+#define KCC_C_COPIES 8
 #endif
-constexpr int H_COPIES = KCC_H_COPIES;
+constexpr int C_COPIES = KCC_C_COPIES;
 #ifndef KCC_H2_COPIES
 #define KCC_H2_COPIES 2
 #endif
 constexpr int H2_COPIES = KCC_H2_COPIES;
-// up to this many specs the spec setup sorts in LDS (one workgroup) and node_prep's
-// search tables live in LDS; larger S takes the brute-force rank kernels and global
-// searches
+// up to this many specs node_prep's search and count tables live in LDS; larger S
+// searches the same tables in global memory
 #ifndef KCC_CLAMP_LDS_SPECS
 #define KCC_CLAMP_LDS_SPECS 4096
 #endif
@@ -194,20 +190,21 @@ enum {
   CNT_SLOW_ROWS = 4,   // + chunk: rows in that node chunk's slow_list
   CNT_N = 4 + FIT_MAX_CHUNKS
 };
-// Spec setup, three launches: brute-force ranks of every spec (64 queries per workgroup,
-// the candidates split over workgroups and waves) — by request for the clamp correction
-// and within its class for the stable 3-way partition; then one thread per spec places
-// SpecRec / perm and the sorted arrays (cs, ms, dperm, m_less); then one workgroup per
-// group of 64 c-ranks orders it by m_less (gml, kpos).  Zeroes partial[0..2S) and sets
-// the counters.
+// Spec setup, two launches.  spec_rank: brute-force x-ranks by (c, index) and y-ranks by
+// (m, index) (64 queries per workgroup, the candidates split over workgroups and waves,
+// atomics into rank[]) and the class counts per block of 64 specs.  spec_place (one
+// thread per spec): the stable 3-way partition position, the SpecRec / perm there and the
+// clamp correction's arrays (cs, ms, mr_c, cr_m, dperm); zeroes partial[0..2S), rank[] and
+// the call's cells of C, sets the counters.
 // mark != nullptr: the first launch also runs launch_reduce_mark's work for those args
 // (extra workgroups), so the caller skips launch_reduce_mark.
 hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
                             const int64_t* spec_mem, SpecPrep sp, ClampWork cw, int64_t* partial,
                             unsigned long long* counters, hipStream_t s,
                             const MarkArgs* mark = nullptr);
-// H, H2 -> D_s;  partial[s] -= D_s for the normal specs of clamp-free waves (after every
-// node_prep of the call, before the all-reduce); leaves H and H2 zero
+// The clamp correction after every node_prep of the call: clamp_prep (the tables summed
+// over their copies and zeroed, suffix sums) then clamp_query (partial[s] -= D_s for the
+// normal specs of clamp-free waves); leaves the table copies zero.
 hipError_t launch_clamp_apply(int64_t n_specs, ClampWork cw,
                               const unsigned long long* counters, int64_t* partial, hipStream_t s);
 

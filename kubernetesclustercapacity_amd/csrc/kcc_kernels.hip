@@ -405,7 +405,6 @@ __device__ __forceinline__ int64_t clamp_n_pure(int64_t nN, int64_t S) {
   return (nN % 64 == 0 || nN == S) ? nN : nN / 64 * 64;
 }
 
-// #{k < n : a[k] <= v} for a sorted ascending (binary search, n <= 2^31)
 // #{k < 4096 : a[k] <= v} for a sorted ascending (8-ary: after the step of width s the
 // answer lies in [lo, lo + s])
 template <class T>
@@ -422,6 +421,7 @@ __device__ __forceinline__ uint32_t search8_4096(const T* a, T v) {
   return lo;
 }
 
+// #{k < n : a[k] <= v} for a sorted ascending (binary search, n <= 2^31)
 template <class T>
 __device__ __forceinline__ uint32_t upper_bound_count(const T* __restrict__ a, int64_t n, T v) {
   int64_t lo = 0, hi = n;
@@ -433,14 +433,29 @@ __device__ __forceinline__ uint32_t upper_bound_count(const T* __restrict__ a, i
   return (uint32_t)lo;
 }
 
-// #{j < 64 : a[j] < b} for one group's ascending gml entries (0xffff / 0xffffffff pad)
-template <class T>
-__device__ __forceinline__ uint32_t group_count64(const T* a, uint32_t b) {
-  if ((uint32_t)a[63] < b) return 64;
-  uint32_t lo = 0;
+// #{l < 64 : a[l] < v} over one block of 64 entries (16-B aligned, padding >= every v):
+// the x-group / y-block counts of the clamp tables, unsorted, 64 compares
+__device__ __forceinline__ uint32_t count_lt64(const uint16_t* a, uint32_t v) {
+  const uint4* q = reinterpret_cast<const uint4*>(a);
+  uint32_t n = 0;
+#pragma unroll 2
+  for (int u = 0; u < 8; ++u) {
+    const uint4 w = q[u];
+    const uint32_t h[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-  for (uint32_t s = 32; s >= 1; s >>= 1) lo += (uint32_t)a[lo + s - 1] < b ? s : 0u;
-  return lo;
+    for (int e = 0; e < 4; ++e) n += ((h[e] & 0xffffu) < v ? 1u : 0u) + ((h[e] >> 16) < v ? 1u : 0u);
+  }
+  return n;
+}
+__device__ __forceinline__ uint32_t count_lt64(const uint32_t* __restrict__ a, uint32_t v) {
+  const uint4* q = reinterpret_cast<const uint4*>(a);
+  uint32_t n = 0;
+#pragma unroll 4
+  for (int u = 0; u < 16; ++u) {
+    const uint4 w = q[u];
+    n += (w.x < v ? 1u : 0u) + (w.y < v ? 1u : 0u) + (w.z < v ? 1u : 0u) + (w.w < v ? 1u : 0u);
+  }
+  return n;
 }
 
 // Per-node free capacity (CC:119-135 operands).  Rows that fit the fast-path
@@ -449,13 +464,14 @@ __device__ __forceinline__ uint32_t group_count64(const T* a, uint32_t b) {
 // appended to slow_list for the exact path.  Covers the padding of the last group too
 // (zero fields, not listed).  SlowNode records are written for the slow rows, and for
 // every row when exact-path specs exist (their waves walk all rows).  Clamp correction:
-// each fast row with P >= 1 adds its weight to one cell of H (full c-rank groups) and
-// one of H2 (its partial group), rows with P <= 0 to H[T][nN] (ClampWork).
+// each fast row with P >= 1 that dominates some spec adds its weight to at most one
+// cell each of C, H2 and H3; rows with P <= 0 to C[T+1][T+1] (ClampWork).
 #define KCC_NODE_PREP_BLOCK 1024
 static_assert(CLAMP_LDS_SPECS % KCC_NODE_PREP_BLOCK == 0, "node_prep table fill");
 #ifndef KCC_NODE_PREP_GRID
 #define KCC_NODE_PREP_GRID 512  // workgroups at most (2 per CU, one round; each fills its LDS tables once)
 #endif
+constexpr size_t NODE_PREP_LDS = 16 * (size_t)CLAMP_LDS_SPECS;  // cs u32, ms i64, 2 x u16
 __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_cpu,
                                  const int64_t* __restrict__ alloc_mem,
                                  const int64_t* __restrict__ alloc_pods,
@@ -469,47 +485,47 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   const int lane = threadIdx.x & 63;
   const int64_t n_pad = fit_groups(n) * FIT_GROUP;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const bool want_b = counters[CNT_SPECS_B] != 0;  // written by spec_prep (same stream)
+  const bool want_b = counters[CNT_SPECS_B] != 0;  // written by spec setup (same stream)
   const int64_t nN = clamp_n_normal(counters);     // normal specs (clamp correction)
   const bool slow_all = nN < S;                    // exact-path specs exist
-  const int64_t T = (nN + 63) / 64, hw = nN + 1;
-  // this workgroup's copies of H and H2: workgroups are dealt round-robin over the XCDs
-  int64_t* Hc = cw.H + (int64_t)(blockIdx.x % H_COPIES) * cw.h_stride;
-  int64_t* H2c = cw.H2 + (int64_t)(blockIdx.x % H2_COPIES) * cw.h2_stride;
-  // the sorted spec requests of the searches and the groups' m_less orders, in LDS when
-  // they fit: c clamped to 2^23 (> every U = fc / P, fc < 2^23) as u32, m as i64, the
-  // gml entries as u16 (< 4096, padding 0xffff)
+  const int64_t T = (nN + 63) / 64, W = T + 2;
+  // this workgroup's copies of the tables: workgroups are dealt round-robin over the XCDs
+  int64_t* Cc = cw.C + (int64_t)(blockIdx.x % C_COPIES) * cw.c_stride;
+  int64_t* H2c = cw.H2 + (int64_t)(blockIdx.x % H2_COPIES) * cw.h_stride;
+  int64_t* H3c = cw.H3 + (int64_t)(blockIdx.x % H2_COPIES) * cw.h_stride;
+  // the sorted spec requests of the searches and the x-group / y-block members, in LDS
+  // when they fit: c clamped to 2^23 (> every U = fc / P, fc < 2^23) as u32, m as i64,
+  // y-rank by x-rank and x-group by y-rank as u16 (padding 0xffff)
   extern __shared__ __attribute__((aligned(16))) unsigned char np_lds[];
   int64_t* ms_l = reinterpret_cast<int64_t*>(np_lds);
   uint32_t* cs_l = reinterpret_cast<uint32_t*>(np_lds + 8 * CLAMP_LDS_SPECS);
-  uint16_t* gml_l = reinterpret_cast<uint16_t*>(np_lds + 12 * CLAMP_LDS_SPECS);
+  uint16_t* mrc_l = reinterpret_cast<uint16_t*>(np_lds + 12 * CLAMP_LDS_SPECS);
+  uint16_t* xg_l = reinterpret_cast<uint16_t*>(np_lds + 14 * CLAMP_LDS_SPECS);
   const bool lds = S <= CLAMP_LDS_SPECS;
   // smallest normal requests (rows below either dominate no spec); cs[0] >= 1
   const uint32_t cmin = nN > 0 ? (cw.cs[0] < FAST_FC_MAX ? (uint32_t)cw.cs[0] : (uint32_t)FAST_FC_MAX)
                                : 0xffffffffu;
   const int64_t mmin = nN > 0 ? cw.ms[0] : INT64_MAX;
-#ifndef KCC_DIAG_NO_FILL  // diagnostic timing build only: results are wrong
   if (lds) {
-#else
-  if (false) {
-#endif
     // every load first (one memory round trip), then the LDS writes
     constexpr int PER = (int)(CLAMP_LDS_SPECS / KCC_NODE_PREP_BLOCK);
     uint64_t cv[PER], mv[PER];
-    uint32_t gv[PER];
+    uint32_t yv[PER], xv[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int64_t k = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
       cv[u] = k < nN ? cw.cs[k] : ~0ull;  // padded: +inf
       mv[u] = k < nN ? (uint64_t)cw.ms[k] : (uint64_t)INT64_MAX;
-      gv[u] = k < 64 * T ? cw.gml[k] : 0xffffffffu;
+      yv[u] = k < 64 * T ? cw.mr_c[k] : 0xffffffffu;
+      xv[u] = k < 64 * T ? cw.cr_m[k] : 0xffffffffu;
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int64_t k = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
       cs_l[k] = cv[u] < FAST_FC_MAX ? (uint32_t)cv[u] : 0xffffffffu;
       ms_l[k] = (int64_t)mv[u];
-      gml_l[k] = gv[u] < 0xffffu ? (uint16_t)gv[u] : (uint16_t)0xffffu;
+      mrc_l[k] = yv[u] < 0xffffu ? (uint16_t)yv[u] : (uint16_t)0xffffu;
+      xg_l[k] = xv[u] < 0xffffu ? (uint16_t)(xv[u] >> 6) : (uint16_t)0xffffu;
     }
   }
   __syncthreads();
@@ -576,10 +592,6 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
         const int64_t V = (int64_t)((double)fm_ok * rP);
         if (U >= cmin && V >= mmin) {  // else no spec is dominated
           uint32_t L, b;
-#ifdef KCC_DIAG_NO_SEARCH  // diagnostic timing build only: results are wrong
-          L = U % (uint32_t)(nN + 1);
-          b = (uint32_t)(V % (nN + 1));
-#else
           if (lds) {  // 8-ary searches over the +inf-padded 4096-entry tables: 4 steps of
                       // 7 independent LDS reads each (a binary search chains 12)
             L = search8_4096(cs_l, U);
@@ -588,26 +600,35 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
             L = upper_bound_count(cw.cs, nN, (uint64_t)U);
             b = upper_bound_count(cw.ms, nN, V);
           }
-#endif
-          const uint32_t G = L >> 6, r = L & 63u;  // L >= 1, b >= 1 (U >= cmin, V >= mmin)
-#ifndef KCC_DIAG_NO_H_ATOMIC  // diagnostic timing build only: results are wrong
-          if (G > 0) atomic_add_u64(reinterpret_cast<uint64_t*>(&Hc[G * hw + b]), (uint64_t)w);
-          if (r > 0) {
-            const uint32_t kq = lds ? group_count64(gml_l + 64 * G, b)
-                                    : group_count64(cw.gml + 64 * G, b);
-            if (kq > 0)
-              atomic_add_u64(reinterpret_cast<uint64_t*>(&H2c[((int64_t)G * 64 + r) * 65 + kq]),
+          // L >= 1, b >= 1 (U >= cmin, V >= mmin)
+          const uint32_t GX = L >> 6, rx = L & 63u, GY = b >> 6, ry = b & 63u;
+          if (GX > 0 && GY > 0)
+            atomic_add_u64(reinterpret_cast<uint64_t*>(&Cc[(int64_t)GX * W + GY]), (uint64_t)w);
+          if (rx > 0) {  // x-group GX: k = #{its specs with y < b}
+            const uint32_t k = lds ? count_lt64(mrc_l + 64 * GX, b) : count_lt64(cw.mr_c + 64 * GX, b);
+            if (k > 0)
+              atomic_add_u64(reinterpret_cast<uint64_t*>(&H2c[((int64_t)GX * 65 + k) * 64 + rx]),
                              (uint64_t)w);
           }
-#endif
+          if (ry > 0 && GX > 0) {  // y-block GY: j = #{its specs whose x-group < GX}
+            uint32_t j;
+            if (lds) {
+              j = count_lt64(xg_l + 64 * GY, GX);
+            } else {  // x >> 6 < GX  <=>  x < 64 GX (padding: never)
+              j = count_lt64(cw.cr_m + 64 * GY, GX << 6);
+            }
+            if (j > 0)
+              atomic_add_u64(reinterpret_cast<uint64_t*>(&H3c[((int64_t)GY * 65 + j) * 64 + ry]),
+                             (uint64_t)w);
+          }
         }
       }
     }
-    {  // rows clamped for every spec: one wave-summed atomic into H[T][nN]
+    {  // rows clamped for every spec: one wave-summed atomic into C[T+1][T+1]
       uint64_t v = always ? (uint64_t)w : 0ull;
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-      if (lane == 0 && v) atomic_add_u64(reinterpret_cast<uint64_t*>(&Hc[T * hw + nN]), v);
+      if (lane == 0 && v) atomic_add_u64(reinterpret_cast<uint64_t*>(&Cc[(T + 1) * W + T + 1]), v);
     }
     const unsigned long long bl = __ballot(valid && !ok);
     if (bl) {
@@ -632,253 +653,183 @@ __device__ __forceinline__ float recip_up_f32(uint64_t v) {
   return r;
 }
 
-// ---- spec setup: partition + ranks + sorted arrays, one launch --------------------
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return (uint64_t)hi << 32 | lo;
+}
+
+// ---- spec setup: ranks by counting, then one thread per spec places it -------------
 constexpr int SPEC_BLOCK = 1024;
 constexpr int SPEC_NW = SPEC_BLOCK / 64;
-constexpr int RANK_SLICES = 4;  // workgroups per block of 64 queries
+constexpr int64_t RANK_SLICE_MAX = 4096;  // candidates staged per workgroup (64 KiB)
 
-// Spec setup, three launches (the work is tiny: what costs is dependent memory round
-// trips and device-scope fences, so every thread does one step of one spec and the
-// kernel boundaries carry the results).
-//
-// spec_rank_kernel: (S/64) x RANK_SLICES workgroups of 1024 threads; lane = query spec i
-// (64 per workgroup), the candidates j split over the RANK_SLICES workgroups of a query
-// block, staged in LDS (S <= 8192: 64-bit keys request << 13 | index, one compare per
-// rank) and walked by the 16 waves with broadcast reads.  Per normal query (ties by
-// index):
-//   c-rank(i) = #{normal j : (c_j, j) < (c_i, i)},  m-rank(i) = #{normal j : (m_j, j) < (m_i, i)},
-//   m-less(i) = #{normal j : m_j < m_i},
-// and per query its rank within its class, #{j < i : class(j) == class(i)} (the stable
-// 3-way partition: class A, then B, then the exact-path specs); the waves' counts meet
-// in LDS, then one atomic per query and count into rank[] (zero between calls).  The
-// query block's first workgroup also writes the query's SpecRec by caller index (rec_o)
-// and zeroes its partial[] entries; the first query block counts the classes.
-// Workgroups from rank_blocks on run reduce_mark_body instead (the reduce's mark fused
-// into this launch: the two are independent, and one launch fewer sits on the step).
+// Candidates per slice: a power of two <= 4096 (so a slice never straddles the 8192-spec
+// chunks of the keys' 13-bit index field), about S / 4 (>= 4 workgroups per query block).
+__host__ __device__ inline int64_t rank_slice(int64_t S) {
+  int64_t L = 64;
+  while (L < RANK_SLICE_MAX && 4 * L < S) L *= 2;
+  return L;
+}
+
+// spec_rank_kernel: ceil(S/64) query blocks x ceil(S/L) slices, workgroups of 1024 threads;
+// lane = query spec i (64 per workgroup), the L candidates of the slice staged in LDS as
+// keys v << 13 | (j mod 8192) (v = c or m < 2^51; non-normal specs ~0) and walked by the 16
+// waves with broadcast 16-B reads.  Per normal query (ties by index):
+//   x(i) = #{normal j : (c_j, j) < (c_i, i)},   y(i) = #{normal j : (m_j, j) < (m_i, i)},
+// each slice counting keys below a threshold uniform over the slice: (v_i + 1) << 13 for
+// candidates in an earlier 8192-chunk than i (equal v sorts before), v_i << 13 | (i mod
+// 8192) in i's chunk, v_i << 13 in a later chunk.  The waves' counts meet in LDS, then one
+// atomic per query and rank into rank[] (zero between calls: spec_place zeroes what it
+// reads).  The first slice of a query block also stores the block's class-A / class-B
+// counts in bcnt[].  Workgroups from rank_blocks on run reduce_mark_body instead (the
+// reduce's mark fused into this launch: independent work, one launch fewer on the step).
 __global__ __launch_bounds__(SPEC_BLOCK) void spec_rank_kernel(int64_t S, const uint64_t* __restrict__ c_in,
                                                                const int64_t* __restrict__ m_in,
-                                                               SpecPrep sp, ClampWork cw,
-                                                               int64_t* __restrict__ partial,
-                                                               int64_t rank_blocks, MarkArgs mark) {
+                                                               ClampWork cw, int64_t rank_blocks,
+                                                               MarkArgs mark) {
   if ((int64_t)blockIdx.x >= rank_blocks) {  // workgroup-uniform, before any barrier
     reduce_mark_body((int64_t)blockIdx.x - rank_blocks, (int64_t)gridDim.x - rank_blocks, mark);
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  KCC_TL(blockIdx.x, 0);
-  constexpr int SLICE_LDS = (int)(8192 / RANK_SLICES);  // staged candidates (S <= 8192)
-  __shared__ uint64_t kc_l[SLICE_LDS], km_l[SLICE_LDS];
-  __shared__ uint8_t cls_l[SLICE_LDS];
-  __shared__ uint32_t part[SPEC_NW][4][64];
-  const int64_t qb = blockIdx.x / RANK_SLICES, sl = blockIdx.x % RANK_SLICES;
+  typedef uint64_t u64x2_t __attribute__((ext_vector_type(2)));
+  __shared__ u64x2_t key_l[RANK_SLICE_MAX];
+  __shared__ uint32_t part[SPEC_NW][2][64];
+  const int64_t L = rank_slice(S), ns = (S + L - 1) / L;
+  const int64_t qb = blockIdx.x / ns, sl = blockIdx.x % ns;
   const int64_t i = qb * 64 + lane;  // this lane's query
   const bool qv = i < S;
   const uint64_t c = qv ? c_in[i] : 0;
   const int64_t m = qv ? m_in[i] : 0;
   const int32_t ci = qv ? spec_class(c, m) : SPEC_EXACT;
-  const bool qn = qv && ci != SPEC_EXACT;
-  const int64_t j0 = S * sl / RANK_SLICES, j1 = S * (sl + 1) / RANK_SLICES;  // this slice
-  uint32_t rc = 0, rm = 0, ml = 0, cp = 0;
-  if (S <= 8192) {
-    uint32_t na = 0, nb = 0;
-    for (int64_t j = j0 + tid; j < j1; j += SPEC_BLOCK) {  // stage the slice's keys
-      const uint64_t cj = c_in[j];
-      const int64_t mj = m_in[j];
-      const int32_t kj = spec_class(cj, mj);
-      const bool nj = kj != SPEC_EXACT;
-      kc_l[j - j0] = nj ? cj << 13 | (uint64_t)j : ~0ull;
-      km_l[j - j0] = nj ? (uint64_t)mj << 13 | (uint64_t)j : ~0ull;
-      cls_l[j - j0] = (uint8_t)kj;
-      na += kj == SPEC_A ? 1u : 0u;
-      nb += kj == SPEC_B ? 1u : 0u;
+  const bool qn = ci != SPEC_EXACT;
+  if (sl == 0 && wv == 0) {  // this query block's class counts
+    const uint32_t na = (uint32_t)__popcll(__ballot(ci == SPEC_A));
+    const uint32_t nb = (uint32_t)__popcll(__ballot(ci == SPEC_B));
+    if (lane == 0) {
+      cw.bcnt[2 * qb] = na;
+      cw.bcnt[2 * qb + 1] = nb;
     }
-    if (qb == 0) {  // class totals, one atomic per wave and class
-      uint32_t ta = na, tb = nb;
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) {
-        ta += __shfl_xor(ta, d);
-        tb += __shfl_xor(tb, d);
-      }
-      if (lane == 0 && ta) atomicAdd(&cw.sync[1], ta);
-      if (lane == 0 && tb) atomicAdd(&cw.sync[2], tb);
-    }
-    __syncthreads();
-    const uint64_t kc = c << 13 | (uint64_t)i, km = (uint64_t)m << 13 | (uint64_t)i;
-    const uint64_t km0 = (uint64_t)m << 13;
-    const int n = (int)(j1 - j0);
-    const int w0 = n * wv / SPEC_NW, w1 = n * (wv + 1) / SPEC_NW;  // this wave's part
+  }
+  const int64_t j0 = sl * L, j1 = j0 + L < S ? j0 + L : S;  // this slice
+  for (int64_t j = j0 + tid; j < j1; j += SPEC_BLOCK) {  // stage the slice's keys
+    const uint64_t cj = c_in[j];
+    const int64_t mj = m_in[j];
+    const bool nj = spec_class(cj, mj) != SPEC_EXACT;
+    u64x2_t k;
+    k.x = nj ? cj << 13 | (uint64_t)(j & 8191) : ~0ull;
+    k.y = nj ? (uint64_t)mj << 13 | (uint64_t)(j & 8191) : ~0ull;
+    key_l[j - j0] = k;
+  }
+  __syncthreads();
+  const int64_t chq = i >> 13, chs = j0 >> 13;  // 8192-chunks of the query and the slice
+  const uint64_t tc = chs < chq ? (c + 1) << 13 : (chs == chq ? c << 13 | (uint64_t)(i & 8191) : c << 13);
+  const uint64_t tm = chs < chq ? ((uint64_t)m + 1) << 13
+                                : (chs == chq ? (uint64_t)m << 13 | (uint64_t)(i & 8191) : (uint64_t)m << 13);
+  const int n = (int)(j1 - j0);
+  const int w0 = n * wv / SPEC_NW, w1 = n * (wv + 1) / SPEC_NW;  // this wave's part
+  uint32_t rc = 0, rm = 0;
 #pragma unroll 4
-    for (int j = w0; j < w1; ++j) {
-      const uint64_t kcj = kc_l[j], kmj = km_l[j];  // broadcast reads
-      const int32_t kj = cls_l[j];
-      rc += kcj < kc ? 1u : 0u;
-      rm += kmj < km ? 1u : 0u;
-      ml += kmj < km0 ? 1u : 0u;
-      cp += (kj == ci && j0 + j < i) ? 1u : 0u;
-    }
-  } else {  // straight from memory (large S)
-    const int64_t n = j1 - j0;
-    uint32_t na = 0, nb = 0;
-    for (int64_t j = j0 + n * wv / SPEC_NW; j < j0 + n * (wv + 1) / SPEC_NW; ++j) {
-      const uint64_t cj = c_in[j];
-      const int64_t mj = m_in[j];
-      const int32_t kj = spec_class(cj, mj);
-      na += kj == SPEC_A ? 1u : 0u;
-      nb += kj == SPEC_B ? 1u : 0u;
-      cp += (kj == ci && j < i) ? 1u : 0u;
-      if (kj == SPEC_EXACT) continue;  // wave-uniform
-      rc += (cj < c || (cj == c && j < i)) ? 1u : 0u;
-      rm += (mj < m || (mj == m && j < i)) ? 1u : 0u;
-      ml += mj < m ? 1u : 0u;
-    }
-    if (qb == 0 && lane == 0) {  // wave-uniform counts
-      if (na) atomicAdd(&cw.sync[1], na);
-      if (nb) atomicAdd(&cw.sync[2], nb);
-    }
+  for (int j = w0; j < w1; ++j) {
+    const u64x2_t k = key_l[j];  // broadcast read
+    rc += k.x < tc ? 1u : 0u;
+    rm += k.y < tm ? 1u : 0u;
   }
   part[wv][0][lane] = rc;
   part[wv][1][lane] = rm;
-  part[wv][2][lane] = ml;
-  part[wv][3][lane] = cp;
   __syncthreads();
-  if (wv < 4 && qv && (qn || wv == 3)) {  // wave r adds count r (the class rank for all)
+  if (wv < 2 && qv && qn) {  // wave r adds count r
     uint32_t t = 0;
 #pragma unroll
     for (int k = 0; k < SPEC_NW; ++k) t += part[k][wv][lane];
     if (t) atomicAdd(&cw.rank[(int64_t)wv * S + i], t);
   }
-  if (sl == 0 && wv == 4 && qv) {  // the query's SpecRec fields, by caller index
-    SpecRec r;
-    r.c = c;
-    r.m = m;
-    r.rc = qn ? recip_up_f64(c) : 0.0;
-    r.rm = qn ? recip_up_f64((uint64_t)m) : 0.0;
-    r.rcf = ci == SPEC_A ? recip_up_f32(c) : 0.0f;
-    r.cls = ci;
-    r.pad = 0;
-    sp.rec_o[i] = r;
-  }
-  if (sl == 0 && wv == 5 && qv) {
-    partial[i] = 0;
-    partial[S + i] = 0;
-  }
-  KCC_TL(blockIdx.x, 1);
 }
 
-// spec_place_kernel: one thread per spec (caller index i): SpecRec / perm at the
-// partitioned position, and for the normal specs cs, dperm, m_less (by c-rank) and ms;
-// zeroes the spec's rank[] entries; thread 0 sets the counters.
-__global__ __launch_bounds__(256) void spec_place_kernel(int64_t S, SpecPrep sp, ClampWork cw,
+// spec_place_kernel: one thread per spec (caller index i), 64 * ceil(S / 64) threads (a
+// wave = a query block).  Partition position = class base + the class counts of the
+// earlier query blocks (bcnt) + the wave's ballot prefix.  Writes the SpecRec (with its
+// rounded-up reciprocals) and perm there, zeroes partial[i] and partial[S + i], and for
+// normal specs cs[x], ms[y], mr_c[x] = y, cr_m[y] = x, dperm[x] = position; zeroes its
+// rank[] entries; the threads [nN, 64 T) pad mr_c and cr_m; thread 0 sets the counters;
+// this call's cells of the clamp table C are zeroed (clamp_apply leaves them dirty).
+__global__ __launch_bounds__(256) void spec_place_kernel(int64_t S, const uint64_t* __restrict__ c_in,
+                                                         const int64_t* __restrict__ m_in,
+                                                         SpecPrep sp, ClampWork cw,
+                                                         int64_t* __restrict__ partial,
                                                          unsigned long long* __restrict__ counters) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t nA = cw.sync[1], nB = cw.sync[2];
+  const int lane = threadIdx.x & 63;
+  const int64_t nqb = (S + 63) / 64, qb = i >> 6;
+  const bool in = i < S;
+  const uint64_t c = in ? c_in[i] : 0;
+  const int64_t m = in ? m_in[i] : 0;
+  const int32_t cls = in ? spec_class(c, m) : SPEC_EXACT;
+  const bool normal = cls != SPEC_EXACT;
+  uint32_t x = 0, y = 0;
+  if (in && normal) {
+    x = cw.rank[i];
+    y = cw.rank[S + i];
+  }
+  // class totals and this block's prefix: the wave's lanes take every 64th block (the
+  // counts packed A | B << 32), then one DPP scan each
+  uint64_t tot = 0, pre = 0;
+  const uint64_t* bc = reinterpret_cast<const uint64_t*>(cw.bcnt);
+  for (int64_t b = lane; b < nqb; b += 64) {
+    const uint64_t v = bc[b];
+    tot += v;
+    pre += b < qb ? v : 0ull;
+  }
+  tot = readlane_u64(wave_incl_scan_u64(tot), 63);
+  pre = readlane_u64(wave_incl_scan_u64(pre), 63);
+  const uint32_t nA = (uint32_t)tot, nB = (uint32_t)(tot >> 32);
+  const uint32_t pA = (uint32_t)pre, pB = (uint32_t)(pre >> 32);
+  const int64_t nN = (int64_t)nA + nB;
+  const unsigned long long mA = __ballot(cls == SPEC_A && in), mB = __ballot(cls == SPEC_B && in);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  const uint32_t rA = (uint32_t)__popcll(mA & below), rB = (uint32_t)__popcll(mB & below);
+  if (i >= nN && i < (nN + 63) / 64 * 64) {  // padding of the last x-group / y-block
+    cw.mr_c[i] = 0xffffffffu;
+    cw.cr_m[i] = 0xffffffffu;
+  }
   if (i == 0) {
     for (int k = 0; k < CNT_N; ++k)
       counters[k] = k == CNT_SPECS_A ? (unsigned long long)nA
                   : k == CNT_SPECS_B ? (unsigned long long)nB : 0ull;
   }
-  if (i >= S) return;
-  typedef uint64_t u64x2_t __attribute__((ext_vector_type(2)));
-  const u64x2_t* rec_o = reinterpret_cast<const u64x2_t*>(sp.rec_o);
-  // a SpecRec moves as three 16-B words (c, m | rc, rm | rcf, cls, pad)
-  const u64x2_t w0 = rec_o[3 * i], w1 = rec_o[3 * i + 1], w2 = rec_o[3 * i + 2];
-  const uint32_t q = cw.rank[i], mr = cw.rank[S + i], ml = cw.rank[2 * S + i];
-  const uint32_t cp = cw.rank[3 * S + i];
-  const int32_t k = (int32_t)(w2.x >> 32);
-  const int64_t pos = k == SPEC_A ? cp : (k == SPEC_B ? nA + cp : (int64_t)nA + nB + cp);
-  u64x2_t* dst = reinterpret_cast<u64x2_t*>(sp.rec + pos);
-  dst[0] = w0;
-  dst[1] = w1;
-  dst[2] = w2;
+  {
+    const int64_t W = (nN + 63) / 64 + 2, cells = W * W;
+    for (int64_t e = i; e < C_COPIES * cells; e += (int64_t)gridDim.x * blockDim.x)
+      cw.C[(e / cells) * cw.c_stride + e % cells] = 0;
+  }
+  if (!in) return;
+  const int64_t pos = cls == SPEC_A ? (int64_t)pA + rA
+                    : cls == SPEC_B ? (int64_t)nA + pB + rB
+                                    : nN + (qb * 64 - pA - pB) + (lane - rA - rB);
+  SpecRec rec;
+  rec.c = c;
+  rec.m = m;
+  rec.rc = normal ? recip_up_f64(c) : 0.0;
+  rec.rm = normal ? recip_up_f64((uint64_t)m) : 0.0;
+  rec.rcf = cls == SPEC_A ? recip_up_f32(c) : 0.0f;
+  rec.cls = cls;
+  rec.pad = 0;
+  sp.rec[pos] = rec;
   sp.perm[pos] = (int32_t)i;
-  if (k != SPEC_EXACT) {
-    cw.cs[q] = w0.x;
-    cw.dperm[q] = (int32_t)pos;
-    cw.m_less[q] = ml;
-    cw.ms[mr] = (int64_t)w0.y;
-  }
-#pragma unroll
-  for (int r4 = 0; r4 < 4; ++r4) cw.rank[(int64_t)r4 * S + i] = 0;
-}
-
-// spec_groups_kernel: one 1024-thread workgroup per group g of 64 c-ranks: each spec's
-// position in the group's m_less order (keys m_less << 6 | lane), counted by 16 threads
-// over 4 candidates each: kpos by c-rank, gml (the group's m_less ascending, 0xffffffff
-// padding).  Workgroup 0 zeroes the class counts of spec_rank (read by spec_place).
-__global__ __launch_bounds__(1024) void spec_groups_kernel(ClampWork cw,
-                                                           const unsigned long long* __restrict__ counters) {
-  const int64_t nN = clamp_n_normal(counters);
-  const int64_t g = blockIdx.x;
-  if (g == 0 && threadIdx.x < 2) cw.sync[1 + threadIdx.x] = 0u;
-  if (g * 64 >= nN) return;  // whole block
-  __shared__ uint32_t key_l[64];
-  __shared__ uint32_t cnt_l[16][64];
-  const int tid = threadIdx.x, l = tid & 63, p = tid >> 6;
-  const uint32_t pad = (1u << 26) - 1;  // sorts last
-  if (tid < 64) {
-    const int64_t q = 64 * g + tid;
-    key_l[tid] = (q < nN ? cw.m_less[q] : pad) << 6 | (uint32_t)tid;
-  }
-  __syncthreads();
-  const uint32_t key = key_l[l];
-  uint32_t c = 0;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) c += key_l[4 * p + u] < key ? 1u : 0u;
-  cnt_l[p][l] = c;
-  __syncthreads();
-  if (tid < 64) {
-    uint32_t pos = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) pos += cnt_l[k][tid];
-    const int64_t q = 64 * g + tid;
-    if (q < nN) cw.kpos[q] = (uint8_t)pos;
-    cw.gml[64 * g + pos] = q < nN ? (key >> 6) : 0xffffffffu;
-  }
+  partial[i] = 0;
+  partial[S + i] = 0;
+  if (!normal) return;
+  cw.rank[i] = 0;
+  cw.rank[S + i] = 0;
+  cw.cs[x] = c;
+  cw.ms[y] = m;
+  cw.mr_c[x] = y;
+  cw.cr_m[y] = x;
+  cw.dperm[x] = (int32_t)pos;
 }
 
 // ---- clamp correction: D_s and partial[s] -= D_s ------------------------------------
-
-// Tile (G, t) of H (every copy summed, then zeroed) -> R[G][b] = Σ_{b' >= b in the tile}
-// H[G][b'] and Rtot[G][t] = the tile's total; grid (T+1, rtiles), 1024 threads.
-__global__ __launch_bounds__(1024) void clamp_rows_kernel(ClampWork cw,
-                                                          const unsigned long long* __restrict__ counters) {
-  const int64_t nN = clamp_n_normal(counters);
-  const int64_t G = blockIdx.x, t = blockIdx.y;
-  const int64_t T = (nN + 63) / 64, w = nN + 1;
-  if (nN == 0 || G > T || t * CLAMP_RTILE >= w) return;  // whole block
-  __shared__ uint64_t wtot[16];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  KCC_TL(2048 + (G * 8 + t) % 1024, 0);
-  const int64_t end = (t + 1) * CLAMP_RTILE < w ? (t + 1) * CLAMP_RTILE : w;
-  const int64_t i = end - 1 - tid;  // thread tid walks the tile backwards
-  const bool in = i >= t * CLAMP_RTILE;
-  uint64_t v = 0;
-  if (in) {
-    uint64_t h[H_COPIES];
-#pragma unroll
-    for (int c = 0; c < H_COPIES; ++c) h[c] = (uint64_t)cw.H[c * cw.h_stride + G * w + i];
-#pragma unroll
-    for (int c = 0; c < H_COPIES; ++c) {
-      v += h[c];
-      cw.H[c * cw.h_stride + G * w + i] = 0;  // zero between calls
-    }
-  }
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {  // inclusive scan in thread order = suffix in b
-    const uint64_t u = __shfl_up(v, d);
-    if (lane >= d) v += u;
-  }
-  if (lane == 63) wtot[wv] = v;
-  __syncthreads();
-  uint64_t before = 0, all = 0;
-  for (int k = 0; k < 16; ++k) {
-    if (k < wv) before += wtot[k];
-    all += wtot[k];
-  }
-  if (in) cw.R[G * w + i] = (int64_t)(v + before);
-  if (tid == 0) cw.Rtot[G * cw.rt_stride + t] = (int64_t)all;
-  KCC_TL(2048 + (G * 8 + t) % 1024, 1);
-}
 
 // inclusive suffix sum over the 64 lanes (lane k: Σ_{k' >= k})
 __device__ __forceinline__ uint64_t wave_suffix_u64(uint64_t v, int lane) {
@@ -890,115 +841,169 @@ __device__ __forceinline__ uint64_t wave_suffix_u64(uint64_t v, int lane) {
   return v;
 }
 
-// One workgroup per group g of 64 c-ranks: the group's H2 table (copies summed, then
-// zeroed) -> its 2-D suffix sums S2 in LDS; for each spec of the group (c-rank
-// q = 64g + l, kpos = its position in the group's m_less order)
-//   D = Σ_{G > g} R[G][m_less + 1]  +  S2[l + 1][kpos + 1],
-// R read as the in-tile suffix plus the totals of the later tiles; partial[p] -= D for
-// the normal specs of clamp-free waves.
-constexpr int CG_CELLS = 63 * 65;  // H2 rows r = 1..63
-constexpr int CG_PER = (CG_CELLS + 1023) / 1024;
-__global__ __launch_bounds__(1024) void clamp_groups_kernel(ClampWork cw,
-                                                            const unsigned long long* __restrict__ counters,
-                                                            int64_t S, int64_t* __restrict__ partial) {
+
+// ---- clamp correction: D_s and partial[s] -= D_s (one launch) ----------------------
+// clamp_apply_kernel: 2T workgroups of 1024 threads, after the fit.
+//   workgroup g < T (x-group g, the specs x = 64 g + l): H2[g] summed over its copies into
+//     LDS and the copies zeroed, its 2-D suffix sums S2[k][r] = Σ_{k' >= k, r' >= r} H2; the
+//     coarse part Σ_{G > g, GY > gy} C from the column sums of C's rows below g (LDS
+//     atomics) and one suffix scan (when (T+2)^2 <= C_FULL_CELLS; otherwise
+//     clamp_crows_kernel wrote C's row suffix sums to Crow and each lane sums its column);
+//     then for each spec (wave 0, lane l; y = mr_c[x], kpos = #{specs of the group with a
+//     smaller y}):  D_x = Csuf(g, y >> 6) + S2[kpos + 1][l + 1]  (r = 64 does not exist: 0);
+//   workgroup T + Y (y-block Y, the specs y = 64 Y + l): H3[Y] likewise -> S3; for each spec
+//     (x = cr_m[y], jpos = #{specs of the block with a smaller x}):  D_y = S3[jpos + 1][l + 1].
+// partial[dperm[x]] -= D_x and -= D_y (atomics: two workgroups touch one spec) for the
+// normal specs of clamp-free waves.  C's copies are read by every x-group and stay dirty:
+// the next call's spec_place zeroes them.  The scans are DPP (VALU), not lane shuffles.
+constexpr int CP_THREADS = 1024;
+constexpr int CP_WAVES = CP_THREADS / 64;
+constexpr int64_t C_FULL_CELLS = 4624;  // (T+2)^2 for T <= 66 (S <= 4224)
+constexpr int H_CELLS = 65 * 64;
+__host__ __device__ inline bool clamp_c_full(int64_t T) { return (T + 2) * (T + 2) <= C_FULL_CELLS; }
+
+__global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
+                                                                 const unsigned long long* __restrict__ counters,
+                                                                 int64_t S, int64_t* __restrict__ partial) {
+  __shared__ uint64_t tab[H_CELLS];
+  __shared__ uint64_t ctot[CP_WAVES][64];
+  __shared__ uint64_t colsum[128];
   const int64_t nN = clamp_n_normal(counters);
-  const int64_t T = (nN + 63) / 64, w = nN + 1;
-  const int64_t g = blockIdx.x;
-  if (g >= T) return;  // whole block
-  constexpr int NW = 16;
-  constexpr int MAX_RT = 64;  // tiles per row held in LDS (nN < 64 * CLAMP_RTILE)
-  __shared__ uint64_t t2[65][65];  // [r][k]; rows 0 and 64 stay 0
-  __shared__ uint64_t d1p[NW][64];
-  __shared__ uint64_t rts[65][MAX_RT + 1];  // per G <= T (of this call, G > g): Σ tiles > t
+  const int64_t T = (nN + 63) / 64, W = T + 2;
+  const int64_t u = blockIdx.x;
+  if (u >= 2 * T) return;  // whole workgroup
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  KCC_TL(1024 + g, 0);
-  const int64_t nt = (w + CLAMP_RTILE - 1) / CLAMP_RTILE;
-  {  // all copies of all this thread's cells first (independent loads), then the zeros
-    uint64_t v[CG_PER] = {};
+  const bool x_side = u < T;
+  const int64_t g = x_side ? u : u - T;
+  const bool full = clamp_c_full(T);
+  // this workgroup's 64 specs (wave 0), loaded up front
+  const int64_t q = 64 * g + lane;  // x (x side) or y (y side)
+  uint32_t other = 0xffffffffu;
+  if (wv == 0) other = (x_side ? cw.mr_c : cw.cr_m)[q];  // y of x, or x of y (padding: ~0)
+  if (tid < 128) colsum[tid] = 0;
+  // the table: every copy's cells first, then LDS and zeroes
+  int64_t* H = (x_side ? cw.H2 : cw.H3) + g * H_CELLS;
+  constexpr int PER = (H_CELLS + CP_THREADS - 1) / CP_THREADS;
+  uint64_t v[PER];
 #pragma unroll
-    for (int u = 0; u < CG_PER; ++u) {
-      const int cell = tid + 1024 * u;
-      if (cell < CG_CELLS) {
-        const int64_t at = g * 64 * 65 + 65 + cell;  // row r = 1 + cell / 65
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + CP_THREADS * k;
+    v[k] = 0;
 #pragma unroll
-        for (int c = 0; c < H2_COPIES; ++c) v[u] += (uint64_t)cw.H2[c * cw.h2_stride + at];
-      }
-    }
+    for (int c = 0; c < H2_COPIES; ++c) v[k] += e < H_CELLS ? (uint64_t)H[c * cw.h_stride + e] : 0ull;
+  }
+  // the coarse table's rows G > g (x side, C in the full form): loads first as well
+  constexpr int CPER = (int)((C_FULL_CELLS + CP_THREADS - 1) / CP_THREADS);
+  uint64_t cv[CPER];
+  const int64_t c0 = (g + 1) * W, c1 = W * W;  // cells of rows g+1 .. T+1
+  const bool do_c = x_side && full;
 #pragma unroll
-    for (int u = 0; u < CG_PER; ++u) {
-      const int cell = tid + 1024 * u;
-      if (cell < CG_CELLS) {
-        const int64_t at = g * 64 * 65 + 65 + cell;
+  for (int k = 0; k < CPER; ++k) {
+    const int64_t e = c0 + tid + CP_THREADS * k;
+    cv[k] = 0;
+    if (do_c && e < c1) {
 #pragma unroll
-        for (int c = 0; c < H2_COPIES; ++c) cw.H2[c * cw.h2_stride + at] = 0;  // zero between calls
-        t2[1 + cell / 65][cell % 65] = v[u];
-      }
-    }
-    if (tid < 65) {
-      t2[0][tid] = 0;
-      t2[64][tid] = 0;
+      for (int c = 0; c < C_COPIES; ++c) cv[k] += (uint64_t)cw.C[c * cw.c_stride + e];
     }
   }
-  const bool rts_lds = nt <= MAX_RT && T < 65;
-  if (rts_lds) {  // the later tiles' totals: one load per thread, then a suffix per row
-    for (int64_t e = tid; e < (T - g) * nt; e += 1024) {
-      const int64_t G = g + 1 + e / nt, t = e % nt;
-      rts[G][t] = (uint64_t)cw.Rtot[G * cw.rt_stride + t];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + CP_THREADS * k;
+    if (e < H_CELLS) {
+      tab[e] = v[k];
+#pragma unroll
+      for (int c = 0; c < H2_COPIES; ++c) H[c * cw.h_stride + e] = 0;  // zero between calls
     }
   }
-  // this lane's spec: its m_less, internal position and kpos, loaded up front
-  const int64_t q = 64 * g + lane;
-  const uint32_t ml = q < nN ? cw.m_less[q] : 0u;
-  const int32_t p_q = q < nN ? cw.dperm[q] : 0;
-  const uint32_t kp_q = q < nN ? cw.kpos[q] : 0u;
-  __syncthreads();
-  if (rts_lds && tid < 65 && tid > g && tid <= T) {  // rts[G][t] = Σ_{u > t} Rtot[G][u]
-    uint64_t run = 0;
-    for (int64_t t = nt - 1; t >= 0; --t) {
-      const uint64_t v = rts[tid][t];
-      rts[tid][t] = run;
-      run += v;
+  __syncthreads();  // tab and colsum's zeroes
+  if (do_c) {
+#pragma unroll
+    for (int k = 0; k < CPER; ++k) {
+      const int64_t e = c0 + tid + CP_THREADS * k;
+      if (e < c1 && cv[k]) atomicAdd(reinterpret_cast<unsigned long long*>(&colsum[e % W]), cv[k]);
     }
   }
-  __syncthreads();
-  KCC_TL(1024 + g, 1);
-  {  // full groups: Σ_{G > g} R[G][m_less + 1], the waves taking every NW-th G
-    uint64_t d = 0;
-    const int64_t b1 = (int64_t)ml + 1;
-    if (q < nN && b1 <= nN) {
-      const int64_t t1 = b1 / CLAMP_RTILE;
-      for (int64_t G = g + 1 + wv; G <= T; G += NW) {
-        d += (uint64_t)cw.R[G * w + b1];
-        if (rts_lds) {
-          d += rts[G][t1];
-        } else {
-          for (int64_t t = t1 + 1; t < nt; ++t) d += (uint64_t)cw.Rtot[G * cw.rt_stride + t];
-        }
-      }
-    }
-    d1p[wv][lane] = d;
-  }
-  for (int r = wv; r < 65; r += NW) {  // suffix over k within each row (k = 64 on top)
-    const uint64_t top = t2[r][64];
-    const uint64_t v = wave_suffix_u64(t2[r][lane], lane);
-    t2[r][lane] = v + top;
+  // rows of tab: suffix along r (lanes reversed, DPP inclusive scan)
+  for (int k = wv; k < 65; k += CP_WAVES) {
+    const uint64_t s = wave_incl_scan_u64(tab[k * 64 + 63 - lane]);
+    tab[k * 64 + 63 - lane] = s;
   }
   __syncthreads();
-  for (int k = wv; k < 65; k += NW) {  // suffix over r within each column (r = 64 on top)
-    const uint64_t top = t2[64][k];
-    const uint64_t v = wave_suffix_u64(t2[lane][k], lane);
-    t2[lane][k] = v + top;
+  // columns of tab: suffix along k, 16 chunks of 5 rows, then the later chunks' totals
+  constexpr int KCH = (65 + CP_WAVES - 1) / CP_WAVES;
+  const int k0 = wv * KCH, k1 = k0 + KCH < 65 ? k0 + KCH : 65;
+  uint64_t run = 0;
+  for (int k = k1 - 1; k >= k0; --k) {
+    run += tab[k * 64 + lane];
+    tab[k * 64 + lane] = run;
   }
+  ctot[wv][lane] = run;
   __syncthreads();
-  KCC_TL(1024 + g, 2);
-  if (wv == 0 && q < nN) {
-    const int32_t p = p_q;
-    if (p < clamp_n_pure(nN, S)) {
-      uint64_t d = t2[lane + 1][kp_q + 1];
-#pragma unroll
-      for (int k = 0; k < NW; ++k) d += d1p[k][lane];
-      if (d) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[p]), 0ull - d);
+  if (wv != 0) {
+    uint64_t later = 0;
+    for (int w2 = wv + 1; w2 < CP_WAVES; ++w2) later += ctot[w2][lane];
+    for (int k = k0; k < k1; ++k) tab[k * 64 + lane] += later;
+    __syncthreads();
+    return;
+  }
+  {
+    uint64_t later = 0;
+    for (int w2 = 1; w2 < CP_WAVES; ++w2) later += ctot[w2][lane];
+    for (int k = k0; k < k1; ++k) tab[k * 64 + lane] += later;
+  }
+  __syncthreads();  // every wave's column totals are in tab
+  // wave 0: the 64 specs
+  uint64_t csuf = 0;  // x side: Σ_{GY > gy} colsum[GY] per lane
+  if (do_c) {  // suffix of colsum over GY in place (W <= 68: two chunks from the top)
+    uint64_t carry = 0;
+    for (int ch = 1; ch >= 0; --ch) {
+      const int col = ch * 64 + 63 - lane;  // lanes reversed: an inclusive scan is the suffix
+      uint64_t s = col < W ? colsum[col] : 0ull;
+      s = wave_incl_scan_u64(s) + carry;
+      carry = readlane_u64(s, 63);
+      if (col < W) colsum[col] = s;
     }
+    const uint32_t gy1 = other == 0xffffffffu ? 0xffffffffu : (other >> 6) + 1;
+    csuf = gy1 < W ? colsum[gy1] : 0ull;
+  }
+  uint32_t pos = 0;
+  for (int l = 0; l < 64; ++l) pos += (uint32_t)__builtin_amdgcn_readlane((int)other, l) < other ? 1u : 0u;
+  if (q >= nN) return;
+  uint64_t d = csuf;
+  if (lane < 63) d += tab[(pos + 1) * 64 + lane + 1];
+  if (x_side && !full) {
+    const int64_t gy = other >> 6;
+    uint64_t part[8] = {};
+    for (int64_t G = g + 1; G <= T + 1; G += 8) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        part[r] += G + r <= T + 1 ? (uint64_t)cw.Crow[(G + r) * W + gy + 1] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) d += part[r];
+  }
+  const int32_t p = cw.dperm[x_side ? q : (int64_t)other];
+  if (d && p < clamp_n_pure(nN, S)) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[p]), 0ull - d);
+}
+
+// clamp_crows_kernel (only when C does not fit clamp_apply's full form): one wave per row
+// G of C: the copies summed and Crow[G][GY] = Σ_{GY' >= GY} C[G][GY'].
+__global__ __launch_bounds__(256) void clamp_crows_kernel(ClampWork cw,
+                                                          const unsigned long long* __restrict__ counters) {
+  const int64_t nN = clamp_n_normal(counters);
+  const int64_t T = (nN + 63) / 64, W = T + 2;
+  const int64_t G = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (nN == 0 || clamp_c_full(T) || G >= W) return;
+  uint64_t carry = 0;
+  for (int64_t ch = (W + 63) / 64 - 1; ch >= 0; --ch) {
+    const int64_t gy = ch * 64 + 63 - lane;  // lanes reversed: an inclusive scan is the suffix
+    uint64_t v = 0;
+#pragma unroll
+    for (int c = 0; c < C_COPIES; ++c) v += gy < W ? (uint64_t)cw.C[c * cw.c_stride + G * W + gy] : 0ull;
+    v = wave_incl_scan_u64(v) + carry;
+    carry = readlane_u64(v, 63);
+    if (gy < W) cw.Crow[G * W + gy] = (int64_t)v;
   }
 }
 
@@ -1067,6 +1072,9 @@ static_assert(FIT_SPW == 64 || FIT_SPW == 128 || FIT_SPW == 256, "FIT_SPW");
 constexpr int FIT_CHUNK_GROUPS = 128;  // 1024 nodes: |sum of contributions| <= 2^30 in i32
 #ifndef KCC_FIT_TARGET_BLOCKS
 #define KCC_FIT_TARGET_BLOCKS 32768
+#endif
+#ifndef KCC_FIT_MIN_GPB
+#define KCC_FIT_MIN_GPB 32  // node groups per workgroup at least (8-way shards: 8 -> 32 took 9 us off the fit)
 #endif
 
 __device__ __forceinline__ double f64_at(const i32x16& v, int k) {
@@ -1361,7 +1369,7 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
   hipLaunchKernelGGL(node_prep_kernel,
                      dim3(grid_for(fit_groups(n_nodes) * FIT_GROUP, KCC_NODE_PREP_BLOCK,
                                    KCC_NODE_PREP_GRID)),
-                     dim3(KCC_NODE_PREP_BLOCK), (size_t)(14 * CLAMP_LDS_SPECS), s,
+                     dim3(KCC_NODE_PREP_BLOCK), NODE_PREP_LDS, s,
                      n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu, used_mem,
                      fast_a, fast_b, slow, slow_list, n_specs, cw, counters, (int32_t)chunk);
   return hipGetLastError();
@@ -1371,27 +1379,27 @@ hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu, const int
                             SpecPrep sp, ClampWork cw, int64_t* partial,
                             unsigned long long* counters, hipStream_t s, const MarkArgs* mark) {
   if (n_specs <= 0) return hipSuccess;
-  const int64_t blocks = (n_specs + 63) / 64 * RANK_SLICES;
+  const int64_t L = rank_slice(n_specs);
+  const int64_t blocks = (n_specs + 63) / 64 * ((n_specs + L - 1) / L);
   const int64_t mblocks = mark && mark->n_nodes > 0 ? grid_for(mark->n_nodes, SPEC_BLOCK, 2048) : 0;
   if (blocks + mblocks > 0x7fffffffLL) return hipErrorInvalidValue;
   MarkArgs none{};
   hipLaunchKernelGGL(spec_rank_kernel, dim3((unsigned)(blocks + mblocks)), dim3(SPEC_BLOCK), 0, s,
-                     n_specs, spec_cpu, spec_mem, sp, cw, partial, blocks, mblocks ? *mark : none);
-  hipLaunchKernelGGL(spec_place_kernel, dim3(grid_for(n_specs, 256, 1 << 30)), dim3(256), 0, s,
-                     n_specs, sp, cw, counters);
-  hipLaunchKernelGGL(spec_groups_kernel, dim3((unsigned)((n_specs + 63) / 64)), dim3(1024), 0, s,
-                     cw, counters);
+                     n_specs, spec_cpu, spec_mem, cw, blocks, mblocks ? *mark : none);
+  hipLaunchKernelGGL(spec_place_kernel, dim3(grid_for((n_specs + 63) / 64 * 64, 256, 1 << 30)),
+                     dim3(256), 0, s, n_specs, spec_cpu, spec_mem, sp, cw, partial, counters);
   return hipGetLastError();
 }
 
 hipError_t launch_clamp_apply(int64_t n_specs, ClampWork cw,
                               const unsigned long long* counters, int64_t* partial, hipStream_t s) {
   if (n_specs <= 0) return hipSuccess;
-  const int64_t t_max = (n_specs + 63) / 64;
-  hipLaunchKernelGGL(clamp_rows_kernel, dim3((unsigned)(t_max + 1), (unsigned)clamp_rtiles(n_specs)),
-                     dim3(1024), 0, s, cw, counters);
-  hipLaunchKernelGGL(clamp_groups_kernel, dim3((unsigned)t_max), dim3(1024), 0, s, cw, counters,
-                     n_specs, partial);
+  const int64_t T = (n_specs + 63) / 64;  // >= this call's T (normal specs only)
+  if (!clamp_c_full(T))  // C's row suffix sums (the kernel exits when this call's C is full)
+    hipLaunchKernelGGL(clamp_crows_kernel, dim3((unsigned)((T + 2 + 3) / 4)), dim3(256), 0, s, cw,
+                       counters);
+  hipLaunchKernelGGL(clamp_apply_kernel, dim3((unsigned)(2 * T)), dim3(CP_THREADS), 0, s, cw,
+                     counters, n_specs, partial);
   return hipGetLastError();
 }
 
@@ -1411,7 +1419,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
   if (gy_target < 1) gy_target = 1;
   const int64_t grid_groups = fit_groups(grid_nodes > n_nodes ? grid_nodes : n_nodes);
   int64_t gpb = (grid_groups + gy_target - 1) / gy_target;
-  if (gpb < 8) gpb = 8;
+  if (gpb < KCC_FIT_MIN_GPB) gpb = KCC_FIT_MIN_GPB;
   int64_t gy = (n_groups + gpb - 1) / gpb;
   // 1-D grid of gx * roundup(gy, 8) workgroups, remapped XCD-aware in the kernel; the
   // buffer descriptor of a block's groups needs gpb * 160 B < 2^31

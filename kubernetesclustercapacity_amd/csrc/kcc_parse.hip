@@ -271,9 +271,11 @@ __device__ __forceinline__ int64_t bytes_value(P s, int n, int8_t& st) {
 // algorithm — apimachinery is not vendored and its version is unpinned (DESIGN.md §4.6:
 // parity unpinned): [+-] digits [. digits] then a suffix — "", Ki..Ei (2^10k), n u m k M
 // G T P E (10^3k), or e/E<int64> (10^int32(exp)); parse errors (ErrFormatWrong /
-// ErrSuffix) -> PARSE_ERR.  The amount is capped at 2^63 - 1 in magnitude and Value()
-// rounds up away from zero: v = sign * min(ceil(|x|), 2^63 - 1).  Binary suffixes with a
-// fraction are exact for <= 19 significant digits (else PARSE_UNSUPPORTED).
+// ErrSuffix) -> PARSE_ERR.  Value() rounds up away from zero; binary amounts are capped at
+// 2^63 - 1 (ParseQuantity caps only BinarySI): v = sign * min(ceil(|x|), 2^63 - 1).
+// PARSE_UNSUPPORTED: a decimal amount beyond 2^63 - 1 (k8s wraps it, path-dependent), a
+// negative amount off ParseQuantity's int64 fast path (rounding not pinned), and binary
+// suffixes with a fraction of more than 19 significant digits.
 __device__ __forceinline__ bool mul10_sat(uint64_t& v, uint32_t d) {  // v = v*10 + d, false on > 2^63-1
   const uint64_t lim = 0x7fffffffffffffffull;
   if (v > (lim - d) / 10u) return false;
@@ -420,12 +422,31 @@ __device__ __forceinline__ int64_t quantity_value(P s, int n, int8_t& st) {
       else I = (uint64_t)Q;
     }
   }
+  // ParseQuantity's int64 fast path: <= 18 digits at a scale >= -9 (decimal suffixes), no
+  // fraction and 14 - 3k digits at most (2^10k)
+  const int nnum = num1 - num0, nden = den1 - den0;
+  const bool fast = binary ? (nden == 0 && nnum <= 14 - 3 * (bexp / 10))
+                           : (nnum + nden <= 18 && e10 - nden >= -9);
   uint64_t mag;
   if (over) {
-    mag = MAXV;  // capped at maxAllowed
+    if (!binary) {  // a decimal amount beyond 2^63 - 1: k8s wraps it (path-dependent)
+      st = PARSE_UNSUPPORTED;
+      return 0;
+    }
+    mag = MAXV;  // binary amounts are capped at maxAllowed
   } else {
     mag = I + (frac ? 1u : 0u);  // rounded up away from zero
-    if (mag > MAXV) mag = MAXV;
+    if (mag > MAXV) {
+      if (!binary) {
+        st = PARSE_UNSUPPORTED;
+        return 0;
+      }
+      mag = MAXV;
+    }
+  }
+  if (neg && !fast && mag != 0) {  // off the int64 path, negative: rounding not pinned
+    st = PARSE_UNSUPPORTED;
+    return 0;
   }
   st = PARSE_OK;
   return neg ? -(int64_t)mag : (int64_t)mag;
@@ -707,13 +728,12 @@ __global__ __launch_bounds__(PS_THREADS) void parse_quantity_kernel(int64_t n, c
         const bool ok = okh && okl;
         if (ok) {
           const uint64_t D = hiv * 100000000ull + lov;  // < 10^13
-          uint64_t mag;
-          if (bexp)
-            mag = D > (MAXV >> bexp) ? MAXV : D << bexp;
-          else
-            mag = D > lim10 ? MAXV : D * m10;
-          v = (int64_t)mag;
-          st = PARSE_OK;
+          // binary amounts capped at 2^63 - 1; a decimal one beyond it is unsupported
+          // (k8s wraps it)
+          const bool dec_over = !bexp && D > lim10;
+          const uint64_t mag = bexp ? (D > (MAXV >> bexp) ? MAXV : D << bexp) : D * m10;
+          v = dec_over ? 0 : (int64_t)mag;
+          st = dec_over ? PARSE_UNSUPPORTED : PARSE_OK;
           done = true;
         }
       }

@@ -5,12 +5,18 @@ unpinned -> parity unpinned) — test infrastructure for kcc_parse_quantity.
 parseQuantityString: [+-], leading zeros, numerator digits, optional '.' + denominator
 digits, then a suffix of "eEinumkKMGTP" letters, an optional sign and digits, to the end
 (else ErrFormatWrong).  interpret: "" | Ki..Ei (2^10k) | n u m k M G T P E (10^3k) |
-e/E<ParseInt64> (10^int32(exp)) (else ErrSuffix).  The amount is capped at 2^63 - 1 in
-magnitude (maxAllowed) and Value() rounds up away from zero.  Exact rationals throughout.
+e/E<ParseInt64> (10^int32(exp)) (else ErrSuffix).  Value() rounds up away from zero;
+binary (Ki..Ei) amounts are capped at 2^63 - 1 in magnitude (ParseQuantity caps only
+BinarySI at maxAllowed).  Two cases the engine reports as UNSUP (its "outside the exact
+domain" status) instead of guessing: a decimal amount beyond 2^63 - 1 (k8s wraps it, in a
+way that depends on which of ParseQuantity's two representations it takes), and a
+negative nonzero amount that leaves ParseQuantity's int64 fast path (<= 18 digits and a
+scale >= -9 for decimal suffixes; no fraction and few enough digits for binary ones),
+whose Value() rounding is not pinned.  Exact rationals throughout.
 """
 from fractions import Fraction
 
-OK, ERR = 1, 0
+OK, ERR, UNSUP = 1, 0, -1
 MAXV = (1 << 63) - 1
 _BIN = {"Ki": 10, "Mi": 20, "Gi": 30, "Ti": 40, "Pi": 50, "Ei": 60}
 _DEC = {"n": -9, "u": -6, "m": -3, "": 0, "k": 3, "M": 6, "G": 9, "T": 12, "P": 15, "E": 18}
@@ -60,23 +66,31 @@ def value(s: str):
         return 0, ERR
     suf = s[suf0:]
     x = Fraction(int(num or "0") * 10 ** len(den) + int(den or "0"), 10 ** len(den))
-    if suf in _BIN:
+    binary = suf in _BIN
+    if binary:
         x *= 2 ** _BIN[suf]
+        fast = len(den) == 0 and len(num) <= 14 - 3 * (_BIN[suf] // 10)
     elif suf in _DEC:
         x *= Fraction(10) ** _DEC[suf]
+        fast = len(num) + len(den) <= 18 and _DEC[suf] - len(den) >= -9
     elif len(suf) > 1 and suf[0] in "eE":
         e = _go_parse_int64(suf[1:])
         if e is None:
             return 0, ERR
         e = (e + (1 << 31)) % (1 << 32) - (1 << 31)  # int32(parsed)
+        fast = len(num) + len(den) <= 18 and e - len(den) >= -9
         if e > 400 and x != 0:
-            x = Fraction(MAXV + 1)  # beyond the cap anyway
+            x = Fraction(MAXV + 1)  # beyond 2^63 - 1 anyway
         elif e < -400:
             x = Fraction(1, 10 ** 400) if x != 0 else Fraction(0)  # rounds up to 1 anyway
         else:
             x *= Fraction(10) ** e
     else:
         return 0, ERR
+    if not binary and x > MAXV:
+        return 0, UNSUP
+    if neg and not fast and x != 0:
+        return 0, UNSUP
     if x > MAXV:
         x = Fraction(MAXV)
     mag = -((-x.numerator) // x.denominator)  # ceil

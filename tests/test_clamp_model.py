@@ -6,39 +6,28 @@ w = P - cl (= podCount) wherever x >= P.  The correction subtracts, per spec,
 
     D_s = Σ_i w_i [x_is >= P_i]
 
-computed as a 2-D dominance count: x >= P <=> c_s <= U_i = fc_i // P_i and
-m_s <= V_i = fm_i // P_i (P_i >= 1; P_i <= 0 rows are clamped for every spec).  This
-module restates the kernels' algorithm in numpy — c-ranks in groups of 64, the
-(T+1) x (nN+1) table H of fully covered groups read through its row suffix sums R
-(clamp_rows_kernel), and per group the 64 x 65 table H2 of partially covered groups
-indexed by (r, k), k = #{group specs with m_less < b}, read through its 2-D suffix sums
-(clamp_groups_kernel) — and checks it against the direct definition, then the whole
-per-spec total against the C oracle.
+computed as a 2-D dominance sum: x >= P <=> c_s <= U_i = fc_i // P_i and
+m_s <= V_i = fm_i // P_i (P_i >= 1; P_i <= 0 rows are clamped for every spec).  With
+the normal specs ranked by (c, index) -> x_s and by (m, index) -> y_s (permutations of
+0..nN-1), node i dominates exactly the specs with x_s < L_i and y_s < b_i (L_i = #{c <=
+U_i}, b_i = #{m <= V_i}).  Both axes are cut into blocks of 64 ranks (T blocks):
+  - coarse table C[L_i >> 6][b_i >> 6] ((T+2)^2; P <= 0 rows in the extra last cell),
+    read through its 2-D suffix sums at (x_s >> 6) + 1, (y_s >> 6) + 1;
+  - x-group table H2[g][r][k] (T x 65 x 65) for the rows with L_i >> 6 == g (r = L_i & 63,
+    k = #{specs of x-group g with y < b_i}), read at (x_s & 63) + 1, kpos_s + 1 (kpos_s =
+    #{specs of s's x-group with y < y_s});
+  - y-block table H3[Y][r][j] for the rows with b_i >> 6 == Y (r = b_i & 63, j = #{specs of
+    y-block Y whose x-group < L_i >> 6}), read at (y_s & 63) + 1, jpos_s + 1 (jpos_s =
+    #{specs of s's y-block with x < x_s}).
+All three are linear in S (the earlier (T+1) x (nN+1) table grew as S^2/64).  This module
+restates that algorithm in numpy and checks it against the direct definition, then the
+whole per-spec total against the C oracle.
 """
 import numpy as np
 import pytest
 
 # uint64 sums wrap on purpose (Go's int64 arithmetic)
 pytestmark = pytest.mark.filterwarnings("ignore:overflow encountered:RuntimeWarning")
-
-INF32 = 0xFFFFFFFF
-
-
-def group_orders(mlq, nN):
-    """spec_prep_kernel / clamp_group_kernel: per group of 64 c-ranks, each spec's
-    position in the group's m_less order (ties by lane) and the ascending m_less list."""
-    T = (nN + 63) // 64
-    kpos = np.zeros(nN, np.int64)
-    gml = np.full(64 * T, INF32, np.int64)
-    for g in range(T):
-        v = np.full(64, INF32, np.int64)
-        n = min(64, nN - 64 * g)
-        v[:n] = mlq[64 * g: 64 * g + n]
-        pos = np.empty(64, np.int64)
-        pos[np.lexsort((np.arange(64), v))] = np.arange(64)
-        kpos[64 * g: 64 * g + n] = pos[:n]
-        gml[64 * g + pos] = v
-    return kpos, gml
 
 
 def suffix2(a):
@@ -51,41 +40,47 @@ def clamp_correction(U, V, w, always, c, m):
     """D_s for every spec by the kernels' algorithm (numpy, exact int64 wrap)."""
     nN = c.size
     T = (nN + 63) // 64
-    order_c = np.lexsort((np.arange(nN), c))          # c-rank -> spec (ties by position)
-    cs = c[order_c]
-    ms = np.sort(m, kind="stable")
-    mlq = np.searchsorted(ms, m, side="left")[order_c]  # by c-rank: #specs with a smaller m
-    kpos, gml = group_orders(mlq, nN)
-    H = np.zeros((T + 1, nN + 1), np.uint64)
-    H2 = np.zeros((T, 65, 65), np.uint64)             # [G][r][k], rows r = 0 and 64 empty
+    idx = np.arange(nN)
+    order_c = np.lexsort((idx, c))                    # x-rank -> spec
+    order_m = np.lexsort((idx, m))                    # y-rank -> spec
+    x = np.empty(nN, np.int64)
+    x[order_c] = idx
+    y = np.empty(nN, np.int64)
+    y[order_m] = idx
+    cs, ms = c[order_c], m[order_m]
+    y_by_x = y[order_c]                               # spec_place: mr_c
+    x_by_y = x[order_m]                               # spec_place: cr_m
+    C = np.zeros((T + 2, T + 2), np.uint64)
+    H2 = np.zeros((T, 65, 65), np.uint64)             # [g][r][k]
+    H3 = np.zeros((T, 65, 65), np.uint64)             # [Y][r][j]
     for Ui, Vi, wi, al in zip(U, V, w, always):
         wi = np.uint64(np.int64(wi).view(np.uint64))
         if al:
-            H[T, nN] += wi
+            C[T + 1, T + 1] += wi
             continue
         L = int(np.searchsorted(cs, Ui, side="right"))
         b = int(np.searchsorted(ms, Vi, side="right"))
         if L == 0 or b == 0:
             continue
-        G, r = L >> 6, L & 63
-        if G:
-            H[G, b] += wi
-        if r:
-            k = int((gml[64 * G: 64 * G + 64] < b).sum())
+        GX, rx, GY, ry = L >> 6, L & 63, b >> 6, b & 63
+        C[GX, GY] += wi
+        if rx:                                        # node_prep: count over the x-group
+            k = int((y_by_x[64 * GX: 64 * GX + 64] < b).sum())
             if k:
-                H2[G, r, k] += wi
-    R = H[:, ::-1].cumsum(axis=1, dtype=np.uint64)[:, ::-1]   # clamp_rows_kernel
-    S2 = suffix2(H2)                                          # clamp_groups_kernel
+                H2[GX, rx, k] += wi
+        if ry and GX:                                 # count over the y-block
+            j = int(((x_by_y[64 * GY: 64 * GY + 64] >> 6) < GX).sum())
+            if j:
+                H3[GY, ry, j] += wi
+    Cs = suffix2(C)
+    S2, S3 = suffix2(H2), suffix2(H3)
     D = np.zeros(nN, np.uint64)
-    for q in range(nN):
-        s = order_c[q]
-        g, lane = q >> 6, q & 63
-        b1 = mlq[q] + 1
-        d = np.uint64(0)
-        if b1 <= nN:
-            d += R[g + 1:, b1].sum(dtype=np.uint64)
-        d += S2[g, lane + 1, kpos[q] + 1]
-        D[s] = d
+    for s in range(nN):
+        xs, ys = int(x[s]), int(y[s])
+        gx, gy = xs >> 6, ys >> 6
+        kpos = int((y_by_x[64 * gx: 64 * gx + 64] < ys).sum())
+        jpos = int((x_by_y[64 * gy: 64 * gy + 64] < xs).sum())
+        D[s] = Cs[gx + 1, gy + 1] + S2[gx, (xs & 63) + 1, kpos + 1] + S3[gy, (ys & 63) + 1, jpos + 1]
     return D.view(np.int64)
 
 
@@ -95,7 +90,7 @@ def direct(U, V, w, always, c, m):
 
 
 @pytest.mark.parametrize("seed,n,s", [(0, 3000, 1), (1, 2000, 63), (2, 2000, 64), (3, 2500, 130),
-                                      (4, 1500, 257)])
+                                      (4, 1500, 257), (5, 1200, 640), (6, 800, 1031)])
 def test_dominance_matches_definition(seed, n, s):
     rng = np.random.default_rng(seed)
     c = rng.integers(1, 300, s)
