@@ -428,16 +428,24 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   }
   // k == 1: the reduce's mark runs as extra workgroups of the first spec-setup launch
   // (same stream, independent work: one launch fewer on the step)
-  const bool fuse_mark = k == 1 && n_specs > 0 && n_nodes > 0;
+  // k == 1: the reduce's mark runs as extra workgroups of the spec-rank launch, and
+  // spec_place as extra workgroups of the reduce launch (same stream, independent work:
+  // two launches fewer on the step); the reduce leaves spec_place's wave slots free
+  const bool fuse = k == 1 && n_specs > 0 && n_nodes > 0;
+  kcc::PlaceArgs pa{};
+  if (fuse)
+    pa = kcc::PlaceArgs{n_specs, spec_cpu, spec_mem, spec_prep_of(dv), clamp_of(dv), partial,
+                        as<unsigned long long>(dv.counters), kcc::place_blocks(n_specs)};
+  const int64_t reserve = (int64_t)kcc::RED_WAVES_PER_BLOCK * pa.n_blocks;
   if (n_specs > 0) {  // spec partition on s (concurrent with the first reduce when k > 1)
     rc = clamp_clean(ctx, dv, s);
     if (rc) return rc;
     dv.clamp_dirty = true;  // until every kernel that leaves the tables zero is queued
     const kcc::MarkArgs ma = kcc::mark_args(n_nodes, 0, n_cont, ptr, as<int64_t>(dv.wave_node),
-                                            used_cpu, used_mem, nullptr, nullptr);
+                                            used_cpu, used_mem, nullptr, nullptr, reserve);
     KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv),
                                        clamp_of(dv), partial, as<unsigned long long>(dv.counters),
-                                       s, fuse_mark ? &ma : nullptr));
+                                       s, fuse ? &ma : nullptr, !fuse));
   }
   for (int c = 0; c < k; ++c) {
     const int64_t n = hi[c] - lo[c];
@@ -447,13 +455,13 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
       KCC_HIP(ctx, prof_event(dv, &pp.b));
       KCC_HIP(ctx, hipEventRecord(pp.a, rs));
     }
-    if (!fuse_mark)
+    if (!fuse)
       KCC_HIP(ctx, kcc::launch_reduce_mark(n, c0[c], c1[c] - c0[c], ptr + lo[c],
                                            as<int64_t>(dv.wave_node), used_cpu + lo[c],
                                            used_mem + lo[c], nullptr, nullptr, rs));
     KCC_HIP(ctx, kcc::launch_reduce(n, c0[c], c1[c] - c0[c], ptr + lo[c], cpu, mem, nullptr,
                                     nullptr, as<int64_t>(dv.wave_node), used_cpu + lo[c],
-                                    used_mem + lo[c], nullptr, nullptr, rs));
+                                    used_mem + lo[c], nullptr, nullptr, rs, fuse ? &pa : nullptr));
     if (dv.prof_on) {
       KCC_HIP(ctx, hipEventRecord(pp.b, rs));
       pp.kind = 0;

@@ -6,6 +6,8 @@
 
 namespace kcc {
 
+struct PlaceArgs;  // below: spec_place's work, fused into a reduce launch
+
 // ---- (a) segmented request reduce -------------------------------------------
 // One wavefront owns a contiguous range of reduce_range() containers and walks it in
 // tiles of RED_TILE (RED_IPL containers per lane: two 16-B loads per lane per array).
@@ -27,9 +29,11 @@ constexpr int64_t RED_MAX_NODES = (int64_t)1 << 28;
 // of 6144 resident waves).  Small inputs get one tile per wave.  `limits` selects the
 // 4-array kernel (more registers, fewer resident waves).  Both reduce launches of a call
 // use the same range.
-int32_t reduce_range(int64_t n_containers, bool limits);
-inline int64_t reduce_n_waves(int64_t n_containers, bool limits) {
-  const int64_t r = reduce_range(n_containers, limits);
+// reserve_waves: resident wave slots left to other work of the same launch (spec_place
+// workgroups in front of the reduce's)
+int32_t reduce_range(int64_t n_containers, bool limits, int64_t reserve_waves = 0);
+inline int64_t reduce_n_waves(int64_t n_containers, bool limits, int64_t reserve_waves = 0) {
+  const int64_t r = reduce_range(n_containers, limits, reserve_waves);
   return (n_containers + r - 1) / r;
 }
 // workspace bound for wave_node (shortest range)
@@ -52,16 +56,20 @@ struct MarkArgs {
 };
 MarkArgs mark_args(int64_t n_nodes, int64_t c0, int64_t n_containers, const int64_t* node_ptr,
                    int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu,
-                   int64_t* lim_mem);
+                   int64_t* lim_mem, int64_t reserve_waves = 0);
 hipError_t launch_reduce_mark(int64_t n_nodes, int64_t c0, int64_t n_containers,
                               const int64_t* node_ptr, int64_t* wave_node, uint64_t* used_cpu,
                               int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s);
 
+// place != nullptr (with place->n_blocks > 0): spec_place runs as that many extra
+// workgroups of this launch (the mark must then have been computed with the same
+// reserve_waves = 4 * n_blocks).
 hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, const int64_t* node_ptr,
                          const uint64_t* cpu_req, const int64_t* mem_req,
                          const uint64_t* cpu_lim, const int64_t* mem_lim,
                          const int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem,
-                         uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s);
+                         uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s,
+                         const PlaceArgs* place = nullptr);
 
 // ---- (b) fit -----------------------------------------------------------------
 // Node streams of the fit kernel: groups of FIT_GROUP nodes, field-major inside the
@@ -178,6 +186,20 @@ constexpr int H2_COPIES = KCC_H2_COPIES;
 #endif
 constexpr int64_t CLAMP_LDS_SPECS = KCC_CLAMP_LDS_SPECS;
 
+// spec_place's work (one thread per spec), run as extra workgroups in front of a reduce
+// launch (launch_reduce with a PlaceArgs) or as a launch of its own
+struct PlaceArgs {
+  int64_t S;
+  const uint64_t* c_in;
+  const int64_t* m_in;
+  SpecPrep sp;
+  ClampWork cw;
+  int64_t* partial;
+  unsigned long long* counters;
+  int32_t n_blocks;  // 256-thread workgroups (0: none)
+};
+inline int32_t place_blocks(int64_t S) { return (int32_t)((S + 255) / 256); }
+
 // counters (CNT_*): exact-path (node, spec) pairs, class-B specs, and per node chunk
 // of a pipelined call (kcc_capacity_partial_async) the rows in that chunk's slow_list.
 // spec_prep zeroes partial[0..2S) and the counters; node_prep appends to slow_list.
@@ -198,10 +220,11 @@ enum {
 // the call's cells of C, sets the counters.
 // mark != nullptr: the first launch also runs launch_reduce_mark's work for those args
 // (extra workgroups), so the caller skips launch_reduce_mark.
+// with_place = false: the caller runs spec_place inside its reduce launch (PlaceArgs).
 hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
                             const int64_t* spec_mem, SpecPrep sp, ClampWork cw, int64_t* partial,
                             unsigned long long* counters, hipStream_t s,
-                            const MarkArgs* mark = nullptr);
+                            const MarkArgs* mark = nullptr, bool with_place = true);
 // The clamp correction after every node_prep of the call: clamp_prep (the tables summed
 // over their copies and zeroed, suffix sums) then clamp_query (partial[s] -= D_s for the
 // normal specs of clamp-free waves); leaves the table copies zero.

@@ -157,6 +157,8 @@ __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff
 constexpr uint32_t RED_OOB_OFFSET = 0x7ffffff0u;  // > any output's range (n_nodes < 2^28)
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+__device__ void spec_place_body(const PlaceArgs& pa, int64_t blk);
+
 template <int NA>
 __global__ __launch_bounds__(256)
 #ifdef KCC_RED_WAVES_PER_EU
@@ -167,11 +169,17 @@ void reduce_kernel(
     const uint64_t* __restrict__ in0, const uint64_t* __restrict__ in1,
     const uint64_t* __restrict__ in2, const uint64_t* __restrict__ in3,
     const int64_t* __restrict__ wave_node, uint64_t* __restrict__ out0,
-    uint64_t* __restrict__ out1, uint64_t* __restrict__ out2, uint64_t* __restrict__ out3) {
+    uint64_t* __restrict__ out1, uint64_t* __restrict__ out2, uint64_t* __restrict__ out3,
+    PlaceArgs pa) {
   __shared__ __attribute__((aligned(16))) uint64_t pre_s[RED_WAVES_PER_BLOCK][NA][RED_TILE];
+  if ((int32_t)blockIdx.x < pa.n_blocks) {  // spec_place's workgroups, in front
+    spec_place_body(pa, blockIdx.x);
+    return;
+  }
   const int lane = threadIdx.x & 63;
   // wave index made provably uniform (T20: no waterfall loops around the buffer ops)
-  const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)(blockIdx.x * RED_WAVES_PER_BLOCK +
+  const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)((blockIdx.x - pa.n_blocks) *
+                                                             RED_WAVES_PER_BLOCK +
                                                              (threadIdx.x >> 6)));
   // containers [c0, n_cont): absolute indices, like the offsets in ptr (node indices
   // are local to the launch)
@@ -467,6 +475,18 @@ __device__ __forceinline__ uint32_t count_lt64(const uint32_t* __restrict__ a, u
 // each fast row with P >= 1 that dominates some spec adds its weight to at most one
 // cell each of C, H2 and H3; rows with P <= 0 to C[T+1][T+1] (ClampWork).
 #define KCC_NODE_PREP_BLOCK 1024
+// diagnostic timing builds only (results are wrong): KCC_DIAG_NP bit 0 drops the clamp
+// tables' atomics (the cells stay live), bit 1 the x-group / y-block counts
+#ifndef KCC_DIAG_NP
+#define KCC_DIAG_NP 0
+#endif
+__device__ __forceinline__ void np_atomic(int64_t* p, int64_t w) {
+  if (KCC_DIAG_NP & 1) {
+    if (w == 0x5a5a5a5a5a5a5a5all) *p = w;
+  } else {
+    atomic_add_u64(reinterpret_cast<uint64_t*>(p), (uint64_t)w);
+  }
+}
 static_assert(CLAMP_LDS_SPECS % KCC_NODE_PREP_BLOCK == 0, "node_prep table fill");
 #ifndef KCC_NODE_PREP_GRID
 #define KCC_NODE_PREP_GRID 512  // workgroups at most (2 per CU, one round; each fills its LDS tables once)
@@ -603,23 +623,24 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
           // L >= 1, b >= 1 (U >= cmin, V >= mmin)
           const uint32_t GX = L >> 6, rx = L & 63u, GY = b >> 6, ry = b & 63u;
           if (GX > 0 && GY > 0)
-            atomic_add_u64(reinterpret_cast<uint64_t*>(&Cc[(int64_t)GX * W + GY]), (uint64_t)w);
+            np_atomic(&Cc[(int64_t)GX * W + GY], w);
           if (rx > 0) {  // x-group GX: k = #{its specs with y < b}
-            const uint32_t k = lds ? count_lt64(mrc_l + 64 * GX, b) : count_lt64(cw.mr_c + 64 * GX, b);
+            const uint32_t k = (KCC_DIAG_NP & 2) ? 1u
+                             : lds ? count_lt64(mrc_l + 64 * GX, b) : count_lt64(cw.mr_c + 64 * GX, b);
             if (k > 0)
-              atomic_add_u64(reinterpret_cast<uint64_t*>(&H2c[((int64_t)GX * 65 + k) * 64 + rx]),
-                             (uint64_t)w);
+              np_atomic(&H2c[((int64_t)GX * 65 + k) * 64 + rx], w);
           }
           if (ry > 0 && GX > 0) {  // y-block GY: j = #{its specs whose x-group < GX}
             uint32_t j;
-            if (lds) {
+            if (KCC_DIAG_NP & 2) {
+              j = 1;
+            } else if (lds) {
               j = count_lt64(xg_l + 64 * GY, GX);
             } else {  // x >> 6 < GX  <=>  x < 64 GX (padding: never)
               j = count_lt64(cw.cr_m + 64 * GY, GX << 6);
             }
             if (j > 0)
-              atomic_add_u64(reinterpret_cast<uint64_t*>(&H3c[((int64_t)GY * 65 + j) * 64 + ry]),
-                             (uint64_t)w);
+              np_atomic(&H3c[((int64_t)GY * 65 + j) * 64 + ry], w);
           }
         }
       }
@@ -754,12 +775,15 @@ __global__ __launch_bounds__(SPEC_BLOCK) void spec_rank_kernel(int64_t S, const 
 // normal specs cs[x], ms[y], mr_c[x] = y, cr_m[y] = x, dperm[x] = position; zeroes its
 // rank[] entries; the threads [nN, 64 T) pad mr_c and cr_m; thread 0 sets the counters;
 // this call's cells of the clamp table C are zeroed (clamp_apply leaves them dirty).
-__global__ __launch_bounds__(256) void spec_place_kernel(int64_t S, const uint64_t* __restrict__ c_in,
-                                                         const int64_t* __restrict__ m_in,
-                                                         SpecPrep sp, ClampWork cw,
-                                                         int64_t* __restrict__ partial,
-                                                         unsigned long long* __restrict__ counters) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
+  const int64_t S = pa.S;
+  const uint64_t* __restrict__ c_in = pa.c_in;
+  const int64_t* __restrict__ m_in = pa.m_in;
+  const SpecPrep& sp = pa.sp;
+  const ClampWork& cw = pa.cw;
+  int64_t* __restrict__ partial = pa.partial;
+  unsigned long long* __restrict__ counters = pa.counters;
+  const int64_t i = blk * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const int64_t nqb = (S + 63) / 64, qb = i >> 6;
   const bool in = i < S;
@@ -800,7 +824,7 @@ __global__ __launch_bounds__(256) void spec_place_kernel(int64_t S, const uint64
   }
   {
     const int64_t W = (nN + 63) / 64 + 2, cells = W * W;
-    for (int64_t e = i; e < C_COPIES * cells; e += (int64_t)gridDim.x * blockDim.x)
+    for (int64_t e = i; e < C_COPIES * cells; e += (int64_t)pa.n_blocks * 256)
       cw.C[(e / cells) * cw.c_stride + e % cells] = 0;
   }
   if (!in) return;
@@ -828,6 +852,8 @@ __global__ __launch_bounds__(256) void spec_place_kernel(int64_t S, const uint64
   cw.cr_m[y] = x;
   cw.dperm[x] = (int32_t)pos;
 }
+
+__global__ __launch_bounds__(256) void spec_place_kernel(PlaceArgs pa) { spec_place_body(pa, blockIdx.x); }
 
 // ---- clamp correction: D_s and partial[s] -= D_s ------------------------------------
 
@@ -1296,8 +1322,10 @@ int64_t reduce_resident_waves(bool limits) {
 }
 }  // namespace
 
-int32_t reduce_range(int64_t n_containers, bool limits) {
-  const int64_t r = reduce_resident_waves(limits) * KCC_RED_ROUNDS * RED_TILE;
+int32_t reduce_range(int64_t n_containers, bool limits, int64_t reserve_waves) {
+  int64_t slots = reduce_resident_waves(limits) - reserve_waves;
+  if (slots < 64) slots = 64;
+  const int64_t r = slots * KCC_RED_ROUNDS * RED_TILE;
   int64_t t = (n_containers + r - 1) / r;
   if (t < 1) t = 1;
   if (t > ((int64_t)1 << 20)) t = (int64_t)1 << 20;  // range < 2^28 (int32 relative offsets)
@@ -1316,12 +1344,12 @@ hipError_t launch_reduce_mark(int64_t n_nodes, int64_t c0, int64_t n_containers,
 
 MarkArgs mark_args(int64_t n_nodes, int64_t c0, int64_t n_containers, const int64_t* node_ptr,
                    int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu,
-                   int64_t* lim_mem) {
+                   int64_t* lim_mem, int64_t reserve_waves) {
   MarkArgs a;
   a.n_nodes = n_nodes;
   a.c0 = c0;
   a.c_end = c0 + n_containers;
-  a.range = reduce_range(n_containers, lim_cpu != nullptr);
+  a.range = reduce_range(n_containers, lim_cpu != nullptr, reserve_waves);
   a.ptr = node_ptr;
   a.wave_node = wave_node;
   a.o0 = used_cpu;
@@ -1335,26 +1363,33 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
                          const uint64_t* cpu_req, const int64_t* mem_req,
                          const uint64_t* cpu_lim, const int64_t* mem_lim,
                          const int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem,
-                         uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s) {
-  if (n_nodes <= 0 || n_containers <= 0) return hipSuccess;
+                         uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s,
+                         const PlaceArgs* place) {
+  PlaceArgs pa{};
+  if (place) pa = *place;
+  const int64_t nb_place = pa.n_blocks;
+  const bool red = n_nodes > 0 && n_containers > 0;
+  if (!red && nb_place == 0) return hipSuccess;
   if (n_nodes >= RED_MAX_NODES) return hipErrorInvalidValue;
   const bool limits = cpu_lim && mem_lim && lim_cpu && lim_mem;
-  const int32_t range = reduce_range(n_containers, limits);
-  const int64_t waves = reduce_n_waves(n_containers, limits);
-  const unsigned blocks = (unsigned)((waves + RED_WAVES_PER_BLOCK - 1) / RED_WAVES_PER_BLOCK);
+  const int64_t reserve = RED_WAVES_PER_BLOCK * nb_place;
+  const int32_t range = red ? reduce_range(n_containers, limits, reserve) : RED_TILE;
+  const int64_t waves = red ? reduce_n_waves(n_containers, limits, reserve) : 0;
+  const unsigned blocks =
+      (unsigned)((waves + RED_WAVES_PER_BLOCK - 1) / RED_WAVES_PER_BLOCK + nb_place);
   const bool lim = cpu_lim && mem_lim && lim_cpu && lim_mem;
   if (lim) {
     hipLaunchKernelGGL(reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, n_nodes, c0,
                        c0 + n_containers, range, node_ptr, cpu_req, reinterpret_cast<const uint64_t*>(mem_req), cpu_lim,
                        reinterpret_cast<const uint64_t*>(mem_lim), wave_node, used_cpu,
                        reinterpret_cast<uint64_t*>(used_mem), lim_cpu,
-                       reinterpret_cast<uint64_t*>(lim_mem));
+                       reinterpret_cast<uint64_t*>(lim_mem), pa);
   } else {
     hipLaunchKernelGGL(reduce_kernel<2>, dim3(blocks), dim3(256), 0, s, n_nodes, c0,
                        c0 + n_containers, range, node_ptr, cpu_req, reinterpret_cast<const uint64_t*>(mem_req),
                        (const uint64_t*)nullptr, (const uint64_t*)nullptr, wave_node, used_cpu,
                        reinterpret_cast<uint64_t*>(used_mem), (uint64_t*)nullptr,
-                       (uint64_t*)nullptr);
+                       (uint64_t*)nullptr, pa);
   }
   return hipGetLastError();
 }
@@ -1377,7 +1412,8 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
 
 hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
                             SpecPrep sp, ClampWork cw, int64_t* partial,
-                            unsigned long long* counters, hipStream_t s, const MarkArgs* mark) {
+                            unsigned long long* counters, hipStream_t s, const MarkArgs* mark,
+                            bool with_place) {
   if (n_specs <= 0) return hipSuccess;
   const int64_t L = rank_slice(n_specs);
   const int64_t blocks = (n_specs + 63) / 64 * ((n_specs + L - 1) / L);
@@ -1386,8 +1422,10 @@ hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu, const int
   MarkArgs none{};
   hipLaunchKernelGGL(spec_rank_kernel, dim3((unsigned)(blocks + mblocks)), dim3(SPEC_BLOCK), 0, s,
                      n_specs, spec_cpu, spec_mem, cw, blocks, mblocks ? *mark : none);
-  hipLaunchKernelGGL(spec_place_kernel, dim3(grid_for((n_specs + 63) / 64 * 64, 256, 1 << 30)),
-                     dim3(256), 0, s, n_specs, spec_cpu, spec_mem, sp, cw, partial, counters);
+  if (with_place) {
+    PlaceArgs pa{n_specs, spec_cpu, spec_mem, sp, cw, partial, counters, place_blocks(n_specs)};
+    hipLaunchKernelGGL(spec_place_kernel, dim3((unsigned)pa.n_blocks), dim3(256), 0, s, pa);
+  }
   return hipGetLastError();
 }
 
