@@ -215,6 +215,16 @@ int kcc_profile_enable(kcc_ctx* ctx, int on);
 int kcc_profile_read(kcc_ctx* ctx, double* reduce_ms, int64_t* reduce_launches, double* fit_ms,
                      int64_t* fit_launches);
 
+/* The fit streams only the node rows that can add to its fast sum (free CPU, free
+ * memory and allocatable pods > 0, within the fast bounds): every other row contributes
+ * exactly 0 there (x = findMin(qc, qm) = 0; P <= 0 rows are applied by the clamp
+ * correction; rows outside the bounds take the exact path), so the totals are the same
+ * bit for bit.  kcc_set_fit_dense(ctx, 1) streams every row instead (diagnostic / A-B).
+ * kcc_fit_stream_rows: node rows (padded to groups of 8) the last fit streamed, summed
+ * over its node chunks (synchronises the device). */
+int kcc_set_fit_dense(kcc_ctx* ctx, int dense);
+int kcc_fit_stream_rows(kcc_ctx* ctx, int64_t* streamed);
+
 /* Fraction of (node, spec) pairs of the last kcc_fit* call that took the exact
  * 64-bit path instead of the saturating fast path (diagnostic; host-computed from
  * the class counters the fit kernel keeps).  -1 if unknown. */

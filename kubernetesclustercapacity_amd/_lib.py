@@ -46,6 +46,8 @@ SIGNATURES = {
     "kcc_capacity_partial_async": (_int, [_vp, _i64, _i64] + [_vp] * 10 + [_i64] + [_vp] * 3
                                    + [_int, _vp]),
     "kcc_set_node_shards": (_int, [_vp, _int]),
+    "kcc_set_fit_dense": (_int, [_vp, _int]),
+    "kcc_fit_stream_rows": (_int, [_vp, C.POINTER(_i64)]),
     "kcc_comm_unique_id": (_int, [_vp]),
     "kcc_comm_init": (_int, [_vp, _vp, _int, _int]),
     "kcc_allreduce_partial_async": (_int, [_vp, _i64, _vp, _vp]),

@@ -68,6 +68,8 @@ struct Dev {
   int64_t last_pairs = 0;  // node x spec pairs of the last fit_prepare on this device
   int64_t c_stride = 0;    // cells per copy of the clamp table C
   int64_t h_stride = 0;    // cells per copy of the clamp tables H2 / H3
+  bool fit_dense = false;  // kcc_set_fit_dense: stream every node row through the fit
+  int stream_chunks = 0;   // node chunks of the last fit prepare (their stream counters)
   int64_t prep_nodes = -1, prep_specs = -1;  // sizes the workspace was last prepared for
   // staging of the host-array entry points
   DevBuf ptr, cpu, mem, cpul, meml, used_cpu, used_mem, lim_cpu, lim_mem;
@@ -289,7 +291,8 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
                                      used_cpu, used_mem, as<kcc::FitGroupA>(dv.fast_a),
                                      as<kcc::FitGroup>(dv.fast_b), as<kcc::SlowNode>(dv.slow),
                                      as<int64_t>(dv.slow_list), n_specs, clamp_of(dv),
-                                     as<unsigned long long>(dv.counters), 0, s));
+                                     as<unsigned long long>(dv.counters), 0, s, dv.fit_dense));
+  dv.stream_chunks = 1;
   KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, clamp_of(dv),
                                        as<unsigned long long>(dv.counters), partial, s));
   dv.clamp_dirty = false;
@@ -416,6 +419,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   for (int c = 0; c < k; ++c)
     if (!dv.ev_red[c]) KCC_HIP(ctx, hipEventCreateWithFlags(&dv.ev_red[c], hipEventDisableTiming));
   dv.last_pairs = n_nodes * n_specs;
+  dv.stream_chunks = k;
   dv.prep_nodes = -1;  // the split fit_run API must not reuse this call's workspace state
   dv.prep_specs = -1;
   // k > 1: the reduces run on the side stream, forked from s (they wait for everything
@@ -479,7 +483,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                        as<kcc::FitGroup>(dv.fast_b) + lo[c] / kcc::FIT_GROUP,
                                        as<kcc::SlowNode>(dv.slow) + lo[c],
                                        as<int64_t>(dv.slow_list) + lo[c], n_specs, clamp_of(dv),
-                                       as<unsigned long long>(dv.counters), c, s));
+                                       as<unsigned long long>(dv.counters), c, s, dv.fit_dense));
     ProfPair pp{};
     if (dv.prof_on) {
       KCC_HIP(ctx, prof_event(dv, &pp.a));
@@ -952,6 +956,26 @@ int kcc_fit_slow_pairs(kcc_ctx* ctx, int64_t* slow_pairs, int64_t* pairs) {
   if (dv.counters.p) KCC_HIP(ctx, hipMemcpy(&c, dv.counters.p, sizeof(c), hipMemcpyDeviceToHost));
   *slow_pairs = (int64_t)c;
   *pairs = dv.last_pairs;
+  return KCC_OK;
+}
+
+int kcc_set_fit_dense(kcc_ctx* ctx, int dense) {
+  if (!ctx) return KCC_EINVAL;
+  for (Dev& dv : ctx->devs) dv.fit_dense = dense != 0;
+  return KCC_OK;
+}
+
+int kcc_fit_stream_rows(kcc_ctx* ctx, int64_t* streamed) {
+  if (!ctx || !streamed) return ctx ? fail(ctx, KCC_EINVAL, "NULL output") : KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  KCC_HIP(ctx, hipDeviceSynchronize());
+  unsigned long long c[kcc::CNT_N] = {};
+  if (dv.counters.p)
+    KCC_HIP(ctx, hipMemcpy(c, dv.counters.p, sizeof(c), hipMemcpyDeviceToHost));
+  int64_t t = 0;
+  for (int k = 0; k < dv.stream_chunks && k < kcc::FIT_MAX_CHUNKS; ++k) t += (int64_t)c[kcc::CNT_STREAM + k];
+  *streamed = t;
   return KCC_OK;
 }
 

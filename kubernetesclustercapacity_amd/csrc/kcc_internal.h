@@ -210,7 +210,8 @@ enum {
   CNT_SPECS_B = 2,     // class-B specs (internal positions [nA, nA + nB))
   CNT_SPARE = 3,
   CNT_SLOW_ROWS = 4,   // + chunk: rows in that node chunk's slow_list
-  CNT_N = 4 + FIT_MAX_CHUNKS
+  CNT_STREAM = 4 + FIT_MAX_CHUNKS,  // + chunk: node rows in that chunk's fit stream (x 8)
+  CNT_N = 4 + 2 * FIT_MAX_CHUNKS
 };
 // Spec setup, two launches.  spec_rank: brute-force x-ranks by (c, index) and y-ranks by
 // (m, index) (64 queries per workgroup, the candidates split over workgroups and waves,
@@ -231,12 +232,19 @@ hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
 hipError_t launch_clamp_apply(int64_t n_specs, ClampWork cw,
                               const unsigned long long* counters, int64_t* partial, hipStream_t s);
 
+// The fit's node stream (FitGroupA / FitGroup records) holds the rows that can contribute
+// to the fast sum Σ min(findMin(qc, qm), P): fast-bound rows with free CPU, free memory
+// and P >= 1 (every other row adds exactly 0 there: qc = 0 or qm = 0 makes x = 0, and
+// P <= 0 rows are the clamp correction's), compacted per workgroup pass into
+// counters[CNT_STREAM + chunk] rows (padded to whole groups).  dense: stream every row (the
+// round-1 layout's cost: zero fields for the rows that add nothing).
 hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
                             SlowNode* slow, int64_t* slow_list, int64_t n_specs, ClampWork cw,
-                            unsigned long long* counters, int chunk, hipStream_t s);
+                            unsigned long long* counters, int chunk, hipStream_t s,
+                            bool dense = false);
 
 // partial[0..S) += Σ_i q(i,s), partial[S..2S) += #div-by-zero rows (internal order).
 hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,

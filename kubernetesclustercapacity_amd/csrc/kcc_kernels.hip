@@ -501,10 +501,12 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
                                  FitGroupA* __restrict__ fast_a, FitGroup* __restrict__ fast_b,
                                  SlowNode* __restrict__ slow, int64_t* __restrict__ slow_list,
                                  int64_t S, ClampWork cw, unsigned long long* __restrict__ counters,
-                                 int32_t chunk) {
-  const int lane = threadIdx.x & 63;
-  const int64_t n_pad = fit_groups(n) * FIT_GROUP;
+                                 int32_t chunk, int32_t dense) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  __shared__ uint32_t np_wc[KCC_NODE_PREP_BLOCK / 64];  // streamed rows per wave
+  __shared__ uint64_t np_base;                          // this pass's stream position
+  __shared__ uint32_t np_tot;
   const bool want_b = counters[CNT_SPECS_B] != 0;  // written by spec setup (same stream)
   const int64_t nN = clamp_n_normal(counters);     // normal specs (clamp correction)
   const bool slow_all = nN < S;                    // exact-path specs exist
@@ -550,9 +552,9 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   }
   __syncthreads();
   KCC_TL(3072 + blockIdx.x % 1024, 0);
-  // wave-uniform trip count (wave-wide sums and ballots below)
-  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < n_pad; i0 += stride) {
-    const int64_t i = i0 + lane;
+  // workgroup-uniform trip count (the stream positions meet in LDS)
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
+    const int64_t i = i0 + threadIdx.x;
     const bool valid = i < n;
     bool ok = false;
     uint64_t fc_ok = 0;
@@ -582,18 +584,41 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
         slow[i] = sn;
       }
     }
-    if (i < n_pad) {
-      const int k = (int)(i % FIT_GROUP);
-      FitGroupA& a = fast_a[i / FIT_GROUP];
-      a.fm[k] = (uint64_t)fm_ok;
-      a.fc[k] = (uint32_t)fc_ok;
-      a.P[k] = (uint32_t)(P_ok > 0 ? P_ok : 0);  // P <= 0: x >= P always (clamp), as for P = 0
-      if (want_b) {
-        FitGroup& g = fast_b[i / FIT_GROUP];
-        g.fc[k] = (double)fc_ok;                                         // exact
-        g.fm[k] = (double)fm_ok;                                         // exact (< 2^50)
-        g.Pb[k] = FIT_BIAS + (double)(P_ok > 0 ? P_ok : 0);              // exact (P <= 2^20)
+    {  // the fit's node stream: this pass's rows with something to add, compacted
+      const bool stream = dense ? valid : (ok && fc_ok > 0 && fm_ok > 0 && P_ok > 0);
+      const unsigned long long sb = __ballot(stream);
+      if (lane == 0) np_wc[wv] = (uint32_t)__popcll(sb);
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int u = 0; u < KCC_NODE_PREP_BLOCK / 64; ++u) t += np_wc[u];
+        const uint32_t padded = (t + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP;  // whole groups
+        np_base = padded ? atomicAdd(&counters[CNT_STREAM + chunk], (unsigned long long)padded) : 0ull;
+        np_tot = t;
       }
+      __syncthreads();
+      uint32_t before = 0;
+      for (int u = 0; u < wv; ++u) before += np_wc[u];
+      const uint64_t b0 = np_base;
+      const uint32_t tot = np_tot;
+      const uint32_t pad = (tot + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP - tot;
+      auto put = [&](uint64_t pos, uint64_t fmv, uint32_t fcv, uint32_t Pv) {
+        const int k = (int)(pos % FIT_GROUP);
+        FitGroupA& a = fast_a[pos / FIT_GROUP];
+        a.fm[k] = fmv;
+        a.fc[k] = fcv;
+        a.P[k] = Pv;
+        if (want_b) {
+          FitGroup& g = fast_b[pos / FIT_GROUP];
+          g.fc[k] = (double)fcv;                      // exact
+          g.fm[k] = (double)fmv;                      // exact (< 2^50)
+          g.Pb[k] = FIT_BIAS + (double)Pv;            // exact (P <= 2^20)
+        }
+      };
+      if (stream)  // P <= 0 streams only in the dense layout, as P = 0
+        put(b0 + before + (uint32_t)__popcll(sb & ((1ull << lane) - 1ull)), (uint64_t)fm_ok,
+            (uint32_t)fc_ok, P_ok > 0 ? (uint32_t)P_ok : 0u);
+      if (threadIdx.x < pad) put(b0 + tot + threadIdx.x, 0ull, 0u, 0u);  // the last group's padding
     }
     // clamp correction: where (and with which weight) this row's pod-slot clamp applies
     bool always = false;
@@ -659,6 +684,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       base = __shfl(base, 0);
       if (valid && !ok) slow_list[base + __popcll(bl & ((1ull << lane) - 1ull))] = i;
     }
+    __syncthreads();  // np_wc / np_base are rewritten by the next pass
   }
   KCC_TL(3072 + blockIdx.x % 1024, 1);
 }
@@ -1140,9 +1166,15 @@ __global__ __launch_bounds__(256) void fit_kernel(
   const bool wave_exact = __any(sr.cls == SPEC_EXACT);
   const bool wave_b = __any(sr.cls == SPEC_B);
 
-  const int64_t n_groups = fit_groups(n_nodes);
-  int64_t g0 = (int64_t)by * groups_per_block;
-  int64_t g1 = g0 + groups_per_block < n_groups ? g0 + groups_per_block : n_groups;
+  // this block's share of the node stream node_prep wrote (its length is on the device)
+  // (32-bit: the stream holds < 2^31 groups; keeps the kernel's SGPRs at 80, 8 waves/SIMD)
+  const uint32_t n_groups = (uint32_t)(counters[CNT_STREAM + chunk] / FIT_GROUP);
+  const uint32_t per = (n_groups + (uint32_t)gy - 1u) / (uint32_t)gy;
+  (void)groups_per_block;
+  uint32_t g0u = (uint32_t)by * per;
+  if (g0u > n_groups) g0u = n_groups;
+  int64_t g0 = g0u;
+  int64_t g1 = g0u + per < n_groups ? g0u + per : n_groups;
   if (FIT_SPLIT > 1) {  // this wave's part of the workgroup's node chunk
     const int64_t part = (g1 - g0 + FIT_SPLIT - 1) / FIT_SPLIT;
     g0 = g0 + wv * part < g1 ? g0 + wv * part : g1;
@@ -1240,9 +1272,17 @@ __global__ __launch_bounds__(256) void fit_kernel(
       acc += (uint64_t)(int64_t)acc32;
     }
     set_round_nearest();
-  } else {
-    const int64_t i1 = g1 * FIT_GROUP < n_nodes ? g1 * FIT_GROUP : n_nodes;
-    for (int64_t i = g0 * FIT_GROUP; i < i1; ++i) eval_slow(i);
+  } else {  // exact-path specs: every node row (SlowNode), this block's share of them
+    const uint32_t nn = (uint32_t)n_nodes;  // < 2^28 per device
+    const uint32_t pn = (nn + (uint32_t)gy - 1u) / (uint32_t)gy;
+    const uint32_t a0 = (uint32_t)by * pn < nn ? (uint32_t)by * pn : nn;
+    int64_t i0 = a0, i1 = a0 + pn < nn ? a0 + pn : nn;
+    if (FIT_SPLIT > 1) {
+      const int64_t part = (i1 - i0 + FIT_SPLIT - 1) / FIT_SPLIT;
+      i0 = i0 + wv * part < i1 ? i0 + wv * part : i1;
+      i1 = i0 + part < i1 ? i0 + part : i1;
+    }
+    for (int64_t i = i0; i < i1; ++i) eval_slow(i);
   }
   if (!wave_exact) {  // rows outside the fast bounds, shared out over the node-chunk waves
     const int64_t n_slow = (int64_t)counters[CNT_SLOW_ROWS + chunk];
@@ -1399,14 +1439,15 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
                             SlowNode* slow, int64_t* slow_list, int64_t n_specs, ClampWork cw,
-                            unsigned long long* counters, int chunk, hipStream_t s) {
+                            unsigned long long* counters, int chunk, hipStream_t s, bool dense) {
   if (n_nodes <= 0) return hipSuccess;
   hipLaunchKernelGGL(node_prep_kernel,
                      dim3(grid_for(fit_groups(n_nodes) * FIT_GROUP, KCC_NODE_PREP_BLOCK,
                                    KCC_NODE_PREP_GRID)),
                      dim3(KCC_NODE_PREP_BLOCK), NODE_PREP_LDS, s,
                      n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu, used_mem,
-                     fast_a, fast_b, slow, slow_list, n_specs, cw, counters, (int32_t)chunk);
+                     fast_a, fast_b, slow, slow_list, n_specs, cw, counters, (int32_t)chunk,
+                     (int32_t)(dense ? 1 : 0));
   return hipGetLastError();
 }
 

@@ -414,6 +414,17 @@ class CapacityEngine:
                                                C.byref(fn)))
         return rm.value, rn.value, fm.value, fn.value
 
+    def set_fit_dense(self, dense: bool):
+        """Stream every node row through the fit (diagnostic); default: only the rows
+        that can add to its fast sum."""
+        self._check(self._lib.kcc_set_fit_dense(self._h, 1 if dense else 0))
+
+    def fit_stream_rows(self) -> int:
+        """Node rows (padded to groups of 8) the last fit streamed."""
+        v = C.c_int64()
+        self._check(self._lib.kcc_fit_stream_rows(self._h, C.byref(v)))
+        return v.value
+
     def fit_slow_pairs(self):
         a, b = C.c_int64(), C.c_int64()
         self._check(self._lib.kcc_fit_slow_pairs(self._h, C.byref(a), C.byref(b)))

@@ -223,3 +223,25 @@ def test_bench_two_ranks_equal_one():
     assert two["config"]["nodes_rank0"] == 50_000
     assert two["totals_checksum"] == one["totals_checksum"]
     assert two["spec_errors"] == one["spec_errors"]
+
+
+# ---- the fit's node stream: compacted (default) == every row (dense) -----------------------
+def test_fit_stream_compacted_equals_dense(engine, c4, c4_oracle):
+    c, (sc, sm) = c4
+    t, e = capacity(engine, c, sc, sm)
+    streamed = engine.fit_stream_rows()
+    engine.set_fit_dense(True)
+    try:
+        td, ed = capacity(engine, c, sc, sm)
+        dense = engine.fit_stream_rows()
+    finally:
+        engine.set_fit_dense(False)
+    np.testing.assert_array_equal(t, c4_oracle[0])
+    np.testing.assert_array_equal(td, c4_oracle[0])
+    np.testing.assert_array_equal(ed, e)
+    assert dense >= c.n_nodes and 0 < streamed < dense
+    # streamed = the rows with free CPU, free memory and allocatable pods (whole groups)
+    uc = seg_sums(c.node_ptr, c.cpu_req)
+    um = seg_sums(c.node_ptr, c.mem_req).view(np.int64)
+    free = (c.alloc_cpu > uc) & (c.alloc_mem > um) & (c.alloc_pods > 0)
+    assert int(free.sum()) <= streamed <= int(free.sum()) + 7 * (c.n_nodes // 1024 + 1)
