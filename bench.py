@@ -69,6 +69,8 @@ def parse():
                     help="node chunks of the pipelined step (reduce of chunk k overlaps the fit "
                          "of chunk k-1); 1 = reduce, then fit")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dense", action="store_true",
+                    help="skip the dense-layout comparison steps (every row through the fit)")
     ap.add_argument("--no-pods", action="store_true",
                     help="skip the opt-in scheduler pod-request leg (SURVEY §8f row 4)")
     ap.add_argument("--no-keyed", action="store_true",
@@ -258,12 +260,16 @@ def main():
     if args.emulate_world > 1:  # per-rank rate x world (no all-reduce): an upper bound
         value = n * S * args.emulate_world / (elapsed / args.steps)
 
+    # the fit's node stream: the rows that can add to its fast sum (free CPU, free memory,
+    # pods > 0; every other row adds exactly 0 there), compacted by node_prep
+    streamed = eng.fit_stream_rows()
+
     # algorithmic bytes per launch (DESIGN.md "Roofline accounting"): a step runs
     # `chunks` reduce launches and `chunks` fit launches over node ranges of ~n/chunks
-    fit_bytes = (n * 16 + chunks * (S * 48 + S * 8)) / chunks  # FitGroupA + spec records in, totals out
+    fit_bytes = (streamed * 16 + chunks * (S * 48 + S * 8)) / chunks  # FitGroupA + specs in, totals out
     red_bytes = (C * 16 + (n + 1) * 8 + n * 16) / chunks       # requests + CSR offsets in, sums out
     fit_gbs = fit_bytes / (fit_ms * 1e-3) / 1e9
-    fit_valu = n / chunks * ((S + 63) // 64) * FIT_VALU_PER_NODE_WAVE / (fit_ms * 1e-3)
+    fit_valu = streamed / chunks * ((S + 63) // 64) * FIT_VALU_PER_NODE_WAVE / (fit_ms * 1e-3)
     red_gbs = red_bytes / (red_ms * 1e-3) / 1e9
     fit_traffic, tsrc = pmc_traffic("fit_kernel") if args.config == "C4" and world == 1 else (None, None)
     red_traffic, _ = pmc_traffic("reduce_kernel<2>") if tsrc else (None, None)
@@ -311,6 +317,16 @@ def main():
             "frac": fit_valu / VALU_ISSUE_PEAK,
             "valu_per_node_wave": FIT_VALU_PER_NODE_WAVE,
             "fit_evals_per_s": n / chunks * S / (fit_ms * 1e-3),
+            "fit_streamed_pairs_per_s": streamed / chunks * S / (fit_ms * 1e-3),
+            "note": "counted over the streamed rows (the instructions the kernel issues)",
+        },
+        "fit_stream": {
+            "rows": n, "rows_streamed": streamed, "fraction": streamed / max(n, 1),
+            "note": "node_prep streams into the fit only rows with free CPU, free memory and "
+                    "allocatable pods > 0 (padded to groups of 8); the others add exactly 0 to "
+                    "its sum of min(findMin(qc, qm), P) (their clamp terms are the clamp "
+                    "correction's) — same totals bit for bit (tests/test_gpu_shards_configs.py); "
+                    "value counts every node x spec pair; see dense_layout",
         },
         "roofline_reduce": {
             "bound": "hbm", "kernel": "reduce_kernel<2> (its mark runs inside the spec_rank launch)",
@@ -320,8 +336,8 @@ def main():
         },
         "pipeline": {"chunks": chunks, "reduce_ms_per_step": red_ms_tot / args.steps,
                      "fit_ms_per_step": fit_ms_tot / args.steps,
-                     "note": "reduce launches run on a side stream under the fit launches; "
-                             "their durations include that overlap"},
+                     "note": "per-kernel HIP events, recorded in --kernel-events "
+                             f"{args.kernel_events} steps"},
         "fast_path_fraction": 1.0 - (slow_pairs / pairs if pairs else 0.0),
         "gen_seconds": gen_s,
     }
@@ -333,6 +349,30 @@ def main():
     out["totals_checksum"] = int(((tot_np * np.uint64(0x9E3779B97F4A7C15)) ^ (tot_np >> np.uint64(29)))
                                  .sum(dtype=np.uint64))
     out["spec_errors"] = int(err.cpu().numpy().sum())
+    if not args.no_dense:  # the same step with every node row streamed through the fit
+        eng.set_fit_dense(True)
+        with torch.cuda.stream(stream):
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t1 = time.perf_counter()
+        eng.set_fit_dense(False)
+        dt = t1 - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        out["dense_layout"] = {"ms_per_step": dt / args.steps * 1e3,
+                               "value": n_total * S / (dt / args.steps),
+                               "note": "every node row streamed through the fit (round-1 layout)"}
     if rank == 0 and world == 1 and args.emulate_world <= 1:
         out["h2d"] = h2d_leg([cl.node_ptr, cl.cpu_req, cl.mem_req, cl.alloc_cpu, cl.alloc_mem,
                               cl.alloc_pods, cl.pod_count, sc, sm], dev, ms_step, n_total * S)

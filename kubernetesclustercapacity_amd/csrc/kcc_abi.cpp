@@ -59,6 +59,8 @@ struct Dev {
   int64_t prof_n[2] = {0, 0};
   // workspace of the *_async entry points
   DevBuf wave_node, fast_a, fast_b, slow, slow_list, srec, sperm, counters;
+  DevBuf fit_q;          // the fit's per-column work queues (zero between launches)
+  bool fitq_dirty = true;
   // spec setup + clamp correction (kcc::ClampWork)
   DevBuf c_rank, c_bcnt, c_cs, c_ms, c_mrc, c_crm, c_dperm;
   DevBuf c_C, c_H2, c_H3, c_Crow, c_S2, c_S3;
@@ -202,6 +204,10 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.srec, sizeof(kcc::SpecRec) * S));
   KCC_HIP(ctx, ensure(dv.sperm, 4 * S));
   KCC_HIP(ctx, ensure(dv.counters, sizeof(unsigned long long) * kcc::CNT_N));
+  // (a new allocation is a larger one: compare sizes, hipMalloc may hand back the address)
+  const size_t q_before = dv.fit_q.bytes;
+  KCC_HIP(ctx, ensure(dv.fit_q, 4 * (size_t)kcc::fit_queue_words((int64_t)S)));
+  if (dv.fit_q.bytes != q_before) dv.fitq_dirty = true;
   const size_t S64 = (S + 63) / 64 * 64;
   KCC_HIP(ctx, ensure(dv.c_bcnt, 8 * (S64 / 64)));
   KCC_HIP(ctx, ensure(dv.c_cs, 8 * S));
@@ -212,7 +218,7 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   // the table copies stay all-zero between calls (clamp_prep zeroes what it reads); a
   // new or grown allocation, or a layout change, is zeroed before its first use
   const int64_t cs_ = kcc::clamp_c_cells((int64_t)S), hs = kcc::clamp_h_cells((int64_t)S);
-  void* const before[4] = {dv.c_C.p, dv.c_H2.p, dv.c_H3.p, dv.c_rank.p};
+  const size_t before[4] = {dv.c_C.bytes, dv.c_H2.bytes, dv.c_H3.bytes, dv.c_rank.bytes};
   KCC_HIP(ctx, ensure(dv.c_rank, 4 * 2 * S));
   KCC_HIP(ctx, ensure(dv.c_C, 8 * (size_t)kcc::C_COPIES * (size_t)cs_));
   KCC_HIP(ctx, ensure(dv.c_H2, 8 * (size_t)kcc::H2_COPIES * (size_t)hs));
@@ -220,8 +226,8 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.c_Crow, 8 * (size_t)cs_));
   KCC_HIP(ctx, ensure(dv.c_S2, 8 * (size_t)hs));
   KCC_HIP(ctx, ensure(dv.c_S3, 8 * (size_t)hs));
-  if (dv.c_C.p != before[0] || dv.c_H2.p != before[1] || dv.c_H3.p != before[2] ||
-      dv.c_rank.p != before[3] ||
+  if (dv.c_C.bytes != before[0] || dv.c_H2.bytes != before[1] || dv.c_H3.bytes != before[2] ||
+      dv.c_rank.bytes != before[3] ||
       dv.c_stride != cs_ || dv.h_stride != hs)
     dv.clamp_dirty = true;
   dv.c_stride = cs_;
@@ -231,6 +237,10 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
 
 // Zero the table copies when they are not known to be zero (before node_prep adds to them).
 int clamp_clean(kcc_ctx* ctx, Dev& dv, hipStream_t s) {
+  if (dv.fitq_dirty) {  // a new allocation of the fit queues (every launch leaves them zero)
+    KCC_HIP(ctx, hipMemsetAsync(dv.fit_q.p, 0, dv.fit_q.bytes, s));
+    dv.fitq_dirty = false;
+  }
   if (!dv.clamp_dirty) return KCC_OK;
   KCC_HIP(ctx, hipMemsetAsync(dv.c_C.p, 0, dv.c_C.bytes, s));
   KCC_HIP(ctx, hipMemsetAsync(dv.c_H2.p, 0, dv.c_H2.bytes, s));
@@ -308,7 +318,8 @@ int fit_run_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_specs, int64_t
   KCC_HIP(ctx, kcc::launch_fit(n_nodes, as<kcc::FitGroupA>(dv.fast_a), as<kcc::FitGroup>(dv.fast_b),
                                as<kcc::SlowNode>(dv.slow),
                                as<int64_t>(dv.slow_list), n_specs, spec_prep_of(dv), partial,
-                               as<unsigned long long>(dv.counters), 0, n_nodes, s));
+                               as<unsigned long long>(dv.counters), as<uint32_t>(dv.fit_q), 0,
+                               n_nodes, s));
   return KCC_OK;
 }
 
@@ -494,7 +505,8 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                  as<kcc::FitGroup>(dv.fast_b) + lo[c] / kcc::FIT_GROUP,
                                  as<kcc::SlowNode>(dv.slow) + lo[c],
                                  as<int64_t>(dv.slow_list) + lo[c], n_specs, spec_prep_of(dv),
-                                 partial, as<unsigned long long>(dv.counters), c, n_nodes, s));
+                                 partial, as<unsigned long long>(dv.counters),
+                                 as<uint32_t>(dv.fit_q), c, n_nodes, s));
     if (dv.prof_on) {
       KCC_HIP(ctx, hipEventRecord(pp.b, s));
       pp.kind = 1;
@@ -708,7 +720,7 @@ void kcc_destroy(kcc_ctx* ctx) {
                       &dv.c_mrc, &dv.c_crm, &dv.c_dperm, &dv.c_C, &dv.c_H2, &dv.c_H3,
                       &dv.c_Crow, &dv.c_S2, &dv.c_S3,
                       &dv.wave_node, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
-                      &dv.sperm,
+                      &dv.sperm,     &dv.fit_q,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
                       &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,
                       &dv.alloc_cpu, &dv.alloc_mem, &dv.alloc_pods, &dv.pod_count, &dv.spec_cpu,

@@ -250,7 +250,12 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
 hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,
                       const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
-                      unsigned long long* counters, int chunk, int64_t grid_nodes, hipStream_t s);
+                      unsigned long long* counters, uint32_t* queue, int chunk,
+                      int64_t grid_nodes, hipStream_t s);
+// the fit's work queues: fit_queue_words(S) uint32 (a 64-B line per spec column of 256 and
+// sub-queue), zero before the first launch (each launch leaves them zero)
+constexpr int64_t FIT_QSUBS_MAX = 32;
+inline int64_t fit_queue_words(int64_t S) { return (S + 255) / 256 * FIT_QSUBS_MAX * 16; }
 
 hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial,
                                const int32_t* perm, int64_t* totals, int32_t* spec_err,

@@ -1115,40 +1115,78 @@ __device__ __forceinline__ double min_f64_s(double x, double p) {
   return d;
 }
 
-#ifndef KCC_FIT_SPECS_PER_WG
-#define KCC_FIT_SPECS_PER_WG 256  // 64/128 (waves split the node chunk, LDS-reduced atomics) measured slower
-#endif
-constexpr int FIT_SPW = KCC_FIT_SPECS_PER_WG;  // specs per 256-thread workgroup (64 or 256)
-constexpr int FIT_SPLIT = 256 / FIT_SPW;       // waves per spec group (node chunk split)
-static_assert(FIT_SPW == 64 || FIT_SPW == 128 || FIT_SPW == 256, "FIT_SPW");
+constexpr int FIT_SPW = 256;           // specs per 256-thread workgroup (one column per wave)
 constexpr int FIT_CHUNK_GROUPS = 128;  // 1024 nodes: |sum of contributions| <= 2^30 in i32
+#ifndef KCC_FIT_QUEUE
+#define KCC_FIT_QUEUE 1  // 0: static node shares per wave (KCC_FIT_TARGET_BLOCKS grid)
+#endif
+#ifndef KCC_FIT_QCHUNK
+#define KCC_FIT_QCHUNK 32  // node groups per claim from a sub-queue
+#endif
+constexpr uint32_t FIT_QCHUNK = KCC_FIT_QCHUNK;
+static_assert(FIT_QCHUNK >= 2 && FIT_QCHUNK <= FIT_CHUNK_GROUPS, "claims sum in i32");
+#ifndef KCC_FIT_Q_HALVE
+#define KCC_FIT_Q_HALVE 128  // claims of FIT_QCHUNK / 2 when a workgroup's share is below this
+#endif
+#ifndef KCC_FIT_WG_PER_SUB
+#define KCC_FIT_WG_PER_SUB 24  // workgroups per sub-queue at most, about (8 to 32 sub-queues)
+#endif
+constexpr uint32_t FIT_QSUBS = (uint32_t)FIT_QSUBS_MAX;
 #ifndef KCC_FIT_TARGET_BLOCKS
 #define KCC_FIT_TARGET_BLOCKS 32768
 #endif
 #ifndef KCC_FIT_MIN_GPB
 #define KCC_FIT_MIN_GPB 32  // node groups per workgroup at least (8-way shards: 8 -> 32 took 9 us off the fit)
 #endif
+#ifndef KCC_FIT_ROUNDS
+#define KCC_FIT_ROUNDS 1  // queue grid: this many rounds of resident workgroups
+#endif
 
 __device__ __forceinline__ double f64_at(const i32x16& v, int k) {
   return __longlong_as_double(((int64_t)(uint32_t)v[2 * k + 1] << 32) | (uint32_t)v[2 * k]);
 }
 
-__global__ __launch_bounds__(256) void fit_kernel(
-    int64_t n_nodes, int64_t groups_per_block, const FitGroupA* __restrict__ fast_a,
+// Work distribution: a workgroup = 4 waves = 256 specs (a spec column), each wave 64
+// specs; node groups come from a queue.  The grid holds gx * gy workgroups (one round of
+// resident workgroups).  A column's stream is cut into nsub segments (the workgroups with
+// by % nsub == sub, i.e. of one XCD, share segment sub), and the workgroups of a segment
+// claim FIT_QCHUNK node groups at a time from its sub-queue: one returning 32-bit atomic
+// by wave 0, in flight while the current chunk is summed, its result handed to the four
+// waves through LDS at the chunk's barrier (the four waves read the same node groups:
+// scalar-cache hits).  The workgroups that run faster take more chunks and none waits for
+// a ragged last round; each wave sums its claims in registers and adds them to partial
+// with one 64-bit atomic per spec at the end: S * gy atomics per launch (C4: gy ~ 450,
+// 3.7 MB) instead of one per spec and static node share.  Sub-queues sit in 64-B lines of
+// their own ([0] claims, [1] workgroups done: returning atomics on one line serialise);
+// the last workgroup of a sub-queue to finish resets both to zero for the next launch
+// (every workgroup of it has made its last claim by then); the buffer is zeroed once when
+// allocated.  KCC_FIT_QUEUE=0: static shares (each workgroup one range of the stream).
+// 8 waves per SIMD: the register budget that leaves (the compiler otherwise takes ~106
+// SGPRs, 6 waves); the loops stay spill-free (tests/test_isa.py)
+#ifndef KCC_FIT_WAVES_PER_EU
+#define KCC_FIT_WAVES_PER_EU 8
+#endif
+#if KCC_FIT_WAVES_PER_EU > 0
+#define KCC_FIT_ATTR __attribute__((amdgpu_waves_per_eu(KCC_FIT_WAVES_PER_EU)))
+#else
+#define KCC_FIT_ATTR
+#endif
+__global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
+    int64_t n_nodes, uint32_t* __restrict__ queue, const FitGroupA* __restrict__ fast_a,
     const FitGroup* __restrict__ fast_b, const SlowNode* __restrict__ slow,
     const int64_t* __restrict__ slow_list, int64_t S, const SpecRec* __restrict__ specs,
     int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t chunk,
     int32_t gx, int32_t gy) {
   // XCD-aware order (speed only, never correctness): workgroups are dealt round-robin
-  // over the 8 XCDs, so give every spec group of one node chunk the same b % 8 — the
-  // chunk's FitGroup records then stay in that XCD's L2 for all of them.
+  // over the 8 XCDs, so give every spec group of one node chunk the same b % 8
   const int32_t b = blockIdx.x, xcd = b & 7, r = b >> 3;
   const int32_t bx = r % gx, by = (r / gx) * 8 + xcd;
   if (by >= gy) return;  // padding of gy up to a multiple of 8 (whole workgroup)
-  // FIT_SPW specs per workgroup; its FIT_SPLIT waves share them and split the node chunk
-  const int32_t wv = __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6) / (FIT_SPW / 64));
-  const int64_t s = (int64_t)bx * FIT_SPW + (threadIdx.x % FIT_SPW);
+  const int32_t wv = __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const int64_t s = (int64_t)bx * FIT_SPW + threadIdx.x;
   const bool active = s < S;
+  const bool idle = !__any(active);  // a wave wholly past S (still takes the barriers)
   SpecRec sr;  // one 48-B record per lane
   if (active) {
     sr = specs[s];
@@ -1165,20 +1203,53 @@ __global__ __launch_bounds__(256) void fit_kernel(
   const double rm = sr.rm, rc = sr.rc;
   const bool wave_exact = __any(sr.cls == SPEC_EXACT);
   const bool wave_b = __any(sr.cls == SPEC_B);
+  const bool wave_fast = !wave_exact && !idle;  // sums the node stream
 
-  // this block's share of the node stream node_prep wrote (its length is on the device)
-  // (32-bit: the stream holds < 2^31 groups; keeps the kernel's SGPRs at 80, 8 waves/SIMD)
+  // the node stream node_prep wrote (its length is on the device; 32-bit: < 2^31 groups)
   const uint32_t n_groups = (uint32_t)(counters[CNT_STREAM + chunk] / FIT_GROUP);
-  const uint32_t per = (n_groups + (uint32_t)gy - 1u) / (uint32_t)gy;
-  (void)groups_per_block;
-  uint32_t g0u = (uint32_t)by * per;
-  if (g0u > n_groups) g0u = n_groups;
-  int64_t g0 = g0u;
-  int64_t g1 = g0u + per < n_groups ? g0u + per : n_groups;
-  if (FIT_SPLIT > 1) {  // this wave's part of the workgroup's node chunk
-    const int64_t part = (g1 - g0 + FIT_SPLIT - 1) / FIT_SPLIT;
-    g0 = g0 + wv * part < g1 ? g0 + wv * part : g1;
-    g1 = g0 + part < g1 ? g0 + part : g1;
+  uint32_t lim = n_groups;  // claims end here
+  uint32_t base = 0;        // queue: the segment's start
+  uint32_t nxt = 0;         // queue: the claim in flight (wave 0, lane 0); static: next chunk
+  // sub-queues: gy if gy < 8, else 8, 16 or 32 (a power of two: whole XCDs each), about
+  // KCC_FIT_WG_PER_SUB workgroups per sub-queue (measured: 56 per line 8 % slower at C4
+  // than 28; fewer than 2 per line lose the balancing)
+  uint32_t nsub = (uint32_t)gy / KCC_FIT_WG_PER_SUB;
+  nsub = nsub <= 8u ? 8u : (nsub >= FIT_QSUBS ? FIT_QSUBS : 1u << (31 - __builtin_clz(nsub)));
+  if ((uint32_t)gy < nsub) nsub = (uint32_t)gy;
+  const uint32_t sub = (uint32_t)by % nsub;
+  uint32_t* const qp = queue + ((uint32_t)bx * FIT_QSUBS + sub) * 16u;
+  // claim size: halved when a workgroup's share is small (8-way shards of C4: ~35 groups
+  // per workgroup; two claims each keep the balancing)
+  const uint32_t qsz = KCC_FIT_QUEUE && n_groups / (uint32_t)gy < KCC_FIT_Q_HALVE
+                          ? FIT_QCHUNK / 2u : FIT_QCHUNK;
+  __shared__ uint32_t q_slot[2];
+  // lane 0 of wave 0 issues the claim in asm, so the compiler does not wait for it where
+  // it is issued (its atomic-optimizer expansion reads the result at once); wave 0 waits
+  // for it (vmcnt) at the end of the chunk — the loop bodies issue no other vector memory
+  // operations
+  auto claim_issue = [&]() {
+    if (wv == 0 && lane == 0)
+      asm volatile("global_atomic_add %0, %1, %2, off sc0"
+                   : "=v"(nxt) : "v"(qp), "v"(qsz) : "memory");
+  };
+  auto claim_publish = [&](uint32_t slot) {
+    if (wv == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(nxt) : : "memory");
+      if (lane == 0) q_slot[slot] = nxt;
+    }
+    __syncthreads();
+  };
+  if (KCC_FIT_QUEUE) {
+    const uint32_t seg = ((n_groups + nsub - 1u) / nsub + qsz - 1u) / qsz * qsz;
+    base = sub * seg < n_groups ? sub * seg : n_groups;
+    lim = base + seg < n_groups ? base + seg : n_groups;
+    claim_issue();
+    claim_publish(0);
+  } else {  // static: this workgroup's share [by * per, (by + 1) * per)
+    const uint32_t per = (n_groups + (uint32_t)gy - 1u) / (uint32_t)gy;
+    const uint32_t g0 = (uint32_t)by * per < n_groups ? (uint32_t)by * per : n_groups;
+    lim = g0 + per < n_groups ? g0 + per : n_groups;
+    nxt = g0;
   }
   uint64_t acc = 0;
   uint64_t errs = 0;
@@ -1205,107 +1276,116 @@ __global__ __launch_bounds__(256) void fit_kernel(
     acc += z ? 0ull : (uint64_t)q;
   };
 
-  const int cnt = (int)(g1 - g0);
-  if (!wave_exact && !wave_b) {
-    // class A
+  // class A: node groups [g0, g0 + cnt)
+  auto sum_a = [&](uint32_t g0, int cnt) {
+    cnt = __builtin_amdgcn_readfirstlane(cnt);  // keep the trip count scalar
     const FitGroupA* gbase = fast_a + g0;
     const f32x2 rcf2 = {sr.rcf, sr.rcf};
+    int32_t acc32 = 0;
     set_round_down();
-    for (int cb = 0; cb < cnt; cb += FIT_CHUNK_GROUPS) {
-      const int ce = cb + FIT_CHUNK_GROUPS < cnt ? cb + FIT_CHUNK_GROUPS : cnt;
-      int32_t acc32 = 0;
-      for (int gi = cb; gi < ce; ++gi) {
-        // index opaque to loop-strength reduction: one base per group, immediate offsets
-        int io = gi;
-        asm volatile("" : "+s"(io));
-        const FitGroupA* g = gbase + io;
-        const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
-        const i32x8 fcv = *reinterpret_cast<const i32x8*>(g->fc);
-        const i32x8 Pv = *reinterpret_cast<const i32x8*>(g->P);
+    for (int gi = 0; gi < cnt; ++gi) {
+      // index opaque to loop-strength reduction: one base per group, immediate offsets
+      int io = gi;
+      asm volatile("" : "+s"(io));
+      const FitGroupA* g = gbase + io;
+      const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
+      const i32x8 fcv = *reinterpret_cast<const i32x8*>(g->fc);
+      const i32x8 Pv = *reinterpret_cast<const i32x8*>(g->P);
 #pragma unroll
-        for (int u = 0; u < FIT_GROUP / 2; ++u) {
-          const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
-          const f32x2 q = fcp * rcf2;  // two nodes' floor(fc / c), as integers
-          uint32_t m3[2];
+      for (int u = 0; u < FIT_GROUP / 2; ++u) {
+        const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
+        const f32x2 q = fcp * rcf2;  // two nodes' floor(fc / c), as integers
+        uint32_t m3[2];
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int k = 2 * u + h;
-            const uint32_t qm = (uint32_t)__double_as_longlong(f64_at(fmv, k) * rm);
-            const uint32_t qc = __float_as_uint(h ? q.y : q.x);
-            m3[h] = min(min(qc, qm), (uint32_t)Pv[k]);  // min(findMin(qc, qm), P)
-          }
-          acc32 += (int32_t)(m3[0] + m3[1]);
+        for (int h = 0; h < 2; ++h) {
+          const int k = 2 * u + h;
+          const uint32_t qm = (uint32_t)__double_as_longlong(f64_at(fmv, k) * rm);
+          const uint32_t qc = __float_as_uint(h ? q.y : q.x);
+          m3[h] = min(min(qc, qm), (uint32_t)Pv[k]);  // min(findMin(qc, qm), P)
         }
+        acc32 += (int32_t)(m3[0] + m3[1]);
       }
-      acc += (uint64_t)(int64_t)acc32;
     }
     set_round_nearest();
-  } else if (!wave_exact) {
-    // class B (and class-A lanes sharing its wave)
+    acc += (uint64_t)(int64_t)acc32;
+  };
+  // class B (and class-A lanes sharing its wave)
+  auto sum_b = [&](uint32_t g0, int cnt) {
+    cnt = __builtin_amdgcn_readfirstlane(cnt);  // keep the trip count scalar
     const FitGroup* gbase = fast_b + g0;
     const double bias = FIT_BIAS;
+    int32_t acc32 = 0;
     set_round_down();
-    for (int cb = 0; cb < cnt; cb += FIT_CHUNK_GROUPS) {
-      const int ce = cb + FIT_CHUNK_GROUPS < cnt ? cb + FIT_CHUNK_GROUPS : cnt;
-      int32_t acc32 = 0;
-      for (int gi = cb; gi < ce; ++gi) {
-        int io = gi;
-        asm volatile("" : "+s"(io));
-        const FitGroup* g = gbase + io;
-        const i32x16 fcv = *reinterpret_cast<const i32x16*>(g->fc);
-        const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
-        const i32x16 Pv = *reinterpret_cast<const i32x16*>(g->Pb);
+    for (int gi = 0; gi < cnt; ++gi) {
+      int io = gi;
+      asm volatile("" : "+s"(io));
+      const FitGroup* g = gbase + io;
+      const i32x16 fcv = *reinterpret_cast<const i32x16*>(g->fc);
+      const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
+      const i32x16 Pv = *reinterpret_cast<const i32x16*>(g->Pb);
 #pragma unroll
-        for (int u = 0; u < FIT_GROUP / 2; ++u) {
-          int32_t x[2];
+      for (int u = 0; u < FIT_GROUP / 2; ++u) {
+        int32_t x[2];
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int k = 2 * u + h;
-            const double qc = __builtin_fma(f64_at(fcv, k), rc, bias);  // 2^52 + floor(fc/c)
-            const double qm = __builtin_fma(f64_at(fmv, k), rm, bias);  // 2^52 + floor(fm/m)
-            const double xb = min_f64_s(__builtin_fmin(qc, qm), f64_at(Pv, k));
-            x[h] = (int32_t)(uint32_t)__double_as_longlong(xb);  // min(findMin(qc, qm), P)
-          }
-          acc32 += x[0] + x[1];
+        for (int h = 0; h < 2; ++h) {
+          const int k = 2 * u + h;
+          const double qc = __builtin_fma(f64_at(fcv, k), rc, bias);  // 2^52 + floor(fc/c)
+          const double qm = __builtin_fma(f64_at(fmv, k), rm, bias);  // 2^52 + floor(fm/m)
+          const double xb = min_f64_s(__builtin_fmin(qc, qm), f64_at(Pv, k));
+          x[h] = (int32_t)(uint32_t)__double_as_longlong(xb);  // min(findMin(qc, qm), P)
         }
+        acc32 += x[0] + x[1];
       }
-      acc += (uint64_t)(int64_t)acc32;
     }
     set_round_nearest();
-  } else {  // exact-path specs: every node row (SlowNode), this block's share of them
+    acc += (uint64_t)(int64_t)acc32;
+  };
+
+  if (KCC_FIT_QUEUE) {
+    // every wave of the workgroup runs the loop (the barrier per chunk); the slot the
+    // chunk's claim is read from was written before the previous barrier, the slot
+    // wave 0 writes during it was last read before that barrier
+    for (uint32_t k = 0;; ++k) {
+      const uint32_t cur = base + __builtin_amdgcn_readfirstlane(q_slot[k & 1u]);
+      if (cur >= lim) break;  // workgroup-uniform
+      claim_issue();
+      const int cnt = (int)((cur + qsz < lim ? cur + qsz : lim) - cur);
+      if (wave_fast) {
+        if (!wave_b) sum_a(cur, cnt);
+        else sum_b(cur, cnt);
+      }
+      claim_publish((k + 1u) & 1u);
+    }
+    if (wv == 0 && lane == 0) {  // this workgroup made its last claim
+      const uint32_t d = atomicAdd(qp + 1, 1u);
+      if (d == ((uint32_t)gy - sub + nsub - 1u) / nsub - 1u) {  // the segment's last one:
+        qp[0] = 0;                                               // reset for the next launch
+        qp[1] = 0;
+      }
+    }
+  } else if (wave_fast) {
+    for (uint32_t cur = nxt; cur < lim; cur += FIT_QCHUNK) {
+      const int cnt = (int)((cur + FIT_QCHUNK < lim ? cur + FIT_QCHUNK : lim) - cur);
+      if (!wave_b) sum_a(cur, cnt);
+      else sum_b(cur, cnt);
+    }
+  }
+  if (idle) return;
+  if (wave_exact) {  // exact-path specs: every node row (SlowNode), this workgroup's share
     const uint32_t nn = (uint32_t)n_nodes;  // < 2^28 per device
     const uint32_t pn = (nn + (uint32_t)gy - 1u) / (uint32_t)gy;
     const uint32_t a0 = (uint32_t)by * pn < nn ? (uint32_t)by * pn : nn;
-    int64_t i0 = a0, i1 = a0 + pn < nn ? a0 + pn : nn;
-    if (FIT_SPLIT > 1) {
-      const int64_t part = (i1 - i0 + FIT_SPLIT - 1) / FIT_SPLIT;
-      i0 = i0 + wv * part < i1 ? i0 + wv * part : i1;
-      i1 = i0 + part < i1 ? i0 + part : i1;
-    }
-    for (int64_t i = i0; i < i1; ++i) eval_slow(i);
-  }
-  if (!wave_exact) {  // rows outside the fast bounds, shared out over the node-chunk waves
+    const int64_t i1 = a0 + pn < nn ? a0 + pn : nn;
+    for (int64_t i = a0; i < i1; ++i) eval_slow(i);
+  } else {  // rows outside the fast bounds, shared out over the column's workgroups
     const int64_t n_slow = (int64_t)counters[CNT_SLOW_ROWS + chunk];
-    for (int64_t j = (int64_t)by * FIT_SPLIT + wv; j < n_slow; j += (int64_t)gy * FIT_SPLIT)
-      eval_slow(slow_list[j]);
+    for (int64_t j = by; j < n_slow; j += gy) eval_slow(slow_list[j]);
   }
 
   {  // (node, spec) pairs evaluated on the exact path (statistics)
     const unsigned long long act = __ballot(active);
-    if (slow_iters && (threadIdx.x & 63) == 0)
+    if (slow_iters && lane == 0)
       atomicAdd(&counters[CNT_SLOW_PAIRS], (unsigned long long)slow_iters * (unsigned long long)__popcll(act));
-  }
-  if (FIT_SPLIT > 1) {  // the waves of one spec group meet in LDS: one atomic per spec
-    __shared__ uint64_t red_s[2][FIT_SPLIT][FIT_SPW];
-    red_s[0][wv][threadIdx.x % FIT_SPW] = acc;
-    red_s[1][wv][threadIdx.x % FIT_SPW] = errs;
-    __syncthreads();
-    if (wv != 0) return;
-#pragma unroll
-    for (int k = 1; k < FIT_SPLIT; ++k) {
-      acc += red_s[0][k][threadIdx.x];
-      errs += red_s[1][k][threadIdx.x];
-    }
   }
 #ifdef KCC_FIT_DIAG_NO_ATOMICS  // diagnostic timing build only: results are wrong
   if (active && acc == 0x5A5A5A5A5A5A5A5Aull) partial[s] = (int64_t)acc;
@@ -1482,33 +1562,54 @@ hipError_t launch_clamp_apply(int64_t n_specs, ClampWork cw,
   return hipGetLastError();
 }
 
+int64_t fit_resident_blocks() {  // 256-thread fit workgroups resident on the device at once
+  static int64_t cache = 0;
+  if (cache == 0) {
+    int dev = 0, cus = 0, blocks = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fit_kernel, 256, 0) == hipSuccess &&
+        cus > 0 && blocks > 0)
+      cache = (int64_t)cus * blocks;
+    else
+      cache = 2048;
+  }
+  return cache;
+}
+
 hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,
                       const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
-                      unsigned long long* counters, int chunk, int64_t grid_nodes,
-                      hipStream_t s) {
+                      unsigned long long* counters, uint32_t* queue, int chunk,
+                      int64_t grid_nodes, hipStream_t s) {
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
   const int64_t gx = (n_specs + FIT_SPW - 1) / FIT_SPW;
   const int64_t n_groups = fit_groups(n_nodes);
-  // aim for KCC_FIT_TARGET_BLOCKS workgroups over `grid_nodes` nodes (the whole call's
-  // node count: a chunk of a pipelined call gets its share, not a full grid); 2048 =
-  // one round at 8 per CU, 16 rounds keep the ragged end of the last round short
-  // (measured best of 4k..128k at C4); >= 8 groups (64 nodes) each
-  int64_t gy_target = KCC_FIT_TARGET_BLOCKS / gx;
-  if (gy_target < 1) gy_target = 1;
-  const int64_t grid_groups = fit_groups(grid_nodes > n_nodes ? grid_nodes : n_nodes);
-  int64_t gpb = (grid_groups + gy_target - 1) / gy_target;
-  if (gpb < KCC_FIT_MIN_GPB) gpb = KCC_FIT_MIN_GPB;
-  int64_t gy = (n_groups + gpb - 1) / gpb;
-  // 1-D grid of gx * roundup(gy, 8) workgroups, remapped XCD-aware in the kernel; the
-  // buffer descriptor of a block's groups needs gpb * 160 B < 2^31
-  while (gx * ((gy + 7) / 8 * 8) > 0x7fffffffLL) {
-    gpb *= 2;
+  int64_t gy;
+  if (KCC_FIT_QUEUE) {
+    // one round of resident workgroups (the queue balances the waves; the stream's
+    // length is only known on the device); a chunk of a pipelined call gets its node
+    // share of the round; no more waves per column than claims at the full length
+    gy = KCC_FIT_ROUNDS * fit_resident_blocks() / gx;
+    if (grid_nodes > n_nodes) gy = gy * n_nodes / grid_nodes;
+    if (gy >= 16) gy = gy / 8 * 8;  // whole XCD rounds
+    const int64_t claims = (n_groups + FIT_QCHUNK - 1) / FIT_QCHUNK;
+    if (gy > claims) gy = claims;
+    if (gy < 1) gy = 1;
+  } else {
+    // static shares: aim for KCC_FIT_TARGET_BLOCKS workgroups over `grid_nodes` nodes,
+    // >= KCC_FIT_MIN_GPB groups each
+    int64_t gy_target = KCC_FIT_TARGET_BLOCKS / gx;
+    if (gy_target < 1) gy_target = 1;
+    const int64_t grid_groups = fit_groups(grid_nodes > n_nodes ? grid_nodes : n_nodes);
+    int64_t gpb = (grid_groups + gy_target - 1) / gy_target;
+    if (gpb < KCC_FIT_MIN_GPB) gpb = KCC_FIT_MIN_GPB;
     gy = (n_groups + gpb - 1) / gpb;
   }
-  if (gpb * (int64_t)sizeof(FitGroup) >= 0x7fffffffLL) return hipErrorInvalidValue;
+  // 1-D grid of gx * roundup(gy, 8) workgroups, remapped XCD-aware in the kernel
   const int64_t blocks = gx * ((gy + 7) / 8 * 8);
-  hipLaunchKernelGGL(fit_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, gpb, fast_a,
+  if (blocks > 0x7fffffffLL || gy > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fit_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, queue, fast_a,
                      fast_b, slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)chunk,
                      (int32_t)gx, (int32_t)gy);
   return hipGetLastError();

@@ -12,7 +12,7 @@ for W in "$@"; do
   mkdir -p $OUT
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o run \
     -- python3 bench.py --config $CFG --scaling strong --emulate-world $W --no-cpu-baseline \
-       --no-keyed --no-pods --no-parse --steps 50 --warmup 5 > $OUT/bench.log 2>&1 || exit $?
+       --no-keyed --no-pods --no-parse --no-dense --steps 50 --warmup 5 > $OUT/bench.log 2>&1 || exit $?
   f=$(find $OUT -name "*kernel_stats.csv" | head -1)
   echo "== $CFG W=$W: $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench.log)"
   python3 - "$f" <<'PY'

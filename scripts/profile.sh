@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-B="python3 bench.py --no-cpu-baseline"
+B="python3 bench.py --no-cpu-baseline --no-dense"
 timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run \
   -- $B --steps 20 > $OUT/trace.log 2>&1 || exit $?
