@@ -271,7 +271,8 @@ def main():
     fit_gbs = fit_bytes / (fit_ms * 1e-3) / 1e9
     fit_valu = streamed / chunks * ((S + 63) // 64) * FIT_VALU_PER_NODE_WAVE / (fit_ms * 1e-3)
     red_gbs = red_bytes / (red_ms * 1e-3) / 1e9
-    fit_traffic, tsrc = pmc_traffic("fit_kernel") if args.config == "C4" and world == 1 else (None, None)
+    c4_alone = args.config == "C4" and world == 1 and args.emulate_world <= 1  # the profiled run
+    fit_traffic, tsrc = pmc_traffic("fit_kernel") if c4_alone else (None, None)
     red_traffic, _ = pmc_traffic("reduce_kernel<2>") if tsrc else (None, None)
 
     out = {
@@ -391,7 +392,7 @@ def main():
                                            args.cpu_seconds)
     if rank == 0 and world == 1 and not args.no_keyed:
         out["keyed"] = keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream,
-                                 args.steps, args.warmup)
+                                 args.steps, args.warmup, c4_alone)
     if rank == 0 and world == 1 and not args.no_pods:
         out["pods"] = pods_leg(eng, ptr, cpu, mem, n, dev, stream, args.steps, args.warmup)
     if rank == 0 and world == 1 and not args.no_parse:
@@ -405,7 +406,8 @@ def main():
         dist.destroy_process_group()
 
 
-def keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream, steps, warmup):
+def keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream, steps, warmup,
+              with_traffic=True):
     """SURVEY §8f row 1, measured beside the step (not part of `value`): the C4 containers
     in a random order (a cluster-wide pod List, without even a pod's containers kept
     together: every container is its own run, the atomic worst case), each keyed by its
@@ -441,14 +443,21 @@ def keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream, steps, war
     alg = C * 20 + n * 16
     gbs = alg / (ms * 1e-3) / 1e9
     del key, kc, km, oc, om
+    kernels = ["kb_hist", "kb_scan", "kb_scatter<2>", "kb_accum<2>", "kb_escape"]
+    parts = [pmc_traffic(k) if with_traffic else (None, None) for k in kernels]
+    traffic = sum(t for t, _ in parts) if all(t is not None for t, _ in parts) else None
     return {
         "op": "per-row request sums of CC:290-293 from containers in list order (random)",
-        "kernel": "kb_hist + kb_scan + kb_scatter<2> + kb_accum<2>", "containers": C, "rows": n,
+        "kernel": " + ".join(kernels), "containers": C, "rows": n,
         "ms_per_launch": ms, "containers_per_s": C / (ms * 1e-3),
         "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": alg,
-                     "note": "bucketed: LDS histograms, staged scatter, LDS accumulation; "
-                             "no global atomics"},
+                     "traffic": traffic,
+                     "traffic_source": parts[0][1] and f"profiles/pmc_traffic.json ({parts[0][1]}); "
+                                                       "sum of the five kernels per call",
+                     "note": "bucketed: LDS histograms, scatter of 8-B records (row in bucket, "
+                             "low cpu bits, memory / 64; the rest on an escape list), LDS "
+                             "accumulation; no global atomics on the common path"},
         "equals_csr_reduce": diff_rows == 0, "rows_differing": diff_rows,
     }
 

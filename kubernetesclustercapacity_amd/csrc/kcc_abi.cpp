@@ -78,7 +78,8 @@ struct Dev {
   DevBuf alloc_cpu, alloc_mem, alloc_pods, pod_count, spec_cpu, spec_mem, partial, totals, err;
   DevBuf p_bytes, p_off, p_out, p_st;  // kcc_parse_* staging
   DevBuf k_key;                        // kcc_*_keyed staging
-  DevBuf kb_counts, kb_tot, kb_sk, kb_sv;  // kcc::KeyedWork (bucketed keyed reduce)
+  DevBuf kb_counts, kb_tot, kb_sr, kb_sv;  // kcc::KeyedWork (bucketed keyed reduce)
+  DevBuf kb_esc_n, kb_esc_row, kb_esc_cpu, kb_esc_mem;
   // kcc_pod_requests / kcc_reduce_requests_pods staging (app containers in cpu / mem)
   DevBuf q_ptr, q_iptr, q_icpu, q_imem, q_rst, q_ocpu, q_omem, q_pcpu, q_pmem;
 };
@@ -726,7 +727,8 @@ void kcc_destroy(kcc_ctx* ctx) {
                       &dv.alloc_cpu, &dv.alloc_mem, &dv.alloc_pods, &dv.pod_count, &dv.spec_cpu,
                       &dv.spec_mem,  &dv.partial,   &dv.totals,    &dv.err,
                       &dv.p_bytes,   &dv.p_off,     &dv.p_out,     &dv.p_st,      &dv.k_key,
-                      &dv.kb_counts, &dv.kb_tot,    &dv.kb_sk,     &dv.kb_sv,     &dv.q_ptr,
+                      &dv.kb_counts, &dv.kb_tot,    &dv.kb_sr,     &dv.kb_sv,     &dv.q_ptr,
+                      &dv.kb_esc_n,  &dv.kb_esc_row, &dv.kb_esc_cpu, &dv.kb_esc_mem,
                       &dv.q_iptr,    &dv.q_icpu,    &dv.q_imem,    &dv.q_rst,     &dv.q_ocpu,
                       &dv.q_omem,    &dv.q_pcpu,    &dv.q_pmem};
     for (DevBuf* b : bufs)
@@ -1145,14 +1147,26 @@ int keyed_work(kcc_ctx* ctx, Dev& dv, int64_t n_keys, int64_t n, int na, kcc::Ke
   *out = nullptr;
   if (!kcc::keyed_bucketed(n_keys, n)) return KCC_OK;
   const size_t nb = (size_t)kcc::keyed_buckets(n_keys), G = (size_t)kcc::keyed_tiles(n);
+  const size_t m = (size_t)(n > 0 ? n : 1);
   KCC_HIP(ctx, ensure(dv.kb_counts, 4 * nb * (G > 0 ? G : 1)));
   KCC_HIP(ctx, ensure(dv.kb_tot, 4 * nb));
-  KCC_HIP(ctx, ensure(dv.kb_sk, 2 * (size_t)(n > 0 ? n : 1)));
-  if (na > 0) KCC_HIP(ctx, ensure(dv.kb_sv, 8 * (size_t)na * (size_t)(n > 0 ? n : 1)));
+  KCC_HIP(ctx, ensure(dv.kb_sr, 8 * m));
+  if (na > 2) KCC_HIP(ctx, ensure(dv.kb_sv, 8 * (size_t)(na - 2) * m));
+  if (na >= 2) {
+    const size_t ne = (size_t)(n > 0 ? n : 1);
+    KCC_HIP(ctx, ensure(dv.kb_esc_n, 16));
+    KCC_HIP(ctx, ensure(dv.kb_esc_row, 4 * ne));
+    KCC_HIP(ctx, ensure(dv.kb_esc_cpu, 8 * ne));
+    KCC_HIP(ctx, ensure(dv.kb_esc_mem, 8 * ne));
+  }
   kw.counts = as<uint32_t>(dv.kb_counts);
   kw.tot = as<uint32_t>(dv.kb_tot);
-  kw.sk = as<uint16_t>(dv.kb_sk);
-  kw.sv = na > 0 ? as<uint64_t>(dv.kb_sv) : nullptr;
+  kw.sr = as<uint64_t>(dv.kb_sr);
+  kw.sv = na > 2 ? as<uint64_t>(dv.kb_sv) : nullptr;
+  kw.esc_n = na >= 2 ? as<uint32_t>(dv.kb_esc_n) : nullptr;
+  kw.esc_row = na >= 2 ? as<int32_t>(dv.kb_esc_row) : nullptr;
+  kw.esc_cpu = na >= 2 ? as<uint64_t>(dv.kb_esc_cpu) : nullptr;
+  kw.esc_mem = na >= 2 ? as<uint64_t>(dv.kb_esc_mem) : nullptr;
   *out = &kw;
   return KCC_OK;
 }

@@ -279,18 +279,26 @@ hipError_t launch_parse(int mode, int64_t n, const uint8_t* bytes, int64_t n_byt
                         const int64_t* offsets, int64_t* out, int8_t* status, hipStream_t s);
 
 // ---- keyed (list-order) reduce (kcc_keyed.hip) --------------------
-// Bucketed path: rows in buckets of KB_ROWS, containers in tiles of KB_TILE.
+// Bucketed path: rows in buckets of KB_ROWS, containers in tiles of about KB_TILE.
 constexpr int KB_SHIFT = 12;  // 4096 rows per bucket: ~1 KB runs per tile and array
 constexpr int KB_ROWS = 1 << KB_SHIFT;
-constexpr int KB_TILE = 32768;
+#ifndef KCC_KB_TILE
+#define KCC_KB_TILE 32768
+#endif
+constexpr int KB_TILE = KCC_KB_TILE;  // containers per scatter workgroup
 constexpr int64_t KB_NB_MAX = 4096;  // buckets (LDS cursors): n_keys <= 16M rows
 struct KeyedWork {
-  uint32_t* counts;  // [keyed_tiles(n) * keyed_buckets(n_keys)]
-  uint32_t* tot;     // [keyed_buckets(n_keys)]
-  uint16_t* sk;      // [n] scattered rows within the bucket
-  uint64_t* sv;      // [n][NA] scattered values, element-major (NA = 2 requests, 4 with
-                     // limits, 0 counts): one 16-B (32-B) store per element
+  uint32_t* counts;   // [keyed_tiles(n) * keyed_buckets(n_keys)]
+  uint32_t* tot;      // [keyed_buckets(n_keys)]
+  uint64_t* sr;       // [n] scattered 8-B records: row within the bucket, low 20 cpu
+                      // bits, memory / 64 (kcc_keyed.hip kb_record)
+  uint64_t* sv;       // [n][2] the limit values, element-major (NA = 4 only)
+  uint32_t* esc_n;    // escape list: what the records cannot hold (cpu >= 2^20: its high
+  int32_t* esc_row;   // [n]   bits; memory not a multiple of 64 in [0, 2^38): all of it)
+  uint64_t* esc_cpu;  // [n]
+  uint64_t* esc_mem;  // [n]
 };
+int64_t keyed_tile(int64_t n);   // containers per scatter workgroup (whole CU rounds)
 int64_t keyed_tiles(int64_t n);
 int64_t keyed_buckets(int64_t n_keys);
 bool keyed_bucketed(int64_t n_keys, int64_t n);

@@ -881,19 +881,6 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
 
 __global__ __launch_bounds__(256) void spec_place_kernel(PlaceArgs pa) { spec_place_body(pa, blockIdx.x); }
 
-// ---- clamp correction: D_s and partial[s] -= D_s ------------------------------------
-
-// inclusive suffix sum over the 64 lanes (lane k: Σ_{k' >= k})
-__device__ __forceinline__ uint64_t wave_suffix_u64(uint64_t v, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t u = __shfl_down(v, d);
-    if (lane + d < 64) v += u;
-  }
-  return v;
-}
-
-
 // ---- clamp correction: D_s and partial[s] -= D_s (one launch) ----------------------
 // clamp_apply_kernel: 2T workgroups of 1024 threads, after the fit.
 //   workgroup g < T (x-group g, the specs x = 64 g + l): H2[g] summed over its copies into

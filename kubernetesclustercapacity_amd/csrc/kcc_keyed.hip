@@ -32,6 +32,7 @@ constexpr int KY_BLOCK = KY_THREADS * KY_IPL;         // containers per workgrou
 
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void add_u64(uint64_t* p, uint64_t v) {
   __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v,
@@ -127,12 +128,12 @@ constexpr int KB_UNROLL = 8;
 // counts[g * nb + b] = #{valid containers of tile g in bucket b}
 __global__ __launch_bounds__(KB_HIST_THREADS) void kb_hist(int64_t n, int64_t n_keys,
                                                            const int32_t* __restrict__ key, int nb,
-                                                           uint32_t* __restrict__ counts) {
+                                                           uint32_t* __restrict__ counts, int64_t tile) {
   extern __shared__ uint32_t kb_h[];
   for (int b = threadIdx.x; b < nb; b += KB_HIST_THREADS) kb_h[b] = 0;
   __syncthreads();
-  const int64_t t0 = (int64_t)blockIdx.x * KB_TILE;
-  const int64_t t1 = min(t0 + (int64_t)KB_TILE, n);
+  const int64_t t0 = (int64_t)blockIdx.x * tile;
+  const int64_t t1 = min(t0 + tile, n);
   for (int64_t c0 = t0 + threadIdx.x; c0 < t1; c0 += (int64_t)KB_HIST_THREADS * KB_UNROLL) {
     int32_t k[KB_UNROLL];
 #pragma unroll
@@ -167,9 +168,11 @@ __device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t* sh) {
 // the bucket; tot[b] = the bucket's size
 __global__ __launch_bounds__(KB_SCAN_THREADS) void kb_scan(int64_t G, int nb,
                                                           uint32_t* __restrict__ counts,
-                                                          uint32_t* __restrict__ tot) {
+                                                          uint32_t* __restrict__ tot,
+                                                          uint32_t* __restrict__ esc_n) {
   __shared__ uint32_t sh[KB_SCAN_THREADS];
   const int b = blockIdx.x;
+  if (esc_n && b == 0 && threadIdx.x == 0) *esc_n = 0;  // (the call's first chunk)
   const int64_t per = (G + KB_SCAN_THREADS - 1) / KB_SCAN_THREADS;
   const int64_t g0 = (int64_t)threadIdx.x * per, g1 = min(g0 + per, G);
   uint32_t s = 0;
@@ -184,34 +187,67 @@ __global__ __launch_bounds__(KB_SCAN_THREADS) void kb_scan(int64_t G, int nb,
   if (threadIdx.x == KB_SCAN_THREADS - 1) tot[b] = incl;
 }
 
-// tile g: every valid container to its bucket's range (row in bucket, values).  The tile
-// goes in sub-chunks of KB_SUB: each element's rank within its bucket (LDS counters),
-// a scan of the sub-chunk's bucket counts, and a counting sort into an LDS stage, so that
-// the global writes leave in bucket order — a bucket's elements of one sub-chunk land on
-// consecutive addresses (its range in the bucket is this workgroup's, contiguous), and a
-// wave's stores coalesce instead of touching 64 lines.
-// sub-chunk size by value count: the stage (NA x 8 B + 6 B per element) plus up to 51 KB
-// of bucket cursors must fit 160 KB of LDS (4096: 0.38 ms at C4 vs 0.46 ms for 2048)
-constexpr int kb_sub(int na) { return na > 2 ? 2048 : 4096; }
+// tile g: every valid container to its bucket's range, as an 8-B record:
+//   bits  0-11  row within the bucket
+//   bits 12-31  the low 20 bits of the cpu request
+//   bits 32-63  the memory request / 64, when it is a multiple of 64 in [0, 2^38) (every
+//               Mi/Gi/M/G quantity up to 256 GiB), else 0
+// (+ with limits the two limit values as 64-bit words) — 8 B per container instead of 18.
+// A cpu request of 2^20 millicores or more, or a memory request outside that form, also
+// appends (row, cpu high bits, memory) to the escape list, added by kb_escape after the
+// accumulation (wrapping sums: the parts add to the requests exactly).  The tile goes in
+// sub-chunks of KB_SUB: each element's rank within its bucket (LDS counters), a scan of the
+// sub-chunk's bucket counts, and a counting sort into an LDS stage, so that the global
+// writes leave in bucket order — a bucket's elements of one sub-chunk land on consecutive
+// addresses (its range in the bucket is this workgroup's, contiguous), and a wave's stores
+// coalesce instead of touching 64 lines.
+constexpr int KB_CPU_BITS = 32 - KB_SHIFT;  // 20
+constexpr uint64_t KB_CPU_LO = ((uint64_t)1 << KB_CPU_BITS) - 1;
+constexpr int KB_MEM_SHIFT = 6;             // memory in units of 64 B
+constexpr int KB_MEM_MAX_BITS = 32 + KB_MEM_SHIFT;
+constexpr int kb_nv(int na) { return na > 2 ? na - 2 : 1; }  // 64-bit words beside the record
+#ifndef KCC_KB_SUB2
+#define KCC_KB_SUB2 4096
+#endif
+constexpr int kb_sub(int na) { return na > 2 ? 2048 : KCC_KB_SUB2; }
 
+// whether the record holds a memory request (a multiple of 64 in [0, 2^38))
+__device__ __forceinline__ bool kb_mem_ok(uint64_t mem) {
+  return (mem & ((1u << KB_MEM_SHIFT) - 1)) == 0 && (mem >> KB_MEM_MAX_BITS) == 0;
+}
+// the record of one container (NA >= 2)
+__device__ __forceinline__ uint64_t kb_record(uint32_t row, uint64_t cpu, uint64_t mem) {
+  return (uint64_t)row | (cpu & KB_CPU_LO) << KB_SHIFT |
+         (kb_mem_ok(mem) ? (mem >> KB_MEM_SHIFT) << 32 : 0ull);
+}
+
+#ifdef KCC_KB_SCATTER_WPE
+#define KB_SCATTER_ATTR __attribute__((amdgpu_waves_per_eu(KCC_KB_SCATTER_WPE)))
+#else
+#define KB_SCATTER_ATTR
+#endif
 template <int NA>
-__global__ __launch_bounds__(KB_HIST_THREADS) void kb_scatter(
+__global__ __launch_bounds__(KB_HIST_THREADS) KB_SCATTER_ATTR void kb_scatter(
     int64_t n, int64_t n_keys, const int32_t* __restrict__ key, const uint64_t* __restrict__ a0,
     const uint64_t* __restrict__ a1, const uint64_t* __restrict__ a2, const uint64_t* __restrict__ a3,
     int nb, const uint32_t* __restrict__ counts, const uint32_t* __restrict__ tot,
-    uint16_t* __restrict__ sk, uint64_t* __restrict__ sv) {
+    uint64_t* __restrict__ sr, uint64_t* __restrict__ sv, uint32_t* __restrict__ esc_n,
+    int32_t* __restrict__ esc_row, uint64_t* __restrict__ esc_cpu, uint64_t* __restrict__ esc_mem,
+    int64_t tile) {
+  constexpr int NV = kb_nv(NA);
   constexpr int NS = NA > 0 ? NA : 1;
   constexpr int KB_SUB = kb_sub(NA);
   constexpr int KB_SUB_PER = KB_SUB / KB_HIST_THREADS;
+  constexpr int SV_LEN = NA > 2 ? KB_SUB : 1;
   // dynamic LDS: cur[nb], lcnt[nb], lstart[nb], scan scratch[KB_HIST_THREADS]
   extern __shared__ uint32_t kb_dyn[];
   uint32_t* cur = kb_dyn;
   uint32_t* lcnt = cur + nb;
   uint32_t* lstart = lcnt + nb;
   uint32_t* sh = lstart + nb;
-  __shared__ uint64_t st_v[NS][KB_SUB];
+  __shared__ uint64_t st_r[KB_SUB];
+  __shared__ uint64_t st_v[NV][SV_LEN];
   __shared__ uint32_t st_pos[KB_SUB];
-  __shared__ uint16_t st_k[KB_SUB];
   const uint64_t* in[4] = {a0, a1, a2, a3};
   // this tile's cursors: bucket base (exclusive scan of tot) + the tile's offset in it
   const int per = (nb + KB_HIST_THREADS - 1) / KB_HIST_THREADS;
@@ -227,20 +263,42 @@ __global__ __launch_bounds__(KB_HIST_THREADS) void kb_scatter(
     run += tot[b];
   }
   __syncthreads();
-  const int64_t t0 = (int64_t)blockIdx.x * KB_TILE;
-  const int64_t t1 = min(t0 + (int64_t)KB_TILE, n);
+  const int64_t t0 = (int64_t)blockIdx.x * tile;
+  const int64_t t1 = min(t0 + tile, n);
   // sub-chunk loads run one sub-chunk ahead: issued before this one's scan, stage and
   // writes, consumed at the top of the next iteration
   int32_t kn[KB_SUB_PER];
   uint64_t vn[NS][KB_SUB_PER];
+  // 16-B loads: thread t takes quads of consecutive containers (4 keys, 2 x 2 values per
+  // array); the tile and sub-chunk starts are multiples of 4 and the arrays 16-B aligned
   auto load_sub = [&](int64_t c0) {
 #pragma unroll
-    for (int u = 0; u < KB_SUB_PER; ++u) {
-      const int64_t c = c0 + (int64_t)u * KB_HIST_THREADS + threadIdx.x;
-      const bool ok = c < t1;
-      kn[u] = ok ? __builtin_nontemporal_load(key + c) : -1;
+    for (int q = 0; q < KB_SUB_PER / 4; ++q) {
+      const int64_t c = c0 + 4 * ((int64_t)q * KB_HIST_THREADS + threadIdx.x);
+      if (c + 4 <= t1) {
+        const i32x4 kk = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(key + c));
+        kn[4 * q] = kk.x;
+        kn[4 * q + 1] = kk.y;
+        kn[4 * q + 2] = kk.z;
+        kn[4 * q + 3] = kk.w;
 #pragma unroll
-      for (int a = 0; a < NA; ++a) vn[a][u] = ok ? __builtin_nontemporal_load(in[a] + c) : 0;
+        for (int a = 0; a < NA; ++a) {
+          const u64x2 lo = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(in[a] + c));
+          const u64x2 hi = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(in[a] + c + 2));
+          vn[a][4 * q] = lo.x;
+          vn[a][4 * q + 1] = lo.y;
+          vn[a][4 * q + 2] = hi.x;
+          vn[a][4 * q + 3] = hi.y;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool ok = c + j < t1;
+          kn[4 * q + j] = ok ? key[c + j] : -1;
+#pragma unroll
+          for (int a = 0; a < NA; ++a) vn[a][4 * q + j] = ok ? in[a][c + j] : 0;
+        }
+      }
     }
   };
   load_sub(t0);
@@ -259,6 +317,15 @@ __global__ __launch_bounds__(KB_HIST_THREADS) void kb_scatter(
       const bool valid = k[u] >= 0 && (int64_t)k[u] < n_keys;
       if (!valid) k[u] = -1;
       rk[u] = valid ? atomicAdd(&lcnt[k[u] >> KB_SHIFT], 1u) : 0u;
+      if (NA >= 2 && valid) {
+        const bool mem_ok = kb_mem_ok(v[1 % NS][u]);
+        if (!mem_ok || (v[0][u] >> KB_CPU_BITS) != 0) {  // rare: what the record cannot hold
+          const uint32_t e = atomicAdd(esc_n, 1u);
+          esc_row[e] = k[u];
+          esc_cpu[e] = v[0][u] & ~KB_CPU_LO;
+          esc_mem[e] = mem_ok ? 0ull : v[1 % NS][u];
+        }
+      }
     }
     load_sub(c0 + KB_SUB);  // past t1: every lane reads nothing
     __syncthreads();
@@ -288,18 +355,19 @@ __global__ __launch_bounds__(KB_HIST_THREADS) void kb_scatter(
       if (k[u] < 0) continue;
       const int b = k[u] >> KB_SHIFT;
       const uint32_t slot = lstart[b] + rk[u];
+      const uint32_t row = (uint32_t)k[u] & (KB_ROWS - 1);
       st_pos[slot] = cur[b] + rk[u];
-      st_k[slot] = (uint16_t)(k[u] & (KB_ROWS - 1));
+      st_r[slot] = NA >= 2 ? kb_record(row, v[0][u], v[1 % NS][u]) : (uint64_t)row;
 #pragma unroll
-      for (int a = 0; a < NA; ++a) st_v[a][slot] = v[a][u];
+      for (int a = 2; a < NA; ++a) st_v[a - 2][slot] = v[a][u];
     }
     __syncthreads();
     const uint32_t nvalid = sh[KB_HIST_THREADS - 1];  // total of the lcnt scan
     for (uint32_t j = threadIdx.x; j < nvalid; j += KB_HIST_THREADS) {
       const uint32_t pos = st_pos[j];
-      sk[pos] = st_k[j];
+      sr[pos] = st_r[j];
 #pragma unroll
-      for (int a = 0; a < NA; ++a) sv[(int64_t)pos * NA + a] = st_v[a][j];  // element-major
+      for (int a = 2; a < NA; ++a) sv[(int64_t)pos * NV + a - 2] = st_v[a - 2][j];  // element-major
     }
     __syncthreads();  // nvalid read, stage drained before the counters change
     for (int b = b0; b < b1; ++b) {  // advance the cursors, clear the sub-chunk counts
@@ -310,14 +378,15 @@ __global__ __launch_bounds__(KB_HIST_THREADS) void kb_scatter(
   }
 }
 
-// bucket b: its range summed per row in LDS, rows [b * KB_ROWS, ...) written once
-// (NA == 0: counts the containers per row)
+// bucket b: its range summed per row in LDS, rows [b * KB_ROWS, ...) written once, zero
+// rows included (NA == 0: counts the containers per row)
 template <int NA>
 __global__ __launch_bounds__(KB_ACC_THREADS) void kb_accum(
     int64_t n, int64_t n_keys, int nb, const uint32_t* __restrict__ tot,
-    const uint16_t* __restrict__ sk, const uint64_t* __restrict__ sv, uint64_t* __restrict__ o0,
+    const uint64_t* __restrict__ sr, const uint64_t* __restrict__ sv, uint64_t* __restrict__ o0,
     uint64_t* __restrict__ o1, uint64_t* __restrict__ o2, uint64_t* __restrict__ o3) {
   constexpr int NACC = NA > 0 ? NA : 1;
+  constexpr int NV = kb_nv(NA);
   __shared__ unsigned long long acc[NACC][KB_ROWS];
   __shared__ uint32_t sh[KB_ACC_THREADS];
   uint64_t* out[4] = {o0, o1, o2, o3};
@@ -331,24 +400,67 @@ __global__ __launch_bounds__(KB_ACC_THREADS) void kb_accum(
   const uint32_t start = sh[KB_ACC_THREADS - 1];
   (void)base;
   const uint32_t end = start + tot[b];
-  for (int64_t i0 = (int64_t)start + threadIdx.x; i0 < (int64_t)end;
-       i0 += KB_ACC_THREADS * KB_UNROLL) {  // 64-bit: end may be close to 2^32
-    uint32_t r[KB_UNROLL];
-    uint64_t v[NACC][KB_UNROLL];
+  auto add_elem = [&](uint64_t rec, const uint64_t* vals) {  // one record into the LDS rows
+    const uint32_t r = (uint32_t)rec & (KB_ROWS - 1);
+    if (NA == 0) {
+      atomicAdd(&acc[0][r], 1ull);
+    } else {
+      atomicAdd(&acc[0][r], (unsigned long long)(((uint32_t)rec) >> KB_SHIFT));
+      atomicAdd(&acc[1][r], (unsigned long long)((rec >> 32) << KB_MEM_SHIFT));
 #pragma unroll
-    for (int u = 0; u < KB_UNROLL; ++u) {
-      const int64_t i = i0 + (int64_t)u * KB_ACC_THREADS;
-      const bool ok = i < end;
-      r[u] = ok ? (uint32_t)__builtin_nontemporal_load(sk + i) : 0xffffffffu;
-#pragma unroll
-      for (int a = 0; a < NACC; ++a)
-        v[a][u] = NA == 0 ? 1ull : (ok ? __builtin_nontemporal_load(sv + i * NA + a) : 0ull);
+      for (int a = 2; a < NA; ++a) atomicAdd(&acc[a][r], (unsigned long long)vals[a - 2]);
     }
+  };
+  // [start, end) in three parts: the 16-B aligned middle as pairs (one 16-B load of 2
+  // records, NV of 16-B loads of their limit values), the head and tail element by element
+  // (64-bit: end may be close to 2^32)
+  const int64_t a0 = ((int64_t)start + 1) & ~(int64_t)1, a1 = (int64_t)end & ~(int64_t)1;
+  if (a0 >= a1) {
+    for (int64_t i = (int64_t)start + threadIdx.x; i < (int64_t)end; i += KB_ACC_THREADS) {
+      uint64_t vals[NV];
 #pragma unroll
-    for (int u = 0; u < KB_UNROLL; ++u)
-      if (r[u] != 0xffffffffu)
+      for (int a = 0; a < NV; ++a) vals[a] = NA > 2 ? sv[i * NV + a] : 0ull;
+      add_elem(sr[i], vals);
+    }
+  } else {
+    if (threadIdx.x < 2) {  // head [start, a0) and tail [a1, end): at most 1 each
+      const int64_t i = threadIdx.x == 0 ? (int64_t)start : a1;
+      if (threadIdx.x == 0 ? i < a0 : i < (int64_t)end) {
+        uint64_t vals[NV];
 #pragma unroll
-        for (int a = 0; a < NACC; ++a) atomicAdd(&acc[a][r[u]], (unsigned long long)v[a][u]);
+        for (int a = 0; a < NV; ++a) vals[a] = NA > 2 ? sv[i * NV + a] : 0ull;
+        add_elem(sr[i], vals);
+      }
+    }
+    constexpr int QU = KB_UNROLL;  // pairs per thread in flight
+    for (int64_t q0 = a0 + 2 * (int64_t)threadIdx.x; q0 < a1; q0 += 2LL * KB_ACC_THREADS * QU) {
+      u64x2 w[QU];
+      u64x2 v[NV][QU];
+#pragma unroll
+      for (int u = 0; u < QU; ++u) {
+        const int64_t i = q0 + 2LL * KB_ACC_THREADS * u;
+        const bool ok = i < a1;
+        w[u] = ok ? __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(sr + i)) : u64x2{0, 0};
+#pragma unroll
+        for (int h = 0; h < NV; ++h)
+          v[h][u] = NA > 2 && ok ? __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(sv + i * NV) + h)
+                                 : u64x2{0, 0};
+      }
+#pragma unroll
+      for (int u = 0; u < QU; ++u) {
+        if (q0 + 2LL * KB_ACC_THREADS * u >= a1) continue;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          uint64_t vals[NV];
+#pragma unroll
+          for (int a = 0; a < NV; ++a) {
+            const int e = j * NV + a;  // the value's 8-B slot in the pair's limit words
+            vals[a] = (e & 1) ? v[e >> 1][u].y : v[e >> 1][u].x;
+          }
+          add_elem(j ? w[u].y : w[u].x, vals);
+        }
+      }
+    }
   }
   __syncthreads();
   const int64_t row0 = (int64_t)b * KB_ROWS;
@@ -359,9 +471,45 @@ __global__ __launch_bounds__(KB_ACC_THREADS) void kb_accum(
   }
 }
 
+// the escape list, added to its rows after the accumulation: the cpu requests' high parts
+// and the memory requests the records could not hold
+__global__ __launch_bounds__(256) void kb_escape(const uint32_t* __restrict__ esc_n,
+                                                 const int32_t* __restrict__ esc_row,
+                                                 const uint64_t* __restrict__ esc_cpu,
+                                                 const uint64_t* __restrict__ esc_mem,
+                                                 uint64_t* __restrict__ o0, uint64_t* __restrict__ o1) {
+  const uint32_t cnt = *esc_n;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < cnt; i += gridDim.x * 256u) {
+    const int32_t r = esc_row[i];
+    if (esc_cpu[i]) add_u64(o0 + r, esc_cpu[i]);
+    if (esc_mem[i]) add_u64(o1 + r, esc_mem[i]);
+  }
+}
+
 }  // namespace
 
-int64_t keyed_tiles(int64_t n) { return (n + KB_TILE - 1) / KB_TILE; }
+// Containers per scatter workgroup: about KB_TILE, cut so the tiles make whole rounds of
+// one workgroup per CU (the scatter's LDS and registers hold one per CU): 1209 tiles of
+// 32768 at C4 were 4.7 rounds, the last one 70 % full.
+int64_t keyed_tile(int64_t n) {
+  static int64_t cus = 0;
+  if (cus == 0) {
+    int dev = 0, c = 0;
+    cus = hipGetDevice(&dev) == hipSuccess &&
+                  hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                  c > 0
+              ? c
+              : 256;
+  }
+  if (n <= 0) return KB_TILE;
+  const int64_t rounds = (n + KB_TILE * cus - 1) / (KB_TILE * cus);
+  const int64_t t = (n + rounds * cus - 1) / (rounds * cus);
+  return (t + 3) / 4 * 4;  // quads: 16-B loads
+}
+int64_t keyed_tiles(int64_t n) {
+  const int64_t t = keyed_tile(n);
+  return (n + t - 1) / t;
+}
 int64_t keyed_buckets(int64_t n_keys) { return (n_keys + KB_ROWS - 1) / KB_ROWS; }
 bool keyed_bucketed(int64_t n_keys, int64_t n) {
   return n_keys > 0 && keyed_buckets(n_keys) <= KB_NB_MAX && n < ((int64_t)1 << 32);
@@ -371,21 +519,27 @@ template <int NA>
 static hipError_t run_bucketed(int64_t n_keys, int64_t n, const int32_t* key, const uint64_t* const* in,
                                uint64_t* const* out, const KeyedWork& kw, hipStream_t s) {
   const int nb = (int)keyed_buckets(n_keys);
-  const int64_t G = keyed_tiles(n);
-  if (n > 0) {
-    hipLaunchKernelGGL(kb_hist, dim3((unsigned)G), dim3(KB_HIST_THREADS), nb * sizeof(uint32_t), s, n,
-                       n_keys, key, nb, kw.counts);
-    hipLaunchKernelGGL(kb_scan, dim3((unsigned)nb), dim3(KB_SCAN_THREADS), 0, s, G, nb, kw.counts,
-                       kw.tot);
-    hipLaunchKernelGGL(kb_scatter<NA>, dim3((unsigned)G), dim3(KB_HIST_THREADS),
-                       (3 * nb + KB_HIST_THREADS) * sizeof(uint32_t), s, n, n_keys, key, in[0], in[1],
-                       in[2], in[3], nb, kw.counts, kw.tot, kw.sk, kw.sv);
-  } else {
+  if (n == 0) {
     hipError_t e = hipMemsetAsync(kw.tot, 0, sizeof(uint32_t) * (size_t)nb, s);
     if (e != hipSuccess) return e;
+  } else {
+    const int64_t tile = keyed_tile(n), G = keyed_tiles(n);
+    hipLaunchKernelGGL(kb_hist, dim3((unsigned)G), dim3(KB_HIST_THREADS), nb * sizeof(uint32_t), s, n,
+                       n_keys, key, nb, kw.counts, tile);
+    hipLaunchKernelGGL(kb_scan, dim3((unsigned)nb), dim3(KB_SCAN_THREADS), 0, s, G, nb, kw.counts,
+                       kw.tot, kw.esc_n);
+    hipLaunchKernelGGL(kb_scatter<NA>, dim3((unsigned)G), dim3(KB_HIST_THREADS),
+                       (3 * nb + KB_HIST_THREADS) * sizeof(uint32_t), s, n, n_keys, key, in[0], in[1],
+                       in[2], in[3], nb, kw.counts, kw.tot, kw.sr, kw.sv, kw.esc_n, kw.esc_row,
+                       kw.esc_cpu, kw.esc_mem, tile);
   }
   hipLaunchKernelGGL(kb_accum<NA>, dim3((unsigned)nb), dim3(KB_ACC_THREADS), 0, s, n, n_keys, nb,
-                     kw.tot, kw.sk, kw.sv, out[0], out[1], out[2], out[3]);
+                     kw.tot, kw.sr, kw.sv, out[0], out[1], out[2], out[3]);
+  if (NA >= 2 && n > 0) {
+    const int64_t g = (n + 255) / 256;
+    hipLaunchKernelGGL(kb_escape, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, s, kw.esc_n,
+                       kw.esc_row, kw.esc_cpu, kw.esc_mem, out[0], out[1]);
+  }
   return hipGetLastError();
 }
 

@@ -107,6 +107,67 @@ def run(names, config, rounds, reps, shard=1):
                           "identical_outputs": not nm.startswith("diag_")}))
 
 
+def run_keyed(names, config, rounds, reps):
+    """The keyed (list-order) reduce on the config's containers in a random order (the
+    bench's keyed leg), every variant checked equal to the CSR sums."""
+    import numpy as np
+    import torch
+
+    from kubernetesclustercapacity_amd import _lib, synth
+
+    dev = torch.device("cuda", 0)
+    cl = synth.config_cluster(config)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+    ptr, cpu, mem = T(cl.node_ptr), T(cl.cpu_req), T(cl.mem_req)
+    n, nc = cl.n_nodes, cl.n_containers
+    g = torch.Generator(device=dev)
+    g.manual_seed(20261016)
+    perm = torch.randperm(nc, device=dev, generator=g)
+    node_of = torch.repeat_interleave(torch.arange(n, device=dev, dtype=torch.int32), torch.diff(ptr))
+    key = node_of[perm].contiguous()
+    kc, km = cpu[perm].contiguous(), mem[perm].contiguous()
+    del perm, node_of
+    want_c = torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, torch.repeat_interleave(
+        torch.arange(n, device=dev), torch.diff(ptr)), cpu)
+    oc = torch.empty(n, dtype=torch.int64, device=dev)
+    om = torch.empty(n, dtype=torch.int64, device=dev)
+    P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    stream = torch.cuda.Stream(dev)
+    sh = C.c_void_p(stream.cuda_stream)
+    libs, ctxs = {}, {}
+    for nm in names:
+        L = _lib.load(os.path.join(VDIR, f"libkcc_{nm}.so"))
+        h = C.c_void_p()
+        assert L.kcc_create(C.byref(h), 0, 1) == 0, L.kcc_create_error()
+        libs[nm], ctxs[nm] = L, h
+
+    def keyed(nm):
+        assert libs[nm].kcc_reduce_requests_keyed_async(ctxs[nm], n, nc, P(key), P(kc), P(km), None,
+                                                        None, P(oc), P(om), None, None, sh) == 0
+    times = {nm: [] for nm in names}
+    ok = {}
+    with torch.cuda.stream(stream):
+        for nm in names:
+            keyed(nm)
+            torch.cuda.synchronize()
+            ok[nm] = bool(torch.equal(oc, want_c))
+        for _ in range(rounds):
+            for nm in names:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(reps):
+                    keyed(nm)
+                e1.record(stream)
+                e1.synchronize()
+                times[nm].append(e0.elapsed_time(e1) / reps)
+    alg = nc * 20 + n * 16
+    for nm in names:
+        ms = float(np.median(times[nm]))
+        print(json.dumps({"variant": nm, "config": config, "keyed_ms_median": ms,
+                          "keyed_ms_min": float(np.min(times[nm])),
+                          "frac": alg / (ms * 1e-3) / 8e12, "cpu_sums_equal_csr": ok[nm]}))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "build":
         build(sys.argv[2:])
@@ -119,5 +180,9 @@ if __name__ == "__main__":
         ap.add_argument("--rounds", type=int, default=5)
         ap.add_argument("--reps", type=int, default=10)
         ap.add_argument("--shard", type=int, default=1, help="use rank 0's nodes of this many")
+        ap.add_argument("--keyed", action="store_true", help="time the keyed reduce instead")
         a = ap.parse_args()
-        run(a.names, a.config, a.rounds, a.reps, a.shard)
+        if a.keyed:
+            run_keyed(a.names, a.config, a.rounds, a.reps)
+        else:
+            run(a.names, a.config, a.rounds, a.reps, a.shard)

@@ -90,6 +90,23 @@ def test_gpu_keyed_edges(eng):
         2, np.array([1, 1, 0], np.int32), np.array([1 << 63, 1 << 63, 5], np.uint64),
         np.array([-(1 << 63), -(1 << 63), 7], np.int64))
     assert r.cpu_requests.tolist() == [5, 0] and r.memory_requests.tolist() == [7, 0]
+    # staged records: row 4095 of a bucket with the low 20 cpu bits all ones (the all-ones
+    # 32-bit word), and cpu requests of 2^20 and more (their high parts on the escape list)
+    key = np.array([4095, 4095, 4095, 8191, 1], np.int32)
+    cpu = np.array([(1 << 20) - 1, (1 << 20) + 3, (1 << 64) - 1, (1 << 40) + 5, 1 << 20],
+                   np.uint64)
+    mem = np.array([1, 2, 3, 4, 5], np.int64)
+    r = eng.get_pod_cpu_memory_requests_limits_keyed(8192, key, cpu, mem)
+    o = oracle_keyed(8192, key, cpu, mem)
+    assert np.array_equal(r.cpu_requests, o[0]) and np.array_equal(r.memory_requests, o[1])
+    assert int(r.cpu_requests[4095]) == ((1 << 21) + 1) % (1 << 64)
+    # memory requests the 8-B record holds (multiples of 64 below 2^38) and the ones it does
+    # not (odd, negative, 2^38 and above): the latter on the escape list
+    mem = np.array([64, 100, -64, 1 << 38, (1 << 38) - 64], np.int64)
+    cpu = np.array([1, 2, 3, 4, 5], np.uint64)
+    r = eng.get_pod_cpu_memory_requests_limits_keyed(8192, key, cpu, mem)
+    o = oracle_keyed(8192, key, cpu, mem)
+    assert np.array_equal(r.cpu_requests, o[0]) and np.array_equal(r.memory_requests, o[1])
 
 
 @pytest.mark.gpu
