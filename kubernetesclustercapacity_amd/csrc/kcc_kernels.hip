@@ -186,6 +186,7 @@ void reduce_kernel(
   const int64_t wb = c0 + (int64_t)w * range;
   if (wb >= n_cont) return;  // wave-uniform; no block-level barrier in this kernel
   const int32_t len = (int32_t)(n_cont - wb < range ? n_cont - wb : range);
+  __builtin_assume(len >= 1);  // (wb < n_cont: the tile loop runs, its first loads need no guard)
   uint64_t (*pre)[RED_TILE] = pre_s[threadIdx.x >> 6];
   const uint64_t* in[4] = {in0, in1, in2, in3};
   uint64_t* out[4] = {out0, out1, out2, out3};
@@ -194,6 +195,19 @@ void reduce_kernel(
   for (int k = 0; k < NA; ++k)  // whole 16-B pairs only: an odd last item is fixed up below
     rs[k] = __builtin_amdgcn_make_buffer_rsrc((void*)(in[k] + wb), (short)0,
                                               (int)((len & ~1) * 8), 0x00020000);
+  // a ring of KCC_RED_PREFETCH + 1 tiles in registers: KCC_RED_PREFETCH in flight while
+  // one is reduced (static ring indices: the tile loop below is unrolled over the ring).
+  // The first tiles' loads go out first: they depend on the range alone, while the node
+  // lookups below are a chain of dependent loads (wave_node, then ptr)
+  constexpr int RING = KCC_RED_PREFETCH + 1;
+  uint64_t xs[RING][NA][4];
+#ifndef KCC_RED_LATE_PREFETCH
+#pragma unroll
+  for (int u = 0; u < KCC_RED_PREFETCH; ++u)
+#pragma unroll
+    for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 32, u * RED_TILE * 8, xs[u][k]);
+  __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink them below the lookups)
+#endif
 
   const int64_t node0 = wave_node[w];
   const bool first_open = ptr[node0] < wb;           // node0 began in an earlier range
@@ -243,14 +257,12 @@ void reduce_kernel(
     pend = false;
   };
 
-  // a ring of KCC_RED_PREFETCH + 1 tiles in registers: KCC_RED_PREFETCH in flight while
-  // one is reduced (static ring indices: the tile loop below is unrolled over the ring)
-  constexpr int RING = KCC_RED_PREFETCH + 1;
-  uint64_t xs[RING][NA][4];
+#ifdef KCC_RED_LATE_PREFETCH  // (A/B: the round-1 order, after the node lookups)
 #pragma unroll
   for (int u = 0; u < KCC_RED_PREFETCH; ++u)
 #pragma unroll
     for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 32, u * RED_TILE * 8, xs[u][k]);
+#endif
 
   auto tile = [&](uint64_t (&x)[NA][4], uint64_t (&nx)[NA][4], const int32_t tb) {
 #ifndef KCC_DIAG_RED_NOSTORE
