@@ -63,13 +63,14 @@ struct Dev {
   bool fitq_dirty = true;
   // spec setup + clamp correction (kcc::ClampWork)
   DevBuf c_rank, c_bcnt, c_cs, c_ms, c_mrc, c_crm, c_dperm;
-  DevBuf c_C, c_H2, c_H3, c_Crow, c_S2, c_S3;
+  DevBuf c_C, c_H2, c_H3, c_Crow, c_rec, c_dir;
   // the table copies C / H2 / H3 not known to be all zero (fresh allocation or an
   // interrupted call)
   bool clamp_dirty = true;
   int64_t last_pairs = 0;  // node x spec pairs of the last fit_prepare on this device
   int64_t c_stride = 0;    // cells per copy of the clamp table C
   int64_t h_stride = 0;    // cells per copy of the clamp tables H2 / H3
+  int64_t d_stride = 0;    // words per pass of the binned records' directory
   bool fit_dense = false;  // kcc_set_fit_dense: stream every node row through the fit
   int stream_chunks = 0;   // node chunks of the last fit prepare (their stream counters)
   int64_t prep_nodes = -1, prep_specs = -1;  // sizes the workspace was last prepared for
@@ -225,14 +226,18 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.c_H2, 8 * (size_t)kcc::H2_COPIES * (size_t)hs));
   KCC_HIP(ctx, ensure(dv.c_H3, 8 * (size_t)kcc::H2_COPIES * (size_t)hs));
   KCC_HIP(ctx, ensure(dv.c_Crow, 8 * (size_t)cs_));
-  KCC_HIP(ctx, ensure(dv.c_S2, 8 * (size_t)hs));
-  KCC_HIP(ctx, ensure(dv.c_S3, 8 * (size_t)hs));
+  if (kcc::clamp_binned((int64_t)S)) {  // node_prep's binned H2 / H3 records
+    const size_t passes = (size_t)kcc::clamp_passes((int64_t)N);
+    KCC_HIP(ctx, ensure(dv.c_rec, 8 * (size_t)kcc::CLAMP_PASS_RECS * passes));
+    KCC_HIP(ctx, ensure(dv.c_dir, 4 * (size_t)kcc::clamp_d_stride((int64_t)S) * passes));
+  }
   if (dv.c_C.bytes != before[0] || dv.c_H2.bytes != before[1] || dv.c_H3.bytes != before[2] ||
       dv.c_rank.bytes != before[3] ||
       dv.c_stride != cs_ || dv.h_stride != hs)
     dv.clamp_dirty = true;
   dv.c_stride = cs_;
   dv.h_stride = hs;
+  dv.d_stride = kcc::clamp_d_stride((int64_t)S);
   return KCC_OK;
 }
 
@@ -264,10 +269,12 @@ kcc::ClampWork clamp_of(Dev& dv) {
   cw.H2 = as<int64_t>(dv.c_H2);
   cw.H3 = as<int64_t>(dv.c_H3);
   cw.Crow = as<int64_t>(dv.c_Crow);
-  cw.S2 = as<int64_t>(dv.c_S2);
-  cw.S3 = as<int64_t>(dv.c_S3);
+  cw.rec = as<uint64_t>(dv.c_rec);
+  cw.dir = as<uint32_t>(dv.c_dir);
   cw.c_stride = dv.c_stride;
   cw.h_stride = dv.h_stride;
+  cw.d_stride = dv.d_stride;
+  cw.n_pass = 0;
   return cw;
 }
 
@@ -302,9 +309,9 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
                                      used_cpu, used_mem, as<kcc::FitGroupA>(dv.fast_a),
                                      as<kcc::FitGroup>(dv.fast_b), as<kcc::SlowNode>(dv.slow),
                                      as<int64_t>(dv.slow_list), n_specs, clamp_of(dv),
-                                     as<unsigned long long>(dv.counters), 0, s, dv.fit_dense));
+                                     as<unsigned long long>(dv.counters), 0, 0, s, dv.fit_dense));
   dv.stream_chunks = 1;
-  KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, clamp_of(dv),
+  KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, n_nodes, clamp_of(dv),
                                        as<unsigned long long>(dv.counters), partial, s));
   dv.clamp_dirty = false;
   return KCC_OK;
@@ -368,7 +375,7 @@ hipError_t prof_event(Dev& dv, hipEvent_t* ev) {
 // Chunk boundaries: node ranges of ~equal node count, multiples of CHUNK_ALIGN (a
 // multiple of FIT_GROUP: the fit's node groups do not straddle two chunks); at least
 // `min_nodes` nodes per chunk.
-constexpr int64_t CHUNK_ALIGN = 1024;
+constexpr int64_t CHUNK_ALIGN = kcc::CLAMP_PASS_ROWS;  // whole node_prep passes
 int plan_chunks(int64_t n_nodes, int want, int64_t min_nodes, std::vector<int64_t>& lo,
                 std::vector<int64_t>& hi) {
   int k = want;
@@ -495,7 +502,8 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                        as<kcc::FitGroup>(dv.fast_b) + lo[c] / kcc::FIT_GROUP,
                                        as<kcc::SlowNode>(dv.slow) + lo[c],
                                        as<int64_t>(dv.slow_list) + lo[c], n_specs, clamp_of(dv),
-                                       as<unsigned long long>(dv.counters), c, s, dv.fit_dense));
+                                       as<unsigned long long>(dv.counters), c, lo[c], s,
+                                       dv.fit_dense));
     ProfPair pp{};
     if (dv.prof_on) {
       KCC_HIP(ctx, prof_event(dv, &pp.a));
@@ -517,7 +525,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   // the pod-slot clamp of every chunk's fast rows, added back per spec
   if (n_specs > 0) {
     if (n_nodes > 0)
-      KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, clamp_of(dv),
+      KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, n_nodes, clamp_of(dv),
                                            as<unsigned long long>(dv.counters), partial, s));
     dv.clamp_dirty = false;
   }
@@ -719,7 +727,7 @@ void kcc_destroy(kcc_ctx* ctx) {
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
     DevBuf* bufs[] = {&dv.c_rank, &dv.c_bcnt, &dv.c_cs, &dv.c_ms,
                       &dv.c_mrc, &dv.c_crm, &dv.c_dperm, &dv.c_C, &dv.c_H2, &dv.c_H3,
-                      &dv.c_Crow, &dv.c_S2, &dv.c_S3,
+                      &dv.c_Crow, &dv.c_rec, &dv.c_dir,
                       &dv.wave_node, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
                       &dv.sperm,     &dv.fit_q,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,

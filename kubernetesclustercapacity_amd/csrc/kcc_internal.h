@@ -162,10 +162,16 @@ struct ClampWork {
   int64_t* H2;       // [H2_COPIES][h_stride]: T x 65 x 64, cell (g * 65 + k) * 64 + r
   int64_t* H3;       // [H2_COPIES][h_stride]: T x 65 x 64, cell (Y * 65 + j) * 64 + r
   int64_t* Crow;     // [c_stride]: C summed over the copies, suffix sums along GY
-  int64_t* S2;       // [h_stride]: H2 summed over the copies, 2-D suffix sums (k, r)
-  int64_t* S3;       // [h_stride]: the same for H3
+  // binned form of H2 / H3 (clamp_binned(S)): node_prep writes each 1024-row pass's
+  // (cell, w) records sorted by bin (x-group g: bin g; y-block Y: bin T + Y) into the
+  // pass's own slot range, and the bins' starts into dir; clamp_apply's workgroup for a
+  // bin sums that bin's records of every pass into LDS.  No global atomics.
+  uint64_t* rec;     // [n_pass][CLAMP_PASS_RECS]: cell | (int32 w) << 32
+  uint32_t* dir;     // [n_pass][d_stride]: a pass's bin starts (exclusive prefix) + its total
   int64_t c_stride;  // cells per C copy (clamp_c_cells(S) of the workspace)
   int64_t h_stride;  // cells per H2 / H3 copy (clamp_h_cells(S))
+  int64_t d_stride;  // clamp_d_stride(S) of the workspace
+  int64_t n_pass;    // passes of the call's node rows (set by launch_clamp_apply)
 };
 // specs per call
 constexpr int64_t MAX_SPECS = (int64_t)1 << 26;
@@ -179,6 +185,20 @@ constexpr int C_COPIES = KCC_C_COPIES;
 #define KCC_H2_COPIES 2
 #endif
 constexpr int H2_COPIES = KCC_H2_COPIES;
+// binned H2 / H3 (ClampWork::rec): node_prep's passes of CLAMP_PASS_ROWS rows (4 per
+// thread) emit at most one record of each table per row; up to CLAMP_BIN_T_MAX
+// x-groups (S <= 16384), larger S adds to the H2 / H3 copies with device atomics
+constexpr int CLAMP_PASS_ROWS = 4096;
+constexpr int CLAMP_PASS_RECS = 2 * CLAMP_PASS_ROWS;
+constexpr int64_t CLAMP_BIN_T_MAX = 256;
+#ifndef KCC_CLAMP_BINNED
+#define KCC_CLAMP_BINNED 1
+#endif
+__host__ __device__ inline bool clamp_binned(int64_t S) {
+  return KCC_CLAMP_BINNED && (S + 63) / 64 <= CLAMP_BIN_T_MAX;
+}
+inline int64_t clamp_d_stride(int64_t S) { return 2 * ((S + 63) / 64) + 1; }
+inline int64_t clamp_passes(int64_t n_nodes) { return (n_nodes + CLAMP_PASS_ROWS - 1) / CLAMP_PASS_ROWS; }
 // up to this many specs node_prep's search and count tables live in LDS; larger S
 // searches the same tables in global memory
 #ifndef KCC_CLAMP_LDS_SPECS
@@ -226,10 +246,10 @@ hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
                             const int64_t* spec_mem, SpecPrep sp, ClampWork cw, int64_t* partial,
                             unsigned long long* counters, hipStream_t s,
                             const MarkArgs* mark = nullptr, bool with_place = true);
-// The clamp correction after every node_prep of the call: clamp_prep (the tables summed
-// over their copies and zeroed, suffix sums) then clamp_query (partial[s] -= D_s for the
-// normal specs of clamp-free waves); leaves the table copies zero.
-hipError_t launch_clamp_apply(int64_t n_specs, ClampWork cw,
+// The clamp correction after every node_prep of the call (n_nodes: the call's rows, for
+// the binned records' pass count): partial[s] -= D_s for the normal specs of clamp-free
+// waves; leaves the table copies zero.
+hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
                               const unsigned long long* counters, int64_t* partial, hipStream_t s);
 
 // The fit's node stream (FitGroupA / FitGroup records) holds the rows that can contribute
@@ -237,13 +257,14 @@ hipError_t launch_clamp_apply(int64_t n_specs, ClampWork cw,
 // and P >= 1 (every other row adds exactly 0 there: qc = 0 or qm = 0 makes x = 0, and
 // P <= 0 rows are the clamp correction's), compacted per workgroup pass into
 // counters[CNT_STREAM + chunk] rows (padded to whole groups).  dense: stream every row (the
-// round-1 layout's cost: zero fields for the rows that add nothing).
+// round-1 layout's cost: zero fields for the rows that add nothing).  row0: the launch's
+// first row within the call (a multiple of CLAMP_PASS_ROWS; the binned records' passes).
 hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
                             SlowNode* slow, int64_t* slow_list, int64_t n_specs, ClampWork cw,
-                            unsigned long long* counters, int chunk, hipStream_t s,
+                            unsigned long long* counters, int chunk, int64_t row0, hipStream_t s,
                             bool dense = false);
 
 // partial[0..S) += Σ_i q(i,s), partial[S..2S) += #div-by-zero rows (internal order).

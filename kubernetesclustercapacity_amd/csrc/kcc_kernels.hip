@@ -28,6 +28,13 @@ __device__ uint64_t kcc_tl[4096][4];
 #define KCC_TL(slot, k) do { } while (0)
 #endif
 
+// 64-bit add into LDS (ds_add_u64) through a pointer the compiler cannot prove is LDS
+typedef __attribute__((address_space(3))) unsigned long long lds_ull;
+__device__ __forceinline__ void lds_add_u64(unsigned long long* p, uint64_t v) {
+  __hip_atomic_fetch_add((lds_ull*)p, (unsigned long long)v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 __device__ __forceinline__ unsigned long long atomic_add_u64(uint64_t* p, uint64_t v) {
   return atomicAdd(reinterpret_cast<unsigned long long*>(p),
                    static_cast<unsigned long long>(v));
@@ -485,10 +492,15 @@ __device__ __forceinline__ uint32_t count_lt64(const uint32_t* __restrict__ a, u
 // (zero fields, not listed).  SlowNode records are written for the slow rows, and for
 // every row when exact-path specs exist (their waves walk all rows).  Clamp correction:
 // each fast row with P >= 1 that dominates some spec adds its weight to at most one
-// cell each of C, H2 and H3; rows with P <= 0 to C[T+1][T+1] (ClampWork).
+// cell each of C, H2 and H3; rows with P <= 0 to C[T+1][T+1] (ClampWork).  C is summed
+// in LDS (S <= CLAMP_LDS_SPECS) and added to its copy once per workgroup; H2 / H3 leave as
+// binned records (clamp_binned(S)) — no scattered device atomics on the common path.
 #define KCC_NODE_PREP_BLOCK 1024
+constexpr int NP_RPT = CLAMP_PASS_ROWS / KCC_NODE_PREP_BLOCK;  // rows per thread and pass
+static_assert(NP_RPT * KCC_NODE_PREP_BLOCK == CLAMP_PASS_ROWS, "whole rows per thread");
+static_assert(CLAMP_PASS_RECS <= 0xffff, "record ranks packed in 16 bits");
 // diagnostic timing builds only (results are wrong): KCC_DIAG_NP bit 0 drops the clamp
-// tables' atomics (the cells stay live), bit 1 the x-group / y-block counts
+// tables' global atomics (the cells stay live), bit 1 the x-group / y-block counts
 #ifndef KCC_DIAG_NP
 #define KCC_DIAG_NP 0
 #endif
@@ -501,9 +513,16 @@ __device__ __forceinline__ void np_atomic(int64_t* p, int64_t w) {
 }
 static_assert(CLAMP_LDS_SPECS % KCC_NODE_PREP_BLOCK == 0, "node_prep table fill");
 #ifndef KCC_NODE_PREP_GRID
-#define KCC_NODE_PREP_GRID 512  // workgroups at most (2 per CU, one round; each fills its LDS tables once)
+#define KCC_NODE_PREP_GRID 1024  // workgroups at most (one resident round; each fills its LDS tables once)
 #endif
-constexpr size_t NODE_PREP_LDS = 16 * (size_t)CLAMP_LDS_SPECS;  // cs u32, ms i64, 2 x u16
+constexpr int NP_C_CELLS = (int)((CLAMP_LDS_SPECS / 64 + 2) * (CLAMP_LDS_SPECS / 64 + 2));
+// dynamic LDS: the search tables (cs u32, ms i64, 2 x u16) and the private C table, when
+// S <= CLAMP_LDS_SPECS
+#ifndef KCC_NP_CPRIV
+#define KCC_NP_CPRIV 1  // C summed in LDS per workgroup (one node_prep workgroup per CU)
+#endif
+constexpr size_t NODE_PREP_LDS = 16 * (size_t)CLAMP_LDS_SPECS + (KCC_NP_CPRIV ? 8 * (size_t)NP_C_CELLS : 0);
+constexpr int NP_BINS = 2 * (int)CLAMP_BIN_T_MAX;
 __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_cpu,
                                  const int64_t* __restrict__ alloc_mem,
                                  const int64_t* __restrict__ alloc_pods,
@@ -513,33 +532,45 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
                                  FitGroupA* __restrict__ fast_a, FitGroup* __restrict__ fast_b,
                                  SlowNode* __restrict__ slow, int64_t* __restrict__ slow_list,
                                  int64_t S, ClampWork cw, unsigned long long* __restrict__ counters,
-                                 int32_t chunk, int32_t dense) {
+                                 int32_t chunk, int32_t dense, int64_t pass0) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t stride = (int64_t)gridDim.x * CLAMP_PASS_ROWS;
   __shared__ uint32_t np_wc[KCC_NODE_PREP_BLOCK / 64];  // streamed rows per wave
   __shared__ uint64_t np_base;                          // this pass's stream position
   __shared__ uint32_t np_tot;
+  __shared__ uint32_t np_bcnt[NP_BINS];                 // binned records per bin (this pass)
+  __shared__ uint32_t np_bstart[NP_BINS];               // their exclusive prefix
   const bool want_b = counters[CNT_SPECS_B] != 0;  // written by spec setup (same stream)
   const int64_t nN = clamp_n_normal(counters);     // normal specs (clamp correction)
   const bool slow_all = nN < S;                    // exact-path specs exist
   const int64_t T = (nN + 63) / 64, W = T + 2;
+  const bool binned = clamp_binned(S);             // T <= CLAMP_BIN_T_MAX
+  const int NB = (int)(2 * T);                     // bins: x-groups, then y-blocks
   // this workgroup's copies of the tables: workgroups are dealt round-robin over the XCDs
   int64_t* Cc = cw.C + (int64_t)(blockIdx.x % C_COPIES) * cw.c_stride;
   int64_t* H2c = cw.H2 + (int64_t)(blockIdx.x % H2_COPIES) * cw.h_stride;
   int64_t* H3c = cw.H3 + (int64_t)(blockIdx.x % H2_COPIES) * cw.h_stride;
   // the sorted spec requests of the searches and the x-group / y-block members, in LDS
   // when they fit: c clamped to 2^23 (> every U = fc / P, fc < 2^23) as u32, m as i64,
-  // y-rank by x-rank and x-group by y-rank as u16 (padding 0xffff)
+  // y-rank by x-rank and x-group by y-rank as u16 (padding 0xffff); then C's private copy
   extern __shared__ __attribute__((aligned(16))) unsigned char np_lds[];
-  int64_t* ms_l = reinterpret_cast<int64_t*>(np_lds);
-  uint32_t* cs_l = reinterpret_cast<uint32_t*>(np_lds + 8 * CLAMP_LDS_SPECS);
-  uint16_t* mrc_l = reinterpret_cast<uint16_t*>(np_lds + 12 * CLAMP_LDS_SPECS);
-  uint16_t* xg_l = reinterpret_cast<uint16_t*>(np_lds + 14 * CLAMP_LDS_SPECS);
-  const bool lds = S <= CLAMP_LDS_SPECS;
+#ifndef KCC_NP_C_FIRST
+#define KCC_NP_C_FIRST 0
+#endif
+  constexpr size_t TB = KCC_NP_C_FIRST ? 8 * (size_t)NP_C_CELLS : 0;  // search tables' base
+  int64_t* ms_l = reinterpret_cast<int64_t*>(np_lds + TB);
+  uint32_t* cs_l = reinterpret_cast<uint32_t*>(np_lds + TB + 8 * CLAMP_LDS_SPECS);
+  uint16_t* mrc_l = reinterpret_cast<uint16_t*>(np_lds + TB + 12 * CLAMP_LDS_SPECS);
+  uint16_t* xg_l = reinterpret_cast<uint16_t*>(np_lds + TB + 14 * CLAMP_LDS_SPECS);
+  unsigned long long* c_l =
+      reinterpret_cast<unsigned long long*>(np_lds + (KCC_NP_C_FIRST ? 0 : 16 * CLAMP_LDS_SPECS));
+  const bool lds = S <= CLAMP_LDS_SPECS;  // then also W * W <= NP_C_CELLS: C in LDS
+  const bool cpriv = KCC_NP_CPRIV && lds;
   // smallest normal requests (rows below either dominate no spec); cs[0] >= 1
   const uint32_t cmin = nN > 0 ? (cw.cs[0] < FAST_FC_MAX ? (uint32_t)cw.cs[0] : (uint32_t)FAST_FC_MAX)
                                : 0xffffffffu;
   const int64_t mmin = nN > 0 ? cw.ms[0] : INT64_MAX;
+  for (int b = threadIdx.x; b < NP_BINS; b += KCC_NODE_PREP_BLOCK) np_bcnt[b] = 0;
   if (lds) {
     // every load first (one memory round trip), then the LDS writes
     constexpr int PER = (int)(CLAMP_LDS_SPECS / KCC_NODE_PREP_BLOCK);
@@ -561,57 +592,224 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       mrc_l[k] = yv[u] < 0xffffu ? (uint16_t)yv[u] : (uint16_t)0xffffu;
       xg_l[k] = xv[u] < 0xffffu ? (uint16_t)(xv[u] >> 6) : (uint16_t)0xffffu;
     }
+    if (cpriv)
+      for (int64_t e = threadIdx.x; e < W * W; e += KCC_NODE_PREP_BLOCK) c_l[e] = 0ull;
   }
+  // a C cell: the workgroup's LDS copy (an explicit LDS pointer: through the lambda the
+  // generic pointer became flat atomics), or the device copy
+  auto c_add = [&](int64_t cell, int64_t w) {
+    if (cpriv) lds_add_u64(c_l + cell, (uint64_t)w);
+    else np_atomic(&Cc[cell], w);
+  };
   __syncthreads();
   KCC_TL(3072 + blockIdx.x % 1024, 0);
-  // workgroup-uniform trip count (the stream positions meet in LDS)
-  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
-    const int64_t i = i0 + threadIdx.x;
-    const bool valid = i < n;
-    bool ok = false;
-    uint64_t fc_ok = 0;
-    int64_t fm_ok = 0, P_ok = 0;
-    int32_t cl_i = 0;
-    if (valid) {
-      const uint64_t ac = alloc_cpu[i], uc = used_cpu[i];
-      const int64_t am = alloc_mem[i], um = used_mem[i];
-      const int64_t P = alloc_pods[i], pc = pod_count[i];
-      const uint64_t fc = ac > uc ? ac - uc : 0;                                  // CC:119-123
-      const int64_t fm = am > um ? (int64_t)((uint64_t)am - (uint64_t)um) : 0;   // CC:125-129
-      const int64_t cl = (int64_t)((uint64_t)P - (uint64_t)pc);                  // CC:135
-      ok = fc < FAST_FC_MAX && fm >= 0 && fm < FAST_FM_MAX && P >= -FAST_P_ABS &&
-           P <= FAST_P_ABS && cl >= -FAST_CL_ABS && cl <= FAST_CL_ABS;
-      if (ok) {
-        fc_ok = fc;
-        fm_ok = fm;
-        P_ok = P;
-        cl_i = (int32_t)cl;
-      }
-      if (slow_all || !ok) {
-        SlowNode sn;
-        sn.fc = fc;
-        sn.fm = fm;
-        sn.P = P;
-        sn.cl = cl;
-        slow[i] = sn;
+  // Passes of NP_RPT x 1024 rows (thread t: rows i0 + t + 1024 r): every row's loads
+  // first, then the rows one after another; one stream position (a returning atomic on
+  // one word) and one bin scan per pass.  Workgroup-uniform trip count (the stream
+  // positions and the bins meet in LDS).
+  for (int64_t i0 = (int64_t)blockIdx.x * CLAMP_PASS_ROWS; i0 < n; i0 += stride) {
+    const int64_t pass = pass0 + i0 / CLAMP_PASS_ROWS;
+    uint64_t ld_ac[NP_RPT], ld_uc[NP_RPT];
+    int64_t ld_am[NP_RPT], ld_um[NP_RPT], ld_P[NP_RPT], ld_pc[NP_RPT];
+#pragma unroll
+    for (int r = 0; r < NP_RPT; ++r) {
+      const int64_t i = i0 + r * KCC_NODE_PREP_BLOCK + threadIdx.x;
+      ld_ac[r] = ld_uc[r] = 0;
+      ld_am[r] = ld_um[r] = ld_P[r] = ld_pc[r] = 0;
+      if (i < n) {
+        ld_ac[r] = alloc_cpu[i];
+        ld_uc[r] = used_cpu[i];
+        ld_am[r] = alloc_mem[i];
+        ld_um[r] = used_mem[i];
+        ld_P[r] = alloc_pods[i];
+        ld_pc[r] = pod_count[i];
       }
     }
-    {  // the fit's node stream: this pass's rows with something to add, compacted
-      const bool stream = dense ? valid : (ok && fc_ok > 0 && fm_ok > 0 && P_ok > 0);
-      const unsigned long long sb = __ballot(stream);
-      if (lane == 0) np_wc[wv] = (uint32_t)__popcll(sb);
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (int u = 0; u < KCC_NODE_PREP_BLOCK / 64; ++u) t += np_wc[u];
-        const uint32_t padded = (t + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP;  // whole groups
-        np_base = padded ? atomicAdd(&counters[CNT_STREAM + chunk], (unsigned long long)padded) : 0ull;
-        np_tot = t;
+    // phase 1, per row: the free capacity (the stream entry, kept across the barriers),
+    // the slow rows; the 64-bit loads die here
+    uint64_t r_fm[NP_RPT];                 // free memory of a fast row (< 2^50), else 0
+    uint32_t r_fc[NP_RPT];                 // free cpu of a fast row (< 2^23), else 0
+    int32_t r_P[NP_RPT], r_cl[NP_RPT];     // P, clamp of a fast row (|.| <= 2^20), else 0
+    unsigned long long okbal[NP_RPT];
+#pragma unroll
+    for (int r = 0; r < NP_RPT; ++r) {
+      const int64_t i = i0 + r * KCC_NODE_PREP_BLOCK + threadIdx.x;
+      const bool valid = i < n;
+      bool ok = false;
+      r_fm[r] = 0;
+      r_fc[r] = 0;
+      r_P[r] = 0;
+      r_cl[r] = 0;
+      if (valid) {
+        const uint64_t ac = ld_ac[r], uc = ld_uc[r];
+        const int64_t am = ld_am[r], um = ld_um[r];
+        const int64_t P = ld_P[r], pc = ld_pc[r];
+        const uint64_t fc = ac > uc ? ac - uc : 0;                                  // CC:119-123
+        const int64_t fm = am > um ? (int64_t)((uint64_t)am - (uint64_t)um) : 0;   // CC:125-129
+        const int64_t cl = (int64_t)((uint64_t)P - (uint64_t)pc);                  // CC:135
+        ok = fc < FAST_FC_MAX && fm >= 0 && fm < FAST_FM_MAX && P >= -FAST_P_ABS &&
+             P <= FAST_P_ABS && cl >= -FAST_CL_ABS && cl <= FAST_CL_ABS;
+        if (ok) {
+          r_fm[r] = (uint64_t)fm;
+          r_fc[r] = (uint32_t)fc;
+          r_P[r] = (int32_t)P;
+          r_cl[r] = (int32_t)cl;
+        }
+        if (slow_all || !ok) {
+          SlowNode sn;
+          sn.fc = fc;
+          sn.fm = fm;
+          sn.P = P;
+          sn.cl = cl;
+          slow[i] = sn;
+        }
       }
-      __syncthreads();
+      okbal[r] = __ballot(ok);
+      const unsigned long long bl = __ballot(valid && !ok);
+      if (bl) {
+        unsigned long long base = 0;
+        if (lane == 0)
+          base = atomicAdd(&counters[CNT_SLOW_ROWS + chunk], (unsigned long long)__popcll(bl));
+        base = __shfl(base, 0);
+        if (valid && !ok) slow_list[base + __popcll(bl & ((1ull << lane) - 1ull))] = i;
+      }
+    }
+    // phase 2, per row: the clamp correction's cells and records, the stream ballots
+    uint32_t bins[NP_RPT], rks[NP_RPT], cells[NP_RPT];
+    int32_t ws[NP_RPT];
+    unsigned long long sbal[NP_RPT];
+    uint32_t wave_streamed = 0;
+    uint64_t always_sum = 0;
+#pragma unroll
+    for (int r = 0; r < NP_RPT; ++r) {
+      const int64_t i = i0 + r * KCC_NODE_PREP_BLOCK + threadIdx.x;
+      const bool valid = i < n;
+      const bool ok = (okbal[r] >> lane) & 1ull;
+      const uint64_t fc_ok = r_fc[r];
+      const int64_t fm_ok = (int64_t)r_fm[r], P_ok = r_P[r];
+      const int32_t cl_i = r_cl[r];
+      // clamp correction: where (and with which weight) this row's pod-slot clamp applies
+      int64_t w = 0;
+      bool has2 = false, has3 = false;  // binned records of this row
+      uint32_t bin2 = 0, bin3 = 0, cell2 = 0, cell3 = 0;
+      if (ok && nN > 0) {
+        const int64_t P = P_ok, Penc = P > 0 ? P : 0;
+        w = Penc - (int64_t)cl_i;  // contribution = min(x, Penc) - w when clamped
+        if (P <= 0) {
+          always_sum += (uint64_t)w;  // x >= P for every spec
+        } else if (w != 0) {
+          // c <= U  <=>  floor(fc / c) >= P  and  m <= V  <=>  floor(fm / m) >= P, with
+          // U = floor(fc / P), V = floor(fm / P) from the rounded-up reciprocal of P
+          // (exact: fc, fm < 2^50, P < 2^51)
+          const double rP = recip_up_f64((uint64_t)P);
+          const uint32_t U = (uint32_t)((double)fc_ok * rP);
+          const int64_t V = (int64_t)((double)fm_ok * rP);
+          if (U >= cmin && V >= mmin) {  // else no spec is dominated
+            uint32_t L, b;
+            if (lds) {  // 8-ary searches over the +inf-padded 4096-entry tables: 4 steps of
+                        // 7 independent LDS reads each (a binary search chains 12)
+              L = search8_4096(cs_l, U);
+              b = search8_4096(ms_l, V);
+            } else {
+              L = upper_bound_count(cw.cs, nN, (uint64_t)U);
+              b = upper_bound_count(cw.ms, nN, V);
+            }
+            // L >= 1, b >= 1 (U >= cmin, V >= mmin)
+            const uint32_t GX = L >> 6, rx = L & 63u, GY = b >> 6, ry = b & 63u;
+            if (GX > 0 && GY > 0) c_add((int64_t)GX * W + GY, w);
+            if (rx > 0) {  // x-group GX (< T): k = #{its specs with y < b}
+              const uint32_t k = (KCC_DIAG_NP & 2) ? 1u
+                               : lds ? count_lt64(mrc_l + 64 * GX, b) : count_lt64(cw.mr_c + 64 * GX, b);
+              if (k > 0) {
+                if (binned) {
+                  has2 = true;
+                  bin2 = GX;
+                  cell2 = k * 64 + rx;
+                } else {
+                  np_atomic(&H2c[((int64_t)GX * 65 + k) * 64 + rx], w);
+                }
+              }
+            }
+            if (ry > 0 && GX > 0) {  // y-block GY (< T): j = #{its specs whose x-group < GX}
+              uint32_t j;
+              if (KCC_DIAG_NP & 2) {
+                j = 1;
+              } else if (lds) {
+                j = count_lt64(xg_l + 64 * GY, GX);
+              } else {  // x >> 6 < GX  <=>  x < 64 GX (padding: never)
+                j = count_lt64(cw.cr_m + 64 * GY, GX << 6);
+              }
+              if (j > 0) {
+                if (binned) {
+                  has3 = true;
+                  bin3 = (uint32_t)T + GY;
+                  cell3 = j * 64 + ry;
+                } else {
+                  np_atomic(&H3c[((int64_t)GY * 65 + j) * 64 + ry], w);
+                }
+              }
+            }
+          }
+        }
+      }
+      // the records' weight (|w| <= 2^21) and cells (< 2^13), their bins (0xffff: no
+      // record) and ranks within their bins (LDS counters, < 2^13 per pass: zeroed by
+      // the scan below), packed in 16-bit halves
+      ws[r] = (int32_t)w;
+      cells[r] = cell2 | cell3 << 16;
+      const uint32_t rk2 = has2 ? atomicAdd(&np_bcnt[bin2], 1u) : 0u;
+      const uint32_t rk3 = has3 ? atomicAdd(&np_bcnt[bin3], 1u) : 0u;
+      bins[r] = (has2 ? bin2 : 0xffffu) | (has3 ? bin3 : 0xffffu) << 16;
+      rks[r] = rk2 | rk3 << 16;
+      // the fit's node stream: the rows with something to add
+      const bool stream = dense ? valid : (ok && fc_ok > 0 && fm_ok > 0 && P_ok > 0);
+      sbal[r] = __ballot(stream);
+      wave_streamed += (uint32_t)__popcll(sbal[r]);
+    }
+    {  // rows clamped for every spec: one wave-summed add into C[T+1][T+1]
+      uint64_t v = always_sum;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+      if (lane == 0 && v) c_add((T + 1) * W + T + 1, (int64_t)v);
+    }
+    if (lane == 0) np_wc[wv] = wave_streamed;
+    __syncthreads();  // np_wc, and every record's rank
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (int u = 0; u < KCC_NODE_PREP_BLOCK / 64; ++u) t += np_wc[u];
+      const uint32_t padded = (t + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP;  // whole groups
+      np_base = padded ? atomicAdd(&counters[CNT_STREAM + chunk], (unsigned long long)padded) : 0ull;
+      np_tot = t;
+    }
+    if (binned && wv == 1) {
+      // the bins' starts: runs of per bins per lane, a shuffle scan of the run totals;
+      // the pass's directory row (starts + total) goes out here, the counters return to 0
+      const int per = (NB + 63) / 64;
+      const int b0 = lane * per, b1 = min(b0 + per, NB);
+      uint32_t ls = 0;
+      for (int b = b0; b < b1; ++b) ls += np_bcnt[b];
+      uint32_t li = ls;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(li, d, 64);
+        if (lane >= d) li += t;
+      }
+      uint32_t* drow = cw.dir + pass * cw.d_stride;
+      uint32_t run = li - ls;
+      for (int b = b0; b < b1; ++b) {
+        const uint32_t c = np_bcnt[b];
+        np_bstart[b] = run;
+        drow[b] = run;
+        np_bcnt[b] = 0;
+        run += c;
+      }
+      if (lane == 63) drow[NB] = li;
+    }
+    __syncthreads();
+    {
       uint32_t before = 0;
       for (int u = 0; u < wv; ++u) before += np_wc[u];
-      const uint64_t b0 = np_base;
+      const uint64_t sb0 = np_base + before;
       const uint32_t tot = np_tot;
       const uint32_t pad = (tot + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP - tot;
       auto put = [&](uint64_t pos, uint64_t fmv, uint32_t fcv, uint32_t Pv) {
@@ -627,76 +825,28 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
           g.Pb[k] = FIT_BIAS + (double)Pv;            // exact (P <= 2^20)
         }
       };
-      if (stream)  // P <= 0 streams only in the dense layout, as P = 0
-        put(b0 + before + (uint32_t)__popcll(sb & ((1ull << lane) - 1ull)), (uint64_t)fm_ok,
-            (uint32_t)fc_ok, P_ok > 0 ? (uint32_t)P_ok : 0u);
-      if (threadIdx.x < pad) put(b0 + tot + threadIdx.x, 0ull, 0u, 0u);  // the last group's padding
-    }
-    // clamp correction: where (and with which weight) this row's pod-slot clamp applies
-    bool always = false;
-    int64_t w = 0;
-    if (ok && nN > 0) {
-      const int64_t P = P_ok, Penc = P > 0 ? P : 0;
-      w = Penc - (int64_t)cl_i;  // contribution = min(x, Penc) - w when clamped
-      if (P <= 0) {
-        always = true;  // x >= P for every spec
-      } else if (w != 0) {
-        // c <= U  <=>  floor(fc / c) >= P  and  m <= V  <=>  floor(fm / m) >= P, with
-        // U = floor(fc / P), V = floor(fm / P) from the rounded-up reciprocal of P
-        // (exact: fc, fm < 2^50, P < 2^51)
-        const double rP = recip_up_f64((uint64_t)P);
-        const uint32_t U = (uint32_t)((double)fc_ok * rP);
-        const int64_t V = (int64_t)((double)fm_ok * rP);
-        if (U >= cmin && V >= mmin) {  // else no spec is dominated
-          uint32_t L, b;
-          if (lds) {  // 8-ary searches over the +inf-padded 4096-entry tables: 4 steps of
-                      // 7 independent LDS reads each (a binary search chains 12)
-            L = search8_4096(cs_l, U);
-            b = search8_4096(ms_l, V);
-          } else {
-            L = upper_bound_count(cw.cs, nN, (uint64_t)U);
-            b = upper_bound_count(cw.ms, nN, V);
-          }
-          // L >= 1, b >= 1 (U >= cmin, V >= mmin)
-          const uint32_t GX = L >> 6, rx = L & 63u, GY = b >> 6, ry = b & 63u;
-          if (GX > 0 && GY > 0)
-            np_atomic(&Cc[(int64_t)GX * W + GY], w);
-          if (rx > 0) {  // x-group GX: k = #{its specs with y < b}
-            const uint32_t k = (KCC_DIAG_NP & 2) ? 1u
-                             : lds ? count_lt64(mrc_l + 64 * GX, b) : count_lt64(cw.mr_c + 64 * GX, b);
-            if (k > 0)
-              np_atomic(&H2c[((int64_t)GX * 65 + k) * 64 + rx], w);
-          }
-          if (ry > 0 && GX > 0) {  // y-block GY: j = #{its specs whose x-group < GX}
-            uint32_t j;
-            if (KCC_DIAG_NP & 2) {
-              j = 1;
-            } else if (lds) {
-              j = count_lt64(xg_l + 64 * GY, GX);
-            } else {  // x >> 6 < GX  <=>  x < 64 GX (padding: never)
-              j = count_lt64(cw.cr_m + 64 * GY, GX << 6);
-            }
-            if (j > 0)
-              np_atomic(&H3c[((int64_t)GY * 65 + j) * 64 + ry], w);
-          }
-        }
-      }
-    }
-    {  // rows clamped for every spec: one wave-summed atomic into C[T+1][T+1]
-      uint64_t v = always ? (uint64_t)w : 0ull;
+      uint32_t done = 0;  // streamed rows of this wave's earlier row sets
+      uint64_t* prec = cw.rec + pass * CLAMP_PASS_RECS;
 #pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-      if (lane == 0 && v) atomic_add_u64(reinterpret_cast<uint64_t*>(&Cc[(T + 1) * W + T + 1]), v);
+      for (int r = 0; r < NP_RPT; ++r) {
+        if ((sbal[r] >> lane) & 1ull)  // P <= 0 streams only in the dense layout, as P = 0
+          put(sb0 + done + (uint32_t)__popcll(sbal[r] & ((1ull << lane) - 1ull)), r_fm[r], r_fc[r],
+              r_P[r] > 0 ? (uint32_t)r_P[r] : 0u);
+        done += (uint32_t)__popcll(sbal[r]);
+        const uint32_t b2 = bins[r] & 0xffffu, b3 = bins[r] >> 16;
+        const uint64_t wbits = (uint64_t)(uint32_t)ws[r] << 32;  // record: cell | w << 32
+        if (b2 != 0xffffu) prec[np_bstart[b2] + (rks[r] & 0xffffu)] = wbits | (cells[r] & 0xffffu);
+        if (b3 != 0xffffu) prec[np_bstart[b3] + (rks[r] >> 16)] = wbits | (cells[r] >> 16);
+      }
+      if (threadIdx.x < pad) put(np_base + tot + threadIdx.x, 0ull, 0u, 0u);  // the last group's padding
     }
-    const unsigned long long bl = __ballot(valid && !ok);
-    if (bl) {
-      unsigned long long base = 0;
-      if (lane == 0)
-        base = atomicAdd(&counters[CNT_SLOW_ROWS + chunk], (unsigned long long)__popcll(bl));
-      base = __shfl(base, 0);
-      if (valid && !ok) slow_list[base + __popcll(bl & ((1ull << lane) - 1ull))] = i;
+    __syncthreads();  // np_wc / np_base / np_bstart are rewritten by the next pass
+  }
+  if (cpriv) {  // the private C into this workgroup's device copy: its non-zero cells
+    for (int64_t e = threadIdx.x; e < W * W; e += KCC_NODE_PREP_BLOCK) {
+      const unsigned long long v = c_l[e];
+      if (v) np_atomic(&Cc[e], (int64_t)v);
     }
-    __syncthreads();  // np_wc / np_base are rewritten by the next pass
   }
   KCC_TL(3072 + blockIdx.x % 1024, 1);
 }
@@ -913,12 +1063,114 @@ constexpr int64_t C_FULL_CELLS = 4624;  // (T+2)^2 for T <= 66 (S <= 4224)
 constexpr int H_CELLS = 65 * 64;
 __host__ __device__ inline bool clamp_c_full(int64_t T) { return (T + 2) * (T + 2) <= C_FULL_CELLS; }
 
+// The bin's records of every pass summed into tab (64-bit LDS atomics), in windows of
+// CP_PW passes: each thread loads CP_PW / CP_THREADS passes' (start, count) of the bin,
+// a workgroup scan of the counts gives the window's records a flat numbering, and the
+// workgroup's lanes take consecutive records (coalesced loads; a lane per pass re-fetched
+// a whole line per 8-B record: 48 us at C4), CP_RB loads in flight per lane.
+#ifndef KCC_DIAG_CP
+#define KCC_DIAG_CP 0  // diagnostic timing builds only: bit 0 drops the adds, bit 1 the records
+#endif
+constexpr int CP_PW = 4096;
+constexpr int CP_RB = 8;  // records per thread in flight
+__device__ __forceinline__ void clamp_consume_bin(const ClampWork& cw, int64_t bin, uint64_t* tab,
+                                                  uint32_t* w_lo, uint32_t* w_off, uint64_t* scratch) {
+  constexpr int PPT = CP_PW / CP_THREADS;  // passes per thread and window
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint32_t* wsum = reinterpret_cast<uint32_t*>(scratch);  // CP_WAVES wave totals
+  for (int64_t p0 = 0; p0 < cw.n_pass; p0 += CP_PW) {
+    const int np = (int)(cw.n_pass - p0 < CP_PW ? cw.n_pass - p0 : CP_PW);
+    uint32_t lo[PPT], cnt[PPT];
+#pragma unroll
+    for (int u = 0; u < PPT; ++u) {
+      const int p = tid * PPT + u;
+      lo[u] = 0;
+      cnt[u] = 0;
+      if (p < np) {
+        const uint32_t* d = cw.dir + (p0 + p) * cw.d_stride + bin;
+        lo[u] = d[0];
+        cnt[u] = d[1];
+      }
+    }
+    uint32_t ts = 0;
+#pragma unroll
+    for (int u = 0; u < PPT; ++u) {
+      cnt[u] -= lo[u];
+      ts += cnt[u];
+    }
+    uint32_t inc = ts;  // inclusive scan over the workgroup: waves, then the wave totals
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t t = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += t;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < CP_WAVES; ++w2) {
+      const uint32_t t = wsum[w2];
+      before += w2 < wv ? t : 0u;
+      total += t;
+    }
+    uint32_t run = before + inc - ts;
+#pragma unroll
+    for (int u = 0; u < PPT; ++u) {
+      const int p = tid * PPT + u;
+      w_lo[p] = lo[u];
+      w_off[p] = run;
+      run += cnt[u];
+    }
+    if (tid == 0) w_off[CP_PW] = total;  // sentinel (passes past np hold count 0)
+    __syncthreads();
+    // record j of the window's flat numbering goes to thread j % CP_THREADS: a wave's
+    // loads cover consecutive records (one pass's run of the bin: whole lines), and each
+    // lane finds its record's pass by a binary search over w_off; batches of CP_RB loads
+    // per lane, the next batch in flight while the current one is added
+    const uint32_t step = (uint32_t)(CP_THREADS * CP_RB);
+    auto load_batch = [&](uint64_t (&rv)[CP_RB], uint32_t jb) {
+#pragma unroll
+      for (int u = 0; u < CP_RB; ++u) {
+        const uint32_t j = jb + (uint32_t)(u * CP_THREADS + tid);
+        rv[u] = 0;
+        if (j < total) {
+          int p = 0;  // the last pass with w_off[p] <= j (its count is > 0)
+#pragma unroll
+          for (int st = CP_PW / 2; st >= 1; st >>= 1)
+            if (w_off[p + st] <= j) p += st;
+          rv[u] = cw.rec[(p0 + p) * CLAMP_PASS_RECS + w_lo[p] + (j - w_off[p])];
+        }
+      }
+    };
+    auto add_batch = [&](const uint64_t (&rv)[CP_RB], uint32_t jb) {
+#pragma unroll
+      for (int u = 0; u < CP_RB; ++u)
+        if (KCC_DIAG_CP & 1) {  // diagnostic timing builds: no LDS atomics
+          if (rv[u] == 0x5a5a5a5a5a5a5a5aull) tab[0] = rv[u];
+        } else if (jb + (uint32_t)(u * CP_THREADS + tid) < total)
+          atomicAdd(reinterpret_cast<unsigned long long*>(&tab[(uint32_t)rv[u]]),
+                    (unsigned long long)(int64_t)(int32_t)(rv[u] >> 32));
+    };
+    uint64_t ra[CP_RB], rb[CP_RB];
+    load_batch(ra, 0);
+    for (uint32_t jb = 0; jb < ((KCC_DIAG_CP & 2) ? 0u : total); jb += 2 * step) {
+      load_batch(rb, jb + step);
+      add_batch(ra, jb);
+      load_batch(ra, jb + 2 * step);
+      add_batch(rb, jb + step);
+    }
+    __syncthreads();  // tab complete / the window's arrays free
+  }
+}
+
 __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
                                                                  const unsigned long long* __restrict__ counters,
                                                                  int64_t S, int64_t* __restrict__ partial) {
   __shared__ uint64_t tab[H_CELLS];
   __shared__ uint64_t ctot[CP_WAVES][64];
   __shared__ uint64_t colsum[128];
+  __shared__ uint32_t cp_lo[CP_PW];       // binned: a window's passes' bin starts
+  __shared__ uint32_t cp_off[CP_PW + 1];  // and the exclusive prefix of their counts
   const int64_t nN = clamp_n_normal(counters);
   const int64_t T = (nN + 63) / 64, W = T + 2;
   const int64_t u = blockIdx.x;
@@ -932,7 +1184,8 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   uint32_t other = 0xffffffffu;
   if (wv == 0) other = (x_side ? cw.mr_c : cw.cr_m)[q];  // y of x, or x of y (padding: ~0)
   if (tid < 128) colsum[tid] = 0;
-  // the table: every copy's cells first, then LDS and zeroes
+  // the table: binned records (below), or every copy's cells first, then LDS and zeroes
+  const bool binned = clamp_binned(S);
   int64_t* H = (x_side ? cw.H2 : cw.H3) + g * H_CELLS;
   constexpr int PER = (H_CELLS + CP_THREADS - 1) / CP_THREADS;
   uint64_t v[PER];
@@ -940,8 +1193,10 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   for (int k = 0; k < PER; ++k) {
     const int e = tid + CP_THREADS * k;
     v[k] = 0;
+    if (!binned) {
 #pragma unroll
-    for (int c = 0; c < H2_COPIES; ++c) v[k] += e < H_CELLS ? (uint64_t)H[c * cw.h_stride + e] : 0ull;
+      for (int c = 0; c < H2_COPIES; ++c) v[k] += e < H_CELLS ? (uint64_t)H[c * cw.h_stride + e] : 0ull;
+    }
   }
   // the coarse table's rows G > g (x side, C in the full form): loads first as well
   constexpr int CPER = (int)((C_FULL_CELLS + CP_THREADS - 1) / CP_THREADS);
@@ -962,11 +1217,14 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
     const int e = tid + CP_THREADS * k;
     if (e < H_CELLS) {
       tab[e] = v[k];
+      if (!binned) {
 #pragma unroll
-      for (int c = 0; c < H2_COPIES; ++c) H[c * cw.h_stride + e] = 0;  // zero between calls
+        for (int c = 0; c < H2_COPIES; ++c) H[c * cw.h_stride + e] = 0;  // zero between calls
+      }
     }
   }
   __syncthreads();  // tab and colsum's zeroes
+  if (binned) clamp_consume_bin(cw, x_side ? g : T + g, tab, cp_lo, cp_off, &ctot[0][0]);
   if (do_c) {
 #pragma unroll
     for (int k = 0; k < CPER; ++k) {
@@ -1518,15 +1776,33 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
                             SlowNode* slow, int64_t* slow_list, int64_t n_specs, ClampWork cw,
-                            unsigned long long* counters, int chunk, hipStream_t s, bool dense) {
+                            unsigned long long* counters, int chunk, int64_t row0, hipStream_t s,
+                            bool dense) {
   if (n_nodes <= 0) return hipSuccess;
+  if (row0 % CLAMP_PASS_ROWS != 0) return hipErrorInvalidValue;
+  // one resident round of workgroups (LDS-bound at S <= CLAMP_LDS_SPECS: one per CU)
+  const bool lds = n_specs <= CLAMP_LDS_SPECS;
+  const size_t lds_bytes = lds ? NODE_PREP_LDS : 0;
+  static int64_t resident[2] = {0, 0};
+  int64_t& res = resident[lds ? 1 : 0];
+  if (res == 0) {
+    int dev = 0, cus = 0, blocks = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, node_prep_kernel, KCC_NODE_PREP_BLOCK,
+                                                     lds_bytes) == hipSuccess &&
+        cus > 0 && blocks > 0)
+      res = (int64_t)cus * blocks;
+    else
+      res = 256;
+  }
+  const int64_t cap = res < KCC_NODE_PREP_GRID ? res : KCC_NODE_PREP_GRID;
   hipLaunchKernelGGL(node_prep_kernel,
-                     dim3(grid_for(fit_groups(n_nodes) * FIT_GROUP, KCC_NODE_PREP_BLOCK,
-                                   KCC_NODE_PREP_GRID)),
-                     dim3(KCC_NODE_PREP_BLOCK), NODE_PREP_LDS, s,
+                     dim3(grid_for(n_nodes, CLAMP_PASS_ROWS, cap)),
+                     dim3(KCC_NODE_PREP_BLOCK), lds_bytes, s,
                      n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu, used_mem,
                      fast_a, fast_b, slow, slow_list, n_specs, cw, counters, (int32_t)chunk,
-                     (int32_t)(dense ? 1 : 0));
+                     (int32_t)(dense ? 1 : 0), row0 / CLAMP_PASS_ROWS);
   return hipGetLastError();
 }
 
@@ -1549,9 +1825,10 @@ hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu, const int
   return hipGetLastError();
 }
 
-hipError_t launch_clamp_apply(int64_t n_specs, ClampWork cw,
+hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
                               const unsigned long long* counters, int64_t* partial, hipStream_t s) {
   if (n_specs <= 0) return hipSuccess;
+  cw.n_pass = clamp_passes(n_nodes);
   const int64_t T = (n_specs + 63) / 64;  // >= this call's T (normal specs only)
   if (!clamp_c_full(T))  // C's row suffix sums (the kernel exits when this call's C is full)
     hipLaunchKernelGGL(clamp_crows_kernel, dim3((unsigned)((T + 2 + 3) / 4)), dim3(256), 0, s, cw,
