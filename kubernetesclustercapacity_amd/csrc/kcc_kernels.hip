@@ -448,6 +448,18 @@ __device__ __forceinline__ uint32_t search8_4096(const T* a, T v) {
   return lo;
 }
 
+// #{k < 4096 : a[k] <= v} for a sorted ascending (binary: 12 dependent reads)
+#ifndef KCC_NP_SEARCH8
+#define KCC_NP_SEARCH8 0
+#endif
+template <class T>
+__device__ __forceinline__ uint32_t search2_4096(const T* a, T v) {
+  uint32_t lo = 0;  // after the step of width s the answer lies in [lo, lo + s]
+#pragma unroll
+  for (uint32_t s = 2048; s >= 1; s /= 2) lo += a[lo + s - 1] <= v ? s : 0u;
+  return lo;
+}
+
 // #{k < n : a[k] <= v} for a sorted ascending (binary search, n <= 2^31)
 template <class T>
 __device__ __forceinline__ uint32_t upper_bound_count(const T* __restrict__ a, int64_t n, T v) {
@@ -460,20 +472,8 @@ __device__ __forceinline__ uint32_t upper_bound_count(const T* __restrict__ a, i
   return (uint32_t)lo;
 }
 
-// #{l < 64 : a[l] < v} over one block of 64 entries (16-B aligned, padding >= every v):
-// the x-group / y-block counts of the clamp tables, unsorted, 64 compares
-__device__ __forceinline__ uint32_t count_lt64(const uint16_t* a, uint32_t v) {
-  const uint4* q = reinterpret_cast<const uint4*>(a);
-  uint32_t n = 0;
-#pragma unroll 2
-  for (int u = 0; u < 8; ++u) {
-    const uint4 w = q[u];
-    const uint32_t h[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) n += ((h[e] & 0xffffu) < v ? 1u : 0u) + ((h[e] >> 16) < v ? 1u : 0u);
-  }
-  return n;
-}
+// #{l < 64 : a[l] < v} over one unsorted block of 64 entries (16-B aligned, padding >=
+// every v): the counts from global memory (S > CLAMP_LDS_SPECS), 64 compares
 __device__ __forceinline__ uint32_t count_lt64(const uint32_t* __restrict__ a, uint32_t v) {
   const uint4* q = reinterpret_cast<const uint4*>(a);
   uint32_t n = 0;
@@ -500,7 +500,8 @@ constexpr int NP_RPT = CLAMP_PASS_ROWS / KCC_NODE_PREP_BLOCK;  // rows per threa
 static_assert(NP_RPT * KCC_NODE_PREP_BLOCK == CLAMP_PASS_ROWS, "whole rows per thread");
 static_assert(CLAMP_PASS_RECS <= 0xffff, "record ranks packed in 16 bits");
 // diagnostic timing builds only (results are wrong): KCC_DIAG_NP bit 0 drops the clamp
-// tables' global atomics (the cells stay live), bit 1 the x-group / y-block counts
+// tables' global atomics (the cells stay live), bit 1 the x-group / y-block counts, bit 2
+// the searches, bit 3 the stream writes
 #ifndef KCC_DIAG_NP
 #define KCC_DIAG_NP 0
 #endif
@@ -521,7 +522,13 @@ constexpr int NP_C_CELLS = (int)((CLAMP_LDS_SPECS / 64 + 2) * (CLAMP_LDS_SPECS /
 #ifndef KCC_NP_CPRIV
 #define KCC_NP_CPRIV 1  // C summed in LDS per workgroup (one node_prep workgroup per CU)
 #endif
-constexpr size_t NODE_PREP_LDS = 16 * (size_t)CLAMP_LDS_SPECS + (KCC_NP_CPRIV ? 8 * (size_t)NP_C_CELLS : 0);
+static_assert(CLAMP_LDS_SPECS == 4096, "node_prep's LDS member tables are 64 x 64");
+constexpr size_t NP_OFF_CS = 8 * (size_t)CLAMP_LDS_SPECS;            // ms i64, then cs u32
+constexpr size_t NP_OFF_MK = NP_OFF_CS + 4 * (size_t)CLAMP_LDS_SPECS;  // 64 x 64 u64 masks
+constexpr size_t NP_OFF_CK = NP_OFF_MK + 8 * 64 * 64;                 // 64 x 65 u8
+constexpr size_t NP_OFF_CJ = NP_OFF_CK + 64 * 65;                     // 64 x 65 u8
+constexpr size_t NP_OFF_C = (NP_OFF_CJ + 64 * 65 + 15) / 16 * 16;     // private C
+constexpr size_t NODE_PREP_LDS = NP_OFF_C + (KCC_NP_CPRIV ? 8 * (size_t)NP_C_CELLS : 0);
 constexpr int NP_BINS = 2 * (int)CLAMP_BIN_T_MAX;
 __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_cpu,
                                  const int64_t* __restrict__ alloc_mem,
@@ -550,50 +557,69 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   int64_t* Cc = cw.C + (int64_t)(blockIdx.x % C_COPIES) * cw.c_stride;
   int64_t* H2c = cw.H2 + (int64_t)(blockIdx.x % H2_COPIES) * cw.h_stride;
   int64_t* H3c = cw.H3 + (int64_t)(blockIdx.x % H2_COPIES) * cw.h_stride;
-  // the sorted spec requests of the searches and the x-group / y-block members, in LDS
-  // when they fit: c clamped to 2^23 (> every U = fc / P, fc < 2^23) as u32, m as i64,
-  // y-rank by x-rank and x-group by y-rank as u16 (padding 0xffff); then C's private copy
+  // in LDS when S <= CLAMP_LDS_SPECS: the sorted spec requests of the searches (c clamped
+  // to 2^23 (> every U = fc / P, fc < 2^23) as u32, m as i64); the member tables of the
+  // x-group / y-block counts: mk[g][Y] = bit set of the y-ranks in y-block Y of x-group g's
+  // specs, ck[g][Y] = #{specs of x-group g with y < 64 Y}, cj[Y][G] = #{specs of y-block
+  // Y whose x-group < G}; then C's private copy
   extern __shared__ __attribute__((aligned(16))) unsigned char np_lds[];
-#ifndef KCC_NP_C_FIRST
-#define KCC_NP_C_FIRST 0
-#endif
-  constexpr size_t TB = KCC_NP_C_FIRST ? 8 * (size_t)NP_C_CELLS : 0;  // search tables' base
-  int64_t* ms_l = reinterpret_cast<int64_t*>(np_lds + TB);
-  uint32_t* cs_l = reinterpret_cast<uint32_t*>(np_lds + TB + 8 * CLAMP_LDS_SPECS);
-  uint16_t* mrc_l = reinterpret_cast<uint16_t*>(np_lds + TB + 12 * CLAMP_LDS_SPECS);
-  uint16_t* xg_l = reinterpret_cast<uint16_t*>(np_lds + TB + 14 * CLAMP_LDS_SPECS);
-  unsigned long long* c_l =
-      reinterpret_cast<unsigned long long*>(np_lds + (KCC_NP_C_FIRST ? 0 : 16 * CLAMP_LDS_SPECS));
-  const bool lds = S <= CLAMP_LDS_SPECS;  // then also W * W <= NP_C_CELLS: C in LDS
+  int64_t* ms_l = reinterpret_cast<int64_t*>(np_lds);
+  uint32_t* cs_l = reinterpret_cast<uint32_t*>(np_lds + NP_OFF_CS);
+  unsigned long long* mk_l = reinterpret_cast<unsigned long long*>(np_lds + NP_OFF_MK);
+  uint8_t* ck_l = np_lds + NP_OFF_CK;
+  uint8_t* cj_l = np_lds + NP_OFF_CJ;
+  unsigned long long* c_l = reinterpret_cast<unsigned long long*>(np_lds + NP_OFF_C);
+  const bool lds = S <= CLAMP_LDS_SPECS;  // then T <= 64 and W * W <= NP_C_CELLS
   const bool cpriv = KCC_NP_CPRIV && lds;
   // smallest normal requests (rows below either dominate no spec); cs[0] >= 1
   const uint32_t cmin = nN > 0 ? (cw.cs[0] < FAST_FC_MAX ? (uint32_t)cw.cs[0] : (uint32_t)FAST_FC_MAX)
                                : 0xffffffffu;
   const int64_t mmin = nN > 0 ? cw.ms[0] : INT64_MAX;
   for (int b = threadIdx.x; b < NP_BINS; b += KCC_NODE_PREP_BLOCK) np_bcnt[b] = 0;
+  constexpr int PER = (int)(CLAMP_LDS_SPECS / KCC_NODE_PREP_BLOCK);
+  uint32_t yv[PER];  // y-rank of x-rank tid + 1024 u
   if (lds) {
     // every load first (one memory round trip), then the LDS writes
-    constexpr int PER = (int)(CLAMP_LDS_SPECS / KCC_NODE_PREP_BLOCK);
     uint64_t cv[PER], mv[PER];
-    uint32_t yv[PER], xv[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int64_t k = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
       cv[u] = k < nN ? cw.cs[k] : ~0ull;  // padded: +inf
       mv[u] = k < nN ? (uint64_t)cw.ms[k] : (uint64_t)INT64_MAX;
-      yv[u] = k < 64 * T ? cw.mr_c[k] : 0xffffffffu;
-      xv[u] = k < 64 * T ? cw.cr_m[k] : 0xffffffffu;
+      yv[u] = k < nN ? cw.mr_c[k] : 0xffffffffu;
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int64_t k = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
       cs_l[k] = cv[u] < FAST_FC_MAX ? (uint32_t)cv[u] : 0xffffffffu;
       ms_l[k] = (int64_t)mv[u];
-      mrc_l[k] = yv[u] < 0xffffu ? (uint16_t)yv[u] : (uint16_t)0xffffu;
-      xg_l[k] = xv[u] < 0xffffu ? (uint16_t)(xv[u] >> 6) : (uint16_t)0xffffu;
+      mk_l[k] = 0ull;  // 64 x 64 masks: one per spec slot
     }
     if (cpriv)
       for (int64_t e = threadIdx.x; e < W * W; e += KCC_NODE_PREP_BLOCK) c_l[e] = 0ull;
+  }
+  __syncthreads();  // masks zero
+  if (lds) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int64_t x = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
+      if (x < nN)
+        __hip_atomic_fetch_or((lds_ull*)(mk_l + (x >> 6) * 64 + (yv[u] >> 6)), 1ull << (yv[u] & 63),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  __syncthreads();  // masks complete
+  if (lds) {  // the prefix counts: row g along Y and column Y = g along G, lane = index
+    for (int g = wv; g < 64; g += KCC_NODE_PREP_BLOCK / 64) {
+      const uint64_t c1 = (uint64_t)__popcll(mk_l[g * 64 + lane]);
+      const uint64_t i1 = wave_incl_scan_u64(c1);
+      ck_l[g * 65 + lane] = (uint8_t)(i1 - c1);
+      if (lane == 63) ck_l[g * 65 + 64] = (uint8_t)i1;
+      const uint64_t c2 = (uint64_t)__popcll(mk_l[lane * 64 + g]);
+      const uint64_t i2 = wave_incl_scan_u64(c2);
+      cj_l[g * 65 + lane] = (uint8_t)(i2 - c2);
+      if (lane == 63) cj_l[g * 65 + 64] = (uint8_t)i2;
+    }
   }
   // a C cell: the workgroup's LDS copy (an explicit LDS pointer: through the lambda the
   // generic pointer became flat atomics), or the device copy
@@ -675,8 +701,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       }
     }
     // phase 2, per row: the clamp correction's cells and records, the stream ballots
-    uint32_t bins[NP_RPT], rks[NP_RPT], cells[NP_RPT];
-    int32_t ws[NP_RPT];
+    uint32_t pk1[NP_RPT], pk2[NP_RPT], pk3[NP_RPT];  // the records, packed (below)
     unsigned long long sbal[NP_RPT];
     uint32_t wave_streamed = 0;
     uint64_t always_sum = 0;
@@ -706,10 +731,15 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
           const int64_t V = (int64_t)((double)fm_ok * rP);
           if (U >= cmin && V >= mmin) {  // else no spec is dominated
             uint32_t L, b;
-            if (lds) {  // 8-ary searches over the +inf-padded 4096-entry tables: 4 steps of
-                        // 7 independent LDS reads each (a binary search chains 12)
-              L = search8_4096(cs_l, U);
-              b = search8_4096(ms_l, V);
+            if (lds) {  // searches over the +inf-padded 4096-entry tables: binary (12
+                        // dependent LDS reads; four rows per thread overlap them) or
+                        // 8-ary (4 steps of 7 independent reads: 28, LDS-issue-bound)
+              L = KCC_NP_SEARCH8 ? search8_4096(cs_l, U) : search2_4096(cs_l, U);
+              b = KCC_NP_SEARCH8 ? search8_4096(ms_l, V) : search2_4096(ms_l, V);
+              if (KCC_DIAG_NP & 4) {  // diagnostic: no searches
+                L = 1 + (U & 2047);
+                b = 1 + ((uint32_t)V & 2047);
+              }
             } else {
               L = upper_bound_count(cw.cs, nN, (uint64_t)U);
               b = upper_bound_count(cw.ms, nN, V);
@@ -718,8 +748,16 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
             const uint32_t GX = L >> 6, rx = L & 63u, GY = b >> 6, ry = b & 63u;
             if (GX > 0 && GY > 0) c_add((int64_t)GX * W + GY, w);
             if (rx > 0) {  // x-group GX (< T): k = #{its specs with y < b}
-              const uint32_t k = (KCC_DIAG_NP & 2) ? 1u
-                               : lds ? count_lt64(mrc_l + 64 * GX, b) : count_lt64(cw.mr_c + 64 * GX, b);
+              uint32_t k;
+              if (KCC_DIAG_NP & 2) {
+                k = 1;
+              } else if (lds) {  // the members below y-block b >> 6, + those in it below b
+                const uint32_t Yb = b >> 6, o = b & 63u;
+                k = ck_l[GX * 65 + Yb];
+                if (o) k += (uint32_t)__popcll(mk_l[GX * 64 + Yb] & ((1ull << o) - 1ull));
+              } else {
+                k = count_lt64(cw.mr_c + 64 * GX, b);
+              }
               if (k > 0) {
                 if (binned) {
                   has2 = true;
@@ -735,7 +773,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
               if (KCC_DIAG_NP & 2) {
                 j = 1;
               } else if (lds) {
-                j = count_lt64(xg_l + 64 * GY, GX);
+                j = cj_l[GY * 65 + GX];
               } else {  // x >> 6 < GX  <=>  x < 64 GX (padding: never)
                 j = count_lt64(cw.cr_m + 64 * GY, GX << 6);
               }
@@ -752,15 +790,17 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
           }
         }
       }
-      // the records' weight (|w| <= 2^21) and cells (< 2^13), their bins (0xffff: no
-      // record) and ranks within their bins (LDS counters, < 2^13 per pass: zeroed by
-      // the scan below), packed in 16-bit halves
-      ws[r] = (int32_t)w;
-      cells[r] = cell2 | cell3 << 16;
+      // the records in three words: cells (13 bits each, 0: no record — a record's cell
+      // is >= 64), ranks within their bins (LDS counters, < 2^13 per pass: zeroed by the
+      // scan below), bins (9 bits each), and the weight (|w| <= 2^21, 23 bits) in 6/6/11
+      // bit slices: pk1 = cell2 | cell3 << 13 | w[0:6] << 26, pk2 = rk2 | rk3 << 13 |
+      // w[6:12] << 26, pk3 = bin2 | bin3 << 9 | w[12:] << 18 (arithmetic)
       const uint32_t rk2 = has2 ? atomicAdd(&np_bcnt[bin2], 1u) : 0u;
       const uint32_t rk3 = has3 ? atomicAdd(&np_bcnt[bin3], 1u) : 0u;
-      bins[r] = (has2 ? bin2 : 0xffffu) | (has3 ? bin3 : 0xffffu) << 16;
-      rks[r] = rk2 | rk3 << 16;
+      const uint32_t wu = (uint32_t)(int32_t)w;
+      pk1[r] = (has2 ? cell2 : 0u) | (has3 ? cell3 : 0u) << 13 | (wu & 63u) << 26;
+      pk2[r] = rk2 | rk3 << 13 | ((wu >> 6) & 63u) << 26;
+      pk3[r] = bin2 | bin3 << 9 | (uint32_t)((int32_t)wu >> 12) << 18;
       // the fit's node stream: the rows with something to add
       const bool stream = dense ? valid : (ok && fc_ok > 0 && fm_ok > 0 && P_ok > 0);
       sbal[r] = __ballot(stream);
@@ -829,14 +869,17 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       uint64_t* prec = cw.rec + pass * CLAMP_PASS_RECS;
 #pragma unroll
       for (int r = 0; r < NP_RPT; ++r) {
-        if ((sbal[r] >> lane) & 1ull)  // P <= 0 streams only in the dense layout, as P = 0
+        if (!(KCC_DIAG_NP & 8) && ((sbal[r] >> lane) & 1ull))  // P <= 0 streams only in the dense layout, as P = 0
           put(sb0 + done + (uint32_t)__popcll(sbal[r] & ((1ull << lane) - 1ull)), r_fm[r], r_fc[r],
               r_P[r] > 0 ? (uint32_t)r_P[r] : 0u);
         done += (uint32_t)__popcll(sbal[r]);
-        const uint32_t b2 = bins[r] & 0xffffu, b3 = bins[r] >> 16;
-        const uint64_t wbits = (uint64_t)(uint32_t)ws[r] << 32;  // record: cell | w << 32
-        if (b2 != 0xffffu) prec[np_bstart[b2] + (rks[r] & 0xffffu)] = wbits | (cells[r] & 0xffffu);
-        if (b3 != 0xffffu) prec[np_bstart[b3] + (rks[r] >> 16)] = wbits | (cells[r] >> 16);
+        const uint32_t c2 = pk1[r] & 0x1fffu, c3 = (pk1[r] >> 13) & 0x1fffu;
+        if (c2 | c3) {
+          const int32_t wr = (int32_t)pk3[r] >> 18 << 12 | (int32_t)((pk2[r] >> 26) << 6 | pk1[r] >> 26);
+          const uint64_t wbits = (uint64_t)(uint32_t)wr << 32;  // record: cell | w << 32
+          if (c2) prec[np_bstart[pk3[r] & 0x1ffu] + (pk2[r] & 0x1fffu)] = wbits | c2;
+          if (c3) prec[np_bstart[(pk3[r] >> 9) & 0x1ffu] + ((pk2[r] >> 13) & 0x1fffu)] = wbits | c3;
+        }
       }
       if (threadIdx.x < pad) put(np_base + tot + threadIdx.x, 0ull, 0u, 0u);  // the last group's padding
     }
@@ -1065,9 +1108,9 @@ __host__ __device__ inline bool clamp_c_full(int64_t T) { return (T + 2) * (T + 
 
 // The bin's records of every pass summed into tab (64-bit LDS atomics), in windows of
 // CP_PW passes: each thread loads CP_PW / CP_THREADS passes' (start, count) of the bin,
-// a workgroup scan of the counts gives the window's records a flat numbering, and the
-// workgroup's lanes take consecutive records (coalesced loads; a lane per pass re-fetched
-// a whole line per 8-B record: 48 us at C4), CP_RB loads in flight per lane.
+// a workgroup scan of the counts gives the window's records a flat numbering, and each
+// wave's lanes take consecutive records (coalesced loads; a lane per pass re-fetched a
+// whole line per 8-B record: 48 us at C4), CP_RB loads in flight per lane.
 #ifndef KCC_DIAG_CP
 #define KCC_DIAG_CP 0  // diagnostic timing builds only: bit 0 drops the adds, bit 1 the records
 #endif
@@ -1123,22 +1166,39 @@ __device__ __forceinline__ void clamp_consume_bin(const ClampWork& cw, int64_t b
     }
     if (tid == 0) w_off[CP_PW] = total;  // sentinel (passes past np hold count 0)
     __syncthreads();
-    // record j of the window's flat numbering goes to thread j % CP_THREADS: a wave's
-    // loads cover consecutive records (one pass's run of the bin: whole lines), and each
-    // lane finds its record's pass by a binary search over w_off; batches of CP_RB loads
-    // per lane, the next batch in flight while the current one is added
-    const uint32_t step = (uint32_t)(CP_THREADS * CP_RB);
+    // the window's records in flat order, a contiguous share per wave (whole 64-record
+    // rows): lane l takes records J0 + 64 k + l, so a wave's loads cover consecutive
+    // records (one pass's run of the bin: whole lines).  A lane's pass only moves
+    // forward: one step (or a binary search over w_off when it jumps further) per record
+    // instead of a search per record (12 dependent LDS reads each: 16 us at C4).
+    int top = 1;  // highest power of two <= np (w_off[np ..] = total)
+    while (2 * top <= np) top *= 2;
+    auto search = [&](uint32_t j) {  // the last pass with w_off[p] <= j (count > 0)
+      int p = 0;
+      for (int st = top; st >= 1; st >>= 1)
+        if (w_off[p + st] <= j) p += st;
+      return p;
+    };
+    const uint32_t per_w = (total + CP_WAVES * 64 - 1) / (CP_WAVES * 64) * 64;
+    const uint32_t J0 = (uint32_t)wv * per_w;
+    const uint32_t J1 = J0 + per_w < total ? J0 + per_w : total;
+    // a lane's pass p, where its records leave it (nxt = w_off[p + 1]) and its start in
+    // the pass's slots minus its first flat index (gb), in registers
+    int p = J0 + lane < J1 ? search(J0 + lane) : 0;
+    uint32_t nxt = w_off[p + 1], gb = w_lo[p] - w_off[p];
+    const uint64_t* rec0 = cw.rec + p0 * CLAMP_PASS_RECS;
     auto load_batch = [&](uint64_t (&rv)[CP_RB], uint32_t jb) {
 #pragma unroll
       for (int u = 0; u < CP_RB; ++u) {
-        const uint32_t j = jb + (uint32_t)(u * CP_THREADS + tid);
+        const uint32_t j = jb + (uint32_t)(64 * u + lane);
         rv[u] = 0;
-        if (j < total) {
-          int p = 0;  // the last pass with w_off[p] <= j (its count is > 0)
-#pragma unroll
-          for (int st = CP_PW / 2; st >= 1; st >>= 1)
-            if (w_off[p + st] <= j) p += st;
-          rv[u] = cw.rec[(p0 + p) * CLAMP_PASS_RECS + w_lo[p] + (j - w_off[p])];
+        if (j < J1) {
+          if (j >= nxt) {  // the next pass of the bin (or a search when it is further)
+            p = w_off[p + 2] <= j ? search(j) : p + 1;
+            nxt = w_off[p + 1];
+            gb = w_lo[p] - w_off[p];
+          }
+          rv[u] = rec0[(int64_t)p * CLAMP_PASS_RECS + (uint32_t)(j + gb)];
         }
       }
     };
@@ -1147,13 +1207,14 @@ __device__ __forceinline__ void clamp_consume_bin(const ClampWork& cw, int64_t b
       for (int u = 0; u < CP_RB; ++u)
         if (KCC_DIAG_CP & 1) {  // diagnostic timing builds: no LDS atomics
           if (rv[u] == 0x5a5a5a5a5a5a5a5aull) tab[0] = rv[u];
-        } else if (jb + (uint32_t)(u * CP_THREADS + tid) < total)
+        } else if (jb + (uint32_t)(64 * u + lane) < J1)
           atomicAdd(reinterpret_cast<unsigned long long*>(&tab[(uint32_t)rv[u]]),
                     (unsigned long long)(int64_t)(int32_t)(rv[u] >> 32));
     };
+    const uint32_t step = 64u * CP_RB;
     uint64_t ra[CP_RB], rb[CP_RB];
-    load_batch(ra, 0);
-    for (uint32_t jb = 0; jb < ((KCC_DIAG_CP & 2) ? 0u : total); jb += 2 * step) {
+    load_batch(ra, J0);
+    for (uint32_t jb = J0; jb < ((KCC_DIAG_CP & 2) ? 0u : J1); jb += 2 * step) {
       load_batch(rb, jb + step);
       add_batch(ra, jb);
       load_batch(ra, jb + 2 * step);
