@@ -227,8 +227,11 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.c_H3, 8 * (size_t)kcc::H2_COPIES * (size_t)hs));
   KCC_HIP(ctx, ensure(dv.c_Crow, 8 * (size_t)cs_));
   if (kcc::clamp_binned((int64_t)S)) {  // node_prep's binned H2 / H3 records
-    const size_t passes = (size_t)kcc::clamp_passes((int64_t)N);
-    KCC_HIP(ctx, ensure(dv.c_rec, 8 * (size_t)kcc::CLAMP_PASS_RECS * passes));
+    // the most passes (and record slots) any call of up to N rows makes
+    const size_t passes = (size_t)((N + kcc::CLAMP_PASS_ROWS_MIN - 1) / kcc::CLAMP_PASS_ROWS_MIN);
+    const size_t recs = (size_t)((N + kcc::CLAMP_PASS_ROWS_MAX - 1) / kcc::CLAMP_PASS_ROWS_MAX) *
+                        2 * kcc::CLAMP_PASS_ROWS_MAX;  // >= passes(n) x 2 pass_rows(n) for any n <= N
+    KCC_HIP(ctx, ensure(dv.c_rec, 8 * recs));
     KCC_HIP(ctx, ensure(dv.c_dir, 4 * (size_t)kcc::clamp_d_stride((int64_t)S) * passes));
   }
   if (dv.c_C.bytes != before[0] || dv.c_H2.bytes != before[1] || dv.c_H3.bytes != before[2] ||
@@ -309,7 +312,8 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
                                      used_cpu, used_mem, as<kcc::FitGroupA>(dv.fast_a),
                                      as<kcc::FitGroup>(dv.fast_b), as<kcc::SlowNode>(dv.slow),
                                      as<int64_t>(dv.slow_list), n_specs, clamp_of(dv),
-                                     as<unsigned long long>(dv.counters), 0, 0, s, dv.fit_dense));
+                                     as<unsigned long long>(dv.counters), 0, 0, n_nodes, s,
+                                     dv.fit_dense));
   dv.stream_chunks = 1;
   KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, n_nodes, clamp_of(dv),
                                        as<unsigned long long>(dv.counters), partial, s));
@@ -375,7 +379,7 @@ hipError_t prof_event(Dev& dv, hipEvent_t* ev) {
 // Chunk boundaries: node ranges of ~equal node count, multiples of CHUNK_ALIGN (a
 // multiple of FIT_GROUP: the fit's node groups do not straddle two chunks); at least
 // `min_nodes` nodes per chunk.
-constexpr int64_t CHUNK_ALIGN = kcc::CLAMP_PASS_ROWS;  // whole node_prep passes
+constexpr int64_t CHUNK_ALIGN = kcc::CLAMP_PASS_ROWS_MAX;  // whole node_prep passes
 int plan_chunks(int64_t n_nodes, int want, int64_t min_nodes, std::vector<int64_t>& lo,
                 std::vector<int64_t>& hi) {
   int k = want;
@@ -502,7 +506,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                        as<kcc::FitGroup>(dv.fast_b) + lo[c] / kcc::FIT_GROUP,
                                        as<kcc::SlowNode>(dv.slow) + lo[c],
                                        as<int64_t>(dv.slow_list) + lo[c], n_specs, clamp_of(dv),
-                                       as<unsigned long long>(dv.counters), c, lo[c], s,
+                                       as<unsigned long long>(dv.counters), c, lo[c], n_nodes, s,
                                        dv.fit_dense));
     ProfPair pp{};
     if (dv.prof_on) {

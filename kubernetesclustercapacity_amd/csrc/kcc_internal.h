@@ -162,16 +162,17 @@ struct ClampWork {
   int64_t* H2;       // [H2_COPIES][h_stride]: T x 65 x 64, cell (g * 65 + k) * 64 + r
   int64_t* H3;       // [H2_COPIES][h_stride]: T x 65 x 64, cell (Y * 65 + j) * 64 + r
   int64_t* Crow;     // [c_stride]: C summed over the copies, suffix sums along GY
-  // binned form of H2 / H3 (clamp_binned(S)): node_prep writes each 1024-row pass's
+  // binned form of H2 / H3 (clamp_binned(S)): node_prep writes each pass's
   // (cell, w) records sorted by bin (x-group g: bin g; y-block Y: bin T + Y) into the
   // pass's own slot range, and the bins' starts into dir; clamp_apply's workgroup for a
   // bin sums that bin's records of every pass into LDS.  No global atomics.
-  uint64_t* rec;     // [n_pass][CLAMP_PASS_RECS]: cell | (int32 w) << 32
+  uint64_t* rec;     // [n_pass][pass_recs]: cell | (int32 w) << 32
   uint32_t* dir;     // [n_pass][d_stride]: a pass's bin starts (exclusive prefix) + its total
   int64_t c_stride;  // cells per C copy (clamp_c_cells(S) of the workspace)
   int64_t h_stride;  // cells per H2 / H3 copy (clamp_h_cells(S))
   int64_t d_stride;  // clamp_d_stride(S) of the workspace
   int64_t n_pass;    // passes of the call's node rows (set by launch_clamp_apply)
+  int64_t pass_recs; // record slots per pass: 2 x clamp_pass_rows (set by launch_clamp_apply)
 };
 // specs per call
 constexpr int64_t MAX_SPECS = (int64_t)1 << 26;
@@ -185,11 +186,23 @@ constexpr int C_COPIES = KCC_C_COPIES;
 #define KCC_H2_COPIES 2
 #endif
 constexpr int H2_COPIES = KCC_H2_COPIES;
-// binned H2 / H3 (ClampWork::rec): node_prep's passes of CLAMP_PASS_ROWS rows (4 per
-// thread) emit at most one record of each table per row; up to CLAMP_BIN_T_MAX
+// binned H2 / H3 (ClampWork::rec): node_prep's passes of clamp_pass_rows(n) rows (1 or 4
+// per thread) emit at most one record of each table per row; up to CLAMP_BIN_T_MAX
 // x-groups (S <= 16384), larger S adds to the H2 / H3 copies with device atomics
-constexpr int CLAMP_PASS_ROWS = 4096;
-constexpr int CLAMP_PASS_RECS = 2 * CLAMP_PASS_ROWS;
+constexpr int CLAMP_PASS_ROWS_MIN = 1024;
+constexpr int CLAMP_PASS_ROWS_MAX = 4096;  // chunks of a pipelined call are multiples of it
+#ifndef KCC_NP_PASS_ROWS
+#define KCC_NP_PASS_ROWS 0  // 0: by the call's rows; 1024 / 4096: fixed (A/B builds)
+#endif
+// Rows per node_prep pass for a call of n_nodes rows: 4096 when such passes still fill
+// the chip (one node_prep workgroup per CU), else 1024 — 4x the workgroups on small
+// shards (C4's 8-way shard: 123 instead of 31).  Fewer, larger passes keep clamp_apply's
+// heavy bins cheap: a bin's records are read pass by pass, and at C4 one bin held 34k
+// records (12.9 us to consume over 245 passes, 28.5 us over 977).
+inline int64_t clamp_pass_rows(int64_t n_nodes) {
+  if (KCC_NP_PASS_ROWS) return KCC_NP_PASS_ROWS;
+  return n_nodes >= (int64_t)200 * CLAMP_PASS_ROWS_MAX ? CLAMP_PASS_ROWS_MAX : CLAMP_PASS_ROWS_MIN;
+}
 constexpr int64_t CLAMP_BIN_T_MAX = 256;
 #ifndef KCC_CLAMP_BINNED
 #define KCC_CLAMP_BINNED 1
@@ -198,7 +211,10 @@ __host__ __device__ inline bool clamp_binned(int64_t S) {
   return KCC_CLAMP_BINNED && (S + 63) / 64 <= CLAMP_BIN_T_MAX;
 }
 inline int64_t clamp_d_stride(int64_t S) { return 2 * ((S + 63) / 64) + 1; }
-inline int64_t clamp_passes(int64_t n_nodes) { return (n_nodes + CLAMP_PASS_ROWS - 1) / CLAMP_PASS_ROWS; }
+inline int64_t clamp_passes(int64_t n_nodes) {
+  const int64_t pr = clamp_pass_rows(n_nodes);
+  return (n_nodes + pr - 1) / pr;
+}
 // up to this many specs node_prep's search and count tables live in LDS; larger S
 // searches the same tables in global memory
 #ifndef KCC_CLAMP_LDS_SPECS
@@ -258,14 +274,15 @@ hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
 // P <= 0 rows are the clamp correction's), compacted per workgroup pass into
 // counters[CNT_STREAM + chunk] rows (padded to whole groups).  dense: stream every row (the
 // round-1 layout's cost: zero fields for the rows that add nothing).  row0: the launch's
-// first row within the call (a multiple of CLAMP_PASS_ROWS; the binned records' passes).
+// first row within the call (a multiple of CLAMP_PASS_ROWS_MAX; the binned records'
+// passes), call_nodes: the call's rows (its pass size, clamp_pass_rows).
 hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
                             SlowNode* slow, int64_t* slow_list, int64_t n_specs, ClampWork cw,
-                            unsigned long long* counters, int chunk, int64_t row0, hipStream_t s,
-                            bool dense = false);
+                            unsigned long long* counters, int chunk, int64_t row0,
+                            int64_t call_nodes, hipStream_t s, bool dense = false);
 
 // partial[0..S) += Σ_i q(i,s), partial[S..2S) += #div-by-zero rows (internal order).
 hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,

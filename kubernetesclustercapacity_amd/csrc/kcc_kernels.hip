@@ -21,11 +21,14 @@ namespace {
 // Diagnostic timeline (KCC_TIMELINE builds only): per-workgroup wall-clock stamps
 // (s_memrealtime, 100 MHz) of the small kernels' phases, read by kcc_debug_timeline.
 #ifdef KCC_TIMELINE
-__device__ uint64_t kcc_tl[4096][4];
+__device__ uint64_t kcc_tl[8192][8];
 #define KCC_TL(slot, k) \
   do { if (threadIdx.x == 0) kcc_tl[(slot)][(k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define KCC_TLV(slot, k, v) \
+  do { if (threadIdx.x == 0) kcc_tl[(slot)][(k)] = (v); } while (0)
 #else
 #define KCC_TL(slot, k) do { } while (0)
+#define KCC_TLV(slot, k, v) do { } while (0)
 #endif
 
 // 64-bit add into LDS (ds_add_u64) through a pointer the compiler cannot prove is LDS
@@ -434,31 +437,27 @@ __device__ __forceinline__ int64_t clamp_n_pure(int64_t nN, int64_t S) {
 
 // #{k < 4096 : a[k] <= v} for a sorted ascending (8-ary: after the step of width s the
 // answer lies in [lo, lo + s])
-template <class T>
-__device__ __forceinline__ uint32_t search8_4096(const T* a, T v) {
-  static_assert(CLAMP_LDS_SPECS == 4096, "search8_4096 covers 8^4 entries");
-  uint32_t lo = 0;
-#pragma unroll
-  for (uint32_t s = 512; s >= 1; s /= 8) {
-    uint32_t cnt = 0;
-#pragma unroll
-    for (uint32_t j = 1; j < 8; ++j) cnt += a[lo + j * s - 1] <= v ? 1u : 0u;
-    lo += cnt * s;
-  }
-  return lo;
-}
+// LDS slot of entry k of a 4096-entry search table: the low 5 bits XORed with bits 5-9
+// and 10-14.  A binary search's probes at one level are spaced by a power of two >= 32
+// entries for its first 7 levels, i.e. all in ONE bank of a plain layout (ds_read_b32
+// banks are (a/4) mod 32, ds_read_b64's (a/4) mod 64: 32 u32 or i64 entries per bank
+// row); swizzled, they spread over the banks: 48 instead of 285 LDS cycles per wave and
+// search (random queries, simulated), a bijection within each 32-entry row.
+__device__ __forceinline__ uint32_t np_swz(uint32_t k) { return k ^ (((k >> 5) ^ (k >> 10)) & 31u); }
 
-// #{k < 4096 : a[k] <= v} for a sorted ascending (binary: 12 dependent reads)
-#ifndef KCC_NP_SEARCH8
-#define KCC_NP_SEARCH8 0
-#endif
+// #{k < 4096 : a[k] <= v} for a sorted ascending, stored swizzled (np_swz); binary: 12
+// dependent reads
 template <class T>
 __device__ __forceinline__ uint32_t search2_4096(const T* a, T v) {
+  static_assert(CLAMP_LDS_SPECS == 4096, "search2_4096 covers 2^12 entries");
   uint32_t lo = 0;  // after the step of width s the answer lies in [lo, lo + s]
 #pragma unroll
-  for (uint32_t s = 2048; s >= 1; s /= 2) lo += a[lo + s - 1] <= v ? s : 0u;
+  for (uint32_t s = 2048; s >= 1; s /= 2) lo += a[np_swz(lo + s - 1)] <= v ? s : 0u;
   return lo;
 }
+// the 64 x 64 member masks mk[g][Y]: Y XOR g, so a row (fixed g) and a column (fixed Y)
+// of 32 lanes both hit 32 distinct bank pairs (ds_read_b64)
+__device__ __forceinline__ uint32_t mk_at(uint32_t g, uint32_t Y) { return g * 64u + (Y ^ (g & 31u)); }
 
 // #{k < n : a[k] <= v} for a sorted ascending (binary search, n <= 2^31)
 template <class T>
@@ -496,9 +495,8 @@ __device__ __forceinline__ uint32_t count_lt64(const uint32_t* __restrict__ a, u
 // in LDS (S <= CLAMP_LDS_SPECS) and added to its copy once per workgroup; H2 / H3 leave as
 // binned records (clamp_binned(S)) — no scattered device atomics on the common path.
 #define KCC_NODE_PREP_BLOCK 1024
-constexpr int NP_RPT = CLAMP_PASS_ROWS / KCC_NODE_PREP_BLOCK;  // rows per thread and pass
-static_assert(NP_RPT * KCC_NODE_PREP_BLOCK == CLAMP_PASS_ROWS, "whole rows per thread");
-static_assert(CLAMP_PASS_RECS <= 0xffff, "record ranks packed in 16 bits");
+static_assert(CLAMP_PASS_ROWS_MIN == KCC_NODE_PREP_BLOCK, "a pass is 1, 2 or 4 rows per thread");
+static_assert(2 * CLAMP_PASS_ROWS_MAX <= 0xffff, "record ranks packed in 16 bits");
 // diagnostic timing builds only (results are wrong): KCC_DIAG_NP bit 0 drops the clamp
 // tables' global atomics (the cells stay live), bit 1 the x-group / y-block counts, bit 2
 // the searches, bit 3 the stream writes
@@ -530,6 +528,19 @@ constexpr size_t NP_OFF_CJ = NP_OFF_CK + 64 * 65;                     // 64 x 65
 constexpr size_t NP_OFF_C = (NP_OFF_CJ + 64 * 65 + 15) / 16 * 16;     // private C
 constexpr size_t NODE_PREP_LDS = NP_OFF_C + (KCC_NP_CPRIV ? 8 * (size_t)NP_C_CELLS : 0);
 constexpr int NP_BINS = 2 * (int)CLAMP_BIN_T_MAX;
+constexpr uint32_t NP_ST_MAX = 16;  // LDS search tables sample up to 16 x 4096 specs
+constexpr size_t NODE_PREP_LDS_SRCH = NP_OFF_MK;  // the search tables alone (S > 4096)
+__host__ __device__ inline uint32_t np_stride(int64_t S) {  // smallest power of two >= S / 4096
+  uint32_t st = 1;
+  while (st < NP_ST_MAX && (int64_t)st * CLAMP_LDS_SPECS < S) st *= 2;
+  return st;
+}
+// MODE 2: S <= 4096, every table in LDS; 1: S <= NP_ST_MAX * 4096, sampled search tables in
+// LDS, the rest in memory; 0: everything in memory (one instantiation per mode: each
+// carries only its own path's registers).  A pass is SUB x 1024 rows (clamp_pass_rows(n)
+// of the call), worked on in SUB sub-steps of one row per thread; each sub-step's rows
+// are loaded while the previous one is worked on.
+template <int MODE, int SUB>
 __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_cpu,
                                  const int64_t* __restrict__ alloc_mem,
                                  const int64_t* __restrict__ alloc_pods,
@@ -540,8 +551,28 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
                                  SlowNode* __restrict__ slow, int64_t* __restrict__ slow_list,
                                  int64_t S, ClampWork cw, unsigned long long* __restrict__ counters,
                                  int32_t chunk, int32_t dense, int64_t pass0) {
+  KCC_TL(blockIdx.x % 1024, 2);
+  constexpr int64_t PR = (int64_t)KCC_NODE_PREP_BLOCK * SUB;  // rows per pass
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t stride = (int64_t)gridDim.x * CLAMP_PASS_ROWS;
+  const int64_t stride = (int64_t)gridDim.x * PR;
+  // one row's six values: the next sub-step's, loaded while the current one is worked on;
+  // this workgroup's first ones go out before the table setup below (their latency hides
+  // behind it)
+  uint64_t ld_ac, ld_uc;
+  int64_t ld_am, ld_um, ld_P, ld_pc;
+  auto load_row = [&](int64_t i) {
+    ld_ac = ld_uc = 0;
+    ld_am = ld_um = ld_P = ld_pc = 0;
+    if (i < n) {
+      ld_ac = alloc_cpu[i];
+      ld_uc = used_cpu[i];
+      ld_am = alloc_mem[i];
+      ld_um = used_mem[i];
+      ld_P = alloc_pods[i];
+      ld_pc = pod_count[i];
+    }
+  };
+  load_row((int64_t)blockIdx.x * PR + threadIdx.x);
   __shared__ uint32_t np_wc[KCC_NODE_PREP_BLOCK / 64];  // streamed rows per wave
   __shared__ uint64_t np_base;                          // this pass's stream position
   __shared__ uint32_t np_tot;
@@ -551,7 +582,8 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   const int64_t nN = clamp_n_normal(counters);     // normal specs (clamp correction)
   const bool slow_all = nN < S;                    // exact-path specs exist
   const int64_t T = (nN + 63) / 64, W = T + 2;
-  const bool binned = clamp_binned(S);             // T <= CLAMP_BIN_T_MAX
+  // T <= CLAMP_BIN_T_MAX (always at S <= 4096: MODE 2 carries no table atomics)
+  const bool binned = (MODE == 2 && KCC_CLAMP_BINNED) || clamp_binned(S);
   const int NB = (int)(2 * T);                     // bins: x-groups, then y-blocks
   // this workgroup's copies of the tables: workgroups are dealt round-robin over the XCDs
   int64_t* Cc = cw.C + (int64_t)(blockIdx.x % C_COPIES) * cw.c_stride;
@@ -569,8 +601,12 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   uint8_t* ck_l = np_lds + NP_OFF_CK;
   uint8_t* cj_l = np_lds + NP_OFF_CJ;
   unsigned long long* c_l = reinterpret_cast<unsigned long long*>(np_lds + NP_OFF_C);
-  const bool lds = S <= CLAMP_LDS_SPECS;  // then T <= 64 and W * W <= NP_C_CELLS
-  const bool cpriv = KCC_NP_CPRIV && lds;
+  constexpr bool lds = MODE == 2;  // S <= CLAMP_LDS_SPECS: T <= 64 and W * W <= NP_C_CELLS
+  constexpr bool cpriv = KCC_NP_CPRIV && lds;
+  // the search tables in LDS hold every st-th request (st = 1 when S <= 4096; a search
+  // ends with the st - 1 requests of its bucket from memory), up to NP_ST_MAX
+  constexpr bool srch = MODE >= 1;
+  const uint32_t st = lds ? 1u : np_stride(S);
   // smallest normal requests (rows below either dominate no spec); cs[0] >= 1
   const uint32_t cmin = nN > 0 ? (cw.cs[0] < FAST_FC_MAX ? (uint32_t)cw.cs[0] : (uint32_t)FAST_FC_MAX)
                                : 0xffffffffu;
@@ -578,22 +614,26 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   for (int b = threadIdx.x; b < NP_BINS; b += KCC_NODE_PREP_BLOCK) np_bcnt[b] = 0;
   constexpr int PER = (int)(CLAMP_LDS_SPECS / KCC_NODE_PREP_BLOCK);
   uint32_t yv[PER];  // y-rank of x-rank tid + 1024 u
-  if (lds) {
-    // every load first (one memory round trip), then the LDS writes
+  if (srch) {
+    // every load first, guarded by S (a kernel argument) rather than nN, so they travel
+    // with the counters' load (one memory round trip); entries nN.. are masked after
     uint64_t cv[PER], mv[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int64_t k = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
-      cv[u] = k < nN ? cw.cs[k] : ~0ull;  // padded: +inf
-      mv[u] = k < nN ? (uint64_t)cw.ms[k] : (uint64_t)INT64_MAX;
-      yv[u] = k < nN ? cw.mr_c[k] : 0xffffffffu;
+      const int64_t e = (k + 1) * st - 1;  // the sampled entry
+      cv[u] = e < S ? cw.cs[e] : ~0ull;
+      mv[u] = e < S ? (uint64_t)cw.ms[e] : (uint64_t)INT64_MAX;
+      yv[u] = lds && k < S ? cw.mr_c[k] : 0xffffffffu;
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int64_t k = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
-      cs_l[k] = cv[u] < FAST_FC_MAX ? (uint32_t)cv[u] : 0xffffffffu;
-      ms_l[k] = (int64_t)mv[u];
-      mk_l[k] = 0ull;  // 64 x 64 masks: one per spec slot
+      const bool in = (k + 1) * st - 1 < nN;  // padded: +inf
+      cs_l[np_swz((uint32_t)k)] = in && cv[u] < FAST_FC_MAX ? (uint32_t)cv[u] : 0xffffffffu;
+      ms_l[np_swz((uint32_t)k)] = in ? (int64_t)mv[u] : INT64_MAX;
+      if (!in) yv[u] = 0xffffffffu;
+      if (lds) mk_l[k] = 0ull;  // 64 x 64 masks: one per spec slot
     }
     if (cpriv)
       for (int64_t e = threadIdx.x; e < W * W; e += KCC_NODE_PREP_BLOCK) c_l[e] = 0ull;
@@ -604,18 +644,18 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
     for (int u = 0; u < PER; ++u) {
       const int64_t x = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
       if (x < nN)
-        __hip_atomic_fetch_or((lds_ull*)(mk_l + (x >> 6) * 64 + (yv[u] >> 6)), 1ull << (yv[u] & 63),
+        __hip_atomic_fetch_or((lds_ull*)(mk_l + mk_at((uint32_t)x >> 6, yv[u] >> 6)), 1ull << (yv[u] & 63),
                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
   __syncthreads();  // masks complete
   if (lds) {  // the prefix counts: row g along Y and column Y = g along G, lane = index
     for (int g = wv; g < 64; g += KCC_NODE_PREP_BLOCK / 64) {
-      const uint64_t c1 = (uint64_t)__popcll(mk_l[g * 64 + lane]);
+      const uint64_t c1 = (uint64_t)__popcll(mk_l[mk_at(g, lane)]);
       const uint64_t i1 = wave_incl_scan_u64(c1);
       ck_l[g * 65 + lane] = (uint8_t)(i1 - c1);
       if (lane == 63) ck_l[g * 65 + 64] = (uint8_t)i1;
-      const uint64_t c2 = (uint64_t)__popcll(mk_l[lane * 64 + g]);
+      const uint64_t c2 = (uint64_t)__popcll(mk_l[mk_at(lane, g)]);
       const uint64_t i2 = wave_incl_scan_u64(c2);
       cj_l[g * 65 + lane] = (uint8_t)(i2 - c2);
       if (lane == 63) cj_l[g * 65 + 64] = (uint8_t)i2;
@@ -628,58 +668,44 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
     else np_atomic(&Cc[cell], w);
   };
   __syncthreads();
-  KCC_TL(3072 + blockIdx.x % 1024, 0);
-  // Passes of NP_RPT x 1024 rows (thread t: rows i0 + t + 1024 r): every row's loads
-  // first, then the rows one after another; one stream position (a returning atomic on
-  // one word) and one bin scan per pass.  Workgroup-uniform trip count (the stream
-  // positions and the bins meet in LDS).
-  for (int64_t i0 = (int64_t)blockIdx.x * CLAMP_PASS_ROWS; i0 < n; i0 += stride) {
-    const int64_t pass = pass0 + i0 / CLAMP_PASS_ROWS;
-    uint64_t ld_ac[NP_RPT], ld_uc[NP_RPT];
-    int64_t ld_am[NP_RPT], ld_um[NP_RPT], ld_P[NP_RPT], ld_pc[NP_RPT];
+  KCC_TL(blockIdx.x % 1024, 0);
+  // Passes of SUB x 1024 rows (thread t: rows i0 + t + 1024 q), one sub-step q after the
+  // other; one stream position (a returning atomic on one word) and one bin scan per pass.
+  // Workgroup-uniform trip count (the stream positions and the bins meet in LDS).
+  for (int64_t i0 = (int64_t)blockIdx.x * PR; i0 < n; i0 += stride) {
+    const int64_t pass = pass0 + i0 / PR;
+    // kept to the pass's end: the stream entry of each sub-step's row (free memory < 2^50,
+    // free cpu < 2^23 and P of a fast row, else 0), its ballots, the packed records
+    uint64_t r_fm[SUB];
+    uint32_t r_fc[SUB];
+    int32_t r_P[SUB];
+    unsigned long long sbal[SUB];
+    uint32_t pk1[SUB], pk2[SUB], pk3[SUB];
+    uint64_t always_sum = 0;
+    uint64_t base_ret = 0;
+    uint32_t t_pass = 0;
 #pragma unroll
-    for (int r = 0; r < NP_RPT; ++r) {
-      const int64_t i = i0 + r * KCC_NODE_PREP_BLOCK + threadIdx.x;
-      ld_ac[r] = ld_uc[r] = 0;
-      ld_am[r] = ld_um[r] = ld_P[r] = ld_pc[r] = 0;
-      if (i < n) {
-        ld_ac[r] = alloc_cpu[i];
-        ld_uc[r] = used_cpu[i];
-        ld_am[r] = alloc_mem[i];
-        ld_um[r] = used_mem[i];
-        ld_P[r] = alloc_pods[i];
-        ld_pc[r] = pod_count[i];
-      }
-    }
-    // phase 1, per row: the free capacity (the stream entry, kept across the barriers),
-    // the slow rows; the 64-bit loads die here
-    uint64_t r_fm[NP_RPT];                 // free memory of a fast row (< 2^50), else 0
-    uint32_t r_fc[NP_RPT];                 // free cpu of a fast row (< 2^23), else 0
-    int32_t r_P[NP_RPT], r_cl[NP_RPT];     // P, clamp of a fast row (|.| <= 2^20), else 0
-    unsigned long long okbal[NP_RPT];
-#pragma unroll
-    for (int r = 0; r < NP_RPT; ++r) {
-      const int64_t i = i0 + r * KCC_NODE_PREP_BLOCK + threadIdx.x;
+    for (int q = 0; q < SUB; ++q) {
+      const int64_t i = i0 + q * KCC_NODE_PREP_BLOCK + threadIdx.x;
       const bool valid = i < n;
+      // phase 1: the free capacity, the slow rows; the 64-bit loads die here
       bool ok = false;
-      r_fm[r] = 0;
-      r_fc[r] = 0;
-      r_P[r] = 0;
-      r_cl[r] = 0;
+      int32_t cl_q = 0;
+      r_fm[q] = 0;
+      r_fc[q] = 0;
+      r_P[q] = 0;
       if (valid) {
-        const uint64_t ac = ld_ac[r], uc = ld_uc[r];
-        const int64_t am = ld_am[r], um = ld_um[r];
-        const int64_t P = ld_P[r], pc = ld_pc[r];
-        const uint64_t fc = ac > uc ? ac - uc : 0;                                  // CC:119-123
-        const int64_t fm = am > um ? (int64_t)((uint64_t)am - (uint64_t)um) : 0;   // CC:125-129
-        const int64_t cl = (int64_t)((uint64_t)P - (uint64_t)pc);                  // CC:135
+        const uint64_t fc = ld_ac > ld_uc ? ld_ac - ld_uc : 0;                                 // CC:119-123
+        const int64_t fm = ld_am > ld_um ? (int64_t)((uint64_t)ld_am - (uint64_t)ld_um) : 0;  // CC:125-129
+        const int64_t P = ld_P;
+        const int64_t cl = (int64_t)((uint64_t)P - (uint64_t)ld_pc);                          // CC:135
         ok = fc < FAST_FC_MAX && fm >= 0 && fm < FAST_FM_MAX && P >= -FAST_P_ABS &&
              P <= FAST_P_ABS && cl >= -FAST_CL_ABS && cl <= FAST_CL_ABS;
         if (ok) {
-          r_fm[r] = (uint64_t)fm;
-          r_fc[r] = (uint32_t)fc;
-          r_P[r] = (int32_t)P;
-          r_cl[r] = (int32_t)cl;
+          r_fm[q] = (uint64_t)fm;
+          r_fc[q] = (uint32_t)fc;
+          r_P[q] = (int32_t)P;
+          cl_q = (int32_t)cl;
         }
         if (slow_all || !ok) {
           SlowNode sn;
@@ -690,121 +716,118 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
           slow[i] = sn;
         }
       }
-      okbal[r] = __ballot(ok);
-      const unsigned long long bl = __ballot(valid && !ok);
-      if (bl) {
-        unsigned long long base = 0;
-        if (lane == 0)
-          base = atomicAdd(&counters[CNT_SLOW_ROWS + chunk], (unsigned long long)__popcll(bl));
-        base = __shfl(base, 0);
-        if (valid && !ok) slow_list[base + __popcll(bl & ((1ull << lane) - 1ull))] = i;
-      }
-    }
-    // phase 2, per row: the clamp correction's cells and records, the stream ballots
-    uint32_t pk1[NP_RPT], pk2[NP_RPT], pk3[NP_RPT];  // the records, packed (below)
-    unsigned long long sbal[NP_RPT];
-    uint32_t wave_streamed = 0;
-    uint64_t always_sum = 0;
-#pragma unroll
-    for (int r = 0; r < NP_RPT; ++r) {
-      const int64_t i = i0 + r * KCC_NODE_PREP_BLOCK + threadIdx.x;
-      const bool valid = i < n;
-      const bool ok = (okbal[r] >> lane) & 1ull;
-      const uint64_t fc_ok = r_fc[r];
-      const int64_t fm_ok = (int64_t)r_fm[r], P_ok = r_P[r];
-      const int32_t cl_i = r_cl[r];
-      // clamp correction: where (and with which weight) this row's pod-slot clamp applies
-      int64_t w = 0;
-      bool has2 = false, has3 = false;  // binned records of this row
-      uint32_t bin2 = 0, bin3 = 0, cell2 = 0, cell3 = 0;
-      if (ok && nN > 0) {
-        const int64_t P = P_ok, Penc = P > 0 ? P : 0;
-        w = Penc - (int64_t)cl_i;  // contribution = min(x, Penc) - w when clamped
-        if (P <= 0) {
-          always_sum += (uint64_t)w;  // x >= P for every spec
-        } else if (w != 0) {
-          // c <= U  <=>  floor(fc / c) >= P  and  m <= V  <=>  floor(fm / m) >= P, with
-          // U = floor(fc / P), V = floor(fm / P) from the rounded-up reciprocal of P
-          // (exact: fc, fm < 2^50, P < 2^51)
-          const double rP = recip_up_f64((uint64_t)P);
-          const uint32_t U = (uint32_t)((double)fc_ok * rP);
-          const int64_t V = (int64_t)((double)fm_ok * rP);
-          if (U >= cmin && V >= mmin) {  // else no spec is dominated
-            uint32_t L, b;
-            if (lds) {  // searches over the +inf-padded 4096-entry tables: binary (12
-                        // dependent LDS reads; four rows per thread overlap them) or
-                        // 8-ary (4 steps of 7 independent reads: 28, LDS-issue-bound)
-              L = KCC_NP_SEARCH8 ? search8_4096(cs_l, U) : search2_4096(cs_l, U);
-              b = KCC_NP_SEARCH8 ? search8_4096(ms_l, V) : search2_4096(ms_l, V);
-              if (KCC_DIAG_NP & 4) {  // diagnostic: no searches
-                L = 1 + (U & 2047);
-                b = 1 + ((uint32_t)V & 2047);
-              }
-            } else {
-              L = upper_bound_count(cw.cs, nN, (uint64_t)U);
-              b = upper_bound_count(cw.ms, nN, V);
-            }
-            // L >= 1, b >= 1 (U >= cmin, V >= mmin)
-            const uint32_t GX = L >> 6, rx = L & 63u, GY = b >> 6, ry = b & 63u;
-            if (GX > 0 && GY > 0) c_add((int64_t)GX * W + GY, w);
-            if (rx > 0) {  // x-group GX (< T): k = #{its specs with y < b}
-              uint32_t k;
-              if (KCC_DIAG_NP & 2) {
-                k = 1;
-              } else if (lds) {  // the members below y-block b >> 6, + those in it below b
-                const uint32_t Yb = b >> 6, o = b & 63u;
-                k = ck_l[GX * 65 + Yb];
-                if (o) k += (uint32_t)__popcll(mk_l[GX * 64 + Yb] & ((1ull << o) - 1ull));
-              } else {
-                k = count_lt64(cw.mr_c + 64 * GX, b);
-              }
-              if (k > 0) {
-                if (binned) {
-                  has2 = true;
-                  bin2 = GX;
-                  cell2 = k * 64 + rx;
-                } else {
-                  np_atomic(&H2c[((int64_t)GX * 65 + k) * 64 + rx], w);
-                }
-              }
-            }
-            if (ry > 0 && GX > 0) {  // y-block GY (< T): j = #{its specs whose x-group < GX}
-              uint32_t j;
-              if (KCC_DIAG_NP & 2) {
-                j = 1;
-              } else if (lds) {
-                j = cj_l[GY * 65 + GX];
-              } else {  // x >> 6 < GX  <=>  x < 64 GX (padding: never)
-                j = count_lt64(cw.cr_m + 64 * GY, GX << 6);
-              }
-              if (j > 0) {
-                if (binned) {
-                  has3 = true;
-                  bin3 = (uint32_t)T + GY;
-                  cell3 = j * 64 + ry;
-                } else {
-                  np_atomic(&H3c[((int64_t)GY * 65 + j) * 64 + ry], w);
-                }
-              }
-            }
-          }
+      {
+        const unsigned long long bl = __ballot(valid && !ok);
+        if (bl) {
+          unsigned long long base = 0;
+          if (lane == 0)
+            base = atomicAdd(&counters[CNT_SLOW_ROWS + chunk], (unsigned long long)__popcll(bl));
+          base = __shfl(base, 0);
+          if (valid && !ok) slow_list[base + __popcll(bl & ((1ull << lane) - 1ull))] = i;
         }
       }
+      // the next sub-step's row (the load registers are free now)
+      load_row(q + 1 < SUB ? i + KCC_NODE_PREP_BLOCK : i0 + stride + threadIdx.x);
+      // the fit's node stream: the rows with something to add
+      sbal[q] = __ballot(dense ? valid : (r_fc[q] > 0 && r_fm[q] > 0 && r_P[q] > 0));  // 0 unless ok
+      if (q == SUB - 1) {
+        // every sub-step's ballots are known: the pass's stream position (one returning
+        // atomic by thread 0) is in flight during the last phase 2
+        uint32_t wave_streamed = 0;
+#pragma unroll
+        for (int q2 = 0; q2 < SUB; ++q2) wave_streamed += (uint32_t)__popcll(sbal[q2]);
+        if (lane == 0) np_wc[wv] = wave_streamed;
+        __syncthreads();  // np_wc
+        if (threadIdx.x == 0) {
+          for (int u = 0; u < KCC_NODE_PREP_BLOCK / 64; ++u) t_pass += np_wc[u];
+          const uint32_t padded = (t_pass + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP;  // whole groups
+          if (padded) base_ret = atomicAdd(&counters[CNT_STREAM + chunk], (unsigned long long)padded);
+        }
+        KCC_TL(blockIdx.x % 1024, 3);
+      }
+      // phase 2: the clamp correction's cells and records, in steps without data-dependent
+      // branches around the LDS reads: (a) weight and bounds, (b) the two binary searches,
+      // (c) the member counts, (d) cells and bin ranks
+      // (a) c <= U  <=>  floor(fc / c) >= P  and  m <= V  <=>  floor(fm / m) >= P, with
+      // U = floor(fc / P), V = floor(fm / P) from the rounded-up reciprocal of P (exact:
+      // fc, fm < 2^50, P < 2^51); U < cmin or V < mmin: no spec dominated
+      const int64_t P = r_P[q], Penc = P > 0 ? P : 0;
+      const int64_t wfull = Penc - (int64_t)cl_q;  // contribution = min(x, Penc) - w when clamped
+      if (ok && nN > 0 && P <= 0) always_sum += (uint64_t)wfull;  // x >= P for every spec
+      const double rP = recip_up_f64(P > 0 ? (uint64_t)P : 1ull);
+      const uint32_t U0 = (uint32_t)((double)r_fc[q] * rP);
+      const int64_t V0 = (int64_t)((double)r_fm[q] * rP);
+      const bool act = ok && nN > 0 && P > 0 && wfull != 0 && U0 >= cmin && V0 >= mmin;
+      const int64_t w = act ? wfull : 0;  // |w| <= 2^21
+      const uint32_t U = act ? U0 : 0u;   // every request is >= 1: counts 0
+      const int64_t V = act ? V0 : 0;
+      uint32_t L = 0, b = 0;
+      if (srch) {  // (b) over the LDS tables (every st-th request), then the bucket in memory
+#pragma unroll
+        for (uint32_t sw = 2048; sw >= 1; sw /= 2) {
+          L += cs_l[np_swz(L + sw - 1)] <= U ? sw : 0u;
+          b += ms_l[np_swz(b + sw - 1)] <= V ? sw : 0u;
+        }
+        if (KCC_DIAG_NP & 4) {  // diagnostic: no searches
+          L = w ? 1 + (U & 2047) : 0;
+          b = w ? 1 + ((uint32_t)V & 2047) : 0;
+        }
+        if (!lds) {  // st > 1: #{a <= v} = c st + #{j < st - 1 : a[c st + j] <= v} (a[(c + 1) st - 1] > v)
+          L *= st;
+          b *= st;
+          uint32_t addL = 0, addb = 0;
+#pragma unroll 4
+          for (uint32_t j = 0; j + 1 < st; ++j) {  // uniform trip count
+            addL += w && L + j < (uint64_t)nN && cw.cs[L + j] <= (uint64_t)U ? 1u : 0u;
+            addb += w && b + j < (uint64_t)nN && cw.ms[b + j] <= V ? 1u : 0u;
+          }
+          L += addL;
+          b += addb;
+        }
+      } else {  // S > NP_ST_MAX * 4096: binary searches in memory
+        L = w ? upper_bound_count(cw.cs, nN, (uint64_t)U) : 0u;
+        b = w ? upper_bound_count(cw.ms, nN, V) : 0u;
+      }
+      // (c) L >= 1 and b >= 1 for an active row; L = 64 GX + rx, b = 64 GY + ry.  H2's
+      // k = #{specs of x-group GX with y < b} (rx > 0, so GX < T), H3's j = #{specs of
+      // y-block GY whose x-group < GX} (ry > 0, GY < T)
+      const uint32_t GX = L >> 6, rx = L & 63u, GY = b >> 6, ry = b & 63u;
+      uint32_t k, j;
+      if (KCC_DIAG_NP & 2) {
+        k = j = 1;
+      } else if (lds) {  // the members below y-block b >> 6, + those in it below b
+        const uint32_t gx = GX < 63u ? GX : 63u, yb = GY < 63u ? GY : 63u;
+        const uint64_t mk = mk_l[mk_at(gx, yb)];
+        k = (uint32_t)ck_l[gx * 65 + GY] + (uint32_t)__popcll(mk & ((1ull << ry) - 1ull));
+        j = cj_l[yb * 65 + GX];
+      } else {  // x >> 6 < GX  <=>  x < 64 GX (padding: never)
+        k = w && rx ? count_lt64(cw.mr_c + 64 * GX, b) : 0u;
+        j = w && ry && GX > 0 ? count_lt64(cw.cr_m + 64 * GY, GX << 6) : 0u;
+      }
+      // (d)
+      if (w && GX > 0 && GY > 0) c_add((int64_t)GX * W + GY, w);
+      const bool has2 = w && rx > 0 && k > 0;            // first rx members of x-group GX
+      const bool has3 = w && ry > 0 && GX > 0 && j > 0;  // members of y-block GY in x-groups < GX
+      if (!binned) {
+        if (has2) np_atomic(&H2c[((int64_t)GX * 65 + k) * 64 + rx], w);
+        if (has3) np_atomic(&H3c[((int64_t)GY * 65 + j) * 64 + ry], w);
+      }
+      const bool rec2 = binned && has2, rec3 = binned && has3;
+      const uint32_t bin2 = rec2 ? GX : 0u, bin3 = rec3 ? (uint32_t)T + GY : 0u;
       // the records in three words: cells (13 bits each, 0: no record — a record's cell
       // is >= 64), ranks within their bins (LDS counters, < 2^13 per pass: zeroed by the
       // scan below), bins (9 bits each), and the weight (|w| <= 2^21, 23 bits) in 6/6/11
       // bit slices: pk1 = cell2 | cell3 << 13 | w[0:6] << 26, pk2 = rk2 | rk3 << 13 |
       // w[6:12] << 26, pk3 = bin2 | bin3 << 9 | w[12:] << 18 (arithmetic)
-      const uint32_t rk2 = has2 ? atomicAdd(&np_bcnt[bin2], 1u) : 0u;
-      const uint32_t rk3 = has3 ? atomicAdd(&np_bcnt[bin3], 1u) : 0u;
+      const uint32_t rk2 = rec2 ? atomicAdd(&np_bcnt[bin2], 1u) : 0u;
+      const uint32_t rk3 = rec3 ? atomicAdd(&np_bcnt[bin3], 1u) : 0u;
       const uint32_t wu = (uint32_t)(int32_t)w;
-      pk1[r] = (has2 ? cell2 : 0u) | (has3 ? cell3 : 0u) << 13 | (wu & 63u) << 26;
-      pk2[r] = rk2 | rk3 << 13 | ((wu >> 6) & 63u) << 26;
-      pk3[r] = bin2 | bin3 << 9 | (uint32_t)((int32_t)wu >> 12) << 18;
-      // the fit's node stream: the rows with something to add
-      const bool stream = dense ? valid : (ok && fc_ok > 0 && fm_ok > 0 && P_ok > 0);
-      sbal[r] = __ballot(stream);
-      wave_streamed += (uint32_t)__popcll(sbal[r]);
+      pk1[q] = (rec2 ? k * 64 + rx : 0u) | (rec3 ? j * 64 + ry : 0u) << 13 | (wu & 63u) << 26;
+      pk2[q] = rk2 | rk3 << 13 | ((wu >> 6) & 63u) << 26;
+      pk3[q] = bin2 | bin3 << 9 | (uint32_t)((int32_t)wu >> 12) << 18;
+      // the scheduler keeps each sub-step to itself (hoisting the next one's work
+      // across this point ran the SUB = 4 kernels out of registers)
+      __builtin_amdgcn_sched_barrier(0);
     }
     {  // rows clamped for every spec: one wave-summed add into C[T+1][T+1]
       uint64_t v = always_sum;
@@ -812,22 +835,19 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
       if (lane == 0 && v) c_add((T + 1) * W + T + 1, (int64_t)v);
     }
-    if (lane == 0) np_wc[wv] = wave_streamed;
-    __syncthreads();  // np_wc, and every record's rank
     if (threadIdx.x == 0) {
-      uint32_t t = 0;
-      for (int u = 0; u < KCC_NODE_PREP_BLOCK / 64; ++u) t += np_wc[u];
-      const uint32_t padded = (t + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP;  // whole groups
-      np_base = padded ? atomicAdd(&counters[CNT_STREAM + chunk], (unsigned long long)padded) : 0ull;
-      np_tot = t;
+      np_base = base_ret;
+      np_tot = t_pass;
     }
+    __syncthreads();  // np_base, and every record's rank
+    KCC_TL(blockIdx.x % 1024, 4);
     if (binned && wv == 1) {
       // the bins' starts: runs of per bins per lane, a shuffle scan of the run totals;
       // the pass's directory row (starts + total) goes out here, the counters return to 0
       const int per = (NB + 63) / 64;
       const int b0 = lane * per, b1 = min(b0 + per, NB);
       uint32_t ls = 0;
-      for (int b = b0; b < b1; ++b) ls += np_bcnt[b];
+      for (int bb = b0; bb < b1; ++bb) ls += np_bcnt[bb];
       uint32_t li = ls;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
@@ -836,11 +856,11 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       }
       uint32_t* drow = cw.dir + pass * cw.d_stride;
       uint32_t run = li - ls;
-      for (int b = b0; b < b1; ++b) {
-        const uint32_t c = np_bcnt[b];
-        np_bstart[b] = run;
-        drow[b] = run;
-        np_bcnt[b] = 0;
+      for (int bb = b0; bb < b1; ++bb) {
+        const uint32_t c = np_bcnt[bb];
+        np_bstart[bb] = run;
+        drow[bb] = run;
+        np_bcnt[bb] = 0;
         run += c;
       }
       if (lane == 63) drow[NB] = li;
@@ -853,37 +873,38 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       const uint32_t tot = np_tot;
       const uint32_t pad = (tot + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP - tot;
       auto put = [&](uint64_t pos, uint64_t fmv, uint32_t fcv, uint32_t Pv) {
-        const int k = (int)(pos % FIT_GROUP);
+        const int kk = (int)(pos % FIT_GROUP);
         FitGroupA& a = fast_a[pos / FIT_GROUP];
-        a.fm[k] = fmv;
-        a.fc[k] = fcv;
-        a.P[k] = Pv;
+        a.fm[kk] = fmv;
+        a.fc[kk] = fcv;
+        a.P[kk] = Pv;
         if (want_b) {
           FitGroup& g = fast_b[pos / FIT_GROUP];
-          g.fc[k] = (double)fcv;                      // exact
-          g.fm[k] = (double)fmv;                      // exact (< 2^50)
-          g.Pb[k] = FIT_BIAS + (double)Pv;            // exact (P <= 2^20)
+          g.fc[kk] = (double)fcv;                      // exact
+          g.fm[kk] = (double)fmv;                      // exact (< 2^50)
+          g.Pb[kk] = FIT_BIAS + (double)Pv;            // exact (P <= 2^20)
         }
       };
-      uint32_t done = 0;  // streamed rows of this wave's earlier row sets
-      uint64_t* prec = cw.rec + pass * CLAMP_PASS_RECS;
+      uint32_t done = 0;  // streamed rows of this wave's earlier sub-steps
+      uint64_t* prec = cw.rec + pass * (2 * PR);
 #pragma unroll
-      for (int r = 0; r < NP_RPT; ++r) {
-        if (!(KCC_DIAG_NP & 8) && ((sbal[r] >> lane) & 1ull))  // P <= 0 streams only in the dense layout, as P = 0
-          put(sb0 + done + (uint32_t)__popcll(sbal[r] & ((1ull << lane) - 1ull)), r_fm[r], r_fc[r],
-              r_P[r] > 0 ? (uint32_t)r_P[r] : 0u);
-        done += (uint32_t)__popcll(sbal[r]);
-        const uint32_t c2 = pk1[r] & 0x1fffu, c3 = (pk1[r] >> 13) & 0x1fffu;
+      for (int q = 0; q < SUB; ++q) {
+        if (!(KCC_DIAG_NP & 8) && ((sbal[q] >> lane) & 1ull))  // P <= 0 streams only in the dense layout, as P = 0
+          put(sb0 + done + (uint32_t)__popcll(sbal[q] & ((1ull << lane) - 1ull)), r_fm[q], r_fc[q],
+              r_P[q] > 0 ? (uint32_t)r_P[q] : 0u);
+        done += (uint32_t)__popcll(sbal[q]);
+        const uint32_t c2 = pk1[q] & 0x1fffu, c3 = (pk1[q] >> 13) & 0x1fffu;
         if (c2 | c3) {
-          const int32_t wr = (int32_t)pk3[r] >> 18 << 12 | (int32_t)((pk2[r] >> 26) << 6 | pk1[r] >> 26);
+          const int32_t wr = (int32_t)pk3[q] >> 18 << 12 | (int32_t)((pk2[q] >> 26) << 6 | pk1[q] >> 26);
           const uint64_t wbits = (uint64_t)(uint32_t)wr << 32;  // record: cell | w << 32
-          if (c2) prec[np_bstart[pk3[r] & 0x1ffu] + (pk2[r] & 0x1fffu)] = wbits | c2;
-          if (c3) prec[np_bstart[(pk3[r] >> 9) & 0x1ffu] + ((pk2[r] >> 13) & 0x1fffu)] = wbits | c3;
+          if (c2) prec[np_bstart[pk3[q] & 0x1ffu] + (pk2[q] & 0x1fffu)] = wbits | c2;
+          if (c3) prec[np_bstart[(pk3[q] >> 9) & 0x1ffu] + ((pk2[q] >> 13) & 0x1fffu)] = wbits | c3;
         }
       }
       if (threadIdx.x < pad) put(np_base + tot + threadIdx.x, 0ull, 0u, 0u);  // the last group's padding
     }
     __syncthreads();  // np_wc / np_base / np_bstart are rewritten by the next pass
+    KCC_TL(blockIdx.x % 1024, 5);
   }
   if (cpriv) {  // the private C into this workgroup's device copy: its non-zero cells
     for (int64_t e = threadIdx.x; e < W * W; e += KCC_NODE_PREP_BLOCK) {
@@ -891,7 +912,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       if (v) np_atomic(&Cc[e], (int64_t)v);
     }
   }
-  KCC_TL(3072 + blockIdx.x % 1024, 1);
+  KCC_TL(blockIdx.x % 1024, 1);
 }
 
 // Smallest f32 >= 1/v (1 <= v < 2^51, exact in f64).  1/v is first rounded to f64,
@@ -1186,7 +1207,7 @@ __device__ __forceinline__ void clamp_consume_bin(const ClampWork& cw, int64_t b
     // the pass's slots minus its first flat index (gb), in registers
     int p = J0 + lane < J1 ? search(J0 + lane) : 0;
     uint32_t nxt = w_off[p + 1], gb = w_lo[p] - w_off[p];
-    const uint64_t* rec0 = cw.rec + p0 * CLAMP_PASS_RECS;
+    const uint64_t* rec0 = cw.rec + p0 * cw.pass_recs;
     auto load_batch = [&](uint64_t (&rv)[CP_RB], uint32_t jb) {
 #pragma unroll
       for (int u = 0; u < CP_RB; ++u) {
@@ -1198,7 +1219,7 @@ __device__ __forceinline__ void clamp_consume_bin(const ClampWork& cw, int64_t b
             nxt = w_off[p + 1];
             gb = w_lo[p] - w_off[p];
           }
-          rv[u] = rec0[(int64_t)p * CLAMP_PASS_RECS + (uint32_t)(j + gb)];
+          rv[u] = rec0[(int64_t)p * cw.pass_recs + (uint32_t)(j + gb)];
         }
       }
     };
@@ -1236,6 +1257,7 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   const int64_t T = (nN + 63) / 64, W = T + 2;
   const int64_t u = blockIdx.x;
   if (u >= 2 * T) return;  // whole workgroup
+  KCC_TL(1024 + u % 1024, 0);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const bool x_side = u < T;
   const int64_t g = x_side ? u : u - T;
@@ -1285,7 +1307,9 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
     }
   }
   __syncthreads();  // tab and colsum's zeroes
+  KCC_TL(1024 + u % 1024, 1);
   if (binned) clamp_consume_bin(cw, x_side ? g : T + g, tab, cp_lo, cp_off, &ctot[0][0]);
+  KCC_TL(1024 + u % 1024, 2);
   if (do_c) {
 #pragma unroll
     for (int k = 0; k < CPER; ++k) {
@@ -1322,6 +1346,7 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
     for (int k = k0; k < k1; ++k) tab[k * 64 + lane] += later;
   }
   __syncthreads();  // every wave's column totals are in tab
+  KCC_TL(1024 + u % 1024, 3);
   // wave 0: the 64 specs
   uint64_t csuf = 0;  // x side: Σ_{GY > gy} colsum[GY] per lane
   if (do_c) {  // suffix of colsum over GY in place (W <= 68: two chunks from the top)
@@ -1354,6 +1379,7 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   }
   const int32_t p = cw.dperm[x_side ? q : (int64_t)other];
   if (d && p < clamp_n_pure(nN, S)) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[p]), 0ull - d);
+  KCC_TL(1024 + u % 1024, 4);
 }
 
 // clamp_crows_kernel (only when C does not fit clamp_apply's full form): one wave per row
@@ -1500,6 +1526,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   const int32_t b = blockIdx.x, xcd = b & 7, r = b >> 3;
   const int32_t bx = r % gx, by = (r / gx) * 8 + xcd;
   if (by >= gy) return;  // padding of gy up to a multiple of 8 (whole workgroup)
+  KCC_TL(2048 + b % 4096, 0);
   const int32_t wv = __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
   const int64_t s = (int64_t)bx * FIT_SPW + threadIdx.x;
@@ -1563,6 +1590,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     lim = base + seg < n_groups ? base + seg : n_groups;
     claim_issue();
     claim_publish(0);
+    KCC_TL(2048 + b % 4096, 1);
   } else {  // static: this workgroup's share [by * per, (by + 1) * per)
     const uint32_t per = (n_groups + (uint32_t)gy - 1u) / (uint32_t)gy;
     const uint32_t g0 = (uint32_t)by * per < n_groups ? (uint32_t)by * per : n_groups;
@@ -1688,6 +1716,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
       else sum_b(cur, cnt);
     }
   }
+  KCC_TL(2048 + b % 4096, 2);
   if (idle) return;
   if (wave_exact) {  // exact-path specs: every node row (SlowNode), this workgroup's share
     const uint32_t nn = (uint32_t)n_nodes;  // < 2^28 per device
@@ -1713,6 +1742,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     if (errs) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[S + s]), errs);
   }
 #endif
+  KCC_TL(2048 + b % 4096, 3);
 }
 
 __global__ void fit_finalize_kernel(int64_t S, const int64_t* __restrict__ partial,
@@ -1837,20 +1867,23 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
                             SlowNode* slow, int64_t* slow_list, int64_t n_specs, ClampWork cw,
-                            unsigned long long* counters, int chunk, int64_t row0, hipStream_t s,
-                            bool dense) {
+                            unsigned long long* counters, int chunk, int64_t row0,
+                            int64_t call_nodes, hipStream_t s, bool dense) {
   if (n_nodes <= 0) return hipSuccess;
-  if (row0 % CLAMP_PASS_ROWS != 0) return hipErrorInvalidValue;
+  const int64_t pr = clamp_pass_rows(call_nodes);
+  if (row0 % pr != 0 || (pr != 1024 && pr != 4096)) return hipErrorInvalidValue;
   // one resident round of workgroups (LDS-bound at S <= CLAMP_LDS_SPECS: one per CU)
-  const bool lds = n_specs <= CLAMP_LDS_SPECS;
-  const size_t lds_bytes = lds ? NODE_PREP_LDS : 0;
-  static int64_t resident[2] = {0, 0};
-  int64_t& res = resident[lds ? 1 : 0];
+  const int mode = n_specs <= CLAMP_LDS_SPECS ? 2 : n_specs <= (int64_t)NP_ST_MAX * CLAMP_LDS_SPECS ? 1 : 0;
+  const size_t lds_bytes = mode == 2 ? NODE_PREP_LDS : mode == 1 ? NODE_PREP_LDS_SRCH : 0;
+  auto kern = pr == 1024 ? (mode == 2 ? node_prep_kernel<2, 1> : mode == 1 ? node_prep_kernel<1, 1> : node_prep_kernel<0, 1>)
+                         : (mode == 2 ? node_prep_kernel<2, 4> : mode == 1 ? node_prep_kernel<1, 4> : node_prep_kernel<0, 4>);
+  static int64_t resident[2][3] = {{0, 0, 0}, {0, 0, 0}};
+  int64_t& res = resident[pr == 1024 ? 0 : 1][mode];
   if (res == 0) {
     int dev = 0, cus = 0, blocks = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, node_prep_kernel, KCC_NODE_PREP_BLOCK,
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kern, KCC_NODE_PREP_BLOCK,
                                                      lds_bytes) == hipSuccess &&
         cus > 0 && blocks > 0)
       res = (int64_t)cus * blocks;
@@ -1858,12 +1891,12 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
       res = 256;
   }
   const int64_t cap = res < KCC_NODE_PREP_GRID ? res : KCC_NODE_PREP_GRID;
-  hipLaunchKernelGGL(node_prep_kernel,
-                     dim3(grid_for(n_nodes, CLAMP_PASS_ROWS, cap)),
+  hipLaunchKernelGGL(kern,
+                     dim3(grid_for(n_nodes, pr, cap)),
                      dim3(KCC_NODE_PREP_BLOCK), lds_bytes, s,
                      n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu, used_mem,
                      fast_a, fast_b, slow, slow_list, n_specs, cw, counters, (int32_t)chunk,
-                     (int32_t)(dense ? 1 : 0), row0 / CLAMP_PASS_ROWS);
+                     (int32_t)(dense ? 1 : 0), row0 / pr);
   return hipGetLastError();
 }
 
@@ -1890,6 +1923,7 @@ hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
                               const unsigned long long* counters, int64_t* partial, hipStream_t s) {
   if (n_specs <= 0) return hipSuccess;
   cw.n_pass = clamp_passes(n_nodes);
+  cw.pass_recs = 2 * clamp_pass_rows(n_nodes);
   const int64_t T = (n_specs + 63) / 64;  // >= this call's T (normal specs only)
   if (!clamp_c_full(T))  // C's row suffix sums (the kernel exits when this call's C is full)
     hipLaunchKernelGGL(clamp_crows_kernel, dim3((unsigned)((T + 2 + 3) / 4)), dim3(256), 0, s, cw,
@@ -1973,9 +2007,9 @@ hipError_t launch_partial_add(int64_t n, int64_t* dst, const int64_t* src, hipSt
 // diagnostic builds only: copy the timeline stamps (4096 x 4 u64) to `host`, then zero them
 extern "C" int kcc_debug_timeline(void* host) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(kcc::kcc_tl), sizeof(uint64_t) * 4096 * 4) != hipSuccess)
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(kcc::kcc_tl), sizeof(uint64_t) * 8192 * 8) != hipSuccess)
     return -2;
-  static uint64_t zero[4096][4];
+  static uint64_t zero[8192][8];
   return hipMemcpyToSymbol(HIP_SYMBOL(kcc::kcc_tl), zero, sizeof(zero)) == hipSuccess ? 0 : -3;
 }
 #endif

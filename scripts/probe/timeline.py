@@ -1,6 +1,10 @@
 """Diagnostic: per-workgroup phase timeline of the small fit-side kernels (a
--DKCC_TIMELINE build, variants/libkcc_tl.so), C4 inputs.  Stamps are s_memrealtime
-(100 MHz); printed in microseconds relative to the first spec_prep workgroup."""
+-DKCC_TIMELINE build, variants/libkcc_NAME.so).  Stamps are s_memrealtime (100 MHz),
+printed in microseconds relative to node_prep's first workgroup entry.
+
+  python scripts/probe/timeline.py [NAME] [--config C4] [--shard 8]
+"""
+import argparse
 import ctypes as C
 import os
 import sys
@@ -12,15 +16,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 from kubernetesclustercapacity_amd import _lib, synth  # noqa: E402
 
-name = sys.argv[1] if len(sys.argv) > 1 else "tl"
-L = _lib.load(os.path.join(ROOT, "variants", f"libkcc_{name}.so"))
+ap = argparse.ArgumentParser()
+ap.add_argument("name", nargs="?", default="tl")
+ap.add_argument("--config", default="C4")
+ap.add_argument("--shard", type=int, default=1)
+a = ap.parse_args()
+L = _lib.load(os.path.join(ROOT, "variants", f"libkcc_{a.name}.so"))
 L.kcc_debug_timeline.argtypes = [C.c_void_p]
 dev = torch.device("cuda", 0)
-cl = synth.config_cluster("C4")
-sc, sm = synth.config_specs("C4")
-T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+n_all = synth.CONFIGS[a.config]["n_nodes"]
+cl = synth.config_cluster(a.config, node_lo=0, node_hi=n_all // a.shard)
+sc, sm = synth.config_specs(a.config)
+T = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).to(dev)  # noqa: E731
 ptr, cpu, mem = T(cl.node_ptr), T(cl.cpu_req), T(cl.mem_req)
-ac, am, ap, pc = T(cl.alloc_cpu), T(cl.alloc_mem), T(cl.alloc_pods), T(cl.pod_count)
+ac, am, ap_, pc = T(cl.alloc_cpu), T(cl.alloc_mem), T(cl.alloc_pods), T(cl.pod_count)
 s_cpu, s_mem = T(sc), T(sm)
 n, S, nc = cl.n_nodes, sc.size, cl.n_containers
 uc = torch.empty(n, dtype=torch.int64, device=dev)
@@ -30,13 +39,13 @@ P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
 h = C.c_void_p()
 assert L.kcc_create(C.byref(h), 0, 1) == 0
 assert L.kcc_reserve(h, n, nc, S) == 0
-buf = np.zeros((4096, 4), np.uint64)
+buf = np.zeros((8192, 8), np.uint64)
 
 
 def step():
     assert L.kcc_reduce_requests_async(h, n, nc, P(ptr), P(cpu), P(mem), None, None, P(uc), P(um),
                                        None, None, None) == 0
-    assert L.kcc_fit_prepare_async(h, n, P(ac), P(am), P(ap), P(pc), P(uc), P(um), S, P(s_cpu),
+    assert L.kcc_fit_prepare_async(h, n, P(ac), P(am), P(ap_), P(pc), P(uc), P(um), S, P(s_cpu),
                                    P(s_mem), P(part), None) == 0
     assert L.kcc_fit_run_async(h, n, S, P(part), None) == 0
 
@@ -48,28 +57,44 @@ assert L.kcc_debug_timeline(buf.ctypes.data) == 0
 step()
 assert L.kcc_debug_timeline(buf.ctypes.data) == 0
 t = buf.astype(np.float64)
-t0 = t[0:300, 0][t[0:300, 0] > 0].min()
+npr = t[0:1024]
+t0 = npr[:, 2][npr[:, 2] > 0].min()
 us = lambda x: (x - t0) / 100.0  # noqa: E731
+print(f"config {a.config} shard 1/{a.shard}: {n} nodes, {S} specs")
 
 
 def show(label, rows, k0, k1):
     r = rows[(rows[:, k0] > 0) & (rows[:, k1] > 0)]
     if not len(r):
-        print(f"{label:34s} (none)")
+        print(f"{label:36s} (none)")
         return
     d = (r[:, k1] - r[:, k0]) / 100.0
-    print(f"{label:34s} n={len(r):4d} start {us(r[:, k0].min()):8.2f}..{us(r[:, k0].max()):8.2f}"
-          f"  end {us(r[:, k1].min()):8.2f}..{us(r[:, k1].max()):8.2f}"
-          f"  dur min/med/max {d.min():6.2f}/{np.median(d):6.2f}/{d.max():6.2f} us")
+    print(f"{label:36s} n={len(r):4d} start {us(r[:, k0].min()):7.2f}..{us(r[:, k0].max()):7.2f}"
+          f"  end {us(r[:, k1].min()):7.2f}..{us(r[:, k1].max()):7.2f}"
+          f"  dur min/med/max {d.min():6.2f}/{np.median(d):6.2f}/{d.max():6.2f}")
 
 
-sp = t[0:257]
-sp = t[0:300]
-show("spec_rank wgs", sp, 0, 1)
-show("node_prep entry -> after prologue", t[3072:4096], 2, 0)
-show("node_prep (after prologue -> end)", t[3072:4096], 0, 1)
-show("clamp_agg accumulate", t[2048:3072], 0, 1)
-show("clamp_agg suffixes+write", t[2048:3072], 1, 2)
-
-np_rows = t[3072:3072 + 512]
-np.save(os.path.join(ROOT, "gpurun_out", "tl_node_prep.npy"), np.stack([us(np_rows[:, 2]), us(np_rows[:, 0]), us(np_rows[:, 1])], 1))
+show("node_prep entry -> prologue done", npr, 2, 0)
+show("node_prep pass loads + phase 1", npr, 0, 3)
+show("node_prep phase 2 (+barrier)", npr, 3, 4)
+show("node_prep stream + records (+barrier)", npr, 4, 5)
+show("node_prep last pass -> end (C flush)", npr, 5, 1)
+show("node_prep whole", npr, 2, 1)
+fr = t[2048:6144]
+show("fit entry -> first claim", fr, 0, 1)
+show("fit loop", fr, 1, 2)
+show("fit slow rows + atomics", fr, 2, 3)
+show("fit whole", fr, 0, 3)
+cr = t[1024:2048]
+show("clamp_apply entry -> tab loaded", cr, 0, 1)
+show("clamp_apply consume bin", cr, 1, 2)
+show("clamp_apply suffixes", cr, 2, 3)
+show("clamp_apply specs (wave 0)", cr, 3, 4)
+show("clamp_apply whole", cr, 0, 4)
+# clamp_apply: consume time against the bin's record count (column 5)
+ok = (cr[:, 1] > 0) & (cr[:, 2] > 0)
+recs, dur = cr[ok, 5], (cr[ok, 2] - cr[ok, 1]) / 100.0
+order = np.argsort(-recs)[:8]
+print("clamp_apply heaviest bins (records, consume us):",
+      [(int(recs[i]), round(float(dur[i]), 2)) for i in order])
+print("clamp_apply records total", int(recs.sum()), "median", float(np.median(recs)))
