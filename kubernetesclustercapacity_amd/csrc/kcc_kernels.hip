@@ -1469,6 +1469,12 @@ constexpr int FIT_CHUNK_GROUPS = 128;  // 1024 nodes: |sum of contributions| <= 
 #endif
 constexpr uint32_t FIT_QCHUNK = KCC_FIT_QCHUNK;
 static_assert(FIT_QCHUNK >= 2 && FIT_QCHUNK <= FIT_CHUNK_GROUPS, "claims sum in i32");
+#ifndef KCC_FIT_QDIV
+#define KCC_FIT_QDIV 2  // guided claims: (what remains of the segment) / (QDIV x its workgroups)
+#endif
+#ifndef KCC_FIT_QMIN
+#define KCC_FIT_QMIN 2  // node groups per claim at least (guided claims)
+#endif
 #ifndef KCC_FIT_Q_HALVE
 #define KCC_FIT_Q_HALVE 128  // claims of FIT_QCHUNK / 2 when a workgroup's share is below this
 #endif
@@ -1572,11 +1578,18 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   // it is issued (its atomic-optimizer expansion reads the result at once); wave 0 waits
   // for it (vmcnt) at the end of the chunk — the loop bodies issue no other vector memory
   // operations
-  auto claim_issue = [&]() {
+  auto claim_issue = [&](uint32_t sz) {
     if (wv == 0 && lane == 0)
       asm volatile("global_atomic_add %0, %1, %2, off sc0"
-                   : "=v"(nxt) : "v"(qp), "v"(qsz) : "memory");
+                   : "=v"(nxt) : "v"(qp), "v"(sz) : "memory");
   };
+  // guided claims: a claim's size is (what remained of the segment at the workgroup's
+  // current claim) / (2 x its workgroups), between KCC_FIT_QMIN and qsz, so the claims
+  // shrink as the segment drains and the workgroups finish together (fixed claims of
+  // qsz left a tail of one to two claims: 10-20 us at C4).  Every wave computes the
+  // same sizes (workgroup-uniform); claims never overlap (fetch-and-add of each size).
+  const uint32_t wps = ((uint32_t)gy + nsub - 1u) / nsub;  // workgroups per segment
+  uint32_t qcur = qsz;  // size of the claim whose result is read next
   auto claim_publish = [&](uint32_t slot) {
     if (wv == 0) {
       asm volatile("s_waitcnt vmcnt(0)" : "+v"(nxt) : : "memory");
@@ -1585,10 +1598,10 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     __syncthreads();
   };
   if (KCC_FIT_QUEUE) {
-    const uint32_t seg = ((n_groups + nsub - 1u) / nsub + qsz - 1u) / qsz * qsz;
+    const uint32_t seg = ((n_groups + nsub - 1u) / nsub + 7u) / 8u * 8u;
     base = sub * seg < n_groups ? sub * seg : n_groups;
     lim = base + seg < n_groups ? base + seg : n_groups;
-    claim_issue();
+    claim_issue(qsz);
     claim_publish(0);
     KCC_TL(2048 + b % 4096, 1);
   } else {  // static: this workgroup's share [by * per, (by + 1) * per)
@@ -1694,13 +1707,17 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     for (uint32_t k = 0;; ++k) {
       const uint32_t cur = base + __builtin_amdgcn_readfirstlane(q_slot[k & 1u]);
       if (cur >= lim) break;  // workgroup-uniform
-      claim_issue();
-      const int cnt = (int)((cur + qsz < lim ? cur + qsz : lim) - cur);
+      uint32_t qn = (lim - cur) / ((uint32_t)KCC_FIT_QDIV * wps);
+      qn = qn < (uint32_t)KCC_FIT_QMIN ? (uint32_t)KCC_FIT_QMIN : (qn > qsz ? qsz : qn);
+      claim_issue(qn);
+      const int cnt = (int)((cur + qcur < lim ? cur + qcur : lim) - cur);
+      qcur = qn;
       if (wave_fast) {
         if (!wave_b) sum_a(cur, cnt);
         else sum_b(cur, cnt);
       }
       claim_publish((k + 1u) & 1u);
+      KCC_TLV(2048 + b % 4096, 4, (uint64_t)k + 1);
     }
     if (wv == 0 && lane == 0) {  // this workgroup made its last claim
       const uint32_t d = atomicAdd(qp + 1, 1u);

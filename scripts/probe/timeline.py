@@ -98,3 +98,26 @@ order = np.argsort(-recs)[:8]
 print("clamp_apply heaviest bins (records, consume us):",
       [(int(recs[i]), round(float(dur[i]), 2)) for i in order])
 print("clamp_apply records total", int(recs.sum()), "median", float(np.median(recs)))
+# fit: loop end times per XCD (blockIdx & 7) and claims per workgroup (column 4)
+ok = (fr[:, 1] > 0) & (fr[:, 2] > 0)
+idx = np.nonzero(ok)[0]
+ends = us(fr[ok, 2])
+claims = fr[ok, 4]
+for x in range(8):
+    sel = (idx & 7) == x
+    if sel.any():
+        print(f"fit xcd {x}: wgs {int(sel.sum())} loop end min/med/max {ends[sel].min():7.2f}/"
+              f"{np.median(ends[sel]):7.2f}/{ends[sel].max():7.2f}  claims min/med/max "
+              f"{int(claims[sel].min())}/{int(np.median(claims[sel]))}/{int(claims[sel].max())}")
+# fit: per segment (column bx, sub-queue = XCD) loop end spread; gx columns of 256 specs
+gx = (S + 255) // 256
+r_ = idx >> 3
+bx_ = r_ % gx
+seg_end = {}
+for k in range(len(idx)):
+    seg_end.setdefault((int(bx_[k]), int(idx[k] & 7)), []).append(ends[k])
+lo_ = np.array([min(v) for v in seg_end.values()])
+hi_ = np.array([max(v) for v in seg_end.values()])
+md_ = np.array([np.median(v) for v in seg_end.values()])
+print(f"fit segments {len(seg_end)}: within-segment spread med/max {np.median(hi_ - lo_):.2f}/{(hi_ - lo_).max():.2f}"
+      f"  segment median ends min/med/max {md_.min():.2f}/{np.median(md_):.2f}/{md_.max():.2f}")
