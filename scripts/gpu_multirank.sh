@@ -11,7 +11,7 @@ timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node
   --dist-backend gloo --steps 5 --scaling strong > gpurun_out/mr_n2.log 2>&1 || exit $?
 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29532 bench.py --gpus 2 --config $CFG \
-  --dist-backend gloo --steps 5 > gpurun_out/mr_n2w.log 2>&1 || exit $?
+  --dist-backend gloo --steps 5 --scaling weak > gpurun_out/mr_n2w.log 2>&1 || exit $?
 python - <<'PY'
 import json
 a = json.loads(open("gpurun_out/mr_n1.log").read().strip().splitlines()[-1])
