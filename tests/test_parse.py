@@ -366,7 +366,10 @@ def qty_fast_corpus():
             out.append("0" * d + s)
     out += ["7Ei", "8Ei", "8191Pi", "8192Pi", "9223372036854", "9223372036854k",
             "9223372E", "9223373T", "10E", "9224P", "9223372036854T", "1K", "1ki", "1Ei0", "Ki", "k", "1.5Gi", "+1Gi", "-1Gi",
-            "1e3", "1m", "1 ", " 1", "1Kib", "12345678901234"]
+            "1e3", "1m", "1 ", " 1", "1Kib", "12345678901234",
+            # characters beside '0'..'9' in the byte table, inside the digits and last
+            "12:4Mi", "1/2G", "99a", "1:", "/1", "9\x7f9", "12345678:1", "1234567890/23",
+            "123456789012Ki", "1234567890123Ki", "123456789012M", "1234567890123", "0Ki", "0E"]
     return out
 
 
