@@ -195,6 +195,7 @@ void reduce_kernel(
   // are local to the launch)
   const int64_t wb = c0 + (int64_t)w * range;
   if (wb >= n_cont) return;  // wave-uniform; no block-level barrier in this kernel
+  KCC_TL(4096 + (blockIdx.x - pa.n_blocks) % 4096, 0);
   const int32_t len = (int32_t)(n_cont - wb < range ? n_cont - wb : range);
   __builtin_assume(len >= 1);  // (wb < n_cont: the tile loop runs, its first loads need no guard)
   uint64_t (*pre)[RED_TILE] = pre_s[threadIdx.x >> 6];
@@ -395,6 +396,7 @@ void reduce_kernel(
     for (int k = 0; k < NA; ++k)
       if (carry[k] != 0) atomic_add_u64(&out[k][cur], carry[k]);
   }
+  KCC_TL(4096 + (blockIdx.x - pa.n_blocks) % 4096, 1);
 }
 
 // ----------------------------------------------------------------------------

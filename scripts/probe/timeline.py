@@ -121,3 +121,22 @@ hi_ = np.array([max(v) for v in seg_end.values()])
 md_ = np.array([np.median(v) for v in seg_end.values()])
 print(f"fit segments {len(seg_end)}: within-segment spread med/max {np.median(hi_ - lo_):.2f}/{(hi_ - lo_).max():.2f}"
       f"  segment median ends min/med/max {md_.min():.2f}/{np.median(md_):.2f}/{md_.max():.2f}")
+# reduce: wave 0 of each workgroup (slots 4096 + workgroup), start/end (columns 0, 1)
+rr = t[4096:8192]
+okr = (rr[:, 0] > 0) & (rr[:, 1] > 0)
+if okr.any():
+    r0 = rr[okr, 0].min()
+    st_, en_ = (rr[okr, 0] - r0) / 100.0, (rr[okr, 1] - r0) / 100.0
+    print(f"reduce waves {int(okr.sum())}: start max {st_.max():.2f}  end min/p10/med/p90/max "
+          f"{en_.min():.2f}/{np.percentile(en_, 10):.2f}/{np.median(en_):.2f}/{np.percentile(en_, 90):.2f}/{en_.max():.2f}")
+if okr.any():
+    idr = np.nonzero(okr)[0]
+    for x in range(8):
+        sel = (idr & 7) == x
+        e = en_[sel]
+        print(f"reduce xcd {x}: wgs {int(sel.sum())} end min/med/max {e.min():.2f}/{np.median(e):.2f}/{e.max():.2f}")
+    # by position in the grid (dispatch order): quartiles of workgroup index
+    for qd in range(4):
+        sel = (idr >= qd * len(rr) // 4) & (idr < (qd + 1) * len(rr) // 4)
+        if sel.any():
+            print(f"reduce wg quarter {qd}: end med {np.median(en_[sel]):.2f} max {en_[sel].max():.2f}")
