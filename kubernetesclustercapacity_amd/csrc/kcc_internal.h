@@ -179,7 +179,11 @@ constexpr int64_t MAX_SPECS = (int64_t)1 << 26;
 __host__ __device__ inline int64_t clamp_c_cells(int64_t S) { return (S / 64 + 3) * (S / 64 + 3); }
 inline int64_t clamp_h_cells(int64_t S) { return (S / 64 + 1) * 65 * 64; }
 #ifndef KCC_C_COPIES
-#define KCC_C_COPIES 8
+// copies of the coarse table: node_prep flushes its LDS-summed table once per workgroup
+// (S <= 4096), so two spread the flushes enough; clamp_apply's x-group workgroups read
+// every copy (C4 8-way shard, fit prepare + run: 8 copies 60.4 us, 2: 58.2, 1: 58.5; C5's
+// global-memory atomics need more than one: 544.8 / 545.5 / 557.8 us)
+#define KCC_C_COPIES 2
 #endif
 constexpr int C_COPIES = KCC_C_COPIES;
 #ifndef KCC_H2_COPIES
