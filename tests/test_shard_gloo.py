@@ -2,7 +2,8 @@
 
 Each rank generates only its node range of the cluster (synth is shard-stable),
 computes its per-spec partial vector [sums | div-by-zero counts] (the oracle stands
-in for kcc_fit_partial_async here: no GPU in this suite), all-reduces it with
+in for kcc_capacity_partial_async in the CPU tests; the -m gpu test runs libkcc in every
+rank, the ranks sharing one GPU), all-reduces it with
 shard.allreduce_partial and applies the finalize rule.  The result must equal the
 unsharded computation bit for bit — the same exchange bench.py runs over RCCL.
 """
@@ -76,3 +77,58 @@ def test_node_range_partitions_exactly():
             assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
             sizes = [h - l for l, h in b]
             assert max(sizes) - min(sizes) <= 1
+
+
+def _worker_gpu(rank, world, port, n, pods, S, adversarial, out):
+    """As _worker, but the rank's partial comes from libkcc on cuda:0
+    (kcc_capacity_partial_async: reduce + spec setup + node prep + fit + clamp
+    correction of the rank's own nodes), the ranks sharing the one GPU of the box."""
+    import torch
+
+    from kubernetesclustercapacity_amd import CapacityEngine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard.node_range(n, rank, world)
+    c = synth.make_cluster(n, pods, seed=77, node_lo=lo, node_hi=hi, adversarial=adversarial,
+                           chunk=256)
+    sc, sm = synth.make_specs(S, seed=77, adversarial=adversarial)
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+    nl = c.alloc_cpu.size
+    uc = torch.empty(nl, dtype=torch.int64, device=dev)
+    um = torch.empty(nl, dtype=torch.int64, device=dev)
+    part = torch.empty(2 * S, dtype=torch.int64, device=dev)
+    with CapacityEngine(0, 1) as eng:
+        eng.capacity_partial_async(c.node_ptr, T(c.node_ptr), T(c.cpu_req), T(c.mem_req),
+                                   T(c.alloc_cpu), T(c.alloc_mem), T(c.alloc_pods),
+                                   T(c.pod_count), uc, um, T(sc), T(sm), part)
+        torch.cuda.synchronize()
+        p = part.cpu()  # internal spec order (the same on every rank: same specs)
+        shard.allreduce_partial(p)
+        if rank == 0:  # the library's finalize maps it back to caller order
+            totals = torch.empty(S, dtype=torch.int64, device=dev)
+            err = torch.empty(S, dtype=torch.int32, device=dev)
+            eng.fit_finalize_async(S, p.to(dev), totals, err)
+            torch.cuda.synchronize()
+            np.save(out, np.concatenate([totals.cpu().numpy(), err.cpu().numpy().astype(np.int64)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_rank_partials_equal_whole(tmp_path, world):
+    """Rank-local libkcc partials (adversarial rows: slow rows, clamp cases, wraps)
+    summed over a gloo all-reduce == the oracle over the whole cluster."""
+    n, pods, S = 20_011, 300_000, 300
+    out = str(tmp_path / "r0.npy")
+    mp.spawn(_worker_gpu, args=(world, _free_port(), n, pods, S, True, out), nprocs=world,
+             join=True)
+    got = np.load(out)
+    c = synth.make_cluster(n, pods, seed=77, adversarial=True, chunk=256)
+    sc, sm = synth.make_specs(S, seed=77, adversarial=True)
+    from oracle import coracle
+    uc, um, _, _ = coracle.reduce_requests(c.node_ptr, c.cpu_req, c.mem_req)
+    t, e = coracle.fit(c.alloc_cpu, c.alloc_mem, c.alloc_pods, c.pod_count, uc, um, sc, sm)
+    np.testing.assert_array_equal(got[:S], t)
+    np.testing.assert_array_equal(got[S:], e)
