@@ -325,7 +325,10 @@ hipError_t launch_parse(int mode, int64_t n, const uint8_t* bytes, int64_t n_byt
 constexpr int KB_SHIFT = 12;  // 4096 rows per bucket: ~1 KB runs per tile and array
 constexpr int KB_ROWS = 1 << KB_SHIFT;
 #ifndef KCC_KB_TILE
-#define KCC_KB_TILE 32768
+// containers per scatter workgroup (about; keyed_tile cuts whole rounds): at C4 65536
+// (3 rounds, 768 tiles) took the keyed call 0.392 -> 0.340 and 0.395 -> 0.372 ms on two
+// boxes against 32768 (5 rounds); 131072 equal, 262144 slower
+#define KCC_KB_TILE 65536
 #endif
 constexpr int KB_TILE = KCC_KB_TILE;  // containers per scatter workgroup
 constexpr int64_t KB_NB_MAX = 4096;  // buckets (LDS cursors): n_keys <= 16M rows
