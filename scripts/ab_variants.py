@@ -168,6 +168,67 @@ def run_keyed(names, config, rounds, reps):
                           "frac": alg / (ms * 1e-3) / 8e12, "cpu_sums_equal_csr": ok[nm]}))
 
 
+def run_parse(names, config, rounds, reps):
+    """The quantity-string legs (bench parse / parse.quantity): the config's container cpu
+    and memory request strings, kcc_parse_cpu_millis_async and kcc_parse_quantity_async,
+    every variant's outputs checked equal to the first's."""
+    import numpy as np
+    import torch
+
+    from kubernetesclustercapacity_amd import _lib, quantity, synth
+
+    dev = torch.device("cuda", 0)
+    cl = synth.config_cluster(config)
+    legs = {}
+    for leg, fmt in (("cpu", quantity.cpu_quantity_strings), ("qty", quantity.memory_quantity_strings)):
+        buf, off = fmt(cl.cpu_req if leg == "cpu" else cl.mem_req)
+        b = torch.from_numpy(buf).to(dev)
+        o = torch.from_numpy(off.astype(np.int64)).to(dev)
+        legs[leg] = (b, o, torch.empty(o.numel() - 1, dtype=torch.int64, device=dev),
+                     torch.empty(o.numel() - 1, dtype=torch.int8, device=dev))
+    P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    stream = torch.cuda.Stream(dev)
+    sh = C.c_void_p(stream.cuda_stream)
+    libs, ctxs = {}, {}
+    for nm in names:
+        L = _lib.load(os.path.join(VDIR, f"libkcc_{nm}.so"))
+        h = C.c_void_p()
+        assert L.kcc_create(C.byref(h), 0, 1) == 0, L.kcc_create_error()
+        libs[nm], ctxs[nm] = L, h
+
+    def call(nm, leg):
+        b, o, out, st = legs[leg]
+        fn = libs[nm].kcc_parse_cpu_millis_async if leg == "cpu" else libs[nm].kcc_parse_quantity_async
+        assert fn(ctxs[nm], o.numel() - 1, P(b), b.numel(), P(o), P(out), P(st), sh) == 0
+
+    times = {nm: {"cpu": [], "qty": []} for nm in names}
+    ref = {}
+    with torch.cuda.stream(stream):
+        for nm in names:
+            for leg in ("cpu", "qty"):
+                call(nm, leg)
+                torch.cuda.synchronize()
+                got = (legs[leg][2].clone(), legs[leg][3].clone())
+                if leg not in ref:
+                    ref[leg] = got
+                assert torch.equal(got[0], ref[leg][0]) and torch.equal(got[1], ref[leg][1]), (nm, leg)
+        for _ in range(rounds):
+            for nm in names:
+                for leg in ("cpu", "qty"):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    for _ in range(reps):
+                        call(nm, leg)
+                    e1.record(stream)
+                    e1.synchronize()
+                    times[nm][leg].append(e0.elapsed_time(e1) / reps)
+    for nm in names:
+        print(json.dumps({"variant": nm, "config": config,
+                          "cpu_ms_median": float(np.median(times[nm]["cpu"])),
+                          "qty_ms_median": float(np.median(times[nm]["qty"])),
+                          "identical_outputs": True}))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "build":
         build(sys.argv[2:])
@@ -181,8 +242,11 @@ if __name__ == "__main__":
         ap.add_argument("--reps", type=int, default=10)
         ap.add_argument("--shard", type=int, default=1, help="use rank 0's nodes of this many")
         ap.add_argument("--keyed", action="store_true", help="time the keyed reduce instead")
+        ap.add_argument("--parse", action="store_true", help="time the quantity-string kernels instead")
         a = ap.parse_args()
-        if a.keyed:
+        if a.parse:
+            run_parse(a.names, a.config, a.rounds, a.reps)
+        elif a.keyed:
             run_keyed(a.names, a.config, a.rounds, a.reps)
         else:
             run(a.names, a.config, a.rounds, a.reps, a.shard)
