@@ -1253,6 +1253,7 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   __shared__ uint64_t tab[H_CELLS];
   __shared__ uint64_t ctot[CP_WAVES][64];
   __shared__ uint64_t colsum[128];
+  __shared__ uint32_t pos_s[64];          // the specs' kpos / jpos (wave 15 -> every wave)
   __shared__ uint32_t cp_lo[CP_PW];       // binned: a window's passes' bin starts
   __shared__ uint32_t cp_off[CP_PW + 1];  // and the exclusive prefix of their counts
   const int64_t nN = clamp_n_normal(counters);
@@ -1266,8 +1267,8 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   const bool full = clamp_c_full(T);
   // this workgroup's 64 specs (wave 0), loaded up front
   const int64_t q = 64 * g + lane;  // x (x side) or y (y side)
-  uint32_t other = 0xffffffffu;
-  if (wv == 0) other = (x_side ? cw.mr_c : cw.cr_m)[q];  // y of x, or x of y (padding: ~0)
+  uint32_t other = 0xffffffffu;  // wave 0 (the specs' lookups) and wave 15 (their positions)
+  if (wv == 0 || wv == CP_WAVES - 1) other = (x_side ? cw.mr_c : cw.cr_m)[q];  // y of x, or x of y (padding: ~0)
   if (tid < 128) colsum[tid] = 0;
   // the table: binned records (below), or every copy's cells first, then LDS and zeroes
   const bool binned = clamp_binned(S);
@@ -1319,35 +1320,34 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
       if (e < c1 && cv[k]) atomicAdd(reinterpret_cast<unsigned long long*>(&colsum[e % W]), cv[k]);
     }
   }
-  // rows of tab: suffix along r (lanes reversed, DPP inclusive scan)
+  // wave 0: the specs' internal positions, in flight during the suffix work below
+  int32_t p = 0x7fffffff;
+  if (wv == 0 && q < nN) p = cw.dperm[x_side ? q : (int64_t)other];
+  // rows of tab: suffix along r (lanes reversed, DPP inclusive scan); wave 15 (fewest
+  // rows) also ranks the specs: pos = #{members with a smaller y (x side) / x (y side)}
   for (int k = wv; k < 65; k += CP_WAVES) {
-    const uint64_t s = wave_incl_scan_u64(tab[k * 64 + 63 - lane]);
-    tab[k * 64 + 63 - lane] = s;
+    const uint64_t sr = wave_incl_scan_u64(tab[k * 64 + 63 - lane]);
+    tab[k * 64 + 63 - lane] = sr;
+  }
+  if (wv == CP_WAVES - 1) {
+    uint32_t pos = 0;
+    for (int l = 0; l < 64; ++l) pos += (uint32_t)__builtin_amdgcn_readlane((int)other, l) < other ? 1u : 0u;
+    pos_s[lane] = pos;
   }
   __syncthreads();
-  // columns of tab: suffix along k, 16 chunks of 5 rows, then the later chunks' totals
+  // spec l needs S2[pos_l + 1][l + 1] = Σ_{k > pos_l} rowsuf[k][l + 1] (column 64: none):
+  // each wave sums its chunk of rows under that mask, wave 0 adds the chunks
   constexpr int KCH = (65 + CP_WAVES - 1) / CP_WAVES;
   const int k0 = wv * KCH, k1 = k0 + KCH < 65 ? k0 + KCH : 65;
-  uint64_t run = 0;
-  for (int k = k1 - 1; k >= k0; --k) {
-    run += tab[k * 64 + lane];
-    tab[k * 64 + lane] = run;
-  }
-  ctot[wv][lane] = run;
-  __syncthreads();
-  if (wv != 0) {
-    uint64_t later = 0;
-    for (int w2 = wv + 1; w2 < CP_WAVES; ++w2) later += ctot[w2][lane];
-    for (int k = k0; k < k1; ++k) tab[k * 64 + lane] += later;
-    __syncthreads();
-    return;
-  }
   {
-    uint64_t later = 0;
-    for (int w2 = 1; w2 < CP_WAVES; ++w2) later += ctot[w2][lane];
-    for (int k = k0; k < k1; ++k) tab[k * 64 + lane] += later;
+    const uint32_t posl = pos_s[lane];
+    uint64_t part = 0;
+    for (int k = k0; k < k1; ++k)
+      part += (lane < 63 && (uint32_t)k > posl) ? tab[k * 64 + lane + 1] : 0ull;
+    ctot[wv][lane] = part;
   }
-  __syncthreads();  // every wave's column totals are in tab
+  __syncthreads();
+  if (wv != 0) return;  // (no barrier below)
   KCC_TL(1024 + u % 1024, 3);
   // wave 0: the 64 specs
   uint64_t csuf = 0;  // x side: Σ_{GY > gy} colsum[GY] per lane
@@ -1355,19 +1355,18 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
     uint64_t carry = 0;
     for (int ch = 1; ch >= 0; --ch) {
       const int col = ch * 64 + 63 - lane;  // lanes reversed: an inclusive scan is the suffix
-      uint64_t s = col < W ? colsum[col] : 0ull;
-      s = wave_incl_scan_u64(s) + carry;
-      carry = readlane_u64(s, 63);
-      if (col < W) colsum[col] = s;
+      uint64_t sv = col < W ? colsum[col] : 0ull;
+      sv = wave_incl_scan_u64(sv) + carry;
+      carry = readlane_u64(sv, 63);
+      if (col < W) colsum[col] = sv;
     }
     const uint32_t gy1 = other == 0xffffffffu ? 0xffffffffu : (other >> 6) + 1;
     csuf = gy1 < W ? colsum[gy1] : 0ull;
   }
-  uint32_t pos = 0;
-  for (int l = 0; l < 64; ++l) pos += (uint32_t)__builtin_amdgcn_readlane((int)other, l) < other ? 1u : 0u;
   if (q >= nN) return;
   uint64_t d = csuf;
-  if (lane < 63) d += tab[(pos + 1) * 64 + lane + 1];
+#pragma unroll
+  for (int w2 = 0; w2 < CP_WAVES; ++w2) d += ctot[w2][lane];
   if (x_side && !full) {
     const int64_t gy = other >> 6;
     uint64_t part[8] = {};
@@ -1379,7 +1378,6 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
 #pragma unroll
     for (int r = 0; r < 8; ++r) d += part[r];
   }
-  const int32_t p = cw.dperm[x_side ? q : (int64_t)other];
   if (d && p < clamp_n_pure(nN, S)) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[p]), 0ull - d);
   KCC_TL(1024 + u % 1024, 4);
 }
