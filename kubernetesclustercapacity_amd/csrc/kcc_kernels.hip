@@ -1138,9 +1138,13 @@ __host__ __device__ inline bool clamp_c_full(int64_t T) { return (T + 2) * (T + 
 #define KCC_DIAG_CP 0  // diagnostic timing builds only: bit 0 drops the adds, bit 1 the records
 #endif
 constexpr int CP_PW = 4096;
+#ifndef KCC_CP_SPLIT
+#define KCC_CP_SPLIT 4  // workgroups per bin at most (binned clamp tables)
+#endif
 constexpr int CP_RB = 8;  // records per thread in flight
 __device__ __forceinline__ void clamp_consume_bin(const ClampWork& cw, int64_t bin, uint64_t* tab,
-                                                  uint32_t* w_lo, uint32_t* w_off, uint64_t* scratch) {
+                                                  uint32_t* w_lo, uint32_t* w_off, uint64_t* scratch,
+                                                  uint32_t h, uint32_t G) {
   constexpr int PPT = CP_PW / CP_THREADS;  // passes per thread and window
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   uint32_t* wsum = reinterpret_cast<uint32_t*>(scratch);  // CP_WAVES wave totals
@@ -1202,9 +1206,11 @@ __device__ __forceinline__ void clamp_consume_bin(const ClampWork& cw, int64_t b
         if (w_off[p + st] <= j) p += st;
       return p;
     };
-    const uint32_t per_w = (total + CP_WAVES * 64 - 1) / (CP_WAVES * 64) * 64;
-    const uint32_t J0 = (uint32_t)wv * per_w;
-    const uint32_t J1 = J0 + per_w < total ? J0 + per_w : total;
+    // share h of G of the window's records (the bin split over G workgroups)
+    const uint32_t s0 = (uint32_t)((uint64_t)total * h / G), s1 = (uint32_t)((uint64_t)total * (h + 1) / G);
+    const uint32_t per_w = (s1 - s0 + CP_WAVES * 64 - 1) / (CP_WAVES * 64) * 64;
+    const uint32_t J0 = s0 + (uint32_t)wv * per_w;
+    const uint32_t J1 = J0 + per_w < s1 ? J0 + per_w : s1;
     // a lane's pass p, where its records leave it (nxt = w_off[p + 1]) and its start in
     // the pass's slots minus its first flat index (gb), in registers
     int p = J0 + lane < J1 ? search(J0 + lane) : 0;
@@ -1258,9 +1264,12 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   __shared__ uint32_t cp_off[CP_PW + 1];  // and the exclusive prefix of their counts
   const int64_t nN = clamp_n_normal(counters);
   const int64_t T = (nN + 63) / 64, W = T + 2;
-  const int64_t u = blockIdx.x;
+  // blockIdx = h * 2 Tm + u: part h of the G parts of bin u (launch_clamp_apply)
+  const int64_t Tm = (S + 63) / 64;
+  const uint32_t G = gridDim.x / (uint32_t)(2 * Tm), h = blockIdx.x / (uint32_t)(2 * Tm);
+  const int64_t u = blockIdx.x % (uint32_t)(2 * Tm);
   if (u >= 2 * T) return;  // whole workgroup
-  KCC_TL(1024 + u % 1024, 0);
+  KCC_TL(1024 + blockIdx.x % 1024, 0);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const bool x_side = u < T;
   const int64_t g = x_side ? u : u - T;
@@ -1288,7 +1297,7 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   constexpr int CPER = (int)((C_FULL_CELLS + CP_THREADS - 1) / CP_THREADS);
   uint64_t cv[CPER];
   const int64_t c0 = (g + 1) * W, c1 = W * W;  // cells of rows g+1 .. T+1
-  const bool do_c = x_side && full;
+  const bool do_c = x_side && full && h == 0;  // the coarse parts: part 0 of the bin
 #pragma unroll
   for (int k = 0; k < CPER; ++k) {
     const int64_t e = c0 + tid + CP_THREADS * k;
@@ -1310,9 +1319,9 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
     }
   }
   __syncthreads();  // tab and colsum's zeroes
-  KCC_TL(1024 + u % 1024, 1);
-  if (binned) clamp_consume_bin(cw, x_side ? g : T + g, tab, cp_lo, cp_off, &ctot[0][0]);
-  KCC_TL(1024 + u % 1024, 2);
+  KCC_TL(1024 + blockIdx.x % 1024, 1);
+  if (binned) clamp_consume_bin(cw, x_side ? g : T + g, tab, cp_lo, cp_off, &ctot[0][0], h, G);
+  KCC_TL(1024 + blockIdx.x % 1024, 2);
   if (do_c) {
 #pragma unroll
     for (int k = 0; k < CPER; ++k) {
@@ -1348,7 +1357,7 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   }
   __syncthreads();
   if (wv != 0) return;  // (no barrier below)
-  KCC_TL(1024 + u % 1024, 3);
+  KCC_TL(1024 + blockIdx.x % 1024, 3);
   // wave 0: the 64 specs
   uint64_t csuf = 0;  // x side: Σ_{GY > gy} colsum[GY] per lane
   if (do_c) {  // suffix of colsum over GY in place (W <= 68: two chunks from the top)
@@ -1367,7 +1376,7 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   uint64_t d = csuf;
 #pragma unroll
   for (int w2 = 0; w2 < CP_WAVES; ++w2) d += ctot[w2][lane];
-  if (x_side && !full) {
+  if (x_side && !full && h == 0) {
     const int64_t gy = other >> 6;
     uint64_t part[8] = {};
     for (int64_t G = g + 1; G <= T + 1; G += 8) {
@@ -1379,7 +1388,7 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
     for (int r = 0; r < 8; ++r) d += part[r];
   }
   if (d && p < clamp_n_pure(nN, S)) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[p]), 0ull - d);
-  KCC_TL(1024 + u % 1024, 4);
+  KCC_TL(1024 + blockIdx.x % 1024, 4);
 }
 
 // clamp_crows_kernel (only when C does not fit clamp_apply's full form): one wave per row
@@ -1945,7 +1954,23 @@ hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
   if (!clamp_c_full(T))  // C's row suffix sums (the kernel exits when this call's C is full)
     hipLaunchKernelGGL(clamp_crows_kernel, dim3((unsigned)((T + 2 + 3) / 4)), dim3(256), 0, s, cw,
                        counters);
-  hipLaunchKernelGGL(clamp_apply_kernel, dim3((unsigned)(2 * T)), dim3(CP_THREADS), 0, s, cw,
+  // binned: each bin's records split over G workgroups (D is linear in the table: each
+  // part subtracts its own share), up to about two resident workgroups per CU
+  static int64_t resident = 0;  // clamp_apply workgroups resident at once
+  if (resident == 0) {
+    int dev = 0, cus = 0, blocks = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, clamp_apply_kernel, CP_THREADS, 0) == hipSuccess &&
+        cus > 0 && blocks > 0)
+      resident = (int64_t)cus * blocks;
+    else
+      resident = 256;
+  }
+  int64_t G = 1;
+  if (clamp_binned(n_specs))
+    while (G < KCC_CP_SPLIT && 2 * T * G * 2 <= resident) G *= 2;
+  hipLaunchKernelGGL(clamp_apply_kernel, dim3((unsigned)(2 * T * G)), dim3(CP_THREADS), 0, s, cw,
                      counters, n_specs, partial);
   return hipGetLastError();
 }
