@@ -437,25 +437,17 @@ __device__ __forceinline__ int64_t clamp_n_pure(int64_t nN, int64_t S) {
   return (nN % 64 == 0 || nN == S) ? nN : nN / 64 * 64;
 }
 
-// #{k < 4096 : a[k] <= v} for a sorted ascending (8-ary: after the step of width s the
-// answer lies in [lo, lo + s])
-// LDS slot of entry k of a 4096-entry search table: the low 5 bits XORed with bits 5-9
-// and 10-14.  A binary search's probes at one level are spaced by a power of two >= 32
-// entries for its first 7 levels, i.e. all in ONE bank of a plain layout (ds_read_b32
-// banks are (a/4) mod 32, ds_read_b64's (a/4) mod 64: 32 u32 or i64 entries per bank
-// row); swizzled, they spread over the banks: 48 instead of 285 LDS cycles per wave and
-// search (random queries, simulated), a bijection within each 32-entry row.
-__device__ __forceinline__ uint32_t np_swz(uint32_t k) { return k ^ (((k >> 5) ^ (k >> 10)) & 31u); }
-
-// #{k < 4096 : a[k] <= v} for a sorted ascending, stored swizzled (np_swz); binary: 12
-// dependent reads
-template <class T>
-__device__ __forceinline__ uint32_t search2_4096(const T* a, T v) {
-  static_assert(CLAMP_LDS_SPECS == 4096, "search2_4096 covers 2^12 entries");
-  uint32_t lo = 0;  // after the step of width s the answer lies in [lo, lo + s]
-#pragma unroll
-  for (uint32_t s = 2048; s >= 1; s /= 2) lo += a[np_swz(lo + s - 1)] <= v ? s : 0u;
-  return lo;
+// Slot of entry k (rank k < 4096 of a sorted ascending search table): the BFS
+// (Eytzinger) order of the perfect binary tree over entries 0..4094 — slot 1 the root,
+// slots 2i and 2i + 1 its children — and entry 4095 in slot 0.  A search walks
+// i -> 2i + (a[i] <= v) for 12 levels (one compare and one shift-add per level, no index
+// arithmetic), and i - 4096 = #{k < 4095 : a[k] <= v}; slot 0 adds the last entry.  The
+// top levels' probes are shared by many lanes (LDS broadcast), the deeper ones spread
+// over the banks (a sorted layout's probes, 2^j entries apart, sat in one bank).
+__host__ __device__ inline uint32_t np_slot(uint32_t k) {
+  if (k == 4095u) return 0u;
+  const uint32_t t = (uint32_t)__builtin_ctz(k + 1u);
+  return (1u << (11u - t)) + ((k + 1u) >> (t + 1u));
 }
 // the 64 x 64 member masks mk[g][Y]: Y XOR g, so a row (fixed g) and a column (fixed Y)
 // of 32 lanes both hit 32 distinct bank pairs (ds_read_b64)
@@ -632,8 +624,8 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
     for (int u = 0; u < PER; ++u) {
       const int64_t k = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
       const bool in = (k + 1) * st - 1 < nN;  // padded: +inf
-      cs_l[np_swz((uint32_t)k)] = in && cv[u] < FAST_FC_MAX ? (uint32_t)cv[u] : 0xffffffffu;
-      ms_l[np_swz((uint32_t)k)] = in ? (int64_t)mv[u] : INT64_MAX;
+      cs_l[np_slot((uint32_t)k)] = in && cv[u] < FAST_FC_MAX ? (uint32_t)cv[u] : 0xffffffffu;
+      ms_l[np_slot((uint32_t)k)] = in ? (int64_t)mv[u] : INT64_MAX;
       if (!in) yv[u] = 0xffffffffu;
       if (lds) mk_l[k] = 0ull;  // 64 x 64 masks: one per spec slot
     }
@@ -765,11 +757,16 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       const int64_t V = act ? V0 : 0;
       uint32_t L = 0, b = 0;
       if (srch) {  // (b) over the LDS tables (every st-th request), then the bucket in memory
+        uint32_t iL = 1, ib = 1;  // np_slot's tree
 #pragma unroll
-        for (uint32_t sw = 2048; sw >= 1; sw /= 2) {
-          L += cs_l[np_swz(L + sw - 1)] <= U ? sw : 0u;
-          b += ms_l[np_swz(b + sw - 1)] <= V ? sw : 0u;
+        for (int lv = 0; lv < 12; ++lv) {
+          iL = 2 * iL + (cs_l[iL] <= U ? 1u : 0u);
+          ib = 2 * ib + (ms_l[ib] <= V ? 1u : 0u);
         }
+        L = iL - 4096u;
+        b = ib - 4096u;
+        L += L == 4095u && cs_l[0] <= U ? 1u : 0u;  // the last entry (slot 0)
+        b += b == 4095u && ms_l[0] <= V ? 1u : 0u;
         if (KCC_DIAG_NP & 4) {  // diagnostic: no searches
           L = w ? 1 + (U & 2047) : 0;
           b = w ? 1 + ((uint32_t)V & 2047) : 0;
