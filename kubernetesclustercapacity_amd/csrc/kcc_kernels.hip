@@ -128,11 +128,15 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 // The lane offset (voff) is loop-invariant and the tile offset goes in soffset, so no
 // address VGPR is recomputed per tile (a recomputed address register that the
 // allocator shares with an in-flight load's destination forces a vmcnt(0) wait).
+#ifndef KCC_RED_LOAD_AUX
+#define KCC_RED_LOAD_AUX 0  // the loads' cache-policy bits (A/B builds)
+#endif
 __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff, int32_t soff,
                                           uint64_t (&x)[4]) {
-  const u64x2 lo = __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
-  const u64x2 hi =
-      __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16, soff, 0));
+  const u64x2 lo =
+      __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, KCC_RED_LOAD_AUX));
+  const u64x2 hi = __builtin_bit_cast(
+      u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16, soff, KCC_RED_LOAD_AUX));
   x[0] = lo.x;
   x[1] = lo.y;
   x[2] = hi.x;
@@ -1952,7 +1956,9 @@ hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
     hipLaunchKernelGGL(clamp_crows_kernel, dim3((unsigned)((T + 2 + 3) / 4)), dim3(256), 0, s, cw,
                        counters);
   // binned: each bin's records split over G workgroups (D is linear in the table: each
-  // part subtracts its own share), up to about two resident workgroups per CU
+  // part subtracts its own share), as many as one round of resident workgroups holds
+  // (C4: 1 per CU by registers, G = 2; more parts in a second round, G = 4 / 8: +7 / +24 us;
+  // 64 VGPRs for 2 per CU and G = 4: equal)
   static int64_t resident = 0;  // clamp_apply workgroups resident at once
   if (resident == 0) {
     int dev = 0, cus = 0, blocks = 0;
