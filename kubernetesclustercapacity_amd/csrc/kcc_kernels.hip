@@ -105,6 +105,17 @@ __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
   return v;
 }
 
+// 32-bit version (every lane sum below 2^32; also packed fields that never carry)
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, DPP_ROW_SHR + 1, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0u, v, DPP_ROW_SHR + 2, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0u, v, DPP_ROW_SHR + 4, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0u, v, DPP_ROW_SHR + 8, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0u, v, DPP_ROW_BCAST15, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0u, v, DPP_ROW_BCAST31, 0xc, 0xf, false);
+  return v;
+}
+
 // CSR offset of node j relative to the wave range start, clamped into int32.
 __device__ __forceinline__ int32_t rel_clamp(int64_t raw, int64_t wb) {
   const int64_t v = raw - wb;  // any range is < 2^28 (reduce_range)
@@ -637,6 +648,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       for (int64_t e = threadIdx.x; e < W * W; e += KCC_NODE_PREP_BLOCK) c_l[e] = 0ull;
   }
   __syncthreads();  // masks zero
+  KCC_TL(blockIdx.x % 1024, 6);
   if (lds) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -647,16 +659,27 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
     }
   }
   __syncthreads();  // masks complete
-  if (lds) {  // the prefix counts: row g along Y and column Y = g along G, lane = index
-    for (int g = wv; g < 64; g += KCC_NODE_PREP_BLOCK / 64) {
-      const uint64_t c1 = (uint64_t)__popcll(mk_l[mk_at(g, lane)]);
-      const uint64_t i1 = wave_incl_scan_u64(c1);
-      ck_l[g * 65 + lane] = (uint8_t)(i1 - c1);
-      if (lane == 63) ck_l[g * 65 + 64] = (uint8_t)i1;
-      const uint64_t c2 = (uint64_t)__popcll(mk_l[mk_at(lane, g)]);
-      const uint64_t i2 = wave_incl_scan_u64(c2);
-      cj_l[g * 65 + lane] = (uint8_t)(i2 - c2);
-      if (lane == 63) cj_l[g * 65 + 64] = (uint8_t)i2;
+  KCC_TL(blockIdx.x % 1024, 7);
+  if (lds) {  // the prefix counts: row g along Y and column Y = g along G, lane = index;
+    // rows g and g + 16 in one 32-bit scan of four byte fields (each count and prefix is
+    // a member count of one x-group or y-block, <= 64: no carries between the bytes)
+    static_assert(KCC_NODE_PREP_BLOCK == 1024, "16 waves: rows wv, wv + 16, wv + 32, wv + 48");
+    for (int g = wv; g < 64; g += 32) {
+      const uint32_t pk = (uint32_t)__popcll(mk_l[mk_at(g, lane)]) |
+                          (uint32_t)__popcll(mk_l[mk_at(lane, g)]) << 8 |
+                          (uint32_t)__popcll(mk_l[mk_at(g + 16, lane)]) << 16 |
+                          (uint32_t)__popcll(mk_l[mk_at(lane, g + 16)]) << 24;
+      const uint32_t inc = wave_incl_scan_u32(pk), exc = inc - pk;
+      ck_l[g * 65 + lane] = (uint8_t)exc;
+      cj_l[g * 65 + lane] = (uint8_t)(exc >> 8);
+      ck_l[(g + 16) * 65 + lane] = (uint8_t)(exc >> 16);
+      cj_l[(g + 16) * 65 + lane] = (uint8_t)(exc >> 24);
+      if (lane == 63) {
+        ck_l[g * 65 + 64] = (uint8_t)inc;
+        cj_l[g * 65 + 64] = (uint8_t)(inc >> 8);
+        ck_l[(g + 16) * 65 + 64] = (uint8_t)(inc >> 16);
+        cj_l[(g + 16) * 65 + 64] = (uint8_t)(inc >> 24);
+      }
     }
   }
   // a C cell: the workgroup's LDS copy (an explicit LDS pointer: through the lambda the

@@ -75,6 +75,9 @@ def show(label, rows, k0, k1):
 
 
 show("node_prep entry -> prologue done", npr, 2, 0)
+show("  entry -> table loads in LDS", npr, 2, 6)
+show("  member masks (LDS atomics)", npr, 6, 7)
+show("  prefix counts", npr, 7, 0)
 show("node_prep pass loads + phase 1", npr, 0, 3)
 show("node_prep phase 2 (+barrier)", npr, 3, 4)
 show("node_prep stream + records (+barrier)", npr, 4, 5)
