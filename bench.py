@@ -349,9 +349,11 @@ def main():
         out["roofline"] = dict(out["roofline_reduce"], kernel="reduce_kernel<2>",
                                note="dominant kernel of the step (reduce vs fit time per step); "
                                     "the fit's: roofline_fit / roofline_valu")
-    else:
-        out["roofline"] = dict(out["roofline_fit"],
-                               note="dominant kernel of the step; VALU-bound: roofline_valu")
+    else:  # the fit dominates (C5's 16384 specs): its bound is VALU issue, not HBM
+        out["roofline"] = dict(out["roofline_valu"], traffic=fit_traffic,
+                               note="dominant kernel of the step; VALU issue-bound (no MFMA or HBM "
+                                    "bound applies: 3 VALU per node and 64-spec wave); the HBM "
+                                    "view: roofline_fit")
     if args.emulate_world > 1:
         out["emulated_world"] = args.emulate_world
 
