@@ -110,9 +110,43 @@ def relaunch(args) -> int:
     return subprocess.call(cmd)
 
 
+# per-rank timings every N > 1 line carries (rank_stats): the step, each rank's reduce and
+# fit launches, its all-reduce of the partials, and its reduce's HBM roofline fraction
+RANK_KEYS = ("step_ms", "reduce_ms", "fit_ms", "allreduce_ms", "reduce_frac")
+
+
+def rank_stats(dist, world, local, device=None):
+    """Gather every rank's RANK_KEYS values (one all_gather of a float64 vector; None ->
+    NaN -> null) and summarise them: the slowest and fastest rank's step (value uses the
+    slowest), the mean all-reduce time, and the per-rank lists."""
+    import torch
+
+    vec = torch.tensor([float("nan") if local.get(k) is None else float(local[k])
+                        for k in RANK_KEYS], dtype=torch.float64, device=device)
+    if world > 1:
+        bufs = [torch.empty_like(vec) for _ in range(world)]
+        dist.all_gather(bufs, vec)
+        rows = [b.cpu().tolist() for b in bufs]
+    else:
+        rows = [vec.cpu().tolist()]
+    per = {k: [None if r[i] != r[i] else r[i] for r in rows] for i, k in enumerate(RANK_KEYS)}
+    steps = [v for v in per["step_ms"] if v is not None]
+    ar = [v for v in per["allreduce_ms"] if v is not None]
+    return {
+        "step_ms_max": max(steps) if steps else None,
+        "step_ms_min": min(steps) if steps else None,
+        "allreduce_ms": sum(ar) / len(ar) if ar else None,
+        "per_rank": per,
+        "note": "step_ms: each rank's own timed steps (value uses the max); reduce_ms / fit_ms "
+                "/ allreduce_ms: per launch, HIP events on the kernels' stream in the profiled "
+                "steps; reduce_frac: that rank's reduce_kernel at algorithmic bytes / 8 TB/s",
+    }
+
+
 def dry_run(args, rank, world):
     """The launcher path without a GPU: every rank joins a gloo group and all-reduces
-    its rank id; rank 0 reports how many ranks answered."""
+    its rank id; rank 0 reports how many ranks answered, and the per-rank table an N > 1
+    line carries is gathered over the same group (placeholder values, no measurement)."""
     import torch
     import torch.distributed as dist
 
@@ -121,12 +155,17 @@ def dry_run(args, rank, world):
         t = torch.tensor([1, rank], dtype=torch.int64)
         dist.all_reduce(t)
         seen, rank_sum = int(t[0]), int(t[1])
-        dist.destroy_process_group()
     else:
         seen, rank_sum = 1, 0
+    ranks = rank_stats(dist, world, {"step_ms": 1.0 + rank, "reduce_ms": None, "fit_ms": None,
+                                     "allreduce_ms": 0.5 if world > 1 else None,
+                                     "reduce_frac": None})
+    if world > 1:
+        dist.destroy_process_group()
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": seen, "gpus_requested": args.gpus,
-                          "rank_sum": rank_sum, "scaling": args.scaling, "config": args.config}))
+                          "rank_sum": rank_sum, "scaling": args.scaling, "config": args.config,
+                          "ranks": ranks}))
     return 0 if seen == args.gpus else 2
 
 
@@ -209,16 +248,25 @@ def main():
 
     h_ptr = np.ascontiguousarray(cl.node_ptr, np.int64)
 
-    def step():
-        # reduce -> spec setup -> node prep -> fit -> clamp correction, one stream
+    ar_events = []  # profiled steps: HIP event pairs around the all-reduce (its stream)
+
+    def step(prof=False):
+        # reduce + spec ranks -> node prep + spec placement -> fit -> clamp correction,
+        # one stream
         eng.capacity_partial_async(h_ptr, ptr, cpu, mem, a_cpu, a_mem, a_pods, p_cnt, used_cpu,
                                    used_mem, s_cpu, s_mem, partial, n_chunks=args.chunks,
                                    stream=stream)
         if world > 1:
+            if prof:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record(stream)
             if exchange == "kcc":  # RCCL on the same stream: no cross-stream event
                 eng.allreduce_partial_async(S, partial, stream=stream)
             else:
                 dist.all_reduce(partial, op=dist.ReduceOp.SUM)
+            if prof:
+                ev[1].record(stream)
+                ar_events.append(ev)
         eng.fit_finalize_async(S, partial, totals, err, stream=stream)
 
     with torch.cuda.stream(stream):
@@ -242,11 +290,13 @@ def main():
         if args.kernel_events == "after":
             eng.profile_enable(True)
             for _ in range(args.steps):
-                step()
+                step(prof=True)
             torch.cuda.synchronize()
     red_ms_tot, red_launches, fit_ms_tot, fit_launches = eng.profile_read()
     eng.profile_enable(False)
+    ar_ms = (sum(a.elapsed_time(b) for a, b in ar_events) / len(ar_events)) if ar_events else None
     elapsed = t_end - t_start
+    own_ms_step = elapsed / args.steps * 1e3  # this rank's own timed steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -356,6 +406,14 @@ def main():
                                     "view: roofline_fit")
     if args.emulate_world > 1:
         out["emulated_world"] = args.emulate_world
+    # every rank's own numbers (N > 1: who is slowest, and what the exchange costs)
+    out["ranks"] = rank_stats(dist, world, {"step_ms": own_ms_step, "reduce_ms": red_ms,
+                                            "fit_ms": fit_ms, "allreduce_ms": ar_ms,
+                                            "reduce_frac": red_gbs / HBM_PEAK_GBS},
+                              device=dev if args.dist_backend == "nccl" else None)
+    out["allreduce_ms"] = out["ranks"]["allreduce_ms"]
+    faults = eng.reduce_faults()
+    out["reduce_lookback_faults"] = faults  # 0 on a healthy device (else sums are wrong)
 
     # order-independent fingerprint of the per-spec totals: identical for every N
     tot_np = totals.cpu().numpy().view(np.uint64)
@@ -706,8 +764,13 @@ def host_cpus():
                     break
     except OSError:
         pass
+    note = ("all of this process's CPUs" if threads == aff else
+            f"the box's CPU share for this GPU job: OMP_NUM_THREADS={omp} (the GPU box sets it "
+            f"to the slot's CPUs); the {aff} CPUs of the affinity mask / nproc belong to the "
+            "whole host, shared with the other GPU slots, and the harness asks jobs to size "
+            "their worker pools to the share — so every core this job owns is used")
     return {"threads": threads, "nproc": os.cpu_count(), "affinity_cpus": aff,
-            "omp_num_threads": omp or None, "cpu_model": model}
+            "omp_num_threads": omp or None, "cpu_model": model, "core_budget": note}
 
 
 def h2d_leg(arrays, dev, step_ms, evals):

@@ -51,6 +51,9 @@ typedef struct kcc_ctx kcc_ctx;
 
 /* Library / ABI version (KCC_ABI_VERSION). */
 int kcc_abi_version(void);
+/* Build flavour: "release" for the product library; an experiment build (csrc/Makefile
+ * `variant`, its own .so) returns "variant" plus the knobs it was compiled with. */
+const char* kcc_build_info(void);
 
 /* Create a context on `n_gpus` devices starting at `first_device`.
  * n_gpus == 1: one device.  n_gpus > 1: nodes are sharded in contiguous ranges
@@ -214,6 +217,13 @@ int kcc_allreduce_partial_async(kcc_ctx* ctx, int64_t n_specs, int64_t* d_partia
 int kcc_profile_enable(kcc_ctx* ctx, int on);
 int kcc_profile_read(kcc_ctx* ctx, double* reduce_ms, int64_t* reduce_launches, double* fit_ms,
                      int64_t* fit_launches);
+
+/* Look-back waits of the segmented reduce that gave up (summed over the context's
+ * devices since creation; synchronises).  A reduce launch assembles a node cut by wave
+ * ranges from pieces the other waves publish; a wait that never sees its piece (not
+ * expected on a healthy device) is counted here instead of hanging, and the affected
+ * node's sums are then wrong.  Tests and the bench assert 0. */
+int kcc_reduce_faults(kcc_ctx* ctx, int64_t* faults);
 
 /* The fit streams only the node rows that can add to its fast sum (free CPU, free
  * memory and allocatable pods > 0, within the fast bounds): every other row contributes

@@ -29,6 +29,7 @@ _i64, _i32, _int, _vp, _dbl = C.c_int64, C.c_int32, C.c_int, C.c_void_p, C.c_dou
 # symbol -> (restype, argtypes); pointers are passed as c_void_p
 SIGNATURES = {
     "kcc_abi_version": (_int, []),
+    "kcc_build_info": (C.c_char_p, []),
     "kcc_create": (_int, [C.POINTER(_vp), _int, _int]),
     "kcc_destroy": (None, [_vp]),
     "kcc_last_error": (C.c_char_p, [_vp]),
@@ -48,6 +49,7 @@ SIGNATURES = {
     "kcc_set_node_shards": (_int, [_vp, _int]),
     "kcc_set_fit_dense": (_int, [_vp, _int]),
     "kcc_fit_stream_rows": (_int, [_vp, C.POINTER(_i64)]),
+    "kcc_reduce_faults": (_int, [_vp, C.POINTER(_i64)]),
     "kcc_comm_unique_id": (_int, [_vp]),
     "kcc_comm_init": (_int, [_vp, _vp, _int, _int]),
     "kcc_allreduce_partial_async": (_int, [_vp, _i64, _vp, _vp]),

@@ -58,7 +58,11 @@ struct Dev {
   double prof_ms[2] = {0.0, 0.0};
   int64_t prof_n[2] = {0, 0};
   // workspace of the *_async entry points
-  DevBuf wave_node, fast_a, fast_b, slow, slow_list, srec, sperm, counters;
+  DevBuf fast_a, fast_b, slow, slow_list, srec, sperm, counters;
+  // the reduce's per-wave tail records (look-back), zeroed when allocated; each reduce
+  // launch tags its records with a new epoch.  faults: look-back waits that timed out.
+  DevBuf red_tail, red_faults;
+  uint64_t red_epoch = 0;
   DevBuf fit_q;          // the fit's per-column work queues (zero between launches)
   bool fitq_dirty = true;
   // spec setup + clamp correction (kcc::ClampWork)
@@ -95,6 +99,12 @@ struct kcc_ctx {
   int node_shards = 0;  // host-array entry points: node shards (0 = one per device)
   std::string err;
   double slow_frac = -1.0;
+  // kcc_fit / kcc_capacity: each shard's counters, copied into pinned host memory on the
+  // shard's stream (pageable copies could block the host between devices) and summed
+  // after the final synchronisation: exact-path pairs and streamed rows of every shard
+  unsigned long long* host_cnt = nullptr;
+  size_t host_cnt_n = 0;
+  int64_t host_stream_rows = -1;  // streamed rows of the last host-array fit (-1: none)
 };
 
 namespace {
@@ -160,6 +170,27 @@ int h2d(kcc_ctx* ctx, Dev& dv, DevBuf& buf, const T* src, int64_t count) {
 
 // ---- device-level pipeline pieces (no host sync, no allocation beyond growth) ----
 
+// The reduce's look-back workspace: tail records for every wave a launch may have, and
+// the fault counter, zeroed when (re)allocated — synchronously: a stale tag equal to a
+// later epoch would hand a wave a piece that was never published (allocation happens
+// only when the workspace grows; kcc_reserve does it ahead of any capture).
+int reduce_ws(kcc_ctx* ctx, Dev& dv, hipStream_t s) {
+  const size_t tb = sizeof(uint64_t) * kcc::RED_TAIL_WORDS * (size_t)kcc::reduce_tail_records();
+  bool fresh = false;
+  if (dv.red_tail.bytes < tb) {
+    KCC_HIP(ctx, ensure(dv.red_tail, tb));
+    KCC_HIP(ctx, hipMemsetAsync(dv.red_tail.p, 0, dv.red_tail.bytes, s));
+    fresh = true;
+  }
+  if (!dv.red_faults.p) {
+    KCC_HIP(ctx, ensure(dv.red_faults, 16));
+    KCC_HIP(ctx, hipMemsetAsync(dv.red_faults.p, 0, 16, s));
+    fresh = true;
+  }
+  if (fresh) KCC_HIP(ctx, hipStreamSynchronize(s));
+  return KCC_OK;
+}
+
 int reduce_async_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, const int64_t* ptr,
                      const uint64_t* cpu, const int64_t* mem, const uint64_t* cpul,
                      const int64_t* meml, uint64_t* used_cpu, int64_t* used_mem,
@@ -175,14 +206,12 @@ int reduce_async_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, con
     return fail(ctx, KCC_EINVAL, "limits need cpu_lim, mem_lim, lim_cpu and lim_mem");
   if (!aligned16(cpu) || !aligned16(mem) || (lim && (!aligned16(cpul) || !aligned16(meml))))
     return fail(ctx, KCC_EINVAL, "container arrays must be 16-byte aligned");
-  const int64_t waves = kcc::reduce_max_waves(n_cont);
-  KCC_HIP(ctx, ensure(dv.wave_node, sizeof(int64_t) * (size_t)(waves > 0 ? waves : 1)));
-  KCC_HIP(ctx, kcc::launch_reduce_mark(n_nodes, 0, n_cont, ptr, as<int64_t>(dv.wave_node), used_cpu,
-                                       used_mem, lim ? lim_cpu : nullptr,
-                                       lim ? lim_mem : nullptr, s));
+  int rc = reduce_ws(ctx, dv, s);
+  if (rc) return rc;
   KCC_HIP(ctx, kcc::launch_reduce(n_nodes, 0, n_cont, ptr, cpu, mem, lim ? cpul : nullptr,
-                                  lim ? meml : nullptr, as<int64_t>(dv.wave_node), used_cpu,
-                                  used_mem, lim ? lim_cpu : nullptr, lim ? lim_mem : nullptr, s));
+                                  lim ? meml : nullptr, used_cpu, used_mem, lim ? lim_cpu : nullptr,
+                                  lim ? lim_mem : nullptr, as<uint64_t>(dv.red_tail), ++dv.red_epoch,
+                                  as<unsigned long long>(dv.red_faults), s));
   return KCC_OK;
 }
 
@@ -197,8 +226,11 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, hipSetDevice(dv.device));
   const size_t N = (size_t)(n_nodes > 0 ? n_nodes : 1);
   const size_t S = (size_t)(n_specs > 0 ? n_specs : 1);
-  const int64_t waves = kcc::reduce_max_waves(n_cont > 0 ? n_cont : 1);
-  KCC_HIP(ctx, ensure(dv.wave_node, sizeof(int64_t) * (size_t)waves));
+  (void)n_cont;  // the reduce's workspace does not depend on the container count
+  {
+    int rc = reduce_ws(ctx, dv, dv.stream);
+    if (rc) return rc;
+  }
   KCC_HIP(ctx, ensure(dv.fast_a, sizeof(kcc::FitGroupA) * (size_t)kcc::fit_groups((int64_t)N)));
   KCC_HIP(ctx, ensure(dv.fast_b, sizeof(kcc::FitGroup) * (size_t)kcc::fit_groups((int64_t)N)));
   KCC_HIP(ctx, ensure(dv.slow, sizeof(kcc::SlowNode) * N));
@@ -281,11 +313,18 @@ kcc::ClampWork clamp_of(Dev& dv) {
   return cw;
 }
 
+kcc::PlaceArgs place_args(Dev& dv, int64_t n_specs, const uint64_t* spec_cpu,
+                          const int64_t* spec_mem, int64_t* partial) {
+  return kcc::PlaceArgs{n_specs, spec_cpu, spec_mem, spec_prep_of(dv), clamp_of(dv), partial,
+                        as<unsigned long long>(dv.counters), 0};
+}
+
 int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* alloc_cpu,
                     const int64_t* alloc_mem, const int64_t* alloc_pods,
                     const int64_t* pod_count, const uint64_t* used_cpu,
                     const int64_t* used_mem, int64_t n_specs, const uint64_t* spec_cpu,
                     const int64_t* spec_mem, int64_t* partial, hipStream_t s) {
+  ctx->host_stream_rows = -1;  // (kcc_fit_stream_rows: this call's device counters)
   if (n_nodes < 0 || n_specs < 0) return fail(ctx, KCC_EINVAL, "negative size");
   if (n_specs >= kcc::MAX_SPECS) return fail(ctx, KCC_EINVAL, "too many specs (max 2^26 - 1)");
   if (n_specs > 0 && (!spec_cpu || !spec_mem || !partial))
@@ -301,19 +340,26 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
   rc = clamp_clean(ctx, dv, s);
   if (rc) return rc;
   dv.clamp_dirty = true;  // until every kernel that leaves the tables zero is queued
-  // spec_prep also zeroes `partial` and the counters (no memset launches)
-  KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv), clamp_of(dv),
-                                     partial, as<unsigned long long>(dv.counters), s));
+  // spec_rank zeroes the counters and the coarse clamp table; spec_place zeroes
+  // `partial` (no memset launches).  spec_place rides in the node_prep launch when
+  // node_prep builds its tables from the ranks (S <= CLAMP_LDS_SPECS)
+  KCC_HIP(ctx, kcc::launch_spec_rank(kcc::rank_args(n_specs, spec_cpu, spec_mem, clamp_of(dv),
+                                                    as<unsigned long long>(dv.counters)),
+                                     s));
+  const kcc::PlaceArgs pa = place_args(dv, n_specs, spec_cpu, spec_mem, partial);
+  const bool fuse_place = n_specs <= kcc::CLAMP_LDS_SPECS;
+  if (!fuse_place) KCC_HIP(ctx, kcc::launch_spec_place(pa, s));
+  if (n_nodes > 0 || fuse_place)
+    KCC_HIP(ctx, kcc::launch_node_prep(n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count,
+                                       used_cpu, used_mem, as<kcc::FitGroupA>(dv.fast_a),
+                                       as<kcc::FitGroup>(dv.fast_b), as<kcc::SlowNode>(dv.slow),
+                                       as<int64_t>(dv.slow_list), n_specs, spec_cpu, spec_mem,
+                                       clamp_of(dv), as<unsigned long long>(dv.counters), 0, 0,
+                                       n_nodes, s, dv.fit_dense, fuse_place ? &pa : nullptr));
   if (n_nodes == 0) {
     dv.clamp_dirty = false;
     return KCC_OK;
   }
-  KCC_HIP(ctx, kcc::launch_node_prep(n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count,
-                                     used_cpu, used_mem, as<kcc::FitGroupA>(dv.fast_a),
-                                     as<kcc::FitGroup>(dv.fast_b), as<kcc::SlowNode>(dv.slow),
-                                     as<int64_t>(dv.slow_list), n_specs, clamp_of(dv),
-                                     as<unsigned long long>(dv.counters), 0, 0, n_nodes, s,
-                                     dv.fit_dense));
   dv.stream_chunks = 1;
   KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, n_nodes, clamp_of(dv),
                                        as<unsigned long long>(dv.counters), partial, s));
@@ -409,6 +455,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                          const int64_t* alloc_pods, const int64_t* pod_count, uint64_t* used_cpu,
                          int64_t* used_mem, int64_t n_specs, const uint64_t* spec_cpu,
                          const int64_t* spec_mem, int64_t* partial, int n_chunks, hipStream_t s) {
+  ctx->host_stream_rows = -1;  // (kcc_fit_stream_rows: this call's device counters)
   if (n_nodes < 0 || n_cont < 0 || n_specs < 0) return fail(ctx, KCC_EINVAL, "negative size");
   if (n_nodes >= kcc::RED_MAX_NODES)
     return fail(ctx, KCC_EINVAL, "too many nodes per device (max 2^28 - 1)");
@@ -453,26 +500,23 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     KCC_HIP(ctx, hipEventRecord(dv.ev_fork, s));
     KCC_HIP(ctx, hipStreamWaitEvent(dv.side, dv.ev_fork, 0));
   }
-  // k == 1: the reduce's mark runs as extra workgroups of the first spec-setup launch
-  // (same stream, independent work: one launch fewer on the step)
-  // k == 1: the reduce's mark runs as extra workgroups of the spec-rank launch, and
-  // spec_place as extra workgroups of the reduce launch (same stream, independent work:
-  // two launches fewer on the step); the reduce leaves spec_place's wave slots free
-  const bool fuse = k == 1 && n_specs > 0 && n_nodes > 0;
-  kcc::PlaceArgs pa{};
-  if (fuse)
-    pa = kcc::PlaceArgs{n_specs, spec_cpu, spec_mem, spec_prep_of(dv), clamp_of(dv), partial,
-                        as<unsigned long long>(dv.counters), kcc::place_blocks(n_specs)};
-  const int64_t reserve = (int64_t)kcc::RED_WAVES_PER_BLOCK * pa.n_blocks;
-  if (n_specs > 0) {  // spec partition on s (concurrent with the first reduce when k > 1)
+  // k == 1: the spec ranks ride in the reduce launch (extra workgroups in front of the
+  // reduce's: independent work) and spec_place in the node_prep launch (node_prep builds
+  // its tables from the ranks; S <= CLAMP_LDS_SPECS): four launches per call — reduce +
+  // rank, node_prep + place, fit, clamp_apply
+  const bool fuse_place = n_specs > 0 && n_specs <= kcc::CLAMP_LDS_SPECS;
+  const bool fuse_rank = k == 1 && n_specs > 0 && n_nodes > 0 && n_cont > 0;
+  const kcc::RankArgs ra = kcc::rank_args(n_specs, spec_cpu, spec_mem, clamp_of(dv),
+                                          as<unsigned long long>(dv.counters));
+  const kcc::PlaceArgs pa = place_args(dv, n_specs, spec_cpu, spec_mem, partial);
+  if (n_specs > 0) {
     rc = clamp_clean(ctx, dv, s);
     if (rc) return rc;
     dv.clamp_dirty = true;  // until every kernel that leaves the tables zero is queued
-    const kcc::MarkArgs ma = kcc::mark_args(n_nodes, 0, n_cont, ptr, as<int64_t>(dv.wave_node),
-                                            used_cpu, used_mem, nullptr, nullptr, reserve);
-    KCC_HIP(ctx, kcc::launch_spec_prep(n_specs, spec_cpu, spec_mem, spec_prep_of(dv),
-                                       clamp_of(dv), partial, as<unsigned long long>(dv.counters),
-                                       s, fuse ? &ma : nullptr, !fuse));
+    if (!fuse_rank) {
+      KCC_HIP(ctx, kcc::launch_spec_rank(ra, s));
+      if (!fuse_place) KCC_HIP(ctx, kcc::launch_spec_place(pa, s));
+    }
   }
   for (int c = 0; c < k; ++c) {
     const int64_t n = hi[c] - lo[c];
@@ -482,13 +526,11 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
       KCC_HIP(ctx, prof_event(dv, &pp.b));
       KCC_HIP(ctx, hipEventRecord(pp.a, rs));
     }
-    if (!fuse)
-      KCC_HIP(ctx, kcc::launch_reduce_mark(n, c0[c], c1[c] - c0[c], ptr + lo[c],
-                                           as<int64_t>(dv.wave_node), used_cpu + lo[c],
-                                           used_mem + lo[c], nullptr, nullptr, rs));
-    KCC_HIP(ctx, kcc::launch_reduce(n, c0[c], c1[c] - c0[c], ptr + lo[c], cpu, mem, nullptr,
-                                    nullptr, as<int64_t>(dv.wave_node), used_cpu + lo[c],
-                                    used_mem + lo[c], nullptr, nullptr, rs, fuse ? &pa : nullptr));
+    KCC_HIP(ctx, kcc::launch_reduce(n, c0[c], c1[c] - c0[c], ptr + lo[c], cpu, mem, nullptr, nullptr,
+                                    used_cpu + lo[c], used_mem + lo[c], nullptr, nullptr,
+                                    as<uint64_t>(dv.red_tail), ++dv.red_epoch,
+                                    as<unsigned long long>(dv.red_faults), rs,
+                                    fuse_rank ? &ra : nullptr));
     if (dv.prof_on) {
       KCC_HIP(ctx, hipEventRecord(pp.b, rs));
       pp.kind = 0;
@@ -496,18 +538,22 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     }
     if (k > 1) KCC_HIP(ctx, hipEventRecord(dv.ev_red[c], dv.side));
   }
+  if (fuse_rank && !fuse_place) KCC_HIP(ctx, kcc::launch_spec_place(pa, s));
   for (int c = 0; c < k; ++c) {
     if (k > 1) KCC_HIP(ctx, hipStreamWaitEvent(s, dv.ev_red[c], 0));  // also joins the side stream
     const int64_t n = hi[c] - lo[c];
-    if (n_specs == 0 || n == 0) continue;
+    const bool place_here = fuse_place && c == 0;
+    if (n_specs == 0 || (n == 0 && !place_here)) continue;
     KCC_HIP(ctx, kcc::launch_node_prep(n, alloc_cpu + lo[c], alloc_mem + lo[c], alloc_pods + lo[c],
                                        pod_count + lo[c], used_cpu + lo[c], used_mem + lo[c],
                                        as<kcc::FitGroupA>(dv.fast_a) + lo[c] / kcc::FIT_GROUP,
                                        as<kcc::FitGroup>(dv.fast_b) + lo[c] / kcc::FIT_GROUP,
                                        as<kcc::SlowNode>(dv.slow) + lo[c],
-                                       as<int64_t>(dv.slow_list) + lo[c], n_specs, clamp_of(dv),
-                                       as<unsigned long long>(dv.counters), c, lo[c], n_nodes, s,
-                                       dv.fit_dense));
+                                       as<int64_t>(dv.slow_list) + lo[c], n_specs, spec_cpu,
+                                       spec_mem, clamp_of(dv), as<unsigned long long>(dv.counters),
+                                       c, lo[c], n_nodes, s, dv.fit_dense,
+                                       place_here ? &pa : nullptr));
+    if (n == 0) continue;
     ProfPair pp{};
     if (dv.prof_on) {
       KCC_HIP(ctx, prof_event(dv, &pp.a));
@@ -568,7 +614,15 @@ int run_host(kcc_ctx* ctx, bool with_reduce, int64_t n_nodes, int64_t n_cont,
   std::vector<int64_t> lo, hi;
   shard_nodes(n_nodes, ns, lo, hi);
   std::vector<std::vector<int64_t>> rebased(ns);  // per shard: copies may still be in flight
-  std::vector<unsigned long long> shard_slow(ns, 0ull);
+  if (ctx->host_cnt_n < (size_t)ns * kcc::CNT_N) {
+    if (ctx->host_cnt) (void)hipHostFree(ctx->host_cnt);
+    ctx->host_cnt = nullptr;
+    ctx->host_cnt_n = 0;
+    KCC_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->host_cnt),
+                               sizeof(unsigned long long) * (size_t)ns * kcc::CNT_N, hipHostMallocDefault));
+    ctx->host_cnt_n = (size_t)ns * kcc::CNT_N;
+  }
+  ctx->host_stream_rows = -1;
   for (int d = 0; d < nd; ++d) {
     Dev& dv = ctx->devs[d];
     KCC_HIP(ctx, hipSetDevice(dv.device));
@@ -613,8 +667,9 @@ int run_host(kcc_ctx* ctx, bool with_reduce, int64_t n_nodes, int64_t n_cont,
                          as<uint64_t>(dv.spec_cpu), as<int64_t>(dv.spec_mem), part, dv.stream);
     if (rc) return rc;
     // exact-path pair count of this shard (the next shard's spec setup zeroes it)
-    KCC_HIP(ctx, hipMemcpyAsync(&shard_slow[sh], dv.counters.p, sizeof(unsigned long long),
-                                hipMemcpyDeviceToHost, dv.stream));
+    KCC_HIP(ctx, hipMemcpyAsync(ctx->host_cnt + (size_t)sh * kcc::CNT_N, dv.counters.p,
+                                sizeof(unsigned long long) * kcc::CNT_N, hipMemcpyDeviceToHost,
+                                dv.stream));
     if (sh >= nd)  // fold this slot into the device's slot 0 (wrapping int64 adds)
       KCC_HIP(ctx, kcc::launch_partial_add(2 * n_specs, as<int64_t>(dv.partial), part, dv.stream));
   }
@@ -644,7 +699,12 @@ int run_host(kcc_ctx* ctx, bool with_reduce, int64_t n_nodes, int64_t n_cont,
     KCC_HIP(ctx, hipSetDevice(dv.device));
     KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
   }
-  for (int sh = 0; sh < ns; ++sh) slow_pairs += shard_slow[sh];
+  int64_t streamed = 0;
+  for (int sh = 0; sh < ns; ++sh) {
+    slow_pairs += ctx->host_cnt[(size_t)sh * kcc::CNT_N + kcc::CNT_SLOW_PAIRS];
+    streamed += (int64_t)ctx->host_cnt[(size_t)sh * kcc::CNT_N + kcc::CNT_STREAM];
+  }
+  ctx->host_stream_rows = streamed;
   const double pairs = (double)n_nodes * (double)n_specs;
   ctx->slow_frac = pairs > 0 ? (double)slow_pairs / pairs : 0.0;
   return KCC_OK;
@@ -655,6 +715,14 @@ int run_host(kcc_ctx* ctx, bool with_reduce, int64_t n_nodes, int64_t n_cont,
 extern "C" {
 
 int kcc_abi_version(void) { return KCC_ABI_VERSION; }
+
+// The knobs an experiment build was compiled with (csrc/Makefile `variant` passes them in
+// KCC_VARIANT_FLAGS); the release library takes none (the Makefile refuses EXTRA there).
+#ifdef KCC_VARIANT_BUILD
+const char* kcc_build_info(void) { return "variant: " KCC_VARIANT_FLAGS; }
+#else
+const char* kcc_build_info(void) { return "release"; }
+#endif
 
 const char* kcc_create_error(void) { return g_create_error.c_str(); }
 
@@ -732,7 +800,7 @@ void kcc_destroy(kcc_ctx* ctx) {
     DevBuf* bufs[] = {&dv.c_rank, &dv.c_bcnt, &dv.c_cs, &dv.c_ms,
                       &dv.c_mrc, &dv.c_crm, &dv.c_dperm, &dv.c_C, &dv.c_H2, &dv.c_H3,
                       &dv.c_Crow, &dv.c_rec, &dv.c_dir,
-                      &dv.wave_node, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
+                      &dv.red_tail,  &dv.red_faults, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
                       &dv.sperm,     &dv.fit_q,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
                       &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,
@@ -759,6 +827,7 @@ void kcc_destroy(kcc_ctx* ctx) {
     }
     for (hipEvent_t ev : dv.prof_free) (void)hipEventDestroy(ev);
   }
+  if (ctx->host_cnt) (void)hipHostFree(ctx->host_cnt);
   delete ctx;
 }
 
@@ -993,6 +1062,10 @@ int kcc_set_fit_dense(kcc_ctx* ctx, int dense) {
 
 int kcc_fit_stream_rows(kcc_ctx* ctx, int64_t* streamed) {
   if (!ctx || !streamed) return ctx ? fail(ctx, KCC_EINVAL, "NULL output") : KCC_EINVAL;
+  if (ctx->host_stream_rows >= 0) {  // the last fit was kcc_fit / kcc_capacity: every shard
+    *streamed = ctx->host_stream_rows;
+    return KCC_OK;
+  }
   Dev& dv = ctx->devs[0];
   KCC_HIP(ctx, hipSetDevice(dv.device));
   KCC_HIP(ctx, hipDeviceSynchronize());
@@ -1002,6 +1075,21 @@ int kcc_fit_stream_rows(kcc_ctx* ctx, int64_t* streamed) {
   int64_t t = 0;
   for (int k = 0; k < dv.stream_chunks && k < kcc::FIT_MAX_CHUNKS; ++k) t += (int64_t)c[kcc::CNT_STREAM + k];
   *streamed = t;
+  return KCC_OK;
+}
+
+int kcc_reduce_faults(kcc_ctx* ctx, int64_t* faults) {
+  if (!ctx || !faults) return ctx ? fail(ctx, KCC_EINVAL, "NULL output") : KCC_EINVAL;
+  int64_t t = 0;
+  for (Dev& dv : ctx->devs) {
+    if (!dv.red_faults.p) continue;
+    KCC_HIP(ctx, hipSetDevice(dv.device));
+    KCC_HIP(ctx, hipDeviceSynchronize());
+    unsigned long long f = 0;
+    KCC_HIP(ctx, hipMemcpy(&f, dv.red_faults.p, sizeof(f), hipMemcpyDeviceToHost));
+    t += (int64_t)f;
+  }
+  *faults = t;
   return KCC_OK;
 }
 

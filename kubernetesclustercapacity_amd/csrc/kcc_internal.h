@@ -4,13 +4,28 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Diagnostic timing knobs produce wrong results by design (no stores, no atomics,
+// searches skipped) or add stamp stores: only experiment builds (csrc/Makefile `variant`,
+// which defines KCC_VARIANT_BUILD and writes a separate .so) may set them.
+#if !defined(KCC_VARIANT_BUILD) &&                                                       \
+    (defined(KCC_FIT_DIAG_NO_ATOMICS) || defined(KCC_DIAG_RED_NOSTORE) ||                \
+     defined(KCC_DIAG_RED_LOADONLY) || defined(KCC_DIAG_NP) || defined(KCC_DIAG_CP) ||   \
+     defined(KCC_TIMELINE))
+#error "a diagnostic KCC_* knob in a release build: use `make variant` (KCC_VARIANT_BUILD)"
+#endif
+
 namespace kcc {
 
-struct PlaceArgs;  // below: spec_place's work, fused into a reduce launch
+struct RankArgs;   // below: spec ranks, run as extra workgroups of a reduce launch
 
 // ---- (a) segmented request reduce -------------------------------------------
 // One wavefront owns a contiguous range of reduce_range() containers and walks it in
 // tiles of RED_TILE (RED_IPL containers per lane: two 16-B loads per lane per array).
+// The launch is self-contained (no marking pass, no zeroing, no atomics): a wave finds
+// the node owning its first container by a 64-ary search of the CSR offsets, stores
+// every node that ends inside its range, and a node cut by range boundaries is
+// assembled by the wave where it ends from the pieces its predecessors publish
+// (decoupled look-back over per-wave tail records, tagged with the launch's epoch).
 #ifndef KCC_RED_ROUNDS
 #define KCC_RED_ROUNDS 1  // waves = this many rounds of the resident wave capacity
 #endif
@@ -22,54 +37,48 @@ constexpr int RED_TILE = 64 * RED_IPL;  // 256
 constexpr int RED_WAVES_PER_BLOCK = 4;
 // the reduce stores through 32-bit buffer offsets (8 B per node, < 2^31)
 constexpr int64_t RED_MAX_NODES = (int64_t)1 << 28;
+// per-wave tail record: the NA values of the node open at the range end, then the tag
+constexpr int RED_TAIL_WORDS = 8;  // 64 B: one line per wave
+constexpr int RED_TAIL_TAG = 7;
 
 // Containers per wave range: whole tiles, sized so the waves fill the device's resident
 // wave slots (occupancy API) in KCC_RED_ROUNDS rounds: one round of equal, long ranges
 // leaves no half-empty second round (9672 waves of 4096 containers at C4 ran 1.6 rounds
 // of 6144 resident waves).  Small inputs get one tile per wave.  `limits` selects the
-// 4-array kernel (more registers, fewer resident waves).  Both reduce launches of a call
-// use the same range.
-// reserve_waves: resident wave slots left to other work of the same launch (spec_place
-// workgroups in front of the reduce's)
+// 4-array kernel (more registers, fewer resident waves).
+// reserve_waves: resident wave slots left to other work of the same launch (the spec
+// rank workgroups in front of the reduce's)
 int32_t reduce_range(int64_t n_containers, bool limits, int64_t reserve_waves = 0);
 inline int64_t reduce_n_waves(int64_t n_containers, bool limits, int64_t reserve_waves = 0) {
   const int64_t r = reduce_range(n_containers, limits, reserve_waves);
   return (n_containers + r - 1) / r;
 }
-// workspace bound for wave_node (shortest range)
-inline int64_t reduce_max_waves(int64_t n_containers) {
-  return (n_containers + RED_TILE - 1) / RED_TILE + 1;
-}
+// tail records a launch may need: an upper bound of reduce_n_waves (one range per
+// resident wave slot at most)
+int64_t reduce_tail_records();
 
-// Both reduce launches cover nodes [0, n_nodes) of `node_ptr` (the caller offsets
-// node_ptr and the per-node outputs for a node range) and containers [c0, c0 +
-// n_containers): the offsets in node_ptr and the container arrays stay absolute, so a
-// node range of one CSR is reduced without rebasing anything.
-// Zeroes the per-node outputs and records, for every wave range, the node that owns
-// the range's first container (wave_node[n_waves]).
-struct MarkArgs {
+// One reduce launch: nodes [0, n_nodes) of `ptr` (the caller offsets ptr and the
+// per-node outputs for a node range) and containers [c0, c_end); the offsets in ptr and
+// the container arrays stay absolute (ptr[0] == c0), so a node range of one CSR is
+// reduced without rebasing anything.  Every output of [0, n_nodes) is written.
+struct RedArgs {
   int64_t n_nodes, c0, c_end;
   int32_t range;
   const int64_t* ptr;
-  int64_t* wave_node;
-  uint64_t *o0, *o1, *o2, *o3;
+  const uint64_t* in[4];
+  uint64_t* out[4];
+  uint64_t* tail;                  // [reduce_tail_records()][RED_TAIL_WORDS]
+  uint64_t epoch;                  // this launch's tag (never 0, never reused)
+  unsigned long long* faults;      // look-back waits that timed out (stays 0)
 };
-MarkArgs mark_args(int64_t n_nodes, int64_t c0, int64_t n_containers, const int64_t* node_ptr,
-                   int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu,
-                   int64_t* lim_mem, int64_t reserve_waves = 0);
-hipError_t launch_reduce_mark(int64_t n_nodes, int64_t c0, int64_t n_containers,
-                              const int64_t* node_ptr, int64_t* wave_node, uint64_t* used_cpu,
-                              int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s);
-
-// place != nullptr (with place->n_blocks > 0): spec_place runs as that many extra
-// workgroups of this launch (the mark must then have been computed with the same
-// reserve_waves = 4 * n_blocks).
+// rank != nullptr (with rank->n_blocks > 0): the spec ranks run as that many extra
+// workgroups in front of the reduce's (independent work, one launch fewer per step).
 hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, const int64_t* node_ptr,
                          const uint64_t* cpu_req, const int64_t* mem_req,
                          const uint64_t* cpu_lim, const int64_t* mem_lim,
-                         const int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem,
-                         uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s,
-                         const PlaceArgs* place = nullptr);
+                         uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem,
+                         uint64_t* tail, uint64_t epoch, unsigned long long* faults, hipStream_t s,
+                         const RankArgs* rank = nullptr);
 
 // ---- (b) fit -----------------------------------------------------------------
 // Node streams of the fit kernel: groups of FIT_GROUP nodes, field-major inside the
@@ -151,7 +160,8 @@ struct SpecPrep {
 // one copy per XCD, H2/H3 two (node_prep's atomics spread over more cache lines); every
 // copy is zero between calls: clamp_prep zeroes what it reads.
 struct ClampWork {
-  uint32_t* rank;    // [2S] by caller index: x-rank, y-rank (zero between calls)
+  uint32_t* rank;    // [rank_slices(S)][2][S] by caller index: each slice's share of the
+                     // x-rank and the y-rank (plain stores; a rank is the sum over slices)
   uint32_t* bcnt;    // [ceil(S/64)][2] class A / class B specs per block of 64 (caller order)
   uint64_t* cs;      // [S] normal specs' cpu requests by x-rank (ascending)
   int64_t* ms;       // [S] memory requests by y-rank (ascending)
@@ -226,8 +236,35 @@ inline int64_t clamp_passes(int64_t n_nodes) {
 #endif
 constexpr int64_t CLAMP_LDS_SPECS = KCC_CLAMP_LDS_SPECS;
 
-// spec_place's work (one thread per spec), run as extra workgroups in front of a reduce
-// launch (launch_reduce with a PlaceArgs) or as a launch of its own
+// Spec ranks (spec_rank): the x-rank by (c, index) and the y-rank by (m, index) of every
+// normal spec, counted by brute force in slices of RANK_L candidates (a workgroup: 64
+// queries x one slice, staged in LDS); each slice stores its counts (no atomics, nothing
+// to zero), a consumer sums rank_slices(S) of them.  The first slice of each block of 64
+// queries also stores the block's class-A / class-B counts (bcnt).  The rank workgroups
+// also zero the counters (all but CNT_SPECS_A / CNT_SPECS_B, set by spec_place) and the
+// coarse clamp table's cells: the first launch of a step, ahead of every reader.
+constexpr int64_t RANK_L = 1024;  // candidates per slice: 16 KiB of 16-B keys in LDS
+__host__ __device__ inline int64_t rank_slices(int64_t S) { return (S + RANK_L - 1) / RANK_L; }
+struct RankArgs {
+  int64_t S;
+  const uint64_t* c_in;
+  const int64_t* m_in;
+  uint32_t* part;      // ClampWork::rank
+  uint32_t* bcnt;      // ClampWork::bcnt
+  int64_t* C;          // ClampWork::C: cells [0, c_cells) of each copy are zeroed
+  int64_t c_stride, c_cells;
+  unsigned long long* counters;
+  int32_t n_blocks;    // 256-thread workgroups: ceil(S / 64) x rank_slices(S) (0: none)
+};
+RankArgs rank_args(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
+                   const ClampWork& cw, unsigned long long* counters);
+hipError_t launch_spec_rank(const RankArgs& ra, hipStream_t s);
+
+// spec_place's work (one thread per spec), run as extra workgroups in front of a
+// node_prep launch (S <= CLAMP_LDS_SPECS: node_prep builds its tables from the ranks) or
+// as a launch of its own (ahead of node_prep, which then reads cs / ms / mr_c / cr_m):
+// the stable 3-way partition position, the SpecRec / perm there, the clamp correction's
+// arrays (cs, ms, mr_c, cr_m, dperm), partial[0..2S) zeroed, CNT_SPECS_A / CNT_SPECS_B set.
 struct PlaceArgs {
   int64_t S;
   const uint64_t* c_in;
@@ -236,36 +273,25 @@ struct PlaceArgs {
   ClampWork cw;
   int64_t* partial;
   unsigned long long* counters;
-  int32_t n_blocks;  // 256-thread workgroups (0: none)
+  int32_t n_blocks;  // workgroups of the launch's block size (0: none)
 };
-inline int32_t place_blocks(int64_t S) { return (int32_t)((S + 255) / 256); }
+hipError_t launch_spec_place(const PlaceArgs& pa, hipStream_t s);
+
 
 // counters (CNT_*): exact-path (node, spec) pairs, class-B specs, and per node chunk
 // of a pipelined call (kcc_capacity_partial_async) the rows in that chunk's slow_list.
-// spec_prep zeroes partial[0..2S) and the counters; node_prep appends to slow_list.
+// spec_rank zeroes the counters, spec_place sets the class counts and zeroes
+// partial[0..2S); node_prep appends to slow_list and the fit streams.
 constexpr int FIT_MAX_CHUNKS = 16;
 enum {
   CNT_SLOW_PAIRS = 0,  // (node, spec) pairs evaluated on the exact path
   CNT_SPECS_A = 1,     // class-A specs (internal positions [0, nA))
   CNT_SPECS_B = 2,     // class-B specs (internal positions [nA, nA + nB))
-  CNT_SPARE = 3,
+  CNT_SPARE = 3,       // (unused)
   CNT_SLOW_ROWS = 4,   // + chunk: rows in that node chunk's slow_list
   CNT_STREAM = 4 + FIT_MAX_CHUNKS,  // + chunk: node rows in that chunk's fit stream (x 8)
   CNT_N = 4 + 2 * FIT_MAX_CHUNKS
 };
-// Spec setup, two launches.  spec_rank: brute-force x-ranks by (c, index) and y-ranks by
-// (m, index) (64 queries per workgroup, the candidates split over workgroups and waves,
-// atomics into rank[]) and the class counts per block of 64 specs.  spec_place (one
-// thread per spec): the stable 3-way partition position, the SpecRec / perm there and the
-// clamp correction's arrays (cs, ms, mr_c, cr_m, dperm); zeroes partial[0..2S), rank[] and
-// the call's cells of C, sets the counters.
-// mark != nullptr: the first launch also runs launch_reduce_mark's work for those args
-// (extra workgroups), so the caller skips launch_reduce_mark.
-// with_place = false: the caller runs spec_place inside its reduce launch (PlaceArgs).
-hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu,
-                            const int64_t* spec_mem, SpecPrep sp, ClampWork cw, int64_t* partial,
-                            unsigned long long* counters, hipStream_t s,
-                            const MarkArgs* mark = nullptr, bool with_place = true);
 // The clamp correction after every node_prep of the call (n_nodes: the call's rows, for
 // the binned records' pass count): partial[s] -= D_s for the normal specs of clamp-free
 // waves; leaves the table copies zero.
@@ -280,13 +306,18 @@ hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
 // round-1 layout's cost: zero fields for the rows that add nothing).  row0: the launch's
 // first row within the call (a multiple of CLAMP_PASS_ROWS_MAX; the binned records'
 // passes), call_nodes: the call's rows (its pass size, clamp_pass_rows).
+// Needs the spec ranks (and, for S > CLAMP_LDS_SPECS, spec_place's arrays) on the stream
+// before it.  place != nullptr (S <= CLAMP_LDS_SPECS only): spec_place runs as extra
+// workgroups of this launch (place->n_blocks is set here).
 hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
-                            SlowNode* slow, int64_t* slow_list, int64_t n_specs, ClampWork cw,
+                            SlowNode* slow, int64_t* slow_list, int64_t n_specs,
+                            const uint64_t* spec_cpu, const int64_t* spec_mem, ClampWork cw,
                             unsigned long long* counters, int chunk, int64_t row0,
-                            int64_t call_nodes, hipStream_t s, bool dense = false);
+                            int64_t call_nodes, hipStream_t s, bool dense = false,
+                            const PlaceArgs* place = nullptr);
 
 // partial[0..S) += Σ_i q(i,s), partial[S..2S) += #div-by-zero rows (internal order).
 hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,

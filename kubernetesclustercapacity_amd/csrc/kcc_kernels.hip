@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "kcc_internal.h"
 
 namespace kcc {
@@ -47,38 +49,6 @@ __device__ __forceinline__ unsigned long long atomic_add_u64(uint64_t* p, uint64
 // (a) segmented reduce
 // ----------------------------------------------------------------------------
 
-// For every wave range [c0 + x*range, ...) record the node owning its first container,
-// and zero the outputs of the nodes the reduce does not store plainly: those a range
-// boundary cuts (each wave adds its part with an atomic) and the empty nodes ahead of the
-// launch's first container.  Every other node is stored whole by the wave where it ends
-// (block flushes of reduce_kernel).  Node indices are local to the launch (ptr and the
-// outputs are offset by the caller); the container offsets in ptr are absolute and the
-// launch covers containers [c0, c_end).
-__device__ __forceinline__ void reduce_mark_body(int64_t blk, int64_t nblk, const MarkArgs& a) {
-  const int64_t n_nodes = a.n_nodes, c0 = a.c0, c_end = a.c_end;
-  const int32_t range = a.range;
-  const int64_t stride = nblk * blockDim.x;
-  for (int64_t j = blk * blockDim.x + threadIdx.x; j < n_nodes; j += stride) {
-    int64_t b = a.ptr[j] - c0, e = a.ptr[j + 1] - c0;  // relative to the launch's first container
-    b = b < 0 ? 0 : b;
-    e = e > c_end - c0 ? c_end - c0 : e;
-    bool zero = e <= 0;  // empty and ahead of every container (all nodes, when none)
-    if (e > b) {
-      for (int64_t x = (b + range - 1) / range * range; x < e; x += range)
-        a.wave_node[x / range] = j;
-      zero = (b / range + 1) * range < e;  // a range boundary strictly inside (b, e)
-    }
-    if (zero) {
-      a.o0[j] = 0;
-      a.o1[j] = 0;
-      if (a.o2) a.o2[j] = 0;
-      if (a.o3) a.o3[j] = 0;
-    }
-  }
-}
-
-__global__ void reduce_mark_kernel(MarkArgs a) { reduce_mark_body(blockIdx.x, gridDim.x, a); }
-
 // DPP controls (gfx9 family): row_shr:n, row_bcast:15/31, wave_shr:1.
 constexpr int DPP_ROW_SHR = 0x110;
 constexpr int DPP_ROW_BCAST15 = 0x142;
@@ -105,6 +75,15 @@ __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
   return v;
 }
 
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return (uint64_t)hi << 32 | lo;
+}
+__device__ __forceinline__ int64_t readlane_i64(int64_t v, int l) {
+  return (int64_t)readlane_u64((uint64_t)v, l);
+}
+
 // 32-bit version (every lane sum below 2^32; also packed fields that never carry)
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
   v += __builtin_amdgcn_update_dpp(0u, v, DPP_ROW_SHR + 1, 0xf, 0xf, false);
@@ -114,6 +93,41 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
   v += __builtin_amdgcn_update_dpp(0u, v, DPP_ROW_BCAST15, 0xa, 0xf, false);
   v += __builtin_amdgcn_update_dpp(0u, v, DPP_ROW_BCAST31, 0xc, 0xf, false);
   return v;
+}
+
+// Two inclusive 64-bit prefix sums over the 64 lanes at once (wrapping): per DPP step one
+// v_add_co_u32_dpp + v_addc_co_u32_dpp per value (the neighbour's operand read through
+// DPP; out-of-row lanes read 0 (bound_ctrl), rows masked off keep their value), the two
+// scans interleaved so every DPP read is >= 2 wait states after the write it reads.
+// 12 VALU per value instead of 30 (zeroed DPP move targets, moves, 64-bit add).
+#ifndef KCC_RED_ASM_SCAN
+#define KCC_RED_ASM_SCAN 0
+#endif
+#define KCC_SCAN2_STEP(ctl)                                 \
+  "v_add_co_u32_dpp %0, vcc, %0, %0 " ctl "\n\t"            \
+  "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc " ctl "\n\t"      \
+  "v_add_co_u32_dpp %2, vcc, %2, %2 " ctl "\n\t"            \
+  "v_addc_co_u32_dpp %3, vcc, %3, %3, vcc " ctl "\n\t"
+__device__ __forceinline__ void wave_incl_scan2_u64(uint64_t& a, uint64_t& b) {
+#if KCC_RED_ASM_SCAN
+  uint32_t al = (uint32_t)a, ah = (uint32_t)(a >> 32), bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
+  asm volatile("s_nop 1\n\t"
+               KCC_SCAN2_STEP("row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0")
+               KCC_SCAN2_STEP("row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:0")
+               KCC_SCAN2_STEP("row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:0")
+               KCC_SCAN2_STEP("row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:0")
+               KCC_SCAN2_STEP("row_bcast:15 row_mask:0xa bank_mask:0xf")
+               KCC_SCAN2_STEP("row_bcast:31 row_mask:0xc bank_mask:0xf")
+               "s_nop 1"
+               : "+v"(al), "+v"(ah), "+v"(bl), "+v"(bh)
+               :
+               : "vcc");
+  a = (uint64_t)ah << 32 | al;
+  b = (uint64_t)bh << 32 | bl;
+#else
+  a = wave_incl_scan_u64(a);
+  b = wave_incl_scan_u64(b);
+#endif
 }
 
 // CSR offset of node j relative to the wave range start, clamped into int32.
@@ -156,6 +170,9 @@ __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff
 
 // One wavefront walks a contiguous range of `range` containers in tiles of
 // RED_TILE = 256 (4 per lane, coalesced SoA buffer loads, next tile prefetched).
+// Start: the node owning the range's first container (the last node whose CSR offset is
+// <= it) by a 64-ary search of the offsets — one wave-wide load per level (3 levels at
+// 125k nodes, 4 at 1M), issued after the first tiles' data loads, whose latency it hides.
 // Per tile and array:
 //   1. the tile-local inclusive prefix sum of the 256 values: a 4-item running sum per
 //      lane, one DPP inclusive scan (64-bit, all VALU) of the lane totals, written to
@@ -174,48 +191,59 @@ __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff
 //   3. the sums stay in registers (res, one per lane = per node of the block) and a
 //      completed block is written with ONE coalesced 512-B store per array: stores
 //      count in vmcnt like loads, so a store per tile would put its completion latency
-//      in front of the next tile's data wait.  Only the (at most two) nodes crossing
-//      the range boundaries use 64-bit atomics.
-// Nodes before the wave's first owned node and the empty nodes ahead of node0 are
-// zeroed by reduce_mark_kernel; every other node of the wave's run, empty ones
-// included, is written by its flush.
+//      in front of the next tile's data wait.
+// End: every node that ends in the range is stored by this wave (empty ones included;
+// wave 0 starts at node 0, so the empty nodes ahead of the first container too), except
+// node0 when it began in an earlier range: the wave publishes its tail record (the
+// piece of the node open at its range end, `carry`) and then, if node0 began earlier and
+// ended here, sums the tail records of the waves from the one holding node0's first
+// container up to its own and stores node0 (decoupled look-back: each wave publishes
+// before it waits, so waits never chain; a wave waits only for lower-indexed waves,
+// dispatched before it).  No atomics, nothing to zero between launches.
 constexpr uint32_t RED_OOB_OFFSET = 0x7ffffff0u;  // > any output's range (n_nodes < 2^28)
+constexpr uint32_t RED_SPIN_MAX = 1u << 18;       // look-back polls before a wait gives up
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+__device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds);
 __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk);
+
+// The wave's sum of a 64-bit value (wrapping), wave-uniform.
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+  v = wave_incl_scan_u64(v);
+  return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), 63) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, 63);
+}
 
 template <int NA>
 __global__ __launch_bounds__(256)
 #ifdef KCC_RED_WAVES_PER_EU
-__attribute__((amdgpu_waves_per_eu(KCC_RED_WAVES_PER_EU)))
+__attribute__((amdgpu_waves_per_eu(NA == 2 ? KCC_RED_WAVES_PER_EU : 1)))
 #endif
-void reduce_kernel(
-    int64_t n_nodes, int64_t c0, int64_t n_cont, int32_t range, const int64_t* __restrict__ ptr,
-    const uint64_t* __restrict__ in0, const uint64_t* __restrict__ in1,
-    const uint64_t* __restrict__ in2, const uint64_t* __restrict__ in3,
-    const int64_t* __restrict__ wave_node, uint64_t* __restrict__ out0,
-    uint64_t* __restrict__ out1, uint64_t* __restrict__ out2, uint64_t* __restrict__ out3,
-    PlaceArgs pa) {
+void reduce_kernel(RedArgs a, RankArgs ra) {
   __shared__ __attribute__((aligned(16))) uint64_t pre_s[RED_WAVES_PER_BLOCK][NA][RED_TILE];
-  if ((int32_t)blockIdx.x < pa.n_blocks) {  // spec_place's workgroups, in front
-    spec_place_body(pa, blockIdx.x);
+  static_assert(sizeof(pre_s) >= 16 * RANK_L, "the rank workgroups stage RANK_L 16-B keys");
+  if ((int32_t)blockIdx.x < ra.n_blocks) {  // the spec ranks' workgroups, in front
+    spec_rank_body(ra, blockIdx.x, &pre_s[0][0][0]);
     return;
   }
   const int lane = threadIdx.x & 63;
+  const int64_t n_nodes = a.n_nodes, c0 = a.c0, n_cont = a.c_end;
+  const int32_t range = a.range;
+  const int64_t* __restrict__ ptr = a.ptr;
   // wave index made provably uniform (T20: no waterfall loops around the buffer ops)
-  const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)((blockIdx.x - pa.n_blocks) *
+  const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)((blockIdx.x - ra.n_blocks) *
                                                              RED_WAVES_PER_BLOCK +
                                                              (threadIdx.x >> 6)));
   // containers [c0, n_cont): absolute indices, like the offsets in ptr (node indices
   // are local to the launch)
   const int64_t wb = c0 + (int64_t)w * range;
   if (wb >= n_cont) return;  // wave-uniform; no block-level barrier in this kernel
-  KCC_TL(4096 + (blockIdx.x - pa.n_blocks) % 4096, 0);
+  KCC_TL(4096 + (blockIdx.x - ra.n_blocks) % 4096, 0);
   const int32_t len = (int32_t)(n_cont - wb < range ? n_cont - wb : range);
   __builtin_assume(len >= 1);  // (wb < n_cont: the tile loop runs, its first loads need no guard)
   uint64_t (*pre)[RED_TILE] = pre_s[threadIdx.x >> 6];
-  const uint64_t* in[4] = {in0, in1, in2, in3};
-  uint64_t* out[4] = {out0, out1, out2, out3};
+  const uint64_t* in[4] = {a.in[0], a.in[1], a.in[2], a.in[3]};
+  uint64_t* out[4] = {a.out[0], a.out[1], a.out[2], a.out[3]};
   __amdgpu_buffer_rsrc_t rs[NA];
 #pragma unroll
   for (int k = 0; k < NA; ++k)  // whole 16-B pairs only: an odd last item is fixed up below
@@ -224,25 +252,41 @@ void reduce_kernel(
   // a ring of KCC_RED_PREFETCH + 1 tiles in registers: KCC_RED_PREFETCH in flight while
   // one is reduced (static ring indices: the tile loop below is unrolled over the ring).
   // The first tiles' loads go out first: they depend on the range alone, while the node
-  // lookups below are a chain of dependent loads (wave_node, then ptr)
+  // search below is a chain of dependent loads
   constexpr int RING = KCC_RED_PREFETCH + 1;
   uint64_t xs[RING][NA][4];
-#ifndef KCC_RED_LATE_PREFETCH
 #pragma unroll
   for (int u = 0; u < KCC_RED_PREFETCH; ++u)
 #pragma unroll
     for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 32, u * RED_TILE * 8, xs[u][k]);
-  __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink them below the lookups)
-#endif
+  __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink them below the search)
 
-  const int64_t node0 = wave_node[w];
-  const bool first_open = ptr[node0] < wb;           // node0 began in an earlier range
-  const int64_t own_lo = node0 + (first_open ? 1 : 0);  // first node stored plainly
+  // node0: the last node j < n_nodes with ptr[j] <= wb (ptr[0] == c0 <= wb; wave 0 takes
+  // node 0 itself, so the empty nodes ahead of the first container are its to store).
+  // Invariant: ptr[lo] <= wb, and hi == n_nodes or ptr[hi] > wb.
+  int64_t node0 = 0, p0 = c0;  // p0 = ptr[node0]
+  if (w > 0) {
+    int64_t lo = 0, hi = n_nodes;
+    while (hi - lo > 1) {
+      const int64_t step = (hi - lo + 63) >> 6;
+      const int64_t idx = lo + (int64_t)lane * step;
+      const int64_t v = idx < hi ? ptr[idx] : INT64_MAX;
+      const unsigned long long bl = __ballot(v <= wb);  // lane 0 (idx = lo) always
+      const int h = 63 - __builtin_clzll(bl);
+      p0 = readlane_i64(v, h);
+      lo += (int64_t)h * step;
+      hi = lo + step < hi ? lo + step : hi;
+    }
+    node0 = lo;
+  }
+  const bool first_open = p0 < wb;                      // node0 began in an earlier range
+  const int64_t own_lo = node0 + (first_open ? 1 : 0);  // first node stored by the flushes
   int64_t cur = node0;  // node holding the current tile's first item
   uint64_t carry[NA];   // node cur's running sum over the earlier tiles of this range
   uint64_t res[NA];     // sums of block blk's nodes (lane l <-> node 64*blk + l)
+  uint64_t head[NA];    // node0's piece in this range, when first_open (wave-uniform)
 #pragma unroll
-  for (int k = 0; k < NA; ++k) carry[k] = res[k] = 0;
+  for (int k = 0; k < NA; ++k) carry[k] = res[k] = head[k] = 0;
 
   int64_t blk = node0 >> 6;
   int32_t eA = rel_ptr(ptr, 64 * blk + 1 + lane, n_nodes, wb);  // end of node 64*blk + l
@@ -283,13 +327,6 @@ void reduce_kernel(
     pend = false;
   };
 
-#ifdef KCC_RED_LATE_PREFETCH  // (A/B: the round-1 order, after the node lookups)
-#pragma unroll
-  for (int u = 0; u < KCC_RED_PREFETCH; ++u)
-#pragma unroll
-    for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 32, u * RED_TILE * 8, xs[u][k]);
-#endif
-
   auto tile = [&](uint64_t (&x)[NA][4], uint64_t (&nx)[NA][4], const int32_t tb) {
 #ifndef KCC_DIAG_RED_NOSTORE
     issue_pending();
@@ -302,29 +339,33 @@ void reduce_kernel(
     for (int k = 0; k < NA; ++k) carry[k] += x[k][0] + x[k][1] + x[k][2] + x[k][3];
     return;
 #endif
-    const int32_t p0 = tb + 4 * lane;  // relative position of this lane's first item
-    if ((len & 1) && p0 <= len - 1 && len - 1 < p0 + 4) {  // odd tail: last item alone
+    const int32_t p0l = tb + 4 * lane;  // relative position of this lane's first item
+    if ((len & 1) && p0l <= len - 1 && len - 1 < p0l + 4) {  // odd tail: last item alone
 #pragma unroll
       for (int k = 0; k < NA; ++k) {
         const uint64_t v = in[k][wb + len - 1];
 #pragma unroll
         for (int i = 0; i < 4; ++i)  // static indices only (no scratch)
-          if (p0 + i == len - 1) x[k][i] = v;
+          if (p0l + i == len - 1) x[k][i] = v;
       }
     }
 
     // --- 1. tile-local inclusive prefix sums -> LDS -----------------------------
-    uint64_t tot[NA];
+    // the lane's 4-item total, scanned in place; the lane's items' prefixes then walk
+    // back from it (x0 is dead once the total is formed: fewer live registers)
+    uint64_t tot[NA], P[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) P[k] = x[k][0] + x[k][1] + x[k][2] + x[k][3];
+#pragma unroll
+    for (int k = 0; k < NA; k += 2) wave_incl_scan2_u64(P[k], P[k + 1]);
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
-      const uint64_t q0 = x[k][0], q1 = q0 + x[k][1], q2 = q1 + x[k][2], q3 = q2 + x[k][3];
-      const uint64_t P = wave_incl_scan_u64(q3);
-      const uint64_t ex = P - q3;
+      const uint64_t p2 = P[k] - x[k][3], p1 = p2 - x[k][2], p0 = p1 - x[k][1];
       u64x2* dst = reinterpret_cast<u64x2*>(&pre[k][4 * lane]);
-      dst[0] = u64x2{ex + q0, ex + q1};
-      dst[1] = u64x2{ex + q2, P};
-      tot[k] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(P >> 32), 63) << 32) |
-               (uint32_t)__builtin_amdgcn_readlane((uint32_t)P, 63);
+      dst[0] = u64x2{p0, p1};
+      dst[1] = u64x2{p2, P[k]};
+      tot[k] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(P[k] >> 32), 63) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((uint32_t)P[k], 63);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -346,12 +387,15 @@ void reduce_kernel(
             const uint64_t startp = s > tb ? pre[k][s - 1 - tb] : (0ull - carry[k]);
             sum = pre[k][eA - 1 - tb] - startp;
           }
-          if (j == node0 && first_open) atomic_add_u64(&out[k][j], sum);
           res[k] = sum;
         }
       }
       const unsigned long long bal = __ballot(act);
       if (!bal) break;
+      if (first_open && cur == node0 && ((bal >> (node0 & 63)) & 1ull)) {  // node0 ends here
+#pragma unroll
+        for (int k = 0; k < NA; ++k) head[k] = readlane_u64(res[k], (int)(node0 & 63));
+      }
       const int hi = 63 - __builtin_clzll(bal);  // the run is lanes [cur - 64*blk, hi]
       last_end = __builtin_amdgcn_readlane(eA, hi);
       cur = 64 * blk + hi + 1;
@@ -405,13 +449,52 @@ void reduce_kernel(
 #endif
     }
   }
-  // the node open at the end of the range continues into the next wave's range
-  if (wb + len < n_cont && lane == 0 && cur < n_nodes) {
+  // publish: node cur continues into the next range; its piece here is `carry` (the
+  // values with agent-scope (sc1) stores, drained, then the tag, as a separate store)
+  uint64_t* const rec = a.tail + (int64_t)w * RED_TAIL_WORDS;
+  if (wb + len < n_cont) {
+    if (lane < NA) {
+      uint64_t v = carry[0];
 #pragma unroll
-    for (int k = 0; k < NA; ++k)
-      if (carry[k] != 0) atomic_add_u64(&out[k][cur], carry[k]);
+      for (int k = 1; k < NA; ++k) v = lane == k ? carry[k] : v;
+      __hip_atomic_store(rec + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(rec + RED_TAIL_TAG, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  KCC_TL(4096 + (blockIdx.x - pa.n_blocks) % 4096, 1);
+  // look-back: node0 began in an earlier range and ended in this one
+  if (first_open && cur > node0) {
+    uint64_t acc[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) acc[k] = head[k];
+    const int64_t ws = (p0 - c0) / range;  // the wave holding node0's first container
+    for (int64_t b0 = ws; b0 < w; b0 += 64) {
+      const int64_t wi = b0 + lane;
+      uint64_t v[NA];
+#pragma unroll
+      for (int k = 0; k < NA; ++k) v[k] = 0;
+      if (wi < w) {
+        const uint64_t* r = a.tail + wi * RED_TAIL_WORDS;
+        uint32_t spins = 0;
+        while (__hip_atomic_load(r + RED_TAIL_TAG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.epoch) {
+          if (++spins >= RED_SPIN_MAX) {  // never on a healthy device: count it, go on
+            atomicAdd(a.faults, 1ull);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+#pragma unroll
+        for (int k = 0; k < NA; ++k) v[k] = __hip_atomic_load(r + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int k = 0; k < NA; ++k) acc[k] += wave_sum_u64(v[k]);
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < NA; ++k) out[k][node0] = acc[k];
+    }
+  }
+  KCC_TL(4096 + (blockIdx.x - ra.n_blocks) % 4096, 1);
 }
 
 // ----------------------------------------------------------------------------
@@ -558,12 +641,19 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
                                  const int64_t* __restrict__ used_mem,
                                  FitGroupA* __restrict__ fast_a, FitGroup* __restrict__ fast_b,
                                  SlowNode* __restrict__ slow, int64_t* __restrict__ slow_list,
-                                 int64_t S, ClampWork cw, unsigned long long* __restrict__ counters,
-                                 int32_t chunk, int32_t dense, int64_t pass0) {
-  KCC_TL(blockIdx.x % 1024, 2);
+                                 int64_t S, const uint64_t* __restrict__ spec_cpu,
+                                 const int64_t* __restrict__ spec_mem, ClampWork cw,
+                                 unsigned long long* __restrict__ counters,
+                                 int32_t chunk, int32_t dense, int64_t pass0, PlaceArgs pa) {
+  if ((int32_t)blockIdx.x < pa.n_blocks) {  // spec_place's workgroups, in front (MODE 2)
+    spec_place_body(pa, blockIdx.x);
+    return;
+  }
+  const int32_t bid = (int32_t)blockIdx.x - pa.n_blocks, nbid = (int32_t)gridDim.x - pa.n_blocks;
+  KCC_TL(bid % 1024, 2);
   constexpr int64_t PR = (int64_t)KCC_NODE_PREP_BLOCK * SUB;  // rows per pass
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t stride = (int64_t)gridDim.x * PR;
+  const int64_t stride = (int64_t)nbid * PR;
   // one row's six values: the next sub-step's, loaded while the current one is worked on;
   // this workgroup's first ones go out before the table setup below (their latency hides
   // behind it)
@@ -581,23 +671,31 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       ld_pc = pod_count[i];
     }
   };
-  load_row((int64_t)blockIdx.x * PR + threadIdx.x);
+  load_row((int64_t)bid * PR + threadIdx.x);
   __shared__ uint32_t np_wc[KCC_NODE_PREP_BLOCK / 64];  // streamed rows per wave
   __shared__ uint64_t np_base;                          // this pass's stream position
   __shared__ uint32_t np_tot;
   __shared__ uint32_t np_bcnt[NP_BINS];                 // binned records per bin (this pass)
   __shared__ uint32_t np_bstart[NP_BINS];               // their exclusive prefix
-  const bool want_b = counters[CNT_SPECS_B] != 0;  // written by spec setup (same stream)
-  const int64_t nN = clamp_n_normal(counters);     // normal specs (clamp correction)
+  // the class counts from spec_rank's per-block counts (spec_place may run beside this
+  // launch): every wave sums them (one load per lane at S <= 4096)
+  uint64_t cls_n = 0;  // class A | class B << 32
+  {
+    const uint64_t* bc = reinterpret_cast<const uint64_t*>(cw.bcnt);
+    for (int64_t b = lane; b < (S + 63) / 64; b += 64) cls_n += bc[b];
+    cls_n = readlane_u64(wave_incl_scan_u64(cls_n), 63);
+  }
+  const bool want_b = (cls_n >> 32) != 0;                       // class-B specs exist
+  const int64_t nN = (int64_t)(uint32_t)cls_n + (int64_t)(cls_n >> 32);  // normal specs
   const bool slow_all = nN < S;                    // exact-path specs exist
   const int64_t T = (nN + 63) / 64, W = T + 2;
   // T <= CLAMP_BIN_T_MAX (always at S <= 4096: MODE 2 carries no table atomics)
   const bool binned = (MODE == 2 && KCC_CLAMP_BINNED) || clamp_binned(S);
   const int NB = (int)(2 * T);                     // bins: x-groups, then y-blocks
   // this workgroup's copies of the tables: workgroups are dealt round-robin over the XCDs
-  int64_t* Cc = cw.C + (int64_t)(blockIdx.x % C_COPIES) * cw.c_stride;
-  int64_t* H2c = cw.H2 + (int64_t)(blockIdx.x % H2_COPIES) * cw.h_stride;
-  int64_t* H3c = cw.H3 + (int64_t)(blockIdx.x % H2_COPIES) * cw.h_stride;
+  int64_t* Cc = cw.C + (int64_t)(bid % C_COPIES) * cw.c_stride;
+  int64_t* H2c = cw.H2 + (int64_t)(bid % H2_COPIES) * cw.h_stride;
+  int64_t* H3c = cw.H3 + (int64_t)(bid % H2_COPIES) * cw.h_stride;
   // in LDS when S <= CLAMP_LDS_SPECS: the sorted spec requests of the searches (c clamped
   // to 2^23 (> every U = fc / P, fc < 2^23) as u32, m as i64); the member tables of the
   // x-group / y-block counts: mk[g][Y] = bit set of the y-ranks in y-block Y of x-group g's
@@ -616,14 +714,50 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   // ends with the st - 1 requests of its bucket from memory), up to NP_ST_MAX
   constexpr bool srch = MODE >= 1;
   const uint32_t st = lds ? 1u : np_stride(S);
-  // smallest normal requests (rows below either dominate no spec); cs[0] >= 1
-  const uint32_t cmin = nN > 0 ? (cw.cs[0] < FAST_FC_MAX ? (uint32_t)cw.cs[0] : (uint32_t)FAST_FC_MAX)
-                               : 0xffffffffu;
-  const int64_t mmin = nN > 0 ? cw.ms[0] : INT64_MAX;
   for (int b = threadIdx.x; b < NP_BINS; b += KCC_NODE_PREP_BLOCK) np_bcnt[b] = 0;
   constexpr int PER = (int)(CLAMP_LDS_SPECS / KCC_NODE_PREP_BLOCK);
-  uint32_t yv[PER];  // y-rank of x-rank tid + 1024 u
-  if (srch) {
+  if (lds) {
+    // MODE 2: the tables straight from the spec ranks (spec_place, which writes the sorted
+    // arrays, may run beside this launch): every spec's (c, m, x, y) loaded first, the
+    // slots initialised to +inf / empty, then each normal spec scattered to its ranks' slots
+    uint64_t cv[PER];
+    int64_t mv[PER];
+    uint32_t xr[PER], yr[PER];
+    bool nv[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int64_t i = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
+      cv[u] = i < S ? spec_cpu[i] : 0;
+      mv[u] = i < S ? spec_mem[i] : 0;
+      xr[u] = yr[u] = 0;
+      if (i < S) {
+        for (int64_t sl = 0; sl < rank_slices(S); ++sl) {
+          xr[u] += cw.rank[(sl * 2 + 0) * S + i];
+          yr[u] += cw.rank[(sl * 2 + 1) * S + i];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int64_t k = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
+      cs_l[k] = 0xffffffffu;
+      ms_l[k] = INT64_MAX;
+      mk_l[k] = 0ull;
+      nv[u] = k < S && spec_class(cv[u], mv[u]) != SPEC_EXACT;
+    }
+    if (cpriv)
+      for (int64_t e = threadIdx.x; e < W * W; e += KCC_NODE_PREP_BLOCK) c_l[e] = 0ull;
+    __syncthreads();  // slots initialised
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      if (nv[u]) {
+        cs_l[np_slot(xr[u])] = cv[u] < FAST_FC_MAX ? (uint32_t)cv[u] : 0xffffffffu;
+        ms_l[np_slot(yr[u])] = mv[u];
+        __hip_atomic_fetch_or((lds_ull*)(mk_l + mk_at(xr[u] >> 6, yr[u] >> 6)), 1ull << (yr[u] & 63),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  } else if (srch) {
     // every load first, guarded by S (a kernel argument) rather than nN, so they travel
     // with the counters' load (one memory round trip); entries nN.. are masked after
     uint64_t cv[PER], mv[PER];
@@ -633,7 +767,6 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       const int64_t e = (k + 1) * st - 1;  // the sampled entry
       cv[u] = e < S ? cw.cs[e] : ~0ull;
       mv[u] = e < S ? (uint64_t)cw.ms[e] : (uint64_t)INT64_MAX;
-      yv[u] = lds && k < S ? cw.mr_c[k] : 0xffffffffu;
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -641,25 +774,17 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       const bool in = (k + 1) * st - 1 < nN;  // padded: +inf
       cs_l[np_slot((uint32_t)k)] = in && cv[u] < FAST_FC_MAX ? (uint32_t)cv[u] : 0xffffffffu;
       ms_l[np_slot((uint32_t)k)] = in ? (int64_t)mv[u] : INT64_MAX;
-      if (!in) yv[u] = 0xffffffffu;
-      if (lds) mk_l[k] = 0ull;  // 64 x 64 masks: one per spec slot
-    }
-    if (cpriv)
-      for (int64_t e = threadIdx.x; e < W * W; e += KCC_NODE_PREP_BLOCK) c_l[e] = 0ull;
-  }
-  __syncthreads();  // masks zero
-  KCC_TL(blockIdx.x % 1024, 6);
-  if (lds) {
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int64_t x = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
-      if (x < nN)
-        __hip_atomic_fetch_or((lds_ull*)(mk_l + mk_at((uint32_t)x >> 6, yv[u] >> 6)), 1ull << (yv[u] & 63),
-                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
-  __syncthreads();  // masks complete
-  KCC_TL(blockIdx.x % 1024, 7);
+  __syncthreads();  // search tables and masks complete
+  KCC_TL(bid % 1024, 7);
+  // smallest normal requests (rows below either dominate no spec): the tables' first
+  // entries (+inf when there are none; cs[0] >= 1)
+  // (MODE 1's LDS tables are sampled: the first entries from memory)
+  const uint32_t cmin = lds ? cs_l[np_slot(0u)]
+                            : (nN > 0 ? (cw.cs[0] < FAST_FC_MAX ? (uint32_t)cw.cs[0] : 0xffffffffu)
+                                      : 0xffffffffu);
+  const int64_t mmin = lds ? ms_l[np_slot(0u)] : (nN > 0 ? cw.ms[0] : INT64_MAX);
   if (lds) {  // the prefix counts: row g along Y and column Y = g along G, lane = index;
     // rows g and g + 16 in one 32-bit scan of four byte fields (each count and prefix is
     // a member count of one x-group or y-block, <= 64: no carries between the bytes)
@@ -689,11 +814,11 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
     else np_atomic(&Cc[cell], w);
   };
   __syncthreads();
-  KCC_TL(blockIdx.x % 1024, 0);
+  KCC_TL(bid % 1024, 0);
   // Passes of SUB x 1024 rows (thread t: rows i0 + t + 1024 q), one sub-step q after the
   // other; one stream position (a returning atomic on one word) and one bin scan per pass.
   // Workgroup-uniform trip count (the stream positions and the bins meet in LDS).
-  for (int64_t i0 = (int64_t)blockIdx.x * PR; i0 < n; i0 += stride) {
+  for (int64_t i0 = (int64_t)bid * PR; i0 < n; i0 += stride) {
     const int64_t pass = pass0 + i0 / PR;
     // kept to the pass's end: the stream entry of each sub-step's row (free memory < 2^50,
     // free cpu < 2^23 and P of a fast row, else 0), its ballots, the packed records
@@ -764,7 +889,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
           const uint32_t padded = (t_pass + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP;  // whole groups
           if (padded) base_ret = atomicAdd(&counters[CNT_STREAM + chunk], (unsigned long long)padded);
         }
-        KCC_TL(blockIdx.x % 1024, 3);
+        KCC_TL(bid % 1024, 3);
       }
       // phase 2: the clamp correction's cells and records, in steps without data-dependent
       // branches around the LDS reads: (a) weight and bounds, (b) the two binary searches,
@@ -866,7 +991,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       np_tot = t_pass;
     }
     __syncthreads();  // np_base, and every record's rank
-    KCC_TL(blockIdx.x % 1024, 4);
+    KCC_TL(bid % 1024, 4);
     if (binned && wv == 1) {
       // the bins' starts: runs of per bins per lane, a shuffle scan of the run totals;
       // the pass's directory row (starts + total) goes out here, the counters return to 0
@@ -930,7 +1055,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       if (threadIdx.x < pad) put(np_base + tot + threadIdx.x, 0ull, 0u, 0u);  // the last group's padding
     }
     __syncthreads();  // np_wc / np_base / np_bstart are rewritten by the next pass
-    KCC_TL(blockIdx.x % 1024, 5);
+    KCC_TL(bid % 1024, 5);
   }
   if (cpriv) {  // the private C into this workgroup's device copy: its non-zero cells
     for (int64_t e = threadIdx.x; e < W * W; e += KCC_NODE_PREP_BLOCK) {
@@ -938,7 +1063,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       if (v) np_atomic(&Cc[e], (int64_t)v);
     }
   }
-  KCC_TL(blockIdx.x % 1024, 1);
+  KCC_TL(bid % 1024, 1);
 }
 
 // Smallest f32 >= 1/v (1 <= v < 2^51, exact in f64).  1/v is first rounded to f64,
@@ -952,67 +1077,52 @@ __device__ __forceinline__ float recip_up_f32(uint64_t v) {
   return r;
 }
 
-__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
-  return (uint64_t)hi << 32 | lo;
-}
 
-// ---- spec setup: ranks by counting, then one thread per spec places it -------------
-constexpr int SPEC_BLOCK = 1024;
-constexpr int SPEC_NW = SPEC_BLOCK / 64;
-constexpr int64_t RANK_SLICE_MAX = 4096;  // candidates staged per workgroup (64 KiB)
+// ---- spec setup: ranks by counting (slices), then one thread per spec places it -----
 
-// Candidates per slice: a power of two <= 4096 (so a slice never straddles the 8192-spec
-// chunks of the keys' 13-bit index field), about S / 4 (>= 4 workgroups per query block).
-__host__ __device__ inline int64_t rank_slice(int64_t S) {
-  int64_t L = 64;
-  while (L < RANK_SLICE_MAX && 4 * L < S) L *= 2;
-  return L;
-}
-
-// spec_rank_kernel: ceil(S/64) query blocks x ceil(S/L) slices, workgroups of 1024 threads;
-// lane = query spec i (64 per workgroup), the L candidates of the slice staged in LDS as
-// keys v << 13 | (j mod 8192) (v = c or m < 2^51; non-normal specs ~0) and walked by the 16
-// waves with broadcast 16-B reads.  Per normal query (ties by index):
+// The rank of every normal spec in slices of RANK_L candidates: workgroup (qb, sl) of
+// ceil(S/64) x rank_slices(S), 256 threads; lane = query spec i = 64 qb + lane (the 4
+// waves hold the same 64 queries), the slice's candidates staged in LDS as 16-B keys
+// v << 13 | (j mod 8192) (v = c or m < 2^51; non-normal specs ~0), a quarter per wave,
+// read by broadcast.  Per normal query (ties by index):
 //   x(i) = #{normal j : (c_j, j) < (c_i, i)},   y(i) = #{normal j : (m_j, j) < (m_i, i)},
 // each slice counting keys below a threshold uniform over the slice: (v_i + 1) << 13 for
 // candidates in an earlier 8192-chunk than i (equal v sorts before), v_i << 13 | (i mod
-// 8192) in i's chunk, v_i << 13 in a later chunk.  The waves' counts meet in LDS, then one
-// atomic per query and rank into rank[] (zero between calls: spec_place zeroes what it
-// reads).  The first slice of a query block also stores the block's class-A / class-B
-// counts in bcnt[].  Workgroups from rank_blocks on run reduce_mark_body instead (the
-// reduce's mark fused into this launch: independent work, one launch fewer on the step).
-__global__ __launch_bounds__(SPEC_BLOCK) void spec_rank_kernel(int64_t S, const uint64_t* __restrict__ c_in,
-                                                               const int64_t* __restrict__ m_in,
-                                                               ClampWork cw, int64_t rank_blocks,
-                                                               MarkArgs mark) {
-  if ((int64_t)blockIdx.x >= rank_blocks) {  // workgroup-uniform, before any barrier
-    reduce_mark_body((int64_t)blockIdx.x - rank_blocks, (int64_t)gridDim.x - rank_blocks, mark);
-    return;
-  }
+// 8192) in i's chunk, v_i << 13 in a later chunk (RANK_L divides 8192: a slice never
+// straddles two chunks).  The waves' counts meet in LDS; wave 0 stores the slice's x count
+// and wave 1 its y count (plain stores: nothing to zero).  The first slice of a query block
+// stores its class-A / class-B counts in bcnt[].  The workgroups also zero the counters
+// (but the class counts, spec_place's) and the coarse clamp table's cells.  `lds`: 16 KiB.
+__device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds) {
+  const int64_t S = ra.S;
+  const uint64_t* __restrict__ c_in = ra.c_in;
+  const int64_t* __restrict__ m_in = ra.m_in;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  {  // zero duties, spread over the workgroups
+    const int64_t gt = blk * 256 + tid, nt = (int64_t)ra.n_blocks * 256;
+    if (gt < CNT_N && gt != CNT_SPECS_A && gt != CNT_SPECS_B) ra.counters[gt] = 0;
+    for (int64_t e = gt; e < C_COPIES * ra.c_cells; e += nt)
+      ra.C[(e / ra.c_cells) * ra.c_stride + e % ra.c_cells] = 0;
+  }
   typedef uint64_t u64x2_t __attribute__((ext_vector_type(2)));
-  __shared__ u64x2_t key_l[RANK_SLICE_MAX];
-  __shared__ uint32_t part[SPEC_NW][2][64];
-  const int64_t L = rank_slice(S), ns = (S + L - 1) / L;
-  const int64_t qb = blockIdx.x / ns, sl = blockIdx.x % ns;
+  u64x2_t* key_l = reinterpret_cast<u64x2_t*>(lds);
+  const int64_t ns = rank_slices(S);
+  const int64_t qb = blk / ns, sl = blk % ns;
   const int64_t i = qb * 64 + lane;  // this lane's query
   const bool qv = i < S;
   const uint64_t c = qv ? c_in[i] : 0;
   const int64_t m = qv ? m_in[i] : 0;
   const int32_t ci = qv ? spec_class(c, m) : SPEC_EXACT;
-  const bool qn = ci != SPEC_EXACT;
   if (sl == 0 && wv == 0) {  // this query block's class counts
     const uint32_t na = (uint32_t)__popcll(__ballot(ci == SPEC_A));
     const uint32_t nb = (uint32_t)__popcll(__ballot(ci == SPEC_B));
     if (lane == 0) {
-      cw.bcnt[2 * qb] = na;
-      cw.bcnt[2 * qb + 1] = nb;
+      ra.bcnt[2 * qb] = na;
+      ra.bcnt[2 * qb + 1] = nb;
     }
   }
-  const int64_t j0 = sl * L, j1 = j0 + L < S ? j0 + L : S;  // this slice
-  for (int64_t j = j0 + tid; j < j1; j += SPEC_BLOCK) {  // stage the slice's keys
+  const int64_t j0 = sl * RANK_L, j1 = j0 + RANK_L < S ? j0 + RANK_L : S;  // this slice
+  for (int64_t j = j0 + tid; j < j1; j += 256) {  // stage the slice's keys
     const uint64_t cj = c_in[j];
     const int64_t mj = m_in[j];
     const bool nj = spec_class(cj, mj) != SPEC_EXACT;
@@ -1027,7 +1137,7 @@ __global__ __launch_bounds__(SPEC_BLOCK) void spec_rank_kernel(int64_t S, const 
   const uint64_t tm = chs < chq ? ((uint64_t)m + 1) << 13
                                 : (chs == chq ? (uint64_t)m << 13 | (uint64_t)(i & 8191) : (uint64_t)m << 13);
   const int n = (int)(j1 - j0);
-  const int w0 = n * wv / SPEC_NW, w1 = n * (wv + 1) / SPEC_NW;  // this wave's part
+  const int w0 = n * wv / 4, w1 = n * (wv + 1) / 4;  // this wave's quarter
   uint32_t rc = 0, rm = 0;
 #pragma unroll 4
   for (int j = w0; j < w1; ++j) {
@@ -1035,24 +1145,37 @@ __global__ __launch_bounds__(SPEC_BLOCK) void spec_rank_kernel(int64_t S, const 
     rc += k.x < tc ? 1u : 0u;
     rm += k.y < tm ? 1u : 0u;
   }
-  part[wv][0][lane] = rc;
-  part[wv][1][lane] = rm;
+  __syncthreads();  // the keys are read: the area takes the waves' counts
+  uint32_t* part = reinterpret_cast<uint32_t*>(lds);
+  part[(wv * 2 + 0) * 64 + lane] = rc;
+  part[(wv * 2 + 1) * 64 + lane] = rm;
   __syncthreads();
-  if (wv < 2 && qv && qn) {  // wave r adds count r
-    uint32_t t = 0;
-#pragma unroll
-    for (int k = 0; k < SPEC_NW; ++k) t += part[k][wv][lane];
-    if (t) atomicAdd(&cw.rank[(int64_t)wv * S + i], t);
+  if (wv < 2 && qv) {  // wave r stores count r of this slice
+    const uint32_t t = part[(0 * 2 + wv) * 64 + lane] + part[(1 * 2 + wv) * 64 + lane] +
+                       part[(2 * 2 + wv) * 64 + lane] + part[(3 * 2 + wv) * 64 + lane];
+    ra.part[(sl * 2 + wv) * S + i] = t;
   }
 }
 
-// spec_place_kernel: one thread per spec (caller index i), 64 * ceil(S / 64) threads (a
-// wave = a query block).  Partition position = class base + the class counts of the
+__global__ __launch_bounds__(256) void spec_rank_kernel(RankArgs ra) {
+  __shared__ __attribute__((aligned(16))) uint64_t lds[2 * RANK_L];
+  spec_rank_body(ra, blockIdx.x, lds);
+}
+
+// the x-rank (r = 0) or y-rank (r = 1) of spec i: the sum of its slices' counts
+__device__ __forceinline__ uint32_t spec_rank_of(const uint32_t* __restrict__ part, int64_t S,
+                                                 int64_t i, int r) {
+  uint32_t t = 0;
+  for (int64_t sl = 0; sl < rank_slices(S); ++sl) t += part[(sl * 2 + r) * S + i];
+  return t;
+}
+
+// spec_place: one thread per spec (caller index i = blk * blockDim + thread; a wave = a
+// query block of 64).  Partition position = class base + the class counts of the
 // earlier query blocks (bcnt) + the wave's ballot prefix.  Writes the SpecRec (with its
 // rounded-up reciprocals) and perm there, zeroes partial[i] and partial[S + i], and for
-// normal specs cs[x], ms[y], mr_c[x] = y, cr_m[y] = x, dperm[x] = position; zeroes its
-// rank[] entries; the threads [nN, 64 T) pad mr_c and cr_m; thread 0 sets the counters;
-// this call's cells of the clamp table C are zeroed (clamp_apply leaves them dirty).
+// normal specs cs[x], ms[y], mr_c[x] = y, cr_m[y] = x, dperm[x] = position; the threads
+// [nN, 64 T) pad mr_c and cr_m; thread 0 sets the class counters.
 __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   const int64_t S = pa.S;
   const uint64_t* __restrict__ c_in = pa.c_in;
@@ -1061,7 +1184,7 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   const ClampWork& cw = pa.cw;
   int64_t* __restrict__ partial = pa.partial;
   unsigned long long* __restrict__ counters = pa.counters;
-  const int64_t i = blk * 256 + threadIdx.x;
+  const int64_t i = blk * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const int64_t nqb = (S + 63) / 64, qb = i >> 6;
   const bool in = i < S;
@@ -1071,8 +1194,8 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   const bool normal = cls != SPEC_EXACT;
   uint32_t x = 0, y = 0;
   if (in && normal) {
-    x = cw.rank[i];
-    y = cw.rank[S + i];
+    x = spec_rank_of(cw.rank, S, i, 0);
+    y = spec_rank_of(cw.rank, S, i, 1);
   }
   // class totals and this block's prefix: the wave's lanes take every 64th block (the
   // counts packed A | B << 32), then one DPP scan each
@@ -1096,14 +1219,8 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
     cw.cr_m[i] = 0xffffffffu;
   }
   if (i == 0) {
-    for (int k = 0; k < CNT_N; ++k)
-      counters[k] = k == CNT_SPECS_A ? (unsigned long long)nA
-                  : k == CNT_SPECS_B ? (unsigned long long)nB : 0ull;
-  }
-  {
-    const int64_t W = (nN + 63) / 64 + 2, cells = W * W;
-    for (int64_t e = i; e < C_COPIES * cells; e += (int64_t)pa.n_blocks * 256)
-      cw.C[(e / cells) * cw.c_stride + e % cells] = 0;
+    counters[CNT_SPECS_A] = nA;
+    counters[CNT_SPECS_B] = nB;
   }
   if (!in) return;
   const int64_t pos = cls == SPEC_A ? (int64_t)pA + rA
@@ -1122,8 +1239,6 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   partial[i] = 0;
   partial[S + i] = 0;
   if (!normal) return;
-  cw.rank[i] = 0;
-  cw.rank[S + i] = 0;
   cw.cs[x] = c;
   cw.ms[y] = m;
   cw.mr_c[x] = y;
@@ -1822,21 +1937,35 @@ inline unsigned grid_for(int64_t n, int block, int64_t cap) {
 }  // namespace
 
 namespace {
-int64_t reduce_resident_waves(bool limits) {
-  static int64_t cache[2] = {0, 0};
-  int64_t& w = cache[limits ? 1 : 0];
-  if (w == 0) {
-    int dev = 0, cus = 0, blocks = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks, limits ? reduce_kernel<4> : reduce_kernel<2>, 256, 0) == hipSuccess &&
-        cus > 0 && blocks > 0)
-      w = (int64_t)cus * blocks * RED_WAVES_PER_BLOCK;
-    else
-      w = 8192;
+// Resident workgroups of `kern` (block threads, lds dynamic bytes) on the current device:
+// the occupancy API's answer per CU x the CU count, cached per device ordinal (contexts on
+// several devices each get their own; concurrent first calls store the same value).
+constexpr int MAX_DEVS = 64;
+int64_t resident_blocks(std::atomic<int64_t> (&cache)[MAX_DEVS], const void* kern, int block,
+                        size_t lds, int64_t fallback) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return fallback;
+  if (dev < MAX_DEVS) {
+    const int64_t v = cache[dev].load(std::memory_order_relaxed);
+    if (v) return v;
   }
-  return w;
+  int cus = 0, blocks = 0;
+  int64_t v = fallback;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kern, block, lds) == hipSuccess &&
+      cus > 0 && blocks > 0)
+    v = (int64_t)cus * blocks;
+  if (dev < MAX_DEVS) cache[dev].store(v, std::memory_order_relaxed);
+  return v;
+}
+
+int64_t reduce_resident_waves(bool limits) {
+  static std::atomic<int64_t> cache[2][MAX_DEVS];
+  return RED_WAVES_PER_BLOCK *
+         resident_blocks(cache[limits ? 1 : 0],
+                         limits ? reinterpret_cast<const void*>(reduce_kernel<4>)
+                                : reinterpret_cast<const void*>(reduce_kernel<2>),
+                         256, 0, 2048);
 }
 }  // namespace
 
@@ -1850,65 +1979,61 @@ int32_t reduce_range(int64_t n_containers, bool limits, int64_t reserve_waves) {
   return (int32_t)(t * RED_TILE);
 }
 
-hipError_t launch_reduce_mark(int64_t n_nodes, int64_t c0, int64_t n_containers,
-                              const int64_t* node_ptr, int64_t* wave_node, uint64_t* used_cpu,
-                              int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s) {
-  if (n_nodes <= 0) return hipSuccess;
-  const MarkArgs a = mark_args(n_nodes, c0, n_containers, node_ptr, wave_node, used_cpu, used_mem,
-                               lim_cpu, lim_mem);
-  hipLaunchKernelGGL(reduce_mark_kernel, dim3(grid_for(n_nodes, 256, 8192)), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
-MarkArgs mark_args(int64_t n_nodes, int64_t c0, int64_t n_containers, const int64_t* node_ptr,
-                   int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu,
-                   int64_t* lim_mem, int64_t reserve_waves) {
-  MarkArgs a;
-  a.n_nodes = n_nodes;
-  a.c0 = c0;
-  a.c_end = c0 + n_containers;
-  a.range = reduce_range(n_containers, lim_cpu != nullptr, reserve_waves);
-  a.ptr = node_ptr;
-  a.wave_node = wave_node;
-  a.o0 = used_cpu;
-  a.o1 = reinterpret_cast<uint64_t*>(used_mem);
-  a.o2 = lim_cpu;
-  a.o3 = reinterpret_cast<uint64_t*>(lim_mem);
-  return a;
+int64_t reduce_tail_records() {
+  const int64_t a = reduce_resident_waves(false), b = reduce_resident_waves(true);
+  return (a > b ? a : b) * KCC_RED_ROUNDS + 64;
 }
 
 hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, const int64_t* node_ptr,
                          const uint64_t* cpu_req, const int64_t* mem_req,
                          const uint64_t* cpu_lim, const int64_t* mem_lim,
-                         const int64_t* wave_node, uint64_t* used_cpu, int64_t* used_mem,
-                         uint64_t* lim_cpu, int64_t* lim_mem, hipStream_t s,
-                         const PlaceArgs* place) {
-  PlaceArgs pa{};
-  if (place) pa = *place;
-  const int64_t nb_place = pa.n_blocks;
-  const bool red = n_nodes > 0 && n_containers > 0;
-  if (!red && nb_place == 0) return hipSuccess;
-  if (n_nodes >= RED_MAX_NODES) return hipErrorInvalidValue;
+                         uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem,
+                         uint64_t* tail, uint64_t epoch, unsigned long long* faults, hipStream_t s,
+                         const RankArgs* rank) {
+  RankArgs ra{};
+  if (rank) ra = *rank;
   const bool limits = cpu_lim && mem_lim && lim_cpu && lim_mem;
-  const int64_t reserve = RED_WAVES_PER_BLOCK * nb_place;
-  const int32_t range = red ? reduce_range(n_containers, limits, reserve) : RED_TILE;
-  const int64_t waves = red ? reduce_n_waves(n_containers, limits, reserve) : 0;
-  const unsigned blocks =
-      (unsigned)((waves + RED_WAVES_PER_BLOCK - 1) / RED_WAVES_PER_BLOCK + nb_place);
-  const bool lim = cpu_lim && mem_lim && lim_cpu && lim_mem;
-  if (lim) {
-    hipLaunchKernelGGL(reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, n_nodes, c0,
-                       c0 + n_containers, range, node_ptr, cpu_req, reinterpret_cast<const uint64_t*>(mem_req), cpu_lim,
-                       reinterpret_cast<const uint64_t*>(mem_lim), wave_node, used_cpu,
-                       reinterpret_cast<uint64_t*>(used_mem), lim_cpu,
-                       reinterpret_cast<uint64_t*>(lim_mem), pa);
-  } else {
-    hipLaunchKernelGGL(reduce_kernel<2>, dim3(blocks), dim3(256), 0, s, n_nodes, c0,
-                       c0 + n_containers, range, node_ptr, cpu_req, reinterpret_cast<const uint64_t*>(mem_req),
-                       (const uint64_t*)nullptr, (const uint64_t*)nullptr, wave_node, used_cpu,
-                       reinterpret_cast<uint64_t*>(used_mem), (uint64_t*)nullptr,
-                       (uint64_t*)nullptr, pa);
+  const bool red = n_nodes > 0 && n_containers > 0;
+  if (n_nodes >= RED_MAX_NODES) return hipErrorInvalidValue;
+  if (n_nodes > 0 && n_containers == 0) {  // no containers: every sum is 0
+    hipError_t e;
+    if ((e = hipMemsetAsync(used_cpu, 0, 8 * (size_t)n_nodes, s)) != hipSuccess ||
+        (e = hipMemsetAsync(used_mem, 0, 8 * (size_t)n_nodes, s)) != hipSuccess)
+      return e;
+    if (limits && ((e = hipMemsetAsync(lim_cpu, 0, 8 * (size_t)n_nodes, s)) != hipSuccess ||
+                   (e = hipMemsetAsync(lim_mem, 0, 8 * (size_t)n_nodes, s)) != hipSuccess))
+      return e;
   }
+  if (!red && ra.n_blocks == 0) return hipSuccess;
+  if (limits && ra.n_blocks > 0) return hipErrorInvalidValue;  // (the ranks ride NA = 2 only)
+  // the rank workgroups go first: they hold their slots ~2 us, the reduce's range is
+  // sized for the whole device (its last waves start when the rank workgroups exit)
+  const int32_t range = red ? reduce_range(n_containers, limits, 0) : RED_TILE;
+  const int64_t waves = red ? (n_containers + range - 1) / range : 0;
+  if (waves > reduce_tail_records()) return hipErrorInvalidValue;
+  const unsigned blocks =
+      (unsigned)((waves + RED_WAVES_PER_BLOCK - 1) / RED_WAVES_PER_BLOCK + ra.n_blocks);
+  RedArgs a{};
+  a.n_nodes = n_nodes;
+  a.c0 = c0;
+  a.c_end = c0 + n_containers;
+  a.range = range;
+  a.ptr = node_ptr;
+  a.in[0] = cpu_req;
+  a.in[1] = reinterpret_cast<const uint64_t*>(mem_req);
+  a.in[2] = limits ? cpu_lim : nullptr;
+  a.in[3] = limits ? reinterpret_cast<const uint64_t*>(mem_lim) : nullptr;
+  a.out[0] = used_cpu;
+  a.out[1] = reinterpret_cast<uint64_t*>(used_mem);
+  a.out[2] = limits ? lim_cpu : nullptr;
+  a.out[3] = limits ? reinterpret_cast<uint64_t*>(lim_mem) : nullptr;
+  a.tail = tail;
+  a.epoch = epoch;
+  a.faults = faults;
+  if (limits)
+    hipLaunchKernelGGL(reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, a, ra);
+  else
+    hipLaunchKernelGGL(reduce_kernel<2>, dim3(blocks), dim3(256), 0, s, a, ra);
   return hipGetLastError();
 }
 
@@ -1916,56 +2041,66 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
-                            SlowNode* slow, int64_t* slow_list, int64_t n_specs, ClampWork cw,
+                            SlowNode* slow, int64_t* slow_list, int64_t n_specs,
+                            const uint64_t* spec_cpu, const int64_t* spec_mem, ClampWork cw,
                             unsigned long long* counters, int chunk, int64_t row0,
-                            int64_t call_nodes, hipStream_t s, bool dense) {
-  if (n_nodes <= 0) return hipSuccess;
+                            int64_t call_nodes, hipStream_t s, bool dense,
+                            const PlaceArgs* place) {
+  if (n_nodes <= 0 && !place) return hipSuccess;
   const int64_t pr = clamp_pass_rows(call_nodes);
   if (row0 % pr != 0 || (pr != 1024 && pr != 4096)) return hipErrorInvalidValue;
   // one resident round of workgroups (LDS-bound at S <= CLAMP_LDS_SPECS: one per CU)
   const int mode = n_specs <= CLAMP_LDS_SPECS ? 2 : n_specs <= (int64_t)NP_ST_MAX * CLAMP_LDS_SPECS ? 1 : 0;
+  PlaceArgs pa{};
+  if (place) {
+    if (mode != 2) return hipErrorInvalidValue;  // node_prep reads spec_place's arrays there
+    pa = *place;
+    pa.n_blocks = (int32_t)((n_specs + KCC_NODE_PREP_BLOCK - 1) / KCC_NODE_PREP_BLOCK);
+  }
   const size_t lds_bytes = mode == 2 ? NODE_PREP_LDS : mode == 1 ? NODE_PREP_LDS_SRCH : 0;
   auto kern = pr == 1024 ? (mode == 2 ? node_prep_kernel<2, 1> : mode == 1 ? node_prep_kernel<1, 1> : node_prep_kernel<0, 1>)
                          : (mode == 2 ? node_prep_kernel<2, 4> : mode == 1 ? node_prep_kernel<1, 4> : node_prep_kernel<0, 4>);
-  static int64_t resident[2][3] = {{0, 0, 0}, {0, 0, 0}};
-  int64_t& res = resident[pr == 1024 ? 0 : 1][mode];
-  if (res == 0) {
-    int dev = 0, cus = 0, blocks = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kern, KCC_NODE_PREP_BLOCK,
-                                                     lds_bytes) == hipSuccess &&
-        cus > 0 && blocks > 0)
-      res = (int64_t)cus * blocks;
-    else
-      res = 256;
-  }
+  static std::atomic<int64_t> resident[2][3][MAX_DEVS];
+  const int64_t res = resident_blocks(resident[pr == 1024 ? 0 : 1][mode],
+                                      reinterpret_cast<const void*>(kern), KCC_NODE_PREP_BLOCK,
+                                      lds_bytes, 256);
   const int64_t cap = res < KCC_NODE_PREP_GRID ? res : KCC_NODE_PREP_GRID;
-  hipLaunchKernelGGL(kern,
-                     dim3(grid_for(n_nodes, pr, cap)),
-                     dim3(KCC_NODE_PREP_BLOCK), lds_bytes, s,
-                     n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu, used_mem,
-                     fast_a, fast_b, slow, slow_list, n_specs, cw, counters, (int32_t)chunk,
-                     (int32_t)(dense ? 1 : 0), row0 / pr);
+  const unsigned np_blocks = n_nodes > 0 ? grid_for(n_nodes, (int)pr, cap) : 0u;
+  hipLaunchKernelGGL(kern, dim3(np_blocks + (unsigned)pa.n_blocks), dim3(KCC_NODE_PREP_BLOCK),
+                     lds_bytes, s, n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu,
+                     used_mem, fast_a, fast_b, slow, slow_list, n_specs, spec_cpu, spec_mem, cw,
+                     counters, (int32_t)chunk, (int32_t)(dense ? 1 : 0), row0 / pr, pa);
   return hipGetLastError();
 }
 
-hipError_t launch_spec_prep(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
-                            SpecPrep sp, ClampWork cw, int64_t* partial,
-                            unsigned long long* counters, hipStream_t s, const MarkArgs* mark,
-                            bool with_place) {
-  if (n_specs <= 0) return hipSuccess;
-  const int64_t L = rank_slice(n_specs);
-  const int64_t blocks = (n_specs + 63) / 64 * ((n_specs + L - 1) / L);
-  const int64_t mblocks = mark && mark->n_nodes > 0 ? grid_for(mark->n_nodes, SPEC_BLOCK, 2048) : 0;
-  if (blocks + mblocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  MarkArgs none{};
-  hipLaunchKernelGGL(spec_rank_kernel, dim3((unsigned)(blocks + mblocks)), dim3(SPEC_BLOCK), 0, s,
-                     n_specs, spec_cpu, spec_mem, cw, blocks, mblocks ? *mark : none);
-  if (with_place) {
-    PlaceArgs pa{n_specs, spec_cpu, spec_mem, sp, cw, partial, counters, place_blocks(n_specs)};
-    hipLaunchKernelGGL(spec_place_kernel, dim3((unsigned)pa.n_blocks), dim3(256), 0, s, pa);
-  }
+RankArgs rank_args(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
+                   const ClampWork& cw, unsigned long long* counters) {
+  RankArgs ra{};
+  ra.S = n_specs;
+  ra.c_in = spec_cpu;
+  ra.m_in = spec_mem;
+  ra.part = cw.rank;
+  ra.bcnt = cw.bcnt;
+  ra.C = cw.C;
+  ra.c_stride = cw.c_stride;
+  const int64_t wmax = (n_specs + 63) / 64 + 2;  // >= this call's T + 2 (nN <= S)
+  ra.c_cells = wmax * wmax < cw.c_stride ? wmax * wmax : cw.c_stride;
+  ra.counters = counters;
+  ra.n_blocks = n_specs > 0 ? (int32_t)((n_specs + 63) / 64 * rank_slices(n_specs)) : 0;
+  return ra;
+}
+
+hipError_t launch_spec_rank(const RankArgs& ra, hipStream_t s) {
+  if (ra.n_blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(spec_rank_kernel, dim3((unsigned)ra.n_blocks), dim3(256), 0, s, ra);
+  return hipGetLastError();
+}
+
+hipError_t launch_spec_place(const PlaceArgs& pa0, hipStream_t s) {
+  if (pa0.S <= 0) return hipSuccess;
+  PlaceArgs pa = pa0;
+  pa.n_blocks = (int32_t)((pa.S + 255) / 256);
+  hipLaunchKernelGGL(spec_place_kernel, dim3((unsigned)pa.n_blocks), dim3(256), 0, s, pa);
   return hipGetLastError();
 }
 
@@ -1982,17 +2117,9 @@ hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
   // part subtracts its own share), as many as one round of resident workgroups holds
   // (C4: 1 per CU by registers, G = 2; more parts in a second round, G = 4 / 8: +7 / +24 us;
   // 64 VGPRs for 2 per CU and G = 4: equal)
-  static int64_t resident = 0;  // clamp_apply workgroups resident at once
-  if (resident == 0) {
-    int dev = 0, cus = 0, blocks = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, clamp_apply_kernel, CP_THREADS, 0) == hipSuccess &&
-        cus > 0 && blocks > 0)
-      resident = (int64_t)cus * blocks;
-    else
-      resident = 256;
-  }
+  static std::atomic<int64_t> cache[MAX_DEVS];  // clamp_apply workgroups resident at once
+  const int64_t resident = resident_blocks(cache, reinterpret_cast<const void*>(clamp_apply_kernel),
+                                           CP_THREADS, 0, 256);
   int64_t G = 1;
   if (clamp_binned(n_specs))
     while (G < KCC_CP_SPLIT && 2 * T * G * 2 <= resident) G *= 2;
@@ -2002,18 +2129,8 @@ hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
 }
 
 int64_t fit_resident_blocks() {  // 256-thread fit workgroups resident on the device at once
-  static int64_t cache = 0;
-  if (cache == 0) {
-    int dev = 0, cus = 0, blocks = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fit_kernel, 256, 0) == hipSuccess &&
-        cus > 0 && blocks > 0)
-      cache = (int64_t)cus * blocks;
-    else
-      cache = 2048;
-  }
-  return cache;
+  static std::atomic<int64_t> cache[MAX_DEVS];
+  return resident_blocks(cache, reinterpret_cast<const void*>(fit_kernel), 256, 0, 2048);
 }
 
 hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,

@@ -425,6 +425,12 @@ class CapacityEngine:
         self._check(self._lib.kcc_fit_stream_rows(self._h, C.byref(v)))
         return v.value
 
+    def reduce_faults(self) -> int:
+        """Look-back waits of the segmented reduce that gave up (0 on a healthy device)."""
+        v = C.c_int64()
+        self._check(self._lib.kcc_reduce_faults(self._h, C.byref(v)))
+        return v.value
+
     def fit_slow_pairs(self):
         a, b = C.c_int64(), C.c_int64()
         self._check(self._lib.kcc_fit_slow_pairs(self._h, C.byref(a), C.byref(b)))

@@ -74,3 +74,31 @@ def test_null_context_is_einval():
     assert lib.kcc_reserve(None, 1, 1, 1) == _lib.KCC_EINVAL
     assert lib.kcc_fit_run_async(None, 1, 1, None, None) == _lib.KCC_EINVAL
     assert lib.kcc_last_error(None) == b"NULL context"
+
+
+def test_release_library_reports_release_build():
+    # the product library is built with the default knobs only (csrc/Makefile refuses EXTRA
+    # outside `make variant`); an experiment build would report "variant: <flags>"
+    assert _lib.load().kcc_build_info() == b"release"
+
+
+def test_makefile_refuses_knobs_for_the_release_library():
+    csrc = os.path.join(os.path.dirname(_lib.LIB_PATH), "csrc")
+    r = subprocess.run(["make", "-n", "-C", csrc, "EXTRA=-DKCC_FIT_DIAG_NO_ATOMICS"],
+                       capture_output=True, text=True)
+    assert r.returncode != 0 and "make variant" in (r.stdout + r.stderr)
+
+
+def test_every_diagnostic_knob_is_fenced():
+    # a result-breaking diagnostic knob compiles only into a variant build: every such name
+    # used in the sources appears in kcc_internal.h's #error guard
+    import glob
+    import re
+    csrc = os.path.join(os.path.dirname(_lib.LIB_PATH), "csrc")
+    used = set()
+    for f in glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp")):
+        used |= set(re.findall(r"\b(KCC_(?:DIAG|FIT_DIAG)\w*|KCC_TIMELINE)\b", open(f).read()))
+    hdr = open(os.path.join(csrc, "kcc_internal.h")).read()
+    guard = hdr[hdr.index("#if !defined(KCC_VARIANT_BUILD)"):hdr.index("#error")]
+    missing = sorted(k for k in used if f"defined({k})" not in guard)
+    assert used and not missing, f"diagnostic knobs outside the release guard: {missing}"

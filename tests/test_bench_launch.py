@@ -30,6 +30,13 @@ def test_self_launch_starts_n_ranks():
     assert r.returncode == 0, r.stderr[-2000:]
     out = _last_json(r.stdout)
     assert out["n_gpus"] == 2 and out["rank_sum"] == 1 and out["scaling"] == "strong"
+    # the per-rank table of an N > 1 line, gathered over the ranks' group
+    ranks = out["ranks"]
+    assert set(ranks["per_rank"]) == {"step_ms", "reduce_ms", "fit_ms", "allreduce_ms",
+                                      "reduce_frac"}
+    assert ranks["per_rank"]["step_ms"] == [1.0, 2.0]
+    assert ranks["step_ms_max"] == 2.0 and ranks["step_ms_min"] == 1.0
+    assert ranks["allreduce_ms"] == 0.5
 
 
 def test_rank_count_mismatch_is_refused():

@@ -239,6 +239,9 @@ def _reduce_check(engine, sizes, seed=0):
     np.testing.assert_array_equal(r.memory_requests.view(np.uint64), seg_sums(ptr, mem))
     np.testing.assert_array_equal(r.cpu_limits, seg_sums(ptr, cpu ^ np.uint64(7)))
     np.testing.assert_array_equal(r.memory_limits.view(np.uint64), seg_sums(ptr, mem // 3))
+    r2 = engine.get_pod_cpu_memory_requests_limits(ptr, cpu, mem)  # the 2-array kernel
+    np.testing.assert_array_equal(r2.cpu_requests, r.cpu_requests)
+    np.testing.assert_array_equal(r2.memory_requests, r.memory_requests)
 
 
 @pytest.mark.parametrize("name,sizes", [
@@ -409,3 +412,9 @@ def test_c4_fit_sample_linearity_determinism(engine, c4):
     # run-to-run identity
     t2, _ = engine.total_possible_max_replicas(*args, sc, sm)
     np.testing.assert_array_equal(t2, t)
+
+
+def test_reduce_lookback_never_timed_out(engine):
+    """Every reduce launch of this session assembled its range-cut nodes from the pieces
+    the other waves published (decoupled look-back): no wait gave up."""
+    assert engine.reduce_faults() == 0

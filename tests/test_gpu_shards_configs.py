@@ -245,3 +245,7 @@ def test_fit_stream_compacted_equals_dense(engine, c4, c4_oracle):
     um = seg_sums(c.node_ptr, c.mem_req).view(np.int64)
     free = (c.alloc_cpu > uc) & (c.alloc_mem > um) & (c.alloc_pods > 0)
     assert int(free.sum()) <= streamed <= int(free.sum()) + 7 * (c.n_nodes // 1024 + 1)
+
+
+def test_reduce_lookback_never_timed_out_configs(engine):
+    assert engine.reduce_faults() == 0

@@ -119,3 +119,38 @@ def test_no_scratch(asm):
         assert size <= cap, (name, size)
         checked += 1
     assert checked >= 10  # every kernel's descriptor was found
+
+
+def _vregs(line):
+    """VGPR numbers a line names (v7, v[16:19]), operands only (no comment)."""
+    ops = line.split(";")[0]
+    regs = set()
+    for a, b in re.findall(r"\bv\[(\d+):(\d+)\]", ops):
+        regs.update(range(int(a), int(b) + 1))
+    regs.update(int(x) for x in re.findall(r"\bv(\d+)\b", ops))
+    return regs
+
+
+def test_fit_claim_result_untouched_until_drained(asm):
+    """The fit's queue claim is a returning atomic issued in inline asm, so the compiler
+    does not wait for it where it is issued; it believes the destination VGPR is written
+    at issue.  No instruction may read or write that register between the atomic and the
+    s_waitcnt vmcnt(0) that drains it: a copy would read it early, a reuse would be
+    overwritten when the claim returns (advisor, round 2)."""
+    lines = [ln.strip() for ln in kernel_body(asm, "fit_kernel").splitlines()]
+    found = 0
+    for i, ln in enumerate(lines):
+        m = re.match(r"global_atomic_add\s+v(\d+),.*\bsc0\b", ln)
+        if not m:
+            continue
+        found += 1
+        reg = int(m.group(1))
+        for ln2 in lines[i + 1:]:
+            if ln2.startswith("s_waitcnt") and "vmcnt(0)" in ln2:
+                break
+            if not ln2 or ln2.startswith((";", ".")):
+                continue
+            assert reg not in _vregs(ln2), f"v{reg} of `{ln}` touched by `{ln2}` before its wait"
+        else:
+            raise AssertionError(f"no s_waitcnt vmcnt(0) after `{ln}`")
+    assert found >= 2  # the first claim and the loop's
