@@ -252,8 +252,10 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   // the table copies stay all-zero between calls (clamp_prep zeroes what it reads); a
   // new or grown allocation, or a layout change, is zeroed before its first use
   const int64_t cs_ = kcc::clamp_c_cells((int64_t)S), hs = kcc::clamp_h_cells((int64_t)S);
-  const size_t before[4] = {dv.c_C.bytes, dv.c_H2.bytes, dv.c_H3.bytes, dv.c_rank.bytes};
-  KCC_HIP(ctx, ensure(dv.c_rank, 4 * 2 * S));
+  const size_t before[3] = {dv.c_C.bytes, dv.c_H2.bytes, dv.c_H3.bytes};
+  // the spec ranks' per-slice counts: [rank_slices(S)][2][S] u32 (plain stores, nothing
+  // to keep zero)
+  KCC_HIP(ctx, ensure(dv.c_rank, 4 * 2 * S * (size_t)kcc::rank_slices((int64_t)S)));
   KCC_HIP(ctx, ensure(dv.c_C, 8 * (size_t)kcc::C_COPIES * (size_t)cs_));
   KCC_HIP(ctx, ensure(dv.c_H2, 8 * (size_t)kcc::H2_COPIES * (size_t)hs));
   KCC_HIP(ctx, ensure(dv.c_H3, 8 * (size_t)kcc::H2_COPIES * (size_t)hs));
@@ -267,7 +269,6 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
     KCC_HIP(ctx, ensure(dv.c_dir, 4 * (size_t)kcc::clamp_d_stride((int64_t)S) * passes));
   }
   if (dv.c_C.bytes != before[0] || dv.c_H2.bytes != before[1] || dv.c_H3.bytes != before[2] ||
-      dv.c_rank.bytes != before[3] ||
       dv.c_stride != cs_ || dv.h_stride != hs)
     dv.clamp_dirty = true;
   dv.c_stride = cs_;
@@ -286,7 +287,6 @@ int clamp_clean(kcc_ctx* ctx, Dev& dv, hipStream_t s) {
   KCC_HIP(ctx, hipMemsetAsync(dv.c_C.p, 0, dv.c_C.bytes, s));
   KCC_HIP(ctx, hipMemsetAsync(dv.c_H2.p, 0, dv.c_H2.bytes, s));
   KCC_HIP(ctx, hipMemsetAsync(dv.c_H3.p, 0, dv.c_H3.bytes, s));
-  KCC_HIP(ctx, hipMemsetAsync(dv.c_rank.p, 0, dv.c_rank.bytes, s));
   dv.clamp_dirty = false;
   return KCC_OK;
 }
@@ -313,6 +313,22 @@ kcc::ClampWork clamp_of(Dev& dv) {
   return cw;
 }
 
+// The spec-side workspace a call of S specs writes (host-side guard before any launch: a
+// kernel writing past an allocation faults the device).
+int check_spec_ws(kcc_ctx* ctx, Dev& dv, int64_t S) {
+  const size_t S64 = (size_t)(S + 63) / 64 * 64;
+  const bool ok = dv.c_rank.bytes >= 8 * (size_t)S * (size_t)kcc::rank_slices(S) &&
+                  dv.c_bcnt.bytes >= 8 * (S64 / 64) && dv.c_mrc.bytes >= 4 * S64 &&
+                  dv.c_crm.bytes >= 4 * S64 && dv.c_cs.bytes >= 8 * (size_t)S &&
+                  dv.c_ms.bytes >= 8 * (size_t)S && dv.c_dperm.bytes >= 4 * (size_t)S &&
+                  dv.srec.bytes >= sizeof(kcc::SpecRec) * (size_t)S &&
+                  dv.sperm.bytes >= 4 * (size_t)S &&
+                  dv.counters.bytes >= sizeof(unsigned long long) * kcc::CNT_N &&
+                  dv.c_C.bytes >= 8 * (size_t)kcc::C_COPIES * (size_t)dv.c_stride &&
+                  dv.c_stride >= kcc::clamp_c_cells(S);
+  return ok ? KCC_OK : fail(ctx, KCC_EINVAL, "internal: spec workspace smaller than the call");
+}
+
 kcc::PlaceArgs place_args(Dev& dv, int64_t n_specs, const uint64_t* spec_cpu,
                           const int64_t* spec_mem, int64_t* partial) {
   return kcc::PlaceArgs{n_specs, spec_cpu, spec_mem, spec_prep_of(dv), clamp_of(dv), partial,
@@ -337,6 +353,7 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
   dv.prep_nodes = n_nodes;
   dv.prep_specs = n_specs;
   if (n_specs == 0) return KCC_OK;
+  if ((rc = check_spec_ws(ctx, dv, n_specs))) return rc;
   rc = clamp_clean(ctx, dv, s);
   if (rc) return rc;
   dv.clamp_dirty = true;  // until every kernel that leaves the tables zero is queued
@@ -486,6 +503,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   }
   int rc = reserve_dev(ctx, dv, n_nodes, n_cont, n_specs);
   if (rc) return rc;
+  if (n_specs > 0 && (rc = check_spec_ws(ctx, dv, n_specs))) return rc;
   for (int c = 0; c < k; ++c)
     if (!dv.ev_red[c]) KCC_HIP(ctx, hipEventCreateWithFlags(&dv.ev_red[c], hipEventDisableTiming));
   dv.last_pairs = n_nodes * n_specs;
@@ -505,7 +523,9 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   // its tables from the ranks; S <= CLAMP_LDS_SPECS): four launches per call — reduce +
   // rank, node_prep + place, fit, clamp_apply
   const bool fuse_place = n_specs > 0 && n_specs <= kcc::CLAMP_LDS_SPECS;
-  const bool fuse_rank = k == 1 && n_specs > 0 && n_nodes > 0 && n_cont > 0;
+  // (larger S: the O(S^2) counting ranks would hold the device's slots ahead of the
+  // reduce's waves; they keep a launch of their own)
+  const bool fuse_rank = k == 1 && fuse_place && n_nodes > 0 && n_cont > 0;
   const kcc::RankArgs ra = kcc::rank_args(n_specs, spec_cpu, spec_mem, clamp_of(dv),
                                           as<unsigned long long>(dv.counters));
   const kcc::PlaceArgs pa = place_args(dv, n_specs, spec_cpu, spec_mem, partial);

@@ -417,10 +417,13 @@ void reduce_kernel(RedArgs a, RankArgs ra) {
     }
     eNr = ptr_at(ptr, 64 * blk + 65 + lane, n_nodes);  // next block's ends (usually L2 hits)
     have_next = true;
-    if (last_end >= 0) {  // node cur is open at the tile end: its sum so far
+    if (last_end > tb) {  // node cur is open at the tile end: its sum so far
 #pragma unroll
       for (int k = 0; k < NA; ++k)
         carry[k] = tot[k] - pre[k][last_end - 1 - tb];
+    } else if (last_end == tb) {  // only empty nodes ended, at the tile's start (wave 0's
+#pragma unroll                    // leading empty nodes): cur starts here
+      for (int k = 0; k < NA; ++k) carry[k] = tot[k];
     } else {
 #pragma unroll
       for (int k = 0; k < NA; ++k) carry[k] += tot[k];
@@ -483,6 +486,10 @@ void reduce_kernel(RedArgs a, RankArgs ra) {
           }
           __builtin_amdgcn_s_sleep(2);
         }
+        // the values only after the tag matched: relaxed loads of other addresses may be
+        // hoisted above the poll by the compiler (they were), so a compiler barrier here;
+        // the hardware issues them after the poll's data returned (the branch needs it)
+        asm volatile("" ::: "memory");
 #pragma unroll
         for (int k = 0; k < NA; ++k) v[k] = __hip_atomic_load(r + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }

@@ -256,6 +256,7 @@ def _reduce_check(engine, sizes, seed=0):
     ("odd_total", [1, 0, 2, 0, 0, 3] * 1000 + [1]),
     ("trailing_empty", [5, 9] + [0] * 300),
     ("leading_empty", [0] * 300 + [5, 9]),
+    ("leading_empty_then_long", [0, 0, 0, 1763, 5, 0, 700]),  # wave 0: empties end at 0
 ])
 def test_reduce_csr_edges(engine, name, sizes):
     _reduce_check(engine, sizes, seed=hash(name) & 0xFFFF)
