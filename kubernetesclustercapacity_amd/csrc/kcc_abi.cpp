@@ -62,6 +62,7 @@ struct Dev {
   // the reduce's per-wave tail records (look-back), zeroed when allocated; each reduce
   // launch tags its records with a new epoch.  faults: look-back waits that timed out.
   DevBuf red_tail, red_faults;
+  DevBuf rank_arrive;  // spec_rank's per-query-block arrival counters (zero between calls)
   uint64_t red_epoch = 0;
   DevBuf fit_q;          // the fit's per-column work queues (zero between launches)
   bool fitq_dirty = true;
@@ -255,7 +256,12 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   const size_t before[3] = {dv.c_C.bytes, dv.c_H2.bytes, dv.c_H3.bytes};
   // the spec ranks' per-slice counts: [rank_slices(S)][2][S] u32 (plain stores, nothing
   // to keep zero)
-  KCC_HIP(ctx, ensure(dv.c_rank, 4 * 2 * S * (size_t)kcc::rank_slices((int64_t)S)));
+  KCC_HIP(ctx, ensure(dv.c_rank, 4 * (size_t)kcc::rank_words((int64_t)S)));
+  if (dv.rank_arrive.bytes < 4 * (S64 / 64)) {  // every call leaves them zero
+    KCC_HIP(ctx, ensure(dv.rank_arrive, 4 * (S64 / 64)));
+    KCC_HIP(ctx, hipMemsetAsync(dv.rank_arrive.p, 0, dv.rank_arrive.bytes, dv.stream));
+    KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
+  }
   KCC_HIP(ctx, ensure(dv.c_C, 8 * (size_t)kcc::C_COPIES * (size_t)cs_));
   KCC_HIP(ctx, ensure(dv.c_H2, 8 * (size_t)kcc::H2_COPIES * (size_t)hs));
   KCC_HIP(ctx, ensure(dv.c_H3, 8 * (size_t)kcc::H2_COPIES * (size_t)hs));
@@ -317,8 +323,9 @@ kcc::ClampWork clamp_of(Dev& dv) {
 // kernel writing past an allocation faults the device).
 int check_spec_ws(kcc_ctx* ctx, Dev& dv, int64_t S) {
   const size_t S64 = (size_t)(S + 63) / 64 * 64;
-  const bool ok = dv.c_rank.bytes >= 8 * (size_t)S * (size_t)kcc::rank_slices(S) &&
+  const bool ok = dv.c_rank.bytes >= 4 * (size_t)kcc::rank_words(S) &&
                   dv.c_bcnt.bytes >= 8 * (S64 / 64) && dv.c_mrc.bytes >= 4 * S64 &&
+                  dv.rank_arrive.bytes >= 4 * (S64 / 64) &&
                   dv.c_crm.bytes >= 4 * S64 && dv.c_cs.bytes >= 8 * (size_t)S &&
                   dv.c_ms.bytes >= 8 * (size_t)S && dv.c_dperm.bytes >= 4 * (size_t)S &&
                   dv.srec.bytes >= sizeof(kcc::SpecRec) * (size_t)S &&
@@ -361,17 +368,18 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
   // `partial` (no memset launches).  spec_place rides in the node_prep launch when
   // node_prep builds its tables from the ranks (S <= CLAMP_LDS_SPECS)
   KCC_HIP(ctx, kcc::launch_spec_rank(kcc::rank_args(n_specs, spec_cpu, spec_mem, clamp_of(dv),
-                                                    as<unsigned long long>(dv.counters)),
+                                                    as<unsigned long long>(dv.counters),
+                                                    as<uint32_t>(dv.rank_arrive)),
                                      s));
   const kcc::PlaceArgs pa = place_args(dv, n_specs, spec_cpu, spec_mem, partial);
-  const bool fuse_place = n_specs <= kcc::CLAMP_LDS_SPECS;
+  const bool fuse_place = n_specs <= kcc::RANK_FULL_MAX;
   if (!fuse_place) KCC_HIP(ctx, kcc::launch_spec_place(pa, s));
   if (n_nodes > 0 || fuse_place)
     KCC_HIP(ctx, kcc::launch_node_prep(n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count,
                                        used_cpu, used_mem, as<kcc::FitGroupA>(dv.fast_a),
                                        as<kcc::FitGroup>(dv.fast_b), as<kcc::SlowNode>(dv.slow),
-                                       as<int64_t>(dv.slow_list), n_specs, spec_cpu, spec_mem,
-                                       clamp_of(dv), as<unsigned long long>(dv.counters), 0, 0,
+                                       as<int64_t>(dv.slow_list), n_specs, clamp_of(dv),
+                                       as<unsigned long long>(dv.counters), 0, 0,
                                        n_nodes, s, dv.fit_dense, fuse_place ? &pa : nullptr));
   if (n_nodes == 0) {
     dv.clamp_dirty = false;
@@ -522,12 +530,13 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   // reduce's: independent work) and spec_place in the node_prep launch (node_prep builds
   // its tables from the ranks; S <= CLAMP_LDS_SPECS): four launches per call — reduce +
   // rank, node_prep + place, fit, clamp_apply
-  const bool fuse_place = n_specs > 0 && n_specs <= kcc::CLAMP_LDS_SPECS;
+  const bool fuse_place = n_specs > 0 && n_specs <= kcc::RANK_FULL_MAX;
   // (larger S: the O(S^2) counting ranks would hold the device's slots ahead of the
   // reduce's waves; they keep a launch of their own)
   const bool fuse_rank = k == 1 && fuse_place && n_nodes > 0 && n_cont > 0;
   const kcc::RankArgs ra = kcc::rank_args(n_specs, spec_cpu, spec_mem, clamp_of(dv),
-                                          as<unsigned long long>(dv.counters));
+                                          as<unsigned long long>(dv.counters),
+                                          as<uint32_t>(dv.rank_arrive));
   const kcc::PlaceArgs pa = place_args(dv, n_specs, spec_cpu, spec_mem, partial);
   if (n_specs > 0) {
     rc = clamp_clean(ctx, dv, s);
@@ -569,8 +578,8 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                        as<kcc::FitGroupA>(dv.fast_a) + lo[c] / kcc::FIT_GROUP,
                                        as<kcc::FitGroup>(dv.fast_b) + lo[c] / kcc::FIT_GROUP,
                                        as<kcc::SlowNode>(dv.slow) + lo[c],
-                                       as<int64_t>(dv.slow_list) + lo[c], n_specs, spec_cpu,
-                                       spec_mem, clamp_of(dv), as<unsigned long long>(dv.counters),
+                                       as<int64_t>(dv.slow_list) + lo[c], n_specs, clamp_of(dv),
+                                       as<unsigned long long>(dv.counters),
                                        c, lo[c], n_nodes, s, dv.fit_dense,
                                        place_here ? &pa : nullptr));
     if (n == 0) continue;
@@ -820,7 +829,7 @@ void kcc_destroy(kcc_ctx* ctx) {
     DevBuf* bufs[] = {&dv.c_rank, &dv.c_bcnt, &dv.c_cs, &dv.c_ms,
                       &dv.c_mrc, &dv.c_crm, &dv.c_dperm, &dv.c_C, &dv.c_H2, &dv.c_H3,
                       &dv.c_Crow, &dv.c_rec, &dv.c_dir,
-                      &dv.red_tail,  &dv.red_faults, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
+                      &dv.red_tail,  &dv.red_faults, &dv.rank_arrive, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
                       &dv.sperm,     &dv.fit_q,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
                       &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,

@@ -648,8 +648,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
                                  const int64_t* __restrict__ used_mem,
                                  FitGroupA* __restrict__ fast_a, FitGroup* __restrict__ fast_b,
                                  SlowNode* __restrict__ slow, int64_t* __restrict__ slow_list,
-                                 int64_t S, const uint64_t* __restrict__ spec_cpu,
-                                 const int64_t* __restrict__ spec_mem, ClampWork cw,
+                                 int64_t S, ClampWork cw,
                                  unsigned long long* __restrict__ counters,
                                  int32_t chunk, int32_t dense, int64_t pass0, PlaceArgs pa) {
   if ((int32_t)blockIdx.x < pa.n_blocks) {  // spec_place's workgroups, in front (MODE 2)
@@ -723,50 +722,11 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   const uint32_t st = lds ? 1u : np_stride(S);
   for (int b = threadIdx.x; b < NP_BINS; b += KCC_NODE_PREP_BLOCK) np_bcnt[b] = 0;
   constexpr int PER = (int)(CLAMP_LDS_SPECS / KCC_NODE_PREP_BLOCK);
-  if (lds) {
-    // MODE 2: the tables straight from the spec ranks (spec_place, which writes the sorted
-    // arrays, may run beside this launch): every spec's (c, m, x, y) loaded first, the
-    // slots initialised to +inf / empty, then each normal spec scattered to its ranks' slots
-    uint64_t cv[PER];
-    int64_t mv[PER];
-    uint32_t xr[PER], yr[PER];
-    bool nv[PER];
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int64_t i = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
-      cv[u] = i < S ? spec_cpu[i] : 0;
-      mv[u] = i < S ? spec_mem[i] : 0;
-      xr[u] = yr[u] = 0;
-      if (i < S) {
-        for (int64_t sl = 0; sl < rank_slices(S); ++sl) {
-          xr[u] += cw.rank[(sl * 2 + 0) * S + i];
-          yr[u] += cw.rank[(sl * 2 + 1) * S + i];
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int64_t k = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
-      cs_l[k] = 0xffffffffu;
-      ms_l[k] = INT64_MAX;
-      mk_l[k] = 0ull;
-      nv[u] = k < S && spec_class(cv[u], mv[u]) != SPEC_EXACT;
-    }
-    if (cpriv)
-      for (int64_t e = threadIdx.x; e < W * W; e += KCC_NODE_PREP_BLOCK) c_l[e] = 0ull;
-    __syncthreads();  // slots initialised
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      if (nv[u]) {
-        cs_l[np_slot(xr[u])] = cv[u] < FAST_FC_MAX ? (uint32_t)cv[u] : 0xffffffffu;
-        ms_l[np_slot(yr[u])] = mv[u];
-        __hip_atomic_fetch_or((lds_ull*)(mk_l + mk_at(xr[u] >> 6, yr[u] >> 6)), 1ull << (yr[u] & 63),
-                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-  } else if (srch) {
-    // every load first, guarded by S (a kernel argument) rather than nN, so they travel
-    // with the counters' load (one memory round trip); entries nN.. are masked after
+  uint32_t yv[PER];  // y-rank of x-rank tid + 1024 u
+  if (srch) {
+    // the sorted requests (spec_rank writes them when S <= RANK_FULL_MAX, spec_place
+    // above): every load first, guarded by S (a kernel argument) rather than nN, so they
+    // travel with the class counts' load (one memory round trip); entries nN.. are masked
     uint64_t cv[PER], mv[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -774,6 +734,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       const int64_t e = (k + 1) * st - 1;  // the sampled entry
       cv[u] = e < S ? cw.cs[e] : ~0ull;
       mv[u] = e < S ? (uint64_t)cw.ms[e] : (uint64_t)INT64_MAX;
+      yv[u] = lds && k < S ? cw.mr_c[k] : 0xffffffffu;
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -781,13 +742,27 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       const bool in = (k + 1) * st - 1 < nN;  // padded: +inf
       cs_l[np_slot((uint32_t)k)] = in && cv[u] < FAST_FC_MAX ? (uint32_t)cv[u] : 0xffffffffu;
       ms_l[np_slot((uint32_t)k)] = in ? (int64_t)mv[u] : INT64_MAX;
+      if (!in) yv[u] = 0xffffffffu;
+      if (lds) mk_l[k] = 0ull;  // 64 x 64 masks: one per spec slot
+    }
+    if (cpriv)
+      for (int64_t e = threadIdx.x; e < W * W; e += KCC_NODE_PREP_BLOCK) c_l[e] = 0ull;
+  }
+  __syncthreads();  // masks zero
+  KCC_TL(bid % 1024, 6);
+  if (lds) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int64_t x = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
+      if (x < nN)
+        __hip_atomic_fetch_or((lds_ull*)(mk_l + mk_at((uint32_t)x >> 6, yv[u] >> 6)), 1ull << (yv[u] & 63),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
-  __syncthreads();  // search tables and masks complete
+  __syncthreads();  // masks complete
   KCC_TL(bid % 1024, 7);
   // smallest normal requests (rows below either dominate no spec): the tables' first
-  // entries (+inf when there are none; cs[0] >= 1)
-  // (MODE 1's LDS tables are sampled: the first entries from memory)
+  // entries (+inf when there are none; cs[0] >= 1; MODE 1's LDS tables are sampled)
   const uint32_t cmin = lds ? cs_l[np_slot(0u)]
                             : (nN > 0 ? (cw.cs[0] < FAST_FC_MAX ? (uint32_t)cw.cs[0] : 0xffffffffu)
                                       : 0xffffffffu);
@@ -1087,19 +1062,23 @@ __device__ __forceinline__ float recip_up_f32(uint64_t v) {
 
 // ---- spec setup: ranks by counting (slices), then one thread per spec places it -----
 
-// The rank of every normal spec in slices of RANK_L candidates: workgroup (qb, sl) of
-// ceil(S/64) x rank_slices(S), 256 threads; lane = query spec i = 64 qb + lane (the 4
-// waves hold the same 64 queries), the slice's candidates staged in LDS as 16-B keys
-// v << 13 | (j mod 8192) (v = c or m < 2^51; non-normal specs ~0), a quarter per wave,
-// read by broadcast.  Per normal query (ties by index):
+// The rank of every normal spec: workgroup (qb, sl) of ceil(S/64) x rank_slices(S), 256
+// threads; lane = query spec i = 64 qb + lane (the 4 waves hold the same 64 queries), slice
+// sl's RANK_L candidates staged in LDS as 16-B keys v << 13 | (j mod 8192) (v = c or m <
+// 2^51; non-normal specs ~0), a quarter per wave, read by broadcast.  Per normal query
+// (ties by index):
 //   x(i) = #{normal j : (c_j, j) < (c_i, i)},   y(i) = #{normal j : (m_j, j) < (m_i, i)},
 // each slice counting keys below a threshold uniform over the slice: (v_i + 1) << 13 for
 // candidates in an earlier 8192-chunk than i (equal v sorts before), v_i << 13 | (i mod
 // 8192) in i's chunk, v_i << 13 in a later chunk (RANK_L divides 8192: a slice never
-// straddles two chunks).  The waves' counts meet in LDS; wave 0 stores the slice's x count
-// and wave 1 its y count (plain stores: nothing to zero).  The first slice of a query block
-// stores its class-A / class-B counts in bcnt[].  The workgroups also zero the counters
-// (but the class counts, spec_place's) and the coarse clamp table's cells.  `lds`: 16 KiB.
+// straddles two chunks).  The waves' counts meet in LDS; waves 0 / 1 store the slice's x / y
+// count write-through (sc1) and wait for it.  S <= RANK_FULL_MAX: the workgroup then adds
+// to its query block's arrival counter (after the barrier that follows every storing
+// wave's wait); the one that arrives last reads every slice (sc1 loads, after its add
+// returned) and writes the sorted arrays and the packed ranks, and resets the counter.  The
+// first slice of a query block stores its class-A / class-B counts in bcnt[].  The
+// workgroups also zero the counters (but the class counts, spec_place's) and the coarse
+// clamp table's cells.  `lds`: 16 KiB.
 __device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds) {
   const int64_t S = ra.S;
   const uint64_t* __restrict__ c_in = ra.c_in;
@@ -1113,6 +1092,7 @@ __device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds) {
   }
   typedef uint64_t u64x2_t __attribute__((ext_vector_type(2)));
   u64x2_t* key_l = reinterpret_cast<u64x2_t*>(lds);
+  uint32_t* part = reinterpret_cast<uint32_t*>(lds);
   const int64_t ns = rank_slices(S);
   const int64_t qb = blk / ns, sl = blk % ns;
   const int64_t i = qb * 64 + lane;  // this lane's query
@@ -1153,15 +1133,38 @@ __device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds) {
     rm += k.y < tm ? 1u : 0u;
   }
   __syncthreads();  // the keys are read: the area takes the waves' counts
-  uint32_t* part = reinterpret_cast<uint32_t*>(lds);
   part[(wv * 2 + 0) * 64 + lane] = rc;
   part[(wv * 2 + 1) * 64 + lane] = rm;
   __syncthreads();
-  if (wv < 2 && qv) {  // wave r stores count r of this slice
+  uint32_t* const slices = ra.part + S;  // [ns][2][S]
+  if (wv < 2) {  // wave r: count r of this slice
     const uint32_t t = part[(0 * 2 + wv) * 64 + lane] + part[(1 * 2 + wv) * 64 + lane] +
                        part[(2 * 2 + wv) * 64 + lane] + part[(3 * 2 + wv) * 64 + lane];
-    ra.part[(sl * 2 + wv) * S + i] = t;
+    if (qv) __hip_atomic_store(slices + (sl * 2 + wv) * S + i, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  if (S > RANK_FULL_MAX) return;  // spec_place sums the slices
+  __syncthreads();  // every storing wave has waited for its stores
+  __shared__ uint32_t last_s;
+  if (tid == 0)
+    last_s = ns == 1 ? 1u
+                     : (uint32_t)(__hip_atomic_fetch_add(ra.arrive + qb, 1u, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)ns - 1u);
+  __syncthreads();
+  if (!last_s || wv != 0) return;  // (workgroup-uniform, then wave 0 alone)
+  asm volatile("" ::: "memory");   // the slices' loads only after the arrival returned
+  if (ns > 1 && lane == 0) ra.arrive[qb] = 0;  // every slice has arrived: reset for the next call
+  if (!qv || ci == SPEC_EXACT) return;
+  uint32_t x = 0, y = 0;
+  for (int64_t k = 0; k < ns; ++k) {
+    x += __hip_atomic_load(slices + (k * 2 + 0) * S + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    y += __hip_atomic_load(slices + (k * 2 + 1) * S + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  ra.cs[x] = c;
+  ra.ms[y] = m;
+  ra.mr_c[x] = y;
+  ra.cr_m[y] = x;
+  ra.part[i] = x | y << 16;
 }
 
 __global__ __launch_bounds__(256) void spec_rank_kernel(RankArgs ra) {
@@ -1169,11 +1172,12 @@ __global__ __launch_bounds__(256) void spec_rank_kernel(RankArgs ra) {
   spec_rank_body(ra, blockIdx.x, lds);
 }
 
-// the x-rank (r = 0) or y-rank (r = 1) of spec i: the sum of its slices' counts
+// the x-rank (r = 0) or y-rank (r = 1) of normal spec i (spec_rank's layouts)
 __device__ __forceinline__ uint32_t spec_rank_of(const uint32_t* __restrict__ part, int64_t S,
                                                  int64_t i, int r) {
+  if (S <= RANK_FULL_MAX) return (part[i] >> (16 * r)) & 0xffffu;
   uint32_t t = 0;
-  for (int64_t sl = 0; sl < rank_slices(S); ++sl) t += part[(sl * 2 + r) * S + i];
+  for (int64_t sl = 0; sl < rank_slices(S); ++sl) t += part[S + (sl * 2 + r) * S + i];
   return t;
 }
 
@@ -1181,8 +1185,8 @@ __device__ __forceinline__ uint32_t spec_rank_of(const uint32_t* __restrict__ pa
 // query block of 64).  Partition position = class base + the class counts of the
 // earlier query blocks (bcnt) + the wave's ballot prefix.  Writes the SpecRec (with its
 // rounded-up reciprocals) and perm there, zeroes partial[i] and partial[S + i], and for
-// normal specs cs[x], ms[y], mr_c[x] = y, cr_m[y] = x, dperm[x] = position; the threads
-// [nN, 64 T) pad mr_c and cr_m; thread 0 sets the class counters.
+// normal specs dperm[x] = position (and, S > RANK_FULL_MAX, cs[x], ms[y], mr_c[x] = y,
+// cr_m[y] = x); the threads [nN, 64 T) pad mr_c and cr_m; thread 0 sets the class counters.
 __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   const int64_t S = pa.S;
   const uint64_t* __restrict__ c_in = pa.c_in;
@@ -1246,10 +1250,12 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   partial[i] = 0;
   partial[S + i] = 0;
   if (!normal) return;
-  cw.cs[x] = c;
-  cw.ms[y] = m;
-  cw.mr_c[x] = y;
-  cw.cr_m[y] = x;
+  if (S > RANK_FULL_MAX) {  // (spec_rank wrote these itself when its ranks were final)
+    cw.cs[x] = c;
+    cw.ms[y] = m;
+    cw.mr_c[x] = y;
+    cw.cr_m[y] = x;
+  }
   cw.dperm[x] = (int32_t)pos;
 }
 
@@ -1616,9 +1622,6 @@ __device__ __forceinline__ double min_f64_s(double x, double p) {
 
 constexpr int FIT_SPW = 256;           // specs per 256-thread workgroup (one column per wave)
 constexpr int FIT_CHUNK_GROUPS = 128;  // 1024 nodes: |sum of contributions| <= 2^30 in i32
-#ifndef KCC_FIT_QUEUE
-#define KCC_FIT_QUEUE 1  // 0: static node shares per wave (KCC_FIT_TARGET_BLOCKS grid)
-#endif
 #ifndef KCC_FIT_QCHUNK
 #define KCC_FIT_QCHUNK 32  // node groups per claim from a sub-queue
 #endif
@@ -1637,12 +1640,6 @@ static_assert(FIT_QCHUNK >= 2 && FIT_QCHUNK <= FIT_CHUNK_GROUPS, "claims sum in 
 #define KCC_FIT_WG_PER_SUB 24  // workgroups per sub-queue at most, about (8 to 32 sub-queues)
 #endif
 constexpr uint32_t FIT_QSUBS = (uint32_t)FIT_QSUBS_MAX;
-#ifndef KCC_FIT_TARGET_BLOCKS
-#define KCC_FIT_TARGET_BLOCKS 32768
-#endif
-#ifndef KCC_FIT_MIN_GPB
-#define KCC_FIT_MIN_GPB 32  // node groups per workgroup at least (8-way shards: 8 -> 32 took 9 us off the fit)
-#endif
 #ifndef KCC_FIT_ROUNDS
 #define KCC_FIT_ROUNDS 1  // queue grid: this many rounds of resident workgroups
 #endif
@@ -1665,7 +1662,7 @@ __device__ __forceinline__ double f64_at(const i32x16& v, int k) {
 // their own ([0] claims, [1] workgroups done: returning atomics on one line serialise);
 // the last workgroup of a sub-queue to finish resets both to zero for the next launch
 // (every workgroup of it has made its last claim by then); the buffer is zeroed once when
-// allocated.  KCC_FIT_QUEUE=0: static shares (each workgroup one range of the stream).
+// allocated.
 // 8 waves per SIMD: the register budget that leaves (the compiler otherwise takes ~106
 // SGPRs, 6 waves); the loops stay spill-free (tests/test_isa.py)
 #ifndef KCC_FIT_WAVES_PER_EU
@@ -1726,13 +1723,12 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   uint32_t* const qp = queue + ((uint32_t)bx * FIT_QSUBS + sub) * 16u;
   // claim size: halved when a workgroup's share is small (8-way shards of C4: ~35 groups
   // per workgroup; two claims each keep the balancing)
-  const uint32_t qsz = KCC_FIT_QUEUE && n_groups / (uint32_t)gy < KCC_FIT_Q_HALVE
-                          ? FIT_QCHUNK / 2u : FIT_QCHUNK;
+  const uint32_t qsz = n_groups / (uint32_t)gy < KCC_FIT_Q_HALVE ? FIT_QCHUNK / 2u : FIT_QCHUNK;
   __shared__ uint32_t q_slot[2];
   // lane 0 of wave 0 issues the claim in asm, so the compiler does not wait for it where
   // it is issued (its atomic-optimizer expansion reads the result at once); wave 0 waits
   // for it (vmcnt) at the end of the chunk — the loop bodies issue no other vector memory
-  // operations
+  // operations (tests/test_isa.py: nothing touches its register before that wait)
   auto claim_issue = [&](uint32_t sz) {
     if (wv == 0 && lane == 0)
       asm volatile("global_atomic_add %0, %1, %2, off sc0"
@@ -1743,28 +1739,27 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   // shrink as the segment drains and the workgroups finish together (fixed claims of
   // qsz left a tail of one to two claims: 10-20 us at C4).  Every wave computes the
   // same sizes (workgroup-uniform); claims never overlap (fetch-and-add of each size).
-  const uint32_t wps = ((uint32_t)gy + nsub - 1u) / nsub;  // workgroups per segment
+  // The first claim is static — the segment's first wseg x qsz groups, qsz per workgroup
+  // by its rank in the segment — so no workgroup waits on the queue line at launch (2048
+  // returning atomics on 256 lines at once); the queue hands out what follows.
+  const uint32_t wps = ((uint32_t)gy + nsub - 1u) / nsub;  // workgroups per segment (at most)
+  const uint32_t wseg = ((uint32_t)gy - sub + nsub - 1u) / nsub;  // this segment's workgroups
+  const uint32_t dyn0 = wseg * qsz;                        // the queue's first group
   uint32_t qcur = qsz;  // size of the claim whose result is read next
   auto claim_publish = [&](uint32_t slot) {
     if (wv == 0) {
       asm volatile("s_waitcnt vmcnt(0)" : "+v"(nxt) : : "memory");
-      if (lane == 0) q_slot[slot] = nxt;
+      if (lane == 0) q_slot[slot] = dyn0 + nxt;
     }
     __syncthreads();
   };
-  if (KCC_FIT_QUEUE) {
+  {
     const uint32_t seg = ((n_groups + nsub - 1u) / nsub + 7u) / 8u * 8u;
     base = sub * seg < n_groups ? sub * seg : n_groups;
     lim = base + seg < n_groups ? base + seg : n_groups;
-    claim_issue(qsz);
-    claim_publish(0);
     KCC_TL(2048 + b % 4096, 1);
-  } else {  // static: this workgroup's share [by * per, (by + 1) * per)
-    const uint32_t per = (n_groups + (uint32_t)gy - 1u) / (uint32_t)gy;
-    const uint32_t g0 = (uint32_t)by * per < n_groups ? (uint32_t)by * per : n_groups;
-    lim = g0 + per < n_groups ? g0 + per : n_groups;
-    nxt = g0;
   }
+  const uint32_t first = ((uint32_t)by / nsub) * qsz;  // the static first claim's offset
   uint64_t acc = 0;
   uint64_t errs = 0;
   uint32_t slow_iters = 0;
@@ -1855,12 +1850,12 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     acc += (uint64_t)(int64_t)acc32;
   };
 
-  if (KCC_FIT_QUEUE) {
+  {
     // every wave of the workgroup runs the loop (the barrier per chunk); the slot the
     // chunk's claim is read from was written before the previous barrier, the slot
     // wave 0 writes during it was last read before that barrier
     for (uint32_t k = 0;; ++k) {
-      const uint32_t cur = base + __builtin_amdgcn_readfirstlane(q_slot[k & 1u]);
+      const uint32_t cur = base + (k == 0 ? first : __builtin_amdgcn_readfirstlane(q_slot[k & 1u]));
       if (cur >= lim) break;  // workgroup-uniform
       uint32_t qn = (lim - cur) / ((uint32_t)KCC_FIT_QDIV * wps);
       qn = qn < (uint32_t)KCC_FIT_QMIN ? (uint32_t)KCC_FIT_QMIN : (qn > qsz ? qsz : qn);
@@ -1876,16 +1871,10 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     }
     if (wv == 0 && lane == 0) {  // this workgroup made its last claim
       const uint32_t d = atomicAdd(qp + 1, 1u);
-      if (d == ((uint32_t)gy - sub + nsub - 1u) / nsub - 1u) {  // the segment's last one:
+      if (d == wseg - 1u) {  // the segment's last one:
         qp[0] = 0;                                               // reset for the next launch
         qp[1] = 0;
       }
-    }
-  } else if (wave_fast) {
-    for (uint32_t cur = nxt; cur < lim; cur += FIT_QCHUNK) {
-      const int cnt = (int)((cur + FIT_QCHUNK < lim ? cur + FIT_QCHUNK : lim) - cur);
-      if (!wave_b) sum_a(cur, cnt);
-      else sum_b(cur, cnt);
     }
   }
   KCC_TL(2048 + b % 4096, 2);
@@ -1966,13 +1955,24 @@ int64_t resident_blocks(std::atomic<int64_t> (&cache)[MAX_DEVS], const void* ker
   return v;
 }
 
+#ifndef KCC_RED_WG_PER_CU
+#define KCC_RED_WG_PER_CU 0  // A/B: reduce workgroups per CU (0: the occupancy API's answer)
+#endif
 int64_t reduce_resident_waves(bool limits) {
   static std::atomic<int64_t> cache[2][MAX_DEVS];
-  return RED_WAVES_PER_BLOCK *
-         resident_blocks(cache[limits ? 1 : 0],
-                         limits ? reinterpret_cast<const void*>(reduce_kernel<4>)
-                                : reinterpret_cast<const void*>(reduce_kernel<2>),
-                         256, 0, 2048);
+  int64_t r = RED_WAVES_PER_BLOCK *
+              resident_blocks(cache[limits ? 1 : 0],
+                              limits ? reinterpret_cast<const void*>(reduce_kernel<4>)
+                                     : reinterpret_cast<const void*>(reduce_kernel<2>),
+                              256, 0, 2048);
+  if (KCC_RED_WG_PER_CU > 0 && !limits) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        (int64_t)cus * KCC_RED_WG_PER_CU * RED_WAVES_PER_BLOCK < r)
+      r = (int64_t)cus * KCC_RED_WG_PER_CU * RED_WAVES_PER_BLOCK;
+  }
+  return r;
 }
 }  // namespace
 
@@ -2049,8 +2049,7 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* pod_count, const uint64_t* used_cpu,
                             const int64_t* used_mem, FitGroupA* fast_a, FitGroup* fast_b,
                             SlowNode* slow, int64_t* slow_list, int64_t n_specs,
-                            const uint64_t* spec_cpu, const int64_t* spec_mem, ClampWork cw,
-                            unsigned long long* counters, int chunk, int64_t row0,
+                            ClampWork cw, unsigned long long* counters, int chunk, int64_t row0,
                             int64_t call_nodes, hipStream_t s, bool dense,
                             const PlaceArgs* place) {
   if (n_nodes <= 0 && !place) return hipSuccess;
@@ -2059,8 +2058,8 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
   // one resident round of workgroups (LDS-bound at S <= CLAMP_LDS_SPECS: one per CU)
   const int mode = n_specs <= CLAMP_LDS_SPECS ? 2 : n_specs <= (int64_t)NP_ST_MAX * CLAMP_LDS_SPECS ? 1 : 0;
   PlaceArgs pa{};
-  if (place) {
-    if (mode != 2) return hipErrorInvalidValue;  // node_prep reads spec_place's arrays there
+  if (place) {  // (above RANK_FULL_MAX node_prep reads the arrays spec_place writes)
+    if (n_specs > RANK_FULL_MAX || mode != 2) return hipErrorInvalidValue;
     pa = *place;
     pa.n_blocks = (int32_t)((n_specs + KCC_NODE_PREP_BLOCK - 1) / KCC_NODE_PREP_BLOCK);
   }
@@ -2075,19 +2074,24 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
   const unsigned np_blocks = n_nodes > 0 ? grid_for(n_nodes, (int)pr, cap) : 0u;
   hipLaunchKernelGGL(kern, dim3(np_blocks + (unsigned)pa.n_blocks), dim3(KCC_NODE_PREP_BLOCK),
                      lds_bytes, s, n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu,
-                     used_mem, fast_a, fast_b, slow, slow_list, n_specs, spec_cpu, spec_mem, cw,
+                     used_mem, fast_a, fast_b, slow, slow_list, n_specs, cw,
                      counters, (int32_t)chunk, (int32_t)(dense ? 1 : 0), row0 / pr, pa);
   return hipGetLastError();
 }
 
 RankArgs rank_args(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
-                   const ClampWork& cw, unsigned long long* counters) {
+                   const ClampWork& cw, unsigned long long* counters, uint32_t* arrive) {
   RankArgs ra{};
   ra.S = n_specs;
   ra.c_in = spec_cpu;
   ra.m_in = spec_mem;
   ra.part = cw.rank;
+  ra.arrive = arrive;
   ra.bcnt = cw.bcnt;
+  ra.cs = cw.cs;
+  ra.ms = cw.ms;
+  ra.mr_c = cw.mr_c;
+  ra.cr_m = cw.cr_m;
   ra.C = cw.C;
   ra.c_stride = cw.c_stride;
   const int64_t wmax = (n_specs + 63) / 64 + 2;  // >= this call's T + 2 (nN <= S)
@@ -2148,27 +2152,15 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
   const int64_t gx = (n_specs + FIT_SPW - 1) / FIT_SPW;
   const int64_t n_groups = fit_groups(n_nodes);
-  int64_t gy;
-  if (KCC_FIT_QUEUE) {
-    // one round of resident workgroups (the queue balances the waves; the stream's
-    // length is only known on the device); a chunk of a pipelined call gets its node
-    // share of the round; no more waves per column than claims at the full length
-    gy = KCC_FIT_ROUNDS * fit_resident_blocks() / gx;
-    if (grid_nodes > n_nodes) gy = gy * n_nodes / grid_nodes;
-    if (gy >= 16) gy = gy / 8 * 8;  // whole XCD rounds
-    const int64_t claims = (n_groups + FIT_QCHUNK - 1) / FIT_QCHUNK;
-    if (gy > claims) gy = claims;
-    if (gy < 1) gy = 1;
-  } else {
-    // static shares: aim for KCC_FIT_TARGET_BLOCKS workgroups over `grid_nodes` nodes,
-    // >= KCC_FIT_MIN_GPB groups each
-    int64_t gy_target = KCC_FIT_TARGET_BLOCKS / gx;
-    if (gy_target < 1) gy_target = 1;
-    const int64_t grid_groups = fit_groups(grid_nodes > n_nodes ? grid_nodes : n_nodes);
-    int64_t gpb = (grid_groups + gy_target - 1) / gy_target;
-    if (gpb < KCC_FIT_MIN_GPB) gpb = KCC_FIT_MIN_GPB;
-    gy = (n_groups + gpb - 1) / gpb;
-  }
+  // one round of resident workgroups (the queue balances the waves; the stream's length
+  // is only known on the device); a chunk of a pipelined call gets its node share of the
+  // round; no more waves per column than claims at the full length
+  int64_t gy = KCC_FIT_ROUNDS * fit_resident_blocks() / gx;
+  if (grid_nodes > n_nodes) gy = gy * n_nodes / grid_nodes;
+  if (gy >= 16) gy = gy / 8 * 8;  // whole XCD rounds
+  const int64_t claims = (n_groups + FIT_QCHUNK - 1) / FIT_QCHUNK;
+  if (gy > claims) gy = claims;
+  if (gy < 1) gy = 1;
   // 1-D grid of gx * roundup(gy, 8) workgroups, remapped XCD-aware in the kernel
   const int64_t blocks = gx * ((gy + 7) / 8 * 8);
   if (blocks > 0x7fffffffLL || gy > 0x7fffffffLL) return hipErrorInvalidValue;
