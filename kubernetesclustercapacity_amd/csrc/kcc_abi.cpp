@@ -365,22 +365,19 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
   if (rc) return rc;
   dv.clamp_dirty = true;  // until every kernel that leaves the tables zero is queued
   // spec_rank zeroes the counters and the coarse clamp table; spec_place zeroes
-  // `partial` (no memset launches).  spec_place rides in the node_prep launch when
-  // node_prep builds its tables from the ranks (S <= CLAMP_LDS_SPECS)
+  // `partial` (no memset launches) and rides in the node_prep launch (node_prep reads
+  // only the sorted arrays the ranks wrote)
   KCC_HIP(ctx, kcc::launch_spec_rank(kcc::rank_args(n_specs, spec_cpu, spec_mem, clamp_of(dv),
                                                     as<unsigned long long>(dv.counters),
                                                     as<uint32_t>(dv.rank_arrive)),
                                      s));
   const kcc::PlaceArgs pa = place_args(dv, n_specs, spec_cpu, spec_mem, partial);
-  const bool fuse_place = n_specs <= kcc::RANK_FULL_MAX;
-  if (!fuse_place) KCC_HIP(ctx, kcc::launch_spec_place(pa, s));
-  if (n_nodes > 0 || fuse_place)
-    KCC_HIP(ctx, kcc::launch_node_prep(n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count,
+  KCC_HIP(ctx, kcc::launch_node_prep(n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count,
                                        used_cpu, used_mem, as<kcc::FitGroupA>(dv.fast_a),
                                        as<kcc::FitGroup>(dv.fast_b), as<kcc::SlowNode>(dv.slow),
                                        as<int64_t>(dv.slow_list), n_specs, clamp_of(dv),
                                        as<unsigned long long>(dv.counters), 0, 0,
-                                       n_nodes, s, dv.fit_dense, fuse_place ? &pa : nullptr));
+                                       n_nodes, s, dv.fit_dense, &pa));
   if (n_nodes == 0) {
     dv.clamp_dirty = false;
     return KCC_OK;
@@ -527,12 +524,10 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     KCC_HIP(ctx, hipStreamWaitEvent(dv.side, dv.ev_fork, 0));
   }
   // k == 1: the spec ranks ride in the reduce launch (extra workgroups in front of the
-  // reduce's: independent work) and spec_place in the node_prep launch (node_prep builds
-  // its tables from the ranks; S <= CLAMP_LDS_SPECS): four launches per call — reduce +
-  // rank, node_prep + place, fit, clamp_apply
-  const bool fuse_place = n_specs > 0 && n_specs <= kcc::RANK_FULL_MAX;
-  // (larger S: the O(S^2) counting ranks would hold the device's slots ahead of the
-  // reduce's waves; they keep a launch of their own)
+  // reduce's: independent work) and spec_place in the node_prep launch (node_prep reads
+  // only the arrays the ranks wrote): four launches per call — reduce + rank, node_prep +
+  // place, fit, clamp_apply
+  const bool fuse_place = n_specs > 0;
   const bool fuse_rank = k == 1 && fuse_place && n_nodes > 0 && n_cont > 0;
   const kcc::RankArgs ra = kcc::rank_args(n_specs, spec_cpu, spec_mem, clamp_of(dv),
                                           as<unsigned long long>(dv.counters),
@@ -542,10 +537,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     rc = clamp_clean(ctx, dv, s);
     if (rc) return rc;
     dv.clamp_dirty = true;  // until every kernel that leaves the tables zero is queued
-    if (!fuse_rank) {
-      KCC_HIP(ctx, kcc::launch_spec_rank(ra, s));
-      if (!fuse_place) KCC_HIP(ctx, kcc::launch_spec_place(pa, s));
-    }
+    if (!fuse_rank) KCC_HIP(ctx, kcc::launch_spec_rank(ra, s));
   }
   for (int c = 0; c < k; ++c) {
     const int64_t n = hi[c] - lo[c];
@@ -567,7 +559,6 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     }
     if (k > 1) KCC_HIP(ctx, hipEventRecord(dv.ev_red[c], dv.side));
   }
-  if (fuse_rank && !fuse_place) KCC_HIP(ctx, kcc::launch_spec_place(pa, s));
   for (int c = 0; c < k; ++c) {
     if (k > 1) KCC_HIP(ctx, hipStreamWaitEvent(s, dv.ev_red[c], 0));  // also joins the side stream
     const int64_t n = hi[c] - lo[c];

@@ -160,7 +160,7 @@ struct SpecPrep {
 // one copy per XCD, H2/H3 two (node_prep's atomics spread over more cache lines); every
 // copy is zero between calls: clamp_prep zeroes what it reads.
 struct ClampWork {
-  uint32_t* rank;    // [rank_words(S)] by caller index: x | y << 16 (S <= RANK_FULL_MAX),
+  uint32_t* rank;    // [rank_words(S)] by caller index: x-ranks [0, S), y-ranks [S, 2S),
                      // then each slice's share of the x-rank and the y-rank
   uint32_t* bcnt;    // [ceil(S/64)][2] class A / class B specs per block of 64 (caller order)
   uint64_t* cs;      // [S] normal specs' cpu requests by x-rank (ascending)
@@ -237,47 +237,46 @@ inline int64_t clamp_passes(int64_t n_nodes) {
 constexpr int64_t CLAMP_LDS_SPECS = KCC_CLAMP_LDS_SPECS;
 
 // Spec ranks (spec_rank): the x-rank by (c, index) and the y-rank by (m, index) of every
-// normal spec, counted by brute force: workgroup (query block of 64, slice of RANK_L
-// candidates staged in LDS), rank_slices(S) slices per query block, so the work spreads
-// over ~S^2/64K workgroups.  Each slice stores its x and y counts (rank[S + (slice * 2 + r)
-// * S + i], write-through) and adds to its query block's arrival counter; up to
-// RANK_FULL_MAX specs the last slice to arrive (the counter's returned value) sums the
+// normal spec, by sort and search: workgroup (query block of RANK_L, slice of RANK_L
+// candidates), rank_slices(S)^2 workgroups; each sorts its slice's keys in registers and LDS
+// and finds each query's count below it by binary search.  Each slice stores its x and y
+// counts (rank[S + (slice * 2 + r) * S + i], write-through) and adds to its query block's
+// arrival counter; the last slice to arrive (the counter's returned value) sums the
 // slices and writes the sorted arrays itself — cs[x] = c, ms[y] = m, mr_c[x] = y,
-// cr_m[y] = x — and rank[i] = x | y << 16, then resets the counter.  Above, spec_place sums
-// the slices and writes the arrays.  The first slice of each query block stores its
-// class-A / class-B counts (bcnt).  The rank workgroups also zero the counters (all but
-// CNT_SPECS_A / CNT_SPECS_B, set by spec_place) and the coarse clamp table's cells: the
-// first launch of a step, ahead of every reader.
+// cr_m[y] = x — and rank[i] = x, rank[S + i] = y, then resets the counter.  The slice-0 workgroups store
+// the class-A / class-B counts of each block of 64 queries (bcnt).  The rank workgroups
+// also zero the counters (all but CNT_SPECS_A / CNT_SPECS_B, set by spec_place) and the
+// coarse clamp table's cells: the first launch of a step, ahead of every reader.
 constexpr int64_t RANK_L = 1024;         // candidates per slice: 16 KiB of 16-B keys
-constexpr int64_t RANK_FULL_MAX = 4096;  // spec_rank writes the sorted arrays up to this S
+constexpr int64_t RANK_FULL_MAX = 4096;  // up to this S the ranks count (above: sort + search)
 __host__ __device__ inline int64_t rank_slices(int64_t S) { return (S + RANK_L - 1) / RANK_L; }
-// u32 words of ClampWork::rank for S specs: the packed ranks, then the slices' counts
-__host__ __device__ inline int64_t rank_words(int64_t S) { return S + 2 * S * rank_slices(S); }
+// u32 words of ClampWork::rank for S specs: the x- and y-ranks, then the slices' counts
+__host__ __device__ inline int64_t rank_words(int64_t S) { return 2 * S + 2 * S * rank_slices(S); }
 struct RankArgs {
   int64_t S;
   const uint64_t* c_in;
   const int64_t* m_in;
   uint32_t* part;      // ClampWork::rank
-  uint32_t* arrive;    // [ceil(S / 64)] per query block: slices arrived (zero between calls)
+  uint32_t* arrive;    // [rank_slices(S)] per query block: slices arrived (zero between calls)
   uint32_t* bcnt;      // ClampWork::bcnt
-  uint64_t* cs;        // ClampWork::cs / ms / mr_c / cr_m (S <= RANK_FULL_MAX)
+  uint64_t* cs;        // ClampWork::cs / ms / mr_c / cr_m
   int64_t* ms;
   uint32_t* mr_c;
   uint32_t* cr_m;
   int64_t* C;          // ClampWork::C: cells [0, c_cells) of each copy are zeroed
   int64_t c_stride, c_cells;
   unsigned long long* counters;
-  int32_t n_blocks;    // 256-thread workgroups: ceil(S / 64) x rank_slices(S) (0: none)
+  int32_t n_blocks;    // 256-thread workgroups: rank_slices(S)^2 (0: none)
 };
 RankArgs rank_args(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
                    const ClampWork& cw, unsigned long long* counters, uint32_t* arrive);
 hipError_t launch_spec_rank(const RankArgs& ra, hipStream_t s);
 
 // spec_place's work (one thread per spec), run as extra workgroups in front of a
-// node_prep launch (S <= RANK_FULL_MAX: spec_rank wrote the sorted arrays node_prep reads)
-// or as a launch of its own (ahead of node_prep): the stable 3-way partition position, the
-// SpecRec / perm there, dperm (and, S > RANK_FULL_MAX, cs, ms, mr_c, cr_m), mr_c / cr_m's
-// padding, partial[0..2S) zeroed, CNT_SPECS_A / CNT_SPECS_B set.
+// node_prep launch (node_prep reads only the arrays spec_rank wrote, and not the padding
+// spec_place writes) or as a launch of its own: the stable 3-way partition position, the
+// SpecRec / perm there, dperm, mr_c / cr_m's padding, partial[0..2S) zeroed,
+// CNT_SPECS_A / CNT_SPECS_B set.
 struct PlaceArgs {
   int64_t S;
   const uint64_t* c_in;
@@ -319,9 +318,8 @@ hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
 // round-1 layout's cost: zero fields for the rows that add nothing).  row0: the launch's
 // first row within the call (a multiple of CLAMP_PASS_ROWS_MAX; the binned records'
 // passes), call_nodes: the call's rows (its pass size, clamp_pass_rows).
-// Needs the sorted spec arrays (spec_rank's when S <= RANK_FULL_MAX, else spec_place's) on
-// the stream before it.  place != nullptr (S <= RANK_FULL_MAX only): spec_place runs as
-// extra workgroups of this launch (place->n_blocks is set here).
+// Needs the sorted spec arrays (spec_rank's) on the stream before it.  place != nullptr:
+// spec_place runs as extra workgroups of this launch (place->n_blocks is set here).
 hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             const int64_t* alloc_mem, const int64_t* alloc_pods,
                             const int64_t* pod_count, const uint64_t* used_cpu,

@@ -101,7 +101,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
 // scans interleaved so every DPP read is >= 2 wait states after the write it reads.
 // 12 VALU per value instead of 30 (zeroed DPP move targets, moves, 64-bit add).
 #ifndef KCC_RED_ASM_SCAN
-#define KCC_RED_ASM_SCAN 0
+#define KCC_RED_ASM_SCAN 1  // C4 reduce 136.5 -> 134.3 us (A/B in one process, outputs identical)
 #endif
 #define KCC_SCAN2_STEP(ctl)                                 \
   "v_add_co_u32_dpp %0, vcc, %0, %0 " ctl "\n\t"            \
@@ -222,9 +222,11 @@ __attribute__((amdgpu_waves_per_eu(NA == 2 ? KCC_RED_WAVES_PER_EU : 1)))
 void reduce_kernel(RedArgs a, RankArgs ra) {
   __shared__ __attribute__((aligned(16))) uint64_t pre_s[RED_WAVES_PER_BLOCK][NA][RED_TILE];
   static_assert(sizeof(pre_s) >= 16 * RANK_L, "the rank workgroups stage RANK_L 16-B keys");
-  if ((int32_t)blockIdx.x < ra.n_blocks) {  // the spec ranks' workgroups, in front
-    spec_rank_body(ra, blockIdx.x, &pre_s[0][0][0]);
-    return;
+  if constexpr (NA == 2) {  // (launch_reduce: the ranks ride the 2-array reduce only)
+    if ((int32_t)blockIdx.x < ra.n_blocks) {  // the spec ranks' workgroups, in front
+      spec_rank_body(ra, blockIdx.x, &pre_s[0][0][0]);
+      return;
+    }
   }
   const int lane = threadIdx.x & 63;
   const int64_t n_nodes = a.n_nodes, c0 = a.c0, n_cont = a.c_end;
@@ -572,13 +574,16 @@ __device__ __forceinline__ uint32_t upper_bound_count(const T* __restrict__ a, i
 
 // #{l < 64 : a[l] < v} over one unsorted block of 64 entries (16-B aligned, padding >=
 // every v): the counts from global memory (S > CLAMP_LDS_SPECS), 64 compares
-__device__ __forceinline__ uint32_t count_lt64(const uint32_t* __restrict__ a, uint32_t v) {
+// #{entries of a[0..lim) below v} (lim <= 64; the group's padding is not read: spec_place,
+// which writes it, may run in the same launch)
+__device__ __forceinline__ uint32_t count_lt64(const uint32_t* __restrict__ a, uint32_t v, uint32_t lim) {
   const uint4* q = reinterpret_cast<const uint4*>(a);
   uint32_t n = 0;
 #pragma unroll 4
-  for (int u = 0; u < 16; ++u) {
+  for (uint32_t u = 0; u < 16; ++u) {
     const uint4 w = q[u];
-    n += (w.x < v ? 1u : 0u) + (w.y < v ? 1u : 0u) + (w.z < v ? 1u : 0u) + (w.w < v ? 1u : 0u);
+    n += (w.x < v && 4 * u + 0 < lim ? 1u : 0u) + (w.y < v && 4 * u + 1 < lim ? 1u : 0u) +
+         (w.z < v && 4 * u + 2 < lim ? 1u : 0u) + (w.w < v && 4 * u + 3 < lim ? 1u : 0u);
   }
   return n;
 }
@@ -724,8 +729,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   constexpr int PER = (int)(CLAMP_LDS_SPECS / KCC_NODE_PREP_BLOCK);
   uint32_t yv[PER];  // y-rank of x-rank tid + 1024 u
   if (srch) {
-    // the sorted requests (spec_rank writes them when S <= RANK_FULL_MAX, spec_place
-    // above): every load first, guarded by S (a kernel argument) rather than nN, so they
+    // the sorted requests (spec_rank's last arrivers write them): every load first, guarded by S (a kernel argument) rather than nN, so they
     // travel with the class counts' load (one memory round trip); entries nN.. are masked
     uint64_t cv[PER], mv[PER];
 #pragma unroll
@@ -933,9 +937,10 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
         const uint64_t mk = mk_l[mk_at(gx, yb)];
         k = (uint32_t)ck_l[gx * 65 + GY] + (uint32_t)__popcll(mk & ((1ull << ry) - 1ull));
         j = cj_l[yb * 65 + GX];
-      } else {  // x >> 6 < GX  <=>  x < 64 GX (padding: never)
-        k = w && rx ? count_lt64(cw.mr_c + 64 * GX, b) : 0u;
-        j = w && ry && GX > 0 ? count_lt64(cw.cr_m + 64 * GY, GX << 6) : 0u;
+      } else {  // x >> 6 < GX  <=>  x < 64 GX (the groups' members below nN only)
+        const int64_t mx = nN - 64 * (int64_t)GX, my = nN - 64 * (int64_t)GY;
+        k = w && rx ? count_lt64(cw.mr_c + 64 * GX, b, (uint32_t)(mx < 64 ? mx : 64)) : 0u;
+        j = w && ry && GX > 0 ? count_lt64(cw.cr_m + 64 * GY, GX << 6, (uint32_t)(my < 64 ? my : 64)) : 0u;
       }
       // (d)
       if (w && GX > 0 && GY > 0) c_add((int64_t)GX * W + GY, w);
@@ -1060,36 +1065,33 @@ __device__ __forceinline__ float recip_up_f32(uint64_t v) {
 }
 
 
-// ---- spec setup: ranks by counting (slices), then one thread per spec places it -----
+// ---- spec setup: ranks (slices), then one thread per spec places it -----------------
 
-// The rank of every normal spec: workgroup (qb, sl) of ceil(S/64) x rank_slices(S), 256
-// threads; lane = query spec i = 64 qb + lane (the 4 waves hold the same 64 queries), slice
-// sl's RANK_L candidates staged in LDS as 16-B keys v << 13 | (j mod 8192) (v = c or m <
-// 2^51; non-normal specs ~0), a quarter per wave, read by broadcast.  Per normal query
-// (ties by index):
+// The rank of every normal spec (ties by index):
 //   x(i) = #{normal j : (c_j, j) < (c_i, i)},   y(i) = #{normal j : (m_j, j) < (m_i, i)},
-// each slice counting keys below a threshold uniform over the slice: (v_i + 1) << 13 for
-// candidates in an earlier 8192-chunk than i (equal v sorts before), v_i << 13 | (i mod
-// 8192) in i's chunk, v_i << 13 in a later chunk (RANK_L divides 8192: a slice never
-// straddles two chunks).  The waves' counts meet in LDS; waves 0 / 1 store the slice's x / y
-// count write-through (sc1) and wait for it.  S <= RANK_FULL_MAX: the workgroup then adds
-// to its query block's arrival counter (after the barrier that follows every storing
-// wave's wait); the one that arrives last reads every slice (sc1 loads, after its add
-// returned) and writes the sorted arrays and the packed ranks, and resets the counter.  The
-// first slice of a query block stores its class-A / class-B counts in bcnt[].  The
-// workgroups also zero the counters (but the class counts, spec_place's) and the coarse
-// clamp table's cells.  `lds`: 16 KiB.
-__device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds) {
+// summed over slices of RANK_L candidates with 64-bit keys v << 13 | (j mod 8192) (v = c or
+// m < 2^51; non-normal specs ~0).  A slice's share is the count of its keys below a
+// threshold: (v_i + 1) << 13 for an earlier slice (equal v sorts before; v_i = 2^51 - 1:
+// every normal candidate), v_i << 13 | (i mod 8192) for i's own slice, v_i << 13 for a later
+// one (RANK_L divides 8192: a slice never straddles two 8192-chunks, so j mod 8192 orders
+// it by index).  Each slice stores its x / y counts write-through (sc1) and waits for them;
+// the workgroup then adds to its query block's arrival counter (after the barrier that
+// follows every wave's wait); the one that arrives last reads every slice (sc1 loads, after
+// its add returned), writes the sorted arrays (cs, ms, mr_c, cr_m) and the ranks (x at
+// rank[i], y at rank[S + i]), and resets the counter.  The slice-0 workgroups store
+// the class-A / class-B counts of their 64-query blocks in bcnt[].  Every rank workgroup
+// also zeroes its share of the counters (but the class counts, spec_place's) and of the
+// coarse clamp table's cells (spec_rank_body).  `lds`: 16 KiB.
+//
+// S <= RANK_FULL_MAX: counting.  Workgroup (qb, sl) of ceil(S/64) x rank_slices(S); lane =
+// query i = 64 qb + lane (the 4 waves hold the same 64 queries), the slice's RANK_L keys
+// staged in LDS, a quarter per wave, read by broadcast and compared with the threshold.
+// C4 (S = 4096): 256 workgroups of ~1 us riding in the reduce launch.
+__device__ void spec_rank_count(const RankArgs& ra, int64_t blk, uint64_t* lds) {
   const int64_t S = ra.S;
   const uint64_t* __restrict__ c_in = ra.c_in;
   const int64_t* __restrict__ m_in = ra.m_in;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  {  // zero duties, spread over the workgroups
-    const int64_t gt = blk * 256 + tid, nt = (int64_t)ra.n_blocks * 256;
-    if (gt < CNT_N && gt != CNT_SPECS_A && gt != CNT_SPECS_B) ra.counters[gt] = 0;
-    for (int64_t e = gt; e < C_COPIES * ra.c_cells; e += nt)
-      ra.C[(e / ra.c_cells) * ra.c_stride + e % ra.c_cells] = 0;
-  }
   typedef uint64_t u64x2_t __attribute__((ext_vector_type(2)));
   u64x2_t* key_l = reinterpret_cast<u64x2_t*>(lds);
   uint32_t* part = reinterpret_cast<uint32_t*>(lds);
@@ -1136,14 +1138,13 @@ __device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds) {
   part[(wv * 2 + 0) * 64 + lane] = rc;
   part[(wv * 2 + 1) * 64 + lane] = rm;
   __syncthreads();
-  uint32_t* const slices = ra.part + S;  // [ns][2][S]
+  uint32_t* const slices = ra.part + 2 * S;  // [ns][2][S]
   if (wv < 2) {  // wave r: count r of this slice
     const uint32_t t = part[(0 * 2 + wv) * 64 + lane] + part[(1 * 2 + wv) * 64 + lane] +
                        part[(2 * 2 + wv) * 64 + lane] + part[(3 * 2 + wv) * 64 + lane];
     if (qv) __hip_atomic_store(slices + (sl * 2 + wv) * S + i, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  if (S > RANK_FULL_MAX) return;  // spec_place sums the slices
   __syncthreads();  // every storing wave has waited for its stores
   __shared__ uint32_t last_s;
   if (tid == 0)
@@ -1164,7 +1165,227 @@ __device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds) {
   ra.ms[y] = m;
   ra.mr_c[x] = y;
   ra.cr_m[y] = x;
-  ra.part[i] = x | y << 16;
+  ra.part[i] = x;
+  ra.part[S + i] = y;
+}
+
+// S > RANK_FULL_MAX: sort and search, O(S log S).  Workgroup (qb, sl) of rank_slices(S)^2;
+// query block qb = the specs [RANK_L qb, RANK_L (qb + 1)) (4 per thread); the workgroup sorts
+// its slice's keys (bitonic network: registers, then LDS exchanges) and finds each query's
+// count by binary search.  C5 (S = 16384): 256 workgroups (round 2 counted every candidate
+// per query: 4096 workgroups, 44 us in a launch of its own).
+__device__ void spec_rank_sort(const RankArgs& ra, int64_t blk, uint64_t* lds) {
+  const int64_t S = ra.S;
+  const uint64_t* __restrict__ c_in = ra.c_in;
+  const int64_t* __restrict__ m_in = ra.m_in;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t ns = rank_slices(S);
+  const int64_t qb = blk / ns, sl = blk % ns;
+  // the slice's candidates j0 + 4 tid + q (q < 4), keys v << 13 | (j mod 8192) (v < 2^51 for
+  // normal specs; RANK_L divides 8192, so within the slice the key orders (v, j)), ~0 for
+  // the others; sorted ascending by a bitonic network: stages within the 4 registers of a
+  // thread (j < 4), across the lanes of a wave (j < 256: the partner's key of the same q in
+  // lane l ^ (j / 4)), across waves through LDS (j >= 256)
+  const int64_t j0 = sl * RANK_L;
+  uint64_t kx[4], ky[4];
+  uint32_t nrm = 0;  // normal candidates among this thread's 4
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t j = j0 + 4 * tid + q;
+    const uint64_t cj = j < S ? c_in[j] : 0;
+    const int64_t mj = j < S ? m_in[j] : 0;
+    const bool nj = j < S && spec_class(cj, mj) != SPEC_EXACT;
+    kx[q] = nj ? cj << 13 | (uint64_t)(j & 8191) : ~0ull;
+    ky[q] = nj ? (uint64_t)mj << 13 | (uint64_t)(j & 8191) : ~0ull;
+    nrm += nj ? 1u : 0u;
+  }
+  uint64_t* const lx = lds;           // [RANK_L] x keys
+  uint64_t* const ly = lds + RANK_L;  // [RANK_L] y keys
+  auto cx = [](uint64_t& a, uint64_t& b, bool asc) {  // a <= b afterwards when asc
+    const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+    a = asc ? lo : hi;
+    b = asc ? hi : lo;
+  };
+  typedef uint64_t u64x2_t __attribute__((ext_vector_type(2)));
+  // partner lane l ^ m of a wave-local stage (m = j / 4 < 64): DPP quad permutes (m = 1, 2),
+  // ds_swizzle bit masks within 32 lanes (m = 4, 8, 16), ds_bpermute (m = 32); the network
+  // is fully unrolled, so m is a constant at every call
+  auto xlane = [&](uint32_t v, int msk) -> uint32_t {
+    switch (msk) {
+      case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);
+      case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);
+      case 4: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (4 << 10));
+      case 8: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (8 << 10));
+      case 16: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (16 << 10));
+      default: return (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, (int)v);
+    }
+  };
+  auto xlane64 = [&](uint64_t v, int msk) -> uint64_t {
+    return (uint64_t)xlane((uint32_t)(v >> 32), msk) << 32 | xlane((uint32_t)v, msk);
+  };
+#pragma unroll
+  for (int k = 2; k <= RANK_L; k <<= 1) {
+#pragma unroll
+    for (int jj = k >> 1; jj > 0; jj >>= 1) {
+      if (jj >= 256) {  // partner thread in another wave: through LDS
+        const int pt = tid ^ (jj >> 2);
+        u64x2_t* wx = reinterpret_cast<u64x2_t*>(lx + 4 * tid);
+        u64x2_t* wy = reinterpret_cast<u64x2_t*>(ly + 4 * tid);
+        wx[0] = u64x2_t{kx[0], kx[1]};
+        wx[1] = u64x2_t{kx[2], kx[3]};
+        wy[0] = u64x2_t{ky[0], ky[1]};
+        wy[1] = u64x2_t{ky[2], ky[3]};
+        __syncthreads();
+        const u64x2_t* rx = reinterpret_cast<const u64x2_t*>(lx + 4 * pt);
+        const u64x2_t* ry = reinterpret_cast<const u64x2_t*>(ly + 4 * pt);
+        const u64x2_t px0 = rx[0], px1 = rx[1], py0 = ry[0], py1 = ry[1];
+        const uint64_t px[4] = {px0.x, px0.y, px1.x, px1.y}, py[4] = {py0.x, py0.y, py1.x, py1.y};
+        const bool asc = ((4 * tid) & k) == 0, lower = (tid & (jj >> 2)) == 0;
+        const bool keep_min = asc == lower;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          kx[q] = keep_min ? (kx[q] < px[q] ? kx[q] : px[q]) : (kx[q] < px[q] ? px[q] : kx[q]);
+          ky[q] = keep_min ? (ky[q] < py[q] ? ky[q] : py[q]) : (ky[q] < py[q] ? py[q] : ky[q]);
+        }
+        __syncthreads();  // every partner has read before the next writes
+      } else if (jj >= 4) {  // partner lane l ^ (j / 4) of the same wave, same q
+        const int msk = jj >> 2;
+        // element 4 tid + q: ascending block when bit k of it is 0; the lower of the pair
+        // keeps the smaller key in an ascending block
+        const bool asc = ((4 * tid) & k) == 0, lower = (tid & msk) == 0;
+        const bool keep_min = asc == lower;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint64_t px = xlane64(kx[q], msk), py = xlane64(ky[q], msk);
+          kx[q] = keep_min ? (kx[q] < px ? kx[q] : px) : (kx[q] < px ? px : kx[q]);
+          ky[q] = keep_min ? (ky[q] < py ? ky[q] : py) : (ky[q] < py ? py : ky[q]);
+        }
+      } else if (jj == 2) {  // pairs (0, 2), (1, 3)
+        const bool asc = ((4 * tid) & k) == 0;  // k >= 4
+        cx(kx[0], kx[2], asc);
+        cx(kx[1], kx[3], asc);
+        cx(ky[0], ky[2], asc);
+        cx(ky[1], ky[3], asc);
+      } else {  // pairs (0, 1), (2, 3)
+        const bool a0 = ((4 * tid) & k) == 0, a1 = ((4 * tid + 2) & k) == 0;
+        cx(kx[0], kx[1], a0);
+        cx(kx[2], kx[3], a1);
+        cx(ky[0], ky[1], a0);
+        cx(ky[2], ky[3], a1);
+      }
+    }
+  }
+  {  // the sorted keys, for the searches
+    u64x2_t* wx = reinterpret_cast<u64x2_t*>(lx + 4 * tid);
+    u64x2_t* wy = reinterpret_cast<u64x2_t*>(ly + 4 * tid);
+    wx[0] = u64x2_t{kx[0], kx[1]};
+    wx[1] = u64x2_t{kx[2], kx[3]};
+    wy[0] = u64x2_t{ky[0], ky[1]};
+    wy[1] = u64x2_t{ky[2], ky[3]};
+  }
+  // this thread's queries (loaded after the sort: fewer registers live across it): i_e = qb * RANK_L + 256 e + tid (a wave's lanes: 64 neighbours)
+  uint64_t c[4];
+  int64_t m[4];
+  int32_t ci[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t i = qb * RANK_L + 256 * e + tid;
+    const bool qv = i < S;
+    c[e] = qv ? c_in[i] : 0;
+    m[e] = qv ? m_in[i] : 0;
+    ci[e] = qv ? spec_class(c[e], m[e]) : SPEC_EXACT;
+    if (sl == 0) {  // the class counts of the query block of 64 this wave holds
+      const uint32_t na = (uint32_t)__popcll(__ballot(ci[e] == SPEC_A));
+      const uint32_t nb = (uint32_t)__popcll(__ballot(ci[e] == SPEC_B));
+      const int64_t q64 = qb * (RANK_L / 64) + 4 * e + wv;
+      if (lane == 0 && q64 * 64 < S) {
+        ra.bcnt[2 * q64] = na;
+        ra.bcnt[2 * q64 + 1] = nb;
+      }
+    }
+  }
+  // normal candidates in the slice (the count for a query at v = 2^51 - 1, whose
+  // threshold (v + 1) << 13 does not fit)
+  __shared__ uint32_t nrm_s[4];
+  {
+    const uint32_t wsum = (uint32_t)readlane_u64(wave_incl_scan_u64(nrm), 63);
+    if (lane == 0) nrm_s[wv] = wsum;
+  }
+  __syncthreads();
+  const uint32_t n_norm = nrm_s[0] + nrm_s[1] + nrm_s[2] + nrm_s[3];
+  // Per normal query (ties by index), this slice's share of
+  //   x(i) = #{normal j : (c_j, j) < (c_i, i)},   y(i) = #{normal j : (m_j, j) < (m_i, i)}:
+  // an earlier slice counts v_j <= v_i (keys below (v_i + 1) << 13), a later one v_j < v_i
+  // (below v_i << 13), i's own slice the keys below i's own: lower bounds by binary search.
+  auto lower_bound = [](const uint64_t* a, uint64_t t) -> uint32_t {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t step = RANK_L / 2; step > 0; step >>= 1)
+      pos += a[pos + step - 1] < t ? step : 0u;
+    return pos + (a[pos] < t ? 1u : 0u);  // pos <= RANK_L - 1 here
+  };
+  uint32_t* const slices = ra.part + 2 * S;  // [ns][2][S]
+  constexpr uint64_t V_TOP = (1ull << 51) - 1;  // largest normal request
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t i = qb * RANK_L + 256 * e + tid;
+    if (i >= S) continue;
+    uint32_t rx = 0, ry = 0;
+    if (ci[e] != SPEC_EXACT) {
+      const uint64_t own = (uint64_t)(i & 8191);
+      if (sl < qb) {
+        rx = c[e] == V_TOP ? n_norm : lower_bound(lx, (c[e] + 1) << 13);
+        ry = (uint64_t)m[e] == V_TOP ? n_norm : lower_bound(ly, ((uint64_t)m[e] + 1) << 13);
+      } else if (sl > qb) {
+        rx = lower_bound(lx, c[e] << 13);
+        ry = lower_bound(ly, (uint64_t)m[e] << 13);
+      } else {
+        rx = lower_bound(lx, c[e] << 13 | own);
+        ry = lower_bound(ly, (uint64_t)m[e] << 13 | own);
+      }
+    }
+    __hip_atomic_store(slices + (sl * 2 + 0) * S + i, rx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(slices + (sl * 2 + 1) * S + i, ry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave has waited for its stores
+  __shared__ uint32_t last_s;
+  if (tid == 0)
+    last_s = ns == 1 ? 1u
+                     : (uint32_t)(__hip_atomic_fetch_add(ra.arrive + qb, 1u, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)ns - 1u);
+  __syncthreads();
+  if (!last_s) return;            // (workgroup-uniform)
+  asm volatile("" ::: "memory");  // the slices' loads only after the arrival returned
+  if (ns > 1 && tid == 0) ra.arrive[qb] = 0;  // every slice has arrived: reset for the next call
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t i = qb * RANK_L + 256 * e + tid;
+    if (i >= S || ci[e] == SPEC_EXACT) continue;
+    uint32_t x = 0, y = 0;
+    for (int64_t k = 0; k < ns; ++k) {
+      x += __hip_atomic_load(slices + (k * 2 + 0) * S + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      y += __hip_atomic_load(slices + (k * 2 + 1) * S + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    ra.cs[x] = c[e];
+    ra.ms[y] = m[e];
+    ra.mr_c[x] = y;
+    ra.cr_m[y] = x;
+    ra.part[i] = x;
+    ra.part[S + i] = y;
+  }
+}
+
+__device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds) {
+  const int tid = threadIdx.x;
+  {  // zero duties, spread over the workgroups
+    const int64_t gt = blk * 256 + tid, nt = (int64_t)ra.n_blocks * 256;
+    if (gt < CNT_N && gt != CNT_SPECS_A && gt != CNT_SPECS_B) ra.counters[gt] = 0;
+    for (int64_t e = gt; e < C_COPIES * ra.c_cells; e += nt)
+      ra.C[(e / ra.c_cells) * ra.c_stride + e % ra.c_cells] = 0;
+  }
+  if (ra.S <= RANK_FULL_MAX) spec_rank_count(ra, blk, lds);
+  else spec_rank_sort(ra, blk, lds);
 }
 
 __global__ __launch_bounds__(256) void spec_rank_kernel(RankArgs ra) {
@@ -1172,21 +1393,13 @@ __global__ __launch_bounds__(256) void spec_rank_kernel(RankArgs ra) {
   spec_rank_body(ra, blockIdx.x, lds);
 }
 
-// the x-rank (r = 0) or y-rank (r = 1) of normal spec i (spec_rank's layouts)
-__device__ __forceinline__ uint32_t spec_rank_of(const uint32_t* __restrict__ part, int64_t S,
-                                                 int64_t i, int r) {
-  if (S <= RANK_FULL_MAX) return (part[i] >> (16 * r)) & 0xffffu;
-  uint32_t t = 0;
-  for (int64_t sl = 0; sl < rank_slices(S); ++sl) t += part[S + (sl * 2 + r) * S + i];
-  return t;
-}
 
 // spec_place: one thread per spec (caller index i = blk * blockDim + thread; a wave = a
 // query block of 64).  Partition position = class base + the class counts of the
 // earlier query blocks (bcnt) + the wave's ballot prefix.  Writes the SpecRec (with its
 // rounded-up reciprocals) and perm there, zeroes partial[i] and partial[S + i], and for
-// normal specs dperm[x] = position (and, S > RANK_FULL_MAX, cs[x], ms[y], mr_c[x] = y,
-// cr_m[y] = x); the threads [nN, 64 T) pad mr_c and cr_m; thread 0 sets the class counters.
+// normal specs dperm[x] = position; the threads [nN, 64 T) pad mr_c and cr_m; thread 0 sets
+// the class counters.
 __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   const int64_t S = pa.S;
   const uint64_t* __restrict__ c_in = pa.c_in;
@@ -1203,11 +1416,7 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   const int64_t m = in ? m_in[i] : 0;
   const int32_t cls = in ? spec_class(c, m) : SPEC_EXACT;
   const bool normal = cls != SPEC_EXACT;
-  uint32_t x = 0, y = 0;
-  if (in && normal) {
-    x = spec_rank_of(cw.rank, S, i, 0);
-    y = spec_rank_of(cw.rank, S, i, 1);
-  }
+  const uint32_t x = in && normal ? cw.rank[i] : 0u;  // the x-rank (spec_rank's last arrivers)
   // class totals and this block's prefix: the wave's lanes take every 64th block (the
   // counts packed A | B << 32), then one DPP scan each
   uint64_t tot = 0, pre = 0;
@@ -1250,12 +1459,6 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   partial[i] = 0;
   partial[S + i] = 0;
   if (!normal) return;
-  if (S > RANK_FULL_MAX) {  // (spec_rank wrote these itself when its ranks were final)
-    cw.cs[x] = c;
-    cw.ms[y] = m;
-    cw.mr_c[x] = y;
-    cw.cr_m[y] = x;
-  }
   cw.dperm[x] = (int32_t)pos;
 }
 
@@ -2058,8 +2261,7 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
   // one resident round of workgroups (LDS-bound at S <= CLAMP_LDS_SPECS: one per CU)
   const int mode = n_specs <= CLAMP_LDS_SPECS ? 2 : n_specs <= (int64_t)NP_ST_MAX * CLAMP_LDS_SPECS ? 1 : 0;
   PlaceArgs pa{};
-  if (place) {  // (above RANK_FULL_MAX node_prep reads the arrays spec_place writes)
-    if (n_specs > RANK_FULL_MAX || mode != 2) return hipErrorInvalidValue;
+  if (place) {  // (node_prep reads only what spec_rank wrote)
     pa = *place;
     pa.n_blocks = (int32_t)((n_specs + KCC_NODE_PREP_BLOCK - 1) / KCC_NODE_PREP_BLOCK);
   }
@@ -2097,7 +2299,9 @@ RankArgs rank_args(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spe
   const int64_t wmax = (n_specs + 63) / 64 + 2;  // >= this call's T + 2 (nN <= S)
   ra.c_cells = wmax * wmax < cw.c_stride ? wmax * wmax : cw.c_stride;
   ra.counters = counters;
-  ra.n_blocks = n_specs > 0 ? (int32_t)((n_specs + 63) / 64 * rank_slices(n_specs)) : 0;
+  ra.n_blocks = n_specs <= 0 ? 0
+               : n_specs <= RANK_FULL_MAX ? (int32_t)((n_specs + 63) / 64 * rank_slices(n_specs))
+                                          : (int32_t)(rank_slices(n_specs) * rank_slices(n_specs));
   return ra;
 }
 

@@ -120,6 +120,29 @@ def test_spec_count_clamp_paths(engine, s, adv):
     np.testing.assert_array_equal(t, ot)
 
 
+@pytest.mark.parametrize("s", [1025, 3000, 9000])
+def test_spec_rank_top_requests(engine, s):
+    """The spec ranks' slices (1024 candidates each, sorted and searched): requests at the
+    top of the normal range (2^51 - 1, whose 'count v_j <= v_i' threshold does not fit the
+    64-bit key) in several slices, ties across slices, non-normal specs between them."""
+    rng = np.random.default_rng(31 + s)
+    c = synth.make_cluster(2_000, 40_000, seed=13, chunk=1024)
+    sc, sm = synth.make_specs(s, seed=13)
+    top = (1 << 51) - 1
+    sc[[0, 1024 % s, s - 1, s // 2]] = top
+    sm[[1, 1025 % s, s - 2, s // 3]] = top
+    sc[::11] = sc[5]
+    sm[::13] = sm[6]
+    sc[rng.integers(0, s, s // 50)] = 0                   # exact path: div-by-zero flags
+    sm[rng.integers(0, s, s // 50)] = (1 << 51) + 3       # exact path
+    t, e = engine.capacity(c.node_ptr, c.cpu_req, c.mem_req, c.alloc_cpu, c.alloc_mem,
+                           c.alloc_pods, c.pod_count, sc, sm)
+    uc, um, _, _ = coracle.reduce_requests(c.node_ptr, c.cpu_req, c.mem_req, c.cpu_lim, c.mem_lim)
+    ot, oe = coracle.fit(c.alloc_cpu, c.alloc_mem, c.alloc_pods, c.pod_count, uc, um, sc, sm, NT)
+    np.testing.assert_array_equal(e, oe)
+    np.testing.assert_array_equal(t, ot)
+
+
 def test_fit_random_raw_rows(engine):
     """Arbitrary 64-bit rows (not derived from a cluster) against the oracle."""
     rng = np.random.default_rng(99)

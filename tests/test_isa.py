@@ -121,6 +121,15 @@ def test_no_scratch(asm):
     assert checked >= 10  # every kernel's descriptor was found
 
 
+def test_reduce_occupancy(asm):
+    """reduce_kernel<2> (which also carries the spec ranks' workgroups) keeps <= 80 VGPRs:
+    6 waves per SIMD, the occupancy its one-round range sizing was measured at (81 VGPRs
+    round up to 88: 5 waves)."""
+    m = re.search(r"\.name:\s+_ZN3kcc12_GLOBAL__N_1\d+reduce_kernelILi2EE\w*\n(.*?)\.vgpr_count:\s+(\d+)",
+                  asm, re.S)
+    assert m and int(m.group(2)) <= 80, m and m.group(2)
+
+
 def _vregs(line):
     """VGPR numbers a line names (v7, v[16:19]), operands only (no comment)."""
     ops = line.split(";")[0]
