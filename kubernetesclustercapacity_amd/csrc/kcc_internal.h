@@ -32,8 +32,15 @@ struct RankArgs;   // below: spec ranks, run as extra workgroups of a reduce lau
 #ifndef KCC_RED_PREFETCH
 #define KCC_RED_PREFETCH 1  // tiles in flight ahead of the one being reduced
 #endif
-constexpr int RED_IPL = 4;
-constexpr int RED_TILE = 64 * RED_IPL;  // 256
+#ifndef KCC_RED_IPL
+// containers per lane per tile (4 or 8): 8 halves the per-tile work (scan, node walk,
+// stores) per container at 125 VGPRs (4 waves per SIMD instead of 6): C4 reduce
+// 136.4 -> 131.1 us, 8-way shard 20.2 -> 19.5 us (A/B in one process, outputs identical)
+#define KCC_RED_IPL 8
+#endif
+constexpr int RED_IPL = KCC_RED_IPL;
+static_assert(RED_IPL == 4 || RED_IPL == 8, "two or four 16-B loads per lane and array");
+constexpr int RED_TILE = 64 * RED_IPL;  // 512
 constexpr int RED_WAVES_PER_BLOCK = 4;
 // the reduce stores through 32-bit buffer offsets (8 B per node, < 2^31)
 constexpr int64_t RED_MAX_NODES = (int64_t)1 << 28;

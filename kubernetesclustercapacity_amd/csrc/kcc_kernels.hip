@@ -147,7 +147,7 @@ __device__ __forceinline__ int32_t rel_ptr(const int64_t* __restrict__ ptr, int6
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
-// RED_IPL (=4) consecutive 64-bit values of one array for this lane: two 16-B
+// RED_IPL consecutive 64-bit values of one array for this lane: RED_IPL / 2 16-B
 // range-checked buffer loads (outside the descriptor's range they read 0), so the
 // prefetch is branch-free and never waits where it is issued.
 // The lane offset (voff) is loop-invariant and the tile offset goes in soffset, so no
@@ -157,15 +157,14 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 #define KCC_RED_LOAD_AUX 0  // the loads' cache-policy bits (A/B builds)
 #endif
 __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff, int32_t soff,
-                                          uint64_t (&x)[4]) {
-  const u64x2 lo =
-      __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, KCC_RED_LOAD_AUX));
-  const u64x2 hi = __builtin_bit_cast(
-      u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16, soff, KCC_RED_LOAD_AUX));
-  x[0] = lo.x;
-  x[1] = lo.y;
-  x[2] = hi.x;
-  x[3] = hi.y;
+                                          uint64_t (&x)[RED_IPL]) {
+#pragma unroll
+  for (int h = 0; h < RED_IPL / 2; ++h) {
+    const u64x2 v = __builtin_bit_cast(
+        u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16 * h, soff, KCC_RED_LOAD_AUX));
+    x[2 * h] = v.x;
+    x[2 * h + 1] = v.y;
+  }
 }
 
 // One wavefront walks a contiguous range of `range` containers in tiles of
@@ -256,11 +255,11 @@ void reduce_kernel(RedArgs a, RankArgs ra) {
   // The first tiles' loads go out first: they depend on the range alone, while the node
   // search below is a chain of dependent loads
   constexpr int RING = KCC_RED_PREFETCH + 1;
-  uint64_t xs[RING][NA][4];
+  uint64_t xs[RING][NA][RED_IPL];
 #pragma unroll
   for (int u = 0; u < KCC_RED_PREFETCH; ++u)
 #pragma unroll
-    for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 32, u * RED_TILE * 8, xs[u][k]);
+    for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 8 * RED_IPL, u * RED_TILE * 8, xs[u][k]);
   __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink them below the search)
 
   // node0: the last node j < n_nodes with ptr[j] <= wb (ptr[0] == c0 <= wb; wave 0 takes
@@ -329,25 +328,27 @@ void reduce_kernel(RedArgs a, RankArgs ra) {
     pend = false;
   };
 
-  auto tile = [&](uint64_t (&x)[NA][4], uint64_t (&nx)[NA][4], const int32_t tb) {
+  auto tile = [&](uint64_t (&x)[NA][RED_IPL], uint64_t (&nx)[NA][RED_IPL], const int32_t tb) {
 #ifndef KCC_DIAG_RED_NOSTORE
     issue_pending();
 #endif
 #pragma unroll
     for (int k = 0; k < NA; ++k)
-      load_quad(rs[k], lane * 32, (tb + KCC_RED_PREFETCH * RED_TILE) * 8, nx[k]);
+      load_quad(rs[k], lane * 8 * RED_IPL, (tb + KCC_RED_PREFETCH * RED_TILE) * 8, nx[k]);
 #ifdef KCC_DIAG_RED_LOADONLY
 #pragma unroll
-    for (int k = 0; k < NA; ++k) carry[k] += x[k][0] + x[k][1] + x[k][2] + x[k][3];
+    for (int k = 0; k < NA; ++k)
+#pragma unroll
+      for (int i = 0; i < RED_IPL; ++i) carry[k] += x[k][i];
     return;
 #endif
-    const int32_t p0l = tb + 4 * lane;  // relative position of this lane's first item
-    if ((len & 1) && p0l <= len - 1 && len - 1 < p0l + 4) {  // odd tail: last item alone
+    const int32_t p0l = tb + RED_IPL * lane;  // relative position of this lane's first item
+    if ((len & 1) && p0l <= len - 1 && len - 1 < p0l + RED_IPL) {  // odd tail: last item alone
 #pragma unroll
       for (int k = 0; k < NA; ++k) {
         const uint64_t v = in[k][wb + len - 1];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)  // static indices only (no scratch)
+        for (int i = 0; i < RED_IPL; ++i)  // static indices only (no scratch)
           if (p0l + i == len - 1) x[k][i] = v;
       }
     }
@@ -357,15 +358,22 @@ void reduce_kernel(RedArgs a, RankArgs ra) {
     // back from it (x0 is dead once the total is formed: fewer live registers)
     uint64_t tot[NA], P[NA];
 #pragma unroll
-    for (int k = 0; k < NA; ++k) P[k] = x[k][0] + x[k][1] + x[k][2] + x[k][3];
+    for (int k = 0; k < NA; ++k) {
+      P[k] = x[k][0];
+#pragma unroll
+      for (int i = 1; i < RED_IPL; ++i) P[k] += x[k][i];
+    }
 #pragma unroll
     for (int k = 0; k < NA; k += 2) wave_incl_scan2_u64(P[k], P[k + 1]);
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
-      const uint64_t p2 = P[k] - x[k][3], p1 = p2 - x[k][2], p0 = p1 - x[k][1];
-      u64x2* dst = reinterpret_cast<u64x2*>(&pre[k][4 * lane]);
-      dst[0] = u64x2{p0, p1};
-      dst[1] = u64x2{p2, P[k]};
+      uint64_t pp[RED_IPL];  // the lane's items' inclusive prefixes, walked back from P
+      pp[RED_IPL - 1] = P[k];
+#pragma unroll
+      for (int i = RED_IPL - 1; i > 0; --i) pp[i - 1] = pp[i] - x[k][i];
+      u64x2* dst = reinterpret_cast<u64x2*>(&pre[k][RED_IPL * lane]);
+#pragma unroll
+      for (int h = 0; h < RED_IPL / 2; ++h) dst[h] = u64x2{pp[2 * h], pp[2 * h + 1]};
       tot[k] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(P[k] >> 32), 63) << 32) |
                (uint32_t)__builtin_amdgcn_readlane((uint32_t)P[k], 63);
     }

@@ -1,13 +1,10 @@
 #!/bin/bash
-# Guarded GPU session: parity tests, then an A/B of the variants/ builds named in $@.
+# A/B of variants/ builds at C4 and its 8-way shard (one process each, interleaved rounds)
+#   bash scripts/gpu_ab.sh <tag> <variant>...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=$1; shift
 mkdir -p gpurun_out
-timeout -k 10 540 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread \
-  > gpurun_out/pytest_gpu.log 2>&1
-rc=$?
-echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python -u scripts/ab_variants.py run "$@" > gpurun_out/ab.log 2>&1
-rc=$?; echo "ab rc=$rc"; grep -v amdgpu.ids gpurun_out/ab.log | tail -8
-exit $rc
+timeout -k 10 300 python -u scripts/ab_variants.py run --config C4 --rounds 5 --reps 10 "$@" > gpurun_out/ab_${TAG}_c4.txt 2>&1 || exit $?
+timeout -k 10 300 python -u scripts/ab_variants.py run --config C4 --shard 8 --rounds 5 --reps 20 "$@" > gpurun_out/ab_${TAG}_c4w8.txt 2>&1 || exit $?
+grep -h '^{' gpurun_out/ab_${TAG}_c4.txt gpurun_out/ab_${TAG}_c4w8.txt
