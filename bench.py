@@ -11,8 +11,10 @@ Default workload = BASELINE config C4 (1M nodes, ~20M pods / ~40M containers, 40
 specs), which fits one MI355X.  --gpus N: one process per GPU; the SAME 1M-node
 cluster is split into N contiguous node ranges (strong scaling, BASELINE configs[3]:
 "1M nodes x 20M pods, 4096 specs, nodes sharded over 2/4/8 MI355X") and the only
-exchange is the RCCL all-reduce of the per-spec partials, issued by libkcc on the
-kernels' own stream (kcc_allreduce_partial_async).  Launched without torchrun
+exchange is the sum of the per-spec partials: by default one kernel on the kernels' own
+stream that pushes each rank's partial into every peer's mailbox over xGMI peer memory,
+waits for the peers' pushes and finalizes (kcc_exchange_finalize_async, --exchange p2p);
+--exchange kcc: libkcc's RCCL all-reduce (kcc_allreduce_partial_async) + finalize.  Launched without torchrun
 (`python bench.py --gpus N`), the script re-launches itself under
 torch.distributed.run with N ranks before anything touches the GPU.  --scaling weak
 (one C4-sized partition per rank, an N x 1M-node cluster) is a secondary mode.
@@ -62,9 +64,10 @@ def parse():
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong (default): the config's cluster split over the ranks; "
                          "weak: a config-sized node partition per rank")
-    ap.add_argument("--exchange", default="kcc", choices=["kcc", "torch"],
-                    help="N > 1: all-reduce of the partials by libkcc's own RCCL communicator "
-                         "on the kernel stream (kcc), or torch.distributed.all_reduce (torch)")
+    ap.add_argument("--exchange", default="p2p", choices=["p2p", "kcc", "torch"],
+                    help="N > 1: the partials' sum by one push-wait-finalize kernel over xGMI "
+                         "peer memory (p2p, default), libkcc's own RCCL all-reduce on the "
+                         "kernel stream (kcc), or torch.distributed.all_reduce (torch)")
     ap.add_argument("--chunks", type=int, default=1,
                     help="node chunks of the pipelined step (reduce of chunk k overlaps the fit "
                          "of chunk k-1); 1 = reduce, then fit")
@@ -198,7 +201,7 @@ def main():
     local = local % max(n_dev, 1)  # gloo rehearsal: several ranks, one GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    exchange = args.exchange if args.dist_backend == "nccl" else "torch"
+    exchange = args.exchange if args.dist_backend == "nccl" or args.exchange == "p2p" else "torch"
     if world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -232,6 +235,22 @@ def main():
     eng.reserve(n, C, S)
     stream = torch.cuda.Stream(dev)
     exchange_note = None
+    if world > 1 and exchange == "p2p":
+        # every rank's mailbox handle to every rank over the process group; any failure
+        # (on any rank) falls back to libkcc's RCCL all-reduce (gloo: torch's)
+        try:
+            handles = [None] * world
+            dist.all_gather_object(handles, eng.p2p_export(world, S))
+            eng.p2p_open(rank, handles)
+        except Exception as e:  # noqa: BLE001 - every rank falls back the same way below
+            exchange_note = f"p2p exchange setup failed ({e})"
+        ok = torch.tensor([0 if exchange_note else 1], dtype=torch.int64,
+                          device=dev if args.dist_backend == "nccl" else None)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            exchange = "kcc" if args.dist_backend == "nccl" else "torch"
+            exchange_note = (exchange_note or "a peer's p2p setup failed") + f"; {exchange} used"
+        dist.barrier()
     if world > 1 and exchange == "kcc":
         # libkcc's own RCCL communicator: rank 0's id travels over the process group
         try:
@@ -260,13 +279,17 @@ def main():
             if prof:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record(stream)
-            if exchange == "kcc":  # RCCL on the same stream: no cross-stream event
+            if exchange == "p2p":  # push, wait, sum and finalize: one kernel, same stream
+                eng.exchange_finalize_async(S, partial, totals, err, stream=stream)
+            elif exchange == "kcc":  # RCCL on the same stream: no cross-stream event
                 eng.allreduce_partial_async(S, partial, stream=stream)
             else:
                 dist.all_reduce(partial, op=dist.ReduceOp.SUM)
             if prof:
                 ev[1].record(stream)
                 ar_events.append(ev)
+            if exchange == "p2p":
+                return
         eng.fit_finalize_async(S, partial, totals, err, stream=stream)
 
     with torch.cuda.stream(stream):
@@ -348,7 +371,9 @@ def main():
         "world": {
             "ranks": world, "process_group_size": dist.get_world_size() if world > 1 else 1,
             "backend": args.dist_backend if world > 1 else None,
-            "exchange": (("libkcc RCCL (kcc_allreduce_partial_async, kernel stream)"
+            "exchange": (("one-shot push over xGMI peer memory + finalize, one kernel "
+                          "(kcc_exchange_finalize_async, kernel stream)" if exchange == "p2p" else
+                          "libkcc RCCL (kcc_allreduce_partial_async, kernel stream)"
                           if exchange == "kcc" else f"torch.distributed.all_reduce ({args.dist_backend})")
                          if world > 1 else None),
             "exchange_note": exchange_note,
@@ -420,6 +445,24 @@ def main():
     out["totals_checksum"] = int(((tot_np * np.uint64(0x9E3779B97F4A7C15)) ^ (tot_np >> np.uint64(29)))
                                  .sum(dtype=np.uint64))
     out["spec_errors"] = int(err.cpu().numpy().sum())
+    if world > 1 and exchange == "p2p":
+        # the p2p exchange against the process group's all-reduce of the same partials +
+        # the library's finalize (every rank), and the flag waits that gave up (0)
+        torch.cuda.synchronize()
+        rp = partial.clone() if args.dist_backend == "nccl" else partial.cpu()
+        dist.all_reduce(rp, op=dist.ReduceOp.SUM)
+        ref_t = torch.empty_like(totals)
+        ref_e = torch.empty_like(err)
+        eng.fit_finalize_async(S, rp.to(dev), ref_t, ref_e, stream=stream)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(ref_t, totals) and torch.equal(ref_e, err))
+        p2p_faults = eng.p2p_faults()
+        flag = torch.tensor([1 if same and p2p_faults == 0 else 0], dtype=torch.int64,
+                            device=dev if args.dist_backend == "nccl" else None)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        out["exchange_check"] = {
+            "equals_allreduce_finalize": bool(int(flag.item()) == 1), "p2p_faults_rank0": p2p_faults,
+            "note": "allreduce_ms is the one-shot kernel's time: push + wait + sum + finalize"}
     if not args.no_dense:  # the same step with every node row streamed through the fit
         eng.set_fit_dense(True)
         with torch.cuda.stream(stream):

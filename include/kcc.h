@@ -210,6 +210,29 @@ int kcc_comm_unique_id(uint8_t* id /* [KCC_COMM_ID_BYTES] */);
 int kcc_comm_init(kcc_ctx* ctx, const uint8_t* id, int n_ranks, int rank);
 int kcc_allreduce_partial_async(kcc_ctx* ctx, int64_t n_specs, int64_t* d_partial, void* stream);
 
+/* One-shot exchange over xGMI peer memory: the MI355X-native replacement for
+ * kcc_allreduce_partial_async + kcc_fit_finalize_async when each rank is one process on
+ * its own GPU (<= 8 ranks, a 2*S int64 payload: latency-bound, so one push over the
+ * full mesh beats a ring).  Setup, once: kcc_p2p_export allocates this rank's mailbox
+ * (2 parities x n_ranks x (2 * max_specs) int64 + flags) and returns its IPC handle;
+ * every rank's handle travels to every rank (any channel: the bytes are opaque);
+ * kcc_p2p_open maps the peers' mailboxes.  Each step: kcc_exchange_finalize_async (one
+ * kernel on the caller's stream, after kcc_capacity_partial_async) pushes this rank's
+ * partial into every mailbox, waits for every peer's push of the same step, sums and
+ * finalizes totals / spec_err exactly as the all-reduce + finalize do.  Every rank must
+ * call it the same number of times with the same specs.  A wait for a peer that never
+ * pushes gives up after seconds and is counted (kcc_p2p_faults; the totals are then
+ * wrong): tests and the bench assert 0.  Replaces RCCL only where its
+ * ncclAllReduce(partial) stood (ClusterCapacity.go:138, the total over nodes). */
+#define KCC_P2P_HANDLE_BYTES 64
+#define KCC_P2P_MAX_SPECS (1 << 20)
+int kcc_p2p_export(kcc_ctx* ctx, int n_ranks, int64_t max_specs,
+                   uint8_t* handle /* [KCC_P2P_HANDLE_BYTES] */);
+int kcc_p2p_open(kcc_ctx* ctx, int rank, const uint8_t* handles /* [n_ranks][64] */);
+int kcc_exchange_finalize_async(kcc_ctx* ctx, int64_t n_specs, const int64_t* d_partial,
+                                int64_t* d_totals, int32_t* d_spec_err, void* stream);
+int kcc_p2p_faults(kcc_ctx* ctx, int64_t* faults);
+
 /* Per-launch timing of kcc_capacity_partial_async (HIP events recorded on the stream
  * each kernel runs on): enable (1) / disable (0) resets the sums; read synchronises
  * and returns the summed durations and launch counts of the reduces (mark + reduce,

@@ -53,6 +53,10 @@ SIGNATURES = {
     "kcc_comm_unique_id": (_int, [_vp]),
     "kcc_comm_init": (_int, [_vp, _vp, _int, _int]),
     "kcc_allreduce_partial_async": (_int, [_vp, _i64, _vp, _vp]),
+    "kcc_p2p_export": (_int, [_vp, _int, _i64, _vp]),
+    "kcc_p2p_open": (_int, [_vp, _int, _vp]),
+    "kcc_exchange_finalize_async": (_int, [_vp, _i64, _vp, _vp, _vp, _vp]),
+    "kcc_p2p_faults": (_int, [_vp, C.POINTER(_i64)]),
     "kcc_profile_enable": (_int, [_vp, _int]),
     "kcc_profile_read": (_int, [_vp] + [C.POINTER(_dbl), C.POINTER(_i64)] * 2),
     "kcc_last_slow_fraction": (_dbl, [_vp]),

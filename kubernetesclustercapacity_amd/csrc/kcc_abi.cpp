@@ -88,6 +88,14 @@ struct Dev {
   DevBuf kb_esc_n, kb_esc_row, kb_esc_cpu, kb_esc_mem;
   // kcc_pod_requests / kcc_reduce_requests_pods staging (app containers in cpu / mem)
   DevBuf q_ptr, q_iptr, q_icpu, q_imem, q_rst, q_ocpu, q_omem, q_pcpu, q_pmem;
+  // one-shot exchange over xGMI peer memory (kcc_p2p_*): this rank's mailbox (exported),
+  // the push arrival counter and the flag-wait fault counter; the peers' mapped mailboxes
+  DevBuf p2p_mbox, p2p_arrive, p2p_faults;
+  unsigned char* p2p_peer[kcc::P2P_MAX_RANKS] = {};  // opened peer mailboxes (own: p2p_mbox)
+  int p2p_W = 0, p2p_rank = -1;
+  int64_t p2p_smax = 0;
+  uint64_t p2p_epoch = 0;
+  bool p2p_ready = false;
 };
 
 }  // namespace
@@ -817,6 +825,14 @@ void kcc_destroy(kcc_ctx* ctx) {
   for (Dev& dv : ctx->devs) {
     (void)hipSetDevice(dv.device);
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
+    if (dv.p2p_W > 0) {
+      (void)hipDeviceSynchronize();  // exchanges ran on caller streams
+      for (int p = 0; p < dv.p2p_W; ++p)
+        if (p != dv.p2p_rank && dv.p2p_peer[p]) (void)hipIpcCloseMemHandle(dv.p2p_peer[p]);
+      DevBuf* pb[] = {&dv.p2p_mbox, &dv.p2p_arrive, &dv.p2p_faults};
+      for (DevBuf* b : pb)
+        if (b->p) (void)hipFree(b->p);
+    }
     DevBuf* bufs[] = {&dv.c_rank, &dv.c_bcnt, &dv.c_cs, &dv.c_ms,
                       &dv.c_mrc, &dv.c_crm, &dv.c_dperm, &dv.c_C, &dv.c_H2, &dv.c_H3,
                       &dv.c_Crow, &dv.c_rec, &dv.c_dir,
@@ -1156,6 +1172,107 @@ int kcc_allreduce_partial_async(kcc_ctx* ctx, int64_t n_specs, int64_t* d_partia
   KCC_HIP(ctx, hipSetDevice(ctx->devs[0].device));
   KCC_NCCL(ctx, ncclAllReduce(d_partial, d_partial, 2 * (size_t)n_specs, ncclInt64, ncclSum,
                               ctx->proc_comm, static_cast<hipStream_t>(stream)));
+  return KCC_OK;
+}
+
+// ---- one-shot exchange over xGMI peer memory (kcc_p2p_*) ---------------------------
+
+int kcc_p2p_export(kcc_ctx* ctx, int n_ranks, int64_t max_specs, uint8_t* handle) {
+  if (!ctx) return KCC_EINVAL;
+  if (!handle || n_ranks < 1 || n_ranks > kcc::P2P_MAX_RANKS || max_specs < 1 ||
+      max_specs > KCC_P2P_MAX_SPECS)
+    return fail(ctx, KCC_EINVAL, "need a handle buffer, 1 <= n_ranks <= 8, 1 <= max_specs <= 2^20");
+  if (ctx->devs.size() != 1)
+    return fail(ctx, KCC_EINVAL, "a multi-process rank drives exactly one device");
+  Dev& dv = ctx->devs[0];
+  if (dv.p2p_W > 0) return fail(ctx, KCC_EINVAL, "mailbox already exported");
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  const size_t bytes = kcc::p2p_mbox_bytes(n_ranks, max_specs);
+  KCC_HIP(ctx, ensure(dv.p2p_mbox, bytes));
+  KCC_HIP(ctx, ensure(dv.p2p_arrive, 64));
+  KCC_HIP(ctx, ensure(dv.p2p_faults, 64));
+  KCC_HIP(ctx, hipMemset(dv.p2p_mbox.p, 0, bytes));  // flags 0: no epoch seen
+  KCC_HIP(ctx, hipMemset(dv.p2p_arrive.p, 0, 64));
+  KCC_HIP(ctx, hipMemset(dv.p2p_faults.p, 0, 64));
+  KCC_HIP(ctx, hipDeviceSynchronize());
+  static_assert(sizeof(hipIpcMemHandle_t) == KCC_P2P_HANDLE_BYTES, "IPC handle size");
+  hipIpcMemHandle_t h;
+  KCC_HIP(ctx, hipIpcGetMemHandle(&h, dv.p2p_mbox.p));
+  std::memcpy(handle, &h, sizeof(h));
+  dv.p2p_W = n_ranks;
+  dv.p2p_smax = max_specs;
+  return KCC_OK;
+}
+
+int kcc_p2p_open(kcc_ctx* ctx, int rank, const uint8_t* handles) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  if (dv.p2p_W == 0) return fail(ctx, KCC_EINVAL, "kcc_p2p_export first");
+  if (dv.p2p_ready) return fail(ctx, KCC_EINVAL, "peers already opened");
+  if (!handles || rank < 0 || rank >= dv.p2p_W) return fail(ctx, KCC_EINVAL, "need handles and 0 <= rank < n_ranks");
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  for (int p = 0; p < dv.p2p_W; ++p) {
+    if (p == rank) {
+      dv.p2p_peer[p] = static_cast<unsigned char*>(dv.p2p_mbox.p);
+      continue;
+    }
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handles + (size_t)p * KCC_P2P_HANDLE_BYTES, sizeof(h));
+    void* ptr = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+      for (int q = 0; q < p; ++q)
+        if (q != rank && dv.p2p_peer[q]) (void)hipIpcCloseMemHandle(dv.p2p_peer[q]);
+      for (auto& q : dv.p2p_peer) q = nullptr;
+      return fail(ctx, KCC_EHIP, std::string("hipIpcOpenMemHandle(rank ") + std::to_string(p) +
+                                     "): " + hipGetErrorString(e));
+    }
+    dv.p2p_peer[p] = static_cast<unsigned char*>(ptr);
+  }
+  dv.p2p_rank = rank;
+  dv.p2p_ready = true;
+  return KCC_OK;
+}
+
+int kcc_exchange_finalize_async(kcc_ctx* ctx, int64_t n_specs, const int64_t* d_partial,
+                                int64_t* d_totals, int32_t* d_spec_err, void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  if (!dv.p2p_ready) return fail(ctx, KCC_EINVAL, "no peers (kcc_p2p_export + kcc_p2p_open)");
+  if (n_specs < 0 || n_specs > dv.p2p_smax)
+    return fail(ctx, KCC_EINVAL, "n_specs outside [0, the mailbox's max_specs]");
+  if (n_specs == 0) return KCC_OK;
+  if (!d_partial || !d_totals || !d_spec_err) return fail(ctx, KCC_EINVAL, "NULL partial/totals/err");
+  if (dv.sperm.bytes < sizeof(int32_t) * (size_t)n_specs)
+    return fail(ctx, KCC_EINVAL, "exchange without a matching fit_partial");
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  kcc::P2PArgs a{};
+  a.S = n_specs;
+  a.smax = dv.p2p_smax;
+  a.W = dv.p2p_W;
+  a.rank = dv.p2p_rank;
+  a.epoch = ++dv.p2p_epoch;
+  a.partial = d_partial;
+  for (int p = 0; p < dv.p2p_W; ++p) a.mbox[p] = dv.p2p_peer[p];
+  a.perm = as<int32_t>(dv.sperm);
+  a.totals = d_totals;
+  a.spec_err = d_spec_err;
+  a.arrive = as<uint32_t>(dv.p2p_arrive);
+  a.faults = as<unsigned long long>(dv.p2p_faults);
+  KCC_HIP(ctx, kcc::launch_exchange_finalize(a, static_cast<hipStream_t>(stream)));
+  return KCC_OK;
+}
+
+int kcc_p2p_faults(kcc_ctx* ctx, int64_t* faults) {
+  if (!ctx || !faults) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  *faults = 0;
+  if (!dv.p2p_faults.p) return KCC_OK;
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  KCC_HIP(ctx, hipDeviceSynchronize());
+  unsigned long long f = 0;
+  KCC_HIP(ctx, hipMemcpy(&f, dv.p2p_faults.p, sizeof(f), hipMemcpyDeviceToHost));
+  *faults = (int64_t)f;
   return KCC_OK;
 }
 

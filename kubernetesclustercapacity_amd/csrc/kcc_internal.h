@@ -354,6 +354,39 @@ hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial,
 // another on the same device (the host-array entry points with more shards than devices)
 hipError_t launch_partial_add(int64_t n, int64_t* dst, const int64_t* src, hipStream_t s);
 
+// ---- one-shot exchange of the per-spec partials over xGMI peer memory (kcc_p2p_*) -----
+// One process per GPU, W <= P2P_MAX_RANKS.  Every rank owns a mailbox in its own HBM,
+// exported as an IPC handle and mapped by every peer:
+//   flags [2][W][8] u64 (parity, sender: one 64-B line each; the sender's epoch),
+//   data  [2][W][2 smax] i64 (parity, sender: the sender's partial — sums, then div-by-zero
+//         counts).
+// exchange_finalize_kernel (one launch per step, replacing the RCCL all-reduce and
+// fit_finalize): thread i pushes spec i's two partial words into every mailbox (remote
+// stores over xGMI, its own included), the launch's last workgroup to finish pushing
+// (arrival counter) publishes the epoch into every mailbox's flag of this sender (system
+// scope, after every pushing thread's system-scope fence), every workgroup waits for all
+// W flags of this epoch in its own mailbox, then sums the W vectors and finalizes
+// (totals[perm[i]], spec_err[perm[i]]).  Parity = epoch & 1: a rank can only push epoch
+// e + 2 after every peer pushed e + 1, i.e. after every peer's launch for e read its data.
+constexpr int P2P_MAX_RANKS = 8;
+__host__ __device__ inline size_t p2p_flag_words(int W) { return (size_t)2 * W * 8; }
+inline size_t p2p_mbox_bytes(int W, int64_t smax) {
+  return 8 * (p2p_flag_words(W) + (size_t)2 * W * 2 * (size_t)smax);
+}
+struct P2PArgs {
+  int64_t S, smax;
+  int32_t W, rank;
+  uint64_t epoch;                         // >= 1, +1 per launch (every rank the same)
+  const int64_t* partial;                 // [2S] this rank's (internal order)
+  unsigned char* mbox[P2P_MAX_RANKS];     // rank p's mailbox (this rank's own at [rank])
+  const int32_t* perm;                    // internal -> caller index (this rank's fit)
+  int64_t* totals;
+  int32_t* spec_err;
+  uint32_t* arrive;                       // this rank's push arrivals (zero between launches)
+  unsigned long long* faults;             // flag waits that gave up (stays 0)
+};
+hipError_t launch_exchange_finalize(const P2PArgs& a, hipStream_t s);
+
 // ---- quantity-string parse (kcc_parse.hip) ------------------------
 enum ParseMode : int { PARSE_MODE_CPU_MILLIS = 0, PARSE_MODE_BYTES = 1, PARSE_MODE_QUANTITY = 2 };
 // per-string status (include/kcc.h KCC_PARSE_*)

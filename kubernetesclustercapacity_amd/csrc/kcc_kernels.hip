@@ -103,10 +103,14 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
 #ifndef KCC_RED_ASM_SCAN
 #define KCC_RED_ASM_SCAN 1  // C4 reduce 136.5 -> 134.3 us (A/B in one process, outputs identical)
 #endif
+// gfx950 (as gfx942) needs 2 wait states between a VALU write of VCC and a VALU read of it
+// (LLVM puts an s_nop 1 between v_sub_co_u32 and v_subb_co_u32): one after each low half.
 #define KCC_SCAN2_STEP(ctl)                                 \
   "v_add_co_u32_dpp %0, vcc, %0, %0 " ctl "\n\t"            \
+  "s_nop 1\n\t"                                             \
   "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc " ctl "\n\t"      \
   "v_add_co_u32_dpp %2, vcc, %2, %2 " ctl "\n\t"            \
+  "s_nop 1\n\t"                                             \
   "v_addc_co_u32_dpp %3, vcc, %3, %3, vcc " ctl "\n\t"
 __device__ __forceinline__ void wave_incl_scan2_u64(uint64_t& a, uint64_t& b) {
 #if KCC_RED_ASM_SCAN
@@ -385,20 +389,23 @@ void reduce_kernel(RedArgs a, RankArgs ra) {
     const int32_t lim = tb + RED_TILE < len ? tb + RED_TILE : len;
     int32_t last_end = -1;  // end of the last node that ended in this tile (-1: none)
     for (;;) {
-      const int64_t j = 64 * blk + lane;
       int32_t s = __builtin_amdgcn_update_dpp(0, eA, DPP_WAVE_SHR1, 0xf, 0xf, false);
       if (lane == 0) s = sA0;
-      const bool act = (j >= cur) && (j < n_nodes) && (eA <= lim);
-      if (act) {
+      // node 64 blk + lane ends in this tile: lanes [cur - 64 blk, n_nodes - 64 blk) (cur
+      // lies in block blk or at its end) whose end is within the tile
+      const int64_t jb = 64 * blk, nrem = n_nodes - jb;
+      const int32_t lo_l = (int32_t)(cur - jb), hi_l = nrem < 64 ? (int32_t)nrem : 64;
+      const bool act = lane >= lo_l && lane < hi_l && eA <= lim;
+      // branch-free: both prefixes read at positions clamped into the strip, the sum
+      // selected (s <= tb only for node cur, which began in an earlier tile)
+      const int32_t ie = min(max(eA - 1 - tb, 0), RED_TILE - 1);
+      const int32_t is = min(max(s - 1 - tb, 0), RED_TILE - 1);
 #pragma unroll
-        for (int k = 0; k < NA; ++k) {
-          uint64_t sum = 0;
-          if (eA > s) {  // s <= tb only for node cur, which began in an earlier tile
-            const uint64_t startp = s > tb ? pre[k][s - 1 - tb] : (0ull - carry[k]);
-            sum = pre[k][eA - 1 - tb] - startp;
-          }
-          res[k] = sum;
-        }
+      for (int k = 0; k < NA; ++k) {
+        const uint64_t pe = pre[k][ie], ps = pre[k][is];
+        const uint64_t startp = s > tb ? ps : (0ull - carry[k]);
+        const uint64_t sum = eA > s ? pe - startp : 0ull;
+        res[k] = act ? sum : res[k];
       }
       const unsigned long long bal = __ballot(act);
       if (!bal) break;
@@ -2128,6 +2135,66 @@ __global__ void fit_finalize_kernel(int64_t S, const int64_t* __restrict__ parti
   spec_err[dst] = err ? 1 : 0;
 }
 
+// One-shot exchange + finalize (P2PArgs, kcc_internal.h).  256 threads, specs strided over
+// the grid (at most P2P_MAX_WG workgroups: all resident at once, since each waits for the
+// flag the last one publishes).
+constexpr uint32_t P2P_SPIN_MAX = 1u << 21;  // flag polls before a wait gives up (seconds)
+constexpr int64_t P2P_MAX_WG = 256;
+__global__ __launch_bounds__(256) void exchange_finalize_kernel(P2PArgs a) {
+  const int64_t S = a.S, smax = a.smax, i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t gs = (int64_t)gridDim.x * 256;
+  const int W = a.W, par = (int)(a.epoch & 1u);
+  const int64_t slot = ((int64_t)par * W + a.rank) * 2 * smax;  // this sender's data slot
+  const size_t fw = p2p_flag_words(W);
+  // 1. push this rank's two words of each of its specs into every mailbox
+  for (int64_t i = i0; i < S; i += gs) {
+    const int64_t v0 = a.partial[i], v1 = a.partial[S + i];
+    for (int p = 0; p < W; ++p) {
+      int64_t* d = reinterpret_cast<int64_t*>(a.mbox[p]) + fw + slot;
+      d[i] = v0;
+      d[smax + i] = v1;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the pushes are performed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1u) {  // every workgroup has pushed: publish the epoch
+      __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int p = 0; p < W; ++p)
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(a.mbox[p]) + ((int64_t)par * W + a.rank) * 8,
+                           a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  // 2. every sender's flag of this epoch in this rank's own mailbox (thread p polls p's)
+  if (threadIdx.x < (unsigned)W) {
+    const uint64_t* f =
+        reinterpret_cast<const uint64_t*>(a.mbox[a.rank]) + ((int64_t)par * W + threadIdx.x) * 8;
+    uint32_t spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != a.epoch) {
+      if (++spins >= P2P_SPIN_MAX) {  // a peer never pushed: count it, go on (never on a healthy run)
+        atomicAdd(a.faults, 1ull);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale mailbox lines
+  // 3. the sums over the W senders, finalized
+  const int64_t* d = reinterpret_cast<const int64_t*>(a.mbox[a.rank]) + fw + (int64_t)par * W * 2 * smax;
+  for (int64_t i = i0; i < S; i += gs) {
+    uint64_t s0 = 0, s1 = 0;
+    for (int p = 0; p < W; ++p) {
+      s0 += (uint64_t)__builtin_nontemporal_load(d + (int64_t)p * 2 * smax + i);
+      s1 += (uint64_t)__builtin_nontemporal_load(d + (int64_t)p * 2 * smax + smax + i);
+    }
+    const int32_t dst = a.perm[i];
+    a.totals[dst] = s1 != 0 ? 0 : (int64_t)s0;
+    a.spec_err[dst] = s1 != 0 ? 1 : 0;
+  }
+}
+
 __global__ void partial_add_kernel(int64_t n, int64_t* __restrict__ dst,
                                    const int64_t* __restrict__ src) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2387,6 +2454,15 @@ hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial, const in
   if (n_specs <= 0) return hipSuccess;
   hipLaunchKernelGGL(fit_finalize_kernel, dim3(grid_for(n_specs, 256, 1 << 30)), dim3(256), 0, s,
                      n_specs, partial, perm, totals, spec_err);
+  return hipGetLastError();
+}
+
+hipError_t launch_exchange_finalize(const P2PArgs& a, hipStream_t s) {
+  if (a.S <= 0) return hipSuccess;
+  if (a.S > a.smax || a.W < 1 || a.W > P2P_MAX_RANKS || a.rank < 0 || a.rank >= a.W ||
+      a.epoch == 0)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(exchange_finalize_kernel, dim3(grid_for(a.S, 256, P2P_MAX_WG)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@ import numpy as np
 from . import _lib
 
 COMM_ID_BYTES = 128  # KCC_COMM_ID_BYTES
+P2P_HANDLE_BYTES = 64  # KCC_P2P_HANDLE_BYTES
 
 
 class KccError(RuntimeError):
@@ -402,6 +403,35 @@ class CapacityEngine:
         """RCCL all-reduce (sum, int64) of the 2*S partial vector, on `stream`."""
         self._check(self._lib.kcc_allreduce_partial_async(self._h, n_specs, _dp(partial),
                                                           _stream(stream)))
+
+    def p2p_export(self, n_ranks: int, max_specs: int) -> bytes:
+        """One-shot xGMI exchange, setup step 1: allocate this rank's mailbox and return
+        its IPC handle (opaque bytes every rank must receive)."""
+        buf = C.create_string_buffer(P2P_HANDLE_BYTES)
+        self._check(self._lib.kcc_p2p_export(self._h, int(n_ranks), int(max_specs),
+                                             C.cast(buf, C.c_void_p)))
+        return buf.raw
+
+    def p2p_open(self, rank: int, handles):
+        """Setup step 2: map every peer's mailbox (handles: every rank's export, by rank)."""
+        blob = b"".join(handles)
+        if len(blob) != P2P_HANDLE_BYTES * len(handles):
+            raise ValueError(f"each handle holds {P2P_HANDLE_BYTES} bytes")
+        buf = C.create_string_buffer(blob, len(blob))
+        self._check(self._lib.kcc_p2p_open(self._h, int(rank), C.cast(buf, C.c_void_p)))
+
+    def exchange_finalize_async(self, n_specs, partial, totals, spec_err, stream=None):
+        """Each step: push this rank's partial to every peer's mailbox, wait for theirs,
+        sum and finalize (replaces allreduce_partial_async + fit_finalize_async)."""
+        self._check(self._lib.kcc_exchange_finalize_async(self._h, n_specs, _dp(partial),
+                                                          _dp(totals), _dp(spec_err),
+                                                          _stream(stream)))
+
+    def p2p_faults(self) -> int:
+        """Flag waits of the exchange that gave up (0 on a healthy run)."""
+        v = C.c_int64()
+        self._check(self._lib.kcc_p2p_faults(self._h, C.byref(v)))
+        return v.value
 
     def profile_enable(self, on: bool = True):
         self._check(self._lib.kcc_profile_enable(self._h, 1 if on else 0))

@@ -132,3 +132,65 @@ def test_gpu_rank_partials_equal_whole(tmp_path, world):
     t, e = coracle.fit(c.alloc_cpu, c.alloc_mem, c.alloc_pods, c.pod_count, uc, um, sc, sm)
     np.testing.assert_array_equal(got[:S], t)
     np.testing.assert_array_equal(got[S:], e)
+
+
+def _worker_p2p(rank, world, port, n, pods, S, adversarial, steps, out):
+    """Every rank: its node shard's partial from libkcc on cuda:0, then the one-shot
+    exchange (kcc_exchange_finalize_async: push to every peer's mailbox, wait, sum,
+    finalize) — the ranks sharing the box's one GPU, their mailboxes mapped through IPC
+    handles gathered over gloo.  Several steps in a row (both mailbox parities)."""
+    import torch
+
+    from kubernetesclustercapacity_amd import CapacityEngine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard.node_range(n, rank, world)
+    c = synth.make_cluster(n, pods, seed=78, node_lo=lo, node_hi=hi, adversarial=adversarial,
+                           chunk=256)
+    sc, sm = synth.make_specs(S, seed=78, adversarial=adversarial)
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+    nl = c.alloc_cpu.size
+    uc = torch.empty(nl, dtype=torch.int64, device=dev)
+    um = torch.empty(nl, dtype=torch.int64, device=dev)
+    part = torch.empty(2 * S, dtype=torch.int64, device=dev)
+    totals = torch.empty(S, dtype=torch.int64, device=dev)
+    err = torch.empty(S, dtype=torch.int32, device=dev)
+    args = (T(c.node_ptr), T(c.cpu_req), T(c.mem_req), T(c.alloc_cpu), T(c.alloc_mem),
+            T(c.alloc_pods), T(c.pod_count), uc, um, T(sc), T(sm), part)
+    with CapacityEngine(0, 1) as eng:
+        handles = [None] * world
+        dist.all_gather_object(handles, eng.p2p_export(world, S))
+        eng.p2p_open(rank, handles)
+        dist.barrier()
+        got = []
+        for _ in range(steps):
+            eng.capacity_partial_async(c.node_ptr, *args)
+            eng.exchange_finalize_async(S, part, totals, err)
+            got.append(np.concatenate([totals.cpu().numpy(), err.cpu().numpy().astype(np.int64)]))
+        faults = eng.p2p_faults()
+        dist.barrier()  # no rank unmaps its mailbox while a peer may still push
+    np.save(out + f".{rank}.npy", np.stack(got + [np.full(2 * S, faults, np.int64)]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_p2p_exchange_equals_whole(tmp_path, world):
+    """The one-shot xGMI exchange (bench --exchange p2p): every rank's finalized totals
+    after 3 steps == the oracle over the whole cluster, no flag wait gave up."""
+    n, pods, S, steps = 20_011, 300_000, 300, 3
+    out = str(tmp_path / "p2p")
+    mp.spawn(_worker_p2p, args=(world, _free_port(), n, pods, S, True, steps, out), nprocs=world,
+             join=True)
+    c = synth.make_cluster(n, pods, seed=78, adversarial=True, chunk=256)
+    sc, sm = synth.make_specs(S, seed=78, adversarial=True)
+    from oracle import coracle
+    uc, um, _, _ = coracle.reduce_requests(c.node_ptr, c.cpu_req, c.mem_req)
+    t, e = coracle.fit(c.alloc_cpu, c.alloc_mem, c.alloc_pods, c.pod_count, uc, um, sc, sm)
+    for r in range(world):
+        got = np.load(out + f".{r}.npy")
+        assert got[-1][0] == 0, f"rank {r}: {got[-1][0]} flag waits gave up"
+        for k in range(steps):
+            np.testing.assert_array_equal(got[k][:S], t, err_msg=f"rank {r} step {k}")
+            np.testing.assert_array_equal(got[k][S:], e, err_msg=f"rank {r} step {k}")
