@@ -39,7 +39,7 @@ struct RankArgs;   // below: spec ranks, run as extra workgroups of a reduce lau
 #define KCC_RED_IPL 8
 #endif
 constexpr int RED_IPL = KCC_RED_IPL;
-static_assert(RED_IPL == 4 || RED_IPL == 8, "two or four 16-B loads per lane and array");
+static_assert(RED_IPL == 4 || RED_IPL == 8 || RED_IPL == 16, "2, 4 or 8 16-B loads per lane and array");
 constexpr int RED_TILE = 64 * RED_IPL;  // 512
 constexpr int RED_WAVES_PER_BLOCK = 4;
 // the reduce stores through 32-bit buffer offsets (8 B per node, < 2^31)
