@@ -46,12 +46,17 @@ METRIC = "node×spec fit evals/sec at 1M nodes × 4K specs; % of HBM roofline"
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, shard=None):
+    """HBM bytes per launch of `kernel` from profiles/pmc_traffic.json: the N = 1 C4 bench's
+    PMC passes, or (shard = "<config>/w<W>") rank 0's shard of a W-way split."""
     try:
         with open(TRAFFIC_FILE) as f:
             t = json.load(f)
+        if shard:
+            e = t["shards"][shard]
+            return e["kernels"][kernel]["hbm_bytes_per_launch"], f"{e['source']} (rank 0's shard {shard})"
         return t["kernels"][kernel]["hbm_bytes_per_launch"], t["source"]
-    except (OSError, KeyError, ValueError):
+    except (OSError, KeyError, ValueError, TypeError):
         return None, None
 
 
@@ -345,8 +350,14 @@ def main():
     fit_valu = streamed / chunks * ((S + 63) // 64) * FIT_VALU_PER_NODE_WAVE / (fit_ms * 1e-3)
     red_gbs = red_bytes / (red_ms * 1e-3) / 1e9
     c4_alone = args.config == "C4" and world == 1 and args.emulate_world <= 1  # the profiled run
-    fit_traffic, tsrc = pmc_traffic("fit_kernel") if c4_alone else (None, None)
-    red_traffic, _ = pmc_traffic("reduce_kernel<2>") if tsrc else (None, None)
+    w_eff = args.emulate_world if args.emulate_world > 1 else world
+    shard_key = (f"{args.config}/w{w_eff}" if w_eff > 1 and args.scaling == "strong" and chunks == 1
+                 else None)  # rank 0's shard, profiled alone
+    if c4_alone or shard_key:
+        fit_traffic, tsrc = pmc_traffic("fit_kernel", shard_key)
+        red_traffic, _ = pmc_traffic("reduce_kernel<2>", shard_key)
+    else:
+        fit_traffic = red_traffic = tsrc = None
 
     out = {
         "metric": METRIC,

@@ -63,7 +63,11 @@ def main(d, out=None, traffic_json=None):
     if out:
         open(out, "w").write(text)
     if traffic_json:
-        json.dump({"source": os.path.basename(os.path.normpath(d)),
+        keep = {}
+        if os.path.exists(traffic_json):  # the shards' entries (scripts/pmc_shard_sum.py) stay
+            old = json.load(open(traffic_json))
+            keep = {k: old[k] for k in ("shards", "shards_method") if k in old}
+        json.dump({**keep, "source": os.path.basename(os.path.normpath(d)),
                    "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes of "
                              "`python3 bench.py --no-cpu-baseline`; bytes = (2 x FETCH_SIZE + "
                              "WRITE_SIZE) x 1024 per dispatch (gfx950 FETCH_SIZE correction)",
