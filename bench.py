@@ -276,7 +276,11 @@ def main():
 
     def step(prof=False):
         # reduce + spec ranks -> node prep + spec placement -> fit -> clamp correction,
-        # one stream
+        # one stream; one rank: the finalize rides in the clamp correction's launch
+        if world == 1 and args.chunks <= 1:
+            eng.capacity_async(h_ptr, ptr, cpu, mem, a_cpu, a_mem, a_pods, p_cnt, used_cpu,
+                               used_mem, s_cpu, s_mem, totals, err, stream=stream)
+            return
         eng.capacity_partial_async(h_ptr, ptr, cpu, mem, a_cpu, a_mem, a_pods, p_cnt, used_cpu,
                                    used_mem, s_cpu, s_mem, partial, n_chunks=args.chunks,
                                    stream=stream)

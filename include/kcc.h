@@ -183,6 +183,19 @@ int kcc_capacity_partial_async(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containe
                                uint64_t* d_used_cpu, int64_t* d_used_mem, int64_t n_specs,
                                const uint64_t* d_spec_cpu, const int64_t* d_spec_mem,
                                int64_t* d_partial, int n_chunks, void* stream);
+/* The whole step on one device without a cross-GPU exchange: kcc_capacity_partial_async
+ * (one chunk, the partial in a library buffer) followed by the finalize, which rides in
+ * the clamp correction's launch (its last workgroup to finish writes d_totals / d_spec_err):
+ * the same results as partial + kcc_fit_finalize_async, one launch fewer
+ * (ClusterCapacity.go:101-140 for a batch of specs, all on the device). */
+int kcc_capacity_async(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containers,
+                       const int64_t* h_node_ptr, const int64_t* d_node_ptr,
+                       const uint64_t* d_cpu_req, const int64_t* d_mem_req,
+                       const uint64_t* d_alloc_cpu, const int64_t* d_alloc_mem,
+                       const int64_t* d_alloc_pods, const int64_t* d_pod_count,
+                       uint64_t* d_used_cpu, int64_t* d_used_mem, int64_t n_specs,
+                       const uint64_t* d_spec_cpu, const int64_t* d_spec_mem, int64_t* d_totals,
+                       int32_t* d_spec_err, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Node sharding.  Nodes are independent and each per-spec total is a

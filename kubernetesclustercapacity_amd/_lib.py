@@ -46,6 +46,7 @@ SIGNATURES = {
     "kcc_fit_async": (_int, [_vp, _i64] + [_vp] * 6 + [_i64] + [_vp] * 5),
     "kcc_capacity_partial_async": (_int, [_vp, _i64, _i64] + [_vp] * 10 + [_i64] + [_vp] * 3
                                    + [_int, _vp]),
+    "kcc_capacity_async": (_int, [_vp, _i64, _i64] + [_vp] * 10 + [_i64] + [_vp] * 5),
     "kcc_set_node_shards": (_int, [_vp, _int]),
     "kcc_set_fit_dense": (_int, [_vp, _int]),
     "kcc_fit_stream_rows": (_int, [_vp, C.POINTER(_i64)]),

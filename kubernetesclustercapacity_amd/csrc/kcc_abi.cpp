@@ -91,6 +91,7 @@ struct Dev {
   // one-shot exchange over xGMI peer memory (kcc_p2p_*): this rank's mailbox (exported),
   // the push arrival counter and the flag-wait fault counter; the peers' mapped mailboxes
   DevBuf p2p_mbox, p2p_arrive, p2p_faults;
+  DevBuf clamp_arrive;  // clamp_apply's fused finalize: arrivals (zero between launches)
   unsigned char* p2p_peer[kcc::P2P_MAX_RANKS] = {};  // opened peer mailboxes (own: p2p_mbox)
   int p2p_W = 0, p2p_rank = -1;
   int64_t p2p_smax = 0;
@@ -484,7 +485,8 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                          const int64_t* mem, const uint64_t* alloc_cpu, const int64_t* alloc_mem,
                          const int64_t* alloc_pods, const int64_t* pod_count, uint64_t* used_cpu,
                          int64_t* used_mem, int64_t n_specs, const uint64_t* spec_cpu,
-                         const int64_t* spec_mem, int64_t* partial, int n_chunks, hipStream_t s) {
+                         const int64_t* spec_mem, int64_t* partial, int n_chunks, hipStream_t s,
+                         int64_t* totals = nullptr, int32_t* spec_err = nullptr) {
   ctx->host_stream_rows = -1;  // (kcc_fit_stream_rows: this call's device counters)
   if (n_nodes < 0 || n_cont < 0 || n_specs < 0) return fail(ctx, KCC_EINVAL, "negative size");
   if (n_nodes >= kcc::RED_MAX_NODES)
@@ -600,12 +602,22 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
       dv.prof_pending.push_back(pp);
     }
   }
-  // the pod-slot clamp of every chunk's fast rows, added back per spec
+  // the pod-slot clamp of every chunk's fast rows, added back per spec; totals != nullptr:
+  // the clamp launch's last workgroup also finalizes (no fit_finalize launch)
   if (n_specs > 0) {
+    const bool fuse_fin = totals && n_nodes > 0;
+    if (fuse_fin && !dv.clamp_arrive.p) {  // every launch leaves it zero
+      KCC_HIP(ctx, ensure(dv.clamp_arrive, 64));
+      KCC_HIP(ctx, hipMemsetAsync(dv.clamp_arrive.p, 0, 64, s));
+    }
+    const kcc::FinArgs fin{as<int32_t>(dv.sperm), totals, spec_err, as<uint32_t>(dv.clamp_arrive)};
     if (n_nodes > 0)
       KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, n_nodes, clamp_of(dv),
-                                           as<unsigned long long>(dv.counters), partial, s));
+                                           as<unsigned long long>(dv.counters), partial, s,
+                                           fuse_fin ? &fin : nullptr));
     dv.clamp_dirty = false;
+    if (totals && !fuse_fin)
+      return fit_finalize_dev(ctx, dv, n_specs, partial, totals, spec_err, s);
   }
   return KCC_OK;
 }
@@ -833,6 +845,7 @@ void kcc_destroy(kcc_ctx* ctx) {
       for (DevBuf* b : pb)
         if (b->p) (void)hipFree(b->p);
     }
+    if (dv.clamp_arrive.p) (void)hipFree(dv.clamp_arrive.p);
     DevBuf* bufs[] = {&dv.c_rank, &dv.c_bcnt, &dv.c_cs, &dv.c_ms,
                       &dv.c_mrc, &dv.c_crm, &dv.c_dperm, &dv.c_C, &dv.c_H2, &dv.c_H3,
                       &dv.c_Crow, &dv.c_rec, &dv.c_dir,
@@ -1034,6 +1047,26 @@ int kcc_capacity_partial_async(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containe
                               d_mem_req, d_alloc_cpu, d_alloc_mem, d_alloc_pods, d_pod_count,
                               d_used_cpu, d_used_mem, n_specs, d_spec_cpu, d_spec_mem, d_partial,
                               n_chunks, static_cast<hipStream_t>(stream));
+}
+
+int kcc_capacity_async(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containers,
+                       const int64_t* h_node_ptr, const int64_t* d_node_ptr,
+                       const uint64_t* d_cpu_req, const int64_t* d_mem_req,
+                       const uint64_t* d_alloc_cpu, const int64_t* d_alloc_mem,
+                       const int64_t* d_alloc_pods, const int64_t* d_pod_count,
+                       uint64_t* d_used_cpu, int64_t* d_used_mem, int64_t n_specs,
+                       const uint64_t* d_spec_cpu, const int64_t* d_spec_mem, int64_t* d_totals,
+                       int32_t* d_spec_err, void* stream) {
+  if (!ctx) return KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  if (n_specs > 0 && (!d_totals || !d_spec_err)) return fail(ctx, KCC_EINVAL, "NULL totals/err");
+  KCC_HIP(ctx, ensure(dv.partial, sizeof(int64_t) * 2 * (size_t)(n_specs > 0 ? n_specs : 1)));
+  return capacity_partial_dev(ctx, dv, n_nodes, n_containers, h_node_ptr, d_node_ptr, d_cpu_req,
+                              d_mem_req, d_alloc_cpu, d_alloc_mem, d_alloc_pods, d_pod_count,
+                              d_used_cpu, d_used_mem, n_specs, d_spec_cpu, d_spec_mem,
+                              as<int64_t>(dv.partial), 1, static_cast<hipStream_t>(stream),
+                              d_totals, d_spec_err);
 }
 
 int kcc_profile_enable(kcc_ctx* ctx, int on) {

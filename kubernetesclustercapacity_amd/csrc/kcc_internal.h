@@ -279,9 +279,9 @@ RankArgs rank_args(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spe
                    const ClampWork& cw, unsigned long long* counters, uint32_t* arrive);
 hipError_t launch_spec_rank(const RankArgs& ra, hipStream_t s);
 
-// spec_place's work (one thread per spec), run as extra workgroups in front of a
+// spec_place's work (one thread per spec), run as extra workgroups in front of the
 // node_prep launch (node_prep reads only the arrays spec_rank wrote, and not the padding
-// spec_place writes) or as a launch of its own: the stable 3-way partition position, the
+// spec_place writes): the stable 3-way partition position, the
 // SpecRec / perm there, dperm, mr_c / cr_m's padding, partial[0..2S) zeroed,
 // CNT_SPECS_A / CNT_SPECS_B set.
 struct PlaceArgs {
@@ -294,7 +294,6 @@ struct PlaceArgs {
   unsigned long long* counters;
   int32_t n_blocks;  // workgroups of the launch's block size (0: none)
 };
-hipError_t launch_spec_place(const PlaceArgs& pa, hipStream_t s);
 
 
 // counters (CNT_*): exact-path (node, spec) pairs, class-B specs, and per node chunk
@@ -314,8 +313,18 @@ enum {
 // The clamp correction after every node_prep of the call (n_nodes: the call's rows, for
 // the binned records' pass count): partial[s] -= D_s for the normal specs of clamp-free
 // waves; leaves the table copies zero.
+// fin != nullptr (one rank, the call's last kernel): the launch's last workgroup to finish
+// (an arrival counter, zero between launches) also finalizes — totals[perm[i]] = err ? 0 :
+// partial[i], spec_err[perm[i]] = err — instead of a fit_finalize launch.
+struct FinArgs {
+  const int32_t* perm;
+  int64_t* totals;
+  int32_t* spec_err;
+  uint32_t* arrive;
+};
 hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
-                              const unsigned long long* counters, int64_t* partial, hipStream_t s);
+                              const unsigned long long* counters, int64_t* partial, hipStream_t s,
+                              const FinArgs* fin = nullptr);
 
 // The fit's node stream (FitGroupA / FitGroup records) holds the rows that can contribute
 // to the fast sum Σ min(findMin(qc, qm), P): fast-bound rows with free CPU, free memory

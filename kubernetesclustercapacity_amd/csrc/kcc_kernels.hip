@@ -157,15 +157,12 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 // The lane offset (voff) is loop-invariant and the tile offset goes in soffset, so no
 // address VGPR is recomputed per tile (a recomputed address register that the
 // allocator shares with an in-flight load's destination forces a vmcnt(0) wait).
-#ifndef KCC_RED_LOAD_AUX
-#define KCC_RED_LOAD_AUX 0  // the loads' cache-policy bits (A/B builds)
-#endif
 __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff, int32_t soff,
                                           uint64_t (&x)[RED_IPL]) {
 #pragma unroll
   for (int h = 0; h < RED_IPL / 2; ++h) {
     const u64x2 v = __builtin_bit_cast(
-        u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16 * h, soff, KCC_RED_LOAD_AUX));
+        u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16 * h, soff, 0));
     x[2 * h] = v.x;
     x[2 * h + 1] = v.y;
   }
@@ -218,11 +215,7 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }
 
 template <int NA>
-__global__ __launch_bounds__(256)
-#ifdef KCC_RED_WAVES_PER_EU
-__attribute__((amdgpu_waves_per_eu(NA == 2 ? KCC_RED_WAVES_PER_EU : 1)))
-#endif
-void reduce_kernel(RedArgs a, RankArgs ra) {
+__global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
   __shared__ __attribute__((aligned(16))) uint64_t pre_s[RED_WAVES_PER_BLOCK][NA][RED_TILE];
   static_assert(sizeof(pre_s) >= 16 * RANK_L, "the rank workgroups stage RANK_L 16-B keys");
   if constexpr (NA == 2) {  // (launch_reduce: the ranks ride the 2-array reduce only)
@@ -1477,7 +1470,6 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   cw.dperm[x] = (int32_t)pos;
 }
 
-__global__ __launch_bounds__(256) void spec_place_kernel(PlaceArgs pa) { spec_place_body(pa, blockIdx.x); }
 
 // ---- clamp correction: D_s and partial[s] -= D_s (one launch) ----------------------
 // clamp_apply_kernel: 2T workgroups of 1024 threads, after the fit.
@@ -1623,22 +1615,18 @@ __device__ __forceinline__ void clamp_consume_bin(const ClampWork& cw, int64_t b
   }
 }
 
-__global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
-                                                                 const unsigned long long* __restrict__ counters,
-                                                                 int64_t S, int64_t* __restrict__ partial) {
+// One bin's part of the clamp correction (clamp_apply_kernel): every thread of the
+// workgroup enters and leaves together (the fused finalize's barrier follows).
+__device__ __forceinline__ void clamp_apply_bin(const ClampWork& cw, int64_t S,
+                                                int64_t* __restrict__ partial, int64_t nN,
+                                                int64_t u, uint32_t G, uint32_t h) {
   __shared__ uint64_t tab[H_CELLS];
   __shared__ uint64_t ctot[CP_WAVES][64];
   __shared__ uint64_t colsum[128];
   __shared__ uint32_t pos_s[64];          // the specs' kpos / jpos (wave 15 -> every wave)
   __shared__ uint32_t cp_lo[CP_PW];       // binned: a window's passes' bin starts
   __shared__ uint32_t cp_off[CP_PW + 1];  // and the exclusive prefix of their counts
-  const int64_t nN = clamp_n_normal(counters);
   const int64_t T = (nN + 63) / 64, W = T + 2;
-  // blockIdx = h * 2 Tm + u: part h of the G parts of bin u (launch_clamp_apply)
-  const int64_t Tm = (S + 63) / 64;
-  const uint32_t G = gridDim.x / (uint32_t)(2 * Tm), h = blockIdx.x / (uint32_t)(2 * Tm);
-  const int64_t u = blockIdx.x % (uint32_t)(2 * Tm);
-  if (u >= 2 * T) return;  // whole workgroup
   KCC_TL(1024 + blockIdx.x % 1024, 0);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const bool x_side = u < T;
@@ -1759,6 +1747,39 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   }
   if (d && p < clamp_n_pure(nN, S)) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[p]), 0ull - d);
   KCC_TL(1024 + blockIdx.x % 1024, 4);
+}
+
+__global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
+                                                                 const unsigned long long* __restrict__ counters,
+                                                                 int64_t S, int64_t* __restrict__ partial,
+                                                                 FinArgs fin) {
+  const int64_t nN = clamp_n_normal(counters);
+  const int64_t T = (nN + 63) / 64;
+  // blockIdx = h * 2 Tm + u: part h of the G parts of bin u (launch_clamp_apply)
+  const int64_t Tm = (S + 63) / 64;
+  const uint32_t G = gridDim.x / (uint32_t)(2 * Tm), h = blockIdx.x / (uint32_t)(2 * Tm);
+  const int64_t u = blockIdx.x % (uint32_t)(2 * Tm);
+  if (u < 2 * T) clamp_apply_bin(cw, S, partial, nN, u, G, h);  // (else: no bin)
+  if (!fin.totals) return;
+  // the fused finalize: every wave's atomics into partial are performed (vmcnt counts the
+  // stores and atomics too on gfx9) before the workgroup arrives; the last to arrive reads
+  // partial at agent scope
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ uint32_t last_s;
+  if (threadIdx.x == 0)
+    last_s = __hip_atomic_fetch_add(fin.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+             gridDim.x - 1u;
+  __syncthreads();
+  if (!last_s) return;
+  if (threadIdx.x == 0) __hip_atomic_store(fin.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int64_t i = threadIdx.x; i < S; i += CP_THREADS) {
+    const int64_t t = __hip_atomic_load(partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t e = __hip_atomic_load(partial + S + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int32_t dst = fin.perm[i];
+    fin.totals[dst] = e != 0 ? 0 : t;
+    fin.spec_err[dst] = e != 0 ? 1 : 0;
+  }
 }
 
 // clamp_crows_kernel (only when C does not fit clamp_apply's full form): one wave per row
@@ -2233,9 +2254,6 @@ int64_t resident_blocks(std::atomic<int64_t> (&cache)[MAX_DEVS], const void* ker
   return v;
 }
 
-#ifndef KCC_RED_WG_PER_CU
-#define KCC_RED_WG_PER_CU 0  // A/B: reduce workgroups per CU (0: the occupancy API's answer)
-#endif
 int64_t reduce_resident_waves(bool limits) {
   static std::atomic<int64_t> cache[2][MAX_DEVS];
   int64_t r = RED_WAVES_PER_BLOCK *
@@ -2243,13 +2261,6 @@ int64_t reduce_resident_waves(bool limits) {
                               limits ? reinterpret_cast<const void*>(reduce_kernel<4>)
                                      : reinterpret_cast<const void*>(reduce_kernel<2>),
                               256, 0, 2048);
-  if (KCC_RED_WG_PER_CU > 0 && !limits) {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        (int64_t)cus * KCC_RED_WG_PER_CU * RED_WAVES_PER_BLOCK < r)
-      r = (int64_t)cus * KCC_RED_WG_PER_CU * RED_WAVES_PER_BLOCK;
-  }
   return r;
 }
 }  // namespace
@@ -2386,16 +2397,9 @@ hipError_t launch_spec_rank(const RankArgs& ra, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_spec_place(const PlaceArgs& pa0, hipStream_t s) {
-  if (pa0.S <= 0) return hipSuccess;
-  PlaceArgs pa = pa0;
-  pa.n_blocks = (int32_t)((pa.S + 255) / 256);
-  hipLaunchKernelGGL(spec_place_kernel, dim3((unsigned)pa.n_blocks), dim3(256), 0, s, pa);
-  return hipGetLastError();
-}
-
 hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
-                              const unsigned long long* counters, int64_t* partial, hipStream_t s) {
+                              const unsigned long long* counters, int64_t* partial, hipStream_t s,
+                              const FinArgs* fin) {
   if (n_specs <= 0) return hipSuccess;
   cw.n_pass = clamp_passes(n_nodes);
   cw.pass_recs = 2 * clamp_pass_rows(n_nodes);
@@ -2413,8 +2417,9 @@ hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
   int64_t G = 1;
   if (clamp_binned(n_specs))
     while (G < KCC_CP_SPLIT && 2 * T * G * 2 <= resident) G *= 2;
+  const FinArgs f = fin ? *fin : FinArgs{};
   hipLaunchKernelGGL(clamp_apply_kernel, dim3((unsigned)(2 * T * G)), dim3(CP_THREADS), 0, s, cw,
-                     counters, n_specs, partial);
+                     counters, n_specs, partial, f);
   return hipGetLastError();
 }
 

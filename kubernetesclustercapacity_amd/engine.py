@@ -361,6 +361,18 @@ class CapacityEngine:
             _dp(used_cpu), _dp(used_mem), spec_cpu.numel(), _dp(spec_cpu), _dp(spec_mem),
             _dp(partial), int(n_chunks), _stream(stream)))
 
+    def capacity_async(self, h_node_ptr, node_ptr, cpu_req, mem_req, alloc_cpu, alloc_mem,
+                       alloc_pods, pod_count, used_cpu, used_mem, spec_cpu, spec_mem, totals,
+                       spec_err, stream=None):
+        """The whole one-device step (kcc_capacity_async): reduce + fit + clamp correction
+        with the finalize fused into the last launch -> totals (int64) / spec_err (int32)."""
+        h = None if h_node_ptr is None else np.ascontiguousarray(h_node_ptr, np.int64)
+        self._check(self._lib.kcc_capacity_async(
+            self._h, node_ptr.numel() - 1, cpu_req.numel(), _p(h), _dp(node_ptr), _dp(cpu_req),
+            _dp(mem_req), _dp(alloc_cpu), _dp(alloc_mem), _dp(alloc_pods), _dp(pod_count),
+            _dp(used_cpu), _dp(used_mem), spec_cpu.numel(), _dp(spec_cpu), _dp(spec_mem),
+            _dp(totals), _dp(spec_err), _stream(stream)))
+
     def parse_cpu_millis_async(self, buf, off, out, status, stream=None):
         self._check(self._lib.kcc_parse_cpu_millis_async(
             self._h, off.numel() - 1, _dp(buf), buf.numel(), _dp(off), _dp(out), _dp(status),

@@ -349,6 +349,36 @@ def test_device_api_matches_host(engine):
     assert pairs == n * s and 0 < slow < pairs
 
 
+@pytest.mark.parametrize("n,s,adv", [(20_000, 700, True), (9_000, 4097, False),
+                                     (6_000, 300, True), (0, 50, False)])
+def test_capacity_async_fused_finalize(engine, n, s, adv):
+    """kcc_capacity_async (the clamp correction's last workgroup finalizes) == the oracle,
+    three calls in a row (its arrival counter returns to zero), incl. > 4096 specs (C's row
+    suffixes), exact-path specs (adversarial) and no nodes (a finalize launch instead)."""
+    import torch
+    pods = 20 * n
+    c = synth.make_cluster(n, pods, seed=41, chunk=1024, adversarial=adv)
+    sc, sm = synth.make_specs(s, seed=41, adversarial=adv)
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+    used_cpu = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    used_mem = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    totals = torch.empty(s, dtype=torch.int64, device=dev)
+    err = torch.empty(s, dtype=torch.int32, device=dev)
+    uc, um, _, _ = coracle.reduce_requests(c.node_ptr, c.cpu_req, c.mem_req, c.cpu_lim, c.mem_lim)
+    ot, oe = coracle.fit(c.alloc_cpu, c.alloc_mem, c.alloc_pods, c.pod_count, uc, um, sc, sm, NT)
+    stream = torch.cuda.Stream(dev)
+    for _ in range(3):
+        totals.fill_(-7)
+        with torch.cuda.stream(stream):
+            engine.capacity_async(c.node_ptr, T(c.node_ptr), T(c.cpu_req), T(c.mem_req),
+                                  T(c.alloc_cpu), T(c.alloc_mem), T(c.alloc_pods), T(c.pod_count),
+                                  used_cpu, used_mem, T(sc), T(sm), totals, err, stream=stream)
+        stream.synchronize()
+        np.testing.assert_array_equal(totals.cpu().numpy(), ot)
+        np.testing.assert_array_equal(err.cpu().numpy(), oe)
+
+
 # ---- pipelined reduce + fit (node chunks, side stream) == host API ------------------------
 @pytest.mark.parametrize("n_chunks", [1, 2, 3, 4, 16])
 def test_pipelined_capacity_matches_host(engine, n_chunks):
