@@ -151,6 +151,14 @@ __device__ __forceinline__ int32_t rel_ptr(const int64_t* __restrict__ ptr, int6
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
+// cache policy of the container loads (A/B knob; 2 nt, 16 sc1, 18 nt sc1).  Measured
+// (round 3, one process, outputs identical): C4 reduce default 130.5 us, nt 181.8, sc1
+// 183.5, nt sc1 181.5; the 8-way shard 19.5 / 32.3 / 25.2 / 32.2 us: the 16-B lane loads
+// of a wave coalesce in L1, which every non-default policy bypasses
+#ifndef KCC_RED_LOAD_CPOL
+#define KCC_RED_LOAD_CPOL 0
+#endif
+
 // RED_IPL consecutive 64-bit values of one array for this lane: RED_IPL / 2 16-B
 // range-checked buffer loads (outside the descriptor's range they read 0), so the
 // prefetch is branch-free and never waits where it is issued.
@@ -162,7 +170,7 @@ __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff
 #pragma unroll
   for (int h = 0; h < RED_IPL / 2; ++h) {
     const u64x2 v = __builtin_bit_cast(
-        u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16 * h, soff, 0));
+        u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16 * h, soff, KCC_RED_LOAD_CPOL));
     x[2 * h] = v.x;
     x[2 * h + 1] = v.y;
   }
@@ -1773,12 +1781,26 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   __syncthreads();
   if (!last_s) return;
   if (threadIdx.x == 0) __hip_atomic_store(fin.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (int64_t i = threadIdx.x; i < S; i += CP_THREADS) {
-    const int64_t t = __hip_atomic_load(partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int64_t e = __hip_atomic_load(partial + S + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int32_t dst = fin.perm[i];
-    fin.totals[dst] = e != 0 ? 0 : t;
-    fin.spec_err[dst] = e != 0 ? 1 : 0;
+  // FIN_PER specs per thread per round, every load of the round issued before any store
+  // (one memory round trip per round: S <= 4096 is one round)
+  constexpr int FIN_PER = 4;
+  for (int64_t i0 = threadIdx.x; i0 < S; i0 += (int64_t)FIN_PER * CP_THREADS) {
+    int64_t t[FIN_PER], e[FIN_PER];
+    int32_t dst[FIN_PER];
+#pragma unroll
+    for (int k = 0; k < FIN_PER; ++k) {
+      // past the end: reload spec S-1 (branch-free, so no wait splits the batch)
+      const int64_t i = min(i0 + (int64_t)k * CP_THREADS, S - 1);
+      t[k] = __hip_atomic_load(partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      e[k] = __hip_atomic_load(partial + S + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      dst[k] = fin.perm[i];
+    }
+#pragma unroll
+    for (int k = 0; k < FIN_PER; ++k) {
+      if (i0 + (int64_t)k * CP_THREADS >= S) break;
+      fin.totals[dst[k]] = e[k] != 0 ? 0 : t[k];
+      fin.spec_err[dst[k]] = e[k] != 0 ? 1 : 0;
+    }
   }
 }
 
