@@ -1901,6 +1901,12 @@ static_assert(FIT_QCHUNK >= 2 && FIT_QCHUNK <= FIT_CHUNK_GROUPS, "claims sum in 
 #define KCC_FIT_WG_PER_SUB 24  // workgroups per sub-queue at most, about (8 to 32 sub-queues)
 #endif
 constexpr uint32_t FIT_QSUBS = (uint32_t)FIT_QSUBS_MAX;
+#ifndef KCC_FIT_GY_DIV
+// A/B knob: a 1/DIV share of the resident workgroups per column.  Measured (round 3,
+// prepare + run): C4 172 -> 220 / 372 us at DIV 2 / 4, its 8-way shard 57 -> 63 / 83 us:
+// the fit needs its 8 waves per SIMD on small shards too (profiles/r03o_ab_fit_grid.jsonl)
+#define KCC_FIT_GY_DIV 1
+#endif
 #ifndef KCC_FIT_ROUNDS
 #define KCC_FIT_ROUNDS 1  // queue grid: this many rounds of resident workgroups
 #endif
@@ -2461,7 +2467,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
   // one round of resident workgroups (the queue balances the waves; the stream's length
   // is only known on the device); a chunk of a pipelined call gets its node share of the
   // round; no more waves per column than claims at the full length
-  int64_t gy = KCC_FIT_ROUNDS * fit_resident_blocks() / gx;
+  int64_t gy = KCC_FIT_ROUNDS * fit_resident_blocks() / gx / KCC_FIT_GY_DIV;
   if (grid_nodes > n_nodes) gy = gy * n_nodes / grid_nodes;
   if (gy >= 16) gy = gy / 8 * 8;  // whole XCD rounds
   const int64_t claims = (n_groups + FIT_QCHUNK - 1) / FIT_QCHUNK;
