@@ -227,7 +227,8 @@ int kcc_allreduce_partial_async(kcc_ctx* ctx, int64_t n_specs, int64_t* d_partia
  * kcc_allreduce_partial_async + kcc_fit_finalize_async when each rank is one process on
  * its own GPU (<= 8 ranks, a 2*S int64 payload: latency-bound, so one push over the
  * full mesh beats a ring).  Setup, once: kcc_p2p_export allocates this rank's mailbox
- * (2 parities x n_ranks x (2 * max_specs) int64 + flags) and returns its IPC handle;
+ * (2 parities x n_ranks x (2 * max_specs) int64 + flags) in fine-grained, uncached device
+ * memory (peers write it while this GPU polls it) and returns its IPC handle;
  * every rank's handle travels to every rank (any channel: the bytes are opaque);
  * kcc_p2p_open maps the peers' mailboxes.  Each step: kcc_exchange_finalize_async (one
  * kernel on the caller's stream, after kcc_capacity_partial_async) pushes this rank's

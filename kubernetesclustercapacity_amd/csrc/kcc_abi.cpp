@@ -32,6 +32,21 @@ hipError_t ensure(DevBuf& b, size_t bytes) {
   return e;
 }
 
+// Fine-grained, uncached device memory (the p2p mailbox): peers write it over xGMI while
+// this device's kernel polls it, and a line of ordinary (coarse-grained) memory may be
+// served stale from this device's L2 — coarse-grained memory is only coherent with other
+// devices at synchronisation points.  Uncached loads and stores go to memory.
+hipError_t ensure_uncached(DevBuf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.bytes >= bytes) return hipSuccess;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+  hipError_t e = hipExtMallocWithFlags(&b.p, bytes, hipDeviceMallocUncached);
+  if (e == hipSuccess) b.bytes = bytes;
+  return e;
+}
+
 template <class T>
 T* as(DevBuf& b) {
   return static_cast<T*>(b.p);
@@ -1221,7 +1236,7 @@ int kcc_p2p_export(kcc_ctx* ctx, int n_ranks, int64_t max_specs, uint8_t* handle
   if (dv.p2p_W > 0) return fail(ctx, KCC_EINVAL, "mailbox already exported");
   KCC_HIP(ctx, hipSetDevice(dv.device));
   const size_t bytes = kcc::p2p_mbox_bytes(n_ranks, max_specs);
-  KCC_HIP(ctx, ensure(dv.p2p_mbox, bytes));
+  KCC_HIP(ctx, ensure_uncached(dv.p2p_mbox, bytes));
   KCC_HIP(ctx, ensure(dv.p2p_arrive, 64));
   KCC_HIP(ctx, ensure(dv.p2p_faults, 64));
   KCC_HIP(ctx, hipMemset(dv.p2p_mbox.p, 0, bytes));  // flags 0: no epoch seen
