@@ -175,11 +175,12 @@ def _worker_p2p(rank, world, port, n, pods, S, adversarial, steps, out):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_gpu_p2p_exchange_equals_whole(tmp_path, world):
+@pytest.mark.parametrize("world,S", [(2, 300), (3, 300), (4, 5000)])
+def test_gpu_p2p_exchange_equals_whole(tmp_path, world, S):
     """The one-shot xGMI exchange (bench --exchange p2p): every rank's finalized totals
-    after 3 steps == the oracle over the whole cluster, no flag wait gave up."""
-    n, pods, S, steps = 20_011, 300_000, 300, 3
+    after 3 steps == the oracle over the whole cluster, no flag wait gave up.  S = 5000:
+    the spec ranks by sort (S > 4096) and an exchange grid of 20 workgroups."""
+    n, pods, steps = 20_011, 300_000, 3
     out = str(tmp_path / "p2p")
     mp.spawn(_worker_p2p, args=(world, _free_port(), n, pods, S, True, steps, out), nprocs=world,
              join=True)
