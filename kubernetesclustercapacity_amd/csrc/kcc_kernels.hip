@@ -1891,6 +1891,9 @@ static_assert(FIT_QCHUNK >= 2 && FIT_QCHUNK <= FIT_CHUNK_GROUPS, "claims sum in 
 #ifndef KCC_FIT_QDIV
 #define KCC_FIT_QDIV 2  // guided claims: (what remains of the segment) / (QDIV x its workgroups)
 #endif
+#ifndef KCC_FIT_QEST
+#define KCC_FIT_QEST 0  // guided claims sized from the head estimated after the others' claims
+#endif
 #ifndef KCC_FIT_QMIN
 #define KCC_FIT_QMIN 2  // node groups per claim at least (guided claims)
 #endif
@@ -2124,7 +2127,14 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     for (uint32_t k = 0;; ++k) {
       const uint32_t cur = base + (k == 0 ? first : __builtin_amdgcn_readfirstlane(q_slot[k & 1u]));
       if (cur >= lim) break;  // workgroup-uniform
-      uint32_t qn = (lim - cur) / ((uint32_t)KCC_FIT_QDIV * wps);
+      uint32_t rem = lim - cur;
+#if KCC_FIT_QEST
+      // cur is where the queue head stood a chunk ago: the segment's other workgroups have
+      // claimed about a chunk each since
+      const uint32_t ahead = (wps - 1u) * qcur;
+      rem = rem > ahead ? rem - ahead : 0u;
+#endif
+      uint32_t qn = rem / ((uint32_t)KCC_FIT_QDIV * wps);
       qn = qn < (uint32_t)KCC_FIT_QMIN ? (uint32_t)KCC_FIT_QMIN : (qn > qsz ? qsz : qn);
       claim_issue(qn);
       const int cnt = (int)((cur + qcur < lim ? cur + qcur : lim) - cur);
