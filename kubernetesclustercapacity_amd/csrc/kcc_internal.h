@@ -5,12 +5,13 @@
 #include <stdint.h>
 
 // Diagnostic timing knobs produce wrong results by design (no stores, no atomics,
-// searches skipped) or add stamp stores: only experiment builds (csrc/Makefile `variant`,
+// searches skipped), add stamp stores, or are unsafe beside other kernels
+// (KCC_RED_XCD_MAP: a look-back may wait on an undispatched wave): only experiment builds (csrc/Makefile `variant`,
 // which defines KCC_VARIANT_BUILD and writes a separate .so) may set them.
 #if !defined(KCC_VARIANT_BUILD) &&                                                       \
     (defined(KCC_FIT_DIAG_NO_ATOMICS) || defined(KCC_DIAG_RED_NOSTORE) ||                \
      defined(KCC_DIAG_RED_LOADONLY) || defined(KCC_DIAG_NP) || defined(KCC_DIAG_CP) ||   \
-     defined(KCC_TIMELINE))
+     defined(KCC_TIMELINE) || defined(KCC_RED_XCD_MAP))
 #error "a diagnostic KCC_* knob in a release build: use `make variant` (KCC_VARIANT_BUILD)"
 #endif
 

@@ -151,6 +151,9 @@ __device__ __forceinline__ int32_t rel_ptr(const int64_t* __restrict__ ptr, int6
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
+#ifndef KCC_RED_XCD_MAP
+#define KCC_RED_XCD_MAP 0
+#endif
 // cache policy of the container loads (A/B knob; 2 nt, 16 sc1, 18 nt sc1).  Measured
 // (round 3, one process, outputs identical): C4 reduce default 130.5 us, nt 181.8, sc1
 // 183.5, nt sc1 181.5; the 8-way shard 19.5 / 32.3 / 25.2 / 32.2 us: the 16-B lane loads
@@ -237,9 +240,24 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
   const int32_t range = a.range;
   const int64_t* __restrict__ ptr = a.ptr;
   // wave index made provably uniform (T20: no waterfall loops around the buffer ops)
+#if KCC_RED_XCD_MAP
+  // A/B knob (variant builds only): the workgroups of one XCD (blockIdx % 8) take one
+  // contiguous eighth of the ranges (a bijection of the grid), so each XCD's L2 and
+  // translation caches see one eighth of the arrays.  Measured (round 3, r03t): C4 130.8
+  // -> 131.4 us, its 8-way shard 19.7 -> 18.8 us.  Not shipped: a wave's look-back
+  // predecessor may then be dispatched after it, so the waits are safe only while every
+  // wave of the launch is resident at once, which kernels of another stream or process
+  // sharing the GPU can prevent (dispatch order = range order rules that out)
+  const uint32_t rb_ = blockIdx.x - (uint32_t)ra.n_blocks, nb_ = gridDim.x - (uint32_t)ra.n_blocks;
+  const uint32_t xq_ = rb_ & 7u, q8_ = nb_ >> 3, r8_ = nb_ & 7u;
+  const uint32_t lb_ = xq_ * q8_ + (xq_ < r8_ ? xq_ : r8_) + (rb_ >> 3);
+  const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)(lb_ * RED_WAVES_PER_BLOCK +
+                                                             (threadIdx.x >> 6)));
+#else
   const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)((blockIdx.x - ra.n_blocks) *
                                                              RED_WAVES_PER_BLOCK +
                                                              (threadIdx.x >> 6)));
+#endif
   // containers [c0, n_cont): absolute indices, like the offsets in ptr (node indices
   // are local to the launch)
   const int64_t wb = c0 + (int64_t)w * range;
