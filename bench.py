@@ -39,6 +39,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 #  - issue peak: one wave64 VALU instruction per SIMD per 4 cycles (PMC: every
 #    SQ_INSTS_VALU costs one SQ_ACTIVE_INST_VALU quad-cycle), 256 CUs x 4 SIMDs x 2.4 GHz.
 FIT_VALU_PER_NODE_WAVE = 3.0
+# the same loop with the pod-slot clamp applied inside it (kcc_set_clamp_in_fit; small
+# shards): min, compare, a move of the clamp value, select (tests/test_isa.py)
+FIT_NC_VALU_PER_NODE_WAVE = 6.0
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions / s
 METRIC = "node×spec fit evals/sec at 1M nodes × 4K specs; % of HBM roofline"
 # per-launch HBM traffic of each kernel from rocprofv3 PMC passes of this same bench
@@ -77,6 +80,9 @@ def parse():
                     help="node chunks of the pipelined step (reduce of chunk k overlaps the fit "
                          "of chunk k-1); 1 = reduce, then fit")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--clamp-in-fit", type=int, default=-1, choices=[-1, 0, 1],
+                    help="pod-slot clamp inside the fit: -1 by shard size (default), 0 never "
+                         "(clamp correction launch), 1 whenever specs <= 4096")
     ap.add_argument("--no-dense", action="store_true",
                     help="skip the dense-layout comparison steps (every row through the fit)")
     ap.add_argument("--no-pods", action="store_true",
@@ -238,6 +244,7 @@ def main():
 
     eng = CapacityEngine(local, 1)
     eng.reserve(n, C, S)
+    eng.set_clamp_in_fit(args.clamp_in_fit)
     stream = torch.cuda.Stream(dev)
     exchange_note = None
     if world > 1 and exchange == "p2p":
@@ -345,13 +352,15 @@ def main():
     # the fit's node stream: the rows that can add to its fast sum (free CPU, free memory,
     # pods > 0; every other row adds exactly 0 there), compacted by node_prep
     streamed = eng.fit_stream_rows()
+    clamp_in_fit = eng.clamp_in_fit_used()
+    valu_pn = FIT_NC_VALU_PER_NODE_WAVE if clamp_in_fit else FIT_VALU_PER_NODE_WAVE
 
     # algorithmic bytes per launch (DESIGN.md "Roofline accounting"): a step runs
     # `chunks` reduce launches and `chunks` fit launches over node ranges of ~n/chunks
-    fit_bytes = (streamed * 16 + chunks * (S * 48 + S * 8)) / chunks  # FitGroupA + specs in, totals out
+    fit_bytes = (streamed * (20 if clamp_in_fit else 16) + chunks * (S * 48 + S * 8)) / chunks  # FitGroupA (+ clamp values) + specs in, totals out
     red_bytes = (C * 16 + (n + 1) * 8 + n * 16) / chunks       # requests + CSR offsets in, sums out
     fit_gbs = fit_bytes / (fit_ms * 1e-3) / 1e9
-    fit_valu = streamed / chunks * ((S + 63) // 64) * FIT_VALU_PER_NODE_WAVE / (fit_ms * 1e-3)
+    fit_valu = streamed / chunks * ((S + 63) // 64) * valu_pn / (fit_ms * 1e-3)
     red_gbs = red_bytes / (red_ms * 1e-3) / 1e9
     c4_alone = args.config == "C4" and world == 1 and args.emulate_world <= 1  # the profiled run
     w_eff = args.emulate_world if args.emulate_world > 1 else world
@@ -360,6 +369,8 @@ def main():
     if c4_alone or shard_key:
         fit_traffic, tsrc = pmc_traffic("fit_kernel", shard_key)
         red_traffic, _ = pmc_traffic("reduce_kernel<2>", shard_key)
+        if clamp_in_fit:  # (the PMC passes profiled the clamp-correction layout)
+            fit_traffic = None
     else:
         fit_traffic = red_traffic = tsrc = None
 
@@ -402,16 +413,23 @@ def main():
             "traffic_source": tsrc and f"profiles/pmc_traffic.json ({tsrc}); bytes per launch",
             "bytes_per_launch": fit_bytes, "ms_per_launch": fit_ms,
             "note": "the fit is VALU-bound (min(findMin(qc, qm), P) per node and spec, "
-                    "3 VALU per node and 64-spec wave): see roofline_valu",
+                    f"{valu_pn:g} VALU per node and 64-spec wave): see roofline_valu",
         },
         "roofline_valu": {
             "bound": "valu", "kernel": "fit_kernel", "achieved": fit_valu / 1e9,
             "peak": VALU_ISSUE_PEAK / 1e9, "unit": "G wave-instr/s",
             "frac": fit_valu / VALU_ISSUE_PEAK,
-            "valu_per_node_wave": FIT_VALU_PER_NODE_WAVE,
+            "valu_per_node_wave": valu_pn,
             "fit_evals_per_s": n / chunks * S / (fit_ms * 1e-3),
             "fit_streamed_pairs_per_s": streamed / chunks * S / (fit_ms * 1e-3),
             "note": "counted over the streamed rows (the instructions the kernel issues)",
+        },
+        "clamp": {
+            "in_fit": clamp_in_fit, "mode": args.clamp_in_fit,
+            "note": ("the pod-slot clamp (CC:134-135) inside the fit: 6 VALU per node x wave, no "
+                     "clamp_apply launch (small shards)" if clamp_in_fit else
+                     "the pod-slot clamp by the clamp correction (clamp_apply launch), the fit "
+                     "at 3 VALU per node x wave"),
         },
         "fit_stream": {
             "rows": n, "rows_streamed": streamed, "fraction": streamed / max(n, 1),

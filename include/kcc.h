@@ -270,6 +270,17 @@ int kcc_reduce_faults(kcc_ctx* ctx, int64_t* faults);
  * kcc_fit_stream_rows: node rows (padded to groups of 8) the last fit streamed, summed
  * over its node chunks (synchronises the device). */
 int kcc_set_fit_dense(kcc_ctx* ctx, int dense);
+/* Where the pod-slot clamp (CC:134-135, x >= allocatable pods ? allocatable - pod count : x)
+ * is applied by kcc_capacity_partial_async / kcc_capacity_async: by the clamp correction
+ * (a dominance count over the specs, one launch of its own; the fit's loop stays at 3 VALU
+ * per node and spec wave) or inside the fit (5 VALU, no clamp launch, no clamp tables:
+ * cheaper on small shards).  mode -1 (default): inside the fit when node rows x specs <=
+ * 1.1e9 and specs <= 4096; 0: never; 1: whenever specs <= 4096 (one node chunk, not dense).
+ * The totals are the same bit for bit either way. */
+int kcc_set_clamp_in_fit(kcc_ctx* ctx, int mode);
+/* 1 when the last kcc_capacity_partial_async / kcc_capacity_async of the context applied
+ * the clamp inside the fit (its VALU accounting: 6 per node x wave, not 3). */
+int kcc_clamp_in_fit_used(kcc_ctx* ctx, int* used);
 int kcc_fit_stream_rows(kcc_ctx* ctx, int64_t* streamed);
 
 /* Fraction of (node, spec) pairs of the last kcc_fit* call that took the exact

@@ -49,6 +49,8 @@ SIGNATURES = {
     "kcc_capacity_async": (_int, [_vp, _i64, _i64] + [_vp] * 10 + [_i64] + [_vp] * 5),
     "kcc_set_node_shards": (_int, [_vp, _int]),
     "kcc_set_fit_dense": (_int, [_vp, _int]),
+    "kcc_set_clamp_in_fit": (_int, [_vp, _int]),
+    "kcc_clamp_in_fit_used": (_int, [_vp, C.POINTER(C.c_int)]),
     "kcc_fit_stream_rows": (_int, [_vp, C.POINTER(_i64)]),
     "kcc_reduce_faults": (_int, [_vp, C.POINTER(_i64)]),
     "kcc_comm_unique_id": (_int, [_vp]),

@@ -92,6 +92,9 @@ struct Dev {
   int64_t h_stride = 0;    // cells per copy of the clamp tables H2 / H3
   int64_t d_stride = 0;    // words per pass of the binned records' directory
   bool fit_dense = false;  // kcc_set_fit_dense: stream every node row through the fit
+  int clamp_in_fit = -1;   // kcc_set_clamp_in_fit: -1 by size (clamp_in_fit_auto), 0 never, 1 always
+  bool last_nc = false;    // the last capacity call applied the clamp in the fit
+  DevBuf fast_cl;          // the clamp in the fit: each streamed row's clamp value
   int stream_chunks = 0;   // node chunks of the last fit prepare (their stream counters)
   int64_t prep_nodes = -1, prep_specs = -1;  // sizes the workspace was last prepared for
   // staging of the host-array entry points
@@ -258,6 +261,7 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   }
   KCC_HIP(ctx, ensure(dv.fast_a, sizeof(kcc::FitGroupA) * (size_t)kcc::fit_groups((int64_t)N)));
   KCC_HIP(ctx, ensure(dv.fast_b, sizeof(kcc::FitGroup) * (size_t)kcc::fit_groups((int64_t)N)));
+  KCC_HIP(ctx, ensure(dv.fast_cl, sizeof(int32_t) * kcc::FIT_GROUP * (size_t)kcc::fit_groups((int64_t)N)));
   KCC_HIP(ctx, ensure(dv.slow, sizeof(kcc::SlowNode) * N));
   KCC_HIP(ctx, ensure(dv.slow_list, sizeof(int64_t) * N));
   KCC_HIP(ctx, ensure(dv.srec, sizeof(kcc::SpecRec) * S));
@@ -554,6 +558,12 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   // place, fit, clamp_apply
   const bool fuse_place = n_specs > 0;
   const bool fuse_rank = k == 1 && fuse_place && n_nodes > 0 && n_cont > 0;
+  // the clamp in the fit (one node chunk, S <= CLAMP_LDS_SPECS, not dense): no clamp_apply
+  const bool nc = k == 1 && n_specs > 0 && n_specs <= kcc::CLAMP_LDS_SPECS && !dv.fit_dense &&
+                  (dv.clamp_in_fit == 1 ||
+                   (dv.clamp_in_fit < 0 && kcc::clamp_in_fit_auto(n_nodes, n_specs)));
+  int32_t* const fast_cl = nc ? as<int32_t>(dv.fast_cl) : nullptr;
+  dv.last_nc = nc;
   const kcc::RankArgs ra = kcc::rank_args(n_specs, spec_cpu, spec_mem, clamp_of(dv),
                                           as<unsigned long long>(dv.counters),
                                           as<uint32_t>(dv.rank_arrive));
@@ -597,7 +607,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                        as<int64_t>(dv.slow_list) + lo[c], n_specs, clamp_of(dv),
                                        as<unsigned long long>(dv.counters),
                                        c, lo[c], n_nodes, s, dv.fit_dense,
-                                       place_here ? &pa : nullptr));
+                                       place_here ? &pa : nullptr, fast_cl));
     if (n == 0) continue;
     ProfPair pp{};
     if (dv.prof_on) {
@@ -610,7 +620,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                  as<kcc::SlowNode>(dv.slow) + lo[c],
                                  as<int64_t>(dv.slow_list) + lo[c], n_specs, spec_prep_of(dv),
                                  partial, as<unsigned long long>(dv.counters),
-                                 as<uint32_t>(dv.fit_q), c, n_nodes, s));
+                                 as<uint32_t>(dv.fit_q), c, n_nodes, s, fast_cl));
     if (dv.prof_on) {
       KCC_HIP(ctx, hipEventRecord(pp.b, s));
       pp.kind = 1;
@@ -619,6 +629,11 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   }
   // the pod-slot clamp of every chunk's fast rows, added back per spec; totals != nullptr:
   // the clamp launch's last workgroup also finalizes (no fit_finalize launch)
+  if (n_specs > 0 && nc) {  // the fit applied the clamp: no clamp_apply, nothing dirty
+    dv.clamp_dirty = false;
+    if (totals) return fit_finalize_dev(ctx, dv, n_specs, partial, totals, spec_err, s);
+    return KCC_OK;
+  }
   if (n_specs > 0) {
     const bool fuse_fin = totals && n_nodes > 0;
     if (fuse_fin && !dv.clamp_arrive.p) {  // every launch leaves it zero
@@ -1141,6 +1156,20 @@ int kcc_fit_slow_pairs(kcc_ctx* ctx, int64_t* slow_pairs, int64_t* pairs) {
 int kcc_set_fit_dense(kcc_ctx* ctx, int dense) {
   if (!ctx) return KCC_EINVAL;
   for (Dev& dv : ctx->devs) dv.fit_dense = dense != 0;
+  return KCC_OK;
+}
+
+int kcc_clamp_in_fit_used(kcc_ctx* ctx, int* used) {
+  if (!ctx || !used) return KCC_EINVAL;
+  *used = 0;
+  for (const Dev& dv : ctx->devs) *used |= dv.last_nc ? 1 : 0;
+  return KCC_OK;
+}
+
+int kcc_set_clamp_in_fit(kcc_ctx* ctx, int mode) {
+  if (!ctx) return KCC_EINVAL;
+  if (mode < -1 || mode > 1) return fail(ctx, KCC_EINVAL, "mode: -1 (by size), 0 or 1");
+  for (Dev& dv : ctx->devs) dv.clamp_in_fit = mode;
   return KCC_OK;
 }
 

@@ -306,7 +306,8 @@ enum {
   CNT_SLOW_PAIRS = 0,  // (node, spec) pairs evaluated on the exact path
   CNT_SPECS_A = 1,     // class-A specs (internal positions [0, nA))
   CNT_SPECS_B = 2,     // class-B specs (internal positions [nA, nA + nB))
-  CNT_SPARE = 3,       // (unused)
+  CNT_CLAMP_ALL = 3,   // clamp in the fit: Σ (max(P, 0) - clamp) of the rows clamped for
+                       // every spec (P <= 0), subtracted from every normal spec by the fit
   CNT_SLOW_ROWS = 4,   // + chunk: rows in that node chunk's slow_list
   CNT_STREAM = 4 + FIT_MAX_CHUNKS,  // + chunk: node rows in that chunk's fit stream (x 8)
   CNT_N = 4 + 2 * FIT_MAX_CHUNKS
@@ -344,14 +345,26 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             SlowNode* slow, int64_t* slow_list, int64_t n_specs, ClampWork cw,
                             unsigned long long* counters, int chunk, int64_t row0,
                             int64_t call_nodes, hipStream_t s, bool dense = false,
-                            const PlaceArgs* place = nullptr);
+                            const PlaceArgs* place = nullptr, int32_t* fast_cl = nullptr);
+// Clamp in the fit (fast_cl != nullptr; one node chunk, S <= CLAMP_LDS_SPECS, not dense):
+// node_prep streams each row's clamp value (allocatable pods - pod count, CC:135) beside
+// its FitGroupA (fast_cl[row position]) and builds no clamp tables; the fit computes the
+// reference's x >= P ? clamp : x itself (5 VALU per node x wave instead of 3) and
+// subtracts counters[CNT_CLAMP_ALL] from every normal spec; no clamp_apply launch.  The
+// choice for small shards, where clamp_apply's fixed cost exceeds the fit's extra issue.
+#ifndef KCC_CLAMP_IN_FIT_PAIRS
+#define KCC_CLAMP_IN_FIT_PAIRS 1100000000LL  // node rows x specs at most: the C4 8-way (5.1e8) and 4-way (1.0e9) shards
+#endif
+inline bool clamp_in_fit_auto(int64_t n_nodes, int64_t n_specs) {
+  return n_specs <= CLAMP_LDS_SPECS && n_nodes * n_specs <= KCC_CLAMP_IN_FIT_PAIRS;
+}
 
 // partial[0..S) += Σ_i q(i,s), partial[S..2S) += #div-by-zero rows (internal order).
 hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,
                       const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, uint32_t* queue, int chunk,
-                      int64_t grid_nodes, hipStream_t s);
+                      int64_t grid_nodes, hipStream_t s, const int32_t* fast_cl = nullptr);
 // the fit's work queues: fit_queue_words(S) uint32 (a 64-B line per spec column of 256 and
 // sub-queue), zero before the first launch (each launch leaves them zero)
 constexpr int64_t FIT_QSUBS_MAX = 32;

@@ -678,7 +678,10 @@ __host__ __device__ inline uint32_t np_stride(int64_t S) {  // smallest power of
 // carries only its own path's registers).  A pass is SUB x 1024 rows (clamp_pass_rows(n)
 // of the call), worked on in SUB sub-steps of one row per thread; each sub-step's rows
 // are loaded while the previous one is worked on.
-template <int MODE, int SUB>
+// NC: the clamp in the fit (launch_node_prep's fast_cl; MODE 2 only): no search or count
+// tables, no clamp cells or records; each streamed row's clamp value goes to fast_cl and the
+// rows clamped for every spec sum into counters[CNT_CLAMP_ALL].
+template <int MODE, int SUB, bool NC>
 __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t n, const uint64_t* __restrict__ alloc_cpu,
                                  const int64_t* __restrict__ alloc_mem,
                                  const int64_t* __restrict__ alloc_pods,
@@ -689,7 +692,9 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
                                  SlowNode* __restrict__ slow, int64_t* __restrict__ slow_list,
                                  int64_t S, ClampWork cw,
                                  unsigned long long* __restrict__ counters,
-                                 int32_t chunk, int32_t dense, int64_t pass0, PlaceArgs pa) {
+                                 int32_t chunk, int32_t dense, int64_t pass0, PlaceArgs pa,
+                                 int32_t* __restrict__ fast_cl) {
+  static_assert(!NC || MODE == 2, "the clamp in the fit: S <= CLAMP_LDS_SPECS only");
   if ((int32_t)blockIdx.x < pa.n_blocks) {  // spec_place's workgroups, in front (MODE 2)
     spec_place_body(pa, blockIdx.x);
     return;
@@ -762,7 +767,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   for (int b = threadIdx.x; b < NP_BINS; b += KCC_NODE_PREP_BLOCK) np_bcnt[b] = 0;
   constexpr int PER = (int)(CLAMP_LDS_SPECS / KCC_NODE_PREP_BLOCK);
   uint32_t yv[PER];  // y-rank of x-rank tid + 1024 u
-  if (srch) {
+  if (srch && !NC) {
     // the sorted requests (spec_rank's last arrivers write them): every load first, guarded by S (a kernel argument) rather than nN, so they
     // travel with the class counts' load (one memory round trip); entries nN.. are masked
     uint64_t cv[PER], mv[PER];
@@ -788,7 +793,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   }
   __syncthreads();  // masks zero
   KCC_TL(bid % 1024, 6);
-  if (lds) {
+  if (lds && !NC) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int64_t x = threadIdx.x + (int64_t)KCC_NODE_PREP_BLOCK * u;
@@ -801,11 +806,11 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   KCC_TL(bid % 1024, 7);
   // smallest normal requests (rows below either dominate no spec): the tables' first
   // entries (+inf when there are none; cs[0] >= 1; MODE 1's LDS tables are sampled)
-  const uint32_t cmin = lds ? cs_l[np_slot(0u)]
+  const uint32_t cmin = NC ? 0u : lds ? cs_l[np_slot(0u)]
                             : (nN > 0 ? (cw.cs[0] < FAST_FC_MAX ? (uint32_t)cw.cs[0] : 0xffffffffu)
                                       : 0xffffffffu);
-  const int64_t mmin = lds ? ms_l[np_slot(0u)] : (nN > 0 ? cw.ms[0] : INT64_MAX);
-  if (lds) {  // the prefix counts: row g along Y and column Y = g along G, lane = index;
+  const int64_t mmin = NC ? 0 : lds ? ms_l[np_slot(0u)] : (nN > 0 ? cw.ms[0] : INT64_MAX);
+  if (lds && !NC) {  // the prefix counts: row g along Y and column Y = g along G, lane = index;
     // rows g and g + 16 in one 32-bit scan of four byte fields (each count and prefix is
     // a member count of one x-group or y-block, <= 64: no carries between the bytes)
     static_assert(KCC_NODE_PREP_BLOCK == 1024, "16 waves: rows wv, wv + 16, wv + 32, wv + 48");
@@ -845,6 +850,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
     uint64_t r_fm[SUB];
     uint32_t r_fc[SUB];
     int32_t r_P[SUB];
+    int32_t r_cl[SUB];  // NC: the clamp value of a streamed row
     unsigned long long sbal[SUB];
     uint32_t pk1[SUB], pk2[SUB], pk3[SUB];
     uint64_t always_sum = 0;
@@ -920,6 +926,10 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       const int64_t P = r_P[q], Penc = P > 0 ? P : 0;
       const int64_t wfull = Penc - (int64_t)cl_q;  // contribution = min(x, Penc) - w when clamped
       if (ok && nN > 0 && P <= 0) always_sum += (uint64_t)wfull;  // x >= P for every spec
+      r_cl[q] = cl_q;
+      if constexpr (NC) {
+        pk1[q] = pk2[q] = pk3[q] = 0u;
+      } else {
       const double rP = recip_up_f64(P > 0 ? (uint64_t)P : 1ull);
       const uint32_t U0 = (uint32_t)((double)r_fc[q] * rP);
       const int64_t V0 = (int64_t)((double)r_fm[q] * rP);
@@ -997,6 +1007,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       pk1[q] = (rec2 ? k * 64 + rx : 0u) | (rec3 ? j * 64 + ry : 0u) << 13 | (wu & 63u) << 26;
       pk2[q] = rk2 | rk3 << 13 | ((wu >> 6) & 63u) << 26;
       pk3[q] = bin2 | bin3 << 9 | (uint32_t)((int32_t)wu >> 12) << 18;
+      }  // (!NC)
       // the scheduler keeps each sub-step to itself (hoisting the next one's work
       // across this point ran the SUB = 4 kernels out of registers)
       __builtin_amdgcn_sched_barrier(0);
@@ -1005,7 +1016,11 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       uint64_t v = always_sum;
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-      if (lane == 0 && v) c_add((T + 1) * W + T + 1, (int64_t)v);
+      if (NC) {
+        if (lane == 0 && v) atomicAdd(&counters[CNT_CLAMP_ALL], (unsigned long long)v);
+      } else if (lane == 0 && v) {
+        c_add((T + 1) * W + T + 1, (int64_t)v);
+      }
     }
     if (threadIdx.x == 0) {
       np_base = base_ret;
@@ -1013,7 +1028,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
     }
     __syncthreads();  // np_base, and every record's rank
     KCC_TL(bid % 1024, 4);
-    if (binned && wv == 1) {
+    if (binned && !NC && wv == 1) {
       // the bins' starts: runs of per bins per lane, a shuffle scan of the run totals;
       // the pass's directory row (starts + total) goes out here, the counters return to 0
       const int per = (NB + 63) / 64;
@@ -1044,8 +1059,9 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       const uint64_t sb0 = np_base + before;
       const uint32_t tot = np_tot;
       const uint32_t pad = (tot + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP - tot;
-      auto put = [&](uint64_t pos, uint64_t fmv, uint32_t fcv, uint32_t Pv) {
+      auto put = [&](uint64_t pos, uint64_t fmv, uint32_t fcv, uint32_t Pv, int32_t clv) {
         const int kk = (int)(pos % FIT_GROUP);
+        if (NC) fast_cl[pos] = clv;
         FitGroupA& a = fast_a[pos / FIT_GROUP];
         a.fm[kk] = fmv;
         a.fc[kk] = fcv;
@@ -1063,7 +1079,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       for (int q = 0; q < SUB; ++q) {
         if (!(KCC_DIAG_NP & 8) && ((sbal[q] >> lane) & 1ull))  // P <= 0 streams only in the dense layout, as P = 0
           put(sb0 + done + (uint32_t)__popcll(sbal[q] & ((1ull << lane) - 1ull)), r_fm[q], r_fc[q],
-              r_P[q] > 0 ? (uint32_t)r_P[q] : 0u);
+              r_P[q] > 0 ? (uint32_t)r_P[q] : 0u, r_cl[q]);
         done += (uint32_t)__popcll(sbal[q]);
         const uint32_t c2 = pk1[q] & 0x1fffu, c3 = (pk1[q] >> 13) & 0x1fffu;
         if (c2 | c3) {
@@ -1073,12 +1089,12 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
           if (c3) prec[np_bstart[(pk3[q] >> 9) & 0x1ffu] + ((pk2[q] >> 13) & 0x1fffu)] = wbits | c3;
         }
       }
-      if (threadIdx.x < pad) put(np_base + tot + threadIdx.x, 0ull, 0u, 0u);  // the last group's padding
+      if (threadIdx.x < pad) put(np_base + tot + threadIdx.x, 0ull, 0u, 0u, 0);  // the last group's padding
     }
     __syncthreads();  // np_wc / np_base / np_bstart are rewritten by the next pass
     KCC_TL(bid % 1024, 5);
   }
-  if (cpriv) {  // the private C into this workgroup's device copy: its non-zero cells
+  if (cpriv && !NC) {  // the private C into this workgroup's device copy: its non-zero cells
     for (int64_t e = threadIdx.x; e < W * W; e += KCC_NODE_PREP_BLOCK) {
       const unsigned long long v = c_l[e];
       if (v) np_atomic(&Cc[e], (int64_t)v);
@@ -1966,7 +1982,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     const FitGroup* __restrict__ fast_b, const SlowNode* __restrict__ slow,
     const int64_t* __restrict__ slow_list, int64_t S, const SpecRec* __restrict__ specs,
     int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t chunk,
-    int32_t gx, int32_t gy) {
+    int32_t gx, int32_t gy, const int32_t* __restrict__ fast_cl) {
   // XCD-aware order (speed only, never correctness): workgroups are dealt round-robin
   // over the 8 XCDs, so give every spec group of one node chunk the same b % 8
   const int32_t b = blockIdx.x, xcd = b & 7, r = b >> 3;
@@ -2106,6 +2122,76 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     set_round_nearest();
     acc += (uint64_t)(int64_t)acc32;
   };
+  // the clamp in the fit (fast_cl: launch_node_prep's NC mode): x >= P ? clamp : x per
+  // node (CC:133-136), the clamp value from fast_cl, P >= 1 on every streamed row (padding:
+  // x = 0 >= P = 0, clamp 0)
+  auto sum_a_nc = [&](uint32_t g0, int cnt) {
+    cnt = __builtin_amdgcn_readfirstlane(cnt);
+    const FitGroupA* gbase = fast_a + g0;
+    const int32_t* cbase = fast_cl + (size_t)g0 * FIT_GROUP;
+    const f32x2 rcf2 = {sr.rcf, sr.rcf};
+    int32_t acc32 = 0;
+    set_round_down();
+    for (int gi = 0; gi < cnt; ++gi) {
+      int io = gi;
+      asm volatile("" : "+s"(io));
+      const FitGroupA* g = gbase + io;
+      const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
+      const i32x8 fcv = *reinterpret_cast<const i32x8*>(g->fc);
+      const i32x8 Pv = *reinterpret_cast<const i32x8*>(g->P);
+      const i32x8 clv = *reinterpret_cast<const i32x8*>(cbase + (size_t)io * FIT_GROUP);
+#pragma unroll
+      for (int u = 0; u < FIT_GROUP / 2; ++u) {
+        const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
+        const f32x2 q = fcp * rcf2;
+        int32_t m3[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int k = 2 * u + h;
+          const uint32_t qm = (uint32_t)__double_as_longlong(f64_at(fmv, k) * rm);
+          const uint32_t qc = __float_as_uint(h ? q.y : q.x);
+          const uint32_t x = min(qc, qm);                            // findMin(qc, qm)
+          m3[h] = x >= (uint32_t)Pv[k] ? clv[k] : (int32_t)x;        // CC:134-135
+        }
+        acc32 += m3[0] + m3[1];
+      }
+    }
+    set_round_nearest();
+    acc += (uint64_t)(int64_t)acc32;
+  };
+  auto sum_b_nc = [&](uint32_t g0, int cnt) {
+    cnt = __builtin_amdgcn_readfirstlane(cnt);
+    const FitGroup* gbase = fast_b + g0;
+    const int32_t* cbase = fast_cl + (size_t)g0 * FIT_GROUP;
+    const double bias = FIT_BIAS;
+    int32_t acc32 = 0;
+    set_round_down();
+    for (int gi = 0; gi < cnt; ++gi) {
+      int io = gi;
+      asm volatile("" : "+s"(io));
+      const FitGroup* g = gbase + io;
+      const i32x16 fcv = *reinterpret_cast<const i32x16*>(g->fc);
+      const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
+      const i32x16 Pv = *reinterpret_cast<const i32x16*>(g->Pb);
+      const i32x8 clv = *reinterpret_cast<const i32x8*>(cbase + (size_t)io * FIT_GROUP);
+#pragma unroll
+      for (int u = 0; u < FIT_GROUP / 2; ++u) {
+        int32_t x[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int k = 2 * u + h;
+          const double qc = __builtin_fma(f64_at(fcv, k), rc, bias);  // 2^52 + floor(fc/c)
+          const double qm = __builtin_fma(f64_at(fmv, k), rm, bias);  // 2^52 + floor(fm/m)
+          const double xb = __builtin_fmin(qc, qm);
+          const int32_t xi = (int32_t)(uint32_t)__double_as_longlong(xb);
+          x[h] = xb >= f64_at(Pv, k) ? clv[k] : xi;                   // CC:134-135
+        }
+        acc32 += x[0] + x[1];
+      }
+    }
+    set_round_nearest();
+    acc += (uint64_t)(int64_t)acc32;
+  };
   // class B (and class-A lanes sharing its wave)
   auto sum_b = [&](uint32_t g0, int cnt) {
     cnt = __builtin_amdgcn_readfirstlane(cnt);  // keep the trip count scalar
@@ -2158,8 +2244,13 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
       const int cnt = (int)((cur + qcur < lim ? cur + qcur : lim) - cur);
       qcur = qn;
       if (wave_fast) {
-        if (!wave_b) sum_a(cur, cnt);
-        else sum_b(cur, cnt);
+        if (fast_cl) {
+          if (!wave_b) sum_a_nc(cur, cnt);
+          else sum_b_nc(cur, cnt);
+        } else {
+          if (!wave_b) sum_a(cur, cnt);
+          else sum_b(cur, cnt);
+        }
       }
       claim_publish((k + 1u) & 1u);
       KCC_TLV(2048 + b % 4096, 4, (uint64_t)k + 1);
@@ -2190,6 +2281,10 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     if (slow_iters && lane == 0)
       atomicAdd(&counters[CNT_SLOW_PAIRS], (unsigned long long)slow_iters * (unsigned long long)__popcll(act));
   }
+  // the clamp in the fit: the rows clamped for every spec (P <= 0, never streamed), once
+  // per spec (the column's workgroup by == 0) for the normal specs (exact waves walked
+  // every row on the exact path)
+  if (fast_cl && by == 0 && wave_fast) acc -= (uint64_t)counters[CNT_CLAMP_ALL];
 #ifdef KCC_FIT_DIAG_NO_ATOMICS  // diagnostic timing build only: results are wrong
   if (active && acc == 0x5A5A5A5A5A5A5A5Aull) partial[s] = (int64_t)acc;
 #else
@@ -2396,8 +2491,9 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             SlowNode* slow, int64_t* slow_list, int64_t n_specs,
                             ClampWork cw, unsigned long long* counters, int chunk, int64_t row0,
                             int64_t call_nodes, hipStream_t s, bool dense,
-                            const PlaceArgs* place) {
+                            const PlaceArgs* place, int32_t* fast_cl) {
   if (n_nodes <= 0 && !place) return hipSuccess;
+  if (fast_cl && (n_specs > CLAMP_LDS_SPECS || dense)) return hipErrorInvalidValue;
   const int64_t pr = clamp_pass_rows(call_nodes);
   if (row0 % pr != 0 || (pr != 1024 && pr != 4096)) return hipErrorInvalidValue;
   // one resident round of workgroups (LDS-bound at S <= CLAMP_LDS_SPECS: one per CU)
@@ -2407,11 +2503,13 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
     pa = *place;
     pa.n_blocks = (int32_t)((n_specs + KCC_NODE_PREP_BLOCK - 1) / KCC_NODE_PREP_BLOCK);
   }
-  const size_t lds_bytes = mode == 2 ? NODE_PREP_LDS : mode == 1 ? NODE_PREP_LDS_SRCH : 0;
-  auto kern = pr == 1024 ? (mode == 2 ? node_prep_kernel<2, 1> : mode == 1 ? node_prep_kernel<1, 1> : node_prep_kernel<0, 1>)
-                         : (mode == 2 ? node_prep_kernel<2, 4> : mode == 1 ? node_prep_kernel<1, 4> : node_prep_kernel<0, 4>);
-  static std::atomic<int64_t> resident[2][3][MAX_DEVS];
-  const int64_t res = resident_blocks(resident[pr == 1024 ? 0 : 1][mode],
+  const bool nc = fast_cl != nullptr;  // (mode 2)
+  const size_t lds_bytes = nc ? 0 : mode == 2 ? NODE_PREP_LDS : mode == 1 ? NODE_PREP_LDS_SRCH : 0;
+  auto kern = nc ? (pr == 1024 ? node_prep_kernel<2, 1, true> : node_prep_kernel<2, 4, true>)
+            : pr == 1024 ? (mode == 2 ? node_prep_kernel<2, 1, false> : mode == 1 ? node_prep_kernel<1, 1, false> : node_prep_kernel<0, 1, false>)
+                         : (mode == 2 ? node_prep_kernel<2, 4, false> : mode == 1 ? node_prep_kernel<1, 4, false> : node_prep_kernel<0, 4, false>);
+  static std::atomic<int64_t> resident[2][4][MAX_DEVS];
+  const int64_t res = resident_blocks(resident[pr == 1024 ? 0 : 1][nc ? 3 : mode],
                                       reinterpret_cast<const void*>(kern), KCC_NODE_PREP_BLOCK,
                                       lds_bytes, 256);
   const int64_t cap = res < KCC_NODE_PREP_GRID ? res : KCC_NODE_PREP_GRID;
@@ -2419,7 +2517,7 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
   hipLaunchKernelGGL(kern, dim3(np_blocks + (unsigned)pa.n_blocks), dim3(KCC_NODE_PREP_BLOCK),
                      lds_bytes, s, n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu,
                      used_mem, fast_a, fast_b, slow, slow_list, n_specs, cw,
-                     counters, (int32_t)chunk, (int32_t)(dense ? 1 : 0), row0 / pr, pa);
+                     counters, (int32_t)chunk, (int32_t)(dense ? 1 : 0), row0 / pr, pa, fast_cl);
   return hipGetLastError();
 }
 
@@ -2488,7 +2586,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
                       const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, uint32_t* queue, int chunk,
-                      int64_t grid_nodes, hipStream_t s) {
+                      int64_t grid_nodes, hipStream_t s, const int32_t* fast_cl) {
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
   const int64_t gx = (n_specs + FIT_SPW - 1) / FIT_SPW;
   const int64_t n_groups = fit_groups(n_nodes);
@@ -2506,7 +2604,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
   if (blocks > 0x7fffffffLL || gy > 0x7fffffffLL) return hipErrorInvalidValue;
   hipLaunchKernelGGL(fit_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, queue, fast_a,
                      fast_b, slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)chunk,
-                     (int32_t)gx, (int32_t)gy);
+                     (int32_t)gx, (int32_t)gy, fast_cl);
   return hipGetLastError();
 }
 

@@ -461,6 +461,17 @@ class CapacityEngine:
         that can add to its fast sum."""
         self._check(self._lib.kcc_set_fit_dense(self._h, 1 if dense else 0))
 
+    def set_clamp_in_fit(self, mode: int):
+        """-1: the pod-slot clamp inside the fit on small shards (default), 0: always the
+        clamp correction launch, 1: inside the fit whenever specs <= 4096."""
+        self._check(self._lib.kcc_set_clamp_in_fit(self._h, int(mode)))
+
+    def clamp_in_fit_used(self) -> bool:
+        """Whether the last capacity call applied the clamp inside the fit."""
+        v = C.c_int()
+        self._check(self._lib.kcc_clamp_in_fit_used(self._h, C.byref(v)))
+        return bool(v.value)
+
     def fit_stream_rows(self) -> int:
         """Node rows (padded to groups of 8) the last fit streamed."""
         v = C.c_int64()

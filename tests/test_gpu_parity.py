@@ -379,6 +379,47 @@ def test_capacity_async_fused_finalize(engine, n, s, adv):
         np.testing.assert_array_equal(err.cpu().numpy(), oe)
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("n,s,adv,zipf", [(20_000, 700, True, False), (30_011, 4096, False, False),
+                                          (12_345, 1000, False, True), (5_000, 64, True, False)])
+def test_clamp_in_fit_modes(engine, mode, n, s, adv, zipf):
+    """The pod-slot clamp (CC:134-135) applied by the clamp correction launch (mode 0) or
+    inside the fit (mode 1: node_prep's clamp values, x >= P ? clamp : x in the fit's
+    loops, the always-clamped rows' sum subtracted once per spec): both == the oracle, two
+    calls in a row, through kcc_capacity_async and kcc_capacity_partial_async + finalize."""
+    import torch
+    pods = 20 * n
+    c = synth.make_cluster(n, pods, seed=43, chunk=1024, adversarial=adv, skew=zipf)
+    sc, sm = synth.make_specs(s, seed=43, adversarial=adv)
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+    used_cpu = torch.empty(n, dtype=torch.int64, device=dev)
+    used_mem = torch.empty(n, dtype=torch.int64, device=dev)
+    partial = torch.empty(2 * s, dtype=torch.int64, device=dev)
+    totals = torch.empty(s, dtype=torch.int64, device=dev)
+    err = torch.empty(s, dtype=torch.int32, device=dev)
+    uc, um, _, _ = coracle.reduce_requests(c.node_ptr, c.cpu_req, c.mem_req, c.cpu_lim, c.mem_lim)
+    ot, oe = coracle.fit(c.alloc_cpu, c.alloc_mem, c.alloc_pods, c.pod_count, uc, um, sc, sm, NT)
+    args = (T(c.node_ptr), T(c.cpu_req), T(c.mem_req), T(c.alloc_cpu), T(c.alloc_mem),
+            T(c.alloc_pods), T(c.pod_count), used_cpu, used_mem, T(sc), T(sm))
+    stream = torch.cuda.Stream(dev)
+    engine.set_clamp_in_fit(mode)
+    try:
+        for k in range(2):
+            totals.fill_(-7)
+            with torch.cuda.stream(stream):
+                if k == 0:
+                    engine.capacity_async(c.node_ptr, *args, totals, err, stream=stream)
+                else:
+                    engine.capacity_partial_async(c.node_ptr, *args, partial, n_chunks=1, stream=stream)
+                    engine.fit_finalize_async(s, partial, totals, err, stream=stream)
+            stream.synchronize()
+            np.testing.assert_array_equal(totals.cpu().numpy(), ot, err_msg=f"call {k}")
+            np.testing.assert_array_equal(err.cpu().numpy(), oe, err_msg=f"call {k}")
+    finally:
+        engine.set_clamp_in_fit(-1)
+
+
 # ---- pipelined reduce + fit (node chunks, side stream) == host API ------------------------
 @pytest.mark.parametrize("n_chunks", [1, 2, 3, 4, 16])
 def test_pipelined_capacity_matches_host(engine, n_chunks):

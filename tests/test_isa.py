@@ -42,10 +42,29 @@ def kernel_body(asm, name):
     return asm[start:asm.index("s_endpgm", start)]
 
 
-def loop_of(body, marker):
-    i = body.index(marker)
+def loop_of(body, marker, i=None):
+    i = body.index(marker) if i is None else i
     loop = body[body.rfind(".LBB", 0, i):body.index("s_cbranch", i)]
     return [ln.strip() for ln in loop.splitlines() if ln.strip() and not ln.strip().startswith(";")]
+
+
+def loops_with(body, marker):
+    """Every loop body holding `marker` (once each)."""
+    out, seen = [], set()
+    for m in re.finditer(re.escape(marker), body):
+        start = body.rfind(".LBB", 0, m.start())
+        if start not in seen:
+            seen.add(start)
+            out.append(loop_of(body, marker, m.start()))
+    return out
+
+
+def split_clamp(loops):
+    """(the clamp-free loop, the clamp-in-fit loop): the latter selects with v_cndmask."""
+    sel = [lp for lp in loops if any(ln.startswith("v_cndmask") for ln in lp)]
+    free = [lp for lp in loops if lp not in sel]
+    assert len(free) == 1 and len(sel) == 1, (len(free), len(sel))
+    return free[0], sel[0]
 
 
 WIDTH = {"s_load_dword": 1, "s_load_dwordx2": 2, "s_load_dwordx4": 4, "s_load_dwordx8": 8,
@@ -60,7 +79,7 @@ def check_loads(lines, dwords):
 
 def test_fit_class_a_loop(asm):
     import bench
-    lines = loop_of(kernel_body(asm, "fit_kernel"), "v_pk_mul_f32")
+    lines, _ = split_clamp(loops_with(kernel_body(asm, "fit_kernel"), "v_pk_mul_f32"))
     check_loads(lines, GROUP * 4)  # fm (2 dwords), fc, P per node
     valu = [ln for ln in lines if ln.startswith("v_")]
     assert len(valu) / GROUP == pytest.approx(bench.FIT_VALU_PER_NODE_WAVE, abs=1e-9), \
@@ -73,7 +92,7 @@ def test_fit_class_a_loop(asm):
 
 
 def test_fit_class_b_loop(asm):
-    lines = loop_of(kernel_body(asm, "fit_kernel"), "v_fma_f64")
+    lines, _ = split_clamp(loops_with(kernel_body(asm, "fit_kernel"), "v_fma_f64"))
     check_loads(lines, GROUP * 6)  # fc, fm, Pb (f64) per node
     valu = [ln for ln in lines if ln.startswith("v_")]
     assert len(valu) / GROUP == 4.5
@@ -83,14 +102,32 @@ def test_fit_class_b_loop(asm):
     assert not any(o.startswith(("v_cvt", "v_max", "v_mul", "v_cmp", "v_cndmask")) for o in ops)
 
 
+def test_fit_clamp_in_fit_loops(asm):
+    """The clamp-in-fit variants (kcc_set_clamp_in_fit): class A loads 8 more dwords per
+    group (the clamp values) and spends 6.0 VALU per node (min, compare, the clamp value
+    moved into a VGPR, select in place of min3: a gfx9 VOP3 reads one scalar operand at
+    most, vcc included); class B 6.5 (fmin, compare, move, select in place of two
+    min_f64)."""
+    body = kernel_body(asm, "fit_kernel")
+    _, a = split_clamp(loops_with(body, "v_pk_mul_f32"))
+    check_loads(a, GROUP * 5)
+    va = [ln for ln in a if ln.startswith("v_")]
+    assert len(va) / GROUP <= 6.0, f"{len(va)} VALU / {GROUP} nodes"
+    _, b = split_clamp(loops_with(body, "v_fma_f64"))
+    check_loads(b, GROUP * 7)
+    vb = [ln for ln in b if ln.startswith("v_")]
+    assert len(vb) / GROUP <= 6.5, f"{len(vb)} VALU / {GROUP} nodes"
+
+
 def test_fit_round_mode_windows(asm):
     body = kernel_body(asm, "fit_kernel")
     sets = [(m.start(), m.group(1)) for m in
             re.finditer(r"s_setreg\w*\s+hwreg\(HW_REG_MODE[^)]*\),\s*(\S+)", body)]
-    # (round down, back to nearest) around each of the two fast loops, nothing else
-    assert [v for _, v in sets] == ["10", "0", "10", "0"], sets
+    # (round down, back to nearest) around each of the four fast loops (class A / B, clamp
+    # free / clamp in the fit), nothing else
+    assert [v for _, v in sets] == ["10", "0"] * 4, sets
     assert all("hwreg(HW_REG_MODE, 0, 4)" in body[p:p + 60] for p, _ in sets)
-    windows = [(sets[0][0], sets[1][0]), (sets[2][0], sets[3][0])]
+    windows = [(sets[i][0], sets[i + 1][0]) for i in range(0, 8, 2)]
     for op in ("v_pk_mul_f32", "v_mul_f64", "v_fma_f64"):
         pos = [m.start() for m in re.finditer(op, body)]
         assert pos and all(any(a < p < b for a, b in windows) for p in pos), op
