@@ -2124,7 +2124,9 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   };
   // the clamp in the fit (fast_cl: launch_node_prep's NC mode): x >= P ? clamp : x per
   // node (CC:133-136), the clamp value from fast_cl, P >= 1 on every streamed row (padding:
-  // x = 0 >= P = 0, clamp 0)
+  // x = 0 >= P = 0, clamp 0).  6.0 VALU per node (a select reads one scalar operand at
+  // most, vcc included: the clamp value is moved into a VGPR); one inline-asm v_mov_b64 per
+  // two nodes (5.5) measured slower (C4 8-way fit 33.3 -> 36.2 us)
   auto sum_a_nc = [&](uint32_t g0, int cnt) {
     cnt = __builtin_amdgcn_readfirstlane(cnt);
     const FitGroupA* gbase = fast_a + g0;

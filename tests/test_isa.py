@@ -105,7 +105,7 @@ def test_fit_class_b_loop(asm):
 def test_fit_clamp_in_fit_loops(asm):
     """The clamp-in-fit variants (kcc_set_clamp_in_fit): class A loads 8 more dwords per
     group (the clamp values) and spends 6.0 VALU per node (min, compare, the clamp value
-    moved into a VGPR, select in place of min3: a gfx9 VOP3 reads one scalar operand at
+    moved into a VGPR, select in place of min3: a gfx9 select reads one scalar operand at
     most, vcc included); class B 6.5 (fmin, compare, move, select in place of two
     min_f64)."""
     body = kernel_body(asm, "fit_kernel")
