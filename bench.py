@@ -40,8 +40,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 #    SQ_INSTS_VALU costs one SQ_ACTIVE_INST_VALU quad-cycle), 256 CUs x 4 SIMDs x 2.4 GHz.
 FIT_VALU_PER_NODE_WAVE = 3.0
 # the same loop with the pod-slot clamp applied inside it (kcc_set_clamp_in_fit; small
-# shards): min, compare, a move of the clamp value, select (tests/test_isa.py)
-FIT_NC_VALU_PER_NODE_WAVE = 6.0
+# shards): min, compare, select, the clamp values by vector loads (tests/test_isa.py)
+FIT_NC_VALU_PER_NODE_WAVE = 5.0
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions / s
 METRIC = "node×spec fit evals/sec at 1M nodes × 4K specs; % of HBM roofline"
 # per-launch HBM traffic of each kernel from rocprofv3 PMC passes of this same bench
@@ -426,7 +426,7 @@ def main():
         },
         "clamp": {
             "in_fit": clamp_in_fit, "mode": args.clamp_in_fit,
-            "note": ("the pod-slot clamp (CC:134-135) inside the fit: 6 VALU per node x wave, no "
+            "note": ("the pod-slot clamp (CC:134-135) inside the fit: 5 VALU per node x wave, no "
                      "clamp_apply launch (small shards)" if clamp_in_fit else
                      "the pod-slot clamp by the clamp correction (clamp_apply launch), the fit "
                      "at 3 VALU per node x wave"),

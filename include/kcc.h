@@ -273,7 +273,7 @@ int kcc_set_fit_dense(kcc_ctx* ctx, int dense);
 /* Where the pod-slot clamp (CC:134-135, x >= allocatable pods ? allocatable - pod count : x)
  * is applied by kcc_capacity_partial_async / kcc_capacity_async: by the clamp correction
  * (a dominance count over the specs, one launch of its own; the fit's loop stays at 3 VALU
- * per node and spec wave) or inside the fit (6 VALU, no clamp launch, no clamp tables:
+ * per node and spec wave) or inside the fit (5 VALU, no clamp launch, no clamp tables:
  * cheaper on small shards).  mode -1 (default): inside the fit when node rows x specs <=
  * 1.1e9 and specs <= 4096; 0: never; 1: whenever specs <= 4096 (one node chunk, not dense).
  * The totals are the same bit for bit either way. */

@@ -349,7 +349,7 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
 // Clamp in the fit (fast_cl != nullptr; one node chunk, S <= CLAMP_LDS_SPECS, not dense):
 // node_prep streams each row's clamp value (allocatable pods - pod count, CC:135) beside
 // its FitGroupA (fast_cl[row position]) and builds no clamp tables; the fit computes the
-// reference's x >= P ? clamp : x itself (6 VALU per node x wave instead of 3) and
+// reference's x >= P ? clamp : x itself (5 VALU per node x wave instead of 3) and
 // subtracts counters[CNT_CLAMP_ALL] from every normal spec; no clamp_apply launch.  The
 // choice for small shards, where clamp_apply's fixed cost exceeds the fit's extra issue.
 #ifndef KCC_CLAMP_IN_FIT_PAIRS

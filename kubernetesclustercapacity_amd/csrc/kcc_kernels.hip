@@ -1925,6 +1925,14 @@ static_assert(FIT_QCHUNK >= 2 && FIT_QCHUNK <= FIT_CHUNK_GROUPS, "claims sum in 
 #ifndef KCC_FIT_QDIV
 #define KCC_FIT_QDIV 2  // guided claims: (what remains of the segment) / (QDIV x its workgroups)
 #endif
+#ifndef KCC_FIT_NC_VLOAD
+// the clamp-in-fit class-A loop's clamp values by vector loads (5 VALU per node) rather than
+// scalar loads (6: the select reads one scalar operand at most, vcc included, so each
+// clamp value is moved into a VGPR).  Measured (round 3, bench emulation, base / vector /
+// base / vector): C4 8-way rank 0.0632 / 0.0618 / 0.0631 / 0.0620 ms, 4-way 0.0980 /
+// 0.0965 / 0.0986 / 0.0953 ms (profiles/r03z_ab_clamp_vload.txt)
+#define KCC_FIT_NC_VLOAD 1
+#endif
 #ifndef KCC_FIT_QEST
 #define KCC_FIT_QEST 0  // guided claims sized from the head estimated after the others' claims
 #endif
@@ -2124,15 +2132,24 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   };
   // the clamp in the fit (fast_cl: launch_node_prep's NC mode): x >= P ? clamp : x per
   // node (CC:133-136), the clamp value from fast_cl, P >= 1 on every streamed row (padding:
-  // x = 0 >= P = 0, clamp 0).  6.0 VALU per node (a select reads one scalar operand at
-  // most, vcc included: the clamp value is moved into a VGPR); one inline-asm v_mov_b64 per
-  // two nodes (5.5) measured slower (C4 8-way fit 33.3 -> 36.2 us)
+  // x = 0 >= P = 0, clamp 0).  Class A: 5.0 VALU per node with the clamp values from
+  // vector loads (KCC_FIT_NC_VLOAD); with scalar loads 6.0, one inline-asm v_mov_b64 per
+  // two nodes (5.5) measured slower (C4 8-way fit 33.3 -> 36.2 us).  Class B: 6.5.
+#if KCC_FIT_NC_VLOAD
+  // A/B variant: the clamp values by vector loads (uniform addresses: one line per wave),
+  // so the select takes them as VGPRs (no move: 5 VALU per node)
+  const __amdgpu_buffer_rsrc_t cl_rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)fast_cl, (short)0, (int)(fit_groups(n_nodes) * FIT_GROUP * 4), 0x00020000);
+#endif
   auto sum_a_nc = [&](uint32_t g0, int cnt) {
     cnt = __builtin_amdgcn_readfirstlane(cnt);
     const FitGroupA* gbase = fast_a + g0;
     const int32_t* cbase = fast_cl + (size_t)g0 * FIT_GROUP;
     const f32x2 rcf2 = {sr.rcf, sr.rcf};
     int32_t acc32 = 0;
+#if KCC_FIT_NC_VLOAD
+    typedef int32_t i32x4_t __attribute__((ext_vector_type(4)));
+#endif
     set_round_down();
     for (int gi = 0; gi < cnt; ++gi) {
       int io = gi;
@@ -2141,7 +2158,15 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
       const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
       const i32x8 fcv = *reinterpret_cast<const i32x8*>(g->fc);
       const i32x8 Pv = *reinterpret_cast<const i32x8*>(g->P);
+#if KCC_FIT_NC_VLOAD
+      const int so = (int)((g0 + (uint32_t)io) * FIT_GROUP * 4);
+      const i32x4_t c0 = __builtin_bit_cast(i32x4_t, __builtin_amdgcn_raw_buffer_load_b128(cl_rs, 0, so, 0));
+      const i32x4_t c1 = __builtin_bit_cast(i32x4_t, __builtin_amdgcn_raw_buffer_load_b128(cl_rs, 16, so, 0));
+      const int32_t clv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      (void)cbase;
+#else
       const i32x8 clv = *reinterpret_cast<const i32x8*>(cbase + (size_t)io * FIT_GROUP);
+#endif
 #pragma unroll
       for (int u = 0; u < FIT_GROUP / 2; ++u) {
         const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};

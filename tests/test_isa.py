@@ -103,16 +103,18 @@ def test_fit_class_b_loop(asm):
 
 
 def test_fit_clamp_in_fit_loops(asm):
-    """The clamp-in-fit variants (kcc_set_clamp_in_fit): class A loads 8 more dwords per
-    group (the clamp values) and spends 6.0 VALU per node (min, compare, the clamp value
-    moved into a VGPR, select in place of min3: a gfx9 select reads one scalar operand at
-    most, vcc included); class B 6.5 (fmin, compare, move, select in place of two
-    min_f64)."""
+    """The clamp-in-fit variants (kcc_set_clamp_in_fit): class A takes each group's 8 clamp
+    values by two 16-B vector loads (uniform address) so the select reads them as VGPRs: 5.0 VALU per node (min, compare, select in
+    place of min3); class B (scalar loads) 6.5: fmin, compare, a move of the clamp value
+    into a VGPR (a gfx9 select reads one scalar operand at most, vcc included), select in
+    place of two min_f64."""
     body = kernel_body(asm, "fit_kernel")
     _, a = split_clamp(loops_with(body, "v_pk_mul_f32"))
-    check_loads(a, GROUP * 5)
+    assert sum(WIDTH[ln.split()[0]] for ln in a if ln.startswith("s_load_dword")) == GROUP * 4
+    assert [ln.split()[0] for ln in a if ln.startswith(("global_", "buffer_", "flat_"))] == \
+        ["buffer_load_dwordx4"] * 2
     va = [ln for ln in a if ln.startswith("v_")]
-    assert len(va) / GROUP <= 6.0, f"{len(va)} VALU / {GROUP} nodes"
+    assert len(va) / GROUP <= 5.0, f"{len(va)} VALU / {GROUP} nodes"
     _, b = split_clamp(loops_with(body, "v_fma_f64"))
     check_loads(b, GROUP * 7)
     vb = [ln for ln in b if ln.startswith("v_")]
