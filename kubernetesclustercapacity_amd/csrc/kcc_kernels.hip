@@ -1985,6 +1985,10 @@ __device__ __forceinline__ double f64_at(const i32x16& v, int k) {
 #else
 #define KCC_FIT_ATTR
 #endif
+// NC: the clamp in the fit (fast_cl, launch_fit) — its own instantiation, so the
+// clamp-correction layout's registers are not the larger loops' (one kernel holding both
+// spilled 52 SGPRs: C4 fit 116 -> 120 us)
+template <bool NC>
 __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     int64_t n_nodes, uint32_t* __restrict__ queue, const FitGroupA* __restrict__ fast_a,
     const FitGroup* __restrict__ fast_b, const SlowNode* __restrict__ slow,
@@ -2271,7 +2275,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
       const int cnt = (int)((cur + qcur < lim ? cur + qcur : lim) - cur);
       qcur = qn;
       if (wave_fast) {
-        if (fast_cl) {
+        if constexpr (NC) {
           if (!wave_b) sum_a_nc(cur, cnt);
           else sum_b_nc(cur, cnt);
         } else {
@@ -2311,7 +2315,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   // the clamp in the fit: the rows clamped for every spec (P <= 0, never streamed), once
   // per spec (the column's workgroup by == 0) for the normal specs (exact waves walked
   // every row on the exact path)
-  if (fast_cl && by == 0 && wave_fast) acc -= (uint64_t)counters[CNT_CLAMP_ALL];
+  if (NC && by == 0 && wave_fast) acc -= (uint64_t)counters[CNT_CLAMP_ALL];
 #ifdef KCC_FIT_DIAG_NO_ATOMICS  // diagnostic timing build only: results are wrong
   if (active && acc == 0x5A5A5A5A5A5A5A5Aull) partial[s] = (int64_t)acc;
 #else
@@ -2606,7 +2610,7 @@ hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
 
 int64_t fit_resident_blocks() {  // 256-thread fit workgroups resident on the device at once
   static std::atomic<int64_t> cache[MAX_DEVS];
-  return resident_blocks(cache, reinterpret_cast<const void*>(fit_kernel), 256, 0, 2048);
+  return resident_blocks(cache, reinterpret_cast<const void*>(fit_kernel<false>), 256, 0, 2048);
 }
 
 hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,
@@ -2629,7 +2633,8 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
   // 1-D grid of gx * roundup(gy, 8) workgroups, remapped XCD-aware in the kernel
   const int64_t blocks = gx * ((gy + 7) / 8 * 8);
   if (blocks > 0x7fffffffLL || gy > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fit_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, queue, fast_a,
+  auto kern = fast_cl ? fit_kernel<true> : fit_kernel<false>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, queue, fast_a,
                      fast_b, slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)chunk,
                      (int32_t)gx, (int32_t)gy, fast_cl);
   return hipGetLastError();

@@ -59,12 +59,9 @@ def loops_with(body, marker):
     return out
 
 
-def split_clamp(loops):
-    """(the clamp-free loop, the clamp-in-fit loop): the latter selects with v_cndmask."""
-    sel = [lp for lp in loops if any(ln.startswith("v_cndmask") for ln in lp)]
-    free = [lp for lp in loops if lp not in sel]
-    assert len(free) == 1 and len(sel) == 1, (len(free), len(sel))
-    return free[0], sel[0]
+# fit_kernel<false>: the clamp-correction layout; fit_kernel<true>: the clamp in the fit
+FIT = "fit_kernelILb0E"
+FIT_NC = "fit_kernelILb1E"
 
 
 WIDTH = {"s_load_dword": 1, "s_load_dwordx2": 2, "s_load_dwordx4": 4, "s_load_dwordx8": 8,
@@ -79,7 +76,7 @@ def check_loads(lines, dwords):
 
 def test_fit_class_a_loop(asm):
     import bench
-    lines, _ = split_clamp(loops_with(kernel_body(asm, "fit_kernel"), "v_pk_mul_f32"))
+    (lines,) = loops_with(kernel_body(asm, FIT), "v_pk_mul_f32")
     check_loads(lines, GROUP * 4)  # fm (2 dwords), fc, P per node
     valu = [ln for ln in lines if ln.startswith("v_")]
     assert len(valu) / GROUP == pytest.approx(bench.FIT_VALU_PER_NODE_WAVE, abs=1e-9), \
@@ -92,7 +89,7 @@ def test_fit_class_a_loop(asm):
 
 
 def test_fit_class_b_loop(asm):
-    lines, _ = split_clamp(loops_with(kernel_body(asm, "fit_kernel"), "v_fma_f64"))
+    (lines,) = loops_with(kernel_body(asm, FIT), "v_fma_f64")
     check_loads(lines, GROUP * 6)  # fc, fm, Pb (f64) per node
     valu = [ln for ln in lines if ln.startswith("v_")]
     assert len(valu) / GROUP == 4.5
@@ -108,35 +105,38 @@ def test_fit_clamp_in_fit_loops(asm):
     place of min3); class B (scalar loads) 6.5: fmin, compare, a move of the clamp value
     into a VGPR (a gfx9 select reads one scalar operand at most, vcc included), select in
     place of two min_f64."""
-    body = kernel_body(asm, "fit_kernel")
-    _, a = split_clamp(loops_with(body, "v_pk_mul_f32"))
+    body = kernel_body(asm, FIT_NC)
+    (a,) = loops_with(body, "v_pk_mul_f32")
+    assert any(ln.startswith("v_cndmask") for ln in a)
     assert sum(WIDTH[ln.split()[0]] for ln in a if ln.startswith("s_load_dword")) == GROUP * 4
     assert [ln.split()[0] for ln in a if ln.startswith(("global_", "buffer_", "flat_"))] == \
         ["buffer_load_dwordx4"] * 2
     va = [ln for ln in a if ln.startswith("v_")]
     assert len(va) / GROUP <= 5.0, f"{len(va)} VALU / {GROUP} nodes"
-    _, b = split_clamp(loops_with(body, "v_fma_f64"))
+    (b,) = loops_with(body, "v_fma_f64")
+    assert any(ln.startswith("v_cndmask") for ln in b)
     check_loads(b, GROUP * 7)
     vb = [ln for ln in b if ln.startswith("v_")]
     assert len(vb) / GROUP <= 6.5, f"{len(vb)} VALU / {GROUP} nodes"
 
 
-def test_fit_round_mode_windows(asm):
-    body = kernel_body(asm, "fit_kernel")
+@pytest.mark.parametrize("name", [FIT, FIT_NC])
+def test_fit_round_mode_windows(asm, name):
+    body = kernel_body(asm, name)
     sets = [(m.start(), m.group(1)) for m in
             re.finditer(r"s_setreg\w*\s+hwreg\(HW_REG_MODE[^)]*\),\s*(\S+)", body)]
-    # (round down, back to nearest) around each of the four fast loops (class A / B, clamp
-    # free / clamp in the fit), nothing else
-    assert [v for _, v in sets] == ["10", "0"] * 4, sets
+    # (round down, back to nearest) around each of the two fast loops, nothing else
+    assert [v for _, v in sets] == ["10", "0", "10", "0"], sets
     assert all("hwreg(HW_REG_MODE, 0, 4)" in body[p:p + 60] for p, _ in sets)
-    windows = [(sets[i][0], sets[i + 1][0]) for i in range(0, 8, 2)]
+    windows = [(sets[0][0], sets[1][0]), (sets[2][0], sets[3][0])]
     for op in ("v_pk_mul_f32", "v_mul_f64", "v_fma_f64"):
         pos = [m.start() for m in re.finditer(op, body)]
         assert pos and all(any(a < p < b for a, b in windows) for p in pos), op
 
 
-def test_denormals_enabled(asm):
-    m = re.search(r"^(_ZN3kcc12_GLOBAL__N_1\d+fit_kernel\w*):", asm, re.M)
+@pytest.mark.parametrize("name", [FIT, FIT_NC])
+def test_denormals_enabled(asm, name):
+    m = re.search(rf"^(_ZN3kcc12_GLOBAL__N_1\d+{name}\w*):", asm, re.M)
     desc = asm[asm.index(".amdhsa_kernel " + m.group(1)):]
     desc = desc[:desc.index(".end_amdhsa_kernel")]
     assert re.search(r"\.amdhsa_float_denorm_mode_32 3", desc)
@@ -184,7 +184,7 @@ def test_fit_claim_result_untouched_until_drained(asm):
     at issue.  No instruction may read or write that register between the atomic and the
     s_waitcnt vmcnt(0) that drains it: a copy would read it early, a reuse would be
     overwritten when the claim returns (advisor, round 2)."""
-    lines = [ln.strip() for ln in kernel_body(asm, "fit_kernel").splitlines()]
+    lines = [ln.strip() for nm in (FIT, FIT_NC) for ln in kernel_body(asm, nm).splitlines()]
     found = 0
     for i, ln in enumerate(lines):
         m = re.match(r"global_atomic_add\s+v(\d+),.*\bsc0\b", ln)
@@ -200,4 +200,4 @@ def test_fit_claim_result_untouched_until_drained(asm):
             assert reg not in _vregs(ln2), f"v{reg} of `{ln}` touched by `{ln2}` before its wait"
         else:
             raise AssertionError(f"no s_waitcnt vmcnt(0) after `{ln}`")
-    assert found >= 2  # the first claim and the loop's
+    assert found >= 4  # the first claim and the loop's, in both instantiations
