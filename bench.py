@@ -105,6 +105,9 @@ def parse():
     ap.add_argument("--kernel-events", default="after", choices=["timed", "after"],
                     help="per-kernel HIP events inside the timed steps (timed) or in as many "
                          "extra steps after them (after)")
+    ap.add_argument("--drill-exchange-fallback", action="store_true",
+                    help="test drill (N > 1): treat the p2p exchange's pre-timing check as failed "
+                         "on the last rank, so every rank takes the RCCL fallback path")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: start the ranks, exchange one gloo "
                          "all-reduce, print the rank count (no measurement)")
@@ -231,7 +234,7 @@ def main():
         lo, hi = node_range(n_total, 0, args.emulate_world)
     t0 = time.time()
     cl = synth.make_cluster(n_total, pods_total, seed=20261015 + int(args.config[1:]),
-                            node_lo=lo, node_hi=hi, skew=cfg["skew"])
+                            node_lo=lo, node_hi=hi, skew=cfg["skew"], limits=False)
     sc, sm = synth.config_specs(args.config)
     n, S, C = cl.n_nodes, sc.size, cl.n_containers
     gen_s = time.time() - t0
@@ -267,19 +270,26 @@ def main():
             exchange = "kcc" if args.dist_backend == "nccl" else "torch"
             exchange_note = (exchange_note or "a peer's p2p setup failed") + f"; {exchange} used"
         dist.barrier()
-    if world > 1 and exchange == "kcc":
-        # libkcc's own RCCL communicator: rank 0's id travels over the process group
+
+    def setup_kcc():
+        # libkcc's own RCCL communicator: rank 0's id travels over the process group;
+        # returns the exchange every rank uses and a note when it is not kcc
+        err_note = None
         try:
             obj = [CapacityEngine.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
             eng.comm_init(obj[0], world, rank)
         except Exception as e:  # noqa: BLE001 - every rank falls back the same way below
-            exchange_note = f"kcc communicator failed ({e}); torch.distributed all-reduce used"
-        ok = torch.tensor([0 if exchange_note else 1], dtype=torch.int64, device=dev)
+            err_note = f"kcc communicator failed ({e}); torch.distributed all-reduce used"
+        ok = torch.tensor([0 if err_note else 1], dtype=torch.int64, device=dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         if int(ok.item()) == 0:
-            exchange = "torch"
-            exchange_note = exchange_note or "a peer's kcc communicator failed; torch all-reduce used"
+            return "torch", err_note or "a peer's kcc communicator failed; torch all-reduce used"
+        return "kcc", None
+
+    if world > 1 and exchange == "kcc":
+        exchange, note = setup_kcc()
+        exchange_note = note or exchange_note
 
     h_ptr = np.ascontiguousarray(cl.node_ptr, np.int64)
 
@@ -312,10 +322,79 @@ def main():
                 return
         eng.fit_finalize_async(S, partial, totals, err, stream=stream)
 
+    def exchange_verified(drill=False):
+        """One step with the current exchange, checked on every rank before anything is
+        timed: its totals / spec_err against the process group's all-reduce of the same
+        partials + the library's finalize, and no device wait gave up (reduce look-back,
+        exchange flag).  True only when every rank agrees (ClusterCapacity.go:138 summed
+        over the node shards)."""
+        with torch.cuda.stream(stream):
+            eng.capacity_partial_async(h_ptr, ptr, cpu, mem, a_cpu, a_mem, a_pods, p_cnt,
+                                       used_cpu, used_mem, s_cpu, s_mem, partial,
+                                       n_chunks=args.chunks, stream=stream)
+            own = partial.clone()
+            totals.fill_(-1)
+            if exchange == "p2p":
+                eng.exchange_finalize_async(S, partial, totals, err, stream=stream)
+            elif exchange == "kcc":
+                eng.allreduce_partial_async(S, partial, stream=stream)
+                eng.fit_finalize_async(S, partial, totals, err, stream=stream)
+        torch.cuda.synchronize()
+        if exchange == "torch":
+            dist.all_reduce(partial, op=dist.ReduceOp.SUM)
+            with torch.cuda.stream(stream):
+                eng.fit_finalize_async(S, partial, totals, err, stream=stream)
+            torch.cuda.synchronize()
+        ref = own if args.dist_backend == "nccl" else own.cpu()
+        dist.all_reduce(ref, op=dist.ReduceOp.SUM)
+        ref_t, ref_e = torch.empty_like(totals), torch.empty_like(err)
+        with torch.cuda.stream(stream):
+            eng.fit_finalize_async(S, ref.to(dev), ref_t, ref_e, stream=stream)
+        torch.cuda.synchronize()
+        good = (torch.equal(ref_t, totals) and torch.equal(ref_e, err) and
+                eng.p2p_faults() == 0 and eng.reduce_faults() == 0 and
+                not (drill and rank == world - 1))
+        flag = torch.tensor([1 if good else 0], dtype=torch.int64,
+                            device=dev if args.dist_backend == "nccl" else None)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return int(flag.item()) == 1
+
+    verified = None
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
+        if world > 1:
+            # the exchange proves itself before anything is timed: a p2p exchange that
+            # disagrees falls back to libkcc's RCCL all-reduce (every rank), and a line is
+            # only printed for totals the process group's own all-reduce reproduces
+            tried = [exchange]
+            ok = exchange_verified(drill=args.drill_exchange_fallback and exchange == "p2p")
+            if not ok and exchange == "p2p":
+                eng.clear_faults()  # (the failed exchange may have set the fault words)
+                if args.dist_backend == "nccl":
+                    exchange, note = setup_kcc()
+                else:
+                    exchange, note = "torch", None
+                exchange_note = ("p2p exchange failed its pre-timing check (totals vs the process "
+                                 f"group's all-reduce + finalize, fault words); {exchange} used"
+                                 + (f"; {note}" if note else ""))
+                tried.append(exchange)
+                ok = exchange_verified()
+            if not ok:
+                print(f"[bench] rank {rank}: the exchange failed its pre-timing check "
+                      f"({' then '.join(tried)}): no line is reported for unverified totals",
+                      file=sys.stderr, flush=True)
+                dist.destroy_process_group()
+                sys.exit(3)
+            verified = {"verified_before_timing": True, "exchanges_tried": tried,
+                        "exchange": exchange,
+                        "check": "one step's totals / spec_err == the process group's all-reduce "
+                                 "of the same partials + kcc_fit_finalize_async, no device wait "
+                                 "gave up, on every rank"}
+            for _ in range(max(args.warmup, 1)):
+                step()
+            torch.cuda.synchronize()
         # per-launch kernel durations from HIP events the library records on the stream
         # each kernel runs on: over exactly the timed steps (--kernel-events timed), or
         # over as many extra steps right after them (after: the timed region has no events)
@@ -396,6 +475,10 @@ def main():
                         "reduce + fit prepare + fit + finalize"
                         + (" + RCCL all-reduce" if world > 1 else ""),
             "nodes": n_total, "pods": pods_total, "containers_rank0": C, "nodes_rank0": n,
+            "pods_rank0": int(cl.pod_count.sum()),
+            "pods_per_node": ("Zipf(s=1.2) capped at 2 x allocatable pods (SURVEY §8d); `pods` "
+                              "is its expected total" if cl.meta["skew"] == "zipf" else
+                              f"{cl.meta['skew']}, mean {pods_total / max(n_total, 1):g}"),
             "specs": S, "parallelism": f"node-sharded x{world}",
         },
         "world": {
@@ -482,9 +565,12 @@ def main():
     out["totals_checksum"] = int(((tot_np * np.uint64(0x9E3779B97F4A7C15)) ^ (tot_np >> np.uint64(29)))
                                  .sum(dtype=np.uint64))
     out["spec_errors"] = int(err.cpu().numpy().sum())
+    if verified is not None:
+        out["exchange_precheck"] = verified
     if world > 1 and exchange == "p2p":
-        # the p2p exchange against the process group's all-reduce of the same partials +
-        # the library's finalize (every rank), and the flag waits that gave up (0)
+        # again after the timed steps: the p2p exchange against the process group's
+        # all-reduce of the same partials + the library's finalize (every rank), and the
+        # flag waits that gave up (0)
         torch.cuda.synchronize()
         rp = partial.clone() if args.dist_backend == "nccl" else partial.cpu()
         dist.all_reduce(rp, op=dist.ReduceOp.SUM)

@@ -22,7 +22,16 @@
  *   - *_async entry points take DEVICE pointers and a hipStream_t (as void*, NULL =
  *     the null stream) and only enqueue work: they never synchronise, and allocate
  *     only when the context workspace must grow — call kcc_reserve first and they
- *     can be captured into a hipGraph.  Container arrays must be 16-byte aligned.
+ *     can be captured into a hipGraph and replayed (no launch depends on host-side
+ *     state that a replay would freeze: the reduce's look-back records are left free by
+ *     every launch, the exchange's epoch is a device word).  Container arrays must be
+ *     16-byte aligned.
+ *   - Device faults: the reduce's look-back waits and the exchange's flag waits are
+ *     bounded; one that gives up (never on a healthy device) sets a sticky fault word
+ *     of the device.  While it is set every finalize marks every spec KCC_SPEC_FAULT
+ *     (totals 0) and the synchronous entry points return KCC_EFAULT; kcc_clear_faults
+ *     resets it.  kcc_reduce_requests_async alone has no per-spec output: check
+ *     kcc_reduce_faults after synchronising.
  *   - A context is not thread-safe; every entry calls hipSetDevice(ctx device), so
  *     Go OS-thread migration between cgo calls is harmless.
  *   - There is no CPU backend: without a usable gfx950 device kcc_create fails.
@@ -44,7 +53,15 @@ enum {
   KCC_ENOMEM = -2,   /* device allocation failed                                  */
   KCC_EHIP = -3,     /* HIP runtime error                                         */
   KCC_ENODEV = -4,   /* no usable device                                          */
-  KCC_ERCCL = -5     /* RCCL error (multi-GPU contexts)                           */
+  KCC_ERCCL = -5,    /* RCCL error (multi-GPU contexts)                           */
+  KCC_EFAULT = -6    /* a bounded device wait gave up: results invalid (see above) */
+};
+
+/* spec_err values of the fit entry points */
+enum {
+  KCC_SPEC_OK = 0,
+  KCC_SPEC_DIVZERO = 1, /* Go would panic with an integer divide by zero; total 0    */
+  KCC_SPEC_FAULT = 2    /* the device faulted (kcc_clear_faults); total 0, not valid */
 };
 
 typedef struct kcc_ctx kcc_ctx;
@@ -104,9 +121,10 @@ int kcc_reduce_requests_async(kcc_ctx* ctx, int64_t n_nodes, int64_t n_container
  *     q  = findMin(qc, qm)                                                                   CC:133
  *     if q >= alloc_pods[i] { q = alloc_pods[i] - pod_count[i] }                             CC:134-136
  *     totals[s] += q                                                                         CC:138
- *   spec_err[s] = 1 iff the Go code would panic with an integer divide by zero
- *   (spec_cpu[s] == 0 reached on a row with free CPU, or spec_mem[s] == 0 on a row
- *   with free memory); totals[s] is then 0.  pod_count = len(pods) (CC:106, CC:135).
+ *   spec_err[s] = KCC_SPEC_DIVZERO (1) iff the Go code would panic with an integer divide
+ *   by zero (spec_cpu[s] == 0 reached on a row with free CPU, or spec_mem[s] == 0 on a
+ *   row with free memory); totals[s] is then 0.  KCC_SPEC_FAULT (2): a device fault, see
+ *   the conventions above.  pod_count = len(pods) (CC:106, CC:135).
  *   The verdict (CC:144) is totals[s] >= replicas[s], left to the caller.
  *   At most 2^26 - 1 specs per call.
  * ------------------------------------------------------------------------- */
@@ -235,8 +253,9 @@ int kcc_allreduce_partial_async(kcc_ctx* ctx, int64_t n_specs, int64_t* d_partia
  * partial into every mailbox, waits for every peer's push of the same step, sums and
  * finalizes totals / spec_err exactly as the all-reduce + finalize do.  Every rank must
  * call it the same number of times with the same specs.  A wait for a peer that never
- * pushes gives up after seconds and is counted (kcc_p2p_faults; the totals are then
- * wrong): tests and the bench assert 0.  Replaces RCCL only where its
+ * pushes gives up after seconds and is counted (kcc_p2p_faults): that launch and every
+ * finalize after it mark every spec KCC_SPEC_FAULT (see the conventions above); tests
+ * and the bench assert 0.  Replaces RCCL only where its
  * ncclAllReduce(partial) stood (ClusterCapacity.go:138, the total over nodes). */
 #define KCC_P2P_HANDLE_BYTES 64
 #define KCC_P2P_MAX_SPECS (1 << 20)
@@ -256,11 +275,15 @@ int kcc_profile_read(kcc_ctx* ctx, double* reduce_ms, int64_t* reduce_launches, 
                      int64_t* fit_launches);
 
 /* Look-back waits of the segmented reduce that gave up (summed over the context's
- * devices since creation; synchronises).  A reduce launch assembles a node cut by wave
- * ranges from pieces the other waves publish; a wait that never sees its piece (not
- * expected on a healthy device) is counted here instead of hanging, and the affected
- * node's sums are then wrong.  Tests and the bench assert 0. */
+ * devices since the last kcc_clear_faults; synchronises).  A reduce launch assembles a
+ * node cut by wave ranges from pieces the other waves publish; a wait that never sees
+ * its piece (not expected on a healthy device) is counted here instead of hanging, and
+ * the affected node's sums are then wrong.  Tests and the bench assert 0. */
 int kcc_reduce_faults(kcc_ctx* ctx, int64_t* faults);
+/* Reset the context's fault words and the reduce's look-back records (synchronises).
+ * After an exchange fault (kcc_p2p_faults > 0) a late peer push may still land in the
+ * mailbox: re-create the mailboxes (a new context) before exchanging again. */
+int kcc_clear_faults(kcc_ctx* ctx);
 
 /* The fit streams only the node rows that can add to its fast sum (free CPU, free
  * memory and allocatable pods > 0, within the fast bounds): every other row contributes
@@ -279,7 +302,8 @@ int kcc_set_fit_dense(kcc_ctx* ctx, int dense);
  * The totals are the same bit for bit either way. */
 int kcc_set_clamp_in_fit(kcc_ctx* ctx, int mode);
 /* 1 when the last kcc_capacity_partial_async / kcc_capacity_async of the context applied
- * the clamp inside the fit (its VALU accounting: 6 per node x wave, not 3). */
+ * the clamp inside the fit (its VALU accounting per node x 64-spec wave: 5 for class-A
+ * specs and 6.5 for class B, against 3 and 4.5 with the clamp correction). */
 int kcc_clamp_in_fit_used(kcc_ctx* ctx, int* used);
 int kcc_fit_stream_rows(kcc_ctx* ctx, int64_t* streamed);
 

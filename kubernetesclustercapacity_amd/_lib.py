@@ -19,10 +19,15 @@ KCC_ENOMEM = -2
 KCC_EHIP = -3
 KCC_ENODEV = -4
 KCC_ERCCL = -5
+KCC_EFAULT = -6
 ERROR_NAMES = {
     KCC_EINVAL: "KCC_EINVAL", KCC_ENOMEM: "KCC_ENOMEM", KCC_EHIP: "KCC_EHIP",
-    KCC_ENODEV: "KCC_ENODEV", KCC_ERCCL: "KCC_ERCCL",
+    KCC_ENODEV: "KCC_ENODEV", KCC_ERCCL: "KCC_ERCCL", KCC_EFAULT: "KCC_EFAULT",
 }
+# spec_err values (include/kcc.h KCC_SPEC_*)
+KCC_SPEC_OK = 0
+KCC_SPEC_DIVZERO = 1
+KCC_SPEC_FAULT = 2
 
 _i64, _i32, _int, _vp, _dbl = C.c_int64, C.c_int32, C.c_int, C.c_void_p, C.c_double
 
@@ -53,6 +58,7 @@ SIGNATURES = {
     "kcc_clamp_in_fit_used": (_int, [_vp, C.POINTER(C.c_int)]),
     "kcc_fit_stream_rows": (_int, [_vp, C.POINTER(_i64)]),
     "kcc_reduce_faults": (_int, [_vp, C.POINTER(_i64)]),
+    "kcc_clear_faults": (_int, [_vp]),
     "kcc_comm_unique_id": (_int, [_vp]),
     "kcc_comm_init": (_int, [_vp, _vp, _int, _int]),
     "kcc_allreduce_partial_async": (_int, [_vp, _i64, _vp, _vp]),
@@ -118,11 +124,13 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     return lib
 
 
-_LIB = None
+_LIBS: dict[str, C.CDLL] = {}
 
 
-def lib() -> C.CDLL:
-    global _LIB
-    if _LIB is None:
-        _LIB = load()
-    return _LIB
+def lib(path: str | None = None) -> C.CDLL:
+    """The release libkcc.so, or (path) another build of it — the fault-path test build
+    (libkcc_faultdiag.so) — each loaded once."""
+    p = os.path.abspath(path or LIB_PATH)
+    if p not in _LIBS:
+        _LIBS[p] = load(p)
+    return _LIBS[p]

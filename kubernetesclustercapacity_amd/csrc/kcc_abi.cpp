@@ -74,11 +74,13 @@ struct Dev {
   int64_t prof_n[2] = {0, 0};
   // workspace of the *_async entry points
   DevBuf fast_a, fast_b, slow, slow_list, srec, sperm, counters;
-  // the reduce's per-wave tail records (look-back), zeroed when allocated; each reduce
-  // launch tags its records with a new epoch.  faults: look-back waits that timed out.
-  DevBuf red_tail, red_faults;
+  // the reduce's per-wave tail records (look-back): zeroed when allocated, and every
+  // launch leaves their tags 0 (each record is cleared by the wave that consumes it)
+  DevBuf red_tail;
+  // the device's fault words (kcc::FAULT_*): reduce look-back / exchange flag waits that
+  // gave up; sticky until kcc_clear_faults
+  DevBuf faults;
   DevBuf rank_arrive;  // spec_rank's per-query-block arrival counters (zero between calls)
-  uint64_t red_epoch = 0;
   DevBuf fit_q;          // the fit's per-column work queues (zero between launches)
   bool fitq_dirty = true;
   // spec setup + clamp correction (kcc::ClampWork)
@@ -107,13 +109,13 @@ struct Dev {
   // kcc_pod_requests / kcc_reduce_requests_pods staging (app containers in cpu / mem)
   DevBuf q_ptr, q_iptr, q_icpu, q_imem, q_rst, q_ocpu, q_omem, q_pcpu, q_pmem;
   // one-shot exchange over xGMI peer memory (kcc_p2p_*): this rank's mailbox (exported),
-  // the push arrival counter and the flag-wait fault counter; the peers' mapped mailboxes
-  DevBuf p2p_mbox, p2p_arrive, p2p_faults;
+  // the push arrival counter (u32 word 0) and the last pushed epoch (u64 word 1, advanced
+  // by the kernel); the peers' mapped mailboxes
+  DevBuf p2p_mbox, p2p_arrive;
   DevBuf clamp_arrive;  // clamp_apply's fused finalize: arrivals (zero between launches)
   unsigned char* p2p_peer[kcc::P2P_MAX_RANKS] = {};  // opened peer mailboxes (own: p2p_mbox)
   int p2p_W = 0, p2p_rank = -1;
   int64_t p2p_smax = 0;
-  uint64_t p2p_epoch = 0;
   bool p2p_ready = false;
 };
 
@@ -198,25 +200,48 @@ int h2d(kcc_ctx* ctx, Dev& dv, DevBuf& buf, const T* src, int64_t count) {
 
 // ---- device-level pipeline pieces (no host sync, no allocation beyond growth) ----
 
-// The reduce's look-back workspace: tail records for every wave a launch may have, and
-// the fault counter, zeroed when (re)allocated — synchronously: a stale tag equal to a
-// later epoch would hand a wave a piece that was never published (allocation happens
-// only when the workspace grows; kcc_reserve does it ahead of any capture).
+// The device's fault words, zeroed when allocated (synchronously: kcc_reserve does it
+// ahead of any capture).
+int faults_ws(kcc_ctx* ctx, Dev& dv, hipStream_t s) {
+  if (dv.faults.p) return KCC_OK;
+  KCC_HIP(ctx, ensure(dv.faults, 8 * kcc::FAULT_WORDS));
+  KCC_HIP(ctx, hipMemsetAsync(dv.faults.p, 0, 8 * kcc::FAULT_WORDS, s));
+  KCC_HIP(ctx, hipStreamSynchronize(s));
+  return KCC_OK;
+}
+
+// The reduce's look-back workspace: tail records for every wave a launch may have, zeroed
+// when (re)allocated — synchronously: a stale tag would hand a wave a piece that was
+// never published (allocation happens only when the workspace grows; kcc_reserve does it
+// ahead of any capture).  Every launch leaves the tags 0.
 int reduce_ws(kcc_ctx* ctx, Dev& dv, hipStream_t s) {
   const size_t tb = sizeof(uint64_t) * kcc::RED_TAIL_WORDS * (size_t)kcc::reduce_tail_records();
-  bool fresh = false;
   if (dv.red_tail.bytes < tb) {
     KCC_HIP(ctx, ensure(dv.red_tail, tb));
     KCC_HIP(ctx, hipMemsetAsync(dv.red_tail.p, 0, dv.red_tail.bytes, s));
-    fresh = true;
+    KCC_HIP(ctx, hipStreamSynchronize(s));
   }
-  if (!dv.red_faults.p) {
-    KCC_HIP(ctx, ensure(dv.red_faults, 16));
-    KCC_HIP(ctx, hipMemsetAsync(dv.red_faults.p, 0, 16, s));
-    fresh = true;
+  return faults_ws(ctx, dv, s);
+}
+
+// After a synchronous entry point's final synchronisation: a set fault word means some
+// wait of this (or an earlier, async) call gave up and results are not trustworthy.
+int check_faults(kcc_ctx* ctx) {
+  unsigned long long red = 0, p2p = 0;
+  for (Dev& dv : ctx->devs) {
+    if (!dv.faults.p) continue;
+    unsigned long long f[2] = {0, 0};
+    KCC_HIP(ctx, hipSetDevice(dv.device));
+    KCC_HIP(ctx, hipMemcpy(f, dv.faults.p, sizeof(f), hipMemcpyDeviceToHost));
+    red += f[kcc::FAULT_RED];
+    p2p += f[kcc::FAULT_P2P];
   }
-  if (fresh) KCC_HIP(ctx, hipStreamSynchronize(s));
-  return KCC_OK;
+  if (red == 0 && p2p == 0) return KCC_OK;
+  return fail(ctx, KCC_EFAULT,
+              "device fault: " + std::to_string(red) + " reduce look-back wait(s) and " +
+                  std::to_string(p2p) +
+                  " exchange flag wait(s) gave up; results are not valid (every spec is marked "
+                  "KCC_SPEC_FAULT) until kcc_clear_faults");
 }
 
 int reduce_async_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, const int64_t* ptr,
@@ -238,8 +263,8 @@ int reduce_async_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, con
   if (rc) return rc;
   KCC_HIP(ctx, kcc::launch_reduce(n_nodes, 0, n_cont, ptr, cpu, mem, lim ? cpul : nullptr,
                                   lim ? meml : nullptr, used_cpu, used_mem, lim ? lim_cpu : nullptr,
-                                  lim ? lim_mem : nullptr, as<uint64_t>(dv.red_tail), ++dv.red_epoch,
-                                  as<unsigned long long>(dv.red_faults), s));
+                                  lim ? lim_mem : nullptr, as<uint64_t>(dv.red_tail),
+                                  as<unsigned long long>(dv.faults), s));
   return KCC_OK;
 }
 
@@ -267,6 +292,11 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.srec, sizeof(kcc::SpecRec) * S));
   KCC_HIP(ctx, ensure(dv.sperm, 4 * S));
   KCC_HIP(ctx, ensure(dv.counters, sizeof(unsigned long long) * kcc::CNT_N));
+  if (!dv.clamp_arrive.p) {  // the fused finalize's arrivals: every launch leaves them zero
+    KCC_HIP(ctx, ensure(dv.clamp_arrive, 64));
+    KCC_HIP(ctx, hipMemsetAsync(dv.clamp_arrive.p, 0, 64, dv.stream));
+    KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
+  }
   // (a new allocation is a larger one: compare sizes, hipMalloc may hand back the address)
   const size_t q_before = dv.fit_q.bytes;
   KCC_HIP(ctx, ensure(dv.fit_q, 4 * (size_t)kcc::fit_queue_words((int64_t)S)));
@@ -450,7 +480,7 @@ int fit_finalize_dev(kcc_ctx* ctx, Dev& dv, int64_t n_specs, const int64_t* part
   if (dv.sperm.bytes < sizeof(int32_t) * (size_t)n_specs)
     return fail(ctx, KCC_EINVAL, "finalize without a matching fit_partial");
   KCC_HIP(ctx, kcc::launch_fit_finalize(n_specs, partial, as<int32_t>(dv.sperm), totals,
-                                        spec_err, s));
+                                        spec_err, as<const unsigned long long>(dv.faults), s));
   return KCC_OK;
 }
 
@@ -584,8 +614,8 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     }
     KCC_HIP(ctx, kcc::launch_reduce(n, c0[c], c1[c] - c0[c], ptr + lo[c], cpu, mem, nullptr, nullptr,
                                     used_cpu + lo[c], used_mem + lo[c], nullptr, nullptr,
-                                    as<uint64_t>(dv.red_tail), ++dv.red_epoch,
-                                    as<unsigned long long>(dv.red_faults), rs,
+                                    as<uint64_t>(dv.red_tail),
+                                    as<unsigned long long>(dv.faults), rs,
                                     fuse_rank ? &ra : nullptr));
     if (dv.prof_on) {
       KCC_HIP(ctx, hipEventRecord(pp.b, rs));
@@ -636,11 +666,9 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   }
   if (n_specs > 0) {
     const bool fuse_fin = totals && n_nodes > 0;
-    if (fuse_fin && !dv.clamp_arrive.p) {  // every launch leaves it zero
-      KCC_HIP(ctx, ensure(dv.clamp_arrive, 64));
-      KCC_HIP(ctx, hipMemsetAsync(dv.clamp_arrive.p, 0, 64, s));
-    }
-    const kcc::FinArgs fin{as<int32_t>(dv.sperm), totals, spec_err, as<uint32_t>(dv.clamp_arrive)};
+    // (clamp_arrive is allocated and zeroed by reserve_dev; every launch leaves it zero)
+    const kcc::FinArgs fin{as<int32_t>(dv.sperm), totals, spec_err, as<uint32_t>(dv.clamp_arrive),
+                           as<const unsigned long long>(dv.faults)};
     if (n_nodes > 0)
       KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, n_nodes, clamp_of(dv),
                                            as<unsigned long long>(dv.counters), partial, s,
@@ -777,7 +805,7 @@ int run_host(kcc_ctx* ctx, bool with_reduce, int64_t n_nodes, int64_t n_cont,
   ctx->host_stream_rows = streamed;
   const double pairs = (double)n_nodes * (double)n_specs;
   ctx->slow_frac = pairs > 0 ? (double)slow_pairs / pairs : 0.0;
-  return KCC_OK;
+  return check_faults(ctx);
 }
 
 }  // namespace
@@ -871,7 +899,7 @@ void kcc_destroy(kcc_ctx* ctx) {
       (void)hipDeviceSynchronize();  // exchanges ran on caller streams
       for (int p = 0; p < dv.p2p_W; ++p)
         if (p != dv.p2p_rank && dv.p2p_peer[p]) (void)hipIpcCloseMemHandle(dv.p2p_peer[p]);
-      DevBuf* pb[] = {&dv.p2p_mbox, &dv.p2p_arrive, &dv.p2p_faults};
+      DevBuf* pb[] = {&dv.p2p_mbox, &dv.p2p_arrive};
       for (DevBuf* b : pb)
         if (b->p) (void)hipFree(b->p);
     }
@@ -879,7 +907,7 @@ void kcc_destroy(kcc_ctx* ctx) {
     DevBuf* bufs[] = {&dv.c_rank, &dv.c_bcnt, &dv.c_cs, &dv.c_ms,
                       &dv.c_mrc, &dv.c_crm, &dv.c_dperm, &dv.c_C, &dv.c_H2, &dv.c_H3,
                       &dv.c_Crow, &dv.c_rec, &dv.c_dir,
-                      &dv.red_tail,  &dv.red_faults, &dv.rank_arrive, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
+                      &dv.red_tail,  &dv.faults, &dv.rank_arrive, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
                       &dv.sperm,     &dv.fit_q,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
                       &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,
@@ -977,7 +1005,7 @@ int kcc_reduce_requests(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containers,
                                 hipMemcpyDeviceToHost, dv.stream));
   }
   KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
-  return KCC_OK;
+  return check_faults(ctx);
 }
 
 int kcc_fit(kcc_ctx* ctx, int64_t n_nodes, const uint64_t* alloc_cpu, const int64_t* alloc_mem,
@@ -1195,14 +1223,28 @@ int kcc_reduce_faults(kcc_ctx* ctx, int64_t* faults) {
   if (!ctx || !faults) return ctx ? fail(ctx, KCC_EINVAL, "NULL output") : KCC_EINVAL;
   int64_t t = 0;
   for (Dev& dv : ctx->devs) {
-    if (!dv.red_faults.p) continue;
+    if (!dv.faults.p) continue;
     KCC_HIP(ctx, hipSetDevice(dv.device));
     KCC_HIP(ctx, hipDeviceSynchronize());
     unsigned long long f = 0;
-    KCC_HIP(ctx, hipMemcpy(&f, dv.red_faults.p, sizeof(f), hipMemcpyDeviceToHost));
+    KCC_HIP(ctx, hipMemcpy(&f, as<unsigned long long>(dv.faults) + kcc::FAULT_RED, sizeof(f),
+                           hipMemcpyDeviceToHost));
     t += (int64_t)f;
   }
   *faults = t;
+  return KCC_OK;
+}
+
+int kcc_clear_faults(kcc_ctx* ctx) {
+  if (!ctx) return KCC_EINVAL;
+  for (Dev& dv : ctx->devs) {
+    KCC_HIP(ctx, hipSetDevice(dv.device));
+    KCC_HIP(ctx, hipDeviceSynchronize());
+    if (dv.faults.p) KCC_HIP(ctx, hipMemset(dv.faults.p, 0, dv.faults.bytes));
+    // a wait that gave up left its record published: every tag back to free
+    if (dv.red_tail.p) KCC_HIP(ctx, hipMemset(dv.red_tail.p, 0, dv.red_tail.bytes));
+    KCC_HIP(ctx, hipDeviceSynchronize());
+  }
   return KCC_OK;
 }
 
@@ -1265,12 +1307,14 @@ int kcc_p2p_export(kcc_ctx* ctx, int n_ranks, int64_t max_specs, uint8_t* handle
   if (dv.p2p_W > 0) return fail(ctx, KCC_EINVAL, "mailbox already exported");
   KCC_HIP(ctx, hipSetDevice(dv.device));
   const size_t bytes = kcc::p2p_mbox_bytes(n_ranks, max_specs);
+  {
+    int rc = faults_ws(ctx, dv, dv.stream);
+    if (rc) return rc;
+  }
   KCC_HIP(ctx, ensure_uncached(dv.p2p_mbox, bytes));
   KCC_HIP(ctx, ensure(dv.p2p_arrive, 64));
-  KCC_HIP(ctx, ensure(dv.p2p_faults, 64));
   KCC_HIP(ctx, hipMemset(dv.p2p_mbox.p, 0, bytes));  // flags 0: no epoch seen
-  KCC_HIP(ctx, hipMemset(dv.p2p_arrive.p, 0, 64));
-  KCC_HIP(ctx, hipMemset(dv.p2p_faults.p, 0, 64));
+  KCC_HIP(ctx, hipMemset(dv.p2p_arrive.p, 0, 64));   // no arrivals, epoch 0 pushed
   KCC_HIP(ctx, hipDeviceSynchronize());
   static_assert(sizeof(hipIpcMemHandle_t) == KCC_P2P_HANDLE_BYTES, "IPC handle size");
   hipIpcMemHandle_t h;
@@ -1328,14 +1372,14 @@ int kcc_exchange_finalize_async(kcc_ctx* ctx, int64_t n_specs, const int64_t* d_
   a.smax = dv.p2p_smax;
   a.W = dv.p2p_W;
   a.rank = dv.p2p_rank;
-  a.epoch = ++dv.p2p_epoch;
+  a.epoch = as<uint64_t>(dv.p2p_arrive) + 1;  // (word 0: the arrival counter)
   a.partial = d_partial;
   for (int p = 0; p < dv.p2p_W; ++p) a.mbox[p] = dv.p2p_peer[p];
   a.perm = as<int32_t>(dv.sperm);
   a.totals = d_totals;
   a.spec_err = d_spec_err;
   a.arrive = as<uint32_t>(dv.p2p_arrive);
-  a.faults = as<unsigned long long>(dv.p2p_faults);
+  a.faults = as<unsigned long long>(dv.faults);
   KCC_HIP(ctx, kcc::launch_exchange_finalize(a, static_cast<hipStream_t>(stream)));
   return KCC_OK;
 }
@@ -1344,11 +1388,12 @@ int kcc_p2p_faults(kcc_ctx* ctx, int64_t* faults) {
   if (!ctx || !faults) return KCC_EINVAL;
   Dev& dv = ctx->devs[0];
   *faults = 0;
-  if (!dv.p2p_faults.p) return KCC_OK;
+  if (!dv.faults.p) return KCC_OK;
   KCC_HIP(ctx, hipSetDevice(dv.device));
   KCC_HIP(ctx, hipDeviceSynchronize());
   unsigned long long f = 0;
-  KCC_HIP(ctx, hipMemcpy(&f, dv.p2p_faults.p, sizeof(f), hipMemcpyDeviceToHost));
+  KCC_HIP(ctx, hipMemcpy(&f, as<unsigned long long>(dv.faults) + kcc::FAULT_P2P, sizeof(f),
+                         hipMemcpyDeviceToHost));
   *faults = (int64_t)f;
   return KCC_OK;
 }
@@ -1800,7 +1845,7 @@ int kcc_reduce_requests_pods(kcc_ctx* ctx, int64_t n_nodes, int64_t n_pods,
   KCC_HIP(ctx, hipMemcpyAsync(used_mem, dv.used_mem.p, 8 * (size_t)n_nodes,
                               hipMemcpyDeviceToHost, dv.stream));
   KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
-  return KCC_OK;
+  return check_faults(ctx);
 }
 
 }  // extern "C"

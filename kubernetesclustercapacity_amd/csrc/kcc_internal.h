@@ -11,7 +11,8 @@
 #if !defined(KCC_VARIANT_BUILD) &&                                                       \
     (defined(KCC_FIT_DIAG_NO_ATOMICS) || defined(KCC_DIAG_RED_NOSTORE) ||                \
      defined(KCC_DIAG_RED_LOADONLY) || defined(KCC_DIAG_NP) || defined(KCC_DIAG_CP) ||   \
-     defined(KCC_TIMELINE) || defined(KCC_RED_XCD_MAP))
+     defined(KCC_TIMELINE) || defined(KCC_RED_XCD_MAP) || defined(KCC_DIAG_RED_GIVEUP) ||  \
+     defined(KCC_DIAG_P2P_GIVEUP))
 #error "a diagnostic KCC_* knob in a release build: use `make variant` (KCC_VARIANT_BUILD)"
 #endif
 
@@ -26,7 +27,10 @@ struct RankArgs;   // below: spec ranks, run as extra workgroups of a reduce lau
 // the node owning its first container by a 64-ary search of the CSR offsets, stores
 // every node that ends inside its range, and a node cut by range boundaries is
 // assembled by the wave where it ends from the pieces its predecessors publish
-// (decoupled look-back over per-wave tail records, tagged with the launch's epoch).
+// (decoupled look-back over per-wave tail records: each record is published at most once
+// per launch and consumed by exactly one wave, which clears its tag — every tag is 0
+// between launches, so nothing in the launch depends on host state and a captured graph
+// replays correctly).
 #ifndef KCC_RED_ROUNDS
 #define KCC_RED_ROUNDS 1  // waves = this many rounds of the resident wave capacity
 #endif
@@ -48,6 +52,15 @@ constexpr int64_t RED_MAX_NODES = (int64_t)1 << 28;
 // per-wave tail record: the NA values of the node open at the range end, then the tag
 constexpr int RED_TAIL_WORDS = 8;  // 64 B: one line per wave
 constexpr int RED_TAIL_TAG = 7;
+constexpr uint64_t RED_TAG_READY = 1;  // published (0: free; the consumer clears it)
+
+// Device fault words (one 64-B line per device, zero until a wait gives up; sticky until
+// kcc_clear_faults): the reduce's look-back waits and the exchange's flag waits that gave
+// up.  Every finalize reads them and marks every spec KCC_SPEC_FAULT while either is set,
+// and the synchronous entry points return KCC_EFAULT.
+enum { FAULT_RED = 0, FAULT_P2P = 1, FAULT_WORDS = 8 };
+constexpr int32_t SPEC_ERR_DIV0 = 1;   // include/kcc.h KCC_SPEC_DIVZERO
+constexpr int32_t SPEC_ERR_FAULT = 2;  // include/kcc.h KCC_SPEC_FAULT
 
 // Containers per wave range: whole tiles, sized so the waves fill the device's resident
 // wave slots (occupancy API) in KCC_RED_ROUNDS rounds: one round of equal, long ranges
@@ -75,9 +88,8 @@ struct RedArgs {
   const int64_t* ptr;
   const uint64_t* in[4];
   uint64_t* out[4];
-  uint64_t* tail;                  // [reduce_tail_records()][RED_TAIL_WORDS]
-  uint64_t epoch;                  // this launch's tag (never 0, never reused)
-  unsigned long long* faults;      // look-back waits that timed out (stays 0)
+  uint64_t* tail;                  // [reduce_tail_records()][RED_TAIL_WORDS], tags 0
+  unsigned long long* faults;      // the device's fault words (FAULT_RED: look-back give-ups)
 };
 // rank != nullptr (with rank->n_blocks > 0): the spec ranks run as that many extra
 // workgroups in front of the reduce's (independent work, one launch fewer per step).
@@ -85,7 +97,7 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
                          const uint64_t* cpu_req, const int64_t* mem_req,
                          const uint64_t* cpu_lim, const int64_t* mem_lim,
                          uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem,
-                         uint64_t* tail, uint64_t epoch, unsigned long long* faults, hipStream_t s,
+                         uint64_t* tail, unsigned long long* faults, hipStream_t s,
                          const RankArgs* rank = nullptr);
 
 // ---- (b) fit -----------------------------------------------------------------
@@ -323,6 +335,7 @@ struct FinArgs {
   int64_t* totals;
   int32_t* spec_err;
   uint32_t* arrive;
+  const unsigned long long* faults;  // the device's fault words: set -> KCC_SPEC_FAULT
 };
 hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
                               const unsigned long long* counters, int64_t* partial, hipStream_t s,
@@ -370,9 +383,11 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
 constexpr int64_t FIT_QSUBS_MAX = 32;
 inline int64_t fit_queue_words(int64_t S) { return (S + 255) / 256 * FIT_QSUBS_MAX * 16; }
 
+// totals[perm[i]] = err ? 0 : partial[i], spec_err[perm[i]] = err (KCC_SPEC_DIVZERO when
+// partial[S + i] != 0; KCC_SPEC_FAULT for every spec while a fault word is set)
 hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial,
                                const int32_t* perm, int64_t* totals, int32_t* spec_err,
-                               hipStream_t s);
+                               const unsigned long long* faults, hipStream_t s);
 // dst[k] += src[k] (wrapping int64), k < n: folds one node shard's partial vector into
 // another on the same device (the host-array entry points with more shards than devices)
 hipError_t launch_partial_add(int64_t n, int64_t* dst, const int64_t* src, hipStream_t s);
@@ -391,6 +406,8 @@ hipError_t launch_partial_add(int64_t n, int64_t* dst, const int64_t* src, hipSt
 // W flags of this epoch in its own mailbox, then sums the W vectors and finalizes
 // (totals[perm[i]], spec_err[perm[i]]).  Parity = epoch & 1: a rank can only push epoch
 // e + 2 after every peer pushed e + 1, i.e. after every peer's launch for e read its data.
+// The epoch lives in device memory (the last workgroup to push advances it), so every
+// launch — a replay of a captured graph included — uses the next one.
 constexpr int P2P_MAX_RANKS = 8;
 __host__ __device__ inline size_t p2p_flag_words(int W) { return (size_t)2 * W * 8; }
 inline size_t p2p_mbox_bytes(int W, int64_t smax) {
@@ -399,14 +416,17 @@ inline size_t p2p_mbox_bytes(int W, int64_t smax) {
 struct P2PArgs {
   int64_t S, smax;
   int32_t W, rank;
-  uint64_t epoch;                         // >= 1, +1 per launch (every rank the same)
+  uint64_t* epoch;                        // this rank's last pushed epoch (device word, 0 at
+                                          // export; the launch pushes *epoch + 1)
   const int64_t* partial;                 // [2S] this rank's (internal order)
   unsigned char* mbox[P2P_MAX_RANKS];     // rank p's mailbox (this rank's own at [rank])
   const int32_t* perm;                    // internal -> caller index (this rank's fit)
   int64_t* totals;
   int32_t* spec_err;
   uint32_t* arrive;                       // this rank's push arrivals (zero between launches)
-  unsigned long long* faults;             // flag waits that gave up (stays 0)
+  unsigned long long* faults;             // the device's fault words (FAULT_P2P: flag waits
+                                          // that gave up; a workgroup that gave up marks its
+                                          // specs KCC_SPEC_FAULT)
 };
 hipError_t launch_exchange_finalize(const P2PArgs& a, hipStream_t s);
 

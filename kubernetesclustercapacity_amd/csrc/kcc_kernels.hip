@@ -45,6 +45,14 @@ __device__ __forceinline__ unsigned long long atomic_add_u64(uint64_t* p, uint64
                    static_cast<unsigned long long>(v));
 }
 
+// A fault word of the device is set (a reduce look-back or exchange flag wait gave up):
+// the step's results are not trustworthy and every finalize marks every spec.
+__device__ __forceinline__ bool device_faulted(const unsigned long long* f) {
+  if (!f) return false;
+  return (__hip_atomic_load(f + FAULT_RED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+          __hip_atomic_load(f + FAULT_P2P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0;
+}
+
 // ----------------------------------------------------------------------------
 // (a) segmented reduce
 // ----------------------------------------------------------------------------
@@ -212,7 +220,15 @@ __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff
 // before it waits, so waits never chain; a wave waits only for lower-indexed waves,
 // dispatched before it).  No atomics, nothing to zero between launches.
 constexpr uint32_t RED_OOB_OFFSET = 0x7ffffff0u;  // > any output's range (n_nodes < 2^28)
-constexpr uint32_t RED_SPIN_MAX = 1u << 18;       // look-back polls before a wait gives up
+[[maybe_unused]] constexpr uint32_t RED_SPIN_MAX = 1u << 18;       // look-back polls before a wait gives up
+// Look-back ordering (KCC_RED_LB_ACQREL, A/B knob): 1 (default) = the memory model's
+// release / acquire — the publishing lane stores the piece, then the tag with a release
+// store at agent scope; the consumer polls the tag relaxed and issues an agent-scope
+// acquire fence once it matched, before it loads the piece.  0 = round 3's form (relaxed
+// agent-scope stores, s_waitcnt vmcnt(0) before the tag, a compiler barrier after the poll).
+#ifndef KCC_RED_LB_ACQREL
+#define KCC_RED_LB_ACQREL 1
+#endif
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds);
@@ -306,6 +322,9 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
   const bool first_open = p0 < wb;                      // node0 began in an earlier range
   const int64_t own_lo = node0 + (first_open ? 1 : 0);  // first node stored by the flushes
   int64_t cur = node0;  // node holding the current tile's first item
+  // start of node cur relative to wb (<= 0 for node0): when it is < len at the range end,
+  // node cur continues into the next range and its piece here is published
+  int32_t open_start = p0 - wb < -1 ? -1 : (int32_t)(p0 - wb);
   uint64_t carry[NA];   // node cur's running sum over the earlier tiles of this range
   uint64_t res[NA];     // sums of block blk's nodes (lane l <-> node 64*blk + l)
   uint64_t head[NA];    // node0's piece in this range, when first_open (wave-uniform)
@@ -453,6 +472,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
     }
     eNr = ptr_at(ptr, 64 * blk + 65 + lane, n_nodes);  // next block's ends (usually L2 hits)
     have_next = true;
+    if (last_end >= 0) open_start = last_end;
     if (last_end > tb) {  // node cur is open at the tile end: its sum so far
 #pragma unroll
       for (int k = 0; k < NA; ++k)
@@ -488,18 +508,24 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
 #endif
     }
   }
-  // publish: node cur continues into the next range; its piece here is `carry` (the
-  // values with agent-scope (sc1) stores, drained, then the tag, as a separate store)
+  // publish: node cur continues into the next range (it began before the range end);
+  // its piece here is `carry`.  Lane 0 stores the piece and then the tag (release).
+  // Exactly one later wave consumes the record (the wave where node cur ends: it looks
+  // back over every range the node spans) and clears the tag, so every tag is 0 between
+  // launches and a record is never published for a node that starts at the next range.
   uint64_t* const rec = a.tail + (int64_t)w * RED_TAIL_WORDS;
-  if (wb + len < n_cont) {
-    if (lane < NA) {
-      uint64_t v = carry[0];
+  if (wb + len < n_cont && open_start < len) {
+    if (lane == 0) {
 #pragma unroll
-      for (int k = 1; k < NA; ++k) v = lane == k ? carry[k] : v;
-      __hip_atomic_store(rec + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = 0; k < NA; ++k)
+        __hip_atomic_store(rec + k, carry[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if KCC_RED_LB_ACQREL
+      __hip_atomic_store(rec + RED_TAIL_TAG, RED_TAG_READY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(rec + RED_TAIL_TAG, RED_TAG_READY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(rec + RED_TAIL_TAG, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // look-back: node0 began in an earlier range and ended in this one
   if (first_open && cur > node0) {
@@ -513,21 +539,35 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
 #pragma unroll
       for (int k = 0; k < NA; ++k) v[k] = 0;
       if (wi < w) {
-        const uint64_t* r = a.tail + wi * RED_TAIL_WORDS;
+        uint64_t* r = a.tail + wi * RED_TAIL_WORDS;
+        bool seen = true;
+#ifdef KCC_DIAG_RED_GIVEUP  // fault-path test builds only: every wait gives up at once
+        seen = false;
+        atomicAdd(&a.faults[FAULT_RED], 1ull);
+#else
         uint32_t spins = 0;
-        while (__hip_atomic_load(r + RED_TAIL_TAG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.epoch) {
+        while (__hip_atomic_load(r + RED_TAIL_TAG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+               RED_TAG_READY) {
           if (++spins >= RED_SPIN_MAX) {  // never on a healthy device: count it, go on
-            atomicAdd(a.faults, 1ull);
+            atomicAdd(&a.faults[FAULT_RED], 1ull);
+            seen = false;
             break;
           }
           __builtin_amdgcn_s_sleep(2);
         }
-        // the values only after the tag matched: relaxed loads of other addresses may be
-        // hoisted above the poll by the compiler (they were), so a compiler barrier here;
-        // the hardware issues them after the poll's data returned (the branch needs it)
+#endif
+#if KCC_RED_LB_ACQREL
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // synchronizes with the release
+#else
+        // relaxed loads of other addresses may be hoisted above the poll by the compiler
+        // (they were); the hardware issues them after the poll's data returned
         asm volatile("" ::: "memory");
+#endif
 #pragma unroll
         for (int k = 0; k < NA; ++k) v[k] = __hip_atomic_load(r + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // consumed: free the record for the next launch (a wait that gave up leaves it:
+        // the context is faulted until kcc_clear_faults re-zeroes the records)
+        if (seen) __hip_atomic_store(r + RED_TAIL_TAG, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
 #pragma unroll
       for (int k = 0; k < NA; ++k) acc[k] += wave_sum_u64(v[k]);
@@ -1815,6 +1855,7 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   __syncthreads();
   if (!last_s) return;
   if (threadIdx.x == 0) __hip_atomic_store(fin.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool faulted = device_faulted(fin.faults);
   // FIN_PER specs per thread per round, every load of the round issued before any store
   // (one memory round trip per round: S <= 4096 is one round)
   constexpr int FIN_PER = 4;
@@ -1832,8 +1873,8 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
 #pragma unroll
     for (int k = 0; k < FIN_PER; ++k) {
       if (i0 + (int64_t)k * CP_THREADS >= S) break;
-      fin.totals[dst[k]] = e[k] != 0 ? 0 : t[k];
-      fin.spec_err[dst[k]] = e[k] != 0 ? 1 : 0;
+      fin.totals[dst[k]] = e[k] != 0 || faulted ? 0 : t[k];
+      fin.spec_err[dst[k]] = faulted ? SPEC_ERR_FAULT : e[k] != 0 ? SPEC_ERR_DIV0 : 0;
     }
   }
 }
@@ -2329,24 +2370,31 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
 
 __global__ void fit_finalize_kernel(int64_t S, const int64_t* __restrict__ partial,
                                     const int32_t* __restrict__ perm, int64_t* __restrict__ totals,
-                                    int32_t* __restrict__ spec_err) {
+                                    int32_t* __restrict__ spec_err,
+                                    const unsigned long long* __restrict__ faults) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= S) return;
   const int32_t dst = perm[i];
-  const bool err = partial[S + i] != 0;
-  totals[dst] = err ? 0 : partial[i];
-  spec_err[dst] = err ? 1 : 0;
+  const bool err = partial[S + i] != 0, faulted = device_faulted(faults);
+  totals[dst] = err || faulted ? 0 : partial[i];
+  spec_err[dst] = faulted ? SPEC_ERR_FAULT : err ? SPEC_ERR_DIV0 : 0;
 }
 
 // One-shot exchange + finalize (P2PArgs, kcc_internal.h).  256 threads, specs strided over
 // the grid (at most P2P_MAX_WG workgroups: all resident at once, since each waits for the
 // flag the last one publishes).
-constexpr uint32_t P2P_SPIN_MAX = 1u << 21;  // flag polls before a wait gives up (seconds)
+[[maybe_unused]] constexpr uint32_t P2P_SPIN_MAX = 1u << 21;  // flag polls before a wait gives up (seconds)
 constexpr int64_t P2P_MAX_WG = 256;
 __global__ __launch_bounds__(256) void exchange_finalize_kernel(P2PArgs a) {
   const int64_t S = a.S, smax = a.smax, i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t gs = (int64_t)gridDim.x * 256;
-  const int W = a.W, par = (int)(a.epoch & 1u);
+  // this launch's epoch: one past the last one pushed (a device word that the launch's last
+  // workgroup to push advances, after every workgroup read it here: each reads it before
+  // it arrives), so a replayed graph pushes a new epoch every time
+  const uint64_t epoch = __hip_atomic_load(a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  // a fault word set before this launch (an earlier give-up): the results stay marked
+  const bool faulted_in = device_faulted(a.faults);
+  const int W = a.W, par = (int)(epoch & 1u);
   const int64_t slot = ((int64_t)par * W + a.rank) * 2 * smax;  // this sender's data slot
   const size_t fw = p2p_flag_words(W);
   // 1. push this rank's two words of each of its specs into every mailbox
@@ -2364,26 +2412,37 @@ __global__ __launch_bounds__(256) void exchange_finalize_kernel(P2PArgs a) {
     const uint32_t old = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (old == gridDim.x - 1u) {  // every workgroup has pushed: publish the epoch
       __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.epoch, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (int p = 0; p < W; ++p)
         __hip_atomic_store(reinterpret_cast<uint64_t*>(a.mbox[p]) + ((int64_t)par * W + a.rank) * 8,
-                           a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                           epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   // 2. every sender's flag of this epoch in this rank's own mailbox (thread p polls p's)
+  __shared__ uint32_t gave_up;
+  if (threadIdx.x == 0) gave_up = 0;
+  __syncthreads();
   if (threadIdx.x < (unsigned)W) {
+#ifdef KCC_DIAG_P2P_GIVEUP  // fault-path test builds only: every wait gives up at once
+    atomicAdd(&a.faults[FAULT_P2P], 1ull);
+    gave_up = 1;
+#else
     const uint64_t* f =
         reinterpret_cast<const uint64_t*>(a.mbox[a.rank]) + ((int64_t)par * W + threadIdx.x) * 8;
     uint32_t spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != a.epoch) {
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
       if (++spins >= P2P_SPIN_MAX) {  // a peer never pushed: count it, go on (never on a healthy run)
-        atomicAdd(a.faults, 1ull);
+        atomicAdd(&a.faults[FAULT_P2P], 1ull);
+        gave_up = 1;  // (a plain LDS store: any waiter that gave up sets it)
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
+#endif
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale mailbox lines
+  const bool faulted = faulted_in || gave_up != 0;
   // 3. the sums over the W senders, finalized
   const int64_t* d = reinterpret_cast<const int64_t*>(a.mbox[a.rank]) + fw + (int64_t)par * W * 2 * smax;
   for (int64_t i = i0; i < S; i += gs) {
@@ -2393,8 +2452,8 @@ __global__ __launch_bounds__(256) void exchange_finalize_kernel(P2PArgs a) {
       s1 += (uint64_t)__builtin_nontemporal_load(d + (int64_t)p * 2 * smax + smax + i);
     }
     const int32_t dst = a.perm[i];
-    a.totals[dst] = s1 != 0 ? 0 : (int64_t)s0;
-    a.spec_err[dst] = s1 != 0 ? 1 : 0;
+    a.totals[dst] = s1 != 0 || faulted ? 0 : (int64_t)s0;
+    a.spec_err[dst] = faulted ? SPEC_ERR_FAULT : s1 != 0 ? SPEC_ERR_DIV0 : 0;
   }
 }
 
@@ -2466,7 +2525,7 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
                          const uint64_t* cpu_req, const int64_t* mem_req,
                          const uint64_t* cpu_lim, const int64_t* mem_lim,
                          uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem,
-                         uint64_t* tail, uint64_t epoch, unsigned long long* faults, hipStream_t s,
+                         uint64_t* tail, unsigned long long* faults, hipStream_t s,
                          const RankArgs* rank) {
   RankArgs ra{};
   if (rank) ra = *rank;
@@ -2506,7 +2565,6 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
   a.out[2] = limits ? lim_cpu : nullptr;
   a.out[3] = limits ? reinterpret_cast<uint64_t*>(lim_mem) : nullptr;
   a.tail = tail;
-  a.epoch = epoch;
   a.faults = faults;
   if (limits)
     hipLaunchKernelGGL(reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, a, ra);
@@ -2641,17 +2699,18 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
 }
 
 hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial, const int32_t* perm,
-                               int64_t* totals, int32_t* spec_err, hipStream_t s) {
+                               int64_t* totals, int32_t* spec_err,
+                               const unsigned long long* faults, hipStream_t s) {
   if (n_specs <= 0) return hipSuccess;
   hipLaunchKernelGGL(fit_finalize_kernel, dim3(grid_for(n_specs, 256, 1 << 30)), dim3(256), 0, s,
-                     n_specs, partial, perm, totals, spec_err);
+                     n_specs, partial, perm, totals, spec_err, faults);
   return hipGetLastError();
 }
 
 hipError_t launch_exchange_finalize(const P2PArgs& a, hipStream_t s) {
   if (a.S <= 0) return hipSuccess;
   if (a.S > a.smax || a.W < 1 || a.W > P2P_MAX_RANKS || a.rank < 0 || a.rank >= a.W ||
-      a.epoch == 0)
+      !a.epoch || !a.faults || !a.arrive)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(exchange_finalize_kernel, dim3(grid_for(a.S, 256, P2P_MAX_WG)), dim3(256), 0, s, a);
   return hipGetLastError();

@@ -61,8 +61,8 @@ class RequestSums:
 class CapacityEngine:
     """One libkcc context (one device, or n_gpus devices with node sharding + RCCL)."""
 
-    def __init__(self, device: int = 0, n_gpus: int = 1):
-        self._lib = _lib.lib()
+    def __init__(self, device: int = 0, n_gpus: int = 1, lib_path: str | None = None):
+        self._lib = _lib.lib(lib_path)
         h = C.c_void_p()
         rc = self._lib.kcc_create(C.byref(h), device, n_gpus)
         if rc != 0:
@@ -399,7 +399,7 @@ class CapacityEngine:
         """Rank 0 of a one-process-per-GPU run: the RCCL id every rank passes to
         comm_init (opaque bytes, distributed by the caller)."""
         buf = C.create_string_buffer(COMM_ID_BYTES)
-        rc = _lib.lib().kcc_comm_unique_id(C.cast(buf, C.c_void_p))
+        rc = _lib.lib().kcc_comm_unique_id(C.cast(buf, C.c_void_p))  # (release build)
         if rc != 0:
             raise KccError(rc, "ncclGetUniqueId failed")
         return buf.raw
@@ -483,6 +483,10 @@ class CapacityEngine:
         v = C.c_int64()
         self._check(self._lib.kcc_reduce_faults(self._h, C.byref(v)))
         return v.value
+
+    def clear_faults(self):
+        """Reset the device fault words and the reduce's look-back records."""
+        self._check(self._lib.kcc_clear_faults(self._h))
 
     def fit_slow_pairs(self):
         a, b = C.c_int64(), C.c_int64()

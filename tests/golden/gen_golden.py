@@ -105,7 +105,7 @@ CASES = {
     "edge": edge_case,
     "small": lambda: cluster_case(300, 6_000, 64, 11),
     "adversarial": lambda: cluster_case(300, 6_000, 64, 12, adversarial=True),
-    "skew": lambda: cluster_case(200, 4_000, 32, 13, skew=True),
+    "skew": lambda: cluster_case(200, 4_000, 32, 13, skew="zipf"),  # SURVEY §8d Zipf(1.2)
     "sparse": lambda: cluster_case(2_000, 300, 16, 14, unhealthy=0.2),   # mostly empty nodes
 }
 
@@ -128,12 +128,15 @@ def parse_case():
 
 
 def main():
-    path = os.path.join(HERE, "parse.npz")
-    np.savez_compressed(path, **parse_case())
-    print(f"{path}")
-    if len(sys.argv) > 1 and sys.argv[1] == "parse":
-        return
+    """No argument: every fixture; otherwise only the named ones (parse, edge, small, ...)."""
+    want = set(sys.argv[1:]) or {"parse", *CASES}
+    if "parse" in want:
+        path = os.path.join(HERE, "parse.npz")
+        np.savez_compressed(path, **parse_case())
+        print(f"{path}")
     for name, fn in CASES.items():
+        if name not in want:
+            continue
         d = fn()
         d.update(expected(d))
         path = os.path.join(HERE, f"{name}.npz")

@@ -11,7 +11,8 @@ so any split of the rows into contiguous shards must give the same totals bit fo
     against its own 1-rank run.
 Configs (BASELINE.json `configs`) against the C oracle, every spec, at full size:
 C2 (10k x 200k pods x 1 spec), C3 (100k x 2M x 256), C4 (1M x 20M x 4096), and the C5
-rank-0 shard of an 8-way split (625k of 5M Zipf-skewed nodes x 16384 specs).
+rank-0 and rank-7 shards of an 8-way split (625k of 5M nodes with Zipf(1.2) pods per node,
+capped at 2 x allocatable pods — SURVEY §8d — x 16384 specs).
 """
 import json
 import os
@@ -122,12 +123,17 @@ def test_c4_rank_shards_like_bench(c4, c4_oracle, k):
     np.testing.assert_array_equal(t, c4_oracle[0])
 
 
-# ---- skewed (Zipf) cluster with the adversarial slice, sharded -----------------------------
-@pytest.mark.parametrize("k", [1, 2, 5, 8])
-def test_zipf_adversarial_shards(engine, k):
-    c = synth.make_cluster(200_003, 4_000_000, seed=55, skew=True, adversarial=True, chunk=4096)
+# ---- skewed (Zipf(1.2) pods per node) cluster with the adversarial slice, sharded ----------
+@pytest.fixture(scope="module")
+def zipf_adv():
+    c = synth.make_cluster(80_003, 0, seed=55, skew="zipf", adversarial=True, chunk=4096)
     sc, sm = synth.make_specs(1000, seed=55, adversarial=True)
-    ot, oe = oracle_totals(c, sc, sm)
+    return c, sc, sm, oracle_totals(c, sc, sm)
+
+
+@pytest.mark.parametrize("k", [1, 2, 5, 8])
+def test_zipf_adversarial_shards(engine, zipf_adv, k):
+    c, sc, sm, (ot, oe) = zipf_adv
     engine.set_node_shards(k)
     try:
         t, e = capacity(engine, c, sc, sm)
@@ -186,12 +192,15 @@ def test_config_every_spec_vs_oracle(engine, name):
     np.testing.assert_array_equal(t, ot)
 
 
-def test_c5_rank0_shard_every_spec_vs_oracle(engine):
-    """C5 = 5M Zipf-skewed nodes x 16384 specs over 8 GPUs: rank 0's node range."""
-    lo, hi = node_range(synth.CONFIGS["C5"]["n_nodes"], 0, 8)
-    c = synth.config_cluster("C5", node_lo=lo, node_hi=hi)
+@pytest.mark.parametrize("rank", [0, 7])
+def test_c5_rank_shard_every_spec_vs_oracle(engine, rank):
+    """C5 = 5M nodes (Zipf(1.2) pods per node, capped at 2 x allocatable pods) x 16384 specs
+    over 8 GPUs: rank 0's and rank 7's node ranges (~150M containers each)."""
+    lo, hi = node_range(synth.CONFIGS["C5"]["n_nodes"], rank, 8)
+    c = synth.config_cluster("C5", node_lo=lo, node_hi=hi, limits=False)
     sc, sm = synth.config_specs("C5")
     assert c.n_nodes == 625_000 and sc.size == 16384
+    assert c.meta["skew"] == "zipf" and c.pod_count.mean() > 100  # the survey's heavy tail
     r = engine.get_pod_cpu_memory_requests_limits(c.node_ptr, c.cpu_req, c.mem_req)
     np.testing.assert_array_equal(r.cpu_requests, seg_sums(c.node_ptr, c.cpu_req))
     np.testing.assert_array_equal(r.memory_requests.view(np.uint64), seg_sums(c.node_ptr, c.mem_req))
@@ -223,6 +232,23 @@ def test_bench_two_ranks_equal_one():
     assert two["config"]["nodes_rank0"] == 50_000
     assert two["totals_checksum"] == one["totals_checksum"]
     assert two["spec_errors"] == one["spec_errors"]
+    # the exchange proved itself before the timed steps (p2p, no fallback needed)
+    pre = two["exchange_precheck"]
+    assert pre["verified_before_timing"] and pre["exchanges_tried"] == ["p2p"]
+    assert two["exchange_check"]["equals_allreduce_finalize"]
+    assert "exchange_precheck" not in one
+
+
+def test_bench_exchange_fallback_drill():
+    """--drill-exchange-fallback: the p2p pre-timing check reads as failed on the last
+    rank, every rank switches to the fallback exchange (gloo: torch's all-reduce; RCCL
+    under nccl), re-verifies it, and the totals are still the single-rank ones."""
+    one = _bench("--gpus", "1")
+    two = _bench("--gpus", "2", "--dist-backend", "gloo", "--drill-exchange-fallback")
+    pre = two["exchange_precheck"]
+    assert pre["verified_before_timing"] and pre["exchanges_tried"] == ["p2p", "torch"]
+    assert "failed its pre-timing check" in two["world"]["exchange_note"]
+    assert two["totals_checksum"] == one["totals_checksum"]
 
 
 # ---- the fit's node stream: compacted (default) == every row (dense) -----------------------

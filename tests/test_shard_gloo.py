@@ -134,7 +134,7 @@ def test_gpu_rank_partials_equal_whole(tmp_path, world):
     np.testing.assert_array_equal(got[S:], e)
 
 
-def _worker_p2p(rank, world, port, n, pods, S, adversarial, steps, out):
+def _worker_p2p(rank, world, port, n, pods, S, adversarial, steps, out, graph=False):
     """Every rank: its node shard's partial from libkcc on cuda:0, then the one-shot
     exchange (kcc_exchange_finalize_async: push to every peer's mailbox, wait, sum,
     finalize) — the ranks sharing the box's one GPU, their mailboxes mapped through IPC
@@ -164,10 +164,36 @@ def _worker_p2p(rank, world, port, n, pods, S, adversarial, steps, out):
         eng.p2p_open(rank, handles)
         dist.barrier()
         got = []
-        for _ in range(steps):
-            eng.capacity_partial_async(c.node_ptr, *args)
-            eng.exchange_finalize_async(S, part, totals, err)
-            got.append(np.concatenate([totals.cpu().numpy(), err.cpu().numpy().astype(np.int64)]))
+        if not graph:
+            for _ in range(steps):
+                eng.capacity_partial_async(c.node_ptr, *args)
+                eng.exchange_finalize_async(S, part, totals, err)
+                got.append(np.concatenate([totals.cpu().numpy(), err.cpu().numpy().astype(np.int64)]))
+        else:
+            # one eager step, then the step captured into a hipGraph and replayed `steps`
+            # times, the spec set alternating between two (copied into the captured
+            # buffers): each replay must push a new epoch (the device word), or a rank
+            # would read the previous replay's mailbox data
+            specs = [synth.make_specs(S, seed=78 + k, adversarial=adversarial) for k in (0, 1)]
+            dspecs = [(T(a), T(b)) for a, b in specs]
+            stream = torch.cuda.Stream(dev)
+            with torch.cuda.stream(stream):
+                eng.capacity_partial_async(c.node_ptr, *args, stream=stream)
+                eng.exchange_finalize_async(S, part, totals, err, stream=stream)
+            stream.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=stream, capture_error_mode="thread_local"):
+                eng.capacity_partial_async(c.node_ptr, *args, stream=stream)
+                eng.exchange_finalize_async(S, part, totals, err, stream=stream)
+            for k in range(steps):
+                with torch.cuda.stream(stream):
+                    args[9].copy_(dspecs[k % 2][0])
+                    args[10].copy_(dspecs[k % 2][1])
+                    totals.fill_(-1)
+                    g.replay()
+                stream.synchronize()
+                got.append(np.concatenate([totals.cpu().numpy(), err.cpu().numpy().astype(np.int64)]))
+            del g
         faults = eng.p2p_faults()
         dist.barrier()  # no rank unmaps its mailbox while a peer may still push
     np.save(out + f".{rank}.npy", np.stack(got + [np.full(2 * S, faults, np.int64)]))
@@ -195,3 +221,29 @@ def test_gpu_p2p_exchange_equals_whole(tmp_path, world, S):
         for k in range(steps):
             np.testing.assert_array_equal(got[k][:S], t, err_msg=f"rank {r} step {k}")
             np.testing.assert_array_equal(got[k][S:], e, err_msg=f"rank {r} step {k}")
+
+
+@pytest.mark.gpu
+def test_gpu_p2p_exchange_graph_replay(tmp_path):
+    """kcc_capacity_partial_async + kcc_exchange_finalize_async captured into a hipGraph on
+    each of 2 ranks (sharing the GPU, mailboxes mapped through IPC) and replayed 4 times
+    with the spec set alternating between two: every replay == the oracle of its specs,
+    no flag wait gave up."""
+    n, pods, S, world, steps = 20_011, 300_000, 300, 2, 4
+    out = str(tmp_path / "p2pg")
+    mp.spawn(_worker_p2p, args=(world, _free_port(), n, pods, S, True, steps, out, True),
+             nprocs=world, join=True)
+    c = synth.make_cluster(n, pods, seed=78, adversarial=True, chunk=256)
+    from oracle import coracle
+    uc, um, _, _ = coracle.reduce_requests(c.node_ptr, c.cpu_req, c.mem_req)
+    ref = []
+    for k in (0, 1):
+        sc, sm = synth.make_specs(S, seed=78 + k, adversarial=True)
+        ref.append(coracle.fit(c.alloc_cpu, c.alloc_mem, c.alloc_pods, c.pod_count, uc, um, sc, sm))
+    for r in range(world):
+        got = np.load(out + f".{r}.npy")
+        assert got[-1][0] == 0, f"rank {r}: {got[-1][0]} flag waits gave up"
+        for k in range(steps):
+            t, e = ref[k % 2]
+            np.testing.assert_array_equal(got[k][:S], t, err_msg=f"rank {r} replay {k}")
+            np.testing.assert_array_equal(got[k][S:], e, err_msg=f"rank {r} replay {k}")
