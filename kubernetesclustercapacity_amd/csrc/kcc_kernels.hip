@@ -221,14 +221,23 @@ __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff
 // dispatched before it).  No atomics, nothing to zero between launches.
 constexpr uint32_t RED_OOB_OFFSET = 0x7ffffff0u;  // > any output's range (n_nodes < 2^28)
 [[maybe_unused]] constexpr uint32_t RED_SPIN_MAX = 1u << 18;       // look-back polls before a wait gives up
-// Look-back ordering (KCC_RED_LB_ACQREL, A/B knob): 1 (default) = the memory model's
-// release / acquire — the publishing lane stores the piece, then the tag with a release
-// store at agent scope; the consumer polls the tag relaxed and issues an agent-scope
-// acquire fence once it matched, before it loads the piece.  0 = round 3's form (relaxed
-// agent-scope stores, s_waitcnt vmcnt(0) before the tag, a compiler barrier after the poll).
-#ifndef KCC_RED_LB_ACQREL
-#define KCC_RED_LB_ACQREL 1
+// Look-back publication (KCC_RED_LB_MODE, A/B knob):
+//   2 (default) = tagged words: each 64-bit value of the piece travels as two 64-bit
+//     words {tag:32 | half:32}, stored by 2 x NA lanes as relaxed agent-scope atomics; the
+//     consumer polls the words until every tag matches and assembles the halves.  Every
+//     word is single-copy atomic and validates itself, so no ordering between the stores
+//     is needed at all — exact under the HIP memory model, without fences or a
+//     vmcnt(0) drain;
+//   1 = release / acquire on a separate tag word (buffer_wbl2 sc1 at the release, an L2
+//     invalidate at the acquire): exact too, but measured 2.3x slower at C4 (0.125 ->
+//     0.290 ms; 8-way shard 0.022 -> 0.096 ms, r04b): every publishing wave writes back
+//     its XCD's L2;
+//   0 = round 3's form: relaxed agent-scope stores, s_waitcnt vmcnt(0), then the tag; a
+//     compiler barrier after the poll (relies on the hardware completing in order).
+#ifndef KCC_RED_LB_MODE
+#define KCC_RED_LB_MODE 2
 #endif
+constexpr uint64_t RED_WORD_TAG = 0x4B43C0DEull << 32;  // upper half of a published word
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds);
@@ -509,24 +518,34 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
     }
   }
   // publish: node cur continues into the next range (it began before the range end);
-  // its piece here is `carry`.  Lane 0 stores the piece and then the tag (release).
-  // Exactly one later wave consumes the record (the wave where node cur ends: it looks
-  // back over every range the node spans) and clears the tag, so every tag is 0 between
-  // launches and a record is never published for a node that starts at the next range.
+  // its piece here is `carry`.  Exactly one later wave consumes the record (the wave where
+  // node cur ends: it looks back over every range the node spans) and frees it, so every
+  // record is free (all zero) between launches; nothing is published for a node that
+  // starts at the next range (no consumer).
   uint64_t* const rec = a.tail + (int64_t)w * RED_TAIL_WORDS;
-  if (wb + len < n_cont && open_start < len) {
-    if (lane == 0) {
+  const bool publish = wb + len < n_cont && open_start < len;
+#if KCC_RED_LB_MODE == 2
+  static_assert(2 * NA <= RED_TAIL_WORDS, "two tagged words per value");
+  if (publish && lane < 2 * NA) {  // lane j: half (j & 1) of value j >> 1
+    uint64_t v = carry[0];
 #pragma unroll
-      for (int k = 0; k < NA; ++k)
-        __hip_atomic_store(rec + k, carry[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#if KCC_RED_LB_ACQREL
-      __hip_atomic_store(rec + RED_TAIL_TAG, RED_TAG_READY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-#else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(rec + RED_TAIL_TAG, RED_TAG_READY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-    }
+    for (int k = 1; k < NA; ++k) v = (lane >> 1) == k ? carry[k] : v;
+    const uint64_t word = RED_WORD_TAG | ((lane & 1) ? v >> 32 : v & 0xffffffffull);
+    __hip_atomic_store(rec + lane, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+#else
+  if (publish && lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NA; ++k)
+      __hip_atomic_store(rec + k, carry[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if KCC_RED_LB_MODE == 1
+    __hip_atomic_store(rec + RED_TAIL_TAG, RED_TAG_READY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(rec + RED_TAIL_TAG, RED_TAG_READY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+  }
+#endif
   // look-back: node0 began in an earlier range and ended in this one
   if (first_open && cur > node0) {
     uint64_t acc[NA];
@@ -541,13 +560,21 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
       if (wi < w) {
         uint64_t* r = a.tail + wi * RED_TAIL_WORDS;
         bool seen = true;
-#ifdef KCC_DIAG_RED_GIVEUP  // fault-path test builds only: every wait gives up at once
-        seen = false;
-        atomicAdd(&a.faults[FAULT_RED], 1ull);
-#else
+#if KCC_RED_LB_MODE == 2
+        uint64_t wd[2 * NA];
         uint32_t spins = 0;
-        while (__hip_atomic_load(r + RED_TAIL_TAG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-               RED_TAG_READY) {
+        for (;;) {
+          bool all = true;
+#pragma unroll
+          for (int j = 0; j < 2 * NA; ++j) {
+            wd[j] = __hip_atomic_load(r + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            all = all && (wd[j] >> 32) == (RED_WORD_TAG >> 32);
+          }
+#ifdef KCC_DIAG_RED_GIVEUP  // fault-path test builds only: every wait gives up at once
+          all = false;
+          spins = RED_SPIN_MAX;
+#endif
+          if (all) break;
           if (++spins >= RED_SPIN_MAX) {  // never on a healthy device: count it, go on
             atomicAdd(&a.faults[FAULT_RED], 1ull);
             seen = false;
@@ -555,19 +582,40 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
           }
           __builtin_amdgcn_s_sleep(2);
         }
+#pragma unroll
+        for (int k = 0; k < NA; ++k) v[k] = (wd[2 * k] & 0xffffffffull) | (wd[2 * k + 1] << 32);
+        // consumed: free the record for the next launch (a wait that gave up leaves it:
+        // the context is faulted until kcc_clear_faults re-zeroes the records)
+        if (seen) {
+#pragma unroll
+          for (int j = 0; j < 2 * NA; ++j)
+            __hip_atomic_store(r + j, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#else
+#ifdef KCC_DIAG_RED_GIVEUP
+        seen = false;
+        atomicAdd(&a.faults[FAULT_RED], 1ull);
+#else
+        uint32_t spins = 0;
+        while (__hip_atomic_load(r + RED_TAIL_TAG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+               RED_TAG_READY) {
+          if (++spins >= RED_SPIN_MAX) {
+            atomicAdd(&a.faults[FAULT_RED], 1ull);
+            seen = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
 #endif
-#if KCC_RED_LB_ACQREL
+#if KCC_RED_LB_MODE == 1
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // synchronizes with the release
 #else
-        // relaxed loads of other addresses may be hoisted above the poll by the compiler
-        // (they were); the hardware issues them after the poll's data returned
         asm volatile("" ::: "memory");
 #endif
 #pragma unroll
         for (int k = 0; k < NA; ++k) v[k] = __hip_atomic_load(r + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // consumed: free the record for the next launch (a wait that gave up leaves it:
-        // the context is faulted until kcc_clear_faults re-zeroes the records)
         if (seen) __hip_atomic_store(r + RED_TAIL_TAG, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
       }
 #pragma unroll
       for (int k = 0; k < NA; ++k) acc[k] += wave_sum_u64(v[k]);

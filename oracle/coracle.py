@@ -12,7 +12,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libkcc_oracle.so")
+# KCC_ORACLE_LIB: another build of the same oracle (the sanitizer build, oracle/Makefile asan)
+LIB_PATH = os.environ.get("KCC_ORACLE_LIB") or os.path.join(_HERE, "_build", "libkcc_oracle.so")
 _LIB = None
 
 

@@ -17,12 +17,13 @@ from oracle import coracle, pyoracle
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HOST = os.path.join(ROOT, "host")
-CLI = os.path.join(HOST, "cluster_capacity")
+# KCC_HOST_LIB / KCC_HOST_CLI: the sanitizer builds (host/Makefile asan, tests/test_sanitizers.py)
+CLI = os.environ.get("KCC_HOST_CLI") or os.path.join(HOST, "cluster_capacity")
 
 
 @pytest.fixture(scope="module")
 def hostlib():
-    path = os.path.join(HOST, "libkcc_host.so")
+    path = os.environ.get("KCC_HOST_LIB") or os.path.join(HOST, "libkcc_host.so")
     if not os.path.exists(path):
         subprocess.run(["make", "-C", HOST, "libkcc_host.so"], check=True)
     L = C.CDLL(path)
