@@ -162,6 +162,12 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 #ifndef KCC_RED_XCD_MAP
 #define KCC_RED_XCD_MAP 0
 #endif
+#ifndef KCC_RED_STORE_AFTER
+#define KCC_RED_STORE_AFTER 0  // pending-block stores behind (1) or ahead of (0) the prefetch
+#endif
+#ifndef KCC_RED_PRIO
+#define KCC_RED_PRIO 0  // progress-based s_setprio in the tile loop (A/B knob, below)
+#endif
 // cache policy of the container loads (A/B knob; 2 nt, 16 sc1, 18 nt sc1).  Measured
 // (round 3, one process, outputs identical): C4 reduce default 130.5 us, nt 181.8, sc1
 // 183.5, nt sc1 181.5; the 8-way shard 19.5 / 32.3 / 25.2 / 32.2 us: the 16-B lane loads
@@ -380,12 +386,17 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
   };
 
   auto tile = [&](uint64_t (&x)[NA][RED_IPL], uint64_t (&nx)[NA][RED_IPL], const int32_t tb) {
-#ifndef KCC_DIAG_RED_NOSTORE
+#if !defined(KCC_DIAG_RED_NOSTORE) && !KCC_RED_STORE_AFTER
     issue_pending();
 #endif
 #pragma unroll
     for (int k = 0; k < NA; ++k)
       load_quad(rs[k], lane * 8 * RED_IPL, (tb + KCC_RED_PREFETCH * RED_TILE) * 8, nx[k]);
+#if !defined(KCC_DIAG_RED_NOSTORE) && KCC_RED_STORE_AFTER
+    // behind the prefetch loads: the next tile's wait for them (vmcnt, in order) does not
+    // include these stores' acknowledgements
+    issue_pending();
+#endif
 #ifdef KCC_DIAG_RED_LOADONLY
 #pragma unroll
     for (int k = 0; k < NA; ++k)
@@ -496,11 +507,32 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   };
+#if KCC_RED_PRIO
+  // progress-based wave priority (A/B knob): the CU's arbiter issues the oldest wave
+  // first among equal priorities, so the waves dispatched first ran ahead and the last
+  // ones finished alone (a bandwidth tail); here a wave's priority falls as its range
+  // advances (3 in its first quarter ... 0 in its last), so the waves that are behind win
+  // the arbitration
+  int32_t prio_lvl = 3;
+  __builtin_amdgcn_s_setprio(3);
+#endif
   for (int32_t tb = 0; tb < len; tb += RING * RED_TILE) {
+#if KCC_RED_PRIO
+    const int32_t lvl = 3 - (int32_t)(((int64_t)tb * 4) / len);  // wave-uniform
+    if (lvl != prio_lvl) {
+      prio_lvl = lvl;
+      if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+      else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+#endif
 #pragma unroll
     for (int u = 0; u < RING; ++u)
       if (tb + u * RED_TILE < len) tile(xs[u], xs[(u + KCC_RED_PREFETCH) % RING], tb + u * RED_TILE);
   }
+#if KCC_RED_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
 #if defined(KCC_DIAG_RED_LOADONLY) || defined(KCC_DIAG_RED_NOSTORE)
   if (carry[0] == 0x123456789ull) out[0][0] = carry[NA - 1] ^ res[0];
 #endif
