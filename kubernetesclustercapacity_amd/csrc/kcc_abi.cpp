@@ -105,6 +105,7 @@ struct Dev {
   DevBuf p_bytes, p_off, p_out, p_st;  // kcc_parse_* staging
   DevBuf k_key;                        // kcc_*_keyed staging
   DevBuf kb_counts, kb_tot, kb_sr, kb_sv;  // kcc::KeyedWork (bucketed keyed reduce)
+  DevBuf kb_part, kb_arrive;               // one-sweep gather: part rows, arrivals (zeroed)
   DevBuf kb_esc_n, kb_esc_row, kb_esc_cpu, kb_esc_mem;
   // kcc_pod_requests / kcc_reduce_requests_pods staging (app containers in cpu / mem)
   DevBuf q_ptr, q_iptr, q_icpu, q_imem, q_rst, q_ocpu, q_omem, q_pcpu, q_pmem;
@@ -915,6 +916,7 @@ void kcc_destroy(kcc_ctx* ctx) {
                       &dv.spec_mem,  &dv.partial,   &dv.totals,    &dv.err,
                       &dv.p_bytes,   &dv.p_off,     &dv.p_out,     &dv.p_st,      &dv.k_key,
                       &dv.kb_counts, &dv.kb_tot,    &dv.kb_sr,     &dv.kb_sv,     &dv.q_ptr,
+                      &dv.kb_part,   &dv.kb_arrive,
                       &dv.kb_esc_n,  &dv.kb_esc_row, &dv.kb_esc_cpu, &dv.kb_esc_mem,
                       &dv.q_iptr,    &dv.q_icpu,    &dv.q_imem,    &dv.q_rst,     &dv.q_ocpu,
                       &dv.q_omem,    &dv.q_pcpu,    &dv.q_pmem};
@@ -1505,15 +1507,25 @@ int keyed_work(kcc_ctx* ctx, Dev& dv, int64_t n_keys, int64_t n, int na, kcc::Ke
                const kcc::KeyedWork** out) {
   *out = nullptr;
   if (!kcc::keyed_bucketed(n_keys, n)) return KCC_OK;
-  const size_t nb = (size_t)kcc::keyed_buckets(n_keys), G = (size_t)kcc::keyed_tiles(n);
+  const size_t nb = (size_t)kcc::keyed_buckets(n_keys);
   const size_t m = (size_t)(n > 0 ? n : 1);
-  KCC_HIP(ctx, ensure(dv.kb_counts, 4 * nb * (G > 0 ? G : 1)));
+  KCC_HIP(ctx, ensure(dv.kb_counts, 4 * (size_t)kcc::keyed_counts_words(n_keys, n)));
   KCC_HIP(ctx, ensure(dv.kb_tot, 4 * nb));
-  KCC_HIP(ctx, ensure(dv.kb_sr, 8 * m));
+  KCC_HIP(ctx, ensure(dv.kb_sr, 8 * (size_t)kcc::keyed_sr_slots(n)));
+  KCC_HIP(ctx, ensure(dv.kb_part, 8 * (size_t)kcc::keyed_part_words(n_keys, na > 2 ? 2 : na)));
+  if (dv.kb_arrive.bytes < 4 * nb) {  // every gather leaves them zero
+    KCC_HIP(ctx, ensure(dv.kb_arrive, 4 * nb));
+    KCC_HIP(ctx, hipMemsetAsync(dv.kb_arrive.p, 0, dv.kb_arrive.bytes, dv.stream));
+    KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
+  }
   if (na > 2) KCC_HIP(ctx, ensure(dv.kb_sv, 8 * (size_t)(na - 2) * m));
   if (na >= 2) {
     const size_t ne = (size_t)(n > 0 ? n : 1);
-    KCC_HIP(ctx, ensure(dv.kb_esc_n, 16));
+    if (!dv.kb_esc_n.p) {  // [0] list length, [1] kb_escape's arrivals: zero between calls
+      KCC_HIP(ctx, ensure(dv.kb_esc_n, 16));
+      KCC_HIP(ctx, hipMemsetAsync(dv.kb_esc_n.p, 0, 16, dv.stream));
+      KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
+    }
     KCC_HIP(ctx, ensure(dv.kb_esc_row, 4 * ne));
     KCC_HIP(ctx, ensure(dv.kb_esc_cpu, 8 * ne));
     KCC_HIP(ctx, ensure(dv.kb_esc_mem, 8 * ne));
@@ -1526,6 +1538,8 @@ int keyed_work(kcc_ctx* ctx, Dev& dv, int64_t n_keys, int64_t n, int na, kcc::Ke
   kw.esc_row = na >= 2 ? as<int32_t>(dv.kb_esc_row) : nullptr;
   kw.esc_cpu = na >= 2 ? as<uint64_t>(dv.kb_esc_cpu) : nullptr;
   kw.esc_mem = na >= 2 ? as<uint64_t>(dv.kb_esc_mem) : nullptr;
+  kw.part_acc = as<uint64_t>(dv.kb_part);
+  kw.arrive = as<uint32_t>(dv.kb_arrive);
   *out = &kw;
   return KCC_OK;
 }

@@ -457,7 +457,8 @@ constexpr int KB_ROWS = 1 << KB_SHIFT;
 constexpr int KB_TILE = KCC_KB_TILE;  // containers per scatter workgroup
 constexpr int64_t KB_NB_MAX = 4096;  // buckets (LDS cursors): n_keys <= 16M rows
 struct KeyedWork {
-  uint32_t* counts;   // [keyed_tiles(n) * keyed_buckets(n_keys)]
+  uint32_t* counts;   // [keyed_tiles(n) * keyed_buckets(n_keys)] (one-sweep path: the tiles'
+                      // bucket starts, [keyed_sweep_tiles(n)][nb + 1])
   uint32_t* tot;      // [keyed_buckets(n_keys)]
   uint64_t* sr;       // [n] scattered 8-B records: row within the bucket, low 20 cpu
                       // bits, memory / 64 (kcc_keyed.hip kb_record)
@@ -466,7 +467,30 @@ struct KeyedWork {
   int32_t* esc_row;   // [n]   bits; memory not a multiple of 64 in [0, 2^38): all of it)
   uint64_t* esc_cpu;  // [n]
   uint64_t* esc_mem;  // [n]
+  // one-sweep path (kb_sweep + kb_gather): a bucket's records are gathered by
+  // keyed_sweep_parts(nb) workgroups; parts > 1 sum through part_acc, the last part to
+  // arrive (arrive[b], zero between calls) adds the others' rows and writes the bucket
+  uint64_t* part_acc; // [nb][parts][NACC][KB_ROWS]
+  uint32_t* arrive;   // [nb]
 };
+// One-sweep keyed reduce (NA = 0 counts, 2 requests; KCC_KB_SWEEP): each tile of
+// KB_SW_TILE containers is counting-sorted by bucket in LDS and written contiguously into
+// its own region of sr (whole lines), with the bucket starts in its table row — no global
+// histogram pass, no scan, keys read once.  kb_gather then sums bucket b's segments of
+// every tile into LDS rows.
+#ifndef KCC_KB_SWEEP
+#define KCC_KB_SWEEP 1
+#endif
+constexpr int KB_SW_THREADS = 1024;
+constexpr int KB_SW_PER = 16;                               // containers per thread
+constexpr int64_t KB_SW_TILE = (int64_t)KB_SW_THREADS * KB_SW_PER;  // 16384
+__host__ __device__ inline int64_t keyed_sweep_tiles(int64_t n) { return (n + KB_SW_TILE - 1) / KB_SW_TILE; }
+int keyed_sweep_parts(int64_t nb);
+// sizes of the KeyedWork arrays for a call (either path): u32 words of counts, u64
+// record slots of sr, u64 words of part_acc
+int64_t keyed_counts_words(int64_t n_keys, int64_t n);
+int64_t keyed_sr_slots(int64_t n);
+int64_t keyed_part_words(int64_t n_keys, int na);
 int64_t keyed_tile(int64_t n);   // containers per scatter workgroup (whole CU rounds)
 int64_t keyed_tiles(int64_t n);
 int64_t keyed_buckets(int64_t n_keys);

@@ -34,6 +34,17 @@ typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// inclusive prefix sum of a 32-bit value over the wave's 64 lanes (DPP, all VALU)
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+
 __device__ __forceinline__ void add_u64(uint64_t* p, uint64_t v) {
   __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -473,16 +484,294 @@ __global__ __launch_bounds__(KB_ACC_THREADS) void kb_accum(
 
 // the escape list, added to its rows after the accumulation: the cpu requests' high parts
 // and the memory requests the records could not hold
-__global__ __launch_bounds__(256) void kb_escape(const uint32_t* __restrict__ esc_n,
+// esc_n[0]: the list's length; esc_n[1]: this launch's arrivals — the last workgroup to
+// finish zeroes both, so the next call's sweep starts from an empty list
+__global__ __launch_bounds__(256) void kb_escape(uint32_t* __restrict__ esc_n,
                                                  const int32_t* __restrict__ esc_row,
                                                  const uint64_t* __restrict__ esc_cpu,
                                                  const uint64_t* __restrict__ esc_mem,
                                                  uint64_t* __restrict__ o0, uint64_t* __restrict__ o1) {
-  const uint32_t cnt = *esc_n;
+  const uint32_t cnt = __hip_atomic_load(esc_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < cnt; i += gridDim.x * 256u) {
     const int32_t r = esc_row[i];
     if (esc_cpu[i]) add_u64(o0 + r, esc_cpu[i]);
     if (esc_mem[i]) add_u64(o1 + r, esc_mem[i]);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(esc_n + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+          gridDim.x - 1u) {
+    __hip_atomic_store(esc_n, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(esc_n + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ---- one-sweep path (KCC_KB_SWEEP, NA = 0 / 2) ----------------------------------------
+// kb_sweep: tile g = containers [g * KB_SW_TILE, ...), 16 per thread, every load issued
+// at once (16-B loads of quads).  Each valid container's rank within its bucket comes from
+// an LDS counter (two 16-bit counters per word: a tile holds at most 16384 containers),
+// one exclusive scan of the counts gives the bucket starts, the records are counting-sorted
+// into an LDS stage and leave as ONE contiguous run of nvalid records (16-B stores: whole
+// lines) into the tile's own region sr[g * KB_SW_TILE ...], the starts into the tile's
+// table row (tab[g][b], tab[g][nb] = nvalid).  No global histogram, no scan launch, and
+// the keys are read once.
+constexpr int KB_SW_WAVES = KB_SW_THREADS / 64;
+constexpr int KB_SW_CNT_WORDS = (int)(KB_NB_MAX / 2);  // two 16-bit bucket counts per word
+
+__device__ __forceinline__ uint32_t kb_half(const uint32_t* w, int b) {
+  return (w[b >> 1] >> (16 * (b & 1))) & 0xffffu;
+}
+
+template <int NA>
+__global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
+    int64_t n, int64_t n_keys, const int32_t* __restrict__ key, const uint64_t* __restrict__ a0,
+    const uint64_t* __restrict__ a1, int nb, uint32_t* __restrict__ tab, uint64_t* __restrict__ sr,
+    uint32_t* __restrict__ esc_n, int32_t* __restrict__ esc_row, uint64_t* __restrict__ esc_cpu,
+    uint64_t* __restrict__ esc_mem) {
+  static_assert(NA == 0 || NA == 2, "one-sweep path: counts or requests");
+  constexpr int NS = NA > 0 ? NA : 1;
+  __shared__ uint64_t st[KB_SW_TILE];            // 128 KiB: the tile's records, bucket order
+  __shared__ uint32_t cnt2[KB_SW_CNT_WORDS];     // bucket counts (2 x 16 bit per word)
+  __shared__ uint32_t sta2[KB_SW_CNT_WORDS];     // bucket starts (2 x 16 bit per word)
+  __shared__ uint32_t wtot[KB_SW_WAVES];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t t0 = (int64_t)blockIdx.x * KB_SW_TILE;
+  const int64_t t1 = min(t0 + KB_SW_TILE, n);
+  const int nw = (nb + 1) / 2;
+  for (int w = tid; w < nw; w += KB_SW_THREADS) cnt2[w] = 0;
+  // every load of the tile first: quads of consecutive containers (16-B loads)
+  int32_t k[KB_SW_PER];
+  uint64_t v[NS][KB_SW_PER];
+#pragma unroll
+  for (int q = 0; q < KB_SW_PER / 4; ++q) {
+    const int64_t c = t0 + 4 * ((int64_t)q * KB_SW_THREADS + tid);
+    if (c + 4 <= t1) {
+      const i32x4 kk = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(key + c));
+      k[4 * q] = kk.x;
+      k[4 * q + 1] = kk.y;
+      k[4 * q + 2] = kk.z;
+      k[4 * q + 3] = kk.w;
+      if constexpr (NA == 2) {
+        const uint64_t* in[2] = {a0, a1};
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const u64x2 lo = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(in[a] + c));
+          const u64x2 hi = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(in[a] + c + 2));
+          v[a][4 * q] = lo.x;
+          v[a][4 * q + 1] = lo.y;
+          v[a][4 * q + 2] = hi.x;
+          v[a][4 * q + 3] = hi.y;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = c + j < t1;
+        k[4 * q + j] = ok ? key[c + j] : -1;
+        if constexpr (NA == 2) {
+          v[0][4 * q + j] = ok ? a0[c + j] : 0;
+          v[1][4 * q + j] = ok ? a1[c + j] : 0;
+        }
+      }
+    }
+  }
+  __syncthreads();  // counters zeroed
+  // per container from here on only its record and (bucket << 16 | rank in the bucket)
+  // (0xffffffff: skipped), so the loaded values die early (no spills at 1024 threads)
+  uint64_t rec[KB_SW_PER];
+  uint32_t br[KB_SW_PER];
+#pragma unroll
+  for (int u = 0; u < KB_SW_PER; ++u) {
+    const bool valid = k[u] >= 0 && (int64_t)k[u] < n_keys;
+    const int b = valid ? k[u] >> KB_SHIFT : 0;
+    const uint32_t sh = 16u * (uint32_t)(b & 1);
+    const uint32_t rk = valid ? (atomicAdd(&cnt2[b >> 1], 1u << sh) >> sh) & 0xffffu : 0u;
+    br[u] = valid ? (uint32_t)b << 16 | rk : 0xffffffffu;
+    const uint32_t row = (uint32_t)k[u] & (KB_ROWS - 1);
+    if constexpr (NA == 2) {
+      rec[u] = kb_record(row, v[0][u], v[1][u]);
+      if (valid) {
+        const bool mem_ok = kb_mem_ok(v[1][u]);
+        if (!mem_ok || (v[0][u] >> KB_CPU_BITS) != 0) {  // rare: what the record cannot hold
+          const uint32_t e = atomicAdd(esc_n, 1u);
+          esc_row[e] = k[u];
+          esc_cpu[e] = v[0][u] & ~KB_CPU_LO;
+          esc_mem[e] = mem_ok ? 0ull : v[1][u];
+        }
+      }
+    } else {
+      rec[u] = row;
+    }
+  }
+  __syncthreads();
+  // exclusive scan of the bucket counts: thread t owns count words 2t, 2t + 1 (buckets
+  // 4t .. 4t + 3); a wave's DPP scan, then the 16 wave totals
+  uint32_t c4[4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int w = 2 * tid + j;
+    const uint32_t x = w < nw ? cnt2[w] : 0u;
+    c4[2 * j] = x & 0xffffu;
+    c4[2 * j + 1] = x >> 16;
+  }
+  const uint32_t s4 = c4[0] + c4[1] + c4[2] + c4[3];
+  const uint32_t incl = wave_incl_scan32(s4);
+  if (lane == 63) wtot[wv] = incl;
+  __syncthreads();
+  uint32_t wbase = 0, nvalid = 0;
+#pragma unroll
+  for (int w = 0; w < KB_SW_WAVES; ++w) {
+    const uint32_t t = wtot[w];
+    wbase += w < wv ? t : 0u;
+    nvalid += t;
+  }
+  {
+    uint32_t run = wbase + incl - s4;
+    uint32_t st4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      st4[j] = run;
+      run += c4[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int w = 2 * tid + j;
+      if (w < nw) sta2[w] = st4[2 * j] | st4[2 * j + 1] << 16;  // starts < 2^14 + 1
+    }
+    // the tile's table row: bucket starts, then nvalid
+    uint32_t* row = tab + (int64_t)blockIdx.x * (nb + 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (4 * tid + j < nb) row[4 * tid + j] = st4[j];
+    if (tid == 0) row[nb] = nvalid;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < KB_SW_PER; ++u) {
+    if (br[u] == 0xffffffffu) continue;
+    st[kb_half(sta2, (int)(br[u] >> 16)) + (br[u] & 0xffffu)] = rec[u];
+  }
+  __syncthreads();
+  // the stage leaves as one contiguous run: 16-B stores of record pairs (whole lines)
+  uint64_t* dst = sr + t0;
+  for (uint32_t j = 2u * (uint32_t)tid; j < nvalid; j += 2u * KB_SW_THREADS) {
+    if (j + 1 < nvalid)
+      *reinterpret_cast<u64x2*>(dst + j) = *reinterpret_cast<const u64x2*>(&st[j]);
+    else
+      dst[j] = st[j];
+  }
+}
+
+// kb_gather: bucket b's records — segment [tab[g][b], tab[g][b + 1]) of every tile g —
+// summed into LDS rows (64-bit LDS atomics), its rows written once.  `parts` workgroups
+// share a bucket (tiles dealt round-robin): each sums its tiles; every part but the last to
+// arrive stores its rows into part_acc, the last one adds them and writes the outputs.
+// A wave works on KB_GA_U segments at once (their loads issued together: a segment is a few
+// hundred bytes, so one per wave would be latency-bound).
+constexpr int KB_GA_THREADS = 1024;
+constexpr int KB_GA_WAVES = KB_GA_THREADS / 64;
+constexpr int KB_GA_U = 8;         // segments per wave in flight
+constexpr int KB_GA_CH = 2048;     // tiles per table chunk in LDS
+
+template <int NA>
+__global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
+    int64_t n, int64_t n_keys, int nb, int parts, const uint32_t* __restrict__ tab,
+    const uint64_t* __restrict__ sr, uint64_t* __restrict__ part_acc, uint32_t* __restrict__ arrive,
+    uint64_t* __restrict__ o0, uint64_t* __restrict__ o1) {
+  constexpr int NACC = NA > 0 ? NA : 1;
+  __shared__ unsigned long long acc[NACC][KB_ROWS];
+  __shared__ uint32_t seg_off[KB_GA_CH];  // start within the tile
+  __shared__ uint32_t seg_len[KB_GA_CH];
+  __shared__ uint32_t last_s;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int b = blockIdx.x / parts, part = blockIdx.x % parts;
+  for (int r = tid; r < KB_ROWS; r += KB_GA_THREADS)
+#pragma unroll
+    for (int a = 0; a < NACC; ++a) acc[a][r] = 0ull;
+  const int64_t G = keyed_sweep_tiles(n);
+  // this part's tiles: g = part, part + parts, ...
+  const int64_t my_tiles = G > part ? (G - part + parts - 1) / parts : 0;
+  auto add_rec = [&](uint64_t rec) {
+    const uint32_t r = (uint32_t)rec & (KB_ROWS - 1);
+    if constexpr (NA == 0) {
+      atomicAdd(&acc[0][r], 1ull);
+    } else {
+      atomicAdd(&acc[0][r], (unsigned long long)(((uint32_t)rec) >> KB_SHIFT));
+      atomicAdd(&acc[1][r], (unsigned long long)((rec >> 32) << KB_MEM_SHIFT));
+    }
+  };
+  for (int64_t c0 = 0; c0 < my_tiles; c0 += KB_GA_CH) {
+    const int ch = (int)min((int64_t)KB_GA_CH, my_tiles - c0);
+    __syncthreads();  // the previous chunk's table entries are consumed
+    for (int i = tid; i < ch; i += KB_GA_THREADS) {
+      const int64_t g = (int64_t)part + (c0 + i) * parts;
+      const uint32_t* row = tab + g * (nb + 1) + b;
+      const uint32_t s0 = row[0], s1 = row[1];
+      seg_off[i] = s0;
+      seg_len[i] = s1 - s0;
+    }
+    __syncthreads();
+    for (int i0 = wv * KB_GA_U; i0 < ch; i0 += KB_GA_WAVES * KB_GA_U) {
+      // KB_GA_U segments: the first 64 records of each loaded at once
+      uint64_t r[KB_GA_U];
+      uint32_t len[KB_GA_U];
+      const uint64_t* base[KB_GA_U];
+#pragma unroll
+      for (int u = 0; u < KB_GA_U; ++u) {
+        const int i = i0 + u;
+        const bool ok = i < ch;
+        const int64_t g = (int64_t)part + (c0 + (ok ? i : 0)) * parts;
+        len[u] = ok ? seg_len[i] : 0u;
+        base[u] = sr + g * KB_SW_TILE + (ok ? seg_off[i] : 0u);
+        r[u] = (uint32_t)lane < len[u] ? __builtin_nontemporal_load(base[u] + lane) : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < KB_GA_U; ++u)
+        if ((uint32_t)lane < len[u]) add_rec(r[u]);
+      // the rest of long segments (skewed keys), 64 records a step
+#pragma unroll 1
+      for (int u = 0; u < KB_GA_U; ++u)
+        for (uint32_t o = 64u + (uint32_t)lane; o < len[u]; o += 64u) add_rec(base[u][o]);
+    }
+  }
+  __syncthreads();
+  const int64_t row0 = (int64_t)b * KB_ROWS;
+  uint64_t* out[2] = {o0, o1};
+  if (parts == 1) {
+    for (int r = tid; r < KB_ROWS; r += KB_GA_THREADS) {
+      if (row0 + r >= n_keys) break;
+#pragma unroll
+      for (int a = 0; a < NACC; ++a) out[a][row0 + r] = acc[a][r];
+    }
+    return;
+  }
+  // several parts: publish this part's rows, the last part to arrive sums and writes
+  uint64_t* mine = part_acc + ((int64_t)b * parts + part) * NACC * KB_ROWS;
+  for (int r = tid; r < KB_ROWS; r += KB_GA_THREADS)
+#pragma unroll
+    for (int a = 0; a < NACC; ++a)
+      __hip_atomic_store(mine + a * KB_ROWS + r, (uint64_t)acc[a][r], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (tid == 0) {
+    // release: this part's rows before its arrival; acquire: the others' rows after it
+    last_s = __hip_atomic_fetch_add(arrive + b, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+             (uint32_t)parts - 1u;
+  }
+  __syncthreads();
+  if (!last_s) return;
+  if (tid == 0) __hip_atomic_store(arrive + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int r = tid; r < KB_ROWS; r += KB_GA_THREADS) {
+    if (row0 + r >= n_keys) break;
+#pragma unroll
+    for (int a = 0; a < NACC; ++a) {
+      uint64_t t = acc[a][r];
+      for (int p = 0; p < parts; ++p)
+        if (p != part)
+          t += __hip_atomic_load(part_acc + ((int64_t)b * parts + p) * NACC * KB_ROWS + a * KB_ROWS + r,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      out[a][row0 + r] = t;
+    }
   }
 }
 
@@ -513,6 +802,54 @@ int64_t keyed_tiles(int64_t n) {
 int64_t keyed_buckets(int64_t n_keys) { return (n_keys + KB_ROWS - 1) / KB_ROWS; }
 bool keyed_bucketed(int64_t n_keys, int64_t n) {
   return n_keys > 0 && keyed_buckets(n_keys) <= KB_NB_MAX && n < ((int64_t)1 << 32);
+}
+
+#ifndef KCC_KB_GA_PARTS
+#define KCC_KB_GA_PARTS 0  // gather workgroups per bucket (0: about one per CU over the buckets)
+#endif
+constexpr int KB_GA_PARTS_MAX = 4;
+int keyed_sweep_parts(int64_t nb) {
+  if (KCC_KB_GA_PARTS > 0) return KCC_KB_GA_PARTS < KB_GA_PARTS_MAX ? KCC_KB_GA_PARTS : KB_GA_PARTS_MAX;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  if (nb <= 0) return 1;
+  const int64_t p = (cus + nb - 1) / nb;
+  return (int)(p < 1 ? 1 : p > KB_GA_PARTS_MAX ? KB_GA_PARTS_MAX : p);
+}
+int64_t keyed_counts_words(int64_t n_keys, int64_t n) {
+  const int64_t nb = keyed_buckets(n_keys);
+  const int64_t a = keyed_tiles(n) * nb, b = keyed_sweep_tiles(n) * (nb + 1);
+  return a > b ? a : b;
+}
+int64_t keyed_sr_slots(int64_t n) {
+  const int64_t t = keyed_sweep_tiles(n) * KB_SW_TILE;
+  return t > n ? t : n;
+}
+int64_t keyed_part_words(int64_t n_keys, int na) {
+  return keyed_buckets(n_keys) * KB_GA_PARTS_MAX * (na > 0 ? na : 1) * (int64_t)KB_ROWS;
+}
+
+// the one-sweep path (NA = 0 / 2): kb_sweep, kb_gather, kb_escape
+template <int NA>
+static hipError_t run_sweep(int64_t n_keys, int64_t n, const int32_t* key, const uint64_t* const* in,
+                            uint64_t* const* out, const KeyedWork& kw, hipStream_t s) {
+  const int nb = (int)keyed_buckets(n_keys);
+  const int64_t G = keyed_sweep_tiles(n);
+  const int parts = keyed_sweep_parts(nb);
+  if (G > 0x7fffffff || (int64_t)nb * parts > 0x7fffffff) return hipErrorInvalidValue;
+  if (G > 0)
+    hipLaunchKernelGGL(kb_sweep<NA>, dim3((unsigned)G), dim3(KB_SW_THREADS), 0, s, n, n_keys, key,
+                       in[0], in[1], nb, kw.counts, kw.sr, kw.esc_n, kw.esc_row, kw.esc_cpu, kw.esc_mem);
+  hipLaunchKernelGGL(kb_gather<NA>, dim3((unsigned)(nb * parts)), dim3(KB_GA_THREADS), 0, s, n, n_keys,
+                     nb, parts, kw.counts, kw.sr, kw.part_acc, kw.arrive, out[0], out[1]);
+  if (NA >= 2 && n > 0) {
+    const int64_t g = (n + 255) / 256;
+    hipLaunchKernelGGL(kb_escape, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, s, kw.esc_n,
+                       kw.esc_row, kw.esc_cpu, kw.esc_mem, out[0], out[1]);
+  }
+  return hipGetLastError();
 }
 
 template <int NA>
@@ -552,8 +889,9 @@ hipError_t launch_reduce_keyed(int64_t n_keys, int64_t n, const int32_t* key, co
                              reinterpret_cast<const uint64_t*>(meml)};
     uint64_t* out[4] = {used_cpu, reinterpret_cast<uint64_t*>(used_mem), lim_cpu,
                         reinterpret_cast<uint64_t*>(lim_mem)};
-    return cpul ? run_bucketed<4>(n_keys, n, key, in, out, *kw, s)
-                : run_bucketed<2>(n_keys, n, key, in, out, *kw, s);
+    if (cpul) return run_bucketed<4>(n_keys, n, key, in, out, *kw, s);
+    return KCC_KB_SWEEP ? run_sweep<2>(n_keys, n, key, in, out, *kw, s)
+                        : run_bucketed<2>(n_keys, n, key, in, out, *kw, s);
   }
   if (n_keys > 0) {  // the sums start from zero (CC:257-260)
     hipError_t e = hipMemsetAsync(used_cpu, 0, 8 * (size_t)n_keys, s);
@@ -583,7 +921,8 @@ hipError_t launch_count_keyed(int64_t n_keys, int64_t n, const int32_t* key, int
   if (kw && keyed_bucketed(n_keys, n)) {
     const uint64_t* in[4] = {nullptr, nullptr, nullptr, nullptr};
     uint64_t* out[4] = {reinterpret_cast<uint64_t*>(count), nullptr, nullptr, nullptr};
-    return run_bucketed<0>(n_keys, n, key, in, out, *kw, s);
+    return KCC_KB_SWEEP ? run_sweep<0>(n_keys, n, key, in, out, *kw, s)
+                        : run_bucketed<0>(n_keys, n, key, in, out, *kw, s);
   }
   if (n_keys > 0) {
     hipError_t e = hipMemsetAsync(count, 0, 8 * (size_t)n_keys, s);

@@ -160,3 +160,28 @@ def test_gpu_keyed_c4_equals_csr(eng):
     s = eng.get_pod_cpu_memory_requests_limits(c.node_ptr, c.cpu_req, c.mem_req)
     assert np.array_equal(r.cpu_requests, s.cpu_requests)
     assert np.array_equal(r.memory_requests, s.memory_requests)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nc", [16383, 16384, 16385, 3 * 16384 + 3, 200_001])
+def test_gpu_keyed_sweep_tiles(eng, nc):
+    """The one-sweep path's tiles (16384 containers each): sizes around and across tile
+    boundaries, a skewed key mix (half of the containers on one row: segments far longer
+    than a wave's 64-record step), skipped keys, the largest key space (4096 buckets: the
+    packed 16-bit LDS counters of all of them), and two calls in a row (the escape list and
+    the gather's arrival counters are left empty / zero)."""
+    nk = 4096 * 4096
+    rng = np.random.default_rng(nc)
+    key = rng.integers(-1, nk + 1, nc).astype(np.int32)
+    key[rng.random(nc) < 0.5] = 12345
+    key[:3] = [nk - 1, 0, 4096]
+    cpu = (rng.integers(0, 41, nc) * 50).astype(np.uint64)
+    cpu[rng.random(nc) < 0.01] = np.uint64(1 << 40)   # escapes
+    mem = rng.integers(0, 8192, nc).astype(np.int64) << 20
+    mem[rng.random(nc) < 0.01] = 12345                # escapes
+    o = oracle_keyed(nk, key, cpu, mem)
+    for _ in range(2):
+        r = eng.get_pod_cpu_memory_requests_limits_keyed(nk, key, cpu, mem)
+        assert np.array_equal(r.cpu_requests, o[0]) and np.array_equal(r.memory_requests, o[1])
+    ok = key[(key >= 0) & (key < nk)]
+    assert np.array_equal(eng.count_by_key(nk, key), np.bincount(ok, minlength=nk).astype(np.int64))
