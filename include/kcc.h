@@ -306,6 +306,12 @@ int kcc_set_clamp_in_fit(kcc_ctx* ctx, int mode);
  * specs and 6.5 for class B, against 3 and 4.5 with the clamp correction). */
 int kcc_clamp_in_fit_used(kcc_ctx* ctx, int* used);
 int kcc_fit_stream_rows(kcc_ctx* ctx, int64_t* streamed);
+/* The memory-bound skip of the fit: node groups x class-A spec waves of the
+ * last kcc_capacity*_async / kcc_fit_*_async on device 0 that were summed without the memory
+ * quotient, because every spec of the wave requests at most floor(free memory / allocatable
+ * pods) of every node of the group (so floor(fm / m) >= allocatable pods there).  The same
+ * totals either way; for the VALU accounting.  Synchronises the device. */
+int kcc_fit_mskip_groups(kcc_ctx* ctx, int64_t* groups);
 
 /* Fraction of (node, spec) pairs of the last kcc_fit* call that took the exact
  * 64-bit path instead of the saturating fast path (diagnostic; host-computed from

@@ -97,6 +97,7 @@ struct Dev {
   int clamp_in_fit = -1;   // kcc_set_clamp_in_fit: -1 by size (clamp_in_fit_auto), 0 never, 1 always
   bool last_nc = false;    // the last capacity call applied the clamp in the fit
   DevBuf fast_cl;          // the clamp in the fit: each streamed row's clamp value
+  DevBuf fast_v;           // KCC_FIT_MSKIP: each stream group's smallest floor(fm / P) (u32)
   int stream_chunks = 0;   // node chunks of the last fit prepare (their stream counters)
   int64_t prep_nodes = -1, prep_specs = -1;  // sizes the workspace was last prepared for
   // staging of the host-array entry points
@@ -288,6 +289,7 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.fast_a, sizeof(kcc::FitGroupA) * (size_t)kcc::fit_groups((int64_t)N)));
   KCC_HIP(ctx, ensure(dv.fast_b, sizeof(kcc::FitGroup) * (size_t)kcc::fit_groups((int64_t)N)));
   KCC_HIP(ctx, ensure(dv.fast_cl, sizeof(int32_t) * kcc::FIT_GROUP * (size_t)kcc::fit_groups((int64_t)N)));
+  KCC_HIP(ctx, ensure(dv.fast_v, sizeof(uint32_t) * (size_t)kcc::fit_groups((int64_t)N)));
   KCC_HIP(ctx, ensure(dv.slow, sizeof(kcc::SlowNode) * N));
   KCC_HIP(ctx, ensure(dv.slow_list, sizeof(int64_t) * N));
   KCC_HIP(ctx, ensure(dv.srec, sizeof(kcc::SpecRec) * S));
@@ -436,7 +438,7 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
                                        as<kcc::FitGroup>(dv.fast_b), as<kcc::SlowNode>(dv.slow),
                                        as<int64_t>(dv.slow_list), n_specs, clamp_of(dv),
                                        as<unsigned long long>(dv.counters), 0, 0,
-                                       n_nodes, s, dv.fit_dense, &pa));
+                                       n_nodes, s, dv.fit_dense, &pa, nullptr, as<uint32_t>(dv.fast_v)));
   if (n_nodes == 0) {
     dv.clamp_dirty = false;
     return KCC_OK;
@@ -458,7 +460,7 @@ int fit_run_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_specs, int64_t
                                as<kcc::SlowNode>(dv.slow),
                                as<int64_t>(dv.slow_list), n_specs, spec_prep_of(dv), partial,
                                as<unsigned long long>(dv.counters), as<uint32_t>(dv.fit_q), 0,
-                               n_nodes, s));
+                               n_nodes, s, nullptr, as<uint32_t>(dv.fast_v)));
   return KCC_OK;
 }
 
@@ -638,7 +640,8 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                        as<int64_t>(dv.slow_list) + lo[c], n_specs, clamp_of(dv),
                                        as<unsigned long long>(dv.counters),
                                        c, lo[c], n_nodes, s, dv.fit_dense,
-                                       place_here ? &pa : nullptr, fast_cl));
+                                       place_here ? &pa : nullptr, fast_cl,
+                                       as<uint32_t>(dv.fast_v) + lo[c] / kcc::FIT_GROUP));
     if (n == 0) continue;
     ProfPair pp{};
     if (dv.prof_on) {
@@ -651,7 +654,8 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                  as<kcc::SlowNode>(dv.slow) + lo[c],
                                  as<int64_t>(dv.slow_list) + lo[c], n_specs, spec_prep_of(dv),
                                  partial, as<unsigned long long>(dv.counters),
-                                 as<uint32_t>(dv.fit_q), c, n_nodes, s, fast_cl));
+                                 as<uint32_t>(dv.fit_q), c, n_nodes, s, fast_cl,
+                                 as<uint32_t>(dv.fast_v) + lo[c] / kcc::FIT_GROUP));
     if (dv.prof_on) {
       KCC_HIP(ctx, hipEventRecord(pp.b, s));
       pp.kind = 1;
@@ -908,7 +912,7 @@ void kcc_destroy(kcc_ctx* ctx) {
     DevBuf* bufs[] = {&dv.c_rank, &dv.c_bcnt, &dv.c_cs, &dv.c_ms,
                       &dv.c_mrc, &dv.c_crm, &dv.c_dperm, &dv.c_C, &dv.c_H2, &dv.c_H3,
                       &dv.c_Crow, &dv.c_rec, &dv.c_dir,
-                      &dv.red_tail,  &dv.faults, &dv.rank_arrive, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
+                      &dv.red_tail,  &dv.faults, &dv.rank_arrive, &dv.fast_v, &dv.fast_cl, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
                       &dv.sperm,     &dv.fit_q,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
                       &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,
@@ -1218,6 +1222,19 @@ int kcc_fit_stream_rows(kcc_ctx* ctx, int64_t* streamed) {
   int64_t t = 0;
   for (int k = 0; k < dv.stream_chunks && k < kcc::FIT_MAX_CHUNKS; ++k) t += (int64_t)c[kcc::CNT_STREAM + k];
   *streamed = t;
+  return KCC_OK;
+}
+
+int kcc_fit_mskip_groups(kcc_ctx* ctx, int64_t* groups) {
+  if (!ctx || !groups) return ctx ? fail(ctx, KCC_EINVAL, "NULL output") : KCC_EINVAL;
+  Dev& dv = ctx->devs[0];
+  KCC_HIP(ctx, hipSetDevice(dv.device));
+  KCC_HIP(ctx, hipDeviceSynchronize());
+  unsigned long long c = 0;
+  if (dv.counters.p)
+    KCC_HIP(ctx, hipMemcpy(&c, as<unsigned long long>(dv.counters) + kcc::CNT_FIT_MSKIP, sizeof(c),
+                           hipMemcpyDeviceToHost));
+  *groups = (int64_t)c;
   return KCC_OK;
 }
 

@@ -322,8 +322,20 @@ enum {
                        // every spec (P <= 0), subtracted from every normal spec by the fit
   CNT_SLOW_ROWS = 4,   // + chunk: rows in that node chunk's slow_list
   CNT_STREAM = 4 + FIT_MAX_CHUNKS,  // + chunk: node rows in that chunk's fit stream (x 8)
-  CNT_N = 4 + 2 * FIT_MAX_CHUNKS
+  CNT_FIT_MSKIP = 4 + 2 * FIT_MAX_CHUNKS,  // (node group, class-A wave) pairs the fit summed
+                                           // without the memory quotient (every lane qm >= P)
+  CNT_N = 5 + 2 * FIT_MAX_CHUNKS
 };
+// The memory-bound skip (KCC_FIT_MSKIP): node_prep stores each stream group's smallest
+// V = floor(free memory / P) (saturated to u32) in gvmin[group]; spec_place orders the
+// class-A specs by memory request (y-rank), so a class-A wave's largest request m_max is
+// known; where m_max <= gvmin[group], floor(fm / m) >= P for every lane and node of the
+// group (m <= fm / P  <=>  m P <= fm), so min(findMin(qc, qm), P) = min(qc, P) and the
+// group is summed without the f64 memory quotient (class A: 2 VALU per node x wave instead
+// of 3; the clamp in the fit: 3 instead of 5).
+#ifndef KCC_FIT_MSKIP
+#define KCC_FIT_MSKIP 1
+#endif
 // The clamp correction after every node_prep of the call (n_nodes: the call's rows, for
 // the binned records' pass count): partial[s] -= D_s for the normal specs of clamp-free
 // waves; leaves the table copies zero.
@@ -358,7 +370,8 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             SlowNode* slow, int64_t* slow_list, int64_t n_specs, ClampWork cw,
                             unsigned long long* counters, int chunk, int64_t row0,
                             int64_t call_nodes, hipStream_t s, bool dense = false,
-                            const PlaceArgs* place = nullptr, int32_t* fast_cl = nullptr);
+                            const PlaceArgs* place = nullptr, int32_t* fast_cl = nullptr,
+                            uint32_t* gvmin = nullptr);
 // Clamp in the fit (fast_cl != nullptr; one node chunk, S <= CLAMP_LDS_SPECS, not dense):
 // node_prep streams each row's clamp value (allocatable pods - pod count, CC:135) beside
 // its FitGroupA (fast_cl[row position]) and builds no clamp tables; the fit computes the
@@ -377,7 +390,8 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
                       const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, uint32_t* queue, int chunk,
-                      int64_t grid_nodes, hipStream_t s, const int32_t* fast_cl = nullptr);
+                      int64_t grid_nodes, hipStream_t s, const int32_t* fast_cl = nullptr,
+                      const uint32_t* gvmin = nullptr);
 // the fit's work queues: fit_queue_words(S) uint32 (a 64-B line per spec column of 256 and
 // sub-queue), zero before the first launch (each launch leaves them zero)
 constexpr int64_t FIT_QSUBS_MAX = 32;
@@ -482,8 +496,11 @@ struct KeyedWork {
 #define KCC_KB_SWEEP 1
 #endif
 constexpr int KB_SW_THREADS = 1024;
-constexpr int KB_SW_PER = 16;                               // containers per thread
-constexpr int64_t KB_SW_TILE = (int64_t)KB_SW_THREADS * KB_SW_PER;  // 16384
+#ifndef KCC_KB_SW_PER
+#define KCC_KB_SW_PER 16  // containers per thread: 16 (128 KiB stage, one workgroup per CU) or 8
+#endif
+constexpr int KB_SW_PER = KCC_KB_SW_PER;
+constexpr int64_t KB_SW_TILE = (int64_t)KB_SW_THREADS * KB_SW_PER;  // 16384 (8192)
 __host__ __device__ inline int64_t keyed_sweep_tiles(int64_t n) { return (n + KB_SW_TILE - 1) / KB_SW_TILE; }
 int keyed_sweep_parts(int64_t nb);
 // sizes of the KeyedWork arrays for a call (either path): u32 words of counts, u64

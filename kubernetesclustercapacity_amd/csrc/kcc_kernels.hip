@@ -813,7 +813,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
                                  int64_t S, ClampWork cw,
                                  unsigned long long* __restrict__ counters,
                                  int32_t chunk, int32_t dense, int64_t pass0, PlaceArgs pa,
-                                 int32_t* __restrict__ fast_cl) {
+                                 int32_t* __restrict__ fast_cl, uint32_t* __restrict__ gvmin) {
   static_assert(!NC || MODE == 2, "the clamp in the fit: S <= CLAMP_LDS_SPECS only");
   if ((int32_t)blockIdx.x < pa.n_blocks) {  // spec_place's workgroups, in front (MODE 2)
     spec_place_body(pa, blockIdx.x);
@@ -847,6 +847,9 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   __shared__ uint32_t np_tot;
   __shared__ uint32_t np_bcnt[NP_BINS];                 // binned records per bin (this pass)
   __shared__ uint32_t np_bstart[NP_BINS];               // their exclusive prefix
+  // KCC_FIT_MSKIP: this pass's stream rows' V = floor(fm / P) (u32, saturated), by stream
+  // position within the pass, for the groups' minima (gvmin)
+  __shared__ uint32_t np_v[KCC_FIT_MSKIP ? (int)PR : 1];
   // the class counts from spec_rank's per-block counts (spec_place may run beside this
   // launch): every wave sums them (one load per lane at S <= 4096)
   uint64_t cls_n = 0;  // class A | class B << 32
@@ -971,6 +974,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
     uint32_t r_fc[SUB];
     int32_t r_P[SUB];
     int32_t r_cl[SUB];  // NC: the clamp value of a streamed row
+    uint32_t r_v[SUB];  // KCC_FIT_MSKIP: min(floor(fm / P), 2^32 - 1) of a streamed row
     unsigned long long sbal[SUB];
     uint32_t pk1[SUB], pk2[SUB], pk3[SUB];
     uint64_t always_sum = 0;
@@ -1047,12 +1051,13 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       const int64_t wfull = Penc - (int64_t)cl_q;  // contribution = min(x, Penc) - w when clamped
       if (ok && nN > 0 && P <= 0) always_sum += (uint64_t)wfull;  // x >= P for every spec
       r_cl[q] = cl_q;
+      const double rP = recip_up_f64(P > 0 ? (uint64_t)P : 1ull);
+      const int64_t V0 = (int64_t)((double)r_fm[q] * rP);  // floor(fm / P): exact (§5)
+      r_v[q] = P > 0 ? (V0 < 0xffffffffll ? (uint32_t)V0 : 0xffffffffu) : 0u;
       if constexpr (NC) {
         pk1[q] = pk2[q] = pk3[q] = 0u;
       } else {
-      const double rP = recip_up_f64(P > 0 ? (uint64_t)P : 1ull);
       const uint32_t U0 = (uint32_t)((double)r_fc[q] * rP);
-      const int64_t V0 = (int64_t)((double)r_fm[q] * rP);
       const bool act = ok && nN > 0 && P > 0 && wfull != 0 && U0 >= cmin && V0 >= mmin;
       const int64_t w = act ? wfull : 0;  // |w| <= 2^21
       const uint32_t U = act ? U0 : 0u;   // every request is >= 1: counts 0
@@ -1179,8 +1184,9 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       const uint64_t sb0 = np_base + before;
       const uint32_t tot = np_tot;
       const uint32_t pad = (tot + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP - tot;
-      auto put = [&](uint64_t pos, uint64_t fmv, uint32_t fcv, uint32_t Pv, int32_t clv) {
+      auto put = [&](uint64_t pos, uint64_t fmv, uint32_t fcv, uint32_t Pv, int32_t clv, uint32_t vv) {
         const int kk = (int)(pos % FIT_GROUP);
+        if (KCC_FIT_MSKIP) np_v[pos - np_base] = vv;
         if (NC) fast_cl[pos] = clv;
         FitGroupA& a = fast_a[pos / FIT_GROUP];
         a.fm[kk] = fmv;
@@ -1199,7 +1205,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       for (int q = 0; q < SUB; ++q) {
         if (!(KCC_DIAG_NP & 8) && ((sbal[q] >> lane) & 1ull))  // P <= 0 streams only in the dense layout, as P = 0
           put(sb0 + done + (uint32_t)__popcll(sbal[q] & ((1ull << lane) - 1ull)), r_fm[q], r_fc[q],
-              r_P[q] > 0 ? (uint32_t)r_P[q] : 0u, r_cl[q]);
+              r_P[q] > 0 ? (uint32_t)r_P[q] : 0u, r_cl[q], r_v[q]);
         done += (uint32_t)__popcll(sbal[q]);
         const uint32_t c2 = pk1[q] & 0x1fffu, c3 = (pk1[q] >> 13) & 0x1fffu;
         if (c2 | c3) {
@@ -1209,9 +1215,18 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
           if (c3) prec[np_bstart[(pk3[q] >> 9) & 0x1ffu] + ((pk2[q] >> 13) & 0x1fffu)] = wbits | c3;
         }
       }
-      if (threadIdx.x < pad) put(np_base + tot + threadIdx.x, 0ull, 0u, 0u, 0);  // the last group's padding
+      if (threadIdx.x < pad) put(np_base + tot + threadIdx.x, 0ull, 0u, 0u, 0, 0u);  // the last group's padding
     }
     __syncthreads();  // np_wc / np_base / np_bstart are rewritten by the next pass
+    if (KCC_FIT_MSKIP) {  // each stream group's smallest V (padding rows: 0, no skip)
+      const uint32_t ng = (np_tot + FIT_GROUP - 1) / FIT_GROUP;
+      if (threadIdx.x < ng) {
+        uint32_t vm = 0xffffffffu;
+#pragma unroll
+        for (int e = 0; e < FIT_GROUP; ++e) vm = min(vm, np_v[threadIdx.x * FIT_GROUP + e]);
+        gvmin[np_base / FIT_GROUP + threadIdx.x] = vm;
+      }
+    }
     KCC_TL(bid % 1024, 5);
   }
   if (cpriv && !NC) {  // the private C into this workgroup's device copy: its non-zero cells
@@ -1613,7 +1628,11 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
     counters[CNT_SPECS_B] = nB;
   }
   if (!in) return;
-  const int64_t pos = cls == SPEC_A ? (int64_t)pA + rA
+  // class A by memory request (KCC_FIT_MSKIP: a wave's largest request is its last lane's):
+  // the class-B specs (m < 2^18 <= every class-A m) hold y-ranks [0, nB), so y - nB is a
+  // permutation of [0, nA)
+  const int64_t posA = KCC_FIT_MSKIP ? (int64_t)cw.rank[S + i] - (int64_t)nB : (int64_t)pA + rA;
+  const int64_t pos = cls == SPEC_A ? posA
                     : cls == SPEC_B ? (int64_t)nA + pB + rB
                                     : nN + (qb * 64 - pA - pB) + (lane - rA - rB);
   SpecRec rec;
@@ -2115,7 +2134,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     const FitGroup* __restrict__ fast_b, const SlowNode* __restrict__ slow,
     const int64_t* __restrict__ slow_list, int64_t S, const SpecRec* __restrict__ specs,
     int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t chunk,
-    int32_t gx, int32_t gy, const int32_t* __restrict__ fast_cl) {
+    int32_t gx, int32_t gy, const int32_t* __restrict__ fast_cl, const uint32_t* __restrict__ gvmin) {
   // XCD-aware order (speed only, never correctness): workgroups are dealt round-robin
   // over the 8 XCDs, so give every spec group of one node chunk the same b % 8
   const int32_t b = blockIdx.x, xcd = b & 7, r = b >> 3;
@@ -2144,6 +2163,20 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   const bool wave_exact = __any(sr.cls == SPEC_EXACT);
   const bool wave_b = __any(sr.cls == SPEC_B);
   const bool wave_fast = !wave_exact && !idle;  // sums the node stream
+  // KCC_FIT_MSKIP: the wave's largest memory request (class-A specs sit in memory order, so
+  // this is the last active lane's) as u32; 0xffffffff: no skip (m >= 2^32, or no table)
+  uint32_t mmax32 = 0xffffffffu;
+  if (KCC_FIT_MSKIP && gvmin) {
+    uint64_t mm = active ? (uint64_t)m : 0ull;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      const uint64_t o = __shfl_xor(mm, d);
+      mm = o > mm ? o : mm;
+    }
+    mmax32 = mm < 0xffffffffull ? (uint32_t)mm : 0xffffffffu;
+    mmax32 = __builtin_amdgcn_readfirstlane(mmax32);
+  }
+  uint32_t nskip = 0;  // node groups summed without the memory quotient (scalar)
 
   // the node stream node_prep wrote (its length is on the device; 32-bit: < 2^31 groups)
   const uint32_t n_groups = (uint32_t)(counters[CNT_STREAM + chunk] / FIT_GROUP);
@@ -2237,6 +2270,24 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
       const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
       const i32x8 fcv = *reinterpret_cast<const i32x8*>(g->fc);
       const i32x8 Pv = *reinterpret_cast<const i32x8*>(g->P);
+      if (KCC_FIT_MSKIP && gvmin) {
+        const uint32_t vmin = gvmin[g0 + io];
+        // every load of the group is issued before the branch (one scalar-load round trip)
+        asm volatile("" : : "s"(fmv), "s"(fcv), "s"(Pv), "s"(vmin));
+        if (mmax32 <= vmin) {  // wave-uniform: every qm >= P
+          ++nskip;
+#pragma unroll
+          for (int u = 0; u < FIT_GROUP / 2; ++u) {
+            const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
+            const f32x2 q = fcp * rcf2;
+            const uint32_t m0 = min(__float_as_uint(q.x), (uint32_t)Pv[2 * u]);      // min(qc, P)
+            const uint32_t m1 = min(__float_as_uint(q.y), (uint32_t)Pv[2 * u + 1]);
+            acc32 += (int32_t)(m0 + m1);
+          }
+          asm volatile("; fit: memory-bound skip" : "+v"(acc32));  // (no tail merging)
+          continue;
+        }
+      }
 #pragma unroll
       for (int u = 0; u < FIT_GROUP / 2; ++u) {
         const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
@@ -2251,6 +2302,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
         }
         acc32 += (int32_t)(m3[0] + m3[1]);
       }
+      if (KCC_FIT_MSKIP) asm volatile("; fit: full" : "+v"(acc32));
     }
     set_round_nearest();
     acc += (uint64_t)(int64_t)acc32;
@@ -2292,6 +2344,28 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
 #else
       const i32x8 clv = *reinterpret_cast<const i32x8*>(cbase + (size_t)io * FIT_GROUP);
 #endif
+      if (KCC_FIT_MSKIP && gvmin) {
+        const uint32_t vmin = gvmin[g0 + io];
+        asm volatile("" : : "s"(fmv), "s"(fcv), "s"(Pv), "s"(vmin));  // loads before the branch
+        if (mmax32 <= vmin) {  // every qm >= P: x >= P <=> qc >= P, and x = qc below P
+          ++nskip;
+#pragma unroll
+          for (int u = 0; u < FIT_GROUP / 2; ++u) {
+            const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
+            const f32x2 q = fcp * rcf2;
+            int32_t m3[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int k = 2 * u + h;
+              const uint32_t qc = __float_as_uint(h ? q.y : q.x);
+              m3[h] = qc >= (uint32_t)Pv[k] ? clv[k] : (int32_t)qc;  // CC:134-135 (x = qc here)
+            }
+            acc32 += m3[0] + m3[1];
+          }
+          asm volatile("; fit: memory-bound skip" : "+v"(acc32));  // (no tail merging)
+          continue;
+        }
+      }
 #pragma unroll
       for (int u = 0; u < FIT_GROUP / 2; ++u) {
         const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
@@ -2307,6 +2381,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
         }
         acc32 += m3[0] + m3[1];
       }
+      if (KCC_FIT_MSKIP) asm volatile("; fit: full" : "+v"(acc32));
     }
     set_round_nearest();
     acc += (uint64_t)(int64_t)acc32;
@@ -2432,6 +2507,8 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     const unsigned long long act = __ballot(active);
     if (slow_iters && lane == 0)
       atomicAdd(&counters[CNT_SLOW_PAIRS], (unsigned long long)slow_iters * (unsigned long long)__popcll(act));
+    if (KCC_FIT_MSKIP && nskip && lane == 0)  // (VALU accounting: bench.py)
+      atomicAdd(&counters[CNT_FIT_MSKIP], (unsigned long long)nskip);
   }
   // the clamp in the fit: the rows clamped for every spec (P <= 0, never streamed), once
   // per spec (the column's workgroup by == 0) for the normal specs (exact waves walked
@@ -2660,7 +2737,8 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             SlowNode* slow, int64_t* slow_list, int64_t n_specs,
                             ClampWork cw, unsigned long long* counters, int chunk, int64_t row0,
                             int64_t call_nodes, hipStream_t s, bool dense,
-                            const PlaceArgs* place, int32_t* fast_cl) {
+                            const PlaceArgs* place, int32_t* fast_cl, uint32_t* gvmin) {
+  if (KCC_FIT_MSKIP && !gvmin && n_nodes > 0) return hipErrorInvalidValue;
   if (n_nodes <= 0 && !place) return hipSuccess;
   if (fast_cl && (n_specs > CLAMP_LDS_SPECS || dense)) return hipErrorInvalidValue;
   const int64_t pr = clamp_pass_rows(call_nodes);
@@ -2686,7 +2764,7 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
   hipLaunchKernelGGL(kern, dim3(np_blocks + (unsigned)pa.n_blocks), dim3(KCC_NODE_PREP_BLOCK),
                      lds_bytes, s, n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu,
                      used_mem, fast_a, fast_b, slow, slow_list, n_specs, cw,
-                     counters, (int32_t)chunk, (int32_t)(dense ? 1 : 0), row0 / pr, pa, fast_cl);
+                     counters, (int32_t)chunk, (int32_t)(dense ? 1 : 0), row0 / pr, pa, fast_cl, gvmin);
   return hipGetLastError();
 }
 
@@ -2755,7 +2833,8 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
                       const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, uint32_t* queue, int chunk,
-                      int64_t grid_nodes, hipStream_t s, const int32_t* fast_cl) {
+                      int64_t grid_nodes, hipStream_t s, const int32_t* fast_cl,
+                      const uint32_t* gvmin) {
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
   const int64_t gx = (n_specs + FIT_SPW - 1) / FIT_SPW;
   const int64_t n_groups = fit_groups(n_nodes);
@@ -2774,7 +2853,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
   auto kern = fast_cl ? fit_kernel<true> : fit_kernel<false>;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, queue, fast_a,
                      fast_b, slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)chunk,
-                     (int32_t)gx, (int32_t)gy, fast_cl);
+                     (int32_t)gx, (int32_t)gy, fast_cl, KCC_FIT_MSKIP ? gvmin : nullptr);
   return hipGetLastError();
 }
 

@@ -484,6 +484,7 @@ __global__ __launch_bounds__(KB_ACC_THREADS) void kb_accum(
 
 // the escape list, added to its rows after the accumulation: the cpu requests' high parts
 // and the memory requests the records could not hold
+constexpr unsigned KB_ESC_WG = 64;  // kb_escape workgroups (one arrival atomic each)
 // esc_n[0]: the list's length; esc_n[1]: this launch's arrivals — the last workgroup to
 // finish zeroes both, so the next call's sweep starts from an empty list
 __global__ __launch_bounds__(256) void kb_escape(uint32_t* __restrict__ esc_n,
@@ -530,9 +531,9 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
     uint64_t* __restrict__ esc_mem) {
   static_assert(NA == 0 || NA == 2, "one-sweep path: counts or requests");
   constexpr int NS = NA > 0 ? NA : 1;
-  __shared__ uint64_t st[KB_SW_TILE];            // 128 KiB: the tile's records, bucket order
-  __shared__ uint32_t cnt2[KB_SW_CNT_WORDS];     // bucket counts (2 x 16 bit per word)
-  __shared__ uint32_t sta2[KB_SW_CNT_WORDS];     // bucket starts (2 x 16 bit per word)
+  __shared__ uint64_t st[KB_SW_TILE];            // the tile's records, bucket order
+  // bucket counts (2 x 16 bit per word), turned into the bucket starts in place by the scan
+  __shared__ uint32_t cnt2[KB_SW_CNT_WORDS];
   __shared__ uint32_t wtot[KB_SW_WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t t0 = (int64_t)blockIdx.x * KB_SW_TILE;
@@ -617,7 +618,7 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
   const uint32_t s4 = c4[0] + c4[1] + c4[2] + c4[3];
   const uint32_t incl = wave_incl_scan32(s4);
   if (lane == 63) wtot[wv] = incl;
-  __syncthreads();
+  __syncthreads();  // (also: every thread has read its count words)
   uint32_t wbase = 0, nvalid = 0;
 #pragma unroll
   for (int w = 0; w < KB_SW_WAVES; ++w) {
@@ -636,7 +637,7 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int w = 2 * tid + j;
-      if (w < nw) sta2[w] = st4[2 * j] | st4[2 * j + 1] << 16;  // starts < 2^14 + 1
+      if (w < nw) cnt2[w] = st4[2 * j] | st4[2 * j + 1] << 16;  // starts <= 2^14
     }
     // the tile's table row: bucket starts, then nvalid
     uint32_t* row = tab + (int64_t)blockIdx.x * (nb + 1);
@@ -649,7 +650,7 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
 #pragma unroll
   for (int u = 0; u < KB_SW_PER; ++u) {
     if (br[u] == 0xffffffffu) continue;
-    st[kb_half(sta2, (int)(br[u] >> 16)) + (br[u] & 0xffffu)] = rec[u];
+    st[kb_half(cnt2, (int)(br[u] >> 16)) + (br[u] & 0xffffu)] = rec[u];
   }
   __syncthreads();
   // the stage leaves as one contiguous run: 16-B stores of record pairs (whole lines)
@@ -670,7 +671,10 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
 // hundred bytes, so one per wave would be latency-bound).
 constexpr int KB_GA_THREADS = 1024;
 constexpr int KB_GA_WAVES = KB_GA_THREADS / 64;
-constexpr int KB_GA_U = 8;         // segments per wave in flight
+#ifndef KCC_KB_GA_U
+#define KCC_KB_GA_U 8
+#endif
+constexpr int KB_GA_U = KCC_KB_GA_U;  // segments per wave in flight (128 records of each)
 constexpr int KB_GA_CH = 2048;     // tiles per table chunk in LDS
 
 template <int NA>
@@ -712,26 +716,31 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
     }
     __syncthreads();
     for (int i0 = wv * KB_GA_U; i0 < ch; i0 += KB_GA_WAVES * KB_GA_U) {
-      // KB_GA_U segments: the first 64 records of each loaded at once
-      uint64_t r[KB_GA_U];
-      uint32_t len[KB_GA_U];
-      const uint64_t* base[KB_GA_U];
+      // KB_GA_U segments: the first 128 records of each loaded at once (two per lane)
+      uint64_t r[KB_GA_U][2];
+      uint32_t len[KB_GA_U], first[KB_GA_U];  // (record indices < 2^32: keyed_bucketed)
 #pragma unroll
       for (int u = 0; u < KB_GA_U; ++u) {
         const int i = i0 + u;
         const bool ok = i < ch;
-        const int64_t g = (int64_t)part + (c0 + (ok ? i : 0)) * parts;
+        const uint32_t g = (uint32_t)part + (uint32_t)(c0 + (ok ? i : 0)) * (uint32_t)parts;
         len[u] = ok ? seg_len[i] : 0u;
-        base[u] = sr + g * KB_SW_TILE + (ok ? seg_off[i] : 0u);
-        r[u] = (uint32_t)lane < len[u] ? __builtin_nontemporal_load(base[u] + lane) : 0ull;
+        first[u] = g * (uint32_t)KB_SW_TILE + (ok ? seg_off[i] : 0u);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t o = (uint32_t)lane + 64u * h;
+          r[u][h] = o < len[u] ? __builtin_nontemporal_load(sr + first[u] + o) : 0ull;
+        }
       }
 #pragma unroll
       for (int u = 0; u < KB_GA_U; ++u)
-        if ((uint32_t)lane < len[u]) add_rec(r[u]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if ((uint32_t)lane + 64u * h < len[u]) add_rec(r[u][h]);
       // the rest of long segments (skewed keys), 64 records a step
 #pragma unroll 1
       for (int u = 0; u < KB_GA_U; ++u)
-        for (uint32_t o = 64u + (uint32_t)lane; o < len[u]; o += 64u) add_rec(base[u][o]);
+        for (uint32_t o = 128u + (uint32_t)lane; o < len[u]; o += 64u) add_rec(sr[first[u] + o]);
     }
   }
   __syncthreads();
@@ -800,8 +809,8 @@ int64_t keyed_tiles(int64_t n) {
   return (n + t - 1) / t;
 }
 int64_t keyed_buckets(int64_t n_keys) { return (n_keys + KB_ROWS - 1) / KB_ROWS; }
-bool keyed_bucketed(int64_t n_keys, int64_t n) {
-  return n_keys > 0 && keyed_buckets(n_keys) <= KB_NB_MAX && n < ((int64_t)1 << 32);
+bool keyed_bucketed(int64_t n_keys, int64_t n) {  // (record indices, padded tiles, < 2^32)
+  return n_keys > 0 && keyed_buckets(n_keys) <= KB_NB_MAX && n < ((int64_t)1 << 32) - KB_SW_TILE;
 }
 
 #ifndef KCC_KB_GA_PARTS
@@ -844,11 +853,9 @@ static hipError_t run_sweep(int64_t n_keys, int64_t n, const int32_t* key, const
                        in[0], in[1], nb, kw.counts, kw.sr, kw.esc_n, kw.esc_row, kw.esc_cpu, kw.esc_mem);
   hipLaunchKernelGGL(kb_gather<NA>, dim3((unsigned)(nb * parts)), dim3(KB_GA_THREADS), 0, s, n, n_keys,
                      nb, parts, kw.counts, kw.sr, kw.part_acc, kw.arrive, out[0], out[1]);
-  if (NA >= 2 && n > 0) {
-    const int64_t g = (n + 255) / 256;
-    hipLaunchKernelGGL(kb_escape, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, s, kw.esc_n,
-                       kw.esc_row, kw.esc_cpu, kw.esc_mem, out[0], out[1]);
-  }
+  if (NA >= 2 && n > 0)  // (few workgroups: each adds to one arrival counter; the list is short)
+    hipLaunchKernelGGL(kb_escape, dim3(KB_ESC_WG), dim3(256), 0, s, kw.esc_n, kw.esc_row, kw.esc_cpu,
+                       kw.esc_mem, out[0], out[1]);
   return hipGetLastError();
 }
 
@@ -872,11 +879,9 @@ static hipError_t run_bucketed(int64_t n_keys, int64_t n, const int32_t* key, co
   }
   hipLaunchKernelGGL(kb_accum<NA>, dim3((unsigned)nb), dim3(KB_ACC_THREADS), 0, s, n, n_keys, nb,
                      kw.tot, kw.sr, kw.sv, out[0], out[1], out[2], out[3]);
-  if (NA >= 2 && n > 0) {
-    const int64_t g = (n + 255) / 256;
-    hipLaunchKernelGGL(kb_escape, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, s, kw.esc_n,
-                       kw.esc_row, kw.esc_cpu, kw.esc_mem, out[0], out[1]);
-  }
+  if (NA >= 2 && n > 0)
+    hipLaunchKernelGGL(kb_escape, dim3(KB_ESC_WG), dim3(256), 0, s, kw.esc_n, kw.esc_row, kw.esc_cpu,
+                       kw.esc_mem, out[0], out[1]);
   return hipGetLastError();
 }
 

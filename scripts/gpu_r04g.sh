@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_keyed.py -m gpu -x -v --timeout 200 --timeout-method thread \
   > gpurun_out/pytest_keyed_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_keyed_$TAG.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u scripts/ab_variants.py run --keyed --config C4 --rounds 5 --reps 10 kbold kbp1 kbp2 kbp4 \
+timeout -k 10 300 python -u scripts/ab_variants.py run --keyed --config C4 --rounds 5 --reps 10 kbold s16u8 s16u8p1 s16u16p1 s8u8p1 s8u16p1 \
   > gpurun_out/ab_keyed_$TAG.txt 2>&1 || exit $?
 grep '^{' gpurun_out/ab_keyed_$TAG.txt
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_keyed_$TAG -o run \

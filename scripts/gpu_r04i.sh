@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 4: the whole -m gpu suite, the memory-bound skip A/B (fit), the keyed path A/B, the
+# default bench line.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-r04i}
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+  > gpurun_out/pytest_$TAG.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
+bash scripts/gpu_ab.sh $TAG base msk0 || exit $?
+timeout -k 10 300 python -u scripts/ab_variants.py run --keyed --config C4 --rounds 5 --reps 10 kbold s16u8 s16u8p1 s16u16p1 s8u8p1 s8u16p1 \
+  > gpurun_out/ab_keyed_$TAG.txt 2>&1 || exit $?
+grep '^{' gpurun_out/ab_keyed_$TAG.txt
+timeout -k 10 240 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?
+python3 -c "
+import json;d=json.load(open('gpurun_out/bench_$TAG.json'))
+v=d['roofline_valu']
+print('step', d['ms_per_step'], 'reduce', d['roofline_reduce']['ms_per_launch'], d['roofline_reduce']['frac'], 'fit', d['roofline_fit']['ms_per_launch'], 'valu', v['frac'], 'mskip', v['mskip_fraction'], 'keyed', d['keyed']['ms_per_launch'], d['keyed']['roofline']['frac'], 'chk', d['totals_checksum'])"

@@ -74,18 +74,51 @@ def check_loads(lines, dwords):
     assert not [ln for ln in lines if ln.startswith(("global_", "flat_", "buffer_", "ds_"))]
 
 
+def block_before(body, marker):
+    """The instructions of the basic block that ends at `marker` (an asm comment the kernel
+    puts at the end of a loop body: the memory-bound skip and the full path, KCC_FIT_MSKIP)."""
+    j = body.index(marker)
+    st = max(body.rfind(".LBB", 0, j), body.rfind("; %bb.", 0, j))
+    return [ln.strip() for ln in body[st:j].splitlines()[1:]
+            if ln.strip() and not ln.strip().startswith(";")]
+
+
+def loop_header_loads(body, marker):
+    """Scalar loads of the inner loop's header: from the loop header label (the last label
+    marked 'Inner Loop Header' before the skip body) to the skip body."""
+    j = body.index(marker)
+    h = body.rfind("Inner Loop Header", 0, j)
+    seg = body[body.rfind(".LBB", 0, h):j]
+    return [ln.strip().split()[0] for ln in seg.splitlines() if ln.strip().startswith("s_load")]
+
+
+SKIP, FULL = "; fit: memory-bound skip", "; fit: full"
+
+
 def test_fit_class_a_loop(asm):
+    """Class A, per 8-node group: the full path (bench.FIT_VALU_PER_NODE_WAVE = 3 VALU per
+    node: packed f32 and f64 multiplies, min3, add) and the memory-bound skip (2: no f64
+    multiply, min with P) — no division, conversion, correction, compare or select; every
+    group's scalar loads (fm, fc, P, its smallest V) issued before the branch, no vector
+    memory in either body."""
     import bench
-    (lines,) = loops_with(kernel_body(asm, FIT), "v_pk_mul_f32")
-    check_loads(lines, GROUP * 4)  # fm (2 dwords), fc, P per node
-    valu = [ln for ln in lines if ln.startswith("v_")]
+    body = kernel_body(asm, FIT)
+    full, skip = block_before(body, FULL), block_before(body, SKIP)
+    for lines in (full, skip):
+        assert not [ln for ln in lines if ln.startswith(("global_", "flat_", "buffer_", "ds_"))]
+    loads = loop_header_loads(body, SKIP)
+    assert loads.count("s_load_dwordx16") == 2 and loads.count("s_load_dword") == 1, loads
+    valu = [ln.split()[0] for ln in full if ln.startswith("v_")]
     assert len(valu) / GROUP == pytest.approx(bench.FIT_VALU_PER_NODE_WAVE, abs=1e-9), \
         f"{len(valu)} VALU / {GROUP} nodes: update bench.FIT_VALU_PER_NODE_WAVE"
-    ops = [ln.split()[0] for ln in valu]
-    assert ops.count("v_pk_mul_f32") == GROUP // 2 and ops.count("v_mul_f64") == GROUP
-    assert ops.count("v_min3_u32") == GROUP and ops.count("v_add3_u32") == GROUP // 2
-    assert not any(o.startswith(("v_mad", "v_cvt", "v_fma", "v_rcp", "v_div", "v_cmp",
-                                 "v_cndmask")) for o in ops)
+    assert valu.count("v_pk_mul_f32") == GROUP // 2 and valu.count("v_mul_f64") == GROUP
+    assert valu.count("v_min3_u32") == GROUP and valu.count("v_add3_u32") == GROUP // 2
+    sv = [ln.split()[0] for ln in skip if ln.startswith("v_")]
+    assert len(sv) / GROUP == pytest.approx(bench.FIT_SKIP_VALU_PER_NODE_WAVE, abs=1e-9)
+    assert sv.count("v_pk_mul_f32") == GROUP // 2 and "v_mul_f64" not in sv
+    for ops in (valu, sv):
+        assert not any(o.startswith(("v_mad", "v_cvt", "v_fma", "v_rcp", "v_div", "v_cmp",
+                                     "v_cndmask")) for o in ops)
 
 
 def test_fit_class_b_loop(asm):
@@ -101,18 +134,21 @@ def test_fit_class_b_loop(asm):
 
 def test_fit_clamp_in_fit_loops(asm):
     """The clamp-in-fit variants (kcc_set_clamp_in_fit): class A takes each group's 8 clamp
-    values by two 16-B vector loads (uniform address) so the select reads them as VGPRs: 5.0 VALU per node (min, compare, select in
-    place of min3); class B (scalar loads) 6.5: fmin, compare, a move of the clamp value
-    into a VGPR (a gfx9 select reads one scalar operand at most, vcc included), select in
-    place of two min_f64."""
+    values by two 16-B vector loads (uniform address) so the select reads them as VGPRs:
+    5.0 VALU per node on the full path (min, compare, select in place of min3), 3.0 on the
+    memory-bound skip (x = qc: no f64 multiply, no min); class B (scalar loads) 6.5: fmin,
+    compare, a move of the clamp value into a VGPR (a gfx9 select reads one scalar operand at
+    most, vcc included), select in place of two min_f64."""
+    import bench
     body = kernel_body(asm, FIT_NC)
-    (a,) = loops_with(body, "v_pk_mul_f32")
-    assert any(ln.startswith("v_cndmask") for ln in a)
-    assert sum(WIDTH[ln.split()[0]] for ln in a if ln.startswith("s_load_dword")) == GROUP * 4
-    assert [ln.split()[0] for ln in a if ln.startswith(("global_", "buffer_", "flat_"))] == \
-        ["buffer_load_dwordx4"] * 2
-    va = [ln for ln in a if ln.startswith("v_")]
-    assert len(va) / GROUP <= 5.0, f"{len(va)} VALU / {GROUP} nodes"
+    full, skip = block_before(body, FULL), block_before(body, SKIP)
+    assert any(ln.startswith("v_cndmask") for ln in full) and any(ln.startswith("v_cndmask") for ln in skip)
+    loads = loop_header_loads(body, SKIP)
+    assert loads.count("s_load_dwordx16") == 2 and loads.count("s_load_dword") == 1, loads
+    va = [ln for ln in full if ln.startswith("v_")]
+    assert len(va) / GROUP == bench.FIT_NC_VALU_PER_NODE_WAVE, f"{len(va)} VALU / {GROUP} nodes"
+    vs = [ln.split()[0] for ln in skip if ln.startswith("v_")]
+    assert len(vs) / GROUP == bench.FIT_NC_SKIP_VALU_PER_NODE_WAVE and "v_mul_f64" not in vs
     (b,) = loops_with(body, "v_fma_f64")
     assert any(ln.startswith("v_cndmask") for ln in b)
     check_loads(b, GROUP * 7)
