@@ -686,7 +686,7 @@ def keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream, steps, war
     alg = C * 20 + n * 16
     gbs = alg / (ms * 1e-3) / 1e9
     del key, kc, km, oc, om
-    kernels = ["kb_hist", "kb_scan", "kb_scatter<2>", "kb_accum<2>", "kb_escape"]
+    kernels = ["kb_sweep<2>", "kb_gather<2>", "kb_escape"]  # the one-sweep path (KCC_KB_SWEEP)
     parts = [pmc_traffic(k) if with_traffic else (None, None) for k in kernels]
     traffic = sum(t for t, _ in parts) if all(t is not None for t, _ in parts) else None
     return {
@@ -697,10 +697,12 @@ def keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream, steps, war
                      "frac": gbs / HBM_PEAK_GBS, "bytes_per_launch": alg,
                      "traffic": traffic,
                      "traffic_source": parts[0][1] and f"profiles/pmc_traffic.json ({parts[0][1]}); "
-                                                       "sum of the five kernels per call",
-                     "note": "bucketed: LDS histograms, scatter of 8-B records (row in bucket, "
-                             "low cpu bits, memory / 64; the rest on an escape list), LDS "
-                             "accumulation; no global atomics on the common path"},
+                                                       "sum of the kernels per call",
+                     "note": "one sweep: each 16384-container tile counting-sorted by bucket in "
+                             "LDS into 8-B records (row in bucket, low cpu bits, memory / 64; the "
+                             "rest on an escape list) written as one contiguous run, then per "
+                             "bucket the tiles' segments summed in LDS; keys read once, no "
+                             "histogram pass, no global atomics on the common path"},
         "equals_csr_reduce": diff_rows == 0, "rows_differing": diff_rows,
     }
 
