@@ -110,6 +110,10 @@ def parse():
     ap.add_argument("--kernel-events", default="after", choices=["timed", "after"],
                     help="per-kernel HIP events inside the timed steps (timed) or in as many "
                          "extra steps after them (after)")
+    ap.add_argument("--graph", type=int, default=0, choices=[0, 1],
+                    help="1: the timed steps replay one step captured into a HIP graph "
+                         "(torch.cuda.CUDAGraph on the bench stream; every kernel still runs "
+                         "each step); not with --exchange torch")
     ap.add_argument("--drill-exchange-fallback", action="store_true",
                     help="test drill (N > 1): treat the p2p exchange's pre-timing check as failed "
                          "on the last rank, so every rank takes the RCCL fallback path")
@@ -400,21 +404,33 @@ def main():
             for _ in range(max(args.warmup, 1)):
                 step()
             torch.cuda.synchronize()
+        # --graph: one whole step (every launch, the exchange included) captured after the
+        # warm-up and the exchange check (workspaces allocated; the library's epochs live
+        # on the device, include/kcc.h), replayed for each timed step; its per-kernel
+        # events come from eager steps after the timed region
+        graph = None
+        if args.graph and exchange != "torch":
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream):
+                step()
+            graph.replay()
+            torch.cuda.synchronize()
+        run = graph.replay if graph is not None else step
         # per-launch kernel durations from HIP events the library records on the stream
         # each kernel runs on: over exactly the timed steps (--kernel-events timed), or
         # over as many extra steps right after them (after: the timed region has no events)
-        eng.profile_enable(args.kernel_events == "timed")
+        eng.profile_enable(args.kernel_events == "timed" and graph is None)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t_start = time.perf_counter()
         for _ in range(args.steps):
-            step()
+            run()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t_end = time.perf_counter()
-        if args.kernel_events == "after":
+        if args.kernel_events == "after" or graph is not None:
             eng.profile_enable(True)
             for _ in range(args.steps):
                 step(prof=True)
@@ -552,8 +568,11 @@ def main():
         },
         "pipeline": {"chunks": chunks, "reduce_ms_per_step": red_ms_tot / args.steps,
                      "fit_ms_per_step": fit_ms_tot / args.steps,
+                     "graph": graph is not None,
                      "note": "per-kernel HIP events, recorded in --kernel-events "
-                             f"{args.kernel_events} steps"},
+                             f"{'after' if graph is not None else args.kernel_events} steps"
+                             + ("; the timed steps replay one captured HIP graph"
+                                if graph is not None else "")},
         "fast_path_fraction": 1.0 - (slow_pairs / pairs if pairs else 0.0),
         "gen_seconds": gen_s,
     }

@@ -974,7 +974,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
     uint32_t r_fc[SUB];
     int32_t r_P[SUB];
     int32_t r_cl[SUB];  // NC: the clamp value of a streamed row
-    uint32_t r_v[SUB];  // KCC_FIT_MSKIP: min(floor(fm / P), 2^32 - 1) of a streamed row
+    uint32_t r_v[SUB];  // KCC_FIT_MSKIP: min(floor(fm / P), 2^32 - 2) of a streamed row
     unsigned long long sbal[SUB];
     uint32_t pk1[SUB], pk2[SUB], pk3[SUB];
     uint64_t always_sum = 0;
@@ -1053,7 +1053,9 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       r_cl[q] = cl_q;
       const double rP = recip_up_f64(P > 0 ? (uint64_t)P : 1ull);
       const int64_t V0 = (int64_t)((double)r_fm[q] * rP);  // floor(fm / P): exact (§5)
-      r_v[q] = P > 0 ? (V0 < 0xffffffffll ? (uint32_t)V0 : 0xffffffffu) : 0u;
+      // saturated at 2^32 - 2: 2^32 - 1 is the fit's "no skip" m_max (m >= 2^32 - 1), which
+      // must never compare <= a group's V_min
+      r_v[q] = P > 0 ? (V0 < 0xfffffffell ? (uint32_t)V0 : 0xfffffffeu) : 0u;
       if constexpr (NC) {
         pk1[q] = pk2[q] = pk3[q] = 0u;
       } else {

@@ -18,3 +18,9 @@ python3 -c "
 import json;d=json.load(open('gpurun_out/bench_$TAG.json'))
 v=d['roofline_valu']
 print('step', d['ms_per_step'], 'reduce', d['roofline_reduce']['ms_per_launch'], d['roofline_reduce']['frac'], 'fit', d['roofline_fit']['ms_per_launch'], 'valu', v['frac'], 'mskip', v['mskip_fraction'], 'keyed', d['keyed']['ms_per_launch'], d['keyed']['roofline']['frac'], 'chk', d['totals_checksum'])"
+# HIP-graph replay of the step: the default line and rank 0 of an 8-way C4 split, eager and graph
+timeout -k 10 240 python -u bench.py --graph 1 --no-cpu-baseline --no-keyed --no-pods --no-parse --no-dense \
+  > gpurun_out/bench_${TAG}_graph.json 2> gpurun_out/bench_${TAG}_graph.err || exit $?
+python3 -c "import json;d=json.load(open('gpurun_out/bench_${TAG}_graph.json'));print('graph step', d['ms_per_step'], 'chk', d['totals_checksum'])"
+bash scripts/gpu_emulate.sh ${TAG} C4 8 || exit $?
+EXTRA="--graph 1" bash scripts/gpu_emulate.sh ${TAG}g C4 8 || exit $?
