@@ -310,7 +310,9 @@ int kcc_fit_stream_rows(kcc_ctx* ctx, int64_t* streamed);
  * last kcc_capacity*_async / kcc_fit_*_async on device 0 that were summed without the memory
  * quotient, because every spec of the wave requests at most floor(free memory / allocatable
  * pods) of every node of the group (so floor(fm / m) >= allocatable pods there).  The same
- * totals either way; for the VALU accounting.  Synchronises the device. */
+ * totals either way; for the VALU accounting.  Counted only by fits launched while
+ * kcc_profile_enable is on (0 otherwise: the count costs a device atomic per wave).
+ * Synchronises the device. */
 int kcc_fit_mskip_groups(kcc_ctx* ctx, int64_t* groups);
 
 /* Fraction of (node, spec) pairs of the last kcc_fit* call that took the exact

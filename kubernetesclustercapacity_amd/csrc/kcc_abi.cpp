@@ -460,7 +460,7 @@ int fit_run_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_specs, int64_t
                                as<kcc::SlowNode>(dv.slow),
                                as<int64_t>(dv.slow_list), n_specs, spec_prep_of(dv), partial,
                                as<unsigned long long>(dv.counters), as<uint32_t>(dv.fit_q), 0,
-                               n_nodes, s, nullptr, as<uint32_t>(dv.fast_v)));
+                               n_nodes, s, nullptr, as<uint32_t>(dv.fast_v), dv.prof_on));
   return KCC_OK;
 }
 
@@ -655,7 +655,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                  as<int64_t>(dv.slow_list) + lo[c], n_specs, spec_prep_of(dv),
                                  partial, as<unsigned long long>(dv.counters),
                                  as<uint32_t>(dv.fit_q), c, n_nodes, s, fast_cl,
-                                 as<uint32_t>(dv.fast_v) + lo[c] / kcc::FIT_GROUP));
+                                 as<uint32_t>(dv.fast_v) + lo[c] / kcc::FIT_GROUP, dv.prof_on));
     if (dv.prof_on) {
       KCC_HIP(ctx, hipEventRecord(pp.b, s));
       pp.kind = 1;

@@ -2136,7 +2136,8 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     const FitGroup* __restrict__ fast_b, const SlowNode* __restrict__ slow,
     const int64_t* __restrict__ slow_list, int64_t S, const SpecRec* __restrict__ specs,
     int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t chunk,
-    int32_t gx, int32_t gy, const int32_t* __restrict__ fast_cl, const uint32_t* __restrict__ gvmin) {
+    int32_t gx, int32_t gy, const int32_t* __restrict__ fast_cl, const uint32_t* __restrict__ gvmin,
+    int32_t count_skips) {
   // XCD-aware order (speed only, never correctness): workgroups are dealt round-robin
   // over the 8 XCDs, so give every spec group of one node chunk the same b % 8
   const int32_t b = blockIdx.x, xcd = b & 7, r = b >> 3;
@@ -2509,7 +2510,9 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     const unsigned long long act = __ballot(active);
     if (slow_iters && lane == 0)
       atomicAdd(&counters[CNT_SLOW_PAIRS], (unsigned long long)slow_iters * (unsigned long long)__popcll(act));
-    if (KCC_FIT_MSKIP && nskip && lane == 0)  // (VALU accounting: bench.py)
+    // (VALU accounting: bench.py) only when profiling: one same-address device atomic per
+    // wave from every XCD serialised past the L2s (8192 waves: +50 us on the C4 fit)
+    if (KCC_FIT_MSKIP && count_skips && nskip && lane == 0)
       atomicAdd(&counters[CNT_FIT_MSKIP], (unsigned long long)nskip);
   }
   // the clamp in the fit: the rows clamped for every spec (P <= 0, never streamed), once
@@ -2836,7 +2839,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, uint32_t* queue, int chunk,
                       int64_t grid_nodes, hipStream_t s, const int32_t* fast_cl,
-                      const uint32_t* gvmin) {
+                      const uint32_t* gvmin, bool count_skips) {
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
   const int64_t gx = (n_specs + FIT_SPW - 1) / FIT_SPW;
   const int64_t n_groups = fit_groups(n_nodes);
@@ -2855,7 +2858,8 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
   auto kern = fast_cl ? fit_kernel<true> : fit_kernel<false>;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, queue, fast_a,
                      fast_b, slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)chunk,
-                     (int32_t)gx, (int32_t)gy, fast_cl, KCC_FIT_MSKIP ? gvmin : nullptr);
+                     (int32_t)gx, (int32_t)gy, fast_cl, KCC_FIT_MSKIP ? gvmin : nullptr,
+                     (int32_t)(count_skips ? 1 : 0));
   return hipGetLastError();
 }
 

@@ -47,7 +47,9 @@ def run(names, config, rounds, reps, shard=1):
     libs, ctxs, outs, golden = {}, {}, {}, {}
     shared_out = dict(uc=torch.empty(n, dtype=torch.int64, device=dev),
                       um=torch.empty(n, dtype=torch.int64, device=dev),
-                      part=torch.empty(2 * S, dtype=torch.int64, device=dev))
+                      part=torch.empty(2 * S, dtype=torch.int64, device=dev),
+                      tot=torch.empty(S, dtype=torch.int64, device=dev),
+                      err=torch.empty(S, dtype=torch.int32, device=dev))
     for nm in names:
         L = _lib.load(os.path.join(VDIR, f"libkcc_{nm}.so"))
         h = C.c_void_p()
@@ -76,9 +78,12 @@ def run(names, config, rounds, reps, shard=1):
 
     times = {nm: {"reduce": [], "fit": []} for nm in names}
     with torch.cuda.stream(stream):
-        for nm in names:  # warm up; each variant's outputs kept for the comparison
-            reduce(nm)
-            fit(nm)
+        for nm in names:  # warm up; each variant's outputs kept for the comparison (the
+            reduce(nm)    # partial is in the variant's internal spec order: its finalized
+            fit(nm)       # totals are compared)
+            o = outs[nm]
+            assert libs[nm].kcc_fit_finalize_async(ctxs[nm], S, P(o["part"]), P(o["tot"]),
+                                                   P(o["err"]), sh) == 0
             torch.cuda.synchronize()
             golden[nm] = {k: v.clone() for k, v in shared_out.items()}
         torch.cuda.synchronize()
@@ -94,7 +99,7 @@ def run(names, config, rounds, reps, shard=1):
                     times[nm][what].append(e0.elapsed_time(e1) / reps)
     ref = names[0]
     for nm in names:
-        for k in ("uc", "um", "part"):
+        for k in ("uc", "um", "tot", "err"):
             if not nm.startswith("diag_"):  # diagnostic builds are timing-only
                 assert torch.equal(golden[nm][k], golden[ref][k]), f"{nm} differs from {ref} in {k}"
         r = times[nm]
