@@ -34,6 +34,9 @@ constexpr int PC_BLOCK = PS_THREADS * PC_PER_THREAD;
 constexpr int PQ_PER_THREAD = KCC_PQ_PER_THREAD;      // parse_quantity_kernel: strings per lane
 constexpr int PQ_BLOCK = PS_THREADS * PQ_PER_THREAD;
 constexpr int PS_LDS_WORDS = 6144;                    // 24 KiB of staged characters
+#ifndef KCC_PQ_V2
+#define KCC_PQ_V2 1  // parse_quantity_kernel's register path: 1 = qty_fast2, 0 = qty_fast (A/B)
+#endif
 
 __device__ __forceinline__ bool go_space(uint32_t c) {
   // strings.TrimSpace on ASCII input: '\t', '\n', '\v', '\f', '\r', ' '
@@ -648,7 +651,7 @@ static_assert(inv5_pow(7) * 78125u == 1u, "inverse of 5^7 mod 2^64");
 // V = D x 10^(16 - d), and D = V / 10^(16 - d) exactly (shift, multiply by the inverse
 // of 5^(16 - d)).  Caps as quantity_value: binary amounts at 2^63 - 1; a decimal amount
 // beyond it is PARSE_UNSUPPORTED (k8s wraps it).
-__device__ __forceinline__ bool qty_fast(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+[[maybe_unused]] __device__ __forceinline__ bool qty_fast(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
                                          uint32_t al, int L, const uint64_t* s_p10,
                                          const uint64_t* s_lim, const uint64_t* s_inv,
                                          int64_t& v, int8_t& st) {
@@ -716,6 +719,91 @@ __device__ __forceinline__ bool qty_fast(uint32_t w0, uint32_t w1, uint32_t w2, 
   return ok;
 }
 
+// Character classes for qty_fast2 (one LDS byte per character): bit 7 a digit; bits 0-2 the
+// decimal suffix k M G T P E (10^3k: 1..6; 'K' alone is none); bits 3-5 the binary prefix
+// K M G T P E of "Ki".."Ei" (2^10k: 1..6); bit 6 'i'.
+__host__ __device__ constexpr uint32_t qty_class(uint32_t ch) {
+  return (ch - '0' <= 9u) ? 0x80u
+       : ch == 'i' ? 0x40u
+       : ch == 'k' ? 1u
+       : ch == 'K' ? (1u << 3)
+       : ch == 'M' ? (2u | (2u << 3))
+       : ch == 'G' ? (3u | (3u << 3))
+       : ch == 'T' ? (4u | (4u << 3))
+       : ch == 'P' ? (5u | (5u << 3))
+       : ch == 'E' ? (6u | (6u << 3)) : 0u;
+}
+
+// qty_fast's contract (same accepted strings, values and statuses), fewer VALU: the suffix
+// from the character-class table; the digits right-aligned by ONE 128-bit shift left by
+// 8 x (16 - d) bytes' worth of bits — the suffix and whatever follows the string fall off
+// the top, zeros (leading '0' digits) come in at the bottom, so no masks and no exact
+// division by 10^(16 - d); four digits per word from two v_dot4_u32_u8 (10 b0 + b1,
+// 10 b2 + b3) and a 24-bit multiply-add.
+__device__ __forceinline__ bool qty_fast2(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+                                          uint32_t al, int L, const uint8_t* s_cls,
+                                          const uint64_t* s_p10, const uint64_t* s_lim,
+                                          int64_t& v, int8_t& st) {
+  const uint64_t MAXV = 0x7fffffffffffffffull;
+  const uint32_t a0 = __builtin_amdgcn_alignbyte(w1, w0, al);
+  const uint32_t a1 = __builtin_amdgcn_alignbyte(w2, w1, al);
+  const uint32_t a2 = __builtin_amdgcn_alignbyte(w3, w2, al);
+  const uint32_t a3 = __builtin_amdgcn_alignbyte(0u, w3, al);
+  // the last two characters: the 16 bits at byte p = L - 2 (L = 1: at 0, shifted)
+  const uint32_t p = L >= 2 ? (uint32_t)(L - 2) : 0u;
+  const uint32_t q = p >> 2;  // 0..2
+  const uint32_t lo = q == 0 ? a0 : (q == 1 ? a1 : a2);
+  const uint32_t hi = q == 0 ? a1 : (q == 1 ? a2 : a3);
+  const uint32_t pair = __builtin_amdgcn_alignbyte(hi, lo, p & 3u);
+  const uint32_t z = L >= 2 ? (pair >> 8) & 0xffu : pair & 0xffu;  // last
+  const uint32_t y = L >= 2 ? pair & 0xffu : 0u;                    // second last
+  const uint32_t zc = s_cls[z], yc = s_cls[y];
+  const bool bin = (zc & 0x40u) != 0u && (yc & 0x38u) != 0u;  // "Ki".."Ei"
+  const uint32_t zd = zc & 7u;                                  // k M G T P E
+  const bool dec = !bin && zd != 0u;
+  const bool dig = (zc & 0x80u) != 0u;
+  const int d = L - (bin ? 2 : (dec ? 1 : 0));  // the digits
+  // T = (characters - '0') << (128 - 8d): the d digits end at byte 15
+  const uint64_t ZZ = 0x3030303030303030ull;
+  const uint64_t l64 = (((uint64_t)a1 << 32) | a0) ^ ZZ;
+  const uint64_t h64 = (((uint64_t)a3 << 32) | a2) ^ ZZ;
+  const uint32_t sh = (uint32_t)(128 - 8 * d);  // 24..120 on the fast path
+  const uint64_t xl = l64 << (sh & 63u);
+  const bool big = sh >= 64u;
+  const uint64_t th = big ? xl : ((h64 << (sh & 63u)) | (l64 >> ((64u - sh) & 63u)));
+  const uint64_t tl = big ? 0ull : xl;
+  const uint32_t t0 = (uint32_t)tl, t1 = (uint32_t)(tl >> 32), t2 = (uint32_t)th, t3 = (uint32_t)(th >> 32);
+  const uint32_t H = 0x76767676u;  // a byte > 9 sets bit 7 of t + 0x76 or of t itself
+  const uint32_t bad = ((t0 + H) | t0 | (t1 + H) | t1 | (t2 + H) | t2 | (t3 + H) | t3) & 0x80808080u;
+  // four digits per word (the first in the low byte): (10 b0 + b1) x 100 + 10 b2 + b3
+  // (24-bit multiply-adds in asm: the compiler otherwise picks the quarter-rate
+  // v_mad_u64_u32 for them)
+  auto mad24 = [](uint32_t a, uint32_t b, uint32_t c) -> uint32_t {
+    uint32_t r;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+  };
+  auto quad = [&](uint32_t t) -> uint32_t {
+    const uint32_t hi2 = __builtin_amdgcn_udot4(t, 0x0000010au, 0u, false);
+    const uint32_t lo2 = __builtin_amdgcn_udot4(t, 0x010a0000u, 0u, false);
+    return mad24(hi2, 100u, lo2);
+  };
+  const uint32_t q01 = mad24(quad(t0), 10000u, quad(t1));
+  const uint32_t q23 = mad24(quad(t2), 10000u, quad(t3));
+  const uint64_t D = (uint64_t)q01 * 100000000u + q23;  // < 10^13
+  const bool ok = (bin || dec || dig) && d >= 1 && bad == 0;
+  const int bexp = bin ? 10 * (int)((yc >> 3) & 7u) : 0;
+  uint64_t mag = D > (MAXV >> bexp) ? MAXV : D << bexp;
+  st = PARSE_OK;
+  if (dec) {
+    const bool over = D > s_lim[zd];
+    mag = over ? 0 : D * s_p10[zd];
+    st = over ? PARSE_UNSUPPORTED : PARSE_OK;
+  }
+  v = (int64_t)mag;
+  return ok;
+}
+
 // Quantity.Value() without LDS, as parse_cpu_kernel: one lane per string, strings of
 // <= 13 characters from one aligned 16-byte buffer load per lane, parsed in registers
 // (qty_fast) when they are plain digits (<= 13) and an optional integral suffix — k M G
@@ -732,6 +820,8 @@ __global__ __launch_bounds__(PS_THREADS) void parse_quantity_kernel(int64_t n, c
   const uint64_t MAXV = 0x7fffffffffffffffull;
   // 10^3k and (2^63 - 1) / 10^3k (k = 0..6), and (5^k)^-1 mod 2^64 (k = 0..15)
   __shared__ uint64_t s_p10[8], s_lim[8], s_inv[16];
+  __shared__ uint8_t s_cls[KCC_PQ_V2 ? 256 : 1];  // qty_class of every byte value
+  if (KCC_PQ_V2) s_cls[threadIdx.x] = (uint8_t)qty_class(threadIdx.x);  // (256 threads)
   if (threadIdx.x < 8) {
     uint64_t p = 1;
     for (unsigned k = 0; k < threadIdx.x && k < 6; ++k) p *= 1000u;
@@ -785,6 +875,17 @@ __global__ __launch_bounds__(PS_THREADS) void parse_quantity_kernel(int64_t n, c
     int64_t v = 0;
     int8_t st = PARSE_BADOFF;
     bool done = false;
+#if KCC_PQ_V2
+    if (fast[r])
+      done = qty_fast2(w[r][0], w[r][1], w[r][2], w[r][3], (uint32_t)sb[r], (int)(se[r] - sb[r]),
+                       s_cls, s_p10, s_lim, v, st);
+    if (!done) {
+      need |= 1u << r;  // the offsets' checks and the general parser: below
+    } else {
+      out[i] = v;
+      status[i] = st;
+    }
+#else
     if (fast[r])
       done = qty_fast(w[r][0], w[r][1], w[r][2], w[r][3], (uint32_t)(sb[r] & 3), (int)(se[r] - sb[r]),
                       s_p10, s_lim, s_inv, v, st);
@@ -795,12 +896,18 @@ __global__ __launch_bounds__(PS_THREADS) void parse_quantity_kernel(int64_t n, c
       out[i] = v;
       status[i] = st;
     }
+#endif
   }
 #pragma unroll 1
   for (int r = 0; r < PQ_PER_THREAD; ++r) {
     if (!((need >> r) & 1u)) continue;
     const int64_t i = base + r * PS_THREADS;
-    const int64_t b = off[i], e = off[i + 1];  // (checked above)
+    const int64_t b = off[i], e = off[i + 1];  // (v1: checked above)
+    if (KCC_PQ_V2 && !(b >= 0 && e >= b && e <= n_bytes && e - b < ((int64_t)1 << 31))) {
+      out[i] = 0;
+      status[i] = PARSE_BADOFF;
+      continue;
+    }
     const QtyResult q = quantity_value_global(bytes + b, (int)(e - b));
     out[i] = q.v;
     status[i] = (int8_t)q.st;

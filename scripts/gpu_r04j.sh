@@ -7,6 +7,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:-r04j}
 mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_parse.py tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread \
+  > gpurun_out/pytest_$TAG.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
 bash scripts/gpu_ab.sh $TAG base msk0 || exit $?
 for v in base msk0; do
   timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_$v -o run \
@@ -27,3 +30,6 @@ timeout -k 10 240 python -u bench.py --graph 1 --no-cpu-baseline --no-keyed --no
 python3 -c "import json;d=json.load(open('gpurun_out/bench_${TAG}_graph.json'));print('graph step', d['ms_per_step'], 'chk', d['totals_checksum'])"
 bash scripts/gpu_emulate.sh ${TAG} C4 8 || exit $?
 EXTRA="--graph 1" bash scripts/gpu_emulate.sh ${TAG}g C4 8 || exit $?
+timeout -k 10 300 python -u scripts/ab_variants.py run --parse --config C4 --rounds 5 --reps 10 base pqv1 \
+  > gpurun_out/ab_parse_$TAG.txt 2>&1 || exit $?
+grep '^{' gpurun_out/ab_parse_$TAG.txt
