@@ -776,20 +776,14 @@ __device__ __forceinline__ bool qty_fast2(uint32_t w0, uint32_t w1, uint32_t w2,
   const uint32_t H = 0x76767676u;  // a byte > 9 sets bit 7 of t + 0x76 or of t itself
   const uint32_t bad = ((t0 + H) | t0 | (t1 + H) | t1 | (t2 + H) | t2 | (t3 + H) | t3) & 0x80808080u;
   // four digits per word (the first in the low byte): (10 b0 + b1) x 100 + 10 b2 + b3
-  // (24-bit multiply-adds in asm: the compiler otherwise picks the quarter-rate
-  // v_mad_u64_u32 for them)
-  auto mad24 = [](uint32_t a, uint32_t b, uint32_t c) -> uint32_t {
-    uint32_t r;
-    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-  };
-  auto quad = [&](uint32_t t) -> uint32_t {
+  // (the second dot4 accumulates 100 x the first; no inline asm here: a VALU read of a
+  // dot4 result needs a wait state the compiler inserts only around instructions it sees)
+  auto quad = [](uint32_t t) -> uint32_t {
     const uint32_t hi2 = __builtin_amdgcn_udot4(t, 0x0000010au, 0u, false);
-    const uint32_t lo2 = __builtin_amdgcn_udot4(t, 0x010a0000u, 0u, false);
-    return mad24(hi2, 100u, lo2);
+    return __builtin_amdgcn_udot4(t, 0x010a0000u, __umul24(hi2, 100u), false);
   };
-  const uint32_t q01 = mad24(quad(t0), 10000u, quad(t1));
-  const uint32_t q23 = mad24(quad(t2), 10000u, quad(t3));
+  const uint32_t q01 = __umul24(quad(t0), 10000u) + quad(t1);
+  const uint32_t q23 = __umul24(quad(t2), 10000u) + quad(t3);
   const uint64_t D = (uint64_t)q01 * 100000000u + q23;  // < 10^13
   const bool ok = (bin || dec || dig) && d >= 1 && bad == 0;
   const int bexp = bin ? 10 * (int)((yc >> 3) & 7u) : 0;
