@@ -740,7 +740,7 @@ __host__ __device__ constexpr uint32_t qty_class(uint32_t ch) {
 // the top, zeros (leading '0' digits) come in at the bottom, so no masks and no exact
 // division by 10^(16 - d); four digits per word from two v_dot4_u32_u8 (10 b0 + b1,
 // 10 b2 + b3) and a 24-bit multiply-add.
-__device__ __forceinline__ bool qty_fast2(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+[[maybe_unused]] __device__ __forceinline__ bool qty_fast2(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
                                           uint32_t al, int L, const uint8_t* s_cls,
                                           const uint64_t* s_p10, const uint64_t* s_lim,
                                           int64_t& v, int8_t& st) {

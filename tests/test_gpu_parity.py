@@ -230,6 +230,40 @@ def test_class_a_wave_boundaries(engine):
     np.testing.assert_array_equal(t, ot)
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+def test_fit_memory_skip_thresholds(engine, mode):
+    """The fit's memory-bound skip at its thresholds: node groups whose
+    V = floor(fm / P) saturates the 32-bit V_min (free memory near 2^50, P = 1..3) or sits
+    exactly on a spec's request (fm = m x P, m x P - 1), against class-A waves whose largest
+    request is 2^32 - 2, 2^32 - 1 (no skip), 2^32, 2^40 or equal to V; both clamp modes."""
+    rng = np.random.default_rng(77)
+    tops = [3 << 30, (1 << 32) - 2, (1 << 32) - 1, 1 << 32, 1 << 40]
+    waves, lo = [], 1 << 18  # wave w (memory order): 63 requests in (top[w-1], top[w]] + top[w]
+    for top in tops:
+        waves.append(np.append(rng.integers(lo, top + 1, 63), top))
+        lo = top + 1
+    sm = rng.permutation(np.concatenate(waves)).astype(np.int64)
+    sc = rng.integers(1, 4000, sm.size).astype(np.uint64)
+    n = 16_000
+    P = rng.integers(1, 4, n)
+    fm = (1 << 50) - rng.integers(1, 1 << 30, n)                  # V saturates
+    on = np.arange(n) % 4 == 1
+    mm = np.asarray(tops, np.int64)[rng.integers(0, len(tops), n)]
+    fm[on] = mm[on] * P[on] - (np.arange(n)[on] % 8 == 1)          # V = m or m - 1 (rounded)
+    fm[np.arange(n) % 4 == 2] = rng.integers(1 << 20, 1 << 34, (np.arange(n) % 4 == 2).sum())
+    fc = rng.integers(1, 1 << 22, n)
+    args = (fc.astype(np.uint64), fm.astype(np.int64), P.astype(np.int64),
+            rng.integers(0, 3, n).astype(np.int64), np.zeros(n, np.uint64), np.zeros(n, np.int64))
+    engine.set_clamp_in_fit(mode)
+    try:
+        t, e = engine.total_possible_max_replicas(*args, sc, sm)
+    finally:
+        engine.set_clamp_in_fit(-1)
+    ot, oe = coracle.fit(*args, sc, sm, NT)
+    np.testing.assert_array_equal(e, oe)
+    np.testing.assert_array_equal(t, ot)
+
+
 def test_mixed_class_waves(engine):
     """64 class-A, 64 class-B (memory < 2^18) and 64 exact-path specs, shuffled: the
     partition regroups them and every class matches the oracle."""
