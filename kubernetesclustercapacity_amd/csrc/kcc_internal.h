@@ -332,9 +332,12 @@ enum {
 // known; where m_max <= gvmin[group], floor(fm / m) >= P for every lane and node of the
 // group (m <= fm / P  <=>  m P <= fm), so min(findMin(qc, qm), P) = min(qc, P) and the
 // group is summed without the f64 memory quotient (class A: 2 VALU per node x wave instead
-// of 3; the clamp in the fit: 3 instead of 5).
+// of 3; the clamp in the fit: 3 instead of 5).  Off by default: measured slower (C4 fit
+// 124.2 -> 129.5 us, node_prep 26.3 -> 29.0 us; 8-way shard prepare + fit 57.2 -> 59.4 us):
+// the per-group branch waits for all of the group's scalar loads and its V_min, and only
+// about half of the (group, wave) pairs skip.
 #ifndef KCC_FIT_MSKIP
-#define KCC_FIT_MSKIP 1
+#define KCC_FIT_MSKIP 0
 #endif
 // The clamp correction after every node_prep of the call (n_nodes: the call's rows, for
 // the binned records' pass count): partial[s] -= D_s for the normal specs of clamp-free

@@ -2305,7 +2305,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
         }
         acc32 += (int32_t)(m3[0] + m3[1]);
       }
-      if (KCC_FIT_MSKIP) asm volatile("; fit: full" : "+v"(acc32));
+      asm volatile("; fit: full" : "+v"(acc32));  // (the ISA tests' marker)
     }
     set_round_nearest();
     acc += (uint64_t)(int64_t)acc32;
@@ -2384,7 +2384,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
         }
         acc32 += m3[0] + m3[1];
       }
-      if (KCC_FIT_MSKIP) asm volatile("; fit: full" : "+v"(acc32));
+      asm volatile("; fit: full" : "+v"(acc32));  // (the ISA tests' marker)
     }
     set_round_nearest();
     acc += (uint64_t)(int64_t)acc32;

@@ -35,6 +35,16 @@ def asm(tmp_path_factory):
     return out.read_text()
 
 
+@pytest.fixture(scope="module")
+def asm_mskip(tmp_path_factory):
+    """The memory-bound skip build (KCC_FIT_MSKIP=1, off in the release library)."""
+    out = tmp_path_factory.mktemp("isa_mskip") / "kcc.s"
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-S",
+                    "--cuda-device-only", "-DKCC_FIT_MSKIP=1", SRC, "-o", str(out)], check=True,
+                   capture_output=True)
+    return out.read_text()
+
+
 def kernel_body(asm, name):
     m = re.search(rf"^(_ZN3kcc12_GLOBAL__N_1\d+{name}\w*):\s*;", asm, re.M)
     assert m, name
@@ -95,27 +105,34 @@ def loop_header_loads(body, marker):
 SKIP, FULL = "; fit: memory-bound skip", "; fit: full"
 
 
-def test_fit_class_a_loop(asm):
+@pytest.mark.parametrize("mskip", [False, True])
+def test_fit_class_a_loop(asm, asm_mskip, mskip):
     """Class A, per 8-node group: the full path (bench.FIT_VALU_PER_NODE_WAVE = 3 VALU per
-    node: packed f32 and f64 multiplies, min3, add) and the memory-bound skip (2: no f64
-    multiply, min with P) — no division, conversion, correction, compare or select; every
-    group's scalar loads (fm, fc, P, its smallest V) issued before the branch, no vector
-    memory in either body."""
+    node: packed f32 and f64 multiplies, min3, add), in the release build and beside the
+    memory-bound skip (KCC_FIT_MSKIP=1: 2, no f64 multiply, min with P) — no division,
+    conversion, correction, compare or select; with the skip every group's scalar loads
+    (fm, fc, P, its smallest V) issued before the branch; no vector memory in any body."""
     import bench
-    body = kernel_body(asm, FIT)
-    full, skip = block_before(body, FULL), block_before(body, SKIP)
+    body = kernel_body(asm_mskip if mskip else asm, FIT)
+    full = block_before(body, FULL)
+    skip = block_before(body, SKIP) if mskip else full
+    assert (SKIP in body) == mskip
     for lines in (full, skip):
         assert not [ln for ln in lines if ln.startswith(("global_", "flat_", "buffer_", "ds_"))]
-    loads = loop_header_loads(body, SKIP)
-    assert loads.count("s_load_dwordx16") == 2 and loads.count("s_load_dword") == 1, loads
+    if mskip:
+        loads = loop_header_loads(body, SKIP)
+        assert loads.count("s_load_dwordx16") == 2 and loads.count("s_load_dword") == 1, loads
+    else:
+        check_loads(loop_of(body, FULL), GROUP * 4)  # fm (f64), fc, P (u32) per node
     valu = [ln.split()[0] for ln in full if ln.startswith("v_")]
     assert len(valu) / GROUP == pytest.approx(bench.FIT_VALU_PER_NODE_WAVE, abs=1e-9), \
         f"{len(valu)} VALU / {GROUP} nodes: update bench.FIT_VALU_PER_NODE_WAVE"
     assert valu.count("v_pk_mul_f32") == GROUP // 2 and valu.count("v_mul_f64") == GROUP
     assert valu.count("v_min3_u32") == GROUP and valu.count("v_add3_u32") == GROUP // 2
     sv = [ln.split()[0] for ln in skip if ln.startswith("v_")]
-    assert len(sv) / GROUP == pytest.approx(bench.FIT_SKIP_VALU_PER_NODE_WAVE, abs=1e-9)
-    assert sv.count("v_pk_mul_f32") == GROUP // 2 and "v_mul_f64" not in sv
+    if mskip:
+        assert len(sv) / GROUP == pytest.approx(bench.FIT_SKIP_VALU_PER_NODE_WAVE, abs=1e-9)
+        assert sv.count("v_pk_mul_f32") == GROUP // 2 and "v_mul_f64" not in sv
     for ops in (valu, sv):
         assert not any(o.startswith(("v_mad", "v_cvt", "v_fma", "v_rcp", "v_div", "v_cmp",
                                      "v_cndmask")) for o in ops)
@@ -132,7 +149,8 @@ def test_fit_class_b_loop(asm):
     assert not any(o.startswith(("v_cvt", "v_max", "v_mul", "v_cmp", "v_cndmask")) for o in ops)
 
 
-def test_fit_clamp_in_fit_loops(asm):
+@pytest.mark.parametrize("mskip", [False, True])
+def test_fit_clamp_in_fit_loops(asm, asm_mskip, mskip):
     """The clamp-in-fit variants (kcc_set_clamp_in_fit): class A takes each group's 8 clamp
     values by two 16-B vector loads (uniform address) so the select reads them as VGPRs:
     5.0 VALU per node on the full path (min, compare, select in place of min3), 3.0 on the
@@ -140,15 +158,18 @@ def test_fit_clamp_in_fit_loops(asm):
     compare, a move of the clamp value into a VGPR (a gfx9 select reads one scalar operand at
     most, vcc included), select in place of two min_f64."""
     import bench
-    body = kernel_body(asm, FIT_NC)
-    full, skip = block_before(body, FULL), block_before(body, SKIP)
-    assert any(ln.startswith("v_cndmask") for ln in full) and any(ln.startswith("v_cndmask") for ln in skip)
-    loads = loop_header_loads(body, SKIP)
-    assert loads.count("s_load_dwordx16") == 2 and loads.count("s_load_dword") == 1, loads
+    body = kernel_body(asm_mskip if mskip else asm, FIT_NC)
+    full = block_before(body, FULL)
+    assert any(ln.startswith("v_cndmask") for ln in full)
     va = [ln for ln in full if ln.startswith("v_")]
     assert len(va) / GROUP == bench.FIT_NC_VALU_PER_NODE_WAVE, f"{len(va)} VALU / {GROUP} nodes"
-    vs = [ln.split()[0] for ln in skip if ln.startswith("v_")]
-    assert len(vs) / GROUP == bench.FIT_NC_SKIP_VALU_PER_NODE_WAVE and "v_mul_f64" not in vs
+    if mskip:
+        skip = block_before(body, SKIP)
+        assert any(ln.startswith("v_cndmask") for ln in skip)
+        loads = loop_header_loads(body, SKIP)
+        assert loads.count("s_load_dwordx16") == 2 and loads.count("s_load_dword") == 1, loads
+        vs = [ln.split()[0] for ln in skip if ln.startswith("v_")]
+        assert len(vs) / GROUP == bench.FIT_NC_SKIP_VALU_PER_NODE_WAVE and "v_mul_f64" not in vs
     (b,) = loops_with(body, "v_fma_f64")
     assert any(ln.startswith("v_cndmask") for ln in b)
     check_loads(b, GROUP * 7)
