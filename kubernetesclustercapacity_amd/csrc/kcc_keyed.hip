@@ -672,7 +672,7 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
 constexpr int KB_GA_THREADS = 1024;
 constexpr int KB_GA_WAVES = KB_GA_THREADS / 64;
 #ifndef KCC_KB_GA_U
-#define KCC_KB_GA_U 8
+#define KCC_KB_GA_U 16  // C4 A/B (one part): 8 -> 0.3404 ms, 16 -> 0.3394 ms
 #endif
 constexpr int KB_GA_U = KCC_KB_GA_U;  // segments per wave in flight (128 records of each)
 constexpr int KB_GA_CH = 2048;     // tiles per table chunk in LDS
@@ -814,7 +814,8 @@ bool keyed_bucketed(int64_t n_keys, int64_t n) {  // (record indices, padded til
 }
 
 #ifndef KCC_KB_GA_PARTS
-#define KCC_KB_GA_PARTS 0  // gather workgroups per bucket (0: about one per CU over the buckets)
+#define KCC_KB_GA_PARTS 1  // gather workgroups per bucket (0: about one per CU over the buckets;
+                           // C4 A/B: 1 -> 0.339-0.340 ms, auto (2 there) 0.372 ms)
 #endif
 constexpr int KB_GA_PARTS_MAX = 4;
 int keyed_sweep_parts(int64_t nb) {
