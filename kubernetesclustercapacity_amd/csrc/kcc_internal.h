@@ -504,7 +504,11 @@ constexpr int KB_SW_THREADS = 1024;
 #endif
 constexpr int KB_SW_PER = KCC_KB_SW_PER;
 constexpr int64_t KB_SW_TILE = (int64_t)KB_SW_THREADS * KB_SW_PER;  // 16384 (8192)
-__host__ __device__ inline int64_t keyed_sweep_tiles(int64_t n) { return (n + KB_SW_TILE - 1) / KB_SW_TILE; }
+// containers per sweep tile: KB_SW_TILE, or (beyond one round of one tile per CU) cut so
+// the tiles make whole rounds (C4: 2418 tiles = 9.4 rounds -> 2560 of 15472 = 10); a
+// tile's records keep the KB_SW_TILE stride in the staging buffer
+int64_t keyed_sweep_tile(int64_t n);
+int64_t keyed_sweep_tiles(int64_t n);
 int keyed_sweep_parts(int64_t nb);
 // sizes of the KeyedWork arrays for a call (either path): u32 words of counts, u64
 // record slots of sr, u64 words of part_acc

@@ -508,7 +508,8 @@ __global__ __launch_bounds__(256) void kb_escape(uint32_t* __restrict__ esc_n,
 }
 
 // ---- one-sweep path (KCC_KB_SWEEP, NA = 0 / 2) ----------------------------------------
-// kb_sweep: tile g = containers [g * KB_SW_TILE, ...), 16 per thread, every load issued
+// kb_sweep: tile g = containers [g * tile, ...) (tile <= KB_SW_TILE: keyed_sweep_tile), 16
+// per thread, every load issued
 // at once (16-B loads of quads).  Each valid container's rank within its bucket comes from
 // an LDS counter (two 16-bit counters per word: a tile holds at most 16384 containers),
 // one exclusive scan of the counts gives the bucket starts, the records are counting-sorted
@@ -528,7 +529,7 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
     int64_t n, int64_t n_keys, const int32_t* __restrict__ key, const uint64_t* __restrict__ a0,
     const uint64_t* __restrict__ a1, int nb, uint32_t* __restrict__ tab, uint64_t* __restrict__ sr,
     uint32_t* __restrict__ esc_n, int32_t* __restrict__ esc_row, uint64_t* __restrict__ esc_cpu,
-    uint64_t* __restrict__ esc_mem) {
+    uint64_t* __restrict__ esc_mem, int64_t tile) {
   static_assert(NA == 0 || NA == 2, "one-sweep path: counts or requests");
   constexpr int NS = NA > 0 ? NA : 1;
   __shared__ uint64_t st[KB_SW_TILE];            // the tile's records, bucket order
@@ -536,8 +537,8 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
   __shared__ uint32_t cnt2[KB_SW_CNT_WORDS];
   __shared__ uint32_t wtot[KB_SW_WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t t0 = (int64_t)blockIdx.x * KB_SW_TILE;
-  const int64_t t1 = min(t0 + KB_SW_TILE, n);
+  const int64_t t0 = (int64_t)blockIdx.x * tile;  // tile <= KB_SW_TILE, a multiple of 4
+  const int64_t t1 = min(t0 + tile, n);
   const int nw = (nb + 1) / 2;
   for (int w = tid; w < nw; w += KB_SW_THREADS) cnt2[w] = 0;
   // every load of the tile first: quads of consecutive containers (16-B loads)
@@ -654,12 +655,17 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
   }
   __syncthreads();
   // the stage leaves as one contiguous run: 16-B stores of record pairs (whole lines)
-  uint64_t* dst = sr + t0;
+  uint64_t* dst = sr + (int64_t)blockIdx.x * KB_SW_TILE;
   for (uint32_t j = 2u * (uint32_t)tid; j < nvalid; j += 2u * KB_SW_THREADS) {
-    if (j + 1 < nvalid)
+    if (j + 1 < nvalid) {
+#if KCC_KB_SW_NTST  // A/B: streaming stores (the gather re-reads the records right after)
+      __builtin_nontemporal_store(*reinterpret_cast<const u64x2*>(&st[j]), reinterpret_cast<u64x2*>(dst + j));
+#else
       *reinterpret_cast<u64x2*>(dst + j) = *reinterpret_cast<const u64x2*>(&st[j]);
-    else
+#endif
+    } else {
       dst[j] = st[j];
+    }
   }
 }
 
@@ -675,11 +681,17 @@ constexpr int KB_GA_WAVES = KB_GA_THREADS / 64;
 #define KCC_KB_GA_U 16  // C4 A/B (one part): 8 -> 0.3404 ms, 16 -> 0.3394 ms
 #endif
 constexpr int KB_GA_U = KCC_KB_GA_U;  // segments per wave in flight (128 records of each)
+#ifndef KCC_KB_SW_NTST
+#define KCC_KB_SW_NTST 0
+#endif
+#ifndef KCC_KB_GA_REV
+#define KCC_KB_GA_REV 1  // tiles in descending order: the last-written records first, while the
+#endif                   // 256 MiB memory-side cache may still hold them
 constexpr int KB_GA_CH = 2048;     // tiles per table chunk in LDS
 
 template <int NA>
 __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
-    int64_t n, int64_t n_keys, int nb, int parts, const uint32_t* __restrict__ tab,
+    int64_t G, int64_t n_keys, int nb, int parts, const uint32_t* __restrict__ tab,
     const uint64_t* __restrict__ sr, uint64_t* __restrict__ part_acc, uint32_t* __restrict__ arrive,
     uint64_t* __restrict__ o0, uint64_t* __restrict__ o1) {
   constexpr int NACC = NA > 0 ? NA : 1;
@@ -692,7 +704,6 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
   for (int r = tid; r < KB_ROWS; r += KB_GA_THREADS)
 #pragma unroll
     for (int a = 0; a < NACC; ++a) acc[a][r] = 0ull;
-  const int64_t G = keyed_sweep_tiles(n);
   // this part's tiles: g = part, part + parts, ...
   const int64_t my_tiles = G > part ? (G - part + parts - 1) / parts : 0;
   auto add_rec = [&](uint64_t rec) {
@@ -708,7 +719,7 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
     const int ch = (int)min((int64_t)KB_GA_CH, my_tiles - c0);
     __syncthreads();  // the previous chunk's table entries are consumed
     for (int i = tid; i < ch; i += KB_GA_THREADS) {
-      const int64_t g = (int64_t)part + (c0 + i) * parts;
+      const int64_t g = (int64_t)part + (KCC_KB_GA_REV ? my_tiles - 1 - (c0 + i) : c0 + i) * parts;
       const uint32_t* row = tab + g * (nb + 1) + b;
       const uint32_t s0 = row[0], s1 = row[1];
       seg_off[i] = s0;
@@ -723,7 +734,8 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
       for (int u = 0; u < KB_GA_U; ++u) {
         const int i = i0 + u;
         const bool ok = i < ch;
-        const uint32_t g = (uint32_t)part + (uint32_t)(c0 + (ok ? i : 0)) * (uint32_t)parts;
+        const uint32_t gi = (uint32_t)(c0 + (ok ? i : 0));
+        const uint32_t g = (uint32_t)part + (KCC_KB_GA_REV ? (uint32_t)my_tiles - 1u - gi : gi) * (uint32_t)parts;
         len[u] = ok ? seg_len[i] : 0u;
         first[u] = g * (uint32_t)KB_SW_TILE + (ok ? seg_off[i] : 0u);
 #pragma unroll
@@ -810,7 +822,31 @@ int64_t keyed_tiles(int64_t n) {
 }
 int64_t keyed_buckets(int64_t n_keys) { return (n_keys + KB_ROWS - 1) / KB_ROWS; }
 bool keyed_bucketed(int64_t n_keys, int64_t n) {  // (record indices, padded tiles, < 2^32)
-  return n_keys > 0 && keyed_buckets(n_keys) <= KB_NB_MAX && n < ((int64_t)1 << 32) - KB_SW_TILE;
+  return n_keys > 0 && keyed_buckets(n_keys) <= KB_NB_MAX && n < ((int64_t)1 << 32) - KB_SW_TILE &&
+         keyed_sweep_tiles(n) * KB_SW_TILE < ((int64_t)1 << 32);
+}
+static int keyed_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, c = 0;
+    cus = hipGetDevice(&dev) == hipSuccess &&
+                  hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                  c > 0
+              ? c
+              : 256;
+  }
+  return cus;
+}
+int64_t keyed_sweep_tile(int64_t n) {
+  const int64_t cus = keyed_cus();
+  if (n <= KB_SW_TILE * cus) return KB_SW_TILE;
+  const int64_t rounds = (n + KB_SW_TILE * cus - 1) / (KB_SW_TILE * cus);
+  const int64_t t = (n + rounds * cus - 1) / (rounds * cus);
+  return (t + 3) / 4 * 4;  // (quads: 16-B loads; <= KB_SW_TILE, a multiple of 4)
+}
+int64_t keyed_sweep_tiles(int64_t n) {
+  const int64_t t = keyed_sweep_tile(n);
+  return n > 0 ? (n + t - 1) / t : 0;
 }
 
 #ifndef KCC_KB_GA_PARTS
@@ -846,13 +882,14 @@ template <int NA>
 static hipError_t run_sweep(int64_t n_keys, int64_t n, const int32_t* key, const uint64_t* const* in,
                             uint64_t* const* out, const KeyedWork& kw, hipStream_t s) {
   const int nb = (int)keyed_buckets(n_keys);
-  const int64_t G = keyed_sweep_tiles(n);
+  const int64_t G = keyed_sweep_tiles(n), tile = keyed_sweep_tile(n);
   const int parts = keyed_sweep_parts(nb);
   if (G > 0x7fffffff || (int64_t)nb * parts > 0x7fffffff) return hipErrorInvalidValue;
   if (G > 0)
     hipLaunchKernelGGL(kb_sweep<NA>, dim3((unsigned)G), dim3(KB_SW_THREADS), 0, s, n, n_keys, key,
-                       in[0], in[1], nb, kw.counts, kw.sr, kw.esc_n, kw.esc_row, kw.esc_cpu, kw.esc_mem);
-  hipLaunchKernelGGL(kb_gather<NA>, dim3((unsigned)(nb * parts)), dim3(KB_GA_THREADS), 0, s, n, n_keys,
+                       in[0], in[1], nb, kw.counts, kw.sr, kw.esc_n, kw.esc_row, kw.esc_cpu, kw.esc_mem,
+                       tile);
+  hipLaunchKernelGGL(kb_gather<NA>, dim3((unsigned)(nb * parts)), dim3(KB_GA_THREADS), 0, s, G, n_keys,
                      nb, parts, kw.counts, kw.sr, kw.part_acc, kw.arrive, out[0], out[1]);
   if (NA >= 2 && n > 0)  // (few workgroups: each adds to one arrival counter; the list is short)
     hipLaunchKernelGGL(kb_escape, dim3(KB_ESC_WG), dim3(256), 0, s, kw.esc_n, kw.esc_row, kw.esc_cpu,
