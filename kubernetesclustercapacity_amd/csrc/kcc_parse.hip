@@ -34,6 +34,19 @@ constexpr int PC_BLOCK = PS_THREADS * PC_PER_THREAD;
 constexpr int PQ_PER_THREAD = KCC_PQ_PER_THREAD;      // parse_quantity_kernel: strings per lane
 constexpr int PQ_BLOCK = PS_THREADS * PQ_PER_THREAD;
 constexpr int PS_LDS_WORDS = 6144;                    // 24 KiB of staged characters
+#ifndef KCC_PARSE_NTST
+#define KCC_PARSE_NTST 1  // the register paths' value / status stores streaming (A/B knob)
+#endif
+// a parsed value and its status (written once, read by a later launch)
+__device__ __forceinline__ void put_parsed(int64_t* out, int8_t* status, int64_t i, int64_t v, int8_t st) {
+  if (KCC_PARSE_NTST) {
+    __builtin_nontemporal_store(v, out + i);
+    __builtin_nontemporal_store(st, status + i);
+  } else {
+    out[i] = v;
+    status[i] = st;
+  }
+}
 #ifndef KCC_PQ_V2
 #define KCC_PQ_V2 1  // parse_quantity_kernel's register path: 1 = qty_fast2, 0 = qty_fast (A/B)
 #endif
@@ -609,8 +622,7 @@ __global__ __launch_bounds__(PS_THREADS) void parse_cpu_kernel(int64_t n, const 
     }
     if (!done && sb[r] >= 0 && se[r] >= sb[r] && se[r] <= n_bytes && se[r] - sb[r] < ((int64_t)1 << 31))
       v = (int64_t)cpu_millis_value(bytes + sb[r], (int)(se[r] - sb[r]), st);
-    out[i] = v;
-    status[i] = st;
+    put_parsed(out, status, i, v, st);
   }
 }
 
@@ -876,8 +888,7 @@ __global__ __launch_bounds__(PS_THREADS) void parse_quantity_kernel(int64_t n, c
     if (!done) {
       need |= 1u << r;  // the offsets' checks and the general parser: below
     } else {
-      out[i] = v;
-      status[i] = st;
+      put_parsed(out, status, i, v, st);
     }
 #else
     if (fast[r])
