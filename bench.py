@@ -114,6 +114,9 @@ def parse():
                     help="1: the timed steps replay one step captured into a HIP graph "
                          "(torch.cuda.CUDAGraph on the bench stream; every kernel still runs "
                          "each step); not with --exchange torch")
+    ap.add_argument("--lib", default=None,
+                    help="diagnostic A/B: load this libkcc build (variants/libkcc_NAME.so) "
+                         "instead of the release library; the line names it")
     ap.add_argument("--drill-exchange-fallback", action="store_true",
                     help="test drill (N > 1): treat the p2p exchange's pre-timing check as failed "
                          "on the last rank, so every rank takes the RCCL fallback path")
@@ -258,7 +261,7 @@ def main():
     totals = torch.empty(S, dtype=torch.int64, device=dev)
     err = torch.empty(S, dtype=torch.int32, device=dev)
 
-    eng = CapacityEngine(local, 1)
+    eng = CapacityEngine(local, 1, lib_path=args.lib)
     eng.reserve(n, C, S)
     eng.set_clamp_in_fit(args.clamp_in_fit)
     stream = torch.cuda.Stream(dev)
@@ -603,6 +606,8 @@ def main():
     out["spec_errors"] = int(err.cpu().numpy().sum())
     if verified is not None:
         out["exchange_precheck"] = verified
+    if args.lib:
+        out["library"] = args.lib  # a diagnostic variant build, not the release library
     if world > 1 and exchange == "p2p":
         # again after the timed steps: the p2p exchange against the process group's
         # all-reduce of the same partials + the library's finalize (every rank), and the

@@ -66,6 +66,7 @@ struct Dev {
   // while the caller's stream fits chunk k-1
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr;
+  hipEvent_t ev_join = nullptr;  // KCC_CLAMP_CONCURRENT: the side stream's clamp correction done
   hipEvent_t ev_red[kcc::FIT_MAX_CHUNKS] = {};
   bool prof_on = false;
   std::vector<ProfPair> prof_pending;
@@ -627,6 +628,16 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     }
     if (k > 1) KCC_HIP(ctx, hipEventRecord(dv.ev_red[c], dv.side));
   }
+  // the clamp correction beside the fit (one chunk, clamp_apply mode): forked onto the side
+  // stream after node_prep, launched before the fit so its workgroups are resident first;
+  // with totals the last workgroup of either kernel finalizes (FinArgs::expect)
+  const bool conc = KCC_CLAMP_CONCURRENT && k == 1 && !nc && n_specs > 0 && n_nodes > 0;
+  const bool fuse_fin = totals && n_nodes > 0;
+  const kcc::FinArgs fin{as<int32_t>(dv.sperm), totals, spec_err, as<uint32_t>(dv.clamp_arrive),
+                         as<const unsigned long long>(dv.faults),
+                         conc ? (uint32_t)(kcc::clamp_apply_blocks(n_specs) +
+                                           kcc::fit_working_blocks(n_nodes, n_specs, n_nodes))
+                              : 0u};
   for (int c = 0; c < k; ++c) {
     if (k > 1) KCC_HIP(ctx, hipStreamWaitEvent(s, dv.ev_red[c], 0));  // also joins the side stream
     const int64_t n = hi[c] - lo[c];
@@ -643,6 +654,14 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                        place_here ? &pa : nullptr, fast_cl,
                                        as<uint32_t>(dv.fast_v) + lo[c] / kcc::FIT_GROUP));
     if (n == 0) continue;
+    if (conc) {  // fork: clamp_apply on the side stream, after node_prep
+      KCC_HIP(ctx, hipEventRecord(dv.ev_fork, s));
+      KCC_HIP(ctx, hipStreamWaitEvent(dv.side, dv.ev_fork, 0));
+      KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, n_nodes, clamp_of(dv),
+                                           as<unsigned long long>(dv.counters), partial, dv.side,
+                                           fuse_fin ? &fin : nullptr));
+      KCC_HIP(ctx, hipEventRecord(dv.ev_join, dv.side));
+    }
     ProfPair pp{};
     if (dv.prof_on) {
       KCC_HIP(ctx, prof_event(dv, &pp.a));
@@ -655,12 +674,20 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                  as<int64_t>(dv.slow_list) + lo[c], n_specs, spec_prep_of(dv),
                                  partial, as<unsigned long long>(dv.counters),
                                  as<uint32_t>(dv.fit_q), c, n_nodes, s, fast_cl,
-                                 as<uint32_t>(dv.fast_v) + lo[c] / kcc::FIT_GROUP, dv.prof_on));
+                                 as<uint32_t>(dv.fast_v) + lo[c] / kcc::FIT_GROUP, dv.prof_on,
+                                 conc && fuse_fin ? &fin : nullptr));
     if (dv.prof_on) {
       KCC_HIP(ctx, hipEventRecord(pp.b, s));
       pp.kind = 1;
       dv.prof_pending.push_back(pp);
     }
+  }
+  if (conc) {  // join: the call's work all ordered on s again
+    KCC_HIP(ctx, hipStreamWaitEvent(s, dv.ev_join, 0));
+    dv.clamp_dirty = false;
+    if (totals && !fuse_fin)
+      return fit_finalize_dev(ctx, dv, n_specs, partial, totals, spec_err, s);
+    return KCC_OK;
   }
   // the pod-slot clamp of every chunk's fast rows, added back per spec; totals != nullptr:
   // the clamp launch's last workgroup also finalizes (no fit_finalize launch)
@@ -670,10 +697,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     return KCC_OK;
   }
   if (n_specs > 0) {
-    const bool fuse_fin = totals && n_nodes > 0;
     // (clamp_arrive is allocated and zeroed by reserve_dev; every launch leaves it zero)
-    const kcc::FinArgs fin{as<int32_t>(dv.sperm), totals, spec_err, as<uint32_t>(dv.clamp_arrive),
-                           as<const unsigned long long>(dv.faults)};
     if (n_nodes > 0)
       KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, n_nodes, clamp_of(dv),
                                            as<unsigned long long>(dv.counters), partial, s,
@@ -869,7 +893,8 @@ int kcc_create(kcc_ctx** out, int first_device, int n_gpus) {
     if ((e = hipSetDevice(dv.device)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&dv.stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&dv.side, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&dv.ev_fork, hipEventDisableTiming)) != hipSuccess) {
+        (e = hipEventCreateWithFlags(&dv.ev_fork, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&dv.ev_join, hipEventDisableTiming)) != hipSuccess) {
       g_create_error = std::string("stream creation failed: ") + hipGetErrorString(e);
       kcc_destroy(ctx);
       return KCC_EHIP;
@@ -932,6 +957,7 @@ void kcc_destroy(kcc_ctx* ctx) {
       (void)hipStreamDestroy(dv.side);
     }
     if (dv.ev_fork) (void)hipEventDestroy(dv.ev_fork);
+    if (dv.ev_join) (void)hipEventDestroy(dv.ev_join);
     for (hipEvent_t ev : dv.ev_red)
       if (ev) (void)hipEventDestroy(ev);
     for (const ProfPair& pp : dv.prof_pending) {

@@ -351,10 +351,23 @@ struct FinArgs {
   int32_t* spec_err;
   uint32_t* arrive;
   const unsigned long long* faults;  // the device's fault words: set -> KCC_SPEC_FAULT
+  // arrivals the last workgroup waits for: 0 = the launch's own grid; the concurrent clamp
+  // correction counts the fit's working workgroups too (the last of either finalizes)
+  uint32_t expect;
 };
 hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
                               const unsigned long long* counters, int64_t* partial, hipStream_t s,
                               const FinArgs* fin = nullptr);
+int64_t clamp_apply_blocks(int64_t n_specs);  // clamp_apply_kernel's grid
+// the fit's working workgroups (gx x gy: the grid less its XCD padding)
+int64_t fit_working_blocks(int64_t n_nodes, int64_t n_specs, int64_t grid_nodes);
+// KCC_CLAMP_CONCURRENT: the clamp correction (clamp_apply, on the context's side stream)
+// runs beside the fit instead of after it — both only add into partial (wrapping atomics),
+// and neither reads what the other writes; with the fused finalize the last workgroup of
+// either kernel writes the totals
+#ifndef KCC_CLAMP_CONCURRENT
+#define KCC_CLAMP_CONCURRENT 1
+#endif
 
 // The fit's node stream (FitGroupA / FitGroup records) holds the rows that can contribute
 // to the fast sum Σ min(findMin(qc, qm), P): fast-bound rows with free CPU, free memory
@@ -394,7 +407,8 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, uint32_t* queue, int chunk,
                       int64_t grid_nodes, hipStream_t s, const int32_t* fast_cl = nullptr,
-                      const uint32_t* gvmin = nullptr, bool count_skips = false);
+                      const uint32_t* gvmin = nullptr, bool count_skips = false,
+                      const FinArgs* fin = nullptr);
 // the fit's work queues: fit_queue_words(S) uint32 (a 64-B line per spec column of 256 and
 // sub-queue), zero before the first launch (each launch leaves them zero)
 constexpr int64_t FIT_QSUBS_MAX = 32;

@@ -1932,6 +1932,46 @@ __device__ __forceinline__ void clamp_apply_bin(const ClampWork& cw, int64_t S,
   KCC_TL(1024 + blockIdx.x % 1024, 4);
 }
 
+// The fused finalize (clamp_apply_kernel, and the fit when the clamp correction runs beside
+// it): every wave's atomics into partial are performed (vmcnt counts the stores and atomics
+// too on gfx9) before the workgroup arrives; the last of the expected arrivals reads partial
+// at agent scope and writes the totals in caller order.  Every thread of the workgroup calls.
+__device__ void fused_finalize(const FinArgs& fin, int64_t S, const int64_t* partial) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ uint32_t last_s;
+  const uint32_t expect = fin.expect ? fin.expect : gridDim.x;
+  if (threadIdx.x == 0)
+    last_s = __hip_atomic_fetch_add(fin.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+             expect - 1u;
+  __syncthreads();
+  if (!last_s) return;
+  if (threadIdx.x == 0) __hip_atomic_store(fin.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool faulted = device_faulted(fin.faults);
+  // FIN_PER specs per thread per round, every load of the round issued before any store
+  // (one memory round trip per round: S <= 4 x the workgroup is one round)
+  constexpr int FIN_PER = 4;
+  const int64_t nt = blockDim.x;
+  for (int64_t i0 = threadIdx.x; i0 < S; i0 += (int64_t)FIN_PER * nt) {
+    int64_t t[FIN_PER], e[FIN_PER];
+    int32_t dst[FIN_PER];
+#pragma unroll
+    for (int k = 0; k < FIN_PER; ++k) {
+      // past the end: reload spec S-1 (branch-free, so no wait splits the batch)
+      const int64_t i = min(i0 + (int64_t)k * nt, S - 1);
+      t[k] = __hip_atomic_load(partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      e[k] = __hip_atomic_load(partial + S + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      dst[k] = fin.perm[i];
+    }
+#pragma unroll
+    for (int k = 0; k < FIN_PER; ++k) {
+      if (i0 + (int64_t)k * nt >= S) break;
+      fin.totals[dst[k]] = e[k] != 0 || faulted ? 0 : t[k];
+      fin.spec_err[dst[k]] = faulted ? SPEC_ERR_FAULT : e[k] != 0 ? SPEC_ERR_DIV0 : 0;
+    }
+  }
+}
+
 __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
                                                                  const unsigned long long* __restrict__ counters,
                                                                  int64_t S, int64_t* __restrict__ partial,
@@ -1943,41 +1983,7 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   const uint32_t G = gridDim.x / (uint32_t)(2 * Tm), h = blockIdx.x / (uint32_t)(2 * Tm);
   const int64_t u = blockIdx.x % (uint32_t)(2 * Tm);
   if (u < 2 * T) clamp_apply_bin(cw, S, partial, nN, u, G, h);  // (else: no bin)
-  if (!fin.totals) return;
-  // the fused finalize: every wave's atomics into partial are performed (vmcnt counts the
-  // stores and atomics too on gfx9) before the workgroup arrives; the last to arrive reads
-  // partial at agent scope
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  __shared__ uint32_t last_s;
-  if (threadIdx.x == 0)
-    last_s = __hip_atomic_fetch_add(fin.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-             gridDim.x - 1u;
-  __syncthreads();
-  if (!last_s) return;
-  if (threadIdx.x == 0) __hip_atomic_store(fin.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const bool faulted = device_faulted(fin.faults);
-  // FIN_PER specs per thread per round, every load of the round issued before any store
-  // (one memory round trip per round: S <= 4096 is one round)
-  constexpr int FIN_PER = 4;
-  for (int64_t i0 = threadIdx.x; i0 < S; i0 += (int64_t)FIN_PER * CP_THREADS) {
-    int64_t t[FIN_PER], e[FIN_PER];
-    int32_t dst[FIN_PER];
-#pragma unroll
-    for (int k = 0; k < FIN_PER; ++k) {
-      // past the end: reload spec S-1 (branch-free, so no wait splits the batch)
-      const int64_t i = min(i0 + (int64_t)k * CP_THREADS, S - 1);
-      t[k] = __hip_atomic_load(partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      e[k] = __hip_atomic_load(partial + S + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      dst[k] = fin.perm[i];
-    }
-#pragma unroll
-    for (int k = 0; k < FIN_PER; ++k) {
-      if (i0 + (int64_t)k * CP_THREADS >= S) break;
-      fin.totals[dst[k]] = e[k] != 0 || faulted ? 0 : t[k];
-      fin.spec_err[dst[k]] = faulted ? SPEC_ERR_FAULT : e[k] != 0 ? SPEC_ERR_DIV0 : 0;
-    }
-  }
+  if (fin.totals) fused_finalize(fin, S, partial);
 }
 
 // clamp_crows_kernel (only when C does not fit clamp_apply's full form): one wave per row
@@ -2137,7 +2143,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     const int64_t* __restrict__ slow_list, int64_t S, const SpecRec* __restrict__ specs,
     int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t chunk,
     int32_t gx, int32_t gy, const int32_t* __restrict__ fast_cl, const uint32_t* __restrict__ gvmin,
-    int32_t count_skips) {
+    int32_t count_skips, FinArgs fin) {
   // XCD-aware order (speed only, never correctness): workgroups are dealt round-robin
   // over the 8 XCDs, so give every spec group of one node chunk the same b % 8
   const int32_t b = blockIdx.x, xcd = b & 7, r = b >> 3;
@@ -2494,7 +2500,10 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     }
   }
   KCC_TL(2048 + b % 4096, 2);
-  if (idle) return;
+  if (idle) {  // (the fused finalize's arrival needs every wave at its barrier)
+    if (fin.totals) fused_finalize(fin, S, partial);
+    return;
+  }
   if (wave_exact) {  // exact-path specs: every node row (SlowNode), this workgroup's share
     const uint32_t nn = (uint32_t)n_nodes;  // < 2^28 per device
     const uint32_t pn = (nn + (uint32_t)gy - 1u) / (uint32_t)gy;
@@ -2528,6 +2537,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   }
 #endif
   KCC_TL(2048 + b % 4096, 3);
+  if (fin.totals) fused_finalize(fin, S, partial);  // (the clamp correction beside the fit)
 }
 
 __global__ void fit_finalize_kernel(int64_t S, const int64_t* __restrict__ partial,
@@ -2817,16 +2827,22 @@ hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
   // part subtracts its own share), as many as one round of resident workgroups holds
   // (C4: 1 per CU by registers, G = 2; more parts in a second round, G = 4 / 8: +7 / +24 us;
   // 64 VGPRs for 2 per CU and G = 4: equal)
+  const FinArgs f = fin ? *fin : FinArgs{};
+  hipLaunchKernelGGL(clamp_apply_kernel, dim3((unsigned)clamp_apply_blocks(n_specs)), dim3(CP_THREADS),
+                     0, s, cw, counters, n_specs, partial, f);
+  return hipGetLastError();
+}
+
+int64_t clamp_apply_blocks(int64_t n_specs) {
+  if (n_specs <= 0) return 0;
+  const int64_t T = (n_specs + 63) / 64;
   static std::atomic<int64_t> cache[MAX_DEVS];  // clamp_apply workgroups resident at once
   const int64_t resident = resident_blocks(cache, reinterpret_cast<const void*>(clamp_apply_kernel),
                                            CP_THREADS, 0, 256);
   int64_t G = 1;
   if (clamp_binned(n_specs))
     while (G < KCC_CP_SPLIT && 2 * T * G * 2 <= resident) G *= 2;
-  const FinArgs f = fin ? *fin : FinArgs{};
-  hipLaunchKernelGGL(clamp_apply_kernel, dim3((unsigned)(2 * T * G)), dim3(CP_THREADS), 0, s, cw,
-                     counters, n_specs, partial, f);
-  return hipGetLastError();
+  return 2 * T * G;
 }
 
 int64_t fit_resident_blocks() {  // 256-thread fit workgroups resident on the device at once
@@ -2834,24 +2850,35 @@ int64_t fit_resident_blocks() {  // 256-thread fit workgroups resident on the de
   return resident_blocks(cache, reinterpret_cast<const void*>(fit_kernel<false>), 256, 0, 2048);
 }
 
-hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,
-                      const SlowNode* slow,
-                      const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
-                      unsigned long long* counters, uint32_t* queue, int chunk,
-                      int64_t grid_nodes, hipStream_t s, const int32_t* fast_cl,
-                      const uint32_t* gvmin, bool count_skips) {
-  if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
+// the fit's workgroups per spec column: one round of resident workgroups (the queue
+// balances the waves; the stream's length is only known on the device); a chunk of a
+// pipelined call gets its node share of the round; no more waves per column than claims
+// at the full length
+static int64_t fit_grid_y(int64_t n_nodes, int64_t n_specs, int64_t grid_nodes) {
   const int64_t gx = (n_specs + FIT_SPW - 1) / FIT_SPW;
   const int64_t n_groups = fit_groups(n_nodes);
-  // one round of resident workgroups (the queue balances the waves; the stream's length
-  // is only known on the device); a chunk of a pipelined call gets its node share of the
-  // round; no more waves per column than claims at the full length
   int64_t gy = KCC_FIT_ROUNDS * fit_resident_blocks() / gx / KCC_FIT_GY_DIV;
   if (grid_nodes > n_nodes) gy = gy * n_nodes / grid_nodes;
   if (gy >= 16) gy = gy / 8 * 8;  // whole XCD rounds
   const int64_t claims = (n_groups + FIT_QCHUNK - 1) / FIT_QCHUNK;
   if (gy > claims) gy = claims;
   if (gy < 1) gy = 1;
+  return gy;
+}
+int64_t fit_working_blocks(int64_t n_nodes, int64_t n_specs, int64_t grid_nodes) {
+  if (n_nodes <= 0 || n_specs <= 0) return 0;
+  return (n_specs + FIT_SPW - 1) / FIT_SPW * fit_grid_y(n_nodes, n_specs, grid_nodes);
+}
+
+hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,
+                      const SlowNode* slow,
+                      const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
+                      unsigned long long* counters, uint32_t* queue, int chunk,
+                      int64_t grid_nodes, hipStream_t s, const int32_t* fast_cl,
+                      const uint32_t* gvmin, bool count_skips, const FinArgs* fin) {
+  if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
+  const int64_t gx = (n_specs + FIT_SPW - 1) / FIT_SPW;
+  const int64_t gy = fit_grid_y(n_nodes, n_specs, grid_nodes);
   // 1-D grid of gx * roundup(gy, 8) workgroups, remapped XCD-aware in the kernel
   const int64_t blocks = gx * ((gy + 7) / 8 * 8);
   if (blocks > 0x7fffffffLL || gy > 0x7fffffffLL) return hipErrorInvalidValue;
@@ -2859,7 +2886,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, queue, fast_a,
                      fast_b, slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)chunk,
                      (int32_t)gx, (int32_t)gy, fast_cl, KCC_FIT_MSKIP ? gvmin : nullptr,
-                     (int32_t)(count_skips ? 1 : 0));
+                     (int32_t)(count_skips ? 1 : 0), fin ? *fin : FinArgs{});
   return hipGetLastError();
 }
 
