@@ -654,14 +654,18 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                        place_here ? &pa : nullptr, fast_cl,
                                        as<uint32_t>(dv.fast_v) + lo[c] / kcc::FIT_GROUP));
     if (n == 0) continue;
-    if (conc) {  // fork: clamp_apply on the side stream, after node_prep
-      KCC_HIP(ctx, hipEventRecord(dv.ev_fork, s));
+    // fork: clamp_apply on the side stream, after node_prep; KCC_CLAMP_CONCURRENT 1 queues
+    // it before the fit (its workgroups resident first), 2 after (it fills the fit's tail)
+    auto fork_clamp = [&]() -> int {
       KCC_HIP(ctx, hipStreamWaitEvent(dv.side, dv.ev_fork, 0));
       KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, n_nodes, clamp_of(dv),
                                            as<unsigned long long>(dv.counters), partial, dv.side,
                                            fuse_fin ? &fin : nullptr));
       KCC_HIP(ctx, hipEventRecord(dv.ev_join, dv.side));
-    }
+      return KCC_OK;
+    };
+    if (conc) KCC_HIP(ctx, hipEventRecord(dv.ev_fork, s));
+    if (conc && KCC_CLAMP_CONCURRENT == 1 && (rc = fork_clamp())) return rc;
     ProfPair pp{};
     if (dv.prof_on) {
       KCC_HIP(ctx, prof_event(dv, &pp.a));
@@ -681,6 +685,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
       pp.kind = 1;
       dv.prof_pending.push_back(pp);
     }
+    if (conc && KCC_CLAMP_CONCURRENT == 2 && (rc = fork_clamp())) return rc;
   }
   if (conc) {  // join: the call's work all ordered on s again
     KCC_HIP(ctx, hipStreamWaitEvent(s, dv.ev_join, 0));
