@@ -381,3 +381,97 @@ def test_gpu_quantity_fast_path(eng):
         gv, gs = eng.quantity_value(batch)
         for s, v, st in zip(batch[1:], gv[1:], gs[1:]):
             assert (int(v), int(st)) == qm.value(s), (shift, s)
+
+
+def _qty_class(ch):
+    """kcc_parse.hip qty_class: bit 7 digit, bits 0-2 k M G T P E, bits 3-5 K M G T P E, bit 6 'i'."""
+    if 48 <= ch <= 57:
+        return 0x80
+    return {ord("i"): 0x40, ord("k"): 1, ord("K"): 1 << 3, ord("M"): 2 | 2 << 3,
+            ord("G"): 3 | 3 << 3, ord("T"): 4 | 4 << 3, ord("P"): 5 | 5 << 3,
+            ord("E"): 6 | 6 << 3}.get(ch, 0)
+
+
+def qty_fast2_model(s: bytes, tail: bytes):
+    """Bit-level restatement of the kernel's register path (kcc_parse.hip qty_fast2) on the
+    16 bytes a lane holds (the string, then `tail`: whatever follows it in the buffer):
+    -> (accepted, value, status).  Rejected strings go to the general parser."""
+    M64, MAXV = (1 << 64) - 1, (1 << 63) - 1
+    L = len(s)
+    A = int.from_bytes((s + tail)[:16].ljust(16, b"\0"), "little")
+    a = [(A >> (32 * j)) & 0xffffffff for j in range(4)]
+    p = L - 2 if L >= 2 else 0
+    pair = (A >> (8 * p)) & 0xffff
+    z = (pair >> 8) & 0xff if L >= 2 else pair & 0xff
+    y = pair & 0xff if L >= 2 else 0
+    zc, yc = _qty_class(z), _qty_class(y)
+    binary = bool(zc & 0x40) and bool(yc & 0x38)
+    zd = zc & 7
+    dec = not binary and zd != 0
+    dig = bool(zc & 0x80)
+    d = L - (2 if binary else (1 if dec else 0))
+    ZZ = 0x3030303030303030
+    l64, h64 = ((a[1] << 32) | a[0]) ^ ZZ, ((a[3] << 32) | a[2]) ^ ZZ
+    sh = (128 - 8 * d) & 0xffffffff  # v_lshlrev_b64 takes the low 6 bits of the amount
+    xl = (l64 << (sh & 63)) & M64
+    big = sh >= 64
+    th = xl if big else (((h64 << (sh & 63)) & M64) | (l64 >> ((64 - sh) & 63)))
+    tl = 0 if big else xl
+    t = [tl & 0xffffffff, tl >> 32, th & 0xffffffff, th >> 32]
+    bad = 0
+    for x in t:
+        bad |= ((x + 0x76767676) & 0xffffffff) | x
+    bad &= 0x80808080
+
+    def dot4(x, w):  # v_dot4_u32_u8
+        return sum(((x >> (8 * i)) & 0xff) * ((w >> (8 * i)) & 0xff) for i in range(4))
+
+    def quad(x):
+        return dot4(x, 0x010a0000) + 100 * dot4(x, 0x0000010a)
+
+    q01 = quad(t[0]) * 10000 + quad(t[1])
+    q23 = quad(t[2]) * 10000 + quad(t[3])
+    D = (q01 * 100000000 + q23) & M64
+    ok = (binary or dec or dig) and d >= 1 and bad == 0
+    bexp = 10 * ((yc >> 3) & 7) if binary else 0
+    mag = MAXV if D > (MAXV >> bexp) else (D << bexp) & M64
+    st = qm.OK
+    if dec:
+        p10 = 1000 ** zd
+        over = D > MAXV // p10
+        mag, st = (0, qm.UNSUP) if over else ((D * p10) & M64, qm.OK)
+    return ok, mag, st
+
+
+def test_qty_fast2_model_equals_quantity_model():
+    """The register path's arithmetic (one 128-bit shift right-aligning the digits, dot4
+    quads, the class table) against the exact-rational Quantity model, on every string it
+    accepts: 1-13 digits x every suffix x near-misses, random neighbouring bytes after the
+    string (they must never change a result)."""
+    rng = np.random.default_rng(41)
+    sufs = ["", "k", "M", "G", "T", "P", "E", "Ki", "Mi", "Gi", "Ti", "Pi", "Ei",
+            "K", "m", "i", "ki", "x", "e3", ".5", "Mi0"]
+    accepted = 0
+    for _ in range(40000):
+        nd = int(rng.integers(0, 14))
+        digs = "".join(str(int(x)) for x in rng.integers(0, 10, nd))
+        if nd and rng.random() < 0.05:  # a stray character inside the digits
+            k = int(rng.integers(0, nd))
+            digs = digs[:k] + "a:/+-. "[int(rng.integers(0, 7))] + digs[k + 1:]
+        s = (digs + sufs[int(rng.integers(0, len(sufs)))]).encode()
+        if not 1 <= len(s) <= 13:
+            continue
+        tail = bytes(rng.integers(0, 256, 16 - len(s), dtype=np.uint8))
+        ok, v, st = qty_fast2_model(s, tail)
+        if not ok:
+            continue
+        accepted += 1
+        want = qm.value(s.decode())
+        assert ((v - (1 << 64)) if v >> 63 else v, st) == want, s
+    assert accepted > 15000
+    # the cap boundaries and the longest accepted forms
+    for s in ["8191Pi", "8192Pi", "7Ei", "8Ei", "9223372036854", "9223372E", "9223373T",
+              "1234567890123", "12345678901Ki", "0Ki", "0E", "1"]:  # (<= 13 characters)
+        ok, v, st = qty_fast2_model(s.encode(), b"9" * 16)
+        assert ok, s
+        assert ((v - (1 << 64)) if v >> 63 else v, st) == qm.value(s), s
