@@ -258,3 +258,24 @@ def test_fit_claim_result_untouched_until_drained(asm):
         else:
             raise AssertionError(f"no s_waitcnt vmcnt(0) after `{ln}`")
     assert found >= 4  # the first claim and the loop's, in both instantiations
+
+
+def test_reduce_lookback_tagged_words(asm):
+    """The reduce's look-back (KCC_RED_LB_MODE 2): each 32-bit half of a
+    carried sum travels in its own 64-bit word under a tag in the high half, so a word is
+    complete when its tag is there — no ready flag, no fence. Pinned: the poll loop (the one
+    with s_sleep) reads the 2 x NA = 4 words as single 64-bit agent-coherent loads
+    (global_load_dwordx2 ... sc1, never split into dwords); the publish and the
+    clean-on-consume are 64-bit sc1 stores; the kernel has no cache invalidate / write-back
+    (the acquire / release variant, KCC_RED_LB_MODE 1, measured 2.3x slower)."""
+    body = kernel_body(asm, "reduce_kernelILi2E")
+    i = body.index("s_sleep")
+    loop = body[body.rfind(".LBB", 0, i):i]
+    loads = [ln.strip() for ln in loop.splitlines()
+             if "load" in ln and not ln.strip().startswith(";")]
+    assert len(loads) == 4, loads
+    assert all(ln.startswith("global_load_dwordx2") and ln.endswith("sc1") for ln in loads), loads
+    assert "buffer_inv" not in body and "buffer_wbl2" not in body
+    stores = [ln.strip() for ln in body.splitlines()
+              if ln.strip().startswith("global_store_dwordx2") and ln.strip().endswith("sc1")]
+    assert len(stores) >= 5, stores  # one publish + the four frees
