@@ -269,10 +269,16 @@ def test_reduce_lookback_tagged_words(asm):
     clean-on-consume are 64-bit sc1 stores; the kernel has no cache invalidate / write-back
     (the acquire / release variant, KCC_RED_LB_MODE 1, measured 2.3x slower)."""
     body = kernel_body(asm, "reduce_kernelILi2E")
-    i = body.index("s_sleep")
-    loop = body[body.rfind(".LBB", 0, i):i]
-    loads = [ln.strip() for ln in loop.splitlines()
-             if "load" in ln and not ln.strip().startswith(";")]
+    polls = []
+    labels = [m.start() for m in re.finditer(r"^\.LBB\w+:", body, re.M)]
+    for m in re.finditer("s_sleep", body):  # (the fused spec ranks wait too)
+        loop = body[max(x for x in labels if x < m.start()):m.start()]
+        loads = [ln.strip() for ln in loop.splitlines()
+                 if "load" in ln and not ln.strip().startswith(";")]
+        if any("dwordx2" in ln for ln in loads):
+            polls.append(loads)
+    assert len(polls) == 1, polls
+    (loads,) = polls
     assert len(loads) == 4, loads
     assert all(ln.startswith("global_load_dwordx2") and ln.endswith("sc1") for ln in loads), loads
     assert "buffer_inv" not in body and "buffer_wbl2" not in body
