@@ -114,6 +114,10 @@ def parse():
                     help="1: the timed steps replay one step captured into a HIP graph "
                          "(torch.cuda.CUDAGraph on the bench stream; every kernel still runs "
                          "each step); not with --exchange torch")
+    ap.add_argument("--prewarm-ms", type=float, default=0.0,
+                    help="diagnostic: this many ms of a dummy GPU load (not the step) before "
+                         "the warmup steps, to see whether the GPU's clock ramp reaches into "
+                         "the timed steps")
     ap.add_argument("--lib", default=None,
                     help="diagnostic A/B: load this libkcc build (variants/libkcc_NAME.so) "
                          "instead of the release library; the line names it")
@@ -372,6 +376,13 @@ def main():
         return int(flag.item()) == 1
 
     verified = None
+    if args.prewarm_ms > 0:  # (diagnostic, off by default: not the step, never timed)
+        x = torch.empty(64 << 20, dtype=torch.float32, device=dev)
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < args.prewarm_ms:
+            x.mul_(1.0001)
+            torch.cuda.synchronize()
+        del x
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
             step()
@@ -608,6 +619,8 @@ def main():
         out["exchange_precheck"] = verified
     if args.lib:
         out["library"] = args.lib  # a diagnostic variant build, not the release library
+    if args.prewarm_ms > 0:
+        out["prewarm_ms"] = args.prewarm_ms  # diagnostic
     if world > 1 and exchange == "p2p":
         # again after the timed steps: the p2p exchange against the process group's
         # all-reduce of the same partials + the library's finalize (every rank), and the
@@ -673,6 +686,20 @@ def main():
         dist.destroy_process_group()
 
 
+def side_warmup(run, warmup, min_s=0.1):
+    """Untimed warm-up of a leg measured beside the step: `warmup` calls, and more until
+    min_s seconds of them have run.  The legs start after seconds of host-only work (the
+    cluster's generation, the CPU baseline, string formatting) with the GPU idle, and three
+    calls of a few hundred microseconds do not bring its clocks back: the same builds timed
+    back to back in scripts/ab_variants.py ran 8-15 % faster."""
+    import torch
+    t0, i = time.perf_counter(), 0
+    while i < warmup or time.perf_counter() - t0 < min_s:
+        run()
+        i += 1
+        torch.cuda.synchronize()
+
+
 def keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream, steps, warmup,
               with_traffic=True):
     """SURVEY §8f row 1, measured beside the step (not part of `value`): the C4 containers
@@ -696,8 +723,8 @@ def keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream, steps, war
     om = torch.empty(n, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()  # the inputs above were made on torch's current stream
     with torch.cuda.stream(stream):
-        for _ in range(warmup):
-            eng.reduce_requests_keyed_async(n, key, kc, km, oc, om, stream=stream)
+        side_warmup(lambda: eng.reduce_requests_keyed_async(n, key, kc, km, oc, om, stream=stream),
+                    warmup)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         ev0.record(stream)
@@ -769,8 +796,7 @@ def pods_leg(eng, ptr, cpu, mem, n, dev, stream, steps, warmup):
     with torch.cuda.stream(stream):
         run = lambda: eng.pod_requests_async(pod_ptr, cpu, mem, pc, pm, init_ptr, init_cpu,
                                              init_mem, rst, ovh_cpu, ovh_mem, stream=stream)
-        for _ in range(warmup):
-            run()
+        side_warmup(run, warmup)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         ev0.record(stream)
@@ -824,8 +850,8 @@ def parse_leg(eng, cl, dev, stream, steps, warmup, with_cpu):
     d_st = torch.empty(n, dtype=torch.int8, device=dev)
     torch.cuda.synchronize()  # the copies above ran on torch's current stream
     with torch.cuda.stream(stream):
-        for _ in range(warmup):
-            eng.parse_cpu_millis_async(d_buf, d_off, d_out, d_st, stream=stream)
+        side_warmup(lambda: eng.parse_cpu_millis_async(d_buf, d_off, d_out, d_st, stream=stream),
+                    warmup)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         ev0.record(stream)
@@ -885,8 +911,8 @@ def quantity_leg(eng, cl, dev, stream, steps, warmup):
     d_st = torch.empty(n, dtype=torch.int8, device=dev)
     torch.cuda.synchronize()
     with torch.cuda.stream(stream):
-        for _ in range(warmup):
-            eng.parse_quantity_async(d_buf, d_off, d_out, d_st, stream=stream)
+        side_warmup(lambda: eng.parse_quantity_async(d_buf, d_off, d_out, d_st, stream=stream),
+                    warmup)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         ev0.record(stream)
