@@ -114,10 +114,6 @@ def parse():
                     help="1: the timed steps replay one step captured into a HIP graph "
                          "(torch.cuda.CUDAGraph on the bench stream; every kernel still runs "
                          "each step); not with --exchange torch")
-    ap.add_argument("--prewarm-ms", type=float, default=0.0,
-                    help="diagnostic: this many ms of a dummy GPU load (not the step) before "
-                         "the warmup steps, to see whether the GPU's clock ramp reaches into "
-                         "the timed steps")
     ap.add_argument("--lib", default=None,
                     help="diagnostic A/B: load this libkcc build (variants/libkcc_NAME.so) "
                          "instead of the release library; the line names it")
@@ -376,13 +372,6 @@ def main():
         return int(flag.item()) == 1
 
     verified = None
-    if args.prewarm_ms > 0:  # (diagnostic, off by default: not the step, never timed)
-        x = torch.empty(64 << 20, dtype=torch.float32, device=dev)
-        t0 = time.perf_counter()
-        while (time.perf_counter() - t0) * 1e3 < args.prewarm_ms:
-            x.mul_(1.0001)
-            torch.cuda.synchronize()
-        del x
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
             step()
@@ -619,8 +608,6 @@ def main():
         out["exchange_precheck"] = verified
     if args.lib:
         out["library"] = args.lib  # a diagnostic variant build, not the release library
-    if args.prewarm_ms > 0:
-        out["prewarm_ms"] = args.prewarm_ms  # diagnostic
     if world > 1 and exchange == "p2p":
         # again after the timed steps: the p2p exchange against the process group's
         # all-reduce of the same partials + the library's finalize (every rank), and the
