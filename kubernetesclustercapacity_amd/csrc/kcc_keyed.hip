@@ -798,19 +798,23 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
 
 }  // namespace
 
+static int keyed_cus() {  // (thread-safe once: a function-local static's initializer)
+  static const int cus = [] {
+    int dev = 0, c = 0;
+    return hipGetDevice(&dev) == hipSuccess &&
+                   hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                   c > 0
+               ? c
+               : 256;
+  }();
+  return cus;
+}
+
 // Containers per scatter workgroup: about KB_TILE, cut so the tiles make whole rounds of
 // one workgroup per CU (the scatter's LDS and registers hold one per CU): 1209 tiles of
 // 32768 at C4 were 4.7 rounds, the last one 70 % full.
 int64_t keyed_tile(int64_t n) {
-  static int64_t cus = 0;
-  if (cus == 0) {
-    int dev = 0, c = 0;
-    cus = hipGetDevice(&dev) == hipSuccess &&
-                  hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-                  c > 0
-              ? c
-              : 256;
-  }
+  const int64_t cus = keyed_cus();
   if (n <= 0) return KB_TILE;
   const int64_t rounds = (n + KB_TILE * cus - 1) / (KB_TILE * cus);
   const int64_t t = (n + rounds * cus - 1) / (rounds * cus);
@@ -824,18 +828,6 @@ int64_t keyed_buckets(int64_t n_keys) { return (n_keys + KB_ROWS - 1) / KB_ROWS;
 bool keyed_bucketed(int64_t n_keys, int64_t n) {  // (record indices, padded tiles, < 2^32)
   return n_keys > 0 && keyed_buckets(n_keys) <= KB_NB_MAX && n < ((int64_t)1 << 32) - KB_SW_TILE &&
          keyed_sweep_tiles(n) * KB_SW_TILE < ((int64_t)1 << 32);
-}
-static int keyed_cus() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0, c = 0;
-    cus = hipGetDevice(&dev) == hipSuccess &&
-                  hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-                  c > 0
-              ? c
-              : 256;
-  }
-  return cus;
 }
 int64_t keyed_sweep_tile(int64_t n) {
   const int64_t cus = keyed_cus();
