@@ -367,6 +367,11 @@ int64_t fit_working_blocks(int64_t n_nodes, int64_t n_specs, int64_t grid_nodes)
 // either kernel writes the totals.  0 = after the fit (default: measured faster), 1 = queued
 // before the fit (C4 step 0.302 -> 0.333 ms: the 1024-lane clamp workgroups and the fit
 // slow each other), 2 = queued after the fit on the side stream
+// the spec ranks' workgroups of a fused reduce launch go behind the reduce's workgroups
+// (1) or in front of them (0)
+#ifndef KCC_RED_RANKS_LAST
+#define KCC_RED_RANKS_LAST 1
+#endif
 #ifndef KCC_CLAMP_CONCURRENT
 #define KCC_CLAMP_CONCURRENT 0
 #endif

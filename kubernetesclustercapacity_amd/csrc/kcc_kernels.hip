@@ -260,9 +260,13 @@ template <int NA>
 __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
   __shared__ __attribute__((aligned(16))) uint64_t pre_s[RED_WAVES_PER_BLOCK][NA][RED_TILE];
   static_assert(sizeof(pre_s) >= 16 * RANK_L, "the rank workgroups stage RANK_L 16-B keys");
+  // the spec ranks' workgroups: behind the reduce's (KCC_RED_RANKS_LAST; dispatched as its
+  // first waves retire, they run in the reduce's tail) or in front of them
+  const int32_t rank0 = KCC_RED_RANKS_LAST ? (int32_t)gridDim.x - ra.n_blocks : 0;  // first rank block
+  const int32_t red0 = KCC_RED_RANKS_LAST ? 0 : ra.n_blocks;                        // first reduce block
   if constexpr (NA == 2) {  // (launch_reduce: the ranks ride the 2-array reduce only)
-    if ((int32_t)blockIdx.x < ra.n_blocks) {  // the spec ranks' workgroups, in front
-      spec_rank_body(ra, blockIdx.x, &pre_s[0][0][0]);
+    if (ra.n_blocks > 0 && (int32_t)blockIdx.x >= rank0 && (int32_t)blockIdx.x < rank0 + ra.n_blocks) {
+      spec_rank_body(ra, (int32_t)blockIdx.x - rank0, &pre_s[0][0][0]);
       return;
     }
   }
@@ -279,13 +283,13 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
   // predecessor may then be dispatched after it, so the waits are safe only while every
   // wave of the launch is resident at once, which kernels of another stream or process
   // sharing the GPU can prevent (dispatch order = range order rules that out)
-  const uint32_t rb_ = blockIdx.x - (uint32_t)ra.n_blocks, nb_ = gridDim.x - (uint32_t)ra.n_blocks;
+  const uint32_t rb_ = blockIdx.x - (uint32_t)red0, nb_ = gridDim.x - (uint32_t)ra.n_blocks;
   const uint32_t xq_ = rb_ & 7u, q8_ = nb_ >> 3, r8_ = nb_ & 7u;
   const uint32_t lb_ = xq_ * q8_ + (xq_ < r8_ ? xq_ : r8_) + (rb_ >> 3);
   const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)(lb_ * RED_WAVES_PER_BLOCK +
                                                              (threadIdx.x >> 6)));
 #else
-  const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)((blockIdx.x - ra.n_blocks) *
+  const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)((blockIdx.x - red0) *
                                                              RED_WAVES_PER_BLOCK +
                                                              (threadIdx.x >> 6)));
 #endif
@@ -293,7 +297,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
   // are local to the launch)
   const int64_t wb = c0 + (int64_t)w * range;
   if (wb >= n_cont) return;  // wave-uniform; no block-level barrier in this kernel
-  KCC_TL(4096 + (blockIdx.x - ra.n_blocks) % 4096, 0);
+  KCC_TL(4096 + (blockIdx.x - red0) % 4096, 0);
   const int32_t len = (int32_t)(n_cont - wb < range ? n_cont - wb : range);
   __builtin_assume(len >= 1);  // (wb < n_cont: the tile loop runs, its first loads need no guard)
   uint64_t (*pre)[RED_TILE] = pre_s[threadIdx.x >> 6];
@@ -657,7 +661,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
       for (int k = 0; k < NA; ++k) out[k][node0] = acc[k];
     }
   }
-  KCC_TL(4096 + (blockIdx.x - ra.n_blocks) % 4096, 1);
+  KCC_TL(4096 + (blockIdx.x - red0) % 4096, 1);
 }
 
 // ----------------------------------------------------------------------------
@@ -2715,8 +2719,9 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
   }
   if (!red && ra.n_blocks == 0) return hipSuccess;
   if (limits && ra.n_blocks > 0) return hipErrorInvalidValue;  // (the ranks ride NA = 2 only)
-  // the rank workgroups go first: they hold their slots ~2 us, the reduce's range is
-  // sized for the whole device (its last waves start when the rank workgroups exit)
+  // the rank workgroups: behind the reduce's (KCC_RED_RANKS_LAST), so they take the slots
+  // of its first waves to finish; in front (0), they held their slots ~2 us while the
+  // reduce's range is sized for the whole device (its last waves started when they exited)
   const int32_t range = red ? reduce_range(n_containers, limits, 0) : RED_TILE;
   const int64_t waves = red ? (n_containers + range - 1) / range : 0;
   if (waves > reduce_tail_records()) return hipErrorInvalidValue;

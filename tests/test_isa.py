@@ -268,7 +268,8 @@ def test_reduce_lookback_tagged_words(asm):
     (global_load_dwordx2 ... sc1, never split into dwords); the publish and the
     clean-on-consume are 64-bit sc1 stores; the kernel has no cache invalidate / write-back
     (the acquire / release variant, KCC_RED_LB_MODE 1, measured 2.3x slower)."""
-    body = kernel_body(asm, "reduce_kernelILi2E")
+    m = re.search(r"^(_ZN3kcc12_GLOBAL__N_1\d+reduce_kernelILi2E\w*):\s*;", asm, re.M)
+    body = asm[m.end():asm.index(".Lfunc_end", m.end())]  # the whole function (several exits)
     polls = []
     labels = [m.start() for m in re.finditer(r"^\.LBB\w+:", body, re.M)]
     for m in re.finditer("s_sleep", body):  # (the fused spec ranks wait too)
