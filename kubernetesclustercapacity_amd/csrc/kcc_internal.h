@@ -90,9 +90,13 @@ struct RedArgs {
   uint64_t* out[4];
   uint64_t* tail;                  // [reduce_tail_records()][RED_TAIL_WORDS], tags 0
   unsigned long long* faults;      // the device's fault words (FAULT_RED: look-back give-ups)
+  int32_t ranks_last;              // the spec ranks' workgroups behind the reduce's (else in front)
 };
 // rank != nullptr (with rank->n_blocks > 0): the spec ranks run as that many extra
-// workgroups in front of the reduce's (independent work, one launch fewer per step).
+// workgroups beside the reduce's (independent work, one launch fewer per step): behind them
+// on long reduces (>= KCC_RED_RANKS_LAST_MIN containers: they take the slots of the first
+// waves to finish; C4 step 0.3059 -> 0.3030 ms), in front on short ones (the 8-way C4 rank:
+// behind, they lengthened its 23 us reduce by 3 us).
 hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, const int64_t* node_ptr,
                          const uint64_t* cpu_req, const int64_t* mem_req,
                          const uint64_t* cpu_lim, const int64_t* mem_lim,
@@ -371,6 +375,9 @@ int64_t fit_working_blocks(int64_t n_nodes, int64_t n_specs, int64_t grid_nodes)
 // (1) or in front of them (0)
 #ifndef KCC_RED_RANKS_LAST
 #define KCC_RED_RANKS_LAST 1
+#endif
+#ifndef KCC_RED_RANKS_LAST_MIN
+#define KCC_RED_RANKS_LAST_MIN (16LL << 20)  // containers of the launch
 #endif
 #ifndef KCC_CLAMP_CONCURRENT
 #define KCC_CLAMP_CONCURRENT 0

@@ -260,10 +260,10 @@ template <int NA>
 __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
   __shared__ __attribute__((aligned(16))) uint64_t pre_s[RED_WAVES_PER_BLOCK][NA][RED_TILE];
   static_assert(sizeof(pre_s) >= 16 * RANK_L, "the rank workgroups stage RANK_L 16-B keys");
-  // the spec ranks' workgroups: behind the reduce's (KCC_RED_RANKS_LAST; dispatched as its
+  // the spec ranks' workgroups: behind the reduce's (RedArgs::ranks_last; dispatched as its
   // first waves retire, they run in the reduce's tail) or in front of them
-  const int32_t rank0 = KCC_RED_RANKS_LAST ? (int32_t)gridDim.x - ra.n_blocks : 0;  // first rank block
-  const int32_t red0 = KCC_RED_RANKS_LAST ? 0 : ra.n_blocks;                        // first reduce block
+  const int32_t rank0 = a.ranks_last ? (int32_t)gridDim.x - ra.n_blocks : 0;  // first rank block
+  const int32_t red0 = a.ranks_last ? 0 : ra.n_blocks;                        // first reduce block
   if constexpr (NA == 2) {  // (launch_reduce: the ranks ride the 2-array reduce only)
     if (ra.n_blocks > 0 && (int32_t)blockIdx.x >= rank0 && (int32_t)blockIdx.x < rank0 + ra.n_blocks) {
       spec_rank_body(ra, (int32_t)blockIdx.x - rank0, &pre_s[0][0][0]);
@@ -2743,6 +2743,7 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
   a.out[3] = limits ? reinterpret_cast<uint64_t*>(lim_mem) : nullptr;
   a.tail = tail;
   a.faults = faults;
+  a.ranks_last = KCC_RED_RANKS_LAST && n_containers >= KCC_RED_RANKS_LAST_MIN ? 1 : 0;
   if (limits)
     hipLaunchKernelGGL(reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, a, ra);
   else
