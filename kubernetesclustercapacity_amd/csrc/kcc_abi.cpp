@@ -628,9 +628,10 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     }
     if (k > 1) KCC_HIP(ctx, hipEventRecord(dv.ev_red[c], dv.side));
   }
-  // the clamp correction beside the fit (one chunk, clamp_apply mode): forked onto the side
-  // stream after node_prep, launched before the fit so its workgroups are resident first;
-  // with totals the last workgroup of either kernel finalizes (FinArgs::expect)
+  // KCC_CLAMP_CONCURRENT (A/B builds; off by default, measured slower — DESIGN.md §6): the
+  // clamp correction beside the fit (one chunk, clamp_apply mode), forked onto the side
+  // stream after node_prep; with totals the last workgroup of either kernel finalizes
+  // (FinArgs::expect)
   const bool conc = KCC_CLAMP_CONCURRENT && k == 1 && !nc && n_specs > 0 && n_nodes > 0;
   const bool fuse_fin = totals && n_nodes > 0;
   const kcc::FinArgs fin{as<int32_t>(dv.sperm), totals, spec_err, as<uint32_t>(dv.clamp_arrive),
