@@ -20,6 +20,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("name", nargs="?", default="tl")
 ap.add_argument("--config", default="C4")
 ap.add_argument("--shard", type=int, default=1)
+ap.add_argument("--pipeline", action="store_true",
+                help="time kcc_capacity_partial_async (the bench's step, incl. the clamp in the "
+                     "fit by size) instead of reduce + fit_prepare + fit_run")
 a = ap.parse_args()
 L = _lib.load(os.path.join(ROOT, "variants", f"libkcc_{a.name}.so"))
 L.kcc_debug_timeline.argtypes = [C.c_void_p]
@@ -43,6 +46,11 @@ buf = np.zeros((8192, 8), np.uint64)
 
 
 def step():
+    if a.pipeline:
+        assert L.kcc_capacity_partial_async(h, n, nc, None, P(ptr), P(cpu), P(mem), P(ac), P(am),
+                                            P(ap_), P(pc), P(uc), P(um), S, P(s_cpu), P(s_mem),
+                                            P(part), 1, None) == 0
+        return
     assert L.kcc_reduce_requests_async(h, n, nc, P(ptr), P(cpu), P(mem), None, None, P(uc), P(um),
                                        None, None, None) == 0
     assert L.kcc_fit_prepare_async(h, n, P(ac), P(am), P(ap_), P(pc), P(uc), P(um), S, P(s_cpu),
