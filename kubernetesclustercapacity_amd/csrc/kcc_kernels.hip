@@ -2176,6 +2176,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   const bool wave_exact = __any(sr.cls == SPEC_EXACT);
   const bool wave_b = __any(sr.cls == SPEC_B);
   const bool wave_fast = !wave_exact && !idle;  // sums the node stream
+  KCC_TL(2048 + b % 4096, 5);  // (the spec records are in)
   // KCC_FIT_MSKIP: the wave's largest memory request (class-A specs sit in memory order, so
   // this is the last active lane's) as u32; 0xffffffff: no skip (m >= 2^32, or no table)
   uint32_t mmax32 = 0xffffffffu;

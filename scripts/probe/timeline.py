@@ -91,8 +91,10 @@ show("node_prep phase 2 (+barrier)", npr, 3, 4)
 show("node_prep stream + records (+barrier)", npr, 4, 5)
 show("node_prep last pass -> end (C flush)", npr, 5, 1)
 show("node_prep whole", npr, 2, 1)
-fr = t[2048:6144]
+fr = t[2048:2048 + 2048]  # (the reduce's slots start at 4096)
 show("fit entry -> first claim", fr, 0, 1)
+show("  entry -> spec records in", fr, 0, 5)
+show("  spec records -> stream length", fr, 5, 1)
 show("fit loop", fr, 1, 2)
 show("fit slow rows + atomics", fr, 2, 3)
 show("fit whole", fr, 0, 3)
