@@ -99,7 +99,6 @@ struct Dev {
   bool last_nc = false;    // the last capacity call applied the clamp in the fit
   DevBuf fast_cl;          // the clamp in the fit: each streamed row's clamp value
   DevBuf fast_v;           // KCC_FIT_MSKIP: each stream group's smallest floor(fm / P) (u32)
-  DevBuf ng_copies;        // the fit streams' lengths, copied by node_prep (kcc::NG_WORDS u32)
   int stream_chunks = 0;   // node chunks of the last fit prepare (their stream counters)
   int64_t prep_nodes = -1, prep_specs = -1;  // sizes the workspace was last prepared for
   // staging of the host-array entry points
@@ -292,7 +291,6 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.fast_b, sizeof(kcc::FitGroup) * (size_t)kcc::fit_groups((int64_t)N)));
   KCC_HIP(ctx, ensure(dv.fast_cl, sizeof(int32_t) * kcc::FIT_GROUP * (size_t)kcc::fit_groups((int64_t)N)));
   KCC_HIP(ctx, ensure(dv.fast_v, sizeof(uint32_t) * (size_t)kcc::fit_groups((int64_t)N)));
-  KCC_HIP(ctx, ensure(dv.ng_copies, sizeof(uint32_t) * (size_t)kcc::NG_WORDS));
   KCC_HIP(ctx, ensure(dv.slow, sizeof(kcc::SlowNode) * N));
   KCC_HIP(ctx, ensure(dv.slow_list, sizeof(int64_t) * N));
   KCC_HIP(ctx, ensure(dv.srec, sizeof(kcc::SpecRec) * S));
@@ -441,8 +439,7 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
                                        as<kcc::FitGroup>(dv.fast_b), as<kcc::SlowNode>(dv.slow),
                                        as<int64_t>(dv.slow_list), n_specs, clamp_of(dv),
                                        as<unsigned long long>(dv.counters), 0, 0,
-                                       n_nodes, s, dv.fit_dense, &pa, nullptr, as<uint32_t>(dv.fast_v),
-                                       as<uint32_t>(dv.ng_copies)));
+                                       n_nodes, s, dv.fit_dense, &pa, nullptr, as<uint32_t>(dv.fast_v)));
   if (n_nodes == 0) {
     dv.clamp_dirty = false;
     return KCC_OK;
@@ -464,8 +461,7 @@ int fit_run_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_specs, int64_t
                                as<kcc::SlowNode>(dv.slow),
                                as<int64_t>(dv.slow_list), n_specs, spec_prep_of(dv), partial,
                                as<unsigned long long>(dv.counters), as<uint32_t>(dv.fit_q), 0,
-                               n_nodes, s, nullptr, as<uint32_t>(dv.fast_v), dv.prof_on, nullptr,
-                               as<uint32_t>(dv.ng_copies)));
+                               n_nodes, s, nullptr, as<uint32_t>(dv.fast_v), dv.prof_on));
   return KCC_OK;
 }
 
@@ -657,8 +653,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                        as<unsigned long long>(dv.counters),
                                        c, lo[c], n_nodes, s, dv.fit_dense,
                                        place_here ? &pa : nullptr, fast_cl,
-                                       as<uint32_t>(dv.fast_v) + lo[c] / kcc::FIT_GROUP,
-                                       as<uint32_t>(dv.ng_copies)));
+                                       as<uint32_t>(dv.fast_v) + lo[c] / kcc::FIT_GROUP));
     if (n == 0) continue;
     // fork: clamp_apply on the side stream, after node_prep; KCC_CLAMP_CONCURRENT 1 queues
     // it before the fit (its workgroups resident first), 2 after (it fills the fit's tail)
@@ -685,7 +680,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                  partial, as<unsigned long long>(dv.counters),
                                  as<uint32_t>(dv.fit_q), c, n_nodes, s, fast_cl,
                                  as<uint32_t>(dv.fast_v) + lo[c] / kcc::FIT_GROUP, dv.prof_on,
-                                 conc && fuse_fin ? &fin : nullptr, as<uint32_t>(dv.ng_copies)));
+                                 conc && fuse_fin ? &fin : nullptr));
     if (dv.prof_on) {
       KCC_HIP(ctx, hipEventRecord(pp.b, s));
       pp.kind = 1;
@@ -948,7 +943,7 @@ void kcc_destroy(kcc_ctx* ctx) {
     DevBuf* bufs[] = {&dv.c_rank, &dv.c_bcnt, &dv.c_cs, &dv.c_ms,
                       &dv.c_mrc, &dv.c_crm, &dv.c_dperm, &dv.c_C, &dv.c_H2, &dv.c_H3,
                       &dv.c_Crow, &dv.c_rec, &dv.c_dir,
-                      &dv.red_tail,  &dv.faults, &dv.rank_arrive, &dv.fast_v, &dv.ng_copies, &dv.fast_cl, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
+                      &dv.red_tail,  &dv.faults, &dv.rank_arrive, &dv.fast_v, &dv.fast_cl, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
                       &dv.sperm,     &dv.fit_q,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
                       &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,

@@ -328,8 +328,7 @@ enum {
   CNT_STREAM = 4 + FIT_MAX_CHUNKS,  // + chunk: node rows in that chunk's fit stream (x 8)
   CNT_FIT_MSKIP = 4 + 2 * FIT_MAX_CHUNKS,  // (node group, class-A wave) pairs the fit summed
                                            // without the memory quotient (every lane qm >= P)
-  CNT_NP_ARRIVE = 5 + 2 * FIT_MAX_CHUNKS,  // + chunk: node_prep workgroups finished
-  CNT_N = 5 + 3 * FIT_MAX_CHUNKS
+  CNT_N = 5 + 2 * FIT_MAX_CHUNKS
 };
 // The memory-bound skip (KCC_FIT_MSKIP): node_prep stores each stream group's smallest
 // V = floor(free memory / P) (saturated to u32) in gvmin[group]; spec_place orders the
@@ -380,15 +379,10 @@ int64_t fit_working_blocks(int64_t n_nodes, int64_t n_specs, int64_t grid_nodes)
 #ifndef KCC_RED_RANKS_LAST_MIN
 #define KCC_RED_RANKS_LAST_MIN (16LL << 20)  // containers of the launch
 #endif
-// The fit's stream length (node groups) in NG_COPIES copies, one per 128-B line, written by
-// node_prep's last workgroup: every fit wave reads it at launch, and 8192 reads of the one
-// counter word made the last workgroups start their loop up to 8 us after the first
-// (KCC_FIT_NG_SPREAD 0: the counter itself)
-#ifndef KCC_FIT_NG_SPREAD
-#define KCC_FIT_NG_SPREAD 1
+// the fit reads its stream's length once per workgroup (1) or once per wave (0)
+#ifndef KCC_FIT_NG_ONCE
+#define KCC_FIT_NG_ONCE 1
 #endif
-constexpr int NG_COPIES = 64, NG_STRIDE = 32;  // (u32 words)
-constexpr int64_t NG_WORDS = (int64_t)FIT_MAX_CHUNKS * NG_COPIES * NG_STRIDE;
 #ifndef KCC_CLAMP_CONCURRENT
 #define KCC_CLAMP_CONCURRENT 0
 #endif
@@ -411,7 +405,7 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             unsigned long long* counters, int chunk, int64_t row0,
                             int64_t call_nodes, hipStream_t s, bool dense = false,
                             const PlaceArgs* place = nullptr, int32_t* fast_cl = nullptr,
-                            uint32_t* gvmin = nullptr, uint32_t* ng_copies = nullptr);
+                            uint32_t* gvmin = nullptr);
 // Clamp in the fit (fast_cl != nullptr; one node chunk, S <= CLAMP_LDS_SPECS, not dense):
 // node_prep streams each row's clamp value (allocatable pods - pod count, CC:135) beside
 // its FitGroupA (fast_cl[row position]) and builds no clamp tables; the fit computes the
@@ -432,7 +426,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
                       unsigned long long* counters, uint32_t* queue, int chunk,
                       int64_t grid_nodes, hipStream_t s, const int32_t* fast_cl = nullptr,
                       const uint32_t* gvmin = nullptr, bool count_skips = false,
-                      const FinArgs* fin = nullptr, const uint32_t* ng_copies = nullptr);
+                      const FinArgs* fin = nullptr);
 // the fit's work queues: fit_queue_words(S) uint32 (a 64-B line per spec column of 256 and
 // sub-queue), zero before the first launch (each launch leaves them zero)
 constexpr int64_t FIT_QSUBS_MAX = 32;

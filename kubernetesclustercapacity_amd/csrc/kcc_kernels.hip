@@ -817,8 +817,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
                                  int64_t S, ClampWork cw,
                                  unsigned long long* __restrict__ counters,
                                  int32_t chunk, int32_t dense, int64_t pass0, PlaceArgs pa,
-                                 int32_t* __restrict__ fast_cl, uint32_t* __restrict__ gvmin,
-                                 uint32_t* __restrict__ ng_copies) {
+                                 int32_t* __restrict__ fast_cl, uint32_t* __restrict__ gvmin) {
   static_assert(!NC || MODE == 2, "the clamp in the fit: S <= CLAMP_LDS_SPECS only");
   if ((int32_t)blockIdx.x < pa.n_blocks) {  // spec_place's workgroups, in front (MODE 2)
     spec_place_body(pa, blockIdx.x);
@@ -1240,18 +1239,6 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
     for (int64_t e = threadIdx.x; e < W * W; e += KCC_NODE_PREP_BLOCK) {
       const unsigned long long v = c_l[e];
       if (v) np_atomic(&Cc[e], (int64_t)v);
-    }
-  }
-  // the last workgroup to finish copies the stream's length into NG_COPIES lines for the
-  // fit (every workgroup gets here; its stream reservations returned before its arrival)
-  if (KCC_FIT_NG_SPREAD && ng_copies) {
-    __syncthreads();
-    if (threadIdx.x == 0 &&
-        atomicAdd(&counters[CNT_NP_ARRIVE + chunk], 1ull) == (unsigned long long)(nbid - 1)) {
-      const unsigned long long rows =
-          __hip_atomic_load(&counters[CNT_STREAM + chunk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint32_t* cp = ng_copies + (int64_t)chunk * NG_COPIES * NG_STRIDE;
-      for (int k = 0; k < NG_COPIES; ++k) cp[k * NG_STRIDE] = (uint32_t)(rows / FIT_GROUP);
     }
   }
   KCC_TL(bid % 1024, 1);
@@ -2160,7 +2147,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     const int64_t* __restrict__ slow_list, int64_t S, const SpecRec* __restrict__ specs,
     int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t chunk,
     int32_t gx, int32_t gy, const int32_t* __restrict__ fast_cl, const uint32_t* __restrict__ gvmin,
-    int32_t count_skips, FinArgs fin, const uint32_t* __restrict__ ng_copies) {
+    int32_t count_skips, FinArgs fin) {
   // XCD-aware order (speed only, never correctness): workgroups are dealt round-robin
   // over the 8 XCDs, so give every spec group of one node chunk the same b % 8
   const int32_t b = blockIdx.x, xcd = b & 7, r = b >> 3;
@@ -2205,12 +2192,23 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   }
   uint32_t nskip = 0;  // node groups summed without the memory quotient (scalar)
 
-  // the node stream node_prep wrote (its length is on the device; 32-bit: < 2^31 groups),
-  // from one of node_prep's NG_COPIES copies (KCC_FIT_NG_SPREAD)
-  const uint32_t n_groups =
-      KCC_FIT_NG_SPREAD && ng_copies
-          ? ng_copies[(int64_t)chunk * NG_COPIES * NG_STRIDE + (b % NG_COPIES) * NG_STRIDE]
-          : (uint32_t)(counters[CNT_STREAM + chunk] / FIT_GROUP);
+  // the node stream node_prep wrote (its length is on the device; 32-bit: < 2^31 groups).
+  // KCC_FIT_NG_ONCE: read once per workgroup (lane 0 of wave 0, a vector load) and shared
+  // through LDS — a scalar load in every wave put 4 x 2048 reads on one line at launch, and
+  // the last workgroups started their loop up to 8 us after the first (8-way C4 shard,
+  // r04w timeline)
+  uint32_t n_groups;
+  if (KCC_FIT_NG_ONCE) {
+    __shared__ uint32_t ng_s;
+    if (threadIdx.x == 0) {
+      const volatile unsigned long long* cp = counters + CNT_STREAM + chunk;
+      ng_s = (uint32_t)(*cp / FIT_GROUP);
+    }
+    __syncthreads();
+    n_groups = __builtin_amdgcn_readfirstlane(ng_s);
+  } else {
+    n_groups = (uint32_t)(counters[CNT_STREAM + chunk] / FIT_GROUP);
+  }
   uint32_t lim = n_groups;  // claims end here
   uint32_t base = 0;        // queue: the segment's start
   uint32_t nxt = 0;         // queue: the claim in flight (wave 0, lane 0); static: next chunk
@@ -2776,8 +2774,7 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             SlowNode* slow, int64_t* slow_list, int64_t n_specs,
                             ClampWork cw, unsigned long long* counters, int chunk, int64_t row0,
                             int64_t call_nodes, hipStream_t s, bool dense,
-                            const PlaceArgs* place, int32_t* fast_cl, uint32_t* gvmin,
-                            uint32_t* ng_copies) {
+                            const PlaceArgs* place, int32_t* fast_cl, uint32_t* gvmin) {
   if (KCC_FIT_MSKIP && !gvmin && n_nodes > 0) return hipErrorInvalidValue;
   if (n_nodes <= 0 && !place) return hipSuccess;
   if (fast_cl && (n_specs > CLAMP_LDS_SPECS || dense)) return hipErrorInvalidValue;
@@ -2804,8 +2801,7 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
   hipLaunchKernelGGL(kern, dim3(np_blocks + (unsigned)pa.n_blocks), dim3(KCC_NODE_PREP_BLOCK),
                      lds_bytes, s, n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu,
                      used_mem, fast_a, fast_b, slow, slow_list, n_specs, cw,
-                     counters, (int32_t)chunk, (int32_t)(dense ? 1 : 0), row0 / pr, pa, fast_cl, gvmin,
-                     ng_copies);
+                     counters, (int32_t)chunk, (int32_t)(dense ? 1 : 0), row0 / pr, pa, fast_cl, gvmin);
   return hipGetLastError();
 }
 
@@ -2901,8 +2897,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, uint32_t* queue, int chunk,
                       int64_t grid_nodes, hipStream_t s, const int32_t* fast_cl,
-                      const uint32_t* gvmin, bool count_skips, const FinArgs* fin,
-                      const uint32_t* ng_copies) {
+                      const uint32_t* gvmin, bool count_skips, const FinArgs* fin) {
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
   const int64_t gx = (n_specs + FIT_SPW - 1) / FIT_SPW;
   const int64_t gy = fit_grid_y(n_nodes, n_specs, grid_nodes);
@@ -2913,7 +2908,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, queue, fast_a,
                      fast_b, slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)chunk,
                      (int32_t)gx, (int32_t)gy, fast_cl, KCC_FIT_MSKIP ? gvmin : nullptr,
-                     (int32_t)(count_skips ? 1 : 0), fin ? *fin : FinArgs{}, ng_copies);
+                     (int32_t)(count_skips ? 1 : 0), fin ? *fin : FinArgs{});
   return hipGetLastError();
 }
 
