@@ -379,10 +379,6 @@ int64_t fit_working_blocks(int64_t n_nodes, int64_t n_specs, int64_t grid_nodes)
 #ifndef KCC_RED_RANKS_LAST_MIN
 #define KCC_RED_RANKS_LAST_MIN (16LL << 20)  // containers of the launch
 #endif
-// the fit reads its stream's length once per workgroup (1) or once per wave (0)
-#ifndef KCC_FIT_NG_ONCE
-#define KCC_FIT_NG_ONCE 1
-#endif
 #ifndef KCC_CLAMP_CONCURRENT
 #define KCC_CLAMP_CONCURRENT 0
 #endif

@@ -2192,23 +2192,8 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   }
   uint32_t nskip = 0;  // node groups summed without the memory quotient (scalar)
 
-  // the node stream node_prep wrote (its length is on the device; 32-bit: < 2^31 groups).
-  // KCC_FIT_NG_ONCE: read once per workgroup (lane 0 of wave 0, a vector load) and shared
-  // through LDS — a scalar load in every wave put 4 x 2048 reads on one line at launch, and
-  // the last workgroups started their loop up to 8 us after the first (8-way C4 shard,
-  // r04w timeline)
-  uint32_t n_groups;
-  if (KCC_FIT_NG_ONCE) {
-    __shared__ uint32_t ng_s;
-    if (threadIdx.x == 0) {
-      const volatile unsigned long long* cp = counters + CNT_STREAM + chunk;
-      ng_s = (uint32_t)(*cp / FIT_GROUP);
-    }
-    __syncthreads();
-    n_groups = __builtin_amdgcn_readfirstlane(ng_s);
-  } else {
-    n_groups = (uint32_t)(counters[CNT_STREAM + chunk] / FIT_GROUP);
-  }
+  // the node stream node_prep wrote (its length is on the device; 32-bit: < 2^31 groups)
+  const uint32_t n_groups = (uint32_t)(counters[CNT_STREAM + chunk] / FIT_GROUP);
   uint32_t lim = n_groups;  // claims end here
   uint32_t base = 0;        // queue: the segment's start
   uint32_t nxt = 0;         // queue: the claim in flight (wave 0, lane 0); static: next chunk
