@@ -2091,6 +2091,9 @@ static_assert(FIT_QCHUNK >= 2 && FIT_QCHUNK <= FIT_CHUNK_GROUPS, "claims sum in 
 #ifndef KCC_FIT_QMIN
 #define KCC_FIT_QMIN 2  // node groups per claim at least (guided claims)
 #endif
+#ifndef KCC_FIT_Q1_DIV
+#define KCC_FIT_Q1_DIV 0  // the static first claim at most share / this (0: qsz)
+#endif
 #ifndef KCC_FIT_Q_HALVE
 #define KCC_FIT_Q_HALVE 128  // claims of FIT_QCHUNK / 2 when a workgroup's share is below this
 #endif
@@ -2208,6 +2211,14 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   // claim size: halved when a workgroup's share is small (8-way shards of C4: ~35 groups
   // per workgroup; two claims each keep the balancing)
   const uint32_t qsz = n_groups / (uint32_t)gy < KCC_FIT_Q_HALVE ? FIT_QCHUNK / 2u : FIT_QCHUNK;
+  // the static first claim: qsz, or (KCC_FIT_Q1_DIV) at most a 1/Q1_DIV of a workgroup's
+  // share — the workgroups begin their loops up to ~11 us apart on small shards, and a late
+  // one's static claim was the fit's tail
+  uint32_t q1 = qsz;
+  if (KCC_FIT_Q1_DIV > 0) {
+    const uint32_t sh = n_groups / (uint32_t)gy / (uint32_t)(KCC_FIT_Q1_DIV > 0 ? KCC_FIT_Q1_DIV : 1);
+    q1 = sh < q1 ? (sh > (uint32_t)KCC_FIT_QMIN ? sh : (uint32_t)KCC_FIT_QMIN) : q1;
+  }
   __shared__ uint32_t q_slot[2];
   // lane 0 of wave 0 issues the claim in asm, so the compiler does not wait for it where
   // it is issued (its atomic-optimizer expansion reads the result at once); wave 0 waits
@@ -2228,8 +2239,8 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   // returning atomics on 256 lines at once); the queue hands out what follows.
   const uint32_t wps = ((uint32_t)gy + nsub - 1u) / nsub;  // workgroups per segment (at most)
   const uint32_t wseg = ((uint32_t)gy - sub + nsub - 1u) / nsub;  // this segment's workgroups
-  const uint32_t dyn0 = wseg * qsz;                        // the queue's first group
-  uint32_t qcur = qsz;  // size of the claim whose result is read next
+  const uint32_t dyn0 = wseg * q1;                         // the queue's first group
+  uint32_t qcur = q1;   // size of the claim whose result is read next
   auto claim_publish = [&](uint32_t slot) {
     if (wv == 0) {
       asm volatile("s_waitcnt vmcnt(0)" : "+v"(nxt) : : "memory");
@@ -2243,7 +2254,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     lim = base + seg < n_groups ? base + seg : n_groups;
     KCC_TL(2048 + b % 4096, 1);
   }
-  const uint32_t first = ((uint32_t)by / nsub) * qsz;  // the static first claim's offset
+  const uint32_t first = ((uint32_t)by / nsub) * q1;  // the static first claim's offset
   uint64_t acc = 0;
   uint64_t errs = 0;
   uint32_t slow_iters = 0;
