@@ -2092,7 +2092,8 @@ static_assert(FIT_QCHUNK >= 2 && FIT_QCHUNK <= FIT_CHUNK_GROUPS, "claims sum in 
 #define KCC_FIT_QMIN 2  // node groups per claim at least (guided claims)
 #endif
 #ifndef KCC_FIT_Q1_DIV
-#define KCC_FIT_Q1_DIV 0  // the static first claim at most share / this (0: qsz)
+#define KCC_FIT_Q1_DIV 8  // the static first claim at most share / this (0: qsz); the 8-way C4
+                          // rank: 0.0624 -> 0.0618 ms (r04z), C4 unchanged (its share / 8 > qsz)
 #endif
 #ifndef KCC_FIT_Q_HALVE
 #define KCC_FIT_Q_HALVE 128  // claims of FIT_QCHUNK / 2 when a workgroup's share is below this
