@@ -42,11 +42,6 @@ FIT_VALU_PER_NODE_WAVE = 3.0
 # the same loop with the pod-slot clamp applied inside it (kcc_set_clamp_in_fit; small
 # shards): min, compare, select, the clamp values by vector loads (tests/test_isa.py)
 FIT_NC_VALU_PER_NODE_WAVE = 5.0
-# the memory-bound skip (KCC_FIT_MSKIP): node groups on which every spec of
-# a class-A wave requests at most floor(free memory / allocatable pods) of each node skip the
-# f64 memory quotient: 2 VALU per node x wave (clamp in the fit: 3)
-FIT_SKIP_VALU_PER_NODE_WAVE = 2.0
-FIT_NC_SKIP_VALU_PER_NODE_WAVE = 3.0
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave-instructions / s
 METRIC = "node×spec fit evals/sec at 1M nodes × 4K specs; % of HBM roofline"
 # per-launch HBM traffic of each kernel from rocprofv3 PMC passes of this same bench
@@ -461,18 +456,13 @@ def main():
     streamed = eng.fit_stream_rows()
     clamp_in_fit = eng.clamp_in_fit_used()
     valu_pn = FIT_NC_VALU_PER_NODE_WAVE if clamp_in_fit else FIT_VALU_PER_NODE_WAVE
-    skip_pn = FIT_NC_SKIP_VALU_PER_NODE_WAVE if clamp_in_fit else FIT_SKIP_VALU_PER_NODE_WAVE
-    # (node group, class-A wave) pairs of the last step's fit that skipped the memory
-    # quotient (every chunk's; the VALU they did not issue)
-    skip_groups = eng.fit_mskip_groups()
-    group_waves = streamed // 8 * ((S + 63) // 64)
 
     # algorithmic bytes per launch (DESIGN.md "Roofline accounting"): a step runs
     # `chunks` reduce launches and `chunks` fit launches over node ranges of ~n/chunks
     fit_bytes = (streamed * (20 if clamp_in_fit else 16) + chunks * (S * 48 + S * 8)) / chunks  # FitGroupA (+ clamp values) + specs in, totals out
     red_bytes = (C * 16 + (n + 1) * 8 + n * 16) / chunks       # requests + CSR offsets in, sums out
     fit_gbs = fit_bytes / (fit_ms * 1e-3) / 1e9
-    fit_instr = streamed * ((S + 63) // 64) * valu_pn - skip_groups * 8 * (valu_pn - skip_pn)
+    fit_instr = streamed * ((S + 63) // 64) * valu_pn
     fit_valu = fit_instr / chunks / (fit_ms * 1e-3)
     red_gbs = red_bytes / (red_ms * 1e-3) / 1e9
     c4_alone = args.config == "C4" and world == 1 and args.emulate_world <= 1  # the profiled run
@@ -537,15 +527,10 @@ def main():
             "peak": VALU_ISSUE_PEAK / 1e9, "unit": "G wave-instr/s",
             "frac": fit_valu / VALU_ISSUE_PEAK,
             "valu_per_node_wave": valu_pn,
-            "valu_per_node_wave_skip": skip_pn,
-            "mskip_group_waves": skip_groups, "group_waves": group_waves,
-            "mskip_fraction": skip_groups / max(group_waves, 1),
             "fit_evals_per_s": n / chunks * S / (fit_ms * 1e-3),
             "fit_streamed_pairs_per_s": streamed / chunks * S / (fit_ms * 1e-3),
             "note": "counted over the streamed rows (the instructions the kernel issues): "
-                    f"{valu_pn:g} per node x wave, {skip_pn:g} on the groups where every spec of "
-                    "the class-A wave requests at most floor(free memory / allocatable pods) of "
-                    "each node (memory quotient skipped, DESIGN.md §4.3)",
+                    f"{valu_pn:g} per node x wave",
         },
         "clamp": {
             "in_fit": clamp_in_fit, "mode": args.clamp_in_fit,

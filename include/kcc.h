@@ -30,8 +30,13 @@
  *     bounded; one that gives up (never on a healthy device) sets a sticky fault word
  *     of the device.  While it is set every finalize marks every spec KCC_SPEC_FAULT
  *     (totals 0) and the synchronous entry points return KCC_EFAULT; kcc_clear_faults
- *     resets it.  kcc_reduce_requests_async alone has no per-spec output: check
- *     kcc_reduce_faults after synchronising.
+ *     resets it.  The fault also travels with the data: a partial produced on a
+ *     faulted device (kcc_*_partial_async, kcc_fit_run_async) carries a fault mark in
+ *     its per-spec counts, so every rank that sums it — over the p2p exchange, an RCCL
+ *     or any other all-reduce, the in-library device fold — marks every spec
+ *     KCC_SPEC_FAULT too, without reading the faulted device's words.
+ *     kcc_reduce_requests_async alone has no per-spec output: check kcc_reduce_faults
+ *     after synchronising.
  *   - A context is not thread-safe; every entry calls hipSetDevice(ctx device), so
  *     Go OS-thread migration between cgo calls is harmless.
  *   - There is no CPU backend: without a usable gfx950 device kcc_create fails.
@@ -144,7 +149,9 @@ int kcc_capacity(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containers,
 
 /* Device-level fit, split so that a node-sharded caller can all-reduce in between:
  *   kcc_fit_partial_async: partial[0..S)  = wrapping Σ over this call's nodes of q(i,s)
- *                          partial[S..2S) = number of divide-by-zero rows
+ *                          partial[S..2S) = number of divide-by-zero rows, + 2^48 per
+ *                          launch on a faulted device (the fault mark: >= 2^48 after
+ *                          any sum means a faulted shard; finalize -> KCC_SPEC_FAULT)
  *                          (both in an internal spec order; zeroed by this call)
  *   <optional all-reduce(sum, int64) of partial[0..2S) over node shards>
  *   kcc_fit_finalize_async: totals[s], spec_err[s] in caller order.
@@ -306,14 +313,6 @@ int kcc_set_clamp_in_fit(kcc_ctx* ctx, int mode);
  * specs and 6.5 for class B, against 3 and 4.5 with the clamp correction). */
 int kcc_clamp_in_fit_used(kcc_ctx* ctx, int* used);
 int kcc_fit_stream_rows(kcc_ctx* ctx, int64_t* streamed);
-/* The memory-bound skip of the fit: node groups x class-A spec waves of the
- * last kcc_capacity*_async / kcc_fit_*_async on device 0 that were summed without the memory
- * quotient, because every spec of the wave requests at most floor(free memory / allocatable
- * pods) of every node of the group (so floor(fm / m) >= allocatable pods there).  The same
- * totals either way; for the VALU accounting.  Counted only by fits launched while
- * kcc_profile_enable is on (0 otherwise: the count costs a device atomic per wave).
- * Synchronises the device. */
-int kcc_fit_mskip_groups(kcc_ctx* ctx, int64_t* groups);
 
 /* Fraction of (node, spec) pairs of the last kcc_fit* call that took the exact
  * 64-bit path instead of the saturating fast path (diagnostic; host-computed from

@@ -57,7 +57,6 @@ SIGNATURES = {
     "kcc_set_clamp_in_fit": (_int, [_vp, _int]),
     "kcc_clamp_in_fit_used": (_int, [_vp, C.POINTER(C.c_int)]),
     "kcc_fit_stream_rows": (_int, [_vp, C.POINTER(_i64)]),
-    "kcc_fit_mskip_groups": (_int, [_vp, C.POINTER(_i64)]),
     "kcc_reduce_faults": (_int, [_vp, C.POINTER(_i64)]),
     "kcc_clear_faults": (_int, [_vp]),
     "kcc_comm_unique_id": (_int, [_vp]),

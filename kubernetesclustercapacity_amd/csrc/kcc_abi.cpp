@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -66,7 +67,6 @@ struct Dev {
   // while the caller's stream fits chunk k-1
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr;
-  hipEvent_t ev_join = nullptr;  // KCC_CLAMP_CONCURRENT: the side stream's clamp correction done
   hipEvent_t ev_red[kcc::FIT_MAX_CHUNKS] = {};
   bool prof_on = false;
   std::vector<ProfPair> prof_pending;
@@ -98,7 +98,6 @@ struct Dev {
   int clamp_in_fit = -1;   // kcc_set_clamp_in_fit: -1 by size (clamp_in_fit_auto), 0 never, 1 always
   bool last_nc = false;    // the last capacity call applied the clamp in the fit
   DevBuf fast_cl;          // the clamp in the fit: each streamed row's clamp value
-  DevBuf fast_v;           // KCC_FIT_MSKIP: each stream group's smallest floor(fm / P) (u32)
   int stream_chunks = 0;   // node chunks of the last fit prepare (their stream counters)
   int64_t prep_nodes = -1, prep_specs = -1;  // sizes the workspace was last prepared for
   // staging of the host-array entry points
@@ -138,6 +137,9 @@ struct kcc_ctx {
   unsigned long long* host_cnt = nullptr;
   size_t host_cnt_n = 0;
   int64_t host_stream_rows = -1;  // streamed rows of the last host-array fit (-1: none)
+  // the in-library all-reduce (comms) has been checked against a host-side sum of the
+  // devices' partials (the first host-array call of the context does it)
+  bool allreduce_verified = false;
 };
 
 namespace {
@@ -290,7 +292,6 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.fast_a, sizeof(kcc::FitGroupA) * (size_t)kcc::fit_groups((int64_t)N)));
   KCC_HIP(ctx, ensure(dv.fast_b, sizeof(kcc::FitGroup) * (size_t)kcc::fit_groups((int64_t)N)));
   KCC_HIP(ctx, ensure(dv.fast_cl, sizeof(int32_t) * kcc::FIT_GROUP * (size_t)kcc::fit_groups((int64_t)N)));
-  KCC_HIP(ctx, ensure(dv.fast_v, sizeof(uint32_t) * (size_t)kcc::fit_groups((int64_t)N)));
   KCC_HIP(ctx, ensure(dv.slow, sizeof(kcc::SlowNode) * N));
   KCC_HIP(ctx, ensure(dv.slow_list, sizeof(int64_t) * N));
   KCC_HIP(ctx, ensure(dv.srec, sizeof(kcc::SpecRec) * S));
@@ -401,7 +402,8 @@ int check_spec_ws(kcc_ctx* ctx, Dev& dv, int64_t S) {
 kcc::PlaceArgs place_args(Dev& dv, int64_t n_specs, const uint64_t* spec_cpu,
                           const int64_t* spec_mem, int64_t* partial) {
   return kcc::PlaceArgs{n_specs, spec_cpu, spec_mem, spec_prep_of(dv), clamp_of(dv), partial,
-                        as<unsigned long long>(dv.counters), 0};
+                        as<unsigned long long>(dv.counters), 0,
+                        as<const unsigned long long>(dv.faults)};
 }
 
 int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* alloc_cpu,
@@ -439,7 +441,7 @@ int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* allo
                                        as<kcc::FitGroup>(dv.fast_b), as<kcc::SlowNode>(dv.slow),
                                        as<int64_t>(dv.slow_list), n_specs, clamp_of(dv),
                                        as<unsigned long long>(dv.counters), 0, 0,
-                                       n_nodes, s, dv.fit_dense, &pa, nullptr, as<uint32_t>(dv.fast_v)));
+                                       n_nodes, s, dv.fit_dense, &pa, nullptr));
   if (n_nodes == 0) {
     dv.clamp_dirty = false;
     return KCC_OK;
@@ -461,7 +463,7 @@ int fit_run_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_specs, int64_t
                                as<kcc::SlowNode>(dv.slow),
                                as<int64_t>(dv.slow_list), n_specs, spec_prep_of(dv), partial,
                                as<unsigned long long>(dv.counters), as<uint32_t>(dv.fit_q), 0,
-                               n_nodes, s, nullptr, as<uint32_t>(dv.fast_v), dv.prof_on));
+                               n_nodes, s, as<const unsigned long long>(dv.faults)));
   return KCC_OK;
 }
 
@@ -628,17 +630,9 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     }
     if (k > 1) KCC_HIP(ctx, hipEventRecord(dv.ev_red[c], dv.side));
   }
-  // KCC_CLAMP_CONCURRENT (A/B builds; off by default, measured slower — DESIGN.md §6): the
-  // clamp correction beside the fit (one chunk, clamp_apply mode), forked onto the side
-  // stream after node_prep; with totals the last workgroup of either kernel finalizes
-  // (FinArgs::expect)
-  const bool conc = KCC_CLAMP_CONCURRENT && k == 1 && !nc && n_specs > 0 && n_nodes > 0;
   const bool fuse_fin = totals && n_nodes > 0;
   const kcc::FinArgs fin{as<int32_t>(dv.sperm), totals, spec_err, as<uint32_t>(dv.clamp_arrive),
-                         as<const unsigned long long>(dv.faults),
-                         conc ? (uint32_t)(kcc::clamp_apply_blocks(n_specs) +
-                                           kcc::fit_working_blocks(n_nodes, n_specs, n_nodes))
-                              : 0u};
+                         as<const unsigned long long>(dv.faults)};
   for (int c = 0; c < k; ++c) {
     if (k > 1) KCC_HIP(ctx, hipStreamWaitEvent(s, dv.ev_red[c], 0));  // also joins the side stream
     const int64_t n = hi[c] - lo[c];
@@ -652,21 +646,8 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                        as<int64_t>(dv.slow_list) + lo[c], n_specs, clamp_of(dv),
                                        as<unsigned long long>(dv.counters),
                                        c, lo[c], n_nodes, s, dv.fit_dense,
-                                       place_here ? &pa : nullptr, fast_cl,
-                                       as<uint32_t>(dv.fast_v) + lo[c] / kcc::FIT_GROUP));
+                                       place_here ? &pa : nullptr, fast_cl));
     if (n == 0) continue;
-    // fork: clamp_apply on the side stream, after node_prep; KCC_CLAMP_CONCURRENT 1 queues
-    // it before the fit (its workgroups resident first), 2 after (it fills the fit's tail)
-    auto fork_clamp = [&]() -> int {
-      KCC_HIP(ctx, hipStreamWaitEvent(dv.side, dv.ev_fork, 0));
-      KCC_HIP(ctx, kcc::launch_clamp_apply(n_specs, n_nodes, clamp_of(dv),
-                                           as<unsigned long long>(dv.counters), partial, dv.side,
-                                           fuse_fin ? &fin : nullptr));
-      KCC_HIP(ctx, hipEventRecord(dv.ev_join, dv.side));
-      return KCC_OK;
-    };
-    if (conc) KCC_HIP(ctx, hipEventRecord(dv.ev_fork, s));
-    if (conc && KCC_CLAMP_CONCURRENT == 1 && (rc = fork_clamp())) return rc;
     ProfPair pp{};
     if (dv.prof_on) {
       KCC_HIP(ctx, prof_event(dv, &pp.a));
@@ -678,22 +659,13 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                  as<kcc::SlowNode>(dv.slow) + lo[c],
                                  as<int64_t>(dv.slow_list) + lo[c], n_specs, spec_prep_of(dv),
                                  partial, as<unsigned long long>(dv.counters),
-                                 as<uint32_t>(dv.fit_q), c, n_nodes, s, fast_cl,
-                                 as<uint32_t>(dv.fast_v) + lo[c] / kcc::FIT_GROUP, dv.prof_on,
-                                 conc && fuse_fin ? &fin : nullptr));
+                                 as<uint32_t>(dv.fit_q), c, n_nodes, s,
+                                 as<const unsigned long long>(dv.faults), fast_cl));
     if (dv.prof_on) {
       KCC_HIP(ctx, hipEventRecord(pp.b, s));
       pp.kind = 1;
       dv.prof_pending.push_back(pp);
     }
-    if (conc && KCC_CLAMP_CONCURRENT == 2 && (rc = fork_clamp())) return rc;
-  }
-  if (conc) {  // join: the call's work all ordered on s again
-    KCC_HIP(ctx, hipStreamWaitEvent(s, dv.ev_join, 0));
-    dv.clamp_dirty = false;
-    if (totals && !fuse_fin)
-      return fit_finalize_dev(ctx, dv, n_specs, partial, totals, spec_err, s);
-    return KCC_OK;
   }
   // the pod-slot clamp of every chunk's fast rows, added back per spec; totals != nullptr:
   // the clamp launch's last workgroup also finalizes (no fit_finalize launch)
@@ -806,14 +778,57 @@ int run_host(kcc_ctx* ctx, bool with_reduce, int64_t n_nodes, int64_t n_cont,
     if (sh >= nd)  // fold this slot into the device's slot 0 (wrapping int64 adds)
       KCC_HIP(ctx, kcc::launch_partial_add(2 * n_specs, as<int64_t>(dv.partial), part, dv.stream));
   }
-  if (nd > 1) {
+  if (!ctx->comms.empty()) {
+    // the context's first all-reduce proves itself (as bench.py's exchange does before it
+    // is timed): every device's result must equal the host's wrapping sum of the devices'
+    // partials (CC:138 summed over devices), else KCC_ERCCL
+    const bool verify = !ctx->allreduce_verified;
+    const size_t words = 2 * (size_t)n_specs;
+    std::vector<uint64_t> expect, got;
+    if (verify) {
+      expect.assign(words, 0);
+      got.resize(words);
+      for (int d = 0; d < nd; ++d) {
+        Dev& dv = ctx->devs[d];
+        KCC_HIP(ctx, hipSetDevice(dv.device));
+        KCC_HIP(ctx, hipMemcpyAsync(got.data(), dv.partial.p, 8 * words, hipMemcpyDeviceToHost,
+                                    dv.stream));
+        KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
+        for (size_t i = 0; i < words; ++i) expect[i] += got[i];
+      }
+    }
     KCC_NCCL(ctx, ncclGroupStart());
     for (int d = 0; d < nd; ++d) {
       Dev& dv = ctx->devs[d];
-      KCC_NCCL(ctx, ncclAllReduce(dv.partial.p, dv.partial.p, 2 * (size_t)n_specs, ncclInt64,
+      KCC_NCCL(ctx, ncclAllReduce(dv.partial.p, dv.partial.p, words, ncclInt64,
                                   ncclSum, ctx->comms[d], dv.stream));
     }
     KCC_NCCL(ctx, ncclGroupEnd());
+#ifdef KCC_DIAG_INLIB_COMM
+    // the drill (variant builds only): a corrupted all-reduce result on the last device
+    if (std::getenv("KCC_DRILL_CORRUPT_ALLREDUCE")) {
+      Dev& dv = ctx->devs[nd - 1];
+      KCC_HIP(ctx, hipSetDevice(dv.device));
+      KCC_HIP(ctx, hipMemsetAsync(dv.partial.p, 0x5a, 8, dv.stream));
+    }
+#endif
+    if (verify) {
+      for (int d = 0; d < nd; ++d) {
+        Dev& dv = ctx->devs[d];
+        KCC_HIP(ctx, hipSetDevice(dv.device));
+        KCC_HIP(ctx, hipMemcpyAsync(got.data(), dv.partial.p, 8 * words, hipMemcpyDeviceToHost,
+                                    dv.stream));
+        KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
+        for (size_t i = 0; i < words; ++i)
+          if (got[i] != expect[i])
+            return fail(ctx, KCC_ERCCL,
+                        "in-library all-reduce verification failed on device " +
+                            std::to_string(dv.device) + ": word " + std::to_string(i) + " is " +
+                            std::to_string(got[i]) + ", the host sum of the devices' partials " +
+                            std::to_string(expect[i]) + "; results not returned");
+      }
+      ctx->allreduce_verified = true;
+    }
   }
   Dev& d0 = ctx->devs[0];
   KCC_HIP(ctx, hipSetDevice(d0.device));
@@ -899,14 +914,18 @@ int kcc_create(kcc_ctx** out, int first_device, int n_gpus) {
     if ((e = hipSetDevice(dv.device)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&dv.stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&dv.side, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&dv.ev_fork, hipEventDisableTiming)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&dv.ev_join, hipEventDisableTiming)) != hipSuccess) {
+        (e = hipEventCreateWithFlags(&dv.ev_fork, hipEventDisableTiming)) != hipSuccess) {
       g_create_error = std::string("stream creation failed: ") + hipGetErrorString(e);
       kcc_destroy(ctx);
       return KCC_EHIP;
     }
   }
-  if (n_gpus > 1) {
+#ifdef KCC_DIAG_INLIB_COMM
+  const bool inlib_comm = true;  // (variant builds: one device goes through RCCL too)
+#else
+  const bool inlib_comm = n_gpus > 1;
+#endif
+  if (inlib_comm) {
     ctx->comms.resize(n_gpus);
     ncclResult_t r = ncclCommInitAll(ctx->comms.data(), n_gpus, ids.data());
     if (r != ncclSuccess) {
@@ -943,7 +962,7 @@ void kcc_destroy(kcc_ctx* ctx) {
     DevBuf* bufs[] = {&dv.c_rank, &dv.c_bcnt, &dv.c_cs, &dv.c_ms,
                       &dv.c_mrc, &dv.c_crm, &dv.c_dperm, &dv.c_C, &dv.c_H2, &dv.c_H3,
                       &dv.c_Crow, &dv.c_rec, &dv.c_dir,
-                      &dv.red_tail,  &dv.faults, &dv.rank_arrive, &dv.fast_v, &dv.fast_cl, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
+                      &dv.red_tail,  &dv.faults, &dv.rank_arrive, &dv.fast_cl, &dv.slow_list, &dv.fast_a, &dv.fast_b, &dv.slow, &dv.srec,
                       &dv.sperm,     &dv.fit_q,
                       &dv.counters,  &dv.ptr,       &dv.cpu,       &dv.mem,       &dv.cpul,
                       &dv.meml,      &dv.used_cpu,  &dv.used_mem,  &dv.lim_cpu,   &dv.lim_mem,
@@ -963,7 +982,6 @@ void kcc_destroy(kcc_ctx* ctx) {
       (void)hipStreamDestroy(dv.side);
     }
     if (dv.ev_fork) (void)hipEventDestroy(dv.ev_fork);
-    if (dv.ev_join) (void)hipEventDestroy(dv.ev_join);
     for (hipEvent_t ev : dv.ev_red)
       if (ev) (void)hipEventDestroy(ev);
     for (const ProfPair& pp : dv.prof_pending) {
@@ -1254,19 +1272,6 @@ int kcc_fit_stream_rows(kcc_ctx* ctx, int64_t* streamed) {
   int64_t t = 0;
   for (int k = 0; k < dv.stream_chunks && k < kcc::FIT_MAX_CHUNKS; ++k) t += (int64_t)c[kcc::CNT_STREAM + k];
   *streamed = t;
-  return KCC_OK;
-}
-
-int kcc_fit_mskip_groups(kcc_ctx* ctx, int64_t* groups) {
-  if (!ctx || !groups) return ctx ? fail(ctx, KCC_EINVAL, "NULL output") : KCC_EINVAL;
-  Dev& dv = ctx->devs[0];
-  KCC_HIP(ctx, hipSetDevice(dv.device));
-  KCC_HIP(ctx, hipDeviceSynchronize());
-  unsigned long long c = 0;
-  if (dv.counters.p)
-    KCC_HIP(ctx, hipMemcpy(&c, as<unsigned long long>(dv.counters) + kcc::CNT_FIT_MSKIP, sizeof(c),
-                           hipMemcpyDeviceToHost));
-  *groups = (int64_t)c;
   return KCC_OK;
 }
 

@@ -4,15 +4,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// Diagnostic timing knobs produce wrong results by design (no stores, no atomics,
-// searches skipped), add stamp stores, or are unsafe beside other kernels
-// (KCC_RED_XCD_MAP: a look-back may wait on an undispatched wave): only experiment builds (csrc/Makefile `variant`,
-// which defines KCC_VARIANT_BUILD and writes a separate .so) may set them.
+// Diagnostic knobs produce wrong results by design (no stores, loads only), add stamp
+// stores, or make every bounded wait give up (the fault-path test build): only experiment
+// builds (csrc/Makefile `variant` / `faultdiag`, which define KCC_VARIANT_BUILD and write a
+// separate .so) may set them.  The tuning choices are constants here: the variants that
+// lost their A/B were deleted (DESIGN.md §10 lists them with their numbers and commits).
 #if !defined(KCC_VARIANT_BUILD) &&                                                       \
-    (defined(KCC_FIT_DIAG_NO_ATOMICS) || defined(KCC_DIAG_RED_NOSTORE) ||                \
-     defined(KCC_DIAG_RED_LOADONLY) || defined(KCC_DIAG_NP) || defined(KCC_DIAG_CP) ||   \
-     defined(KCC_TIMELINE) || defined(KCC_RED_XCD_MAP) || defined(KCC_DIAG_RED_GIVEUP) ||  \
-     defined(KCC_DIAG_P2P_GIVEUP))
+    (defined(KCC_DIAG_RED_NOSTORE) || defined(KCC_DIAG_RED_LOADONLY) ||                  \
+     defined(KCC_TIMELINE) || defined(KCC_DIAG_RED_GIVEUP) || defined(KCC_DIAG_P2P_GIVEUP) || \
+     defined(KCC_DIAG_INLIB_COMM))
 #error "a diagnostic KCC_* knob in a release build: use `make variant` (KCC_VARIANT_BUILD)"
 #endif
 
@@ -31,20 +31,12 @@ struct RankArgs;   // below: spec ranks, run as extra workgroups of a reduce lau
 // per launch and consumed by exactly one wave, which clears its tag — every tag is 0
 // between launches, so nothing in the launch depends on host state and a captured graph
 // replays correctly).
-#ifndef KCC_RED_ROUNDS
-#define KCC_RED_ROUNDS 1  // waves = this many rounds of the resident wave capacity
-#endif
-#ifndef KCC_RED_PREFETCH
-#define KCC_RED_PREFETCH 1  // tiles in flight ahead of the one being reduced
-#endif
-#ifndef KCC_RED_IPL
-// containers per lane per tile (4 or 8): 8 halves the per-tile work (scan, node walk,
-// stores) per container at 125 VGPRs (4 waves per SIMD instead of 6): C4 reduce
-// 136.4 -> 131.1 us, 8-way shard 20.2 -> 19.5 us (A/B in one process, outputs identical)
-#define KCC_RED_IPL 8
-#endif
-constexpr int RED_IPL = KCC_RED_IPL;
-static_assert(RED_IPL == 4 || RED_IPL == 8 || RED_IPL == 16, "2, 4 or 8 16-B loads per lane and array");
+// tiles in flight ahead of the one being reduced (1-6 measured equal: ping-pong)
+constexpr int RED_PREFETCH = 1;
+// containers per lane per tile: 8 halves the per-tile work (scan, node walk, stores) per
+// container against 4, at 125 VGPRs (4 waves per SIMD instead of 6): C4 reduce 136.4 ->
+// 131.1 us, 8-way shard 20.2 -> 19.5 us (A/B in one process, outputs identical)
+constexpr int RED_IPL = 8;
 constexpr int RED_TILE = 64 * RED_IPL;  // 512
 constexpr int RED_WAVES_PER_BLOCK = 4;
 // the reduce stores through 32-bit buffer offsets (8 B per node, < 2^31)
@@ -61,6 +53,14 @@ constexpr uint64_t RED_TAG_READY = 1;  // published (0: free; the consumer clear
 enum { FAULT_RED = 0, FAULT_P2P = 1, FAULT_WORDS = 8 };
 constexpr int32_t SPEC_ERR_DIV0 = 1;   // include/kcc.h KCC_SPEC_DIVZERO
 constexpr int32_t SPEC_ERR_FAULT = 2;  // include/kcc.h KCC_SPEC_FAULT
+// The fault travels with the data: a fit launched while its device is faulted adds
+// SPEC_FAULT_MARK to every spec's div-by-zero count in partial[S..2S), once per spec, so
+// every consumer of the partial — this device's finalize, the p2p exchange, an RCCL or
+// torch.distributed all-reduce summed into another rank's finalize, the in-library device
+// fold — sees a count >= SPEC_FAULT_MARK and marks the spec KCC_SPEC_FAULT.  Real counts
+// are < 2^28 per device (one per node row); the marks of up to 2^14 launches x ranks sum
+// without wrapping.
+constexpr uint64_t SPEC_FAULT_MARK = 1ull << 48;
 
 // Containers per wave range: whole tiles, sized so the waves fill the device's resident
 // wave slots (occupancy API) in KCC_RED_ROUNDS rounds: one round of equal, long ranges
@@ -212,42 +212,27 @@ struct ClampWork {
 constexpr int64_t MAX_SPECS = (int64_t)1 << 26;
 __host__ __device__ inline int64_t clamp_c_cells(int64_t S) { return (S / 64 + 3) * (S / 64 + 3); }
 inline int64_t clamp_h_cells(int64_t S) { return (S / 64 + 1) * 65 * 64; }
-#ifndef KCC_C_COPIES
 // copies of the coarse table: node_prep flushes its LDS-summed table once per workgroup
 // (S <= 4096), so two spread the flushes enough; clamp_apply's x-group workgroups read
 // every copy (C4 8-way shard, fit prepare + run: 8 copies 60.4 us, 2: 58.2, 1: 58.5; C5's
 // global-memory atomics need more than one: 544.8 / 545.5 / 557.8 us)
-#define KCC_C_COPIES 2
-#endif
-constexpr int C_COPIES = KCC_C_COPIES;
-#ifndef KCC_H2_COPIES
-#define KCC_H2_COPIES 2
-#endif
-constexpr int H2_COPIES = KCC_H2_COPIES;
+constexpr int C_COPIES = 2;
+constexpr int H2_COPIES = 2;
 // binned H2 / H3 (ClampWork::rec): node_prep's passes of clamp_pass_rows(n) rows (1 or 4
 // per thread) emit at most one record of each table per row; up to CLAMP_BIN_T_MAX
 // x-groups (S <= 16384), larger S adds to the H2 / H3 copies with device atomics
 constexpr int CLAMP_PASS_ROWS_MIN = 1024;
 constexpr int CLAMP_PASS_ROWS_MAX = 4096;  // chunks of a pipelined call are multiples of it
-#ifndef KCC_NP_PASS_ROWS
-#define KCC_NP_PASS_ROWS 0  // 0: by the call's rows; 1024 / 4096: fixed (A/B builds)
-#endif
 // Rows per node_prep pass for a call of n_nodes rows: 4096 when such passes still fill
 // the chip (one node_prep workgroup per CU), else 1024 — 4x the workgroups on small
 // shards (C4's 8-way shard: 123 instead of 31).  Fewer, larger passes keep clamp_apply's
 // heavy bins cheap: a bin's records are read pass by pass, and at C4 one bin held 34k
 // records (12.9 us to consume over 245 passes, 28.5 us over 977).
 inline int64_t clamp_pass_rows(int64_t n_nodes) {
-  if (KCC_NP_PASS_ROWS) return KCC_NP_PASS_ROWS;
   return n_nodes >= (int64_t)200 * CLAMP_PASS_ROWS_MAX ? CLAMP_PASS_ROWS_MAX : CLAMP_PASS_ROWS_MIN;
 }
 constexpr int64_t CLAMP_BIN_T_MAX = 256;
-#ifndef KCC_CLAMP_BINNED
-#define KCC_CLAMP_BINNED 1
-#endif
-__host__ __device__ inline bool clamp_binned(int64_t S) {
-  return KCC_CLAMP_BINNED && (S + 63) / 64 <= CLAMP_BIN_T_MAX;
-}
+__host__ __device__ inline bool clamp_binned(int64_t S) { return (S + 63) / 64 <= CLAMP_BIN_T_MAX; }
 inline int64_t clamp_d_stride(int64_t S) { return 2 * ((S + 63) / 64) + 1; }
 inline int64_t clamp_passes(int64_t n_nodes) {
   const int64_t pr = clamp_pass_rows(n_nodes);
@@ -255,10 +240,7 @@ inline int64_t clamp_passes(int64_t n_nodes) {
 }
 // up to this many specs node_prep's search and count tables live in LDS; larger S
 // searches the same tables in global memory
-#ifndef KCC_CLAMP_LDS_SPECS
-#define KCC_CLAMP_LDS_SPECS 4096
-#endif
-constexpr int64_t CLAMP_LDS_SPECS = KCC_CLAMP_LDS_SPECS;
+constexpr int64_t CLAMP_LDS_SPECS = 4096;
 
 // Spec ranks (spec_rank): the x-rank by (c, index) and the y-rank by (m, index) of every
 // normal spec, by sort and search: workgroup (query block of RANK_L, slice of RANK_L
@@ -310,6 +292,7 @@ struct PlaceArgs {
   int64_t* partial;
   unsigned long long* counters;
   int32_t n_blocks;  // workgroups of the launch's block size (0: none)
+  const unsigned long long* faults;  // set: partial[S + i] starts at SPEC_FAULT_MARK
 };
 
 
@@ -326,23 +309,8 @@ enum {
                        // every spec (P <= 0), subtracted from every normal spec by the fit
   CNT_SLOW_ROWS = 4,   // + chunk: rows in that node chunk's slow_list
   CNT_STREAM = 4 + FIT_MAX_CHUNKS,  // + chunk: node rows in that chunk's fit stream (x 8)
-  CNT_FIT_MSKIP = 4 + 2 * FIT_MAX_CHUNKS,  // (node group, class-A wave) pairs the fit summed
-                                           // without the memory quotient (every lane qm >= P)
-  CNT_N = 5 + 2 * FIT_MAX_CHUNKS
+  CNT_N = 4 + 2 * FIT_MAX_CHUNKS
 };
-// The memory-bound skip (KCC_FIT_MSKIP): node_prep stores each stream group's smallest
-// V = floor(free memory / P) (saturated to u32) in gvmin[group]; spec_place orders the
-// class-A specs by memory request (y-rank), so a class-A wave's largest request m_max is
-// known; where m_max <= gvmin[group], floor(fm / m) >= P for every lane and node of the
-// group (m <= fm / P  <=>  m P <= fm), so min(findMin(qc, qm), P) = min(qc, P) and the
-// group is summed without the f64 memory quotient (class A: 2 VALU per node x wave instead
-// of 3; the clamp in the fit: 3 instead of 5).  Off by default: measured slower (C4 fit
-// 124.2 -> 129.5 us, node_prep 26.3 -> 29.0 us; 8-way shard prepare + fit 57.2 -> 59.4 us):
-// the per-group branch waits for all of the group's scalar loads and its V_min, and only
-// about half of the (group, wave) pairs skip.
-#ifndef KCC_FIT_MSKIP
-#define KCC_FIT_MSKIP 0
-#endif
 // The clamp correction after every node_prep of the call (n_nodes: the call's rows, for
 // the binned records' pass count): partial[s] -= D_s for the normal specs of clamp-free
 // waves; leaves the table copies zero.
@@ -355,33 +323,14 @@ struct FinArgs {
   int32_t* spec_err;
   uint32_t* arrive;
   const unsigned long long* faults;  // the device's fault words: set -> KCC_SPEC_FAULT
-  // arrivals the last workgroup waits for: 0 = the launch's own grid; the concurrent clamp
-  // correction counts the fit's working workgroups too (the last of either finalizes)
-  uint32_t expect;
 };
 hipError_t launch_clamp_apply(int64_t n_specs, int64_t n_nodes, ClampWork cw,
                               const unsigned long long* counters, int64_t* partial, hipStream_t s,
                               const FinArgs* fin = nullptr);
 int64_t clamp_apply_blocks(int64_t n_specs);  // clamp_apply_kernel's grid
-// the fit's working workgroups (gx x gy: the grid less its XCD padding)
-int64_t fit_working_blocks(int64_t n_nodes, int64_t n_specs, int64_t grid_nodes);
-// KCC_CLAMP_CONCURRENT: the clamp correction (clamp_apply, on the context's side stream)
-// runs beside the fit instead of after it — both only add into partial (wrapping atomics),
-// and neither reads what the other writes; with the fused finalize the last workgroup of
-// either kernel writes the totals.  0 = after the fit (default: measured faster), 1 = queued
-// before the fit (C4 step 0.302 -> 0.333 ms: the 1024-lane clamp workgroups and the fit
-// slow each other), 2 = queued after the fit on the side stream
-// the spec ranks' workgroups of a fused reduce launch go behind the reduce's workgroups
-// (1) or in front of them (0)
-#ifndef KCC_RED_RANKS_LAST
-#define KCC_RED_RANKS_LAST 1
-#endif
-#ifndef KCC_RED_RANKS_LAST_MIN
-#define KCC_RED_RANKS_LAST_MIN (16LL << 20)  // containers of the launch
-#endif
-#ifndef KCC_CLAMP_CONCURRENT
-#define KCC_CLAMP_CONCURRENT 0
-#endif
+// the spec ranks' workgroups of a fused reduce launch go behind the reduce's workgroups on
+// launches of at least this many containers, in front of them on shorter ones
+constexpr int64_t RED_RANKS_LAST_MIN = (int64_t)16 << 20;
 
 // The fit's node stream (FitGroupA / FitGroup records) holds the rows that can contribute
 // to the fast sum Σ min(findMin(qc, qm), P): fast-bound rows with free CPU, free memory
@@ -400,19 +349,17 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             SlowNode* slow, int64_t* slow_list, int64_t n_specs, ClampWork cw,
                             unsigned long long* counters, int chunk, int64_t row0,
                             int64_t call_nodes, hipStream_t s, bool dense = false,
-                            const PlaceArgs* place = nullptr, int32_t* fast_cl = nullptr,
-                            uint32_t* gvmin = nullptr);
+                            const PlaceArgs* place = nullptr, int32_t* fast_cl = nullptr);
 // Clamp in the fit (fast_cl != nullptr; one node chunk, S <= CLAMP_LDS_SPECS, not dense):
 // node_prep streams each row's clamp value (allocatable pods - pod count, CC:135) beside
 // its FitGroupA (fast_cl[row position]) and builds no clamp tables; the fit computes the
 // reference's x >= P ? clamp : x itself (5 VALU per node x wave instead of 3) and
 // subtracts counters[CNT_CLAMP_ALL] from every normal spec; no clamp_apply launch.  The
 // choice for small shards, where clamp_apply's fixed cost exceeds the fit's extra issue.
-#ifndef KCC_CLAMP_IN_FIT_PAIRS
-#define KCC_CLAMP_IN_FIT_PAIRS 1100000000LL  // node rows x specs at most: the C4 8-way (5.1e8) and 4-way (1.0e9) shards
-#endif
+// node rows x specs at most: the C4 8-way (5.1e8) and 4-way (1.0e9) shards
+constexpr int64_t CLAMP_IN_FIT_PAIRS = 1100000000LL;
 inline bool clamp_in_fit_auto(int64_t n_nodes, int64_t n_specs) {
-  return n_specs <= CLAMP_LDS_SPECS && n_nodes * n_specs <= KCC_CLAMP_IN_FIT_PAIRS;
+  return n_specs <= CLAMP_LDS_SPECS && n_nodes * n_specs <= CLAMP_IN_FIT_PAIRS;
 }
 
 // partial[0..S) += Σ_i q(i,s), partial[S..2S) += #div-by-zero rows (internal order).
@@ -420,9 +367,8 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
                       const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, uint32_t* queue, int chunk,
-                      int64_t grid_nodes, hipStream_t s, const int32_t* fast_cl = nullptr,
-                      const uint32_t* gvmin = nullptr, bool count_skips = false,
-                      const FinArgs* fin = nullptr);
+                      int64_t grid_nodes, hipStream_t s, const unsigned long long* faults,
+                      const int32_t* fast_cl = nullptr, const FinArgs* fin = nullptr);
 // the fit's work queues: fit_queue_words(S) uint32 (a 64-B line per spec column of 256 and
 // sub-queue), zero before the first launch (each launch leaves them zero)
 constexpr int64_t FIT_QSUBS_MAX = 32;

@@ -108,9 +108,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
 // DPP; out-of-row lanes read 0 (bound_ctrl), rows masked off keep their value), the two
 // scans interleaved so every DPP read is >= 2 wait states after the write it reads.
 // 12 VALU per value instead of 30 (zeroed DPP move targets, moves, 64-bit add).
-#ifndef KCC_RED_ASM_SCAN
-#define KCC_RED_ASM_SCAN 1  // C4 reduce 136.5 -> 134.3 us (A/B in one process, outputs identical)
-#endif
+// (C4 reduce 136.5 -> 134.3 us against the compiler's scan, A/B in one process, outputs
+// identical)
 // gfx950 (as gfx942) needs 2 wait states between a VALU write of VCC and a VALU read of it
 // (LLVM puts an s_nop 1 between v_sub_co_u32 and v_subb_co_u32): one after each low half.
 #define KCC_SCAN2_STEP(ctl)                                 \
@@ -121,7 +120,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
   "s_nop 1\n\t"                                             \
   "v_addc_co_u32_dpp %3, vcc, %3, %3, vcc " ctl "\n\t"
 __device__ __forceinline__ void wave_incl_scan2_u64(uint64_t& a, uint64_t& b) {
-#if KCC_RED_ASM_SCAN
   uint32_t al = (uint32_t)a, ah = (uint32_t)(a >> 32), bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
   asm volatile("s_nop 1\n\t"
                KCC_SCAN2_STEP("row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0")
@@ -136,10 +134,6 @@ __device__ __forceinline__ void wave_incl_scan2_u64(uint64_t& a, uint64_t& b) {
                : "vcc");
   a = (uint64_t)ah << 32 | al;
   b = (uint64_t)bh << 32 | bl;
-#else
-  a = wave_incl_scan_u64(a);
-  b = wave_incl_scan_u64(b);
-#endif
 }
 
 // CSR offset of node j relative to the wave range start, clamped into int32.
@@ -159,22 +153,10 @@ __device__ __forceinline__ int32_t rel_ptr(const int64_t* __restrict__ ptr, int6
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
-#ifndef KCC_RED_XCD_MAP
-#define KCC_RED_XCD_MAP 0
-#endif
-#ifndef KCC_RED_STORE_AFTER
-#define KCC_RED_STORE_AFTER 0  // pending-block stores behind (1) or ahead of (0) the prefetch
-#endif
-#ifndef KCC_RED_PRIO
-#define KCC_RED_PRIO 0  // progress-based s_setprio in the tile loop (A/B knob, below)
-#endif
-// cache policy of the container loads (A/B knob; 2 nt, 16 sc1, 18 nt sc1).  Measured
-// (round 3, one process, outputs identical): C4 reduce default 130.5 us, nt 181.8, sc1
-// 183.5, nt sc1 181.5; the 8-way shard 19.5 / 32.3 / 25.2 / 32.2 us: the 16-B lane loads
-// of a wave coalesce in L1, which every non-default policy bypasses
-#ifndef KCC_RED_LOAD_CPOL
-#define KCC_RED_LOAD_CPOL 0
-#endif
+// Container loads use the default cache policy.  Measured (round 3, one process, outputs
+// identical): C4 reduce default 130.5 us, nt 181.8, sc1 183.5, nt sc1 181.5; the 8-way
+// shard 19.5 / 32.3 / 25.2 / 32.2 us: the 16-B lane loads of a wave coalesce in L1, which
+// every non-default policy bypasses
 
 // RED_IPL consecutive 64-bit values of one array for this lane: RED_IPL / 2 16-B
 // range-checked buffer loads (outside the descriptor's range they read 0), so the
@@ -187,7 +169,7 @@ __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff
 #pragma unroll
   for (int h = 0; h < RED_IPL / 2; ++h) {
     const u64x2 v = __builtin_bit_cast(
-        u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16 * h, soff, KCC_RED_LOAD_CPOL));
+        u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16 * h, soff, 0));
     x[2 * h] = v.x;
     x[2 * h + 1] = v.y;
   }
@@ -227,22 +209,13 @@ __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff
 // dispatched before it).  No atomics, nothing to zero between launches.
 constexpr uint32_t RED_OOB_OFFSET = 0x7ffffff0u;  // > any output's range (n_nodes < 2^28)
 [[maybe_unused]] constexpr uint32_t RED_SPIN_MAX = 1u << 18;       // look-back polls before a wait gives up
-// Look-back publication (KCC_RED_LB_MODE, A/B knob):
-//   2 (default) = tagged words: each 64-bit value of the piece travels as two 64-bit
-//     words {tag:32 | half:32}, stored by 2 x NA lanes as relaxed agent-scope atomics; the
-//     consumer polls the words until every tag matches and assembles the halves.  Every
-//     word is single-copy atomic and validates itself, so no ordering between the stores
-//     is needed at all — exact under the HIP memory model, without fences or a
-//     vmcnt(0) drain;
-//   1 = release / acquire on a separate tag word (buffer_wbl2 sc1 at the release, an L2
-//     invalidate at the acquire): exact too, but measured 2.3x slower at C4 (0.125 ->
-//     0.290 ms; 8-way shard 0.022 -> 0.096 ms, r04b): every publishing wave writes back
-//     its XCD's L2;
-//   0 = round 3's form: relaxed agent-scope stores, s_waitcnt vmcnt(0), then the tag; a
-//     compiler barrier after the poll (relies on the hardware completing in order).
-#ifndef KCC_RED_LB_MODE
-#define KCC_RED_LB_MODE 2
-#endif
+// Look-back publication: tagged words.  Each 64-bit value of the piece travels as two
+// 64-bit words {tag:32 | half:32}, stored by 2 x NA lanes as relaxed agent-scope atomics;
+// the consumer polls the words until every tag matches and assembles the halves.  Every
+// word is single-copy atomic and validates itself, so no ordering between the stores is
+// needed at all — exact under the HIP memory model, without fences or a vmcnt(0) drain.
+// (Measured and deleted, DESIGN.md §10: a release / acquire tag word, 2.3x slower at C4 —
+// every publishing wave wrote back its XCD's L2; round 3's relaxed stores + vmcnt(0) + tag.)
 constexpr uint64_t RED_WORD_TAG = 0x4B43C0DEull << 32;  // upper half of a published word
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
@@ -274,25 +247,11 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
   const int64_t n_nodes = a.n_nodes, c0 = a.c0, n_cont = a.c_end;
   const int32_t range = a.range;
   const int64_t* __restrict__ ptr = a.ptr;
-  // wave index made provably uniform (T20: no waterfall loops around the buffer ops)
-#if KCC_RED_XCD_MAP
-  // A/B knob (variant builds only): the workgroups of one XCD (blockIdx % 8) take one
-  // contiguous eighth of the ranges (a bijection of the grid), so each XCD's L2 and
-  // translation caches see one eighth of the arrays.  Measured (round 3, r03t): C4 130.8
-  // -> 131.4 us, its 8-way shard 19.7 -> 18.8 us.  Not shipped: a wave's look-back
-  // predecessor may then be dispatched after it, so the waits are safe only while every
-  // wave of the launch is resident at once, which kernels of another stream or process
-  // sharing the GPU can prevent (dispatch order = range order rules that out)
-  const uint32_t rb_ = blockIdx.x - (uint32_t)red0, nb_ = gridDim.x - (uint32_t)ra.n_blocks;
-  const uint32_t xq_ = rb_ & 7u, q8_ = nb_ >> 3, r8_ = nb_ & 7u;
-  const uint32_t lb_ = xq_ * q8_ + (xq_ < r8_ ? xq_ : r8_) + (rb_ >> 3);
-  const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)(lb_ * RED_WAVES_PER_BLOCK +
-                                                             (threadIdx.x >> 6)));
-#else
+  // wave index made provably uniform (T20: no waterfall loops around the buffer ops).
+  // Range order = dispatch order: a wave's look-back predecessors are dispatched before it
   const int32_t w = __builtin_amdgcn_readfirstlane((int32_t)((blockIdx.x - red0) *
                                                              RED_WAVES_PER_BLOCK +
                                                              (threadIdx.x >> 6)));
-#endif
   // containers [c0, n_cont): absolute indices, like the offsets in ptr (node indices
   // are local to the launch)
   const int64_t wb = c0 + (int64_t)w * range;
@@ -308,14 +267,14 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
   for (int k = 0; k < NA; ++k)  // whole 16-B pairs only: an odd last item is fixed up below
     rs[k] = __builtin_amdgcn_make_buffer_rsrc((void*)(in[k] + wb), (short)0,
                                               (int)((len & ~1) * 8), 0x00020000);
-  // a ring of KCC_RED_PREFETCH + 1 tiles in registers: KCC_RED_PREFETCH in flight while
-  // one is reduced (static ring indices: the tile loop below is unrolled over the ring).
+  // a ring of RED_PREFETCH + 1 tiles in registers: RED_PREFETCH in flight while one is
+  // reduced (static ring indices: the tile loop below is unrolled over the ring).
   // The first tiles' loads go out first: they depend on the range alone, while the node
   // search below is a chain of dependent loads
-  constexpr int RING = KCC_RED_PREFETCH + 1;
+  constexpr int RING = RED_PREFETCH + 1;
   uint64_t xs[RING][NA][RED_IPL];
 #pragma unroll
-  for (int u = 0; u < KCC_RED_PREFETCH; ++u)
+  for (int u = 0; u < RED_PREFETCH; ++u)
 #pragma unroll
     for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 8 * RED_IPL, u * RED_TILE * 8, xs[u][k]);
   __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink them below the search)
@@ -390,17 +349,12 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
   };
 
   auto tile = [&](uint64_t (&x)[NA][RED_IPL], uint64_t (&nx)[NA][RED_IPL], const int32_t tb) {
-#if !defined(KCC_DIAG_RED_NOSTORE) && !KCC_RED_STORE_AFTER
+#ifndef KCC_DIAG_RED_NOSTORE
     issue_pending();
 #endif
 #pragma unroll
     for (int k = 0; k < NA; ++k)
-      load_quad(rs[k], lane * 8 * RED_IPL, (tb + KCC_RED_PREFETCH * RED_TILE) * 8, nx[k]);
-#if !defined(KCC_DIAG_RED_NOSTORE) && KCC_RED_STORE_AFTER
-    // behind the prefetch loads: the next tile's wait for them (vmcnt, in order) does not
-    // include these stores' acknowledgements
-    issue_pending();
-#endif
+      load_quad(rs[k], lane * 8 * RED_IPL, (tb + RED_PREFETCH * RED_TILE) * 8, nx[k]);
 #ifdef KCC_DIAG_RED_LOADONLY
 #pragma unroll
     for (int k = 0; k < NA; ++k)
@@ -511,32 +465,11 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   };
-#if KCC_RED_PRIO
-  // progress-based wave priority (A/B knob): the CU's arbiter issues the oldest wave
-  // first among equal priorities, so the waves dispatched first ran ahead and the last
-  // ones finished alone (a bandwidth tail); here a wave's priority falls as its range
-  // advances (3 in its first quarter ... 0 in its last), so the waves that are behind win
-  // the arbitration
-  int32_t prio_lvl = 3;
-  __builtin_amdgcn_s_setprio(3);
-#endif
   for (int32_t tb = 0; tb < len; tb += RING * RED_TILE) {
-#if KCC_RED_PRIO
-    const int32_t lvl = 3 - (int32_t)(((int64_t)tb * 4) / len);  // wave-uniform
-    if (lvl != prio_lvl) {
-      prio_lvl = lvl;
-      if (lvl == 2) __builtin_amdgcn_s_setprio(2);
-      else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-    }
-#endif
 #pragma unroll
     for (int u = 0; u < RING; ++u)
-      if (tb + u * RED_TILE < len) tile(xs[u], xs[(u + KCC_RED_PREFETCH) % RING], tb + u * RED_TILE);
+      if (tb + u * RED_TILE < len) tile(xs[u], xs[(u + RED_PREFETCH) % RING], tb + u * RED_TILE);
   }
-#if KCC_RED_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
 #if defined(KCC_DIAG_RED_LOADONLY) || defined(KCC_DIAG_RED_NOSTORE)
   if (carry[0] == 0x123456789ull) out[0][0] = carry[NA - 1] ^ res[0];
 #endif
@@ -560,7 +493,6 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
   // starts at the next range (no consumer).
   uint64_t* const rec = a.tail + (int64_t)w * RED_TAIL_WORDS;
   const bool publish = wb + len < n_cont && open_start < len;
-#if KCC_RED_LB_MODE == 2
   static_assert(2 * NA <= RED_TAIL_WORDS, "two tagged words per value");
   if (publish && lane < 2 * NA) {  // lane j: half (j & 1) of value j >> 1
     uint64_t v = carry[0];
@@ -569,19 +501,6 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
     const uint64_t word = RED_WORD_TAG | ((lane & 1) ? v >> 32 : v & 0xffffffffull);
     __hip_atomic_store(rec + lane, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-#else
-  if (publish && lane == 0) {
-#pragma unroll
-    for (int k = 0; k < NA; ++k)
-      __hip_atomic_store(rec + k, carry[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#if KCC_RED_LB_MODE == 1
-    __hip_atomic_store(rec + RED_TAIL_TAG, RED_TAG_READY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(rec + RED_TAIL_TAG, RED_TAG_READY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-  }
-#endif
   // look-back: node0 began in an earlier range and ended in this one
   if (first_open && cur > node0) {
     uint64_t acc[NA];
@@ -596,7 +515,6 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
       if (wi < w) {
         uint64_t* r = a.tail + wi * RED_TAIL_WORDS;
         bool seen = true;
-#if KCC_RED_LB_MODE == 2
         uint64_t wd[2 * NA];
         uint32_t spins = 0;
         for (;;) {
@@ -627,31 +545,6 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
           for (int j = 0; j < 2 * NA; ++j)
             __hip_atomic_store(r + j, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-#else
-#ifdef KCC_DIAG_RED_GIVEUP
-        seen = false;
-        atomicAdd(&a.faults[FAULT_RED], 1ull);
-#else
-        uint32_t spins = 0;
-        while (__hip_atomic_load(r + RED_TAIL_TAG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-               RED_TAG_READY) {
-          if (++spins >= RED_SPIN_MAX) {
-            atomicAdd(&a.faults[FAULT_RED], 1ull);
-            seen = false;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
-#endif
-#if KCC_RED_LB_MODE == 1
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // synchronizes with the release
-#else
-        asm volatile("" ::: "memory");
-#endif
-#pragma unroll
-        for (int k = 0; k < NA; ++k) v[k] = __hip_atomic_load(r + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (seen) __hip_atomic_store(r + RED_TAIL_TAG, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
       }
 #pragma unroll
       for (int k = 0; k < NA; ++k) acc[k] += wave_sum_u64(v[k]);
@@ -759,36 +652,22 @@ __device__ __forceinline__ uint32_t count_lt64(const uint32_t* __restrict__ a, u
 #define KCC_NODE_PREP_BLOCK 1024
 static_assert(CLAMP_PASS_ROWS_MIN == KCC_NODE_PREP_BLOCK, "a pass is 1, 2 or 4 rows per thread");
 static_assert(2 * CLAMP_PASS_ROWS_MAX <= 0xffff, "record ranks packed in 16 bits");
-// diagnostic timing builds only (results are wrong): KCC_DIAG_NP bit 0 drops the clamp
-// tables' global atomics (the cells stay live), bit 1 the x-group / y-block counts, bit 2
-// the searches, bit 3 the stream writes
-#ifndef KCC_DIAG_NP
-#define KCC_DIAG_NP 0
-#endif
 __device__ __forceinline__ void np_atomic(int64_t* p, int64_t w) {
-  if (KCC_DIAG_NP & 1) {
-    if (w == 0x5a5a5a5a5a5a5a5all) *p = w;
-  } else {
-    atomic_add_u64(reinterpret_cast<uint64_t*>(p), (uint64_t)w);
-  }
+  atomic_add_u64(reinterpret_cast<uint64_t*>(p), (uint64_t)w);
 }
 static_assert(CLAMP_LDS_SPECS % KCC_NODE_PREP_BLOCK == 0, "node_prep table fill");
-#ifndef KCC_NODE_PREP_GRID
-#define KCC_NODE_PREP_GRID 1024  // workgroups at most (one resident round; each fills its LDS tables once)
-#endif
+// workgroups at most (one resident round; each fills its LDS tables once)
+constexpr int64_t NODE_PREP_GRID = 1024;
 constexpr int NP_C_CELLS = (int)((CLAMP_LDS_SPECS / 64 + 2) * (CLAMP_LDS_SPECS / 64 + 2));
-// dynamic LDS: the search tables (cs u32, ms i64, 2 x u16) and the private C table, when
-// S <= CLAMP_LDS_SPECS
-#ifndef KCC_NP_CPRIV
-#define KCC_NP_CPRIV 1  // C summed in LDS per workgroup (one node_prep workgroup per CU)
-#endif
+// dynamic LDS: the search tables (cs u32, ms i64, 2 x u16) and the private C table (C summed
+// in LDS per workgroup: one node_prep workgroup per CU), when S <= CLAMP_LDS_SPECS
 static_assert(CLAMP_LDS_SPECS == 4096, "node_prep's LDS member tables are 64 x 64");
 constexpr size_t NP_OFF_CS = 8 * (size_t)CLAMP_LDS_SPECS;            // ms i64, then cs u32
 constexpr size_t NP_OFF_MK = NP_OFF_CS + 4 * (size_t)CLAMP_LDS_SPECS;  // 64 x 64 u64 masks
 constexpr size_t NP_OFF_CK = NP_OFF_MK + 8 * 64 * 64;                 // 64 x 65 u8
 constexpr size_t NP_OFF_CJ = NP_OFF_CK + 64 * 65;                     // 64 x 65 u8
 constexpr size_t NP_OFF_C = (NP_OFF_CJ + 64 * 65 + 15) / 16 * 16;     // private C
-constexpr size_t NODE_PREP_LDS = NP_OFF_C + (KCC_NP_CPRIV ? 8 * (size_t)NP_C_CELLS : 0);
+constexpr size_t NODE_PREP_LDS = NP_OFF_C + 8 * (size_t)NP_C_CELLS;
 constexpr int NP_BINS = 2 * (int)CLAMP_BIN_T_MAX;
 constexpr uint32_t NP_ST_MAX = 16;  // LDS search tables sample up to 16 x 4096 specs
 constexpr size_t NODE_PREP_LDS_SRCH = NP_OFF_MK;  // the search tables alone (S > 4096)
@@ -817,7 +696,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
                                  int64_t S, ClampWork cw,
                                  unsigned long long* __restrict__ counters,
                                  int32_t chunk, int32_t dense, int64_t pass0, PlaceArgs pa,
-                                 int32_t* __restrict__ fast_cl, uint32_t* __restrict__ gvmin) {
+                                 int32_t* __restrict__ fast_cl) {
   static_assert(!NC || MODE == 2, "the clamp in the fit: S <= CLAMP_LDS_SPECS only");
   if ((int32_t)blockIdx.x < pa.n_blocks) {  // spec_place's workgroups, in front (MODE 2)
     spec_place_body(pa, blockIdx.x);
@@ -851,9 +730,6 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   __shared__ uint32_t np_tot;
   __shared__ uint32_t np_bcnt[NP_BINS];                 // binned records per bin (this pass)
   __shared__ uint32_t np_bstart[NP_BINS];               // their exclusive prefix
-  // KCC_FIT_MSKIP: this pass's stream rows' V = floor(fm / P) (u32, saturated), by stream
-  // position within the pass, for the groups' minima (gvmin)
-  __shared__ uint32_t np_v[KCC_FIT_MSKIP ? (int)PR : 1];
   // the class counts from spec_rank's per-block counts (spec_place may run beside this
   // launch): every wave sums them (one load per lane at S <= 4096)
   uint64_t cls_n = 0;  // class A | class B << 32
@@ -867,7 +743,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   const bool slow_all = nN < S;                    // exact-path specs exist
   const int64_t T = (nN + 63) / 64, W = T + 2;
   // T <= CLAMP_BIN_T_MAX (always at S <= 4096: MODE 2 carries no table atomics)
-  const bool binned = (MODE == 2 && KCC_CLAMP_BINNED) || clamp_binned(S);
+  const bool binned = MODE == 2 || clamp_binned(S);
   const int NB = (int)(2 * T);                     // bins: x-groups, then y-blocks
   // this workgroup's copies of the tables: workgroups are dealt round-robin over the XCDs
   int64_t* Cc = cw.C + (int64_t)(bid % C_COPIES) * cw.c_stride;
@@ -886,7 +762,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
   uint8_t* cj_l = np_lds + NP_OFF_CJ;
   unsigned long long* c_l = reinterpret_cast<unsigned long long*>(np_lds + NP_OFF_C);
   constexpr bool lds = MODE == 2;  // S <= CLAMP_LDS_SPECS: T <= 64 and W * W <= NP_C_CELLS
-  constexpr bool cpriv = KCC_NP_CPRIV && lds;
+  constexpr bool cpriv = lds;
   // the search tables in LDS hold every st-th request (st = 1 when S <= 4096; a search
   // ends with the st - 1 requests of its bucket from memory), up to NP_ST_MAX
   constexpr bool srch = MODE >= 1;
@@ -978,7 +854,6 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
     uint32_t r_fc[SUB];
     int32_t r_P[SUB];
     int32_t r_cl[SUB];  // NC: the clamp value of a streamed row
-    uint32_t r_v[SUB];  // KCC_FIT_MSKIP: min(floor(fm / P), 2^32 - 2) of a streamed row
     unsigned long long sbal[SUB];
     uint32_t pk1[SUB], pk2[SUB], pk3[SUB];
     uint64_t always_sum = 0;
@@ -1055,14 +930,11 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       const int64_t wfull = Penc - (int64_t)cl_q;  // contribution = min(x, Penc) - w when clamped
       if (ok && nN > 0 && P <= 0) always_sum += (uint64_t)wfull;  // x >= P for every spec
       r_cl[q] = cl_q;
-      const double rP = recip_up_f64(P > 0 ? (uint64_t)P : 1ull);
-      const int64_t V0 = (int64_t)((double)r_fm[q] * rP);  // floor(fm / P): exact (§5)
-      // saturated at 2^32 - 2: 2^32 - 1 is the fit's "no skip" m_max (m >= 2^32 - 1), which
-      // must never compare <= a group's V_min
-      r_v[q] = P > 0 ? (V0 < 0xfffffffell ? (uint32_t)V0 : 0xfffffffeu) : 0u;
       if constexpr (NC) {
         pk1[q] = pk2[q] = pk3[q] = 0u;
       } else {
+      const double rP = recip_up_f64(P > 0 ? (uint64_t)P : 1ull);
+      const int64_t V0 = (int64_t)((double)r_fm[q] * rP);  // floor(fm / P): exact (§5)
       const uint32_t U0 = (uint32_t)((double)r_fc[q] * rP);
       const bool act = ok && nN > 0 && P > 0 && wfull != 0 && U0 >= cmin && V0 >= mmin;
       const int64_t w = act ? wfull : 0;  // |w| <= 2^21
@@ -1080,10 +952,6 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
         b = ib - 4096u;
         L += L == 4095u && cs_l[0] <= U ? 1u : 0u;  // the last entry (slot 0)
         b += b == 4095u && ms_l[0] <= V ? 1u : 0u;
-        if (KCC_DIAG_NP & 4) {  // diagnostic: no searches
-          L = w ? 1 + (U & 2047) : 0;
-          b = w ? 1 + ((uint32_t)V & 2047) : 0;
-        }
         if (!lds) {  // st > 1: #{a <= v} = c st + #{j < st - 1 : a[c st + j] <= v} (a[(c + 1) st - 1] > v)
           L *= st;
           b *= st;
@@ -1105,9 +973,7 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       // y-block GY whose x-group < GX} (ry > 0, GY < T)
       const uint32_t GX = L >> 6, rx = L & 63u, GY = b >> 6, ry = b & 63u;
       uint32_t k, j;
-      if (KCC_DIAG_NP & 2) {
-        k = j = 1;
-      } else if (lds) {  // the members below y-block b >> 6, + those in it below b
+      if (lds) {  // the members below y-block b >> 6, + those in it below b
         const uint32_t gx = GX < 63u ? GX : 63u, yb = GY < 63u ? GY : 63u;
         const uint64_t mk = mk_l[mk_at(gx, yb)];
         k = (uint32_t)ck_l[gx * 65 + GY] + (uint32_t)__popcll(mk & ((1ull << ry) - 1ull));
@@ -1190,9 +1056,8 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       const uint64_t sb0 = np_base + before;
       const uint32_t tot = np_tot;
       const uint32_t pad = (tot + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP - tot;
-      auto put = [&](uint64_t pos, uint64_t fmv, uint32_t fcv, uint32_t Pv, int32_t clv, uint32_t vv) {
+      auto put = [&](uint64_t pos, uint64_t fmv, uint32_t fcv, uint32_t Pv, int32_t clv) {
         const int kk = (int)(pos % FIT_GROUP);
-        if (KCC_FIT_MSKIP) np_v[pos - np_base] = vv;
         if (NC) fast_cl[pos] = clv;
         FitGroupA& a = fast_a[pos / FIT_GROUP];
         a.fm[kk] = fmv;
@@ -1209,9 +1074,9 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       uint64_t* prec = cw.rec + pass * (2 * PR);
 #pragma unroll
       for (int q = 0; q < SUB; ++q) {
-        if (!(KCC_DIAG_NP & 8) && ((sbal[q] >> lane) & 1ull))  // P <= 0 streams only in the dense layout, as P = 0
+        if ((sbal[q] >> lane) & 1ull)  // P <= 0 streams only in the dense layout, as P = 0
           put(sb0 + done + (uint32_t)__popcll(sbal[q] & ((1ull << lane) - 1ull)), r_fm[q], r_fc[q],
-              r_P[q] > 0 ? (uint32_t)r_P[q] : 0u, r_cl[q], r_v[q]);
+              r_P[q] > 0 ? (uint32_t)r_P[q] : 0u, r_cl[q]);
         done += (uint32_t)__popcll(sbal[q]);
         const uint32_t c2 = pk1[q] & 0x1fffu, c3 = (pk1[q] >> 13) & 0x1fffu;
         if (c2 | c3) {
@@ -1221,18 +1086,9 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
           if (c3) prec[np_bstart[(pk3[q] >> 9) & 0x1ffu] + ((pk2[q] >> 13) & 0x1fffu)] = wbits | c3;
         }
       }
-      if (threadIdx.x < pad) put(np_base + tot + threadIdx.x, 0ull, 0u, 0u, 0, 0u);  // the last group's padding
+      if (threadIdx.x < pad) put(np_base + tot + threadIdx.x, 0ull, 0u, 0u, 0);  // the last group's padding
     }
     __syncthreads();  // np_wc / np_base / np_bstart are rewritten by the next pass
-    if (KCC_FIT_MSKIP) {  // each stream group's smallest V (padding rows: 0, no skip)
-      const uint32_t ng = (np_tot + FIT_GROUP - 1) / FIT_GROUP;
-      if (threadIdx.x < ng) {
-        uint32_t vm = 0xffffffffu;
-#pragma unroll
-        for (int e = 0; e < FIT_GROUP; ++e) vm = min(vm, np_v[threadIdx.x * FIT_GROUP + e]);
-        gvmin[np_base / FIT_GROUP + threadIdx.x] = vm;
-      }
-    }
     KCC_TL(bid % 1024, 5);
   }
   if (cpriv && !NC) {  // the private C into this workgroup's device copy: its non-zero cells
@@ -1634,11 +1490,7 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
     counters[CNT_SPECS_B] = nB;
   }
   if (!in) return;
-  // class A by memory request (KCC_FIT_MSKIP: a wave's largest request is its last lane's):
-  // the class-B specs (m < 2^18 <= every class-A m) hold y-ranks [0, nB), so y - nB is a
-  // permutation of [0, nA)
-  const int64_t posA = KCC_FIT_MSKIP ? (int64_t)cw.rank[S + i] - (int64_t)nB : (int64_t)pA + rA;
-  const int64_t pos = cls == SPEC_A ? posA
+  const int64_t pos = cls == SPEC_A ? (int64_t)pA + rA
                     : cls == SPEC_B ? (int64_t)nA + pB + rB
                                     : nN + (qb * 64 - pA - pB) + (lane - rA - rB);
   SpecRec rec;
@@ -1652,7 +1504,8 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   sp.rec[pos] = rec;
   sp.perm[pos] = (int32_t)i;
   partial[i] = 0;
-  partial[S + i] = 0;
+  // (spec_place runs after this step's reduce: its look-back give-ups are in the words)
+  partial[S + i] = device_faulted(pa.faults) ? (int64_t)SPEC_FAULT_MARK : 0;
   if (!normal) return;
   cw.dperm[x] = (int32_t)pos;
 }
@@ -1683,13 +1536,8 @@ __host__ __device__ inline bool clamp_c_full(int64_t T) { return (T + 2) * (T + 
 // a workgroup scan of the counts gives the window's records a flat numbering, and each
 // wave's lanes take consecutive records (coalesced loads; a lane per pass re-fetched a
 // whole line per 8-B record: 48 us at C4), CP_RB loads in flight per lane.
-#ifndef KCC_DIAG_CP
-#define KCC_DIAG_CP 0  // diagnostic timing builds only: bit 0 drops the adds, bit 1 the records
-#endif
 constexpr int CP_PW = 4096;
-#ifndef KCC_CP_SPLIT
-#define KCC_CP_SPLIT 4  // workgroups per bin at most (binned clamp tables)
-#endif
+constexpr int64_t CP_SPLIT = 4;  // workgroups per bin at most (binned clamp tables)
 constexpr int CP_RB = 8;  // records per thread in flight
 __device__ __forceinline__ void clamp_consume_bin(const ClampWork& cw, int64_t bin, uint64_t* tab,
                                                   uint32_t* w_lo, uint32_t* w_off, uint64_t* scratch,
@@ -1783,16 +1631,14 @@ __device__ __forceinline__ void clamp_consume_bin(const ClampWork& cw, int64_t b
     auto add_batch = [&](const uint64_t (&rv)[CP_RB], uint32_t jb) {
 #pragma unroll
       for (int u = 0; u < CP_RB; ++u)
-        if (KCC_DIAG_CP & 1) {  // diagnostic timing builds: no LDS atomics
-          if (rv[u] == 0x5a5a5a5a5a5a5a5aull) tab[0] = rv[u];
-        } else if (jb + (uint32_t)(64 * u + lane) < J1)
+        if (jb + (uint32_t)(64 * u + lane) < J1)
           atomicAdd(reinterpret_cast<unsigned long long*>(&tab[(uint32_t)rv[u]]),
                     (unsigned long long)(int64_t)(int32_t)(rv[u] >> 32));
     };
     const uint32_t step = 64u * CP_RB;
     uint64_t ra[CP_RB], rb[CP_RB];
     load_batch(ra, J0);
-    for (uint32_t jb = J0; jb < ((KCC_DIAG_CP & 2) ? 0u : J1); jb += 2 * step) {
+    for (uint32_t jb = J0; jb < J1; jb += 2 * step) {
       load_batch(rb, jb + step);
       add_batch(ra, jb);
       load_batch(ra, jb + 2 * step);
@@ -1936,18 +1782,17 @@ __device__ __forceinline__ void clamp_apply_bin(const ClampWork& cw, int64_t S,
   KCC_TL(1024 + blockIdx.x % 1024, 4);
 }
 
-// The fused finalize (clamp_apply_kernel, and the fit when the clamp correction runs beside
-// it): every wave's atomics into partial are performed (vmcnt counts the stores and atomics
-// too on gfx9) before the workgroup arrives; the last of the expected arrivals reads partial
-// at agent scope and writes the totals in caller order.  Every thread of the workgroup calls.
+// The fused finalize (clamp_apply_kernel): every wave's atomics into partial are performed
+// (vmcnt counts the stores and atomics too on gfx9) before the workgroup arrives; the last
+// of the launch's workgroups to arrive reads partial at agent scope and writes the totals
+// in caller order.  Every thread of the workgroup calls.
 __device__ void fused_finalize(const FinArgs& fin, int64_t S, const int64_t* partial) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   __shared__ uint32_t last_s;
-  const uint32_t expect = fin.expect ? fin.expect : gridDim.x;
   if (threadIdx.x == 0)
     last_s = __hip_atomic_fetch_add(fin.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-             expect - 1u;
+             gridDim.x - 1u;
   __syncthreads();
   if (!last_s) return;
   if (threadIdx.x == 0) __hip_atomic_store(fin.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1970,8 +1815,9 @@ __device__ void fused_finalize(const FinArgs& fin, int64_t S, const int64_t* par
 #pragma unroll
     for (int k = 0; k < FIN_PER; ++k) {
       if (i0 + (int64_t)k * nt >= S) break;
-      fin.totals[dst[k]] = e[k] != 0 || faulted ? 0 : t[k];
-      fin.spec_err[dst[k]] = faulted ? SPEC_ERR_FAULT : e[k] != 0 ? SPEC_ERR_DIV0 : 0;
+      const bool fk = faulted || (uint64_t)e[k] >= SPEC_FAULT_MARK;
+      fin.totals[dst[k]] = e[k] != 0 || fk ? 0 : t[k];
+      fin.spec_err[dst[k]] = fk ? SPEC_ERR_FAULT : e[k] != 0 ? SPEC_ERR_DIV0 : 0;
     }
   }
 }
@@ -2069,48 +1915,16 @@ __device__ __forceinline__ double min_f64_s(double x, double p) {
 
 constexpr int FIT_SPW = 256;           // specs per 256-thread workgroup (one column per wave)
 constexpr int FIT_CHUNK_GROUPS = 128;  // 1024 nodes: |sum of contributions| <= 2^30 in i32
-#ifndef KCC_FIT_QCHUNK
-#define KCC_FIT_QCHUNK 32  // node groups per claim from a sub-queue
-#endif
-constexpr uint32_t FIT_QCHUNK = KCC_FIT_QCHUNK;
+constexpr uint32_t FIT_QCHUNK = 32;  // node groups per claim from a sub-queue
 static_assert(FIT_QCHUNK >= 2 && FIT_QCHUNK <= FIT_CHUNK_GROUPS, "claims sum in i32");
-#ifndef KCC_FIT_QDIV
-#define KCC_FIT_QDIV 2  // guided claims: (what remains of the segment) / (QDIV x its workgroups)
-#endif
-#ifndef KCC_FIT_NC_VLOAD
-// the clamp-in-fit class-A loop's clamp values by vector loads (5 VALU per node) rather than
-// scalar loads (6: the select reads one scalar operand at most, vcc included, so each
-// clamp value is moved into a VGPR).  Measured (round 3, bench emulation, base / vector /
-// base / vector): C4 8-way rank 0.0632 / 0.0618 / 0.0631 / 0.0620 ms, 4-way 0.0980 /
-// 0.0965 / 0.0986 / 0.0953 ms (profiles/r03z_ab_clamp_vload.txt)
-#define KCC_FIT_NC_VLOAD 1
-#endif
-#ifndef KCC_FIT_QEST
-#define KCC_FIT_QEST 0  // guided claims sized from the head estimated after the others' claims
-#endif
-#ifndef KCC_FIT_QMIN
-#define KCC_FIT_QMIN 2  // node groups per claim at least (guided claims)
-#endif
-#ifndef KCC_FIT_Q1_DIV
-#define KCC_FIT_Q1_DIV 8  // the static first claim at most share / this (0: qsz); the 8-way C4
-                          // rank: 0.0624 -> 0.0618 ms (r04z), C4 unchanged (its share / 8 > qsz)
-#endif
-#ifndef KCC_FIT_Q_HALVE
-#define KCC_FIT_Q_HALVE 128  // claims of FIT_QCHUNK / 2 when a workgroup's share is below this
-#endif
-#ifndef KCC_FIT_WG_PER_SUB
-#define KCC_FIT_WG_PER_SUB 24  // workgroups per sub-queue at most, about (8 to 32 sub-queues)
-#endif
+constexpr uint32_t FIT_QDIV = 2;   // guided claims: (what remains of the segment) / (QDIV x its workgroups)
+constexpr uint32_t FIT_QMIN = 2;   // node groups per claim at least (guided claims)
+// the static first claim at most share / this: the 8-way C4 rank 0.0624 -> 0.0618 ms (r04z),
+// C4 unchanged (its share / 8 > qsz)
+constexpr uint32_t FIT_Q1_DIV = 8;
+constexpr uint32_t FIT_Q_HALVE = 128;  // claims of FIT_QCHUNK / 2 when a workgroup's share is below this
+constexpr uint32_t FIT_WG_PER_SUB = 24;  // workgroups per sub-queue at most, about (8 to 32 sub-queues)
 constexpr uint32_t FIT_QSUBS = (uint32_t)FIT_QSUBS_MAX;
-#ifndef KCC_FIT_GY_DIV
-// A/B knob: a 1/DIV share of the resident workgroups per column.  Measured (round 3,
-// prepare + run): C4 172 -> 220 / 372 us at DIV 2 / 4, its 8-way shard 57 -> 63 / 83 us:
-// the fit needs its 8 waves per SIMD on small shards too (profiles/r03o_ab_fit_grid.jsonl)
-#define KCC_FIT_GY_DIV 1
-#endif
-#ifndef KCC_FIT_ROUNDS
-#define KCC_FIT_ROUNDS 1  // queue grid: this many rounds of resident workgroups
-#endif
 
 __device__ __forceinline__ double f64_at(const i32x16& v, int k) {
   return __longlong_as_double(((int64_t)(uint32_t)v[2 * k + 1] << 32) | (uint32_t)v[2 * k]);
@@ -2132,15 +1946,10 @@ __device__ __forceinline__ double f64_at(const i32x16& v, int k) {
 // (every workgroup of it has made its last claim by then); the buffer is zeroed once when
 // allocated.
 // 8 waves per SIMD: the register budget that leaves (the compiler otherwise takes ~106
-// SGPRs, 6 waves); the loops stay spill-free (tests/test_isa.py)
-#ifndef KCC_FIT_WAVES_PER_EU
-#define KCC_FIT_WAVES_PER_EU 8
-#endif
-#if KCC_FIT_WAVES_PER_EU > 0
-#define KCC_FIT_ATTR __attribute__((amdgpu_waves_per_eu(KCC_FIT_WAVES_PER_EU)))
-#else
-#define KCC_FIT_ATTR
-#endif
+// SGPRs, 6 waves); the loops stay spill-free (tests/test_isa.py).  Half or a quarter of
+// the resident workgroups per column measured slower (round 3, prepare + run: C4 172 ->
+// 220 / 372 us, its 8-way shard 57 -> 63 / 83 us, profiles/r03o_ab_fit_grid.jsonl)
+#define KCC_FIT_ATTR __attribute__((amdgpu_waves_per_eu(8)))
 // NC: the clamp in the fit (fast_cl, launch_fit) — its own instantiation, so the
 // clamp-correction layout's registers are not the larger loops' (one kernel holding both
 // spilled 52 SGPRs: C4 fit 116 -> 120 us)
@@ -2150,8 +1959,8 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     const FitGroup* __restrict__ fast_b, const SlowNode* __restrict__ slow,
     const int64_t* __restrict__ slow_list, int64_t S, const SpecRec* __restrict__ specs,
     int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t chunk,
-    int32_t gx, int32_t gy, const int32_t* __restrict__ fast_cl, const uint32_t* __restrict__ gvmin,
-    int32_t count_skips, FinArgs fin) {
+    int32_t gx, int32_t gy, const int32_t* __restrict__ fast_cl,
+    const unsigned long long* __restrict__ faults, FinArgs fin) {
   // XCD-aware order (speed only, never correctness): workgroups are dealt round-robin
   // over the 8 XCDs, so give every spec group of one node chunk the same b % 8
   const int32_t b = blockIdx.x, xcd = b & 7, r = b >> 3;
@@ -2181,20 +1990,6 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   const bool wave_b = __any(sr.cls == SPEC_B);
   const bool wave_fast = !wave_exact && !idle;  // sums the node stream
   KCC_TL(2048 + b % 4096, 5);  // (the spec records are in)
-  // KCC_FIT_MSKIP: the wave's largest memory request (class-A specs sit in memory order, so
-  // this is the last active lane's) as u32; 0xffffffff: no skip (m >= 2^32, or no table)
-  uint32_t mmax32 = 0xffffffffu;
-  if (KCC_FIT_MSKIP && gvmin) {
-    uint64_t mm = active ? (uint64_t)m : 0ull;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      const uint64_t o = __shfl_xor(mm, d);
-      mm = o > mm ? o : mm;
-    }
-    mmax32 = mm < 0xffffffffull ? (uint32_t)mm : 0xffffffffu;
-    mmax32 = __builtin_amdgcn_readfirstlane(mmax32);
-  }
-  uint32_t nskip = 0;  // node groups summed without the memory quotient (scalar)
 
   // the node stream node_prep wrote (its length is on the device; 32-bit: < 2^31 groups)
   const uint32_t n_groups = (uint32_t)(counters[CNT_STREAM + chunk] / FIT_GROUP);
@@ -2202,23 +1997,23 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   uint32_t base = 0;        // queue: the segment's start
   uint32_t nxt = 0;         // queue: the claim in flight (wave 0, lane 0); static: next chunk
   // sub-queues: gy if gy < 8, else 8, 16 or 32 (a power of two: whole XCDs each), about
-  // KCC_FIT_WG_PER_SUB workgroups per sub-queue (measured: 56 per line 8 % slower at C4
-  // than 28; fewer than 2 per line lose the balancing)
-  uint32_t nsub = (uint32_t)gy / KCC_FIT_WG_PER_SUB;
+  // FIT_WG_PER_SUB workgroups per sub-queue (measured: 56 per line 8 % slower at C4 than
+  // 28; fewer than 2 per line lose the balancing)
+  uint32_t nsub = (uint32_t)gy / FIT_WG_PER_SUB;
   nsub = nsub <= 8u ? 8u : (nsub >= FIT_QSUBS ? FIT_QSUBS : 1u << (31 - __builtin_clz(nsub)));
   if ((uint32_t)gy < nsub) nsub = (uint32_t)gy;
   const uint32_t sub = (uint32_t)by % nsub;
   uint32_t* const qp = queue + ((uint32_t)bx * FIT_QSUBS + sub) * 16u;
   // claim size: halved when a workgroup's share is small (8-way shards of C4: ~35 groups
   // per workgroup; two claims each keep the balancing)
-  const uint32_t qsz = n_groups / (uint32_t)gy < KCC_FIT_Q_HALVE ? FIT_QCHUNK / 2u : FIT_QCHUNK;
-  // the static first claim: qsz, or (KCC_FIT_Q1_DIV) at most a 1/Q1_DIV of a workgroup's
-  // share — the workgroups begin their loops up to ~11 us apart on small shards, and a late
-  // one's static claim was the fit's tail
+  const uint32_t qsz = n_groups / (uint32_t)gy < FIT_Q_HALVE ? FIT_QCHUNK / 2u : FIT_QCHUNK;
+  // the static first claim: qsz, or at most a 1/FIT_Q1_DIV of a workgroup's share — the
+  // workgroups begin their loops up to ~11 us apart on small shards, and a late one's
+  // static claim was the fit's tail
   uint32_t q1 = qsz;
-  if (KCC_FIT_Q1_DIV > 0) {
-    const uint32_t sh = n_groups / (uint32_t)gy / (uint32_t)(KCC_FIT_Q1_DIV > 0 ? KCC_FIT_Q1_DIV : 1);
-    q1 = sh < q1 ? (sh > (uint32_t)KCC_FIT_QMIN ? sh : (uint32_t)KCC_FIT_QMIN) : q1;
+  {
+    const uint32_t sh = n_groups / (uint32_t)gy / FIT_Q1_DIV;
+    q1 = sh < q1 ? (sh > FIT_QMIN ? sh : FIT_QMIN) : q1;
   }
   __shared__ uint32_t q_slot[2];
   // lane 0 of wave 0 issues the claim in asm, so the compiler does not wait for it where
@@ -2231,7 +2026,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
                    : "=v"(nxt) : "v"(qp), "v"(sz) : "memory");
   };
   // guided claims: a claim's size is (what remained of the segment at the workgroup's
-  // current claim) / (2 x its workgroups), between KCC_FIT_QMIN and qsz, so the claims
+  // current claim) / (2 x its workgroups), between FIT_QMIN and qsz, so the claims
   // shrink as the segment drains and the workgroups finish together (fixed claims of
   // qsz left a tail of one to two claims: 10-20 us at C4).  Every wave computes the
   // same sizes (workgroup-uniform); claims never overlap (fetch-and-add of each size).
@@ -2296,24 +2091,6 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
       const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
       const i32x8 fcv = *reinterpret_cast<const i32x8*>(g->fc);
       const i32x8 Pv = *reinterpret_cast<const i32x8*>(g->P);
-      if (KCC_FIT_MSKIP && gvmin) {
-        const uint32_t vmin = gvmin[g0 + io];
-        // every load of the group is issued before the branch (one scalar-load round trip)
-        asm volatile("" : : "s"(fmv), "s"(fcv), "s"(Pv), "s"(vmin));
-        if (mmax32 <= vmin) {  // wave-uniform: every qm >= P
-          ++nskip;
-#pragma unroll
-          for (int u = 0; u < FIT_GROUP / 2; ++u) {
-            const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
-            const f32x2 q = fcp * rcf2;
-            const uint32_t m0 = min(__float_as_uint(q.x), (uint32_t)Pv[2 * u]);      // min(qc, P)
-            const uint32_t m1 = min(__float_as_uint(q.y), (uint32_t)Pv[2 * u + 1]);
-            acc32 += (int32_t)(m0 + m1);
-          }
-          asm volatile("; fit: memory-bound skip" : "+v"(acc32));  // (no tail merging)
-          continue;
-        }
-      }
 #pragma unroll
       for (int u = 0; u < FIT_GROUP / 2; ++u) {
         const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
@@ -2335,24 +2112,19 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   };
   // the clamp in the fit (fast_cl: launch_node_prep's NC mode): x >= P ? clamp : x per
   // node (CC:133-136), the clamp value from fast_cl, P >= 1 on every streamed row (padding:
-  // x = 0 >= P = 0, clamp 0).  Class A: 5.0 VALU per node with the clamp values from
-  // vector loads (KCC_FIT_NC_VLOAD); with scalar loads 6.0, one inline-asm v_mov_b64 per
-  // two nodes (5.5) measured slower (C4 8-way fit 33.3 -> 36.2 us).  Class B: 6.5.
-#if KCC_FIT_NC_VLOAD
-  // A/B variant: the clamp values by vector loads (uniform addresses: one line per wave),
-  // so the select takes them as VGPRs (no move: 5 VALU per node)
+  // x = 0 >= P = 0, clamp 0).  Class A: 5.0 VALU per node, the clamp values by vector loads
+  // (uniform addresses: one line per wave), so the select takes them as VGPRs.  By scalar
+  // loads each needs a move first (a select reads one scalar operand at most, vcc
+  // included): 6.0, 2 % slower per rank (round 3, profiles/r03z_ab_clamp_vload.txt); one
+  // inline-asm v_mov_b64 per two nodes (5.5): C4 8-way fit 33.3 -> 36.2 us.  Class B: 6.5.
   const __amdgpu_buffer_rsrc_t cl_rs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)fast_cl, (short)0, (int)(fit_groups(n_nodes) * FIT_GROUP * 4), 0x00020000);
-#endif
   auto sum_a_nc = [&](uint32_t g0, int cnt) {
     cnt = __builtin_amdgcn_readfirstlane(cnt);
     const FitGroupA* gbase = fast_a + g0;
-    const int32_t* cbase = fast_cl + (size_t)g0 * FIT_GROUP;
     const f32x2 rcf2 = {sr.rcf, sr.rcf};
     int32_t acc32 = 0;
-#if KCC_FIT_NC_VLOAD
     typedef int32_t i32x4_t __attribute__((ext_vector_type(4)));
-#endif
     set_round_down();
     for (int gi = 0; gi < cnt; ++gi) {
       int io = gi;
@@ -2361,37 +2133,10 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
       const i32x16 fmv = *reinterpret_cast<const i32x16*>(g->fm);
       const i32x8 fcv = *reinterpret_cast<const i32x8*>(g->fc);
       const i32x8 Pv = *reinterpret_cast<const i32x8*>(g->P);
-#if KCC_FIT_NC_VLOAD
       const int so = (int)((g0 + (uint32_t)io) * FIT_GROUP * 4);
       const i32x4_t c0 = __builtin_bit_cast(i32x4_t, __builtin_amdgcn_raw_buffer_load_b128(cl_rs, 0, so, 0));
       const i32x4_t c1 = __builtin_bit_cast(i32x4_t, __builtin_amdgcn_raw_buffer_load_b128(cl_rs, 16, so, 0));
       const int32_t clv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-      (void)cbase;
-#else
-      const i32x8 clv = *reinterpret_cast<const i32x8*>(cbase + (size_t)io * FIT_GROUP);
-#endif
-      if (KCC_FIT_MSKIP && gvmin) {
-        const uint32_t vmin = gvmin[g0 + io];
-        asm volatile("" : : "s"(fmv), "s"(fcv), "s"(Pv), "s"(vmin));  // loads before the branch
-        if (mmax32 <= vmin) {  // every qm >= P: x >= P <=> qc >= P, and x = qc below P
-          ++nskip;
-#pragma unroll
-          for (int u = 0; u < FIT_GROUP / 2; ++u) {
-            const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
-            const f32x2 q = fcp * rcf2;
-            int32_t m3[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const int k = 2 * u + h;
-              const uint32_t qc = __float_as_uint(h ? q.y : q.x);
-              m3[h] = qc >= (uint32_t)Pv[k] ? clv[k] : (int32_t)qc;  // CC:134-135 (x = qc here)
-            }
-            acc32 += m3[0] + m3[1];
-          }
-          asm volatile("; fit: memory-bound skip" : "+v"(acc32));  // (no tail merging)
-          continue;
-        }
-      }
 #pragma unroll
       for (int u = 0; u < FIT_GROUP / 2; ++u) {
         const f32x2 fcp = {__int_as_float(fcv[2 * u]), __int_as_float(fcv[2 * u + 1])};
@@ -2484,15 +2229,9 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     for (uint32_t k = 0;; ++k) {
       const uint32_t cur = base + (k == 0 ? first : __builtin_amdgcn_readfirstlane(q_slot[k & 1u]));
       if (cur >= lim) break;  // workgroup-uniform
-      uint32_t rem = lim - cur;
-#if KCC_FIT_QEST
-      // cur is where the queue head stood a chunk ago: the segment's other workgroups have
-      // claimed about a chunk each since
-      const uint32_t ahead = (wps - 1u) * qcur;
-      rem = rem > ahead ? rem - ahead : 0u;
-#endif
-      uint32_t qn = rem / ((uint32_t)KCC_FIT_QDIV * wps);
-      qn = qn < (uint32_t)KCC_FIT_QMIN ? (uint32_t)KCC_FIT_QMIN : (qn > qsz ? qsz : qn);
+      const uint32_t rem = lim - cur;
+      uint32_t qn = rem / (FIT_QDIV * wps);
+      qn = qn < FIT_QMIN ? FIT_QMIN : (qn > qsz ? qsz : qn);
       claim_issue(qn);
       const int cnt = (int)((cur + qcur < lim ? cur + qcur : lim) - cur);
       qcur = qn;
@@ -2536,23 +2275,17 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     const unsigned long long act = __ballot(active);
     if (slow_iters && lane == 0)
       atomicAdd(&counters[CNT_SLOW_PAIRS], (unsigned long long)slow_iters * (unsigned long long)__popcll(act));
-    // (VALU accounting: bench.py) only when profiling: one same-address device atomic per
-    // wave from every XCD serialised past the L2s (8192 waves: +50 us on the C4 fit)
-    if (KCC_FIT_MSKIP && count_skips && nskip && lane == 0)
-      atomicAdd(&counters[CNT_FIT_MSKIP], (unsigned long long)nskip);
   }
   // the clamp in the fit: the rows clamped for every spec (P <= 0, never streamed), once
   // per spec (the column's workgroup by == 0) for the normal specs (exact waves walked
   // every row on the exact path)
   if (NC && by == 0 && wave_fast) acc -= (uint64_t)counters[CNT_CLAMP_ALL];
-#ifdef KCC_FIT_DIAG_NO_ATOMICS  // diagnostic timing build only: results are wrong
-  if (active && acc == 0x5A5A5A5A5A5A5A5Aull) partial[s] = (int64_t)acc;
-#else
+  // a faulted device's partial carries the fault to every consumer (SPEC_FAULT_MARK)
+  if (by == 0 && device_faulted(faults)) errs += SPEC_FAULT_MARK;
   if (active) {
     atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[s]), acc);
     if (errs) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[S + s]), errs);
   }
-#endif
   KCC_TL(2048 + b % 4096, 3);
   if (fin.totals) fused_finalize(fin, S, partial);  // (the clamp correction beside the fit)
 }
@@ -2564,7 +2297,8 @@ __global__ void fit_finalize_kernel(int64_t S, const int64_t* __restrict__ parti
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= S) return;
   const int32_t dst = perm[i];
-  const bool err = partial[S + i] != 0, faulted = device_faulted(faults);
+  const bool err = partial[S + i] != 0;
+  const bool faulted = device_faulted(faults) || (uint64_t)partial[S + i] >= SPEC_FAULT_MARK;
   totals[dst] = err || faulted ? 0 : partial[i];
   spec_err[dst] = faulted ? SPEC_ERR_FAULT : err ? SPEC_ERR_DIV0 : 0;
 }
@@ -2641,8 +2375,9 @@ __global__ __launch_bounds__(256) void exchange_finalize_kernel(P2PArgs a) {
       s1 += (uint64_t)__builtin_nontemporal_load(d + (int64_t)p * 2 * smax + smax + i);
     }
     const int32_t dst = a.perm[i];
-    a.totals[dst] = s1 != 0 || faulted ? 0 : (int64_t)s0;
-    a.spec_err[dst] = faulted ? SPEC_ERR_FAULT : s1 != 0 ? SPEC_ERR_DIV0 : 0;
+    const bool fi = faulted || s1 >= SPEC_FAULT_MARK;  // (a sender's fault, in its counts)
+    a.totals[dst] = s1 != 0 || fi ? 0 : (int64_t)s0;
+    a.spec_err[dst] = fi ? SPEC_ERR_FAULT : s1 != 0 ? SPEC_ERR_DIV0 : 0;
   }
 }
 
@@ -2698,7 +2433,7 @@ int64_t reduce_resident_waves(bool limits) {
 int32_t reduce_range(int64_t n_containers, bool limits, int64_t reserve_waves) {
   int64_t slots = reduce_resident_waves(limits) - reserve_waves;
   if (slots < 64) slots = 64;
-  const int64_t r = slots * KCC_RED_ROUNDS * RED_TILE;
+  const int64_t r = slots * RED_TILE;
   int64_t t = (n_containers + r - 1) / r;
   if (t < 1) t = 1;
   if (t > ((int64_t)1 << 20)) t = (int64_t)1 << 20;  // range < 2^28 (int32 relative offsets)
@@ -2707,7 +2442,7 @@ int32_t reduce_range(int64_t n_containers, bool limits, int64_t reserve_waves) {
 
 int64_t reduce_tail_records() {
   const int64_t a = reduce_resident_waves(false), b = reduce_resident_waves(true);
-  return (a > b ? a : b) * KCC_RED_ROUNDS + 64;
+  return (a > b ? a : b) + 64;
 }
 
 hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, const int64_t* node_ptr,
@@ -2732,7 +2467,7 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
   }
   if (!red && ra.n_blocks == 0) return hipSuccess;
   if (limits && ra.n_blocks > 0) return hipErrorInvalidValue;  // (the ranks ride NA = 2 only)
-  // the rank workgroups: behind the reduce's (KCC_RED_RANKS_LAST), so they take the slots
+  // the rank workgroups: behind the reduce's on long reduces, so they take the slots
   // of its first waves to finish; in front (0), they held their slots ~2 us while the
   // reduce's range is sized for the whole device (its last waves started when they exited)
   const int32_t range = red ? reduce_range(n_containers, limits, 0) : RED_TILE;
@@ -2756,7 +2491,7 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
   a.out[3] = limits ? reinterpret_cast<uint64_t*>(lim_mem) : nullptr;
   a.tail = tail;
   a.faults = faults;
-  a.ranks_last = KCC_RED_RANKS_LAST && n_containers >= KCC_RED_RANKS_LAST_MIN ? 1 : 0;
+  a.ranks_last = n_containers >= RED_RANKS_LAST_MIN ? 1 : 0;
   if (limits)
     hipLaunchKernelGGL(reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, a, ra);
   else
@@ -2771,8 +2506,7 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
                             SlowNode* slow, int64_t* slow_list, int64_t n_specs,
                             ClampWork cw, unsigned long long* counters, int chunk, int64_t row0,
                             int64_t call_nodes, hipStream_t s, bool dense,
-                            const PlaceArgs* place, int32_t* fast_cl, uint32_t* gvmin) {
-  if (KCC_FIT_MSKIP && !gvmin && n_nodes > 0) return hipErrorInvalidValue;
+                            const PlaceArgs* place, int32_t* fast_cl) {
   if (n_nodes <= 0 && !place) return hipSuccess;
   if (fast_cl && (n_specs > CLAMP_LDS_SPECS || dense)) return hipErrorInvalidValue;
   const int64_t pr = clamp_pass_rows(call_nodes);
@@ -2793,12 +2527,12 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
   const int64_t res = resident_blocks(resident[pr == 1024 ? 0 : 1][nc ? 3 : mode],
                                       reinterpret_cast<const void*>(kern), KCC_NODE_PREP_BLOCK,
                                       lds_bytes, 256);
-  const int64_t cap = res < KCC_NODE_PREP_GRID ? res : KCC_NODE_PREP_GRID;
+  const int64_t cap = res < NODE_PREP_GRID ? res : NODE_PREP_GRID;
   const unsigned np_blocks = n_nodes > 0 ? grid_for(n_nodes, (int)pr, cap) : 0u;
   hipLaunchKernelGGL(kern, dim3(np_blocks + (unsigned)pa.n_blocks), dim3(KCC_NODE_PREP_BLOCK),
                      lds_bytes, s, n_nodes, alloc_cpu, alloc_mem, alloc_pods, pod_count, used_cpu,
                      used_mem, fast_a, fast_b, slow, slow_list, n_specs, cw,
-                     counters, (int32_t)chunk, (int32_t)(dense ? 1 : 0), row0 / pr, pa, fast_cl, gvmin);
+                     counters, (int32_t)chunk, (int32_t)(dense ? 1 : 0), row0 / pr, pa, fast_cl);
   return hipGetLastError();
 }
 
@@ -2860,7 +2594,7 @@ int64_t clamp_apply_blocks(int64_t n_specs) {
                                            CP_THREADS, 0, 256);
   int64_t G = 1;
   if (clamp_binned(n_specs))
-    while (G < KCC_CP_SPLIT && 2 * T * G * 2 <= resident) G *= 2;
+    while (G < CP_SPLIT && 2 * T * G * 2 <= resident) G *= 2;
   return 2 * T * G;
 }
 
@@ -2876,7 +2610,7 @@ int64_t fit_resident_blocks() {  // 256-thread fit workgroups resident on the de
 static int64_t fit_grid_y(int64_t n_nodes, int64_t n_specs, int64_t grid_nodes) {
   const int64_t gx = (n_specs + FIT_SPW - 1) / FIT_SPW;
   const int64_t n_groups = fit_groups(n_nodes);
-  int64_t gy = KCC_FIT_ROUNDS * fit_resident_blocks() / gx / KCC_FIT_GY_DIV;
+  int64_t gy = fit_resident_blocks() / gx;
   if (grid_nodes > n_nodes) gy = gy * n_nodes / grid_nodes;
   if (gy >= 16) gy = gy / 8 * 8;  // whole XCD rounds
   const int64_t claims = (n_groups + FIT_QCHUNK - 1) / FIT_QCHUNK;
@@ -2884,17 +2618,13 @@ static int64_t fit_grid_y(int64_t n_nodes, int64_t n_specs, int64_t grid_nodes) 
   if (gy < 1) gy = 1;
   return gy;
 }
-int64_t fit_working_blocks(int64_t n_nodes, int64_t n_specs, int64_t grid_nodes) {
-  if (n_nodes <= 0 || n_specs <= 0) return 0;
-  return (n_specs + FIT_SPW - 1) / FIT_SPW * fit_grid_y(n_nodes, n_specs, grid_nodes);
-}
 
 hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,
                       const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, uint32_t* queue, int chunk,
-                      int64_t grid_nodes, hipStream_t s, const int32_t* fast_cl,
-                      const uint32_t* gvmin, bool count_skips, const FinArgs* fin) {
+                      int64_t grid_nodes, hipStream_t s, const unsigned long long* faults,
+                      const int32_t* fast_cl, const FinArgs* fin) {
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
   const int64_t gx = (n_specs + FIT_SPW - 1) / FIT_SPW;
   const int64_t gy = fit_grid_y(n_nodes, n_specs, grid_nodes);
@@ -2904,8 +2634,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
   auto kern = fast_cl ? fit_kernel<true> : fit_kernel<false>;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, queue, fast_a,
                      fast_b, slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)chunk,
-                     (int32_t)gx, (int32_t)gy, fast_cl, KCC_FIT_MSKIP ? gvmin : nullptr,
-                     (int32_t)(count_skips ? 1 : 0), fin ? *fin : FinArgs{});
+                     (int32_t)gx, (int32_t)gy, fast_cl, faults, fin ? *fin : FinArgs{});
   return hipGetLastError();
 }
 

@@ -23,33 +23,18 @@ namespace {
 constexpr int PS_THREADS = 256;
 constexpr int PS_PER_THREAD = 4;
 constexpr int PS_BLOCK = PS_THREADS * PS_PER_THREAD;  // strings per workgroup
-#ifndef KCC_PC_PER_THREAD
-#define KCC_PC_PER_THREAD 4  // 8 measured equal or slower (86 VGPRs)
-#endif
-constexpr int PC_PER_THREAD = KCC_PC_PER_THREAD;      // parse_cpu_kernel: strings per lane
+constexpr int PC_PER_THREAD = 4;  // parse_cpu_kernel: strings per lane (8: equal or slower, 86 VGPRs)
 constexpr int PC_BLOCK = PS_THREADS * PC_PER_THREAD;
-#ifndef KCC_PQ_PER_THREAD
-#define KCC_PQ_PER_THREAD 8  // parse_quantity_kernel (51 VGPRs at 4): 4 -> 8 took C4's 39.6M memory strings 0.260 -> 0.233 ms
-#endif
-constexpr int PQ_PER_THREAD = KCC_PQ_PER_THREAD;      // parse_quantity_kernel: strings per lane
+// parse_quantity_kernel: strings per lane (51 VGPRs at 4): 4 -> 8 took C4's 39.6M memory
+// strings 0.260 -> 0.233 ms
+constexpr int PQ_PER_THREAD = 8;
 constexpr int PQ_BLOCK = PS_THREADS * PQ_PER_THREAD;
 constexpr int PS_LDS_WORDS = 6144;                    // 24 KiB of staged characters
-#ifndef KCC_PARSE_NTST
-#define KCC_PARSE_NTST 1  // the register paths' value / status stores streaming (A/B knob)
-#endif
-// a parsed value and its status (written once, read by a later launch)
+// a parsed value and its status (written once, read by a later launch): streaming stores
 __device__ __forceinline__ void put_parsed(int64_t* out, int8_t* status, int64_t i, int64_t v, int8_t st) {
-  if (KCC_PARSE_NTST) {
-    __builtin_nontemporal_store(v, out + i);
-    __builtin_nontemporal_store(st, status + i);
-  } else {
-    out[i] = v;
-    status[i] = st;
-  }
+  __builtin_nontemporal_store(v, out + i);
+  __builtin_nontemporal_store(st, status + i);
 }
-#ifndef KCC_PQ_V2
-#define KCC_PQ_V2 1  // parse_quantity_kernel's register path: 1 = qty_fast2, 0 = qty_fast (A/B)
-#endif
 
 __device__ __forceinline__ bool go_space(uint32_t c) {
   // strings.TrimSpace on ASCII input: '\t', '\n', '\v', '\f', '\r', ' '
@@ -638,99 +623,6 @@ __device__ __noinline__ QtyResult quantity_value_global(const uint8_t* s, int n)
   return QtyResult{v, st};
 }
 
-// 10^k x 2^-k inverted: (5^k)^-1 mod 2^64, so that for V a multiple of 10^k,
-// V / 10^k = (V >> k) * inv5(k) mod 2^64 (an exact division without a divide)
-constexpr uint64_t inv_odd64(uint64_t x) {  // Newton: each step doubles the correct bits
-  uint64_t y = x;                            // x * x = 1 mod 8 for odd x: 3 bits
-  for (int i = 0; i < 5; ++i) y *= 2u - x * y;
-  return y;
-}
-constexpr uint64_t inv5_pow(int k) {
-  uint64_t p = 1;
-  for (int i = 0; i < k; ++i) p *= 5u;
-  return inv_odd64(p);
-}
-static_assert(inv5_pow(7) * 78125u == 1u, "inverse of 5^7 mod 2^64");
-
-// The register fast path of Quantity.Value(): s[0, L) = the 16 bytes w0..w3 from byte
-// `al` on (L <= 13).  Accepts plain digits (d = 1..13) followed by nothing, a decimal
-// suffix k M G T P E (10^3k) or a binary one Ki Mi Gi Ti Pi Ei (2^10k); everything else
-// (a sign, a fraction, an exponent, m/u/n, a malformed string) returns false for the
-// general parser.  All 32-bit work, no branches: the characters byte-aligned with
-// v_alignbyte; the last two read from the word pair holding them; the d digits kept
-// (the rest masked to '0') and checked per word; four digits per word converted with
-// shifts and a 24-bit multiply-add, the words joined with one 64-bit multiply-add into
-// V = D x 10^(16 - d), and D = V / 10^(16 - d) exactly (shift, multiply by the inverse
-// of 5^(16 - d)).  Caps as quantity_value: binary amounts at 2^63 - 1; a decimal amount
-// beyond it is PARSE_UNSUPPORTED (k8s wraps it).
-[[maybe_unused]] __device__ __forceinline__ bool qty_fast(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
-                                         uint32_t al, int L, const uint64_t* s_p10,
-                                         const uint64_t* s_lim, const uint64_t* s_inv,
-                                         int64_t& v, int8_t& st) {
-  const uint64_t MAXV = 0x7fffffffffffffffull;
-  const uint32_t a0 = __builtin_amdgcn_alignbyte(w1, w0, al);
-  const uint32_t a1 = __builtin_amdgcn_alignbyte(w2, w1, al);
-  const uint32_t a2 = __builtin_amdgcn_alignbyte(w3, w2, al);
-  const uint32_t a3 = __builtin_amdgcn_alignbyte(0u, w3, al);
-  // the last two characters: the 16 bits at byte p = L - 2 (L = 1: at 0, shifted)
-  const uint32_t p = L >= 2 ? (uint32_t)(L - 2) : 0u;
-  const uint32_t q = p >> 2;  // 0..2
-  const uint32_t lo = q == 0 ? a0 : (q == 1 ? a1 : a2);
-  const uint32_t hi = q == 0 ? a1 : (q == 1 ? a2 : a3);
-  const uint32_t pair = __builtin_amdgcn_alignbyte(hi, lo, p & 3u);
-  const uint32_t z = L >= 2 ? (pair >> 8) & 0xffu : pair & 0xffu;  // last
-  const uint32_t y = L >= 2 ? pair & 0xffu : 0u;                    // second last
-  // suffix decode by table: 3-bit index per character 'E'..'Y' (offset ch - 'E' <= 20) —
-  // E 6, G 3, K 1, M 2, P 5, T 4 — then 10^3k and its overflow threshold from LDS tables
-  constexpr uint64_t SFX = (6ull << 0) | (3ull << 6) | (1ull << 18) | (2ull << 24) |
-                           (5ull << 33) | (4ull << 45);
-  auto sfx = [](uint32_t ch) -> uint32_t {
-    const uint32_t o = ch - 'E';
-    return o <= 20u ? (uint32_t)(SFX >> (3u * o)) & 7u : 0u;
-  };
-  const uint32_t yb = sfx(y);                                    // Ki..Ei ('k' -> 0)
-  const uint32_t zd = z == 'k' ? 1u : (z == 'K' ? 0u : sfx(z));  // k M G T P E
-  const bool bin = z == 'i' && yb != 0;
-  const bool dec = !bin && zd != 0;
-  const bool dig = z - '0' <= 9u;
-  const int d = L - (bin ? 2 : (dec ? 1 : 0));  // the digits
-  // bytes d.. masked: t = the digit values (0..9 per byte for a digit)
-  const uint32_t Z = 0x30303030u;
-  const uint64_t m01 = d >= 8 ? ~0ull : (1ull << (8 * (d > 0 ? d : 0))) - 1u;
-  const int d2 = d - 8;
-  const uint64_t m23 = d2 <= 0 ? 0ull : (1ull << (8 * d2)) - 1u;
-  const uint32_t t0 = (a0 ^ Z) & (uint32_t)m01, t1 = (a1 ^ Z) & (uint32_t)(m01 >> 32);
-  const uint32_t t2 = (a2 ^ Z) & (uint32_t)m23, t3 = (a3 ^ Z) & (uint32_t)(m23 >> 32);
-  // a byte > 9 sets bit 7 of t + 0x76 or of t itself (a carry out of a bad byte can only
-  // flag its neighbour too)
-  const uint32_t H = 0x76767676u;
-  const uint32_t bad = ((t0 + H) | t0 | (t1 + H) | t1 | (t2 + H) | t2 | (t3 + H) | t3) & 0x80808080u;
-  // four digits per word (the first in the low byte): byte pairs 10 b0 + b1 and
-  // 10 b2 + b3 (no carries: <= 99), then the pairs
-  auto quad = [](uint32_t t) -> uint32_t {  // shifts and 24-bit multiplies: full rate
-    const uint32_t u = (t << 3) + ((t << 1) + (t >> 8));
-    return __umul24(u & 0xffu, 100u) + ((u >> 16) & 0xffu);
-  };
-  const uint32_t q01 = __umul24(quad(t0), 10000u) + quad(t1);
-  const uint32_t q23 = __umul24(quad(t2), 10000u) + quad(t3);
-  const uint64_t V = (uint64_t)q01 * 100000000u + q23;  // D x 10^(16 - d), < 10^16
-  const int k = 16 - d;                                  // 3..15 on the fast path
-  const bool ok = (bin || dec || dig) && d >= 1 && bad == 0;
-  const uint64_t D = (V >> (k & 15)) * s_inv[k & 15];   // < 10^13
-  // binary (and none): a shift, capped; decimal: 10^3k, beyond 2^63 - 1 unsupported — the
-  // 64-bit multiply behind a branch (whole waves of binary / plain amounts skip it)
-  const int bexp = bin ? 10 * (int)yb : 0;
-  uint64_t mag = D > (MAXV >> bexp) ? MAXV : D << bexp;
-  st = PARSE_OK;
-  if (dec) {
-    const bool over = D > s_lim[zd];
-    mag = over ? 0 : D * s_p10[zd];
-    st = over ? PARSE_UNSUPPORTED : PARSE_OK;
-  }
-  v = (int64_t)mag;
-  return ok;
-}
-
 // Character classes for qty_fast2 (one LDS byte per character): bit 7 a digit; bits 0-2 the
 // decimal suffix k M G T P E (10^3k: 1..6; 'K' alone is none); bits 3-5 the binary prefix
 // K M G T P E of "Ki".."Ei" (2^10k: 1..6); bit 6 'i'.
@@ -746,7 +638,8 @@ __host__ __device__ constexpr uint32_t qty_class(uint32_t ch) {
        : ch == 'E' ? (6u | (6u << 3)) : 0u;
 }
 
-// qty_fast's contract (same accepted strings, values and statuses), fewer VALU: the suffix
+// The register fast path of Quantity.Value() (round 4; replaced round 2's qty_fast, whose
+// contract it keeps: the same accepted strings, values and statuses, fewer VALU): the suffix
 // from the character-class table; the digits right-aligned by ONE 128-bit shift left by
 // 8 x (16 - d) bytes' worth of bits — the suffix and whatever follows the string fall off
 // the top, zeros (leading '0' digits) come in at the bottom, so no masks and no exact
@@ -812,7 +705,7 @@ __host__ __device__ constexpr uint32_t qty_class(uint32_t ch) {
 
 // Quantity.Value() without LDS, as parse_cpu_kernel: one lane per string, strings of
 // <= 13 characters from one aligned 16-byte buffer load per lane, parsed in registers
-// (qty_fast) when they are plain digits (<= 13) and an optional integral suffix — k M G
+// (qty_fast2) when they are plain digits (<= 13) and an optional integral suffix — k M G
 // T P E (10^3k) or Ki Mi Gi Ti Pi Ei (2^10k) — which covers every canonical memory
 // quantity of a container (Quantity.String() of a BinarySI or DecimalSI integer amount);
 // the value is capped at 2^63 - 1 exactly as quantity_value does.  Anything else (a sign,
@@ -824,19 +717,15 @@ __global__ __launch_bounds__(PS_THREADS) void parse_quantity_kernel(int64_t n, c
                                                                     int64_t* __restrict__ out,
                                                                     int8_t* __restrict__ status) {
   const uint64_t MAXV = 0x7fffffffffffffffull;
-  // 10^3k and (2^63 - 1) / 10^3k (k = 0..6), and (5^k)^-1 mod 2^64 (k = 0..15)
-  __shared__ uint64_t s_p10[8], s_lim[8], s_inv[16];
-  __shared__ uint8_t s_cls[KCC_PQ_V2 ? 256 : 1];  // qty_class of every byte value
-  if (KCC_PQ_V2) s_cls[threadIdx.x] = (uint8_t)qty_class(threadIdx.x);  // (256 threads)
+  // 10^3k and (2^63 - 1) / 10^3k (k = 0..6)
+  __shared__ uint64_t s_p10[8], s_lim[8];
+  __shared__ uint8_t s_cls[256];  // qty_class of every byte value
+  s_cls[threadIdx.x] = (uint8_t)qty_class(threadIdx.x);  // (256 threads)
   if (threadIdx.x < 8) {
     uint64_t p = 1;
     for (unsigned k = 0; k < threadIdx.x && k < 6; ++k) p *= 1000u;
     s_p10[threadIdx.x] = p;
     s_lim[threadIdx.x] = MAXV / p;
-  }
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) s_inv[k] = inv5_pow(k);  // folded to constants
   }
   __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * PQ_BLOCK;
@@ -881,7 +770,6 @@ __global__ __launch_bounds__(PS_THREADS) void parse_quantity_kernel(int64_t n, c
     int64_t v = 0;
     int8_t st = PARSE_BADOFF;
     bool done = false;
-#if KCC_PQ_V2
     if (fast[r])
       done = qty_fast2(w[r][0], w[r][1], w[r][2], w[r][3], (uint32_t)sb[r], (int)(se[r] - sb[r]),
                        s_cls, s_p10, s_lim, v, st);
@@ -890,25 +778,13 @@ __global__ __launch_bounds__(PS_THREADS) void parse_quantity_kernel(int64_t n, c
     } else {
       put_parsed(out, status, i, v, st);
     }
-#else
-    if (fast[r])
-      done = qty_fast(w[r][0], w[r][1], w[r][2], w[r][3], (uint32_t)(sb[r] & 3), (int)(se[r] - sb[r]),
-                      s_p10, s_lim, s_inv, v, st);
-    const bool sane = sb[r] >= 0 && se[r] >= sb[r] && se[r] <= n_bytes && se[r] - sb[r] < ((int64_t)1 << 31);
-    if (!done && sane) {
-      need |= 1u << r;
-    } else {
-      out[i] = v;
-      status[i] = st;
-    }
-#endif
   }
 #pragma unroll 1
   for (int r = 0; r < PQ_PER_THREAD; ++r) {
     if (!((need >> r) & 1u)) continue;
     const int64_t i = base + r * PS_THREADS;
-    const int64_t b = off[i], e = off[i + 1];  // (v1: checked above)
-    if (KCC_PQ_V2 && !(b >= 0 && e >= b && e <= n_bytes && e - b < ((int64_t)1 << 31))) {
+    const int64_t b = off[i], e = off[i + 1];
+    if (!(b >= 0 && e >= b && e <= n_bytes && e - b < ((int64_t)1 << 31))) {
       out[i] = 0;
       status[i] = PARSE_BADOFF;
       continue;

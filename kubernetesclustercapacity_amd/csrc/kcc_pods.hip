@@ -26,15 +26,10 @@ namespace {
 constexpr int POD_BATCH = 4;   // app containers loaded per round trip
 constexpr int INIT_BATCH = 2;  // init containers loaded per round trip
 
-#ifndef KCC_POD_LDS
-// 1: stage each workgroup's container ranges in LDS by coalesced loads first.  Measured
-// slower at C4 (scripts/ab_pods.py: 0.359 vs 0.347 ms; the per-lane loads already move
-// only the algorithmic bytes, PMC 1.69 GB vs 1.72 GB), so off by default.
-#define KCC_POD_LDS 0
-#endif
+// (Staging each workgroup's container ranges in LDS by coalesced loads first measured
+// slower at C4 and was deleted: scripts/ab_pods.py 0.359 vs 0.347 ms; the per-lane loads
+// already move only the algorithmic bytes, PMC 1.69 GB vs 1.72 GB.)
 constexpr int POD_WG = 256;
-[[maybe_unused]] constexpr int POD_CAP_C = 1024;  // app containers staged per workgroup (16 KB)
-[[maybe_unused]] constexpr int POD_CAP_I = 512;   // init containers staged per workgroup (8.5 KB)
 
 // Clamp [lo, hi) into [0, n).
 __device__ __forceinline__ void clamp_range(int64_t& lo, int64_t& hi, int64_t n) {
@@ -100,11 +95,8 @@ __device__ __forceinline__ void pod_request(int64_t lo, int64_t hi, int64_t a, i
   out_m = ((int64_t)am > im ? am : (uint64_t)im) + om;
 }
 
-// One lane per pod.  The workgroup's pods [p0, p0 + 256) hold one contiguous range of
-// app containers and one of init containers (CSR): with KCC_POD_LDS the first POD_CAP_C / POD_CAP_I of them
-// are loaded by all lanes together (coalesced) into LDS, and each lane then walks its
-// pods' containers there; containers past the caps (a workgroup of unusually large
-// pods) are read from global memory by the lane itself.
+// One lane per pod: each lane walks its pod's app and init containers (CSR) from global
+// memory, its loads batched (POD_BATCH / INIT_BATCH per round trip).
 __global__ __launch_bounds__(POD_WG) void pod_requests_kernel(
     int64_t n_pods, int64_t n_cont, int64_t n_init, const int64_t* __restrict__ pod_ptr,
     const uint64_t* __restrict__ cpu_req, const int64_t* __restrict__ mem_req,
@@ -131,58 +123,6 @@ __global__ __launch_bounds__(POD_WG) void pod_requests_kernel(
     oc = ovh_cpu ? ovh_cpu[p] : 0;
     om = ovh_mem ? (uint64_t)ovh_mem[p] : 0;
   }
-#if KCC_POD_LDS
-  __shared__ uint64_t s_c[POD_CAP_C], s_m[POD_CAP_C], s_ic[POD_CAP_I], s_im[POD_CAP_I];
-  __shared__ uint8_t s_rs[POD_CAP_I];
-  const int64_t pe = p0 + POD_WG < n_pods ? p0 + POD_WG : n_pods;
-  int64_t cb = pod_ptr[p0], ce = pod_ptr[pe];  // wave-uniform
-  clamp_range(cb, ce, n_cont);
-  const int64_t wc = ce - cb < POD_CAP_C ? ce - cb : POD_CAP_C;
-  int64_t ib = 0, ie = 0;
-  if (has_init) {
-    ib = init_ptr[p0];
-    ie = init_ptr[pe];
-    clamp_range(ib, ie, n_init);
-  }
-  const int64_t wi = ie - ib < POD_CAP_I ? ie - ib : POD_CAP_I;
-  for (int64_t i = threadIdx.x; i < wc; i += POD_WG) {
-    s_c[i] = cpu_req[cb + i];
-    s_m[i] = (uint64_t)mem_req[cb + i];
-  }
-  for (int64_t i = threadIdx.x; i < wi; i += POD_WG) {
-    s_ic[i] = init_cpu[ib + i];
-    s_im[i] = (uint64_t)init_mem[ib + i];
-    s_rs[i] = restartable ? restartable[ib + i] : 0;
-  }
-  __syncthreads();
-  if (!live) return;
-  uint64_t rc, rm;
-  pod_request(
-      lo, hi, a, b, has_init, oc, om,
-      [&](int64_t c, uint64_t& vc, uint64_t& vm) {
-        const int64_t j = c - cb;  // in [0, wc) unless past the cap (or a malformed CSR)
-        if (j >= 0 && j < wc) {
-          vc = s_c[j];
-          vm = s_m[j];
-        } else {
-          vc = cpu_req[c];
-          vm = (uint64_t)mem_req[c];
-        }
-      },
-      [&](int64_t k, uint64_t& vc, uint64_t& vm, bool& rs) {
-        const int64_t j = k - ib;
-        if (j >= 0 && j < wi) {
-          vc = s_ic[j];
-          vm = s_im[j];
-          rs = s_rs[j] != 0;
-        } else {
-          vc = init_cpu[k];
-          vm = (uint64_t)init_mem[k];
-          rs = restartable ? restartable[k] != 0 : false;
-        }
-      },
-      rc, rm);
-#else
   if (!live) return;
   uint64_t rc, rm;
   pod_request(
@@ -197,7 +137,6 @@ __global__ __launch_bounds__(POD_WG) void pod_requests_kernel(
         rs = restartable ? restartable[k] != 0 : false;
       },
       rc, rm);
-#endif
   pod_cpu[p] = rc;
   pod_mem[p] = (int64_t)rm;
 }

@@ -478,12 +478,6 @@ class CapacityEngine:
         self._check(self._lib.kcc_fit_stream_rows(self._h, C.byref(v)))
         return v.value
 
-    def fit_mskip_groups(self) -> int:
-        """(node group, class-A wave) pairs the last fit summed without the memory quotient."""
-        v = C.c_int64()
-        self._check(self._lib.kcc_fit_mskip_groups(self._h, C.byref(v)))
-        return v.value
-
     def reduce_faults(self) -> int:
         """Look-back waits of the segmented reduce that gave up (0 on a healthy device)."""
         v = C.c_int64()

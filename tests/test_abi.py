@@ -84,7 +84,7 @@ def test_release_library_reports_release_build():
 
 def test_makefile_refuses_knobs_for_the_release_library():
     csrc = os.path.join(os.path.dirname(_lib.LIB_PATH), "csrc")
-    r = subprocess.run(["make", "-n", "-C", csrc, "EXTRA=-DKCC_FIT_DIAG_NO_ATOMICS"],
+    r = subprocess.run(["make", "-n", "-C", csrc, "EXTRA=-DKCC_DIAG_RED_NOSTORE"],
                        capture_output=True, text=True)
     assert r.returncode != 0 and "make variant" in (r.stdout + r.stderr)
 

@@ -10,9 +10,10 @@ so any split of the rows into contiguous shards must give the same totals bit fo
   - bench.py itself with 2 ranks sharing GPU 0 over gloo (the launcher + exchange path)
     against its own 1-rank run.
 Configs (BASELINE.json `configs`) against the C oracle, every spec, at full size:
-C2 (10k x 200k pods x 1 spec), C3 (100k x 2M x 256), C4 (1M x 20M x 4096), and the C5
-rank-0 and rank-7 shards of an 8-way split (625k of 5M nodes with Zipf(1.2) pods per node,
-capped at 2 x allocatable pods — SURVEY §8d — x 16384 specs).
+C2 (10k x 200k pods x 1 spec), C3 (100k x 2M x 256), C4 (1M x 20M x 4096), C5 (5M nodes with
+Zipf(1.2) pods per node, capped at 2 x allocatable pods — SURVEY §8d — x 16384 specs: the
+whole cluster, as 8 rank shards and on one device, plus the rank-0 and rank-7 shards alone).
+C1 (100 nodes x 1k pods x 1 spec) runs end to end through the host CLI in test_host.py.
 """
 import json
 import os
@@ -208,6 +209,99 @@ def test_c5_rank_shard_every_spec_vs_oracle(engine, rank):
     t, e = capacity(engine, c, sc, sm)
     np.testing.assert_array_equal(e, oe)
     np.testing.assert_array_equal(t, ot)
+
+
+def test_c5_whole_cluster_every_spec_vs_oracle():
+    """C5 at full size: 5M nodes (Zipf(1.2) pods per node, capped at 2 x allocatable pods;
+    ~1.21e9 containers) x 16384 specs, every spec against the C oracle over the whole
+    cluster.  Generated one 8-way rank shard at a time (host memory stays at one shard);
+    the oracle's whole-cluster totals are assembled from its shard results (a spec's total
+    is the wrapping sum of the shards' totals; it is flagged when any shard flags it —
+    CC:138, CC:119-130).  Two device paths, both vs those totals:
+      (a) the 8-GPU decomposition: each shard's kcc_capacity_partial_async on its own
+          arrays, the partials summed (the all-reduce), one finalize;
+      (b) one GPU: the whole cluster resident (the shards copied into one CSR), one
+          kcc_capacity_async over all 5M nodes."""
+    import torch
+
+    from kubernetesclustercapacity_amd import CapacityEngine
+    torch.cuda.init()
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+    N, W = synth.CONFIGS["C5"]["n_nodes"], 8
+    sc, sm = synth.config_specs("C5")
+    S = sc.size
+    assert S == 16384
+    # the whole cluster's device arrays, filled shard by shard
+    n_cont, shards = 0, []
+    for r in range(W):
+        lo, hi = node_range(N, r, W)
+        c = synth.config_cluster("C5", node_lo=lo, node_hi=hi, limits=False)
+        shards.append(c)
+        n_cont += c.n_containers
+    assert n_cont > 1_100_000_000
+    whole = {k: torch.empty(N, dtype=torch.int64, device=dev)
+             for k in ("ac", "am", "ap", "pc", "uc", "um")}
+    wptr = torch.empty(N + 1, dtype=torch.int64, device=dev)
+    wcpu = torch.empty(n_cont, dtype=torch.int64, device=dev)
+    wmem = torch.empty(n_cont, dtype=torch.int64, device=dev)
+    acc = torch.zeros(2 * S, dtype=torch.int64, device=dev)
+    ot = np.zeros(S, np.uint64)
+    oe = np.zeros(S, np.int32)
+    s_cpu, s_mem = T(sc), T(sm)
+    c_off = 0
+    with CapacityEngine(0, 1) as eng:
+        stream = torch.cuda.Stream(dev)
+        for r, c in enumerate(shards):
+            lo, hi = node_range(N, r, W)
+            n, nc = c.n_nodes, c.n_containers
+            # (a) this shard as one rank
+            used = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(2)]
+            partial = torch.empty(2 * S, dtype=torch.int64, device=dev)
+            arrs = [T(x) for x in (c.node_ptr, c.cpu_req, c.mem_req, c.alloc_cpu, c.alloc_mem,
+                                   c.alloc_pods, c.pod_count)]
+            with torch.cuda.stream(stream):
+                eng.capacity_partial_async(c.node_ptr, *arrs, used[0], used[1], s_cpu, s_mem,
+                                           partial, stream=stream)
+            stream.synchronize()
+            acc += partial
+            # the per-node sums of the shard's reduce vs numpy
+            np.testing.assert_array_equal(used[0].cpu().numpy().view(np.uint64),
+                                          seg_sums(c.node_ptr, c.cpu_req))
+            np.testing.assert_array_equal(used[1].cpu().numpy().view(np.uint64),
+                                          seg_sums(c.node_ptr, c.mem_req))
+            # (b) into the whole cluster's arrays
+            wptr[lo:hi + 1] = arrs[0] + c_off
+            wcpu[c_off:c_off + nc] = arrs[1]
+            wmem[c_off:c_off + nc] = arrs[2]
+            for k, a in zip(("ac", "am", "ap", "pc"), arrs[3:]):
+                whole[k][lo:hi] = a
+            c_off += nc
+            # the oracle on this shard
+            st, se = oracle_totals(c, sc, sm)
+            ot += st.view(np.uint64)
+            oe |= se
+            del arrs, used, partial
+            shards[r] = None
+        ot = np.where(oe != 0, np.uint64(0), ot).view(np.int64)
+        totals = torch.empty(S, dtype=torch.int64, device=dev)
+        err = torch.empty(S, dtype=torch.int32, device=dev)
+        with torch.cuda.stream(stream):
+            eng.fit_finalize_async(S, acc, totals, err, stream=stream)
+        stream.synchronize()
+        np.testing.assert_array_equal(err.cpu().numpy(), oe)
+        np.testing.assert_array_equal(totals.cpu().numpy(), ot)
+        # (b) the whole cluster on one device, one call
+        totals.fill_(-1)
+        err.fill_(-1)
+        with torch.cuda.stream(stream):
+            eng.capacity_async(None, wptr, wcpu, wmem, whole["ac"], whole["am"], whole["ap"],
+                               whole["pc"], whole["uc"], whole["um"], s_cpu, s_mem, totals, err,
+                               stream=stream)
+        stream.synchronize()
+        np.testing.assert_array_equal(err.cpu().numpy(), oe)
+        np.testing.assert_array_equal(totals.cpu().numpy(), ot)
+        assert eng.reduce_faults() == 0
 
 
 # ---- bench.py: 2 ranks (gloo, sharing GPU 0) == 1 rank -------------------------------------

@@ -293,3 +293,65 @@ def test_cli_scheduler_requests_opt_in(cli, tmp_path):
         r = _run(["-cluster", str(path), "-cpuRequests=200m", "-memRequests=250mb"] + flag)
         assert r.returncode == 0, r.stderr
         assert f"Total possible replicas for the pod with required input specs : {t[0]}" in r.stdout, flag
+
+
+def write_synth_cluster(path, c):
+    """A kubernetesclustercapacity_amd.synth cluster as a cluster file: every engine row a
+    node object (zero rows — the generator's unhealthy nodes — as nodes whose condition 1 is
+    True, which getHealthyNodes turns back into zero rows, CC:212-226), each node's
+    containers dealt over its pods (1-3 per pod, as generated), every pod Running."""
+    lines = []
+    ptr = c.node_ptr
+    for i in range(c.n_nodes):
+        if c.alloc_cpu[i] == 0 and c.alloc_mem[i] == 0 and c.alloc_pods[i] == 0:
+            lines.append(f"node n{i} 4 16331524Ki 110 False True False False")
+            assert c.pod_count[i] == 0 and ptr[i + 1] == ptr[i]
+            continue
+        assert c.alloc_mem[i] % 1024 == 0
+        lines.append(f"node n{i} {int(c.alloc_cpu[i])}m {int(c.alloc_mem[i]) // 1024}Ki "
+                     f"{int(c.alloc_pods[i])} False False False False")
+        p, cont = int(c.pod_count[i]), list(range(int(ptr[i]), int(ptr[i + 1])))
+        assert p <= len(cont) <= 3 * p
+        for k in range(p):
+            lines.append(f"pod n{i} ns p{i}-{k} Running")
+            for j in cont[k::p]:
+                lines.append(f"container {int(c.cpu_req[j])}m 0 {int(c.mem_req[j])} 0")
+    open(path, "w").write("\n".join(lines) + "\n")
+    return path
+
+
+@pytest.mark.gpu
+def test_cli_c1_baseline_config(cli, tmp_path):
+    """BASELINE.json configs[0] (C1): 100 nodes, 1k pods, one spec 200m / 250mb x 10
+    replicas (ClusterCapacity.go:57-61, 142-149).  The reference ran it on a client-go fake
+    clientset (Go is absent here); its engine half runs here end to end: the seeded C1
+    cluster through the C++ host CLI (the reference's flags and verdict text) and through
+    the C-ABI, both against the C oracle."""
+    from kubernetesclustercapacity_amd import CapacityEngine, synth
+    c = synth.config_cluster("C1")
+    assert c.n_nodes == 100 and 900 <= int(c.pod_count.sum()) <= 1100
+    uc = np.zeros(c.n_nodes, np.uint64)
+    um = np.zeros(c.n_nodes, np.int64)
+    for i in range(c.n_nodes):
+        uc[i] = np.sum(c.cpu_req[c.node_ptr[i]:c.node_ptr[i + 1]], dtype=np.uint64)
+        um[i] = np.sum(c.mem_req[c.node_ptr[i]:c.node_ptr[i + 1]], dtype=np.int64)
+    sc, sm = np.array([200], np.uint64), np.array([262_144_000], np.int64)
+    ot, oe = coracle.fit(c.alloc_cpu, c.alloc_mem, c.alloc_pods, c.pod_count, uc, um, sc, sm)
+    assert oe.tolist() == [0]
+    # the C-ABI (kcc_capacity: reduce + fit on the device)
+    with CapacityEngine(0, 1) as eng:
+        t, e = eng.capacity(c.node_ptr, c.cpu_req, c.mem_req, c.alloc_cpu, c.alloc_mem,
+                            c.alloc_pods, c.pod_count, sc, sm)
+    assert t.tolist() == ot.tolist() and e.tolist() == [0]
+    # the host CLI over the same cluster as objects (node / pod / container strings)
+    path = write_synth_cluster(str(tmp_path / "c1.txt"), c)
+    r = _run(["-cluster", path, "-cpuRequests=200m", "-memRequests=250mb", "-replicas=10"])
+    assert r.returncode == 0, r.stderr
+    assert f"Total possible replicas for the pod with required input specs : {ot[0]}" in r.stdout
+    verdict = "So you can go ahead" if ot[0] >= 10 else "Unfortunately"
+    assert verdict in r.stdout
+    # -v: one "Max replicas" line per engine row, their sum the total (CC:137-138)
+    r = _run(["-cluster", path, "-cpuRequests=200m", "-memRequests=250mb", "-replicas=10", "-v"])
+    assert r.returncode == 0, r.stderr
+    rows = [int(ln.rsplit(":", 1)[1]) for ln in r.stdout.splitlines() if "Max replicas :" in ln]
+    assert len(rows) == c.n_nodes and sum(rows) == int(ot[0])

@@ -35,16 +35,6 @@ def asm(tmp_path_factory):
     return out.read_text()
 
 
-@pytest.fixture(scope="module")
-def asm_mskip(tmp_path_factory):
-    """The memory-bound skip build (KCC_FIT_MSKIP=1, off in the release library)."""
-    out = tmp_path_factory.mktemp("isa_mskip") / "kcc.s"
-    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-S",
-                    "--cuda-device-only", "-DKCC_FIT_MSKIP=1", SRC, "-o", str(out)], check=True,
-                   capture_output=True)
-    return out.read_text()
-
-
 def kernel_body(asm, name):
     m = re.search(rf"^(_ZN3kcc12_GLOBAL__N_1\d+{name}\w*):\s*;", asm, re.M)
     assert m, name
@@ -86,56 +76,32 @@ def check_loads(lines, dwords):
 
 def block_before(body, marker):
     """The instructions of the basic block that ends at `marker` (an asm comment the kernel
-    puts at the end of a loop body: the memory-bound skip and the full path, KCC_FIT_MSKIP)."""
+    puts at the end of a loop body)."""
     j = body.index(marker)
     st = max(body.rfind(".LBB", 0, j), body.rfind("; %bb.", 0, j))
     return [ln.strip() for ln in body[st:j].splitlines()[1:]
             if ln.strip() and not ln.strip().startswith(";")]
 
 
-def loop_header_loads(body, marker):
-    """Scalar loads of the inner loop's header: from the loop header label (the last label
-    marked 'Inner Loop Header' before the skip body) to the skip body."""
-    j = body.index(marker)
-    h = body.rfind("Inner Loop Header", 0, j)
-    seg = body[body.rfind(".LBB", 0, h):j]
-    return [ln.strip().split()[0] for ln in seg.splitlines() if ln.strip().startswith("s_load")]
+FULL = "; fit: full"
 
 
-SKIP, FULL = "; fit: memory-bound skip", "; fit: full"
-
-
-@pytest.mark.parametrize("mskip", [False, True])
-def test_fit_class_a_loop(asm, asm_mskip, mskip):
-    """Class A, per 8-node group: the full path (bench.FIT_VALU_PER_NODE_WAVE = 3 VALU per
-    node: packed f32 and f64 multiplies, min3, add), in the release build and beside the
-    memory-bound skip (KCC_FIT_MSKIP=1: 2, no f64 multiply, min with P) — no division,
-    conversion, correction, compare or select; with the skip every group's scalar loads
-    (fm, fc, P, its smallest V) issued before the branch; no vector memory in any body."""
+def test_fit_class_a_loop(asm):
+    """Class A, per 8-node group (bench.FIT_VALU_PER_NODE_WAVE = 3 VALU per node: packed f32
+    and f64 multiplies, min3, add) — no division, conversion, correction, compare or select;
+    no vector memory in the body."""
     import bench
-    body = kernel_body(asm_mskip if mskip else asm, FIT)
+    body = kernel_body(asm, FIT)
     full = block_before(body, FULL)
-    skip = block_before(body, SKIP) if mskip else full
-    assert (SKIP in body) == mskip
-    for lines in (full, skip):
-        assert not [ln for ln in lines if ln.startswith(("global_", "flat_", "buffer_", "ds_"))]
-    if mskip:
-        loads = loop_header_loads(body, SKIP)
-        assert loads.count("s_load_dwordx16") == 2 and loads.count("s_load_dword") == 1, loads
-    else:
-        check_loads(loop_of(body, FULL), GROUP * 4)  # fm (f64), fc, P (u32) per node
+    assert not [ln for ln in full if ln.startswith(("global_", "flat_", "buffer_", "ds_"))]
+    check_loads(loop_of(body, FULL), GROUP * 4)  # fm (f64), fc, P (u32) per node
     valu = [ln.split()[0] for ln in full if ln.startswith("v_")]
     assert len(valu) / GROUP == pytest.approx(bench.FIT_VALU_PER_NODE_WAVE, abs=1e-9), \
         f"{len(valu)} VALU / {GROUP} nodes: update bench.FIT_VALU_PER_NODE_WAVE"
     assert valu.count("v_pk_mul_f32") == GROUP // 2 and valu.count("v_mul_f64") == GROUP
     assert valu.count("v_min3_u32") == GROUP and valu.count("v_add3_u32") == GROUP // 2
-    sv = [ln.split()[0] for ln in skip if ln.startswith("v_")]
-    if mskip:
-        assert len(sv) / GROUP == pytest.approx(bench.FIT_SKIP_VALU_PER_NODE_WAVE, abs=1e-9)
-        assert sv.count("v_pk_mul_f32") == GROUP // 2 and "v_mul_f64" not in sv
-    for ops in (valu, sv):
-        assert not any(o.startswith(("v_mad", "v_cvt", "v_fma", "v_rcp", "v_div", "v_cmp",
-                                     "v_cndmask")) for o in ops)
+    assert not any(o.startswith(("v_mad", "v_cvt", "v_fma", "v_rcp", "v_div", "v_cmp",
+                                 "v_cndmask")) for o in valu)
 
 
 def test_fit_class_b_loop(asm):
@@ -149,27 +115,18 @@ def test_fit_class_b_loop(asm):
     assert not any(o.startswith(("v_cvt", "v_max", "v_mul", "v_cmp", "v_cndmask")) for o in ops)
 
 
-@pytest.mark.parametrize("mskip", [False, True])
-def test_fit_clamp_in_fit_loops(asm, asm_mskip, mskip):
+def test_fit_clamp_in_fit_loops(asm):
     """The clamp-in-fit variants (kcc_set_clamp_in_fit): class A takes each group's 8 clamp
     values by two 16-B vector loads (uniform address) so the select reads them as VGPRs:
-    5.0 VALU per node on the full path (min, compare, select in place of min3), 3.0 on the
-    memory-bound skip (x = qc: no f64 multiply, no min); class B (scalar loads) 6.5: fmin,
-    compare, a move of the clamp value into a VGPR (a gfx9 select reads one scalar operand at
-    most, vcc included), select in place of two min_f64."""
+    5.0 VALU per node (min, compare, select in place of min3); class B (scalar loads) 6.5:
+    fmin, compare, a move of the clamp value into a VGPR (a gfx9 select reads one scalar
+    operand at most, vcc included), select in place of two min_f64."""
     import bench
-    body = kernel_body(asm_mskip if mskip else asm, FIT_NC)
+    body = kernel_body(asm, FIT_NC)
     full = block_before(body, FULL)
     assert any(ln.startswith("v_cndmask") for ln in full)
     va = [ln for ln in full if ln.startswith("v_")]
     assert len(va) / GROUP == bench.FIT_NC_VALU_PER_NODE_WAVE, f"{len(va)} VALU / {GROUP} nodes"
-    if mskip:
-        skip = block_before(body, SKIP)
-        assert any(ln.startswith("v_cndmask") for ln in skip)
-        loads = loop_header_loads(body, SKIP)
-        assert loads.count("s_load_dwordx16") == 2 and loads.count("s_load_dword") == 1, loads
-        vs = [ln.split()[0] for ln in skip if ln.startswith("v_")]
-        assert len(vs) / GROUP == bench.FIT_NC_SKIP_VALU_PER_NODE_WAVE and "v_mul_f64" not in vs
     (b,) = loops_with(body, "v_fma_f64")
     assert any(ln.startswith("v_cndmask") for ln in b)
     check_loads(b, GROUP * 7)
@@ -261,13 +218,13 @@ def test_fit_claim_result_untouched_until_drained(asm):
 
 
 def test_reduce_lookback_tagged_words(asm):
-    """The reduce's look-back (KCC_RED_LB_MODE 2): each 32-bit half of a
+    """The reduce's look-back (tagged words): each 32-bit half of a
     carried sum travels in its own 64-bit word under a tag in the high half, so a word is
     complete when its tag is there — no ready flag, no fence. Pinned: the poll loop (the one
     with s_sleep) reads the 2 x NA = 4 words as single 64-bit agent-coherent loads
     (global_load_dwordx2 ... sc1, never split into dwords); the publish and the
     clean-on-consume are 64-bit sc1 stores; the kernel has no cache invalidate / write-back
-    (the acquire / release variant, KCC_RED_LB_MODE 1, measured 2.3x slower)."""
+    (the acquire / release variant measured 2.3x slower and was deleted)."""
     m = re.search(r"^(_ZN3kcc12_GLOBAL__N_1\d+reduce_kernelILi2E\w*):\s*;", asm, re.M)
     body = asm[m.end():asm.index(".Lfunc_end", m.end())]  # the whole function (several exits)
     polls = []

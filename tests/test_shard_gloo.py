@@ -247,3 +247,72 @@ def test_gpu_p2p_exchange_graph_replay(tmp_path):
             t, e = ref[k % 2]
             np.testing.assert_array_equal(got[k][:S], t, err_msg=f"rank {r} replay {k}")
             np.testing.assert_array_equal(got[k][S:], e, err_msg=f"rank {r} replay {k}")
+
+
+def _worker_fault(rank, world, port, n, pods, S, exchange, faultdiag, out):
+    """One rank's step with the library of `faultdiag` on rank `world - 1` only (every
+    bounded wait there gives up, so its reduce's look-back faults its device), the others
+    the release library; then the exchange: the one-shot p2p push (`p2p`) or a gloo
+    all-reduce of the partials finalized on every rank (`allreduce`)."""
+    import torch
+
+    from kubernetesclustercapacity_amd import CapacityEngine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard.node_range(n, rank, world)
+    c = synth.make_cluster(n, pods, seed=79, node_lo=lo, node_hi=hi, chunk=256)
+    sc, sm = synth.make_specs(S, seed=79)
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+    nl = c.alloc_cpu.size
+    uc = torch.empty(nl, dtype=torch.int64, device=dev)
+    um = torch.empty(nl, dtype=torch.int64, device=dev)
+    part = torch.empty(2 * S, dtype=torch.int64, device=dev)
+    totals = torch.empty(S, dtype=torch.int64, device=dev)
+    err = torch.empty(S, dtype=torch.int32, device=dev)
+    lib = faultdiag if rank == world - 1 else None
+    with CapacityEngine(0, 1, lib_path=lib) as eng:
+        if exchange == "p2p":
+            handles = [None] * world
+            dist.all_gather_object(handles, eng.p2p_export(world, S))
+            eng.p2p_open(rank, handles)
+            dist.barrier()
+        eng.capacity_partial_async(c.node_ptr, T(c.node_ptr), T(c.cpu_req), T(c.mem_req),
+                                   T(c.alloc_cpu), T(c.alloc_mem), T(c.alloc_pods),
+                                   T(c.pod_count), uc, um, T(sc), T(sm), part)
+        if exchange == "p2p":
+            eng.exchange_finalize_async(S, part, totals, err)
+        else:
+            torch.cuda.synchronize()
+            p = part.cpu()
+            shard.allreduce_partial(p)
+            eng.fit_finalize_async(S, p.to(dev), totals, err)
+        torch.cuda.synchronize()
+        got = np.concatenate([totals.cpu().numpy(), err.cpu().numpy().astype(np.int64),
+                              [eng.reduce_faults()]])
+        dist.barrier()  # no rank unmaps its mailbox while a peer may still push
+    np.save(out + f".{rank}.npy", got)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exchange", ["p2p", "allreduce"])
+def test_gpu_fault_reaches_every_rank(tmp_path, exchange):
+    """A device fault on ONE rank (its reduce's look-back gave up: the fault-path build on
+    the last rank) reaches every rank's totals: the faulted rank's partial carries
+    SPEC_FAULT_MARK in its div-by-zero counts, so the healthy rank's finalize — after the
+    p2p exchange or after an all-reduce — marks every spec KCC_SPEC_FAULT with total 0,
+    never a wrong total with spec_err 0."""
+    faultdiag = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                             "kubernetesclustercapacity_amd", "libkcc_faultdiag.so")
+    if not os.path.exists(faultdiag):
+        pytest.fail("libkcc_faultdiag.so missing: __graft_entry__.build() builds it")
+    n, pods, S, world = 20_011, 300_000, 300, 2
+    out = str(tmp_path / "flt")
+    mp.spawn(_worker_fault, args=(world, _free_port(), n, pods, S, exchange, faultdiag, out),
+             nprocs=world, join=True)
+    for r in range(world):
+        got = np.load(out + f".{r}.npy")
+        assert (got[S:2 * S] == 2).all(), f"rank {r}: spec_err {np.unique(got[S:2 * S])}"
+        assert (got[:S] == 0).all(), f"rank {r}"
+        assert (got[-1] > 0) == (r == world - 1), f"rank {r} reduce faults {got[-1]}"
