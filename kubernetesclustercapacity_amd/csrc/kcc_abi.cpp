@@ -298,8 +298,9 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.sperm, 4 * S));
   KCC_HIP(ctx, ensure(dv.counters, sizeof(unsigned long long) * kcc::CNT_N));
   if (!dv.clamp_arrive.p) {  // the fused finalize's arrivals: every launch leaves them zero
-    KCC_HIP(ctx, ensure(dv.clamp_arrive, 64));
-    KCC_HIP(ctx, hipMemsetAsync(dv.clamp_arrive.p, 0, 64, dv.stream));
+    // (top counter + 8 group counters, one 64-B line each)
+    KCC_HIP(ctx, ensure(dv.clamp_arrive, 9 * 64));
+    KCC_HIP(ctx, hipMemsetAsync(dv.clamp_arrive.p, 0, 9 * 64, dv.stream));
     KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
   }
   // (a new allocation is a larger one: compare sizes, hipMalloc may hand back the address)
@@ -403,7 +404,7 @@ kcc::PlaceArgs place_args(Dev& dv, int64_t n_specs, const uint64_t* spec_cpu,
                           const int64_t* spec_mem, int64_t* partial) {
   return kcc::PlaceArgs{n_specs, spec_cpu, spec_mem, spec_prep_of(dv), clamp_of(dv), partial,
                         as<unsigned long long>(dv.counters), 0,
-                        as<const unsigned long long>(dv.faults)};
+                        as<const unsigned long long>(dv.faults), 0};
 }
 
 int fit_prepare_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, const uint64_t* alloc_cpu,
@@ -600,10 +601,13 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                    (dv.clamp_in_fit < 0 && kcc::clamp_in_fit_auto(n_nodes, n_specs)));
   int32_t* const fast_cl = nc ? as<int32_t>(dv.fast_cl) : nullptr;
   dv.last_nc = nc;
+  // the clamp in the fit needs no spec ranks (no clamp tables): the reduce launch carries
+  // one workgroup that zeroes the counters, and spec_place counts the classes itself
   const kcc::RankArgs ra = kcc::rank_args(n_specs, spec_cpu, spec_mem, clamp_of(dv),
                                           as<unsigned long long>(dv.counters),
-                                          as<uint32_t>(dv.rank_arrive));
-  const kcc::PlaceArgs pa = place_args(dv, n_specs, spec_cpu, spec_mem, partial);
+                                          as<uint32_t>(dv.rank_arrive), nc);
+  kcc::PlaceArgs pa = place_args(dv, n_specs, spec_cpu, spec_mem, partial);
+  pa.no_ranks = nc ? 1 : 0;
   if (n_specs > 0) {
     rc = clamp_clean(ctx, dv, s);
     if (rc) return rc;
@@ -660,7 +664,8 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                  as<int64_t>(dv.slow_list) + lo[c], n_specs, spec_prep_of(dv),
                                  partial, as<unsigned long long>(dv.counters),
                                  as<uint32_t>(dv.fit_q), c, n_nodes, s,
-                                 as<const unsigned long long>(dv.faults), fast_cl));
+                                 as<const unsigned long long>(dv.faults), fast_cl,
+                                 nc && fuse_fin ? &fin : nullptr));
     if (dv.prof_on) {
       KCC_HIP(ctx, hipEventRecord(pp.b, s));
       pp.kind = 1;
@@ -671,7 +676,8 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   // the clamp launch's last workgroup also finalizes (no fit_finalize launch)
   if (n_specs > 0 && nc) {  // the fit applied the clamp: no clamp_apply, nothing dirty
     dv.clamp_dirty = false;
-    if (totals) return fit_finalize_dev(ctx, dv, n_specs, partial, totals, spec_err, s);
+    // (the fit's last workgroup finalized, unless there were no nodes: no fit launch)
+    if (totals && !fuse_fin) return fit_finalize_dev(ctx, dv, n_specs, partial, totals, spec_err, s);
     return KCC_OK;
   }
   if (n_specs > 0) {

@@ -273,9 +273,13 @@ struct RankArgs {
   int64_t c_stride, c_cells;
   unsigned long long* counters;
   int32_t n_blocks;    // 256-thread workgroups: rank_slices(S)^2 (0: none)
+  // 1: the clamp in the fit needs no ranks — one workgroup that zeroes the counters and
+  // writes the block class counts (bcnt) alone (PlaceArgs::no_ranks)
+  int32_t zero_only;
 };
 RankArgs rank_args(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
-                   const ClampWork& cw, unsigned long long* counters, uint32_t* arrive);
+                   const ClampWork& cw, unsigned long long* counters, uint32_t* arrive,
+                   bool zero_only = false);
 hipError_t launch_spec_rank(const RankArgs& ra, hipStream_t s);
 
 // spec_place's work (one thread per spec), run as extra workgroups in front of the
@@ -293,6 +297,9 @@ struct PlaceArgs {
   unsigned long long* counters;
   int32_t n_blocks;  // workgroups of the launch's block size (0: none)
   const unsigned long long* faults;  // set: partial[S + i] starts at SPEC_FAULT_MARK
+  // 1 (the clamp in the fit, S <= CLAMP_LDS_SPECS): no spec ranks ran (only bcnt was
+  // written): nothing rank-indexed is read or written
+  int32_t no_ranks;
 };
 
 

@@ -1425,6 +1425,32 @@ __device__ void spec_rank_sort(const RankArgs& ra, int64_t blk, uint64_t* lds) {
 
 __device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds) {
   const int tid = threadIdx.x;
+  if (ra.zero_only) {
+    // the clamp in the fit needs no ranks: this one workgroup zeroes the counters and
+    // writes what spec_place and node_prep read of the ranks' output — the class counts
+    // of every 64-spec block (bcnt) — from the classes of the S <= CLAMP_LDS_SPECS specs
+    // (wave w: blocks w, w + 4, ...; one ballot per block)
+    if (tid < CNT_N && tid != CNT_SPECS_A && tid != CNT_SPECS_B) ra.counters[tid] = 0;
+    const int lane = tid & 63;
+    const int64_t nqb = (ra.S + 63) / 64;
+    int32_t cls[CLAMP_LDS_SPECS / 256];
+#pragma unroll
+    for (int u = 0; u < (int)(CLAMP_LDS_SPECS / 256); ++u) {  // every load first
+      const int64_t j = ((int64_t)(tid >> 6) + 4 * u) * 64 + lane;
+      cls[u] = j < ra.S ? spec_class(ra.c_in[j], ra.m_in[j]) : SPEC_EXACT;
+    }
+#pragma unroll
+    for (int u = 0; u < (int)(CLAMP_LDS_SPECS / 256); ++u) {
+      const int64_t qb = (tid >> 6) + 4 * u;
+      const uint32_t na = (uint32_t)__popcll(__ballot(cls[u] == SPEC_A));
+      const uint32_t nb = (uint32_t)__popcll(__ballot(cls[u] == SPEC_B));
+      if (qb < nqb && lane == 0) {
+        ra.bcnt[2 * qb] = na;
+        ra.bcnt[2 * qb + 1] = nb;
+      }
+    }
+    return;
+  }
   {  // zero duties, spread over the workgroups
     const int64_t gt = blk * 256 + tid, nt = (int64_t)ra.n_blocks * 256;
     if (gt < CNT_N && gt != CNT_SPECS_A && gt != CNT_SPECS_B) ra.counters[gt] = 0;
@@ -1463,7 +1489,8 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   const int64_t m = in ? m_in[i] : 0;
   const int32_t cls = in ? spec_class(c, m) : SPEC_EXACT;
   const bool normal = cls != SPEC_EXACT;
-  const uint32_t x = in && normal ? cw.rank[i] : 0u;  // the x-rank (spec_rank's last arrivers)
+  // the x-rank (spec_rank's last arrivers; none with no_ranks)
+  const uint32_t x = in && normal && !pa.no_ranks ? cw.rank[i] : 0u;
   // class totals and this block's prefix: the wave's lanes take every 64th block (the
   // counts packed A | B << 32), then one DPP scan each
   uint64_t tot = 0, pre = 0;
@@ -1481,7 +1508,7 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   const unsigned long long mA = __ballot(cls == SPEC_A && in), mB = __ballot(cls == SPEC_B && in);
   const unsigned long long below = (1ull << lane) - 1ull;
   const uint32_t rA = (uint32_t)__popcll(mA & below), rB = (uint32_t)__popcll(mB & below);
-  if (i >= nN && i < (nN + 63) / 64 * 64) {  // padding of the last x-group / y-block
+  if (!pa.no_ranks && i >= nN && i < (nN + 63) / 64 * 64) {  // padding of the last x-group / y-block
     cw.mr_c[i] = 0xffffffffu;
     cw.cr_m[i] = 0xffffffffu;
   }
@@ -1506,7 +1533,7 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   partial[i] = 0;
   // (spec_place runs after this step's reduce: its look-back give-ups are in the words)
   partial[S + i] = device_faulted(pa.faults) ? (int64_t)SPEC_FAULT_MARK : 0;
-  if (!normal) return;
+  if (!normal || pa.no_ranks) return;
   cw.dperm[x] = (int32_t)pos;
 }
 
@@ -1782,17 +1809,35 @@ __device__ __forceinline__ void clamp_apply_bin(const ClampWork& cw, int64_t S,
   KCC_TL(1024 + blockIdx.x % 1024, 4);
 }
 
-// The fused finalize (clamp_apply_kernel): every wave's atomics into partial are performed
-// (vmcnt counts the stores and atomics too on gfx9) before the workgroup arrives; the last
-// of the launch's workgroups to arrive reads partial at agent scope and writes the totals
-// in caller order.  Every thread of the workgroup calls.
-__device__ void fused_finalize(const FinArgs& fin, int64_t S, const int64_t* partial) {
+// The fused finalize (clamp_apply_kernel; the fit when it applies the clamp itself): every
+// wave's atomics into partial are performed (vmcnt counts the stores and atomics too on
+// gfx9) before the workgroup arrives; the last workgroup to arrive reads partial at agent
+// scope and writes the totals in caller order.  Every thread of the workgroup calls, from
+// one call site.
+// One counter takes about 12 ns per arrival when they bunch up (MI355X_MICROARCH.md
+// 'fanin'): fine for clamp_apply's ~256 workgroups, 25 us for the fit's 2048.  With
+// `groups` > 0 the arrivals are two-level: a workgroup arrives on the counter of its group
+// `grp` (one 64-B line each, `grp_n` arrivals), the last of each group on the top counter
+// (`groups` arrivals), and the last of those finalizes.  `arrivals` (one level): the
+// workgroups that call it (every one of the launch by default).  Counters: FinArgs::arrive
+// (top at word 0, group g at word 16 (g + 1)); each last arriver resets its counter.
+__device__ void fused_finalize(const FinArgs& fin, int64_t S, const int64_t* partial,
+                               uint32_t arrivals = 0, uint32_t groups = 0, uint32_t grp = 0,
+                               uint32_t grp_n = 0) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   __shared__ uint32_t last_s;
-  if (threadIdx.x == 0)
-    last_s = __hip_atomic_fetch_add(fin.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-             gridDim.x - 1u;
+  const uint32_t expect = groups ? groups : arrivals ? arrivals : gridDim.x;
+  if (threadIdx.x == 0) {
+    bool go = true;
+    if (groups) {  // the group's counter first
+      uint32_t* g = fin.arrive + 16u * (grp + 1u);
+      go = __hip_atomic_fetch_add(g, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == grp_n - 1u;
+      if (go) __hip_atomic_store(g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    last_s = go && __hip_atomic_fetch_add(fin.arrive, 1u, __ATOMIC_ACQ_REL,
+                                          __HIP_MEMORY_SCOPE_AGENT) == expect - 1u;
+  }
   __syncthreads();
   if (!last_s) return;
   if (threadIdx.x == 0) __hip_atomic_store(fin.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1992,7 +2037,16 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   KCC_TL(2048 + b % 4096, 5);  // (the spec records are in)
 
   // the node stream node_prep wrote (its length is on the device; 32-bit: < 2^31 groups)
+#ifdef KCC_FIT_NG_VLOAD
+  // A/B: the stream length by a vector load (the vector memory path, not the scalar cache
+  // that the running waves' node groups stream through)
+  const __amdgpu_buffer_rsrc_t ng_rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(counters + CNT_STREAM + chunk), (short)0, 8, 0x00020000);
+  const uint32_t n_groups = (uint32_t)__builtin_amdgcn_readfirstlane(
+      (int32_t)((uint32_t)__builtin_amdgcn_raw_buffer_load_b32(ng_rs, 0, 0, 0) / FIT_GROUP));
+#else
   const uint32_t n_groups = (uint32_t)(counters[CNT_STREAM + chunk] / FIT_GROUP);
+#endif
   uint32_t lim = n_groups;  // claims end here
   uint32_t base = 0;        // queue: the segment's start
   uint32_t nxt = 0;         // queue: the claim in flight (wave 0, lane 0); static: next chunk
@@ -2015,6 +2069,9 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     const uint32_t sh = n_groups / (uint32_t)gy / FIT_Q1_DIV;
     q1 = sh < q1 ? (sh > FIT_QMIN ? sh : FIT_QMIN) : q1;
   }
+#ifdef KCC_FIT_QFIX  // A/B: every claim (the static first one too) of KCC_FIT_QFIX groups
+  q1 = KCC_FIT_QFIX;
+#endif
   __shared__ uint32_t q_slot[2];
   // lane 0 of wave 0 issues the claim in asm, so the compiler does not wait for it where
   // it is issued (its atomic-optimizer expansion reads the result at once); wave 0 waits
@@ -2232,6 +2289,10 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
       const uint32_t rem = lim - cur;
       uint32_t qn = rem / (FIT_QDIV * wps);
       qn = qn < FIT_QMIN ? FIT_QMIN : (qn > qsz ? qsz : qn);
+#ifdef KCC_FIT_QFIX
+      qn = KCC_FIT_QFIX;
+      (void)rem;
+#endif
       claim_issue(qn);
       const int cnt = (int)((cur + qcur < lim ? cur + qcur : lim) - cur);
       qcur = qn;
@@ -2256,10 +2317,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     }
   }
   KCC_TL(2048 + b % 4096, 2);
-  if (idle) {  // (the fused finalize's arrival needs every wave at its barrier)
-    if (fin.totals) fused_finalize(fin, S, partial);
-    return;
-  }
+  if (!idle) {  // (a wave wholly past S falls through to the fused finalize's barrier)
   if (wave_exact) {  // exact-path specs: every node row (SlowNode), this workgroup's share
     const uint32_t nn = (uint32_t)n_nodes;  // < 2^28 per device
     const uint32_t pn = (nn + (uint32_t)gy - 1u) / (uint32_t)gy;
@@ -2286,8 +2344,17 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[s]), acc);
     if (errs) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[S + s]), errs);
   }
+  }  // (!idle)
   KCC_TL(2048 + b % 4096, 3);
-  if (fin.totals) fused_finalize(fin, S, partial);  // (the clamp correction beside the fit)
+  // the clamp in the fit at N = 1 (the step's last kernel): the last of the gx x gy working
+  // workgroups to arrive writes the totals (the grid's XCD padding returned at entry).
+  // Two-level arrivals by blockIdx % 8 (one XCD each under round-robin placement): group x
+  // holds the workgroups with by = 8 t + x < gy, gx x ceil((gy - x) / 8) of them
+  if (fin.totals) {
+    const uint32_t ngrp = gy < 8 ? (uint32_t)gy : 8u;
+    const uint32_t gn = (uint32_t)gx * (((uint32_t)gy - (uint32_t)xcd + 7u) / 8u);
+    fused_finalize(fin, S, partial, 0, ngrp, (uint32_t)xcd, gn);
+  }
 }
 
 __global__ void fit_finalize_kernel(int64_t S, const int64_t* __restrict__ partial,
@@ -2467,10 +2534,13 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
   }
   if (!red && ra.n_blocks == 0) return hipSuccess;
   if (limits && ra.n_blocks > 0) return hipErrorInvalidValue;  // (the ranks ride NA = 2 only)
-  // the rank workgroups: behind the reduce's on long reduces, so they take the slots
-  // of its first waves to finish; in front (0), they held their slots ~2 us while the
-  // reduce's range is sized for the whole device (its last waves started when they exited)
-  const int32_t range = red ? reduce_range(n_containers, limits, 0) : RED_TILE;
+  // the rank workgroups: behind the reduce's on long reduces, so they take the slots of
+  // its first waves to finish; in front on short ones, where the reduce's range is sized
+  // for the slots they leave (one round of workgroups: a reduce workgroup that waited for
+  // a rank workgroup's slot started ~10 us late on the 8-way C4 rank, round 5)
+  const bool ranks_last = n_containers >= RED_RANKS_LAST_MIN;
+  const int64_t reserve = ranks_last ? 0 : (int64_t)RED_WAVES_PER_BLOCK * ra.n_blocks;
+  const int32_t range = red ? reduce_range(n_containers, limits, reserve) : RED_TILE;
   const int64_t waves = red ? (n_containers + range - 1) / range : 0;
   if (waves > reduce_tail_records()) return hipErrorInvalidValue;
   const unsigned blocks =
@@ -2491,7 +2561,7 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
   a.out[3] = limits ? reinterpret_cast<uint64_t*>(lim_mem) : nullptr;
   a.tail = tail;
   a.faults = faults;
-  a.ranks_last = n_containers >= RED_RANKS_LAST_MIN ? 1 : 0;
+  a.ranks_last = ranks_last ? 1 : 0;
   if (limits)
     hipLaunchKernelGGL(reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, a, ra);
   else
@@ -2537,7 +2607,8 @@ hipError_t launch_node_prep(int64_t n_nodes, const uint64_t* alloc_cpu,
 }
 
 RankArgs rank_args(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
-                   const ClampWork& cw, unsigned long long* counters, uint32_t* arrive) {
+                   const ClampWork& cw, unsigned long long* counters, uint32_t* arrive,
+                   bool zero_only) {
   RankArgs ra{};
   ra.S = n_specs;
   ra.c_in = spec_cpu;
@@ -2555,8 +2626,10 @@ RankArgs rank_args(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spe
   ra.c_cells = wmax * wmax < cw.c_stride ? wmax * wmax : cw.c_stride;
   ra.counters = counters;
   ra.n_blocks = n_specs <= 0 ? 0
+               : zero_only ? 1
                : n_specs <= RANK_FULL_MAX ? (int32_t)((n_specs + 63) / 64 * rank_slices(n_specs))
                                           : (int32_t)(rank_slices(n_specs) * rank_slices(n_specs));
+  ra.zero_only = zero_only ? 1 : 0;
   return ra;
 }
 

@@ -112,6 +112,68 @@ def run(names, config, rounds, reps, shard=1):
                           "identical_outputs": not nm.startswith("diag_")}))
 
 
+def run_step(names, config, rounds, reps, shard=1):
+    """The whole device step (kcc_capacity_async: reduce + spec setup + node prep + fit +
+    clamp / finalize, the clamp in the fit by size) on rank 0's shard of `shard`, every
+    variant's totals checked equal to the first's."""
+    import numpy as np
+    import torch
+
+    from kubernetesclustercapacity_amd import _lib, synth
+
+    dev = torch.device("cuda", 0)
+    n_all = synth.CONFIGS[config]["n_nodes"]
+    cl = synth.config_cluster(config, node_lo=0, node_hi=n_all // shard, limits=False)
+    sc, sm = synth.config_specs(config)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+    args = [T(x) for x in (cl.node_ptr, cl.cpu_req, cl.mem_req, cl.alloc_cpu, cl.alloc_mem,
+                           cl.alloc_pods, cl.pod_count)]
+    n, S, nc = cl.n_nodes, sc.size, cl.n_containers
+    uc = torch.empty(n, dtype=torch.int64, device=dev)
+    um = torch.empty(n, dtype=torch.int64, device=dev)
+    s_cpu, s_mem = T(sc), T(sm)
+    tot = torch.empty(S, dtype=torch.int64, device=dev)
+    err = torch.empty(S, dtype=torch.int32, device=dev)
+    P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    stream = torch.cuda.Stream(dev)
+    sh = C.c_void_p(stream.cuda_stream)
+    libs, ctxs = {}, {}
+    for nm in names:
+        L = _lib.load(os.path.join(VDIR, f"libkcc_{nm}.so"))
+        h = C.c_void_p()
+        assert L.kcc_create(C.byref(h), 0, 1) == 0, L.kcc_create_error()
+        assert L.kcc_reserve(h, n, nc, S) == 0
+        libs[nm], ctxs[nm] = L, h
+
+    def step(nm):
+        assert libs[nm].kcc_capacity_async(ctxs[nm], n, nc, None, *[P(a) for a in args], P(uc),
+                                           P(um), S, P(s_cpu), P(s_mem), P(tot), P(err), sh) == 0
+    times = {nm: [] for nm in names}
+    golden = {}
+    with torch.cuda.stream(stream):
+        for nm in names:
+            for _ in range(3):
+                step(nm)
+            torch.cuda.synchronize()
+            golden[nm] = (tot.clone(), err.clone())
+        for _ in range(rounds):
+            for nm in names:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(reps):
+                    step(nm)
+                e1.record(stream)
+                e1.synchronize()
+                times[nm].append(e0.elapsed_time(e1) / reps)
+    ref = names[0]
+    for nm in names:
+        same = bool(torch.equal(golden[nm][0], golden[ref][0]) and torch.equal(golden[nm][1], golden[ref][1]))
+        assert same or nm.startswith("diag_"), f"{nm} totals differ from {ref}"
+        print(json.dumps({"variant": nm, "config": config, "shard": shard,
+                          "step_ms_median": float(np.median(times[nm])),
+                          "step_ms_min": float(np.min(times[nm])), "identical_totals": same}))
+
+
 def run_keyed(names, config, rounds, reps):
     """The keyed (list-order) reduce on the config's containers in a random order (the
     bench's keyed leg), every variant checked equal to the CSR sums."""
@@ -248,8 +310,11 @@ if __name__ == "__main__":
         ap.add_argument("--shard", type=int, default=1, help="use rank 0's nodes of this many")
         ap.add_argument("--keyed", action="store_true", help="time the keyed reduce instead")
         ap.add_argument("--parse", action="store_true", help="time the quantity-string kernels instead")
+        ap.add_argument("--step", action="store_true", help="time the whole kcc_capacity_async step")
         a = ap.parse_args()
-        if a.parse:
+        if a.step:
+            run_step(a.names, a.config, a.rounds, a.reps, a.shard)
+        elif a.parse:
             run_parse(a.names, a.config, a.rounds, a.reps)
         elif a.keyed:
             run_keyed(a.names, a.config, a.rounds, a.reps)
