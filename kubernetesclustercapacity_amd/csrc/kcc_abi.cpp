@@ -637,6 +637,12 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   const bool fuse_fin = totals && n_nodes > 0;
   const kcc::FinArgs fin{as<int32_t>(dv.sperm), totals, spec_err, as<uint32_t>(dv.clamp_arrive),
                          as<const unsigned long long>(dv.faults)};
+  int last_fit = -1;  // the chunk whose fit launch is the step's last (it finalizes in NC mode)
+  for (int c = 0; c < k; ++c)
+    if (hi[c] > lo[c]) last_fit = c;
+#ifdef KCC_AB_NOFITFUSE
+  last_fit = -2;
+#endif
   for (int c = 0; c < k; ++c) {
     if (k > 1) KCC_HIP(ctx, hipStreamWaitEvent(s, dv.ev_red[c], 0));  // also joins the side stream
     const int64_t n = hi[c] - lo[c];
@@ -665,7 +671,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                  partial, as<unsigned long long>(dv.counters),
                                  as<uint32_t>(dv.fit_q), c, n_nodes, s,
                                  as<const unsigned long long>(dv.faults), fast_cl,
-                                 nc && fuse_fin ? &fin : nullptr));
+                                 nc && fuse_fin && c == last_fit ? &fin : nullptr));
     if (dv.prof_on) {
       KCC_HIP(ctx, hipEventRecord(pp.b, s));
       pp.kind = 1;
@@ -677,7 +683,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   if (n_specs > 0 && nc) {  // the fit applied the clamp: no clamp_apply, nothing dirty
     dv.clamp_dirty = false;
     // (the fit's last workgroup finalized, unless there were no nodes: no fit launch)
-    if (totals && !fuse_fin) return fit_finalize_dev(ctx, dv, n_specs, partial, totals, spec_err, s);
+    if (totals && (!fuse_fin || last_fit < 0)) return fit_finalize_dev(ctx, dv, n_specs, partial, totals, spec_err, s);
     return KCC_OK;
   }
   if (n_specs > 0) {

@@ -207,6 +207,13 @@ __device__ __forceinline__ void load_quad(__amdgpu_buffer_rsrc_t r, int32_t voff
 // container up to its own and stores node0 (decoupled look-back: each wave publishes
 // before it waits, so waits never chain; a wave waits only for lower-indexed waves,
 // dispatched before it).  No atomics, nothing to zero between launches.
+// The tile-local prefix strip: position p (lane p / RED_IPL's item p % RED_IPL) at
+// strip_at(p) of the wave's strip: pair-major — item pair h of every lane together, so the
+// lanes' 16-B stores are 16 B apart (conflict-free; lane-major, 64 B apart, is 4-way)
+__device__ __forceinline__ int32_t strip_at(int32_t p) {
+  static_assert(RED_IPL == 8, "pair-major strip");
+  return ((p & 6) << 6) + ((p >> 3) << 1) + (p & 1);
+}
 constexpr uint32_t RED_OOB_OFFSET = 0x7ffffff0u;  // > any output's range (n_nodes < 2^28)
 [[maybe_unused]] constexpr uint32_t RED_SPIN_MAX = 1u << 18;       // look-back polls before a wait gives up
 // Look-back publication: tagged words.  Each 64-bit value of the piece travels as two
@@ -391,9 +398,9 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
       pp[RED_IPL - 1] = P[k];
 #pragma unroll
       for (int i = RED_IPL - 1; i > 0; --i) pp[i - 1] = pp[i] - x[k][i];
-      u64x2* dst = reinterpret_cast<u64x2*>(&pre[k][RED_IPL * lane]);
+      u64x2* dst = reinterpret_cast<u64x2*>(&pre[k][0]);  // pair h at strip_at(8 lane + 2 h)
 #pragma unroll
-      for (int h = 0; h < RED_IPL / 2; ++h) dst[h] = u64x2{pp[2 * h], pp[2 * h + 1]};
+      for (int h = 0; h < RED_IPL / 2; ++h) dst[h * 64 + lane] = u64x2{pp[2 * h], pp[2 * h + 1]};
       tot[k] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(P[k] >> 32), 63) << 32) |
                (uint32_t)__builtin_amdgcn_readlane((uint32_t)P[k], 63);
     }
@@ -418,7 +425,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
       const int32_t is = min(max(s - 1 - tb, 0), RED_TILE - 1);
 #pragma unroll
       for (int k = 0; k < NA; ++k) {
-        const uint64_t pe = pre[k][ie], ps = pre[k][is];
+        const uint64_t pe = pre[k][strip_at(ie)], ps = pre[k][strip_at(is)];
         const uint64_t startp = s > tb ? ps : (0ull - carry[k]);
         const uint64_t sum = eA > s ? pe - startp : 0ull;
         res[k] = act ? sum : res[k];
@@ -454,7 +461,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
     if (last_end > tb) {  // node cur is open at the tile end: its sum so far
 #pragma unroll
       for (int k = 0; k < NA; ++k)
-        carry[k] = tot[k] - pre[k][last_end - 1 - tb];
+        carry[k] = tot[k] - pre[k][strip_at(last_end - 1 - tb)];
     } else if (last_end == tb) {  // only empty nodes ended, at the tile's start (wave 0's
 #pragma unroll                    // leading empty nodes): cur starts here
       for (int k = 0; k < NA; ++k) carry[k] = tot[k];
@@ -1814,28 +1821,33 @@ __device__ __forceinline__ void clamp_apply_bin(const ClampWork& cw, int64_t S,
 // gfx9) before the workgroup arrives; the last workgroup to arrive reads partial at agent
 // scope and writes the totals in caller order.  Every thread of the workgroup calls, from
 // one call site.
-// One counter takes about 12 ns per arrival when they bunch up (MI355X_MICROARCH.md
-// 'fanin'): fine for clamp_apply's ~256 workgroups, 25 us for the fit's 2048.  With
-// `groups` > 0 the arrivals are two-level: a workgroup arrives on the counter of its group
-// `grp` (one 64-B line each, `grp_n` arrivals), the last of each group on the top counter
-// (`groups` arrivals), and the last of those finalizes.  `arrivals` (one level): the
-// workgroups that call it (every one of the launch by default).  Counters: FinArgs::arrive
-// (top at word 0, group g at word 16 (g + 1)); each last arriver resets its counter.
+//
+// The hand-off needs no cache maintenance: the payload (partial) is written only by 8-B
+// agent-scope atomics and read only by 8-B agent-scope loads, every wave waits for its
+// atomics (vmcnt(0)) before the workgroup barrier, and one lane then makes a RELAXED
+// agent-scope add to the arrival counter — MI355X_MICROARCH.md's "{8-B agent atomics both
+// sides}" form with the "workgroup whose add came last" signal (an acq_rel add lowers to a
+// buffer_wbl2 + buffer_inv pair per workgroup: an L2 write-back each).
+//
+// One counter takes about 12 ns per arrival when they bunch up ('fanin'): with `groups`
+// > 0 the arrivals are two-level — a workgroup arrives on its group `grp`'s counter
+// (`grp_n` arrivals), the last of each group on the top counter (`groups` arrivals), and
+// the last of those finalizes.  Counters: FinArgs::arrive (top at word 0, group g at word
+// 16 (g + 1)); each last arriver resets its counter.
 __device__ void fused_finalize(const FinArgs& fin, int64_t S, const int64_t* partial,
-                               uint32_t arrivals = 0, uint32_t groups = 0, uint32_t grp = 0,
-                               uint32_t grp_n = 0) {
+                               uint32_t groups = 0, uint32_t grp = 0, uint32_t grp_n = 0) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   __shared__ uint32_t last_s;
-  const uint32_t expect = groups ? groups : arrivals ? arrivals : gridDim.x;
+  const uint32_t expect = groups ? groups : gridDim.x;
   if (threadIdx.x == 0) {
     bool go = true;
     if (groups) {  // the group's counter first
       uint32_t* g = fin.arrive + 16u * (grp + 1u);
-      go = __hip_atomic_fetch_add(g, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == grp_n - 1u;
+      go = __hip_atomic_fetch_add(g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == grp_n - 1u;
       if (go) __hip_atomic_store(g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    last_s = go && __hip_atomic_fetch_add(fin.arrive, 1u, __ATOMIC_ACQ_REL,
+    last_s = go && __hip_atomic_fetch_add(fin.arrive, 1u, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT) == expect - 1u;
   }
   __syncthreads();
@@ -2037,19 +2049,10 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   KCC_TL(2048 + b % 4096, 5);  // (the spec records are in)
 
   // the node stream node_prep wrote (its length is on the device; 32-bit: < 2^31 groups)
-#ifdef KCC_FIT_NG_VLOAD
-  // A/B: the stream length by a vector load (the vector memory path, not the scalar cache
-  // that the running waves' node groups stream through)
-  const __amdgpu_buffer_rsrc_t ng_rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(counters + CNT_STREAM + chunk), (short)0, 8, 0x00020000);
-  const uint32_t n_groups = (uint32_t)__builtin_amdgcn_readfirstlane(
-      (int32_t)((uint32_t)__builtin_amdgcn_raw_buffer_load_b32(ng_rs, 0, 0, 0) / FIT_GROUP));
-#else
   const uint32_t n_groups = (uint32_t)(counters[CNT_STREAM + chunk] / FIT_GROUP);
-#endif
   uint32_t lim = n_groups;  // claims end here
   uint32_t base = 0;        // queue: the segment's start
-  uint32_t nxt = 0;         // queue: the claim in flight (wave 0, lane 0); static: next chunk
+  uint32_t nxt = 0;         // queue: the claim in flight (wave 0, lane 0)
   // sub-queues: gy if gy < 8, else 8, 16 or 32 (a power of two: whole XCDs each), about
   // FIT_WG_PER_SUB workgroups per sub-queue (measured: 56 per line 8 % slower at C4 than
   // 28; fewer than 2 per line lose the balancing)
@@ -2069,9 +2072,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     const uint32_t sh = n_groups / (uint32_t)gy / FIT_Q1_DIV;
     q1 = sh < q1 ? (sh > FIT_QMIN ? sh : FIT_QMIN) : q1;
   }
-#ifdef KCC_FIT_QFIX  // A/B: every claim (the static first one too) of KCC_FIT_QFIX groups
-  q1 = KCC_FIT_QFIX;
-#endif
+
   __shared__ uint32_t q_slot[2];
   // lane 0 of wave 0 issues the claim in asm, so the compiler does not wait for it where
   // it is issued (its atomic-optimizer expansion reads the result at once); wave 0 waits
@@ -2289,10 +2290,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
       const uint32_t rem = lim - cur;
       uint32_t qn = rem / (FIT_QDIV * wps);
       qn = qn < FIT_QMIN ? FIT_QMIN : (qn > qsz ? qsz : qn);
-#ifdef KCC_FIT_QFIX
-      qn = KCC_FIT_QFIX;
-      (void)rem;
-#endif
+
       claim_issue(qn);
       const int cnt = (int)((cur + qcur < lim ? cur + qcur : lim) - cur);
       qcur = qn;
@@ -2353,7 +2351,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   if (fin.totals) {
     const uint32_t ngrp = gy < 8 ? (uint32_t)gy : 8u;
     const uint32_t gn = (uint32_t)gx * (((uint32_t)gy - (uint32_t)xcd + 7u) / 8u);
-    fused_finalize(fin, S, partial, 0, ngrp, (uint32_t)xcd, gn);
+    fused_finalize(fin, S, partial, ngrp, (uint32_t)xcd, gn);
   }
 }
 

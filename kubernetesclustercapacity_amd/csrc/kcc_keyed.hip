@@ -669,6 +669,168 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
   }
 }
 
+// kb_sweep_p (KCC_KB_SWP): kb_sweep as a persistent, software-pipelined loop.  One
+// workgroup per CU walks the tiles g = blockIdx.x, + gridDim.x, ... of KB_SWP_TILE
+// containers (8 per thread); the next tile's loads (range-checked buffer loads, so their
+// count is static) go out before the current tile's ranks, scan, scatter and stores, so
+// the CU's HBM traffic never stops for the LDS work (kb_sweep: load, then work, then
+// store, one tile at a time, every phase alone on the CU).  Same records, table rows and
+// escape list as kb_sweep; tile g's records at sr[g * KB_SWP_TILE].
+constexpr int KB_SWP_PER = 8;
+constexpr int KB_SWP_TILE = KB_SW_THREADS * KB_SWP_PER;  // 8192
+template <int NA>
+__global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep_p(
+    int64_t n, int64_t n_keys, const int32_t* __restrict__ key, const uint64_t* __restrict__ a0,
+    const uint64_t* __restrict__ a1, int nb, uint32_t* __restrict__ tab, uint64_t* __restrict__ sr,
+    uint32_t* __restrict__ esc_n, int32_t* __restrict__ esc_row, uint64_t* __restrict__ esc_cpu,
+    uint64_t* __restrict__ esc_mem, int64_t tile, int64_t G) {
+  static_assert(NA == 0 || NA == 2, "one-sweep path: counts or requests");
+  constexpr int NS = NA > 0 ? NA : 1;
+  constexpr int PER = KB_SWP_PER;
+  __shared__ uint64_t st[KB_SWP_TILE];
+  __shared__ uint32_t cnt2[KB_SW_CNT_WORDS];
+  __shared__ uint32_t wtot[KB_SW_WAVES];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nw = (nb + 1) / 2;
+  // tile g's loads: quads of consecutive containers (16-B buffer loads through descriptors
+  // that end at the tile's end: outside, they read 0 and the validity test drops them)
+  int32_t kn[PER];
+  uint64_t vn[NS][PER];
+  auto issue = [&](int64_t g) {
+    const int64_t t0 = g * tile, t1 = min(t0 + tile, n);
+    const int32_t len = (int32_t)(t1 > t0 ? t1 - t0 : 0);
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(key + t0), (short)0, 4 * len, 0x00020000);
+#pragma unroll
+    for (int q = 0; q < PER / 4; ++q) {
+      const int32_t o = 4 * (q * KB_SW_THREADS + tid);
+      const i32x4 kk = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, 4 * o, 0, 2));
+      kn[4 * q] = kk.x;
+      kn[4 * q + 1] = kk.y;
+      kn[4 * q + 2] = kk.z;
+      kn[4 * q + 3] = kk.w;
+    }
+    if constexpr (NA == 2) {
+      const uint64_t* in[2] = {a0, a1};
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(in[a] + t0), (short)0, 8 * len, 0x00020000);
+#pragma unroll
+        for (int q = 0; q < PER / 4; ++q) {
+          const int32_t o = 4 * (q * KB_SW_THREADS + tid);
+          const u64x2 lo = __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(rv, 8 * o, 0, 2));
+          const u64x2 hi = __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(rv, 8 * o + 16, 0, 2));
+          vn[a][4 * q] = lo.x;
+          vn[a][4 * q + 1] = lo.y;
+          vn[a][4 * q + 2] = hi.x;
+          vn[a][4 * q + 3] = hi.y;
+        }
+      }
+    }
+  };
+  int64_t g = blockIdx.x;
+  if (g < G) issue(g);
+  for (; g < G; g += gridDim.x) {
+    const int64_t t0 = g * tile, t1 = min(t0 + tile, n);
+    int32_t k[PER];
+    uint64_t v[NS][PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      k[u] = kn[u];
+#pragma unroll
+      for (int a = 0; a < NS; ++a) v[a][u] = NA == 2 ? vn[a][u] : 0ull;
+    }
+    if (g + gridDim.x < G) issue(g + gridDim.x);  // in flight during this tile's work
+    for (int w = tid; w < nw; w += KB_SW_THREADS) cnt2[w] = 0;
+    __syncthreads();  // counters zeroed (and the previous tile's stage read)
+    uint64_t rec[PER];
+    uint32_t br[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int64_t c = t0 + 4 * ((int64_t)(u / 4) * KB_SW_THREADS + tid) + (u & 3);
+      const bool valid = c < t1 && k[u] >= 0 && (int64_t)k[u] < n_keys;
+      const int b = valid ? k[u] >> KB_SHIFT : 0;
+      const uint32_t sh = 16u * (uint32_t)(b & 1);
+      const uint32_t rk = valid ? (atomicAdd(&cnt2[b >> 1], 1u << sh) >> sh) & 0xffffu : 0u;
+      br[u] = valid ? (uint32_t)b << 16 | rk : 0xffffffffu;
+      const uint32_t row = (uint32_t)k[u] & (KB_ROWS - 1);
+      if constexpr (NA == 2) {
+        rec[u] = kb_record(row, v[0][u], v[1][u]);
+        if (valid) {
+          const bool mem_ok = kb_mem_ok(v[1][u]);
+          if (!mem_ok || (v[0][u] >> KB_CPU_BITS) != 0) {  // rare: what the record cannot hold
+            const uint32_t e = atomicAdd(esc_n, 1u);
+            esc_row[e] = k[u];
+            esc_cpu[e] = v[0][u] & ~KB_CPU_LO;
+            esc_mem[e] = mem_ok ? 0ull : v[1][u];
+          }
+        }
+      } else {
+        rec[u] = row;
+      }
+    }
+    __syncthreads();
+    uint32_t c4[4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int w = 2 * tid + j;
+      const uint32_t x = w < nw ? cnt2[w] : 0u;
+      c4[2 * j] = x & 0xffffu;
+      c4[2 * j + 1] = x >> 16;
+    }
+    const uint32_t s4 = c4[0] + c4[1] + c4[2] + c4[3];
+    const uint32_t incl = wave_incl_scan32(s4);
+    if (lane == 63) wtot[wv] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, nvalid = 0;
+#pragma unroll
+    for (int w = 0; w < KB_SW_WAVES; ++w) {
+      const uint32_t t = wtot[w];
+      wbase += w < wv ? t : 0u;
+      nvalid += t;
+    }
+    {
+      uint32_t run = wbase + incl - s4;
+      uint32_t st4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        st4[j] = run;
+        run += c4[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int w = 2 * tid + j;
+        if (w < nw) cnt2[w] = st4[2 * j] | st4[2 * j + 1] << 16;
+      }
+      uint32_t* rowp = tab + g * (nb + 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (4 * tid + j < nb) rowp[4 * tid + j] = st4[j];
+      if (tid == 0) rowp[nb] = nvalid;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      if (br[u] == 0xffffffffu) continue;
+      st[kb_half(cnt2, (int)(br[u] >> 16)) + (br[u] & 0xffffu)] = rec[u];
+    }
+    __syncthreads();
+    // the stage leaves as one contiguous run: a fixed number of 16-B streaming stores per
+    // thread, through a descriptor that ends at nvalid records (past it they are dropped;
+    // an odd last record goes as a pair with the zero slot after it, which is in range of
+    // the tile's region but past nvalid: harmless)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(sr + g * KB_SWP_TILE), (short)0, 8 * (int)((nvalid + 1u) & ~1u), 0x00020000);
+#pragma unroll
+    for (int h = 0; h < KB_SWP_TILE / (2 * KB_SW_THREADS); ++h) {
+      const uint32_t j = 2u * (uint32_t)(h * KB_SW_THREADS + tid);
+      const u64x2 pr = *reinterpret_cast<const u64x2*>(&st[j]);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, pr), rs, (int)(8 * j), 0, 2);
+    }
+  }
+}
+
 // kb_gather: bucket b's records — segment [tab[g][b], tab[g][b + 1]) of every tile g —
 // summed into LDS rows (64-bit LDS atomics), its rows written once.  `parts` workgroups
 // share a bucket (tiles dealt round-robin): each sums its tiles; every part but the last to
@@ -691,7 +853,7 @@ constexpr int KB_GA_CH = 2048;     // tiles per table chunk in LDS
 
 template <int NA>
 __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
-    int64_t G, int64_t n_keys, int nb, int parts, const uint32_t* __restrict__ tab,
+    int64_t G, int64_t n_keys, int nb, int parts, uint32_t stride, const uint32_t* __restrict__ tab,
     const uint64_t* __restrict__ sr, uint64_t* __restrict__ part_acc, uint32_t* __restrict__ arrive,
     uint64_t* __restrict__ o0, uint64_t* __restrict__ o1) {
   constexpr int NACC = NA > 0 ? NA : 1;
@@ -737,7 +899,7 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
         const uint32_t gi = (uint32_t)(c0 + (ok ? i : 0));
         const uint32_t g = (uint32_t)part + (KCC_KB_GA_REV ? (uint32_t)my_tiles - 1u - gi : gi) * (uint32_t)parts;
         len[u] = ok ? seg_len[i] : 0u;
-        first[u] = g * (uint32_t)KB_SW_TILE + (ok ? seg_off[i] : 0u);
+        first[u] = g * stride + (ok ? seg_off[i] : 0u);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const uint32_t o = (uint32_t)lane + 64u * h;
@@ -798,6 +960,11 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
 
 }  // namespace
 
+#ifdef KCC_KB_SWP
+constexpr int64_t KB_SWX_TILE = KB_SWP_TILE;  // a tile's record slots (the pipelined sweep)
+#else
+constexpr int64_t KB_SWX_TILE = KB_SW_TILE;
+#endif
 static int keyed_cus() {  // (thread-safe once: a function-local static's initializer)
   static const int cus = [] {
     int dev = 0, c = 0;
@@ -827,14 +994,14 @@ int64_t keyed_tiles(int64_t n) {
 int64_t keyed_buckets(int64_t n_keys) { return (n_keys + KB_ROWS - 1) / KB_ROWS; }
 bool keyed_bucketed(int64_t n_keys, int64_t n) {  // (record indices, padded tiles, < 2^32)
   return n_keys > 0 && keyed_buckets(n_keys) <= KB_NB_MAX && n < ((int64_t)1 << 32) - KB_SW_TILE &&
-         keyed_sweep_tiles(n) * KB_SW_TILE < ((int64_t)1 << 32);
+         keyed_sweep_tiles(n) * KB_SWX_TILE < ((int64_t)1 << 32);
 }
 int64_t keyed_sweep_tile(int64_t n) {
   const int64_t cus = keyed_cus();
-  if (n <= KB_SW_TILE * cus) return KB_SW_TILE;
-  const int64_t rounds = (n + KB_SW_TILE * cus - 1) / (KB_SW_TILE * cus);
+  if (n <= KB_SWX_TILE * cus) return KB_SWX_TILE;
+  const int64_t rounds = (n + KB_SWX_TILE * cus - 1) / (KB_SWX_TILE * cus);
   const int64_t t = (n + rounds * cus - 1) / (rounds * cus);
-  return (t + 3) / 4 * 4;  // (quads: 16-B loads; <= KB_SW_TILE, a multiple of 4)
+  return (t + 3) / 4 * 4;  // (quads: 16-B loads; <= KB_SWX_TILE, a multiple of 4)
 }
 int64_t keyed_sweep_tiles(int64_t n) {
   const int64_t t = keyed_sweep_tile(n);
@@ -862,7 +1029,7 @@ int64_t keyed_counts_words(int64_t n_keys, int64_t n) {
   return a > b ? a : b;
 }
 int64_t keyed_sr_slots(int64_t n) {
-  const int64_t t = keyed_sweep_tiles(n) * KB_SW_TILE;
+  const int64_t t = keyed_sweep_tiles(n) * KB_SWX_TILE;
   return t > n ? t : n;
 }
 int64_t keyed_part_words(int64_t n_keys, int na) {
@@ -877,12 +1044,22 @@ static hipError_t run_sweep(int64_t n_keys, int64_t n, const int32_t* key, const
   const int64_t G = keyed_sweep_tiles(n), tile = keyed_sweep_tile(n);
   const int parts = keyed_sweep_parts(nb);
   if (G > 0x7fffffff || (int64_t)nb * parts > 0x7fffffff) return hipErrorInvalidValue;
+#ifdef KCC_KB_SWP
+  if (G > 0) {  // one persistent workgroup per CU at most
+    const int64_t wg = G < keyed_cus() ? G : keyed_cus();
+    hipLaunchKernelGGL(kb_sweep_p<NA>, dim3((unsigned)wg), dim3(KB_SW_THREADS), 0, s, n, n_keys, key,
+                       in[0], in[1], nb, kw.counts, kw.sr, kw.esc_n, kw.esc_row, kw.esc_cpu, kw.esc_mem,
+                       tile, G);
+  }
+#else
   if (G > 0)
     hipLaunchKernelGGL(kb_sweep<NA>, dim3((unsigned)G), dim3(KB_SW_THREADS), 0, s, n, n_keys, key,
                        in[0], in[1], nb, kw.counts, kw.sr, kw.esc_n, kw.esc_row, kw.esc_cpu, kw.esc_mem,
                        tile);
+#endif
   hipLaunchKernelGGL(kb_gather<NA>, dim3((unsigned)(nb * parts)), dim3(KB_GA_THREADS), 0, s, G, n_keys,
-                     nb, parts, kw.counts, kw.sr, kw.part_acc, kw.arrive, out[0], out[1]);
+                     nb, parts, (uint32_t)KB_SWX_TILE, kw.counts, kw.sr, kw.part_acc, kw.arrive,
+                     out[0], out[1]);
   if (NA >= 2 && n > 0)  // (few workgroups: each adds to one arrival counter; the list is short)
     hipLaunchKernelGGL(kb_escape, dim3(KB_ESC_WG), dim3(256), 0, s, kw.esc_n, kw.esc_row, kw.esc_cpu,
                        kw.esc_mem, out[0], out[1]);
