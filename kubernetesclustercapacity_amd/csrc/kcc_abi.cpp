@@ -298,9 +298,8 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.sperm, 4 * S));
   KCC_HIP(ctx, ensure(dv.counters, sizeof(unsigned long long) * kcc::CNT_N));
   if (!dv.clamp_arrive.p) {  // the fused finalize's arrivals: every launch leaves them zero
-    // (top counter + 8 group counters, one 64-B line each)
-    KCC_HIP(ctx, ensure(dv.clamp_arrive, 9 * 64));
-    KCC_HIP(ctx, hipMemsetAsync(dv.clamp_arrive.p, 0, 9 * 64, dv.stream));
+    KCC_HIP(ctx, ensure(dv.clamp_arrive, 64));
+    KCC_HIP(ctx, hipMemsetAsync(dv.clamp_arrive.p, 0, 64, dv.stream));
     KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
   }
   // (a new allocation is a larger one: compare sizes, hipMalloc may hand back the address)
@@ -637,12 +636,6 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   const bool fuse_fin = totals && n_nodes > 0;
   const kcc::FinArgs fin{as<int32_t>(dv.sperm), totals, spec_err, as<uint32_t>(dv.clamp_arrive),
                          as<const unsigned long long>(dv.faults)};
-  int last_fit = -1;  // the chunk whose fit launch is the step's last (it finalizes in NC mode)
-  for (int c = 0; c < k; ++c)
-    if (hi[c] > lo[c]) last_fit = c;
-#ifdef KCC_AB_NOFITFUSE
-  last_fit = -2;
-#endif
   for (int c = 0; c < k; ++c) {
     if (k > 1) KCC_HIP(ctx, hipStreamWaitEvent(s, dv.ev_red[c], 0));  // also joins the side stream
     const int64_t n = hi[c] - lo[c];
@@ -670,8 +663,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                  as<int64_t>(dv.slow_list) + lo[c], n_specs, spec_prep_of(dv),
                                  partial, as<unsigned long long>(dv.counters),
                                  as<uint32_t>(dv.fit_q), c, n_nodes, s,
-                                 as<const unsigned long long>(dv.faults), fast_cl,
-                                 nc && fuse_fin && c == last_fit ? &fin : nullptr));
+                                 as<const unsigned long long>(dv.faults), fast_cl));
     if (dv.prof_on) {
       KCC_HIP(ctx, hipEventRecord(pp.b, s));
       pp.kind = 1;
@@ -682,8 +674,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   // the clamp launch's last workgroup also finalizes (no fit_finalize launch)
   if (n_specs > 0 && nc) {  // the fit applied the clamp: no clamp_apply, nothing dirty
     dv.clamp_dirty = false;
-    // (the fit's last workgroup finalized, unless there were no nodes: no fit launch)
-    if (totals && (!fuse_fin || last_fit < 0)) return fit_finalize_dev(ctx, dv, n_specs, partial, totals, spec_err, s);
+    if (totals) return fit_finalize_dev(ctx, dv, n_specs, partial, totals, spec_err, s);
     return KCC_OK;
   }
   if (n_specs > 0) {

@@ -1816,7 +1816,7 @@ __device__ __forceinline__ void clamp_apply_bin(const ClampWork& cw, int64_t S,
   KCC_TL(1024 + blockIdx.x % 1024, 4);
 }
 
-// The fused finalize (clamp_apply_kernel; the fit when it applies the clamp itself): every
+// The fused finalize (clamp_apply_kernel): every
 // wave's atomics into partial are performed (vmcnt counts the stores and atomics too on
 // gfx9) before the workgroup arrives; the last workgroup to arrive reads partial at agent
 // scope and writes the totals in caller order.  Every thread of the workgroup calls, from
@@ -1829,49 +1829,39 @@ __device__ __forceinline__ void clamp_apply_bin(const ClampWork& cw, int64_t S,
 // sides}" form with the "workgroup whose add came last" signal (an acq_rel add lowers to a
 // buffer_wbl2 + buffer_inv pair per workgroup: an L2 write-back each).
 //
-// One counter takes about 12 ns per arrival when they bunch up ('fanin'): with `groups`
-// > 0 the arrivals are two-level — a workgroup arrives on its group `grp`'s counter
-// (`grp_n` arrivals), the last of each group on the top counter (`groups` arrivals), and
-// the last of those finalizes.  Counters: FinArgs::arrive (top at word 0, group g at word
-// 16 (g + 1)); each last arriver resets its counter.
+// The arrivals go to `ctr` (`expect` of them; the last arriver resets it), and the last
+// arriver finalizes specs [s0, s1) of the S.
 __device__ void fused_finalize(const FinArgs& fin, int64_t S, const int64_t* partial,
-                               uint32_t groups = 0, uint32_t grp = 0, uint32_t grp_n = 0) {
+                               uint32_t* ctr, uint32_t expect, int64_t s0, int64_t s1) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   __shared__ uint32_t last_s;
-  const uint32_t expect = groups ? groups : gridDim.x;
   if (threadIdx.x == 0) {
-    bool go = true;
-    if (groups) {  // the group's counter first
-      uint32_t* g = fin.arrive + 16u * (grp + 1u);
-      go = __hip_atomic_fetch_add(g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == grp_n - 1u;
-      if (go) __hip_atomic_store(g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    last_s = go && __hip_atomic_fetch_add(fin.arrive, 1u, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT) == expect - 1u;
+    last_s = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             expect - 1u;
+    if (last_s) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (!last_s) return;
-  if (threadIdx.x == 0) __hip_atomic_store(fin.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool faulted = device_faulted(fin.faults);
   // FIN_PER specs per thread per round, every load of the round issued before any store
   // (one memory round trip per round: S <= 4 x the workgroup is one round)
   constexpr int FIN_PER = 4;
   const int64_t nt = blockDim.x;
-  for (int64_t i0 = threadIdx.x; i0 < S; i0 += (int64_t)FIN_PER * nt) {
+  for (int64_t i0 = s0 + threadIdx.x; i0 < s1; i0 += (int64_t)FIN_PER * nt) {
     int64_t t[FIN_PER], e[FIN_PER];
     int32_t dst[FIN_PER];
 #pragma unroll
     for (int k = 0; k < FIN_PER; ++k) {
-      // past the end: reload spec S-1 (branch-free, so no wait splits the batch)
-      const int64_t i = min(i0 + (int64_t)k * nt, S - 1);
+      // past the end: reload spec s1-1 (branch-free, so no wait splits the batch)
+      const int64_t i = min(i0 + (int64_t)k * nt, s1 - 1);
       t[k] = __hip_atomic_load(partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       e[k] = __hip_atomic_load(partial + S + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       dst[k] = fin.perm[i];
     }
 #pragma unroll
     for (int k = 0; k < FIN_PER; ++k) {
-      if (i0 + (int64_t)k * nt >= S) break;
+      if (i0 + (int64_t)k * nt >= s1) break;
       const bool fk = faulted || (uint64_t)e[k] >= SPEC_FAULT_MARK;
       fin.totals[dst[k]] = e[k] != 0 || fk ? 0 : t[k];
       fin.spec_err[dst[k]] = fk ? SPEC_ERR_FAULT : e[k] != 0 ? SPEC_ERR_DIV0 : 0;
@@ -1890,7 +1880,7 @@ __global__ __launch_bounds__(CP_THREADS) void clamp_apply_kernel(ClampWork cw,
   const uint32_t G = gridDim.x / (uint32_t)(2 * Tm), h = blockIdx.x / (uint32_t)(2 * Tm);
   const int64_t u = blockIdx.x % (uint32_t)(2 * Tm);
   if (u < 2 * T) clamp_apply_bin(cw, S, partial, nN, u, G, h);  // (else: no bin)
-  if (fin.totals) fused_finalize(fin, S, partial);
+  if (fin.totals) fused_finalize(fin, S, partial, fin.arrive, gridDim.x, 0, S);
 }
 
 // clamp_crows_kernel (only when C does not fit clamp_apply's full form): one wave per row
@@ -2017,12 +2007,15 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     const int64_t* __restrict__ slow_list, int64_t S, const SpecRec* __restrict__ specs,
     int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t chunk,
     int32_t gx, int32_t gy, const int32_t* __restrict__ fast_cl,
-    const unsigned long long* __restrict__ faults, FinArgs fin) {
+    const unsigned long long* __restrict__ faults) {
   // XCD-aware order (speed only, never correctness): workgroups are dealt round-robin
   // over the 8 XCDs, so give every spec group of one node chunk the same b % 8
   const int32_t b = blockIdx.x, xcd = b & 7, r = b >> 3;
   const int32_t bx = r % gx, by = (r / gx) * 8 + xcd;
   if (by >= gy) return;  // padding of gy up to a multiple of 8 (whole workgroup)
+  // issue priority falls with the workgroup's progress through its share (below): the
+  // arbiter otherwise serves the oldest waves first, and a late starter sat on its claims
+  __builtin_amdgcn_s_setprio(3);
   KCC_TL(2048 + b % 4096, 0);
   const int32_t wv = __builtin_amdgcn_readfirstlane((int32_t)(threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
@@ -2109,6 +2102,11 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     KCC_TL(2048 + b % 4096, 1);
   }
   const uint32_t first = ((uint32_t)by / nsub) * q1;  // the static first claim's offset
+  uint32_t pr_done = 0;  // groups summed (workgroup-uniform), against an equal share
+  const uint32_t pr_share = (lim - base) / wseg > 0 ? (lim - base) / wseg : 1u;
+#ifdef KCC_TIMELINE
+  uint32_t tl_done = 0;  // groups this workgroup summed
+#endif
   uint64_t acc = 0;
   uint64_t errs = 0;
   uint32_t slow_iters = 0;
@@ -2304,7 +2302,19 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
         }
       }
       claim_publish((k + 1u) & 1u);
+      {  // priority 3, 2, 1, 0 through the quarters of the share
+        pr_done += (uint32_t)cnt;
+        const uint32_t lv = (4u * pr_done) / pr_share;
+        if (lv == 0) __builtin_amdgcn_s_setprio(3);
+        else if (lv == 1) __builtin_amdgcn_s_setprio(2);
+        else if (lv == 2) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
       KCC_TLV(2048 + b % 4096, 4, (uint64_t)k + 1);
+#ifdef KCC_TIMELINE
+      tl_done += (uint32_t)cnt;
+      if (k == 0) KCC_TL(2048 + b % 4096, 6);
+#endif
     }
     if (wv == 0 && lane == 0) {  // this workgroup made its last claim
       const uint32_t d = atomicAdd(qp + 1, 1u);
@@ -2315,7 +2325,10 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     }
   }
   KCC_TL(2048 + b % 4096, 2);
-  if (!idle) {  // (a wave wholly past S falls through to the fused finalize's barrier)
+#ifdef KCC_TIMELINE
+  KCC_TLV(2048 + b % 4096, 7, tl_done);
+#endif
+  if (idle) return;  // a wave wholly past S (it took the claims' barriers)
   if (wave_exact) {  // exact-path specs: every node row (SlowNode), this workgroup's share
     const uint32_t nn = (uint32_t)n_nodes;  // < 2^28 per device
     const uint32_t pn = (nn + (uint32_t)gy - 1u) / (uint32_t)gy;
@@ -2342,17 +2355,7 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[s]), acc);
     if (errs) atomic_add_u64(reinterpret_cast<uint64_t*>(&partial[S + s]), errs);
   }
-  }  // (!idle)
   KCC_TL(2048 + b % 4096, 3);
-  // the clamp in the fit at N = 1 (the step's last kernel): the last of the gx x gy working
-  // workgroups to arrive writes the totals (the grid's XCD padding returned at entry).
-  // Two-level arrivals by blockIdx % 8 (one XCD each under round-robin placement): group x
-  // holds the workgroups with by = 8 t + x < gy, gx x ceil((gy - x) / 8) of them
-  if (fin.totals) {
-    const uint32_t ngrp = gy < 8 ? (uint32_t)gy : 8u;
-    const uint32_t gn = (uint32_t)gx * (((uint32_t)gy - (uint32_t)xcd + 7u) / 8u);
-    fused_finalize(fin, S, partial, ngrp, (uint32_t)xcd, gn);
-  }
 }
 
 __global__ void fit_finalize_kernel(int64_t S, const int64_t* __restrict__ partial,
@@ -2695,7 +2698,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, uint32_t* queue, int chunk,
                       int64_t grid_nodes, hipStream_t s, const unsigned long long* faults,
-                      const int32_t* fast_cl, const FinArgs* fin) {
+                      const int32_t* fast_cl) {
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
   const int64_t gx = (n_specs + FIT_SPW - 1) / FIT_SPW;
   const int64_t gy = fit_grid_y(n_nodes, n_specs, grid_nodes);
@@ -2705,7 +2708,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
   auto kern = fast_cl ? fit_kernel<true> : fit_kernel<false>;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, queue, fast_a,
                      fast_b, slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)chunk,
-                     (int32_t)gx, (int32_t)gy, fast_cl, faults, fin ? *fin : FinArgs{});
+                     (int32_t)gx, (int32_t)gy, fast_cl, faults);
   return hipGetLastError();
 }
 

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 5: the fit's fused finalize per spec column (base) vs a fit_finalize launch (nofuse).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-r05h}
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_shards_configs.py tests/test_gpu_parity.py tests/test_shard_gloo.py -m gpu -x -q --timeout 300 --timeout-method thread \
+  > gpurun_out/pytest_$TAG.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
+for SH in 8 4 1; do
+  timeout -k 10 300 python3 -u scripts/ab_variants.py run --step --config C4 --shard $SH --rounds 7 --reps 20 base nofuse \
+    > gpurun_out/ab_${TAG}_step_s$SH.txt 2>&1 || exit $?
+  grep '^{' gpurun_out/ab_${TAG}_step_s$SH.txt
+done
+bash scripts/gpu_shard_trace.sh $TAG C4 8 || exit $?

@@ -23,6 +23,7 @@ ap.add_argument("--shard", type=int, default=1)
 ap.add_argument("--pipeline", action="store_true",
                 help="time kcc_capacity_partial_async (the bench's step, incl. the clamp in the "
                      "fit by size) instead of reduce + fit_prepare + fit_run")
+ap.add_argument("--dump", default=None, help="save the raw stamp buffer (.npy) here")
 a = ap.parse_args()
 L = _lib.load(os.path.join(ROOT, "variants", f"libkcc_{a.name}.so"))
 L.kcc_debug_timeline.argtypes = [C.c_void_p]
@@ -65,6 +66,8 @@ assert L.kcc_debug_timeline(buf.ctypes.data) == 0
 step()
 assert L.kcc_debug_timeline(buf.ctypes.data) == 0
 t = buf.astype(np.float64)
+if a.dump:
+    np.save(a.dump, buf)
 npr = t[0:1024]
 t0 = npr[:, 2][npr[:, 2] > 0].min()
 us = lambda x: (x - t0) / 100.0  # noqa: E731
