@@ -446,23 +446,20 @@ hipError_t launch_parse(int mode, int64_t n, const uint8_t* bytes, int64_t n_byt
 // Bucketed path: rows in buckets of KB_ROWS, containers in tiles of about KB_TILE.
 constexpr int KB_SHIFT = 12;  // 4096 rows per bucket: ~1 KB runs per tile and array
 constexpr int KB_ROWS = 1 << KB_SHIFT;
-#ifndef KCC_KB_TILE
 // containers per scatter workgroup (about; keyed_tile cuts whole rounds): at C4 65536
 // (3 rounds, 768 tiles) took the keyed call 0.392 -> 0.340 and 0.395 -> 0.372 ms on two
 // boxes against 32768 (5 rounds); 131072 equal, 262144 slower
-#define KCC_KB_TILE 65536
-#endif
-constexpr int KB_TILE = KCC_KB_TILE;  // containers per scatter workgroup
+constexpr int KB_TILE = 65536;
 constexpr int64_t KB_NB_MAX = 4096;  // buckets (LDS cursors): n_keys <= 16M rows
 struct KeyedWork {
   uint32_t* counts;   // [keyed_tiles(n) * keyed_buckets(n_keys)] (one-sweep path: the tiles'
                       // bucket starts, [keyed_sweep_tiles(n)][nb + 1])
   uint32_t* tot;      // [keyed_buckets(n_keys)]
-  uint64_t* sr;       // [n] scattered 8-B records: row within the bucket, low 20 cpu
-                      // bits, memory / 64 (kcc_keyed.hip kb_record)
+  uint64_t* sr;       // [keyed_sr_slots(n)] the records: the sweep's packed 6-B records
+                      // (kcc_keyed.hip kb_sweep), the limits path's 8-B ones (kb_record)
   uint64_t* sv;       // [n][2] the limit values, element-major (NA = 4 only)
-  uint32_t* esc_n;    // escape list: what the records cannot hold (cpu >= 2^20: its high
-  int32_t* esc_row;   // [n]   bits; memory not a multiple of 64 in [0, 2^38): all of it)
+  uint32_t* esc_n;    // escape list: what the records cannot hold (cpu >= 2^16 (2^20 with
+  int32_t* esc_row;   // [n]   limits): its high bits; memory outside the record's forms: all)
   uint64_t* esc_cpu;  // [n]
   uint64_t* esc_mem;  // [n]
   // one-sweep path (kb_sweep + kb_gather): a bucket's records are gathered by
@@ -471,20 +468,16 @@ struct KeyedWork {
   uint64_t* part_acc; // [nb][parts][NACC][KB_ROWS]
   uint32_t* arrive;   // [nb]
 };
-// One-sweep keyed reduce (NA = 0 counts, 2 requests; KCC_KB_SWEEP): each tile of
-// KB_SW_TILE containers is counting-sorted by bucket in LDS and written contiguously into
-// its own region of sr (whole lines), with the bucket starts in its table row — no global
+// One-sweep keyed reduce (NA = 0 counts, 2 requests): each tile of KB_SW_TILE containers
+// is counting-sorted by bucket in LDS and written contiguously into its own region of sr
+// (whole lines, 6-B records), with the bucket starts in its table row — no global
 // histogram pass, no scan, keys read once.  kb_gather then sums bucket b's segments of
-// every tile into LDS rows.
-#ifndef KCC_KB_SWEEP
-#define KCC_KB_SWEEP 1
-#endif
+// every tile into LDS rows.  (With limits, NA = 4: the bucketed kb_hist / kb_scan /
+// kb_scatter / kb_accum path.)
 constexpr int KB_SW_THREADS = 1024;
-#ifndef KCC_KB_SW_PER
-#define KCC_KB_SW_PER 16  // containers per thread: 16 (128 KiB stage, one workgroup per CU) or 8
-#endif
-constexpr int KB_SW_PER = KCC_KB_SW_PER;
-constexpr int64_t KB_SW_TILE = (int64_t)KB_SW_THREADS * KB_SW_PER;  // 16384 (8192)
+constexpr int KB_SW_PER = 8;  // containers per thread (the next tile's loads in registers)
+constexpr int64_t KB_SW_TILE = (int64_t)KB_SW_THREADS * KB_SW_PER;  // 8192
+constexpr int64_t KB6_BYTES = 6;  // a staged record
 // containers per sweep tile: KB_SW_TILE, or (beyond one round of one tile per CU) cut so
 // the tiles make whole rounds (C4: 2418 tiles = 9.4 rounds -> 2560 of 15472 = 10); a
 // tile's records keep the KB_SW_TILE stride in the staging buffer

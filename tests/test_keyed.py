@@ -90,8 +90,8 @@ def test_gpu_keyed_edges(eng):
         2, np.array([1, 1, 0], np.int32), np.array([1 << 63, 1 << 63, 5], np.uint64),
         np.array([-(1 << 63), -(1 << 63), 7], np.int64))
     assert r.cpu_requests.tolist() == [5, 0] and r.memory_requests.tolist() == [7, 0]
-    # staged records: row 4095 of a bucket with the low 20 cpu bits all ones (the all-ones
-    # 32-bit word), and cpu requests of 2^20 and more (their high parts on the escape list)
+    # staged records: row 4095 of a bucket with the low cpu bits all ones, and cpu requests
+    # past the record's field (their high parts on the escape list)
     key = np.array([4095, 4095, 4095, 8191, 1], np.int32)
     cpu = np.array([(1 << 20) - 1, (1 << 20) + 3, (1 << 64) - 1, (1 << 40) + 5, 1 << 20],
                    np.uint64)
@@ -100,13 +100,35 @@ def test_gpu_keyed_edges(eng):
     o = oracle_keyed(8192, key, cpu, mem)
     assert np.array_equal(r.cpu_requests, o[0]) and np.array_equal(r.memory_requests, o[1])
     assert int(r.cpu_requests[4095]) == ((1 << 21) + 1) % (1 << 64)
-    # memory requests the 8-B record holds (multiples of 64 below 2^38) and the ones it does
-    # not (odd, negative, 2^38 and above): the latter on the escape list
+    # memory requests the record holds and the ones it does not (odd, negative, large):
+    # the latter on the escape list
     mem = np.array([64, 100, -64, 1 << 38, (1 << 38) - 64], np.int64)
     cpu = np.array([1, 2, 3, 4, 5], np.uint64)
     r = eng.get_pod_cpu_memory_requests_limits_keyed(8192, key, cpu, mem)
     o = oracle_keyed(8192, key, cpu, mem)
     assert np.array_equal(r.cpu_requests, o[0]) and np.array_equal(r.memory_requests, o[1])
+
+
+@pytest.mark.gpu
+def test_gpu_keyed_record_fields(eng):
+    """The sweep's 6-byte record (kcc_keyed.hip kb_sweep): 16 cpu bits, memory as a 19-bit
+    count of MiB or of 10^6 B; every value at and around each field's edge, in both units,
+    values of both forms, and the escapes past them — each container alone on its row, and
+    all of them on one row."""
+    MI, M = 1 << 20, 1_000_000
+    cpu_edges = [0, 1, (1 << 16) - 1, 1 << 16, (1 << 16) + 1, (1 << 20) - 1, 1 << 20,
+                 (1 << 64) - 1, (1 << 63) + 7]
+    mem_edges = [0, MI, ((1 << 19) - 1) * MI, (1 << 19) * MI, ((1 << 19) + 1) * MI,
+                 M, ((1 << 19) - 1) * M, (1 << 19) * M, ((1 << 19) - 1) * M + 1,
+                 15625 * MI, 64, 100, -MI, -M, 1 << 62, -(1 << 63), (1 << 63) - 1,
+                 250 * M, 128 * MI, 3 * MI + M]
+    cpu = np.array([c for c in cpu_edges for _ in mem_edges], np.uint64)
+    mem = np.array([m for _ in cpu_edges for m in mem_edges], np.int64)
+    nk = cpu.size
+    for key in (np.arange(nk, dtype=np.int32), np.full(nk, 4097, np.int32)):
+        r = eng.get_pod_cpu_memory_requests_limits_keyed(8192, key, cpu, mem)
+        o = oracle_keyed(8192, key, cpu, mem)
+        assert np.array_equal(r.cpu_requests, o[0]) and np.array_equal(r.memory_requests, o[1])
 
 
 @pytest.mark.gpu
@@ -163,9 +185,10 @@ def test_gpu_keyed_c4_equals_csr(eng):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nc", [16383, 16384, 16385, 3 * 16384 + 3, 200_001])
+@pytest.mark.parametrize("nc", [8191, 8192, 8193, 16385, 3 * 8192 + 3, 200_001, 2_200_001])
 def test_gpu_keyed_sweep_tiles(eng, nc):
-    """The one-sweep path's tiles (16384 containers each): sizes around and across tile
+    """The one-sweep path's tiles (8192 containers each; past one per CU, cut into whole
+    rounds, and several per persistent workgroup): sizes around and across tile
     boundaries, a skewed key mix (half of the containers on one row: segments far longer
     than a wave's 64-record step), skipped keys, the largest key space (4096 buckets: the
     packed 16-bit LDS counters of all of them), and two calls in a row (the escape list and
