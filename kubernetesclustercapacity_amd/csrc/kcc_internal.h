@@ -455,11 +455,11 @@ struct KeyedWork {
   uint32_t* counts;   // [keyed_tiles(n) * keyed_buckets(n_keys)] (one-sweep path: the tiles'
                       // bucket starts, [keyed_sweep_tiles(n)][nb + 1])
   uint32_t* tot;      // [keyed_buckets(n_keys)]
-  uint64_t* sr;       // [keyed_sr_slots(n)] the records: the sweep's packed 6-B records
-                      // (kcc_keyed.hip kb_sweep), the limits path's 8-B ones (kb_record)
+  uint64_t* sr;       // [n] scattered 8-B records: row within the bucket, low 20 cpu
+                      // bits, memory / 64 (kcc_keyed.hip kb_record)
   uint64_t* sv;       // [n][2] the limit values, element-major (NA = 4 only)
-  uint32_t* esc_n;    // escape list: what the records cannot hold (cpu >= 2^16 (2^20 with
-  int32_t* esc_row;   // [n]   limits): its high bits; memory outside the record's forms: all)
+  uint32_t* esc_n;    // escape list: what the records cannot hold (cpu >= 2^20: its high
+  int32_t* esc_row;   // [n]   bits; memory not a multiple of 64 in [0, 2^38): all of it)
   uint64_t* esc_cpu;  // [n]
   uint64_t* esc_mem;  // [n]
   // one-sweep path (kb_sweep + kb_gather): a bucket's records are gathered by
@@ -470,14 +470,12 @@ struct KeyedWork {
 };
 // One-sweep keyed reduce (NA = 0 counts, 2 requests): each tile of KB_SW_TILE containers
 // is counting-sorted by bucket in LDS and written contiguously into its own region of sr
-// (whole lines, 6-B records), with the bucket starts in its table row — no global
-// histogram pass, no scan, keys read once.  kb_gather then sums bucket b's segments of
-// every tile into LDS rows.  (With limits, NA = 4: the bucketed kb_hist / kb_scan /
-// kb_scatter / kb_accum path.)
+// (whole lines), with the bucket starts in its table row — no global histogram pass, no
+// scan, keys read once.  kb_gather then sums bucket b's segments of every tile into LDS
+// rows.  (With limits, NA = 4: the bucketed kb_hist / kb_scan / kb_scatter / kb_accum path.)
 constexpr int KB_SW_THREADS = 1024;
 constexpr int KB_SW_PER = 8;  // containers per thread (the next tile's loads in registers)
 constexpr int64_t KB_SW_TILE = (int64_t)KB_SW_THREADS * KB_SW_PER;  // 8192
-constexpr int64_t KB6_BYTES = 6;  // a staged record
 // containers per sweep tile: KB_SW_TILE, or (beyond one round of one tile per CU) cut so
 // the tiles make whole rounds (C4: 2418 tiles = 9.4 rounds -> 2560 of 15472 = 10); a
 // tile's records keep the KB_SW_TILE stride in the staging buffer

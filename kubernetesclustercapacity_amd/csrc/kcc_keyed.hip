@@ -500,62 +500,27 @@ __global__ __launch_bounds__(256) void kb_escape(uint32_t* __restrict__ esc_n,
 }
 
 // ---- one-sweep path (NA = 0 counts / 2 requests) --------------------------------------
-// kb_sweep: tile g = containers [g * tile, ...) (tile <= KB_SW_TILE: keyed_sweep_tile).
-// Each valid container's rank within its bucket comes from an LDS counter (two 16-bit
-// counters per word), one exclusive scan of the counts gives the bucket starts, the records
-// are counting-sorted into an LDS stage and leave as ONE contiguous run of nvalid 6-byte
-// records (16-B stores: whole lines) into the tile's own region of sr, the starts into the
-// tile's table row (tab[g][b], tab[g][nb] = nvalid).  No global histogram, no scan
-// launch, and the keys are read once.
-//
-// The 6-byte record (a 48-bit little-endian word at byte 6 i of the tile's region):
-//   bits  0-11  row within the bucket
-//   bits 12-27  the low 16 bits of the cpu request
-//   bits 28-47  the memory request: bit 28 set -> (bits 29-47) << 20 (a multiple of 2^20,
-//               "Mi"/"Gi" quantities), clear -> (bits 29-47) x 10^6 ("M"/"G"); values
-//               below 2^19 (512 GiB / 524 GB); 0 for any other request
-// A cpu request of 2^16 millicores or more, or a memory request outside those forms, also
-// appends (row, cpu high bits, memory) to the escape list, added by kb_escape after the
-// gather (wrapping sums: the parts add to the requests exactly).  Round 4's 8-byte record
-// (20 cpu bits, memory / 64) moved 2 bytes more per container out of the sweep and into
-// the gather.
-//
-// Persistent and software-pipelined: one workgroup per CU walks the tiles g = blockIdx.x,
-// + gridDim.x, ...; the next tile's loads (range-checked buffer loads, so their count is
-// static) go out before the current tile's ranks, scan, scatter and stores, so the CU's
-// HBM traffic does not stop for the LDS work (round 4: one tile per workgroup launch,
-// load, then work, then store, every phase alone on the CU — 0.3327 -> 0.3257 ms at C4).
+// kb_sweep: tile g = containers [g * tile, ...) (tile <= KB_SW_TILE: keyed_sweep_tile), 8
+// per thread (16-B loads of quads).  Each valid container's rank within its bucket comes
+// from an LDS counter (two 16-bit counters per word), one exclusive scan of the counts
+// gives the bucket starts, the records are counting-sorted into an LDS stage and leave as
+// ONE contiguous run of nvalid records (16-B stores: whole lines) into the tile's own
+// region sr[g * KB_SW_TILE ...], the starts into the tile's table row (tab[g][b],
+// tab[g][nb] = nvalid).  No global histogram, no scan launch, and the keys are read once.
 constexpr int KB_SW_WAVES = KB_SW_THREADS / 64;
 constexpr int KB_SW_CNT_WORDS = (int)(KB_NB_MAX / 2);  // two 16-bit bucket counts per word
-constexpr int KB6_CPU_BITS = 16;
-constexpr uint64_t KB6_CPU_LO = (1ull << KB6_CPU_BITS) - 1;
-constexpr int KB6_MEM_AT = 12 + KB6_CPU_BITS;  // 28
-constexpr uint64_t KB6_MEM_VMAX = 1ull << 19;
-constexpr uint32_t KB6_NO_MEM = 0xffffffffu;
-static_assert(KB_SHIFT == 12, "the record's row field is 12 bits");
-static_assert(KB_SW_TILE * KB6_BYTES % 16 == 0, "a tile's region is whole 16-B chunks");
 
-// the record's 20-bit memory field of a request, or KB6_NO_MEM
-__device__ __forceinline__ uint32_t kb6_mem(uint64_t mem) {
-  if ((mem & ((1ull << 20) - 1)) == 0 && (mem >> 20) < KB6_MEM_VMAX)
-    return (uint32_t)(mem >> 20) << 1 | 1u;
-  if (mem < KB6_MEM_VMAX * 1000000ull) {  // < 2^39: exact in a double; the quotient of a
-    // multiple of 10^6 comes out exact after rounding (relative error ~1e-16), and the
-    // product check rejects everything else
-    const uint32_t q = (uint32_t)__builtin_rint((double)mem * 1e-6);
-    if ((uint64_t)q * 1000000ull == mem) return q << 1;
-  }
-  return KB6_NO_MEM;
-}
-// a record's memory request
-__device__ __forceinline__ uint64_t kb6_mem_of(uint64_t rec) {
-  const uint32_t f = (uint32_t)(rec >> KB6_MEM_AT);
-  return (f & 1u) ? (uint64_t)(f >> 1) << 20 : (uint64_t)(f >> 1) * 1000000ull;
-}
 __device__ __forceinline__ uint32_t kb_half(const uint32_t* w, int b) {
   return (w[b >> 1] >> (16 * (b & 1))) & 0xffffu;
 }
 
+// Persistent and software-pipelined (round 5): one workgroup per CU walks the tiles
+// g = blockIdx.x, + gridDim.x, ...; the next tile's loads (range-checked buffer loads, so
+// their count is static) go out before the current tile's ranks, scan, scatter and
+// stores, so the CU's HBM traffic does not stop for the LDS work.  Round 4's sweep took one
+// 16384-container tile per workgroup launch — load, then work, then store, every phase
+// alone on the CU: C4 keyed 0.3327 -> 0.3257 ms (sweep 255 -> 223 us, the gather 83 ->
+// 112 us over twice the segments).
 template <int NA>
 __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
     int64_t n, int64_t n_keys, const int32_t* __restrict__ key, const uint64_t* __restrict__ a0,
@@ -565,10 +530,8 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
   static_assert(NA == 0 || NA == 2, "one-sweep path: counts or requests");
   constexpr int NS = NA > 0 ? NA : 1;
   constexpr int PER = KB_SW_PER;
-  // the tile's records in bucket order (8 B each), then packed to 6 B (pk) for the stores
-  __shared__ __attribute__((aligned(16))) uint64_t st[KB_SW_TILE];
-  __shared__ __attribute__((aligned(16))) uint32_t pk[KB_SW_TILE * KB6_BYTES / 4];
-  __shared__ uint32_t cnt2[KB_SW_CNT_WORDS];  // bucket counts, then starts, in place
+  __shared__ uint64_t st[KB_SW_TILE];  // the tile's records, bucket order
+  __shared__ uint32_t cnt2[KB_SW_CNT_WORDS];
   __shared__ uint32_t wtot[KB_SW_WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nw = (nb + 1) / 2;
@@ -625,7 +588,7 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
     for (int w = tid; w < nw; w += KB_SW_THREADS) cnt2[w] = 0;
     __syncthreads();  // counters zeroed (and the previous tile's stage read)
     uint64_t rec[PER];
-    uint32_t br[PER];  // bucket << 16 | rank in the bucket (0xffffffff: skipped)
+    uint32_t br[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int64_t c = t0 + 4 * ((int64_t)(u / 4) * KB_SW_THREADS + tid) + (u & 3);
@@ -636,23 +599,21 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
       br[u] = valid ? (uint32_t)b << 16 | rk : 0xffffffffu;
       const uint32_t row = (uint32_t)k[u] & (KB_ROWS - 1);
       if constexpr (NA == 2) {
-        const uint32_t mf = kb6_mem(v[1][u]);
-        rec[u] = (uint64_t)row | (v[0][u] & KB6_CPU_LO) << 12 |
-                 (uint64_t)(mf == KB6_NO_MEM ? 0u : mf) << KB6_MEM_AT;
-        if (valid && (mf == KB6_NO_MEM || (v[0][u] >> KB6_CPU_BITS) != 0)) {
-          // rare: what the record cannot hold
-          const uint32_t e = atomicAdd(esc_n, 1u);
-          esc_row[e] = k[u];
-          esc_cpu[e] = v[0][u] & ~KB6_CPU_LO;
-          esc_mem[e] = mf == KB6_NO_MEM ? v[1][u] : 0ull;
+        rec[u] = kb_record(row, v[0][u], v[1][u]);
+        if (valid) {
+          const bool mem_ok = kb_mem_ok(v[1][u]);
+          if (!mem_ok || (v[0][u] >> KB_CPU_BITS) != 0) {  // rare: what the record cannot hold
+            const uint32_t e = atomicAdd(esc_n, 1u);
+            esc_row[e] = k[u];
+            esc_cpu[e] = v[0][u] & ~KB_CPU_LO;
+            esc_mem[e] = mem_ok ? 0ull : v[1][u];
+          }
         }
       } else {
         rec[u] = row;
       }
     }
     __syncthreads();
-    // exclusive scan of the bucket counts: thread t owns count words 2t, 2t + 1 (buckets
-    // 4t .. 4t + 3); a wave's DPP scan, then the 16 wave totals
     uint32_t c4[4];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -664,7 +625,7 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
     const uint32_t s4 = c4[0] + c4[1] + c4[2] + c4[3];
     const uint32_t incl = wave_incl_scan32(s4);
     if (lane == 63) wtot[wv] = incl;
-    __syncthreads();  // (also: every thread has read its count words)
+    __syncthreads();
     uint32_t wbase = 0, nvalid = 0;
 #pragma unroll
     for (int w = 0; w < KB_SW_WAVES; ++w) {
@@ -683,7 +644,7 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int w = 2 * tid + j;
-        if (w < nw) cnt2[w] = st4[2 * j] | st4[2 * j + 1] << 16;  // starts <= 2^13
+        if (w < nw) cnt2[w] = st4[2 * j] | st4[2 * j + 1] << 16;
       }
       uint32_t* rowp = tab + g * (nb + 1);
 #pragma unroll
@@ -698,84 +659,46 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
       st[kb_half(cnt2, (int)(br[u] >> 16)) + (br[u] & 0xffffu)] = rec[u];
     }
     __syncthreads();
-    // pack: thread t turns records 8t .. 8t + 7 (64 B) into 48 B (the stage past nvalid
-    // holds stale records: packed and stored with the last chunk, never read as records)
-#pragma unroll
-    for (int h = 0; h < KB_SW_TILE / (8 * KB_SW_THREADS); ++h) {
-      const int j = h * KB_SW_THREADS + tid;
-      uint64_t r8[8];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const u64x2 pr = *reinterpret_cast<const u64x2*>(&st[8 * j + 2 * q]);
-        r8[2 * q] = pr.x;
-        r8[2 * q + 1] = pr.y;
-      }
-      uint32_t w12[12];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {  // records 2q, 2q + 1 -> words 3q .. 3q + 2
-        const uint64_t a = r8[2 * q], b = r8[2 * q + 1];
-        w12[3 * q] = (uint32_t)a;
-        w12[3 * q + 1] = (uint32_t)(a >> 32) | (uint32_t)b << 16;
-        w12[3 * q + 2] = (uint32_t)(b >> 16);
-      }
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        *reinterpret_cast<i32x4*>(&pk[12 * j + 4 * q]) =
-            i32x4{(int)w12[4 * q], (int)w12[4 * q + 1], (int)w12[4 * q + 2], (int)w12[4 * q + 3]};
-    }
-    __syncthreads();
     // the stage leaves as one contiguous run: a fixed number of 16-B streaming stores per
-    // thread, through a descriptor that ends at the last 16-B chunk holding a record (past
-    // it they are dropped; that chunk's bytes past the run are in the tile's region, never
-    // read as records)
+    // thread, through a descriptor that ends at nvalid records (past it they are dropped;
+    // an odd last record goes as a pair with the zero slot after it, which is in range of
+    // the tile's region but past nvalid: harmless)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(reinterpret_cast<uint8_t*>(sr) + g * (KB_SW_TILE * KB6_BYTES)), (short)0,
-        (int)((KB6_BYTES * nvalid + 15u) & ~15u), 0x00020000);
+        (void*)(sr + g * KB_SW_TILE), (short)0, 8 * (int)((nvalid + 1u) & ~1u), 0x00020000);
 #pragma unroll
-    for (int h = 0; h < KB_SW_TILE * KB6_BYTES / (16 * KB_SW_THREADS); ++h) {
-      const uint32_t j = (uint32_t)(h * KB_SW_THREADS + tid);  // 16-B chunk
-      const i32x4 w = *reinterpret_cast<const i32x4*>(&pk[4 * j]);
-      __builtin_amdgcn_raw_buffer_store_b128(w, rs, (int)(16 * j), 0, 2);
+    for (int h = 0; h < KB_SW_TILE / (2 * KB_SW_THREADS); ++h) {
+      const uint32_t j = 2u * (uint32_t)(h * KB_SW_THREADS + tid);
+      const u64x2 pr = *reinterpret_cast<const u64x2*>(&st[j]);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, pr), rs, (int)(8 * j), 0, 2);
     }
   }
 }
 
 // kb_gather: bucket b's records — segment [tab[g][b], tab[g][b + 1]) of every tile g —
 // summed into LDS rows (64-bit LDS atomics), its rows written once.  `parts` workgroups
-// share a bucket (tiles dealt round-robin; keyed_sweep_parts: one, or up to 4 for key
-// spaces of few buckets): each sums its tiles; every part but the last to arrive stores its
-// rows into part_acc, the last one adds them and writes the outputs.
+// share a bucket (tiles dealt round-robin): each sums its tiles; every part but the last to
+// arrive stores its rows into part_acc, the last one adds them and writes the outputs.
 // A wave works on KB_GA_U segments at once (their loads issued together: a segment is a few
-// hundred bytes, so one per wave would be latency-bound); a record is read as the two
-// aligned 32-bit words holding its 6 bytes.
+// hundred bytes, so one per wave would be latency-bound).
 constexpr int KB_GA_THREADS = 1024;
 constexpr int KB_GA_WAVES = KB_GA_THREADS / 64;
-#ifndef KCC_KB_GA_U
-#define KCC_KB_GA_U 16
-#endif
-constexpr int KB_GA_U = KCC_KB_GA_U;  // segments per wave in flight (C4 A/B: 8 -> 0.3404 ms, 16 -> 0.3394)
-constexpr int KB_GA_CH = 2048; // tiles per table chunk in LDS
+// segments per wave in flight, 128 records of each (C4 A/B, one part: 8 -> 0.3404 ms, 16 ->
+// 0.3394 ms; round 5: 24 equal, 32 spills)
+constexpr int KB_GA_U = 16;
+constexpr int KB_GA_CH = 2048;  // tiles per table chunk in LDS
 // Tiles are read newest-first (the last-written records first, while the memory-side cache
 // may hold them): measured equal (0.3427 / 0.3432 ms), kept.
 
-// a record from the two dwords holding its 6 bytes (byte offset o of the first, o even):
-// shifted down when it starts mid-dword
-__device__ __forceinline__ uint64_t kb6_rec(uint32_t lo, uint32_t hi, uint32_t o) {
-  return (((uint64_t)hi << 32 | lo) >> (8u * (o & 3u))) & ((1ull << 48) - 1);
-}
-
 template <int NA>
 __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
-    int64_t G, int64_t n_keys, int nb, int parts, const uint32_t* __restrict__ tab,
+    int64_t G, int64_t n_keys, int nb, int parts, uint32_t stride, const uint32_t* __restrict__ tab,
     const uint64_t* __restrict__ sr, uint64_t* __restrict__ part_acc, uint32_t* __restrict__ arrive,
     uint64_t* __restrict__ o0, uint64_t* __restrict__ o1) {
   constexpr int NACC = NA > 0 ? NA : 1;
-  constexpr uint32_t TILE_B = (uint32_t)(KB6_BYTES * KB_SW_TILE);  // a tile's region in bytes
   __shared__ unsigned long long acc[NACC][KB_ROWS];
   __shared__ uint32_t seg_off[KB_GA_CH];  // start within the tile
   __shared__ uint32_t seg_len[KB_GA_CH];
   __shared__ uint32_t last_s;
-  // (the wave index provably uniform: the descriptors below stay scalar, no waterfall loops)
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x / parts, part = blockIdx.x % parts;
   for (int r = tid; r < KB_ROWS; r += KB_GA_THREADS)
@@ -788,61 +711,48 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
     if constexpr (NA == 0) {
       atomicAdd(&acc[0][r], 1ull);
     } else {
-      atomicAdd(&acc[0][r], (unsigned long long)((rec >> 12) & KB6_CPU_LO));
-      atomicAdd(&acc[1][r], (unsigned long long)kb6_mem_of(rec));
+      atomicAdd(&acc[0][r], (unsigned long long)(((uint32_t)rec) >> KB_SHIFT));
+      atomicAdd(&acc[1][r], (unsigned long long)((rec >> 32) << KB_MEM_SHIFT));
     }
-  };
-  // tile index of chunk entry i (newest first)
-  auto tile_of = [&](int64_t ci) -> uint32_t {
-    return (uint32_t)part + (uint32_t)(my_tiles - 1 - ci) * (uint32_t)parts;
   };
   for (int64_t c0 = 0; c0 < my_tiles; c0 += KB_GA_CH) {
     const int ch = (int)min((int64_t)KB_GA_CH, my_tiles - c0);
     __syncthreads();  // the previous chunk's table entries are consumed
     for (int i = tid; i < ch; i += KB_GA_THREADS) {
-      const uint32_t* row = tab + (int64_t)tile_of(c0 + i) * (nb + 1) + b;
+      const int64_t g = (int64_t)part + (my_tiles - 1 - (c0 + i)) * parts;
+      const uint32_t* row = tab + g * (nb + 1) + b;
       const uint32_t s0 = row[0], s1 = row[1];
       seg_off[i] = s0;
       seg_len[i] = s1 - s0;
     }
     __syncthreads();
     for (int i0 = wv * KB_GA_U; i0 < ch; i0 += KB_GA_WAVES * KB_GA_U) {
-      // KB_GA_U segments: the first 64 records of each loaded at once,
-      // through one descriptor based at the lowest of their tiles (newest first: the last
-      // one's), so the offsets are 32-bit (< KB_GA_U x parts regions)
-      const int ilast = min(i0 + KB_GA_U, ch) - 1;
-      const uint32_t tmin = tile_of(c0 + ilast);
-      const uint64_t span = (uint64_t)(G - tmin) * TILE_B + 8;  // to sr's end: past it, 0
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(reinterpret_cast<const uint8_t*>(sr) + (uint64_t)tmin * TILE_B), (short)0,
-          (int)(span < 0xfffffff0ull ? span : 0xfffffff0ull), 0x00020000);
-      // the two dwords of each segment's record `lane`, loaded unconditionally (a lane past
-      // its segment reads a neighbour's bytes, or 0 past sr's end, and drops them), one
-      // batch before any use: the unpacking waits for nothing but the batch
-      uint32_t wl[KB_GA_U], wh[KB_GA_U];
-      uint32_t len[KB_GA_U], first[KB_GA_U];  // first: the segment's byte offset in rs
+      // KB_GA_U segments: the first 128 records of each loaded at once (two per lane)
+      uint64_t r[KB_GA_U][2];
+      uint32_t len[KB_GA_U], first[KB_GA_U];  // (record indices < 2^32: keyed_bucketed)
 #pragma unroll
       for (int u = 0; u < KB_GA_U; ++u) {
         const int i = i0 + u;
         const bool ok = i < ch;
+        const uint32_t gi = (uint32_t)(c0 + (ok ? i : 0));
+        const uint32_t g = (uint32_t)part + ((uint32_t)my_tiles - 1u - gi) * (uint32_t)parts;
         len[u] = ok ? seg_len[i] : 0u;
-        first[u] = ok ? (tile_of(c0 + i) - tmin) * TILE_B + (uint32_t)KB6_BYTES * seg_off[i] : 0u;
-        const uint32_t o = (first[u] + (uint32_t)KB6_BYTES * (uint32_t)lane) & ~3u;
-        wl[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)o, 0, 2);
-        wh[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)o + 4, 0, 2);
+        first[u] = g * stride + (ok ? seg_off[i] : 0u);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t o = (uint32_t)lane + 64u * h;
+          r[u][h] = o < len[u] ? __builtin_nontemporal_load(sr + first[u] + o) : 0ull;
+        }
       }
 #pragma unroll
       for (int u = 0; u < KB_GA_U; ++u)
-        if ((uint32_t)lane < len[u])
-          add_rec(kb6_rec(wl[u], wh[u], first[u] + (uint32_t)KB6_BYTES * (uint32_t)lane));
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if ((uint32_t)lane + 64u * h < len[u]) add_rec(r[u][h]);
       // the rest of long segments (skewed keys), 64 records a step
 #pragma unroll 1
       for (int u = 0; u < KB_GA_U; ++u)
-        for (uint32_t o = 64u + (uint32_t)lane; o < len[u]; o += 64u) {
-          const uint32_t ob = first[u] + (uint32_t)KB6_BYTES * o;
-          add_rec(kb6_rec(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(ob & ~3u), 0, 2),
-                          __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(ob & ~3u) + 4, 0, 2), ob));
-        }
+        for (uint32_t o = 128u + (uint32_t)lane; o < len[u]; o += 64u) add_rec(sr[first[u] + o]);
     }
   }
   __syncthreads();
@@ -917,7 +827,7 @@ int64_t keyed_tiles(int64_t n) {
 int64_t keyed_buckets(int64_t n_keys) { return (n_keys + KB_ROWS - 1) / KB_ROWS; }
 bool keyed_bucketed(int64_t n_keys, int64_t n) {  // (record indices, padded tiles, < 2^32)
   return n_keys > 0 && keyed_buckets(n_keys) <= KB_NB_MAX && n < ((int64_t)1 << 32) - KB_SW_TILE &&
-         keyed_sweep_tiles(n) * KB_SW_TILE * 3 < ((int64_t)1 << 32);  // (the gather's halfwords)
+         keyed_sweep_tiles(n) * KB_SW_TILE < ((int64_t)1 << 32);
 }
 int64_t keyed_sweep_tile(int64_t n) {
   const int64_t cus = keyed_cus();
@@ -946,9 +856,8 @@ int64_t keyed_counts_words(int64_t n_keys, int64_t n) {
   const int64_t a = keyed_tiles(n) * nb, b = keyed_sweep_tiles(n) * (nb + 1);
   return a > b ? a : b;
 }
-int64_t keyed_sr_slots(int64_t n) {  // (u64 slots: the sweep's 6-B records + one slot the
-  // gather's last 8-B window may reach; the bucketed path's n records)
-  const int64_t t = keyed_sweep_tiles(n) * KB_SW_TILE * KB6_BYTES / 8 + 1;
+int64_t keyed_sr_slots(int64_t n) {
+  const int64_t t = keyed_sweep_tiles(n) * KB_SW_TILE;
   return t > n ? t : n;
 }
 int64_t keyed_part_words(int64_t n_keys, int na) {
@@ -970,7 +879,8 @@ static hipError_t run_sweep(int64_t n_keys, int64_t n, const int32_t* key, const
                        tile, G);
   }
   hipLaunchKernelGGL(kb_gather<NA>, dim3((unsigned)(nb * parts)), dim3(KB_GA_THREADS), 0, s, G, n_keys,
-                     nb, parts, kw.counts, kw.sr, kw.part_acc, kw.arrive, out[0], out[1]);
+                     nb, parts, (uint32_t)KB_SW_TILE, kw.counts, kw.sr, kw.part_acc, kw.arrive,
+                     out[0], out[1]);
   if (NA >= 2 && n > 0)  // (few workgroups: each adds to one arrival counter; the list is short)
     hipLaunchKernelGGL(kb_escape, dim3(KB_ESC_WG), dim3(256), 0, s, kw.esc_n, kw.esc_row, kw.esc_cpu,
                        kw.esc_mem, out[0], out[1]);

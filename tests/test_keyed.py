@@ -111,17 +111,17 @@ def test_gpu_keyed_edges(eng):
 
 @pytest.mark.gpu
 def test_gpu_keyed_record_fields(eng):
-    """The sweep's 6-byte record (kcc_keyed.hip kb_sweep): 16 cpu bits, memory as a 19-bit
-    count of MiB or of 10^6 B; every value at and around each field's edge, in both units,
-    values of both forms, and the escapes past them — each container alone on its row, and
-    all of them on one row."""
+    """The sweep's staged record (kcc_keyed.hip kb_record: 20 cpu bits, memory / 64 below
+    2^38) and round 5's measured-and-dropped 6-byte one (16 cpu bits, memory as 19-bit MiB
+    or 10^6-B counts): values at and around every field edge of both, and the escapes past
+    them — each container alone on its row, and all of them on one row."""
     MI, M = 1 << 20, 1_000_000
     cpu_edges = [0, 1, (1 << 16) - 1, 1 << 16, (1 << 16) + 1, (1 << 20) - 1, 1 << 20,
                  (1 << 64) - 1, (1 << 63) + 7]
     mem_edges = [0, MI, ((1 << 19) - 1) * MI, (1 << 19) * MI, ((1 << 19) + 1) * MI,
                  M, ((1 << 19) - 1) * M, (1 << 19) * M, ((1 << 19) - 1) * M + 1,
                  15625 * MI, 64, 100, -MI, -M, 1 << 62, -(1 << 63), (1 << 63) - 1,
-                 250 * M, 128 * MI, 3 * MI + M]
+                 250 * M, 128 * MI, 3 * MI + M, (1 << 38) - 64, 1 << 38, (1 << 38) + 64]
     cpu = np.array([c for c in cpu_edges for _ in mem_edges], np.uint64)
     mem = np.array([m for _ in cpu_edges for m in mem_edges], np.int64)
     nk = cpu.size
