@@ -721,7 +721,8 @@ def keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream, steps, war
                      "traffic": traffic,
                      "traffic_source": parts[0][1] and f"profiles/pmc_traffic.json ({parts[0][1]}); "
                                                        "sum of the kernels per call",
-                     "note": "one sweep: each 16384-container tile counting-sorted by bucket in "
+                     "note": "one sweep (one persistent workgroup per CU, the next tile's loads in "
+                             "flight): each 8192-container tile counting-sorted by bucket in "
                              "LDS into 8-B records (row in bucket, low cpu bits, memory / 64; the "
                              "rest on an escape list) written as one contiguous run, then per "
                              "bucket the tiles' segments summed in LDS; keys read once, no "
