@@ -1063,18 +1063,22 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
       const uint64_t sb0 = np_base + before;
       const uint32_t tot = np_tot;
       const uint32_t pad = (tot + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP - tot;
+// (non-temporal stores here, so fewer dirty lines wait for the end-of-kernel write-back,
+// measured: C4 step 0.2895 -> 0.3171 ms — the rows' scattered partial-group stores then
+// reach HBM one by one — 8-way rank 0.0594 -> 0.0582; round 5, profiles/r05_ab_np_nt.txt)
+#define NP_ST(ref, v) ((ref) = (v))
       auto put = [&](uint64_t pos, uint64_t fmv, uint32_t fcv, uint32_t Pv, int32_t clv) {
         const int kk = (int)(pos % FIT_GROUP);
-        if (NC) fast_cl[pos] = clv;
+        if (NC) NP_ST(fast_cl[pos], clv);
         FitGroupA& a = fast_a[pos / FIT_GROUP];
-        a.fm[kk] = fmv;
-        a.fc[kk] = fcv;
-        a.P[kk] = Pv;
+        NP_ST(a.fm[kk], fmv);
+        NP_ST(a.fc[kk], fcv);
+        NP_ST(a.P[kk], Pv);
         if (want_b) {
           FitGroup& g = fast_b[pos / FIT_GROUP];
-          g.fc[kk] = (double)fcv;                      // exact
-          g.fm[kk] = (double)fmv;                      // exact (< 2^50)
-          g.Pb[kk] = FIT_BIAS + (double)Pv;            // exact (P <= 2^20)
+          NP_ST(g.fc[kk], (double)fcv);                      // exact
+          NP_ST(g.fm[kk], (double)fmv);                      // exact (< 2^50)
+          NP_ST(g.Pb[kk], FIT_BIAS + (double)Pv);            // exact (P <= 2^20)
         }
       };
       uint32_t done = 0;  // streamed rows of this wave's earlier sub-steps
@@ -1089,8 +1093,8 @@ __global__ __launch_bounds__(KCC_NODE_PREP_BLOCK) void node_prep_kernel(int64_t 
         if (c2 | c3) {
           const int32_t wr = (int32_t)pk3[q] >> 18 << 12 | (int32_t)((pk2[q] >> 26) << 6 | pk1[q] >> 26);
           const uint64_t wbits = (uint64_t)(uint32_t)wr << 32;  // record: cell | w << 32
-          if (c2) prec[np_bstart[pk3[q] & 0x1ffu] + (pk2[q] & 0x1fffu)] = wbits | c2;
-          if (c3) prec[np_bstart[(pk3[q] >> 9) & 0x1ffu] + ((pk2[q] >> 13) & 0x1fffu)] = wbits | c3;
+          if (c2) NP_ST(prec[np_bstart[pk3[q] & 0x1ffu] + (pk2[q] & 0x1fffu)], wbits | c2);
+          if (c3) NP_ST(prec[np_bstart[(pk3[q] >> 9) & 0x1ffu] + ((pk2[q] >> 13) & 0x1fffu)], wbits | c3);
         }
       }
       if (threadIdx.x < pad) put(np_base + tot + threadIdx.x, 0ull, 0u, 0u, 0);  // the last group's padding
