@@ -499,13 +499,10 @@ hipError_t prof_event(Dev& dv, hipEvent_t* ev) {
     dv.prof_free.pop_back();
     return hipSuccess;
   }
-#ifdef KCC_PROF_SYSTEM_FENCE
-  return hipEventCreate(ev);
-#else
   // device-scope release only: a timing event between two kernels of one stream needs no
-  // system-scope fence (with it every record left a ~5.5 us gap on the stream)
+  // system-scope fence (with it, hipEventCreate's default, every record left a ~5.5 us gap
+  // on the stream)
   return hipEventCreateWithFlags(ev, hipEventDisableSystemFence);
-#endif
 }
 
 // Chunk boundaries: node ranges of ~equal node count, multiples of CHUNK_ALIGN (a
