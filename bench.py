@@ -709,7 +709,7 @@ def keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream, steps, war
     alg = C * 20 + n * 16
     gbs = alg / (ms * 1e-3) / 1e9
     del key, kc, km, oc, om
-    kernels = ["kb_sweep<2>", "kb_gather<2>", "kb_escape"]  # the one-sweep path (KCC_KB_SWEEP)
+    kernels = ["kb_sweep<2>", "kb_gather<2>", "kb_escape"]  # the one-sweep path
     parts = [pmc_traffic(k) if with_traffic else (None, None) for k in kernels]
     traffic = sum(t for t, _ in parts) if all(t is not None for t, _ in parts) else None
     return {
