@@ -12,7 +12,7 @@
 #if !defined(KCC_VARIANT_BUILD) &&                                                       \
     (defined(KCC_DIAG_RED_NOSTORE) || defined(KCC_DIAG_RED_LOADONLY) ||                  \
      defined(KCC_TIMELINE) || defined(KCC_DIAG_RED_GIVEUP) || defined(KCC_DIAG_P2P_GIVEUP) || \
-     defined(KCC_DIAG_INLIB_COMM))
+     defined(KCC_DIAG_INLIB_COMM) || defined(KCC_DIAG_GA_NOATOM))
 #error "a diagnostic KCC_* knob in a release build: use `make variant` (KCC_VARIANT_BUILD)"
 #endif
 

@@ -706,6 +706,10 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
     for (int a = 0; a < NACC; ++a) acc[a][r] = 0ull;
   // this part's tiles: g = part, part + parts, ...
   const int64_t my_tiles = G > part ? (G - part + parts - 1) / parts : 0;
+#ifdef KCC_DIAG_GA_NOATOM
+  uint64_t dg = 0;  // timing build: the records summed into a register (wrong sums)
+  auto add_rec = [&](uint64_t rec) { dg += rec; };
+#else
   auto add_rec = [&](uint64_t rec) {
     const uint32_t r = (uint32_t)rec & (KB_ROWS - 1);
     if constexpr (NA == 0) {
@@ -715,6 +719,7 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
       atomicAdd(&acc[1][r], (unsigned long long)((rec >> 32) << KB_MEM_SHIFT));
     }
   };
+#endif
   for (int64_t c0 = 0; c0 < my_tiles; c0 += KB_GA_CH) {
     const int ch = (int)min((int64_t)KB_GA_CH, my_tiles - c0);
     __syncthreads();  // the previous chunk's table entries are consumed
@@ -756,6 +761,9 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
     }
   }
   __syncthreads();
+#ifdef KCC_DIAG_GA_NOATOM
+  if (dg == 0x123456789ull) acc[0][0] = dg;  // (keeps the sums alive)
+#endif
   const int64_t row0 = (int64_t)b * KB_ROWS;
   uint64_t* out[2] = {o0, o1};
   if (parts == 1) {
