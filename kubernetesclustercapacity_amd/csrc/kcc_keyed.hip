@@ -685,7 +685,16 @@ constexpr int KB_GA_WAVES = KB_GA_THREADS / 64;
 // segments per wave in flight, 128 records of each (C4 A/B, one part: 8 -> 0.3404 ms, 16 ->
 // 0.3394 ms; round 5: 24 equal, 32 spills)
 constexpr int KB_GA_U = 16;
-constexpr int KB_GA_CH = 2048;  // tiles per table chunk in LDS
+constexpr int KB_GA_CH = 2048;  // tiles per table chunk in LDS (a barrier each: 1024 measured slower)
+// buckets per gather workgroup: a tile's segments of KB_GA_BPG adjacent buckets are
+// contiguous in its run, so a workgroup reads them as one segment (half the segments, their
+// partial lines and their latency batches, for twice the LDS rows)
+#ifndef KCC_KB_GA_BPG
+#define KCC_KB_GA_BPG 2
+#endif
+constexpr int KB_GA_BPG = KCC_KB_GA_BPG;
+constexpr int KB_GA_ROWS = KB_GA_BPG * KB_ROWS;  // LDS rows per gather workgroup
+static_assert(KB_SW_TILE < 0xffff, "a segment's length and split point pack in 16 bits each");
 // Tiles are read newest-first (the last-written records first, while the memory-side cache
 // may hold them): measured equal (0.3427 / 0.3432 ms), kept.
 
@@ -695,23 +704,25 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
     const uint64_t* __restrict__ sr, uint64_t* __restrict__ part_acc, uint32_t* __restrict__ arrive,
     uint64_t* __restrict__ o0, uint64_t* __restrict__ o1) {
   constexpr int NACC = NA > 0 ? NA : 1;
-  __shared__ unsigned long long acc[NACC][KB_ROWS];
+  __shared__ unsigned long long acc[NACC][KB_GA_ROWS];
   __shared__ uint32_t seg_off[KB_GA_CH];  // start within the tile
-  __shared__ uint32_t seg_len[KB_GA_CH];
+  __shared__ uint32_t seg_len[KB_GA_CH];  // length | (where the group's second bucket starts) << 16
   __shared__ uint32_t last_s;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // b: the bucket group (buckets KB_GA_BPG b .. + nbk - 1)
   const int b = blockIdx.x / parts, part = blockIdx.x % parts;
-  for (int r = tid; r < KB_ROWS; r += KB_GA_THREADS)
+  const int b0 = KB_GA_BPG * b, nbk = nb - b0 < KB_GA_BPG ? nb - b0 : KB_GA_BPG;
+  for (int r = tid; r < KB_GA_ROWS; r += KB_GA_THREADS)
 #pragma unroll
     for (int a = 0; a < NACC; ++a) acc[a][r] = 0ull;
   // this part's tiles: g = part, part + parts, ...
   const int64_t my_tiles = G > part ? (G - part + parts - 1) / parts : 0;
 #ifdef KCC_DIAG_GA_NOATOM
   uint64_t dg = 0;  // timing build: the records summed into a register (wrong sums)
-  auto add_rec = [&](uint64_t rec) { dg += rec; };
+  auto add_rec = [&](uint64_t rec, uint32_t hi) { dg += rec + hi; };
 #else
-  auto add_rec = [&](uint64_t rec) {
-    const uint32_t r = (uint32_t)rec & (KB_ROWS - 1);
+  auto add_rec = [&](uint64_t rec, uint32_t hi) {  // hi: KB_ROWS for the group's second bucket
+    const uint32_t r = ((uint32_t)rec & (KB_ROWS - 1)) + hi;
     if constexpr (NA == 0) {
       atomicAdd(&acc[0][r], 1ull);
     } else {
@@ -725,10 +736,11 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
     __syncthreads();  // the previous chunk's table entries are consumed
     for (int i = tid; i < ch; i += KB_GA_THREADS) {
       const int64_t g = (int64_t)part + (my_tiles - 1 - (c0 + i)) * parts;
-      const uint32_t* row = tab + g * (nb + 1) + b;
-      const uint32_t s0 = row[0], s1 = row[1];
+      const uint32_t* row = tab + g * (nb + 1) + b0;
+      const uint32_t s0 = row[0];
       seg_off[i] = s0;
-      seg_len[i] = s1 - s0;
+      // (tile runs < 2^16 records: 0xffff is "no second bucket", past every index)
+      seg_len[i] = (row[nbk] - s0) | (KB_GA_BPG > 1 && nbk > 1 ? row[1] - s0 : 0xffffu) << 16;
     }
     __syncthreads();
     for (int i0 = wv * KB_GA_U; i0 < ch; i0 += KB_GA_WAVES * KB_GA_U) {
@@ -741,33 +753,38 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
         const bool ok = i < ch;
         const uint32_t gi = (uint32_t)(c0 + (ok ? i : 0));
         const uint32_t g = (uint32_t)part + ((uint32_t)my_tiles - 1u - gi) * (uint32_t)parts;
-        len[u] = ok ? seg_len[i] : 0u;
+        len[u] = ok ? seg_len[i] : 0xffff0000u;  // length | mid << 16 (registers: an LDS
+        // read between the adds would wait for every LDS atomic issued before it)
         first[u] = g * stride + (ok ? seg_off[i] : 0u);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const uint32_t o = (uint32_t)lane + 64u * h;
-          r[u][h] = o < len[u] ? __builtin_nontemporal_load(sr + first[u] + o) : 0ull;
+          r[u][h] = o < (len[u] & 0xffffu) ? __builtin_nontemporal_load(sr + first[u] + o) : 0ull;
         }
       }
 #pragma unroll
-      for (int u = 0; u < KB_GA_U; ++u)
+      for (int u = 0; u < KB_GA_U; ++u) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-          if ((uint32_t)lane + 64u * h < len[u]) add_rec(r[u][h]);
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t o = (uint32_t)lane + 64u * h;
+          if (o < (len[u] & 0xffffu)) add_rec(r[u][h], o >= (len[u] >> 16) ? (uint32_t)KB_ROWS : 0u);
+        }
+      }
       // the rest of long segments (skewed keys), 64 records a step
 #pragma unroll 1
       for (int u = 0; u < KB_GA_U; ++u)
-        for (uint32_t o = 128u + (uint32_t)lane; o < len[u]; o += 64u) add_rec(sr[first[u] + o]);
+        for (uint32_t o = 128u + (uint32_t)lane; o < (len[u] & 0xffffu); o += 64u)
+          add_rec(sr[first[u] + o], o >= (len[u] >> 16) ? (uint32_t)KB_ROWS : 0u);
     }
   }
   __syncthreads();
 #ifdef KCC_DIAG_GA_NOATOM
   if (dg == 0x123456789ull) acc[0][0] = dg;  // (keeps the sums alive)
 #endif
-  const int64_t row0 = (int64_t)b * KB_ROWS;
+  const int64_t row0 = (int64_t)b0 * KB_ROWS;
   uint64_t* out[2] = {o0, o1};
   if (parts == 1) {
-    for (int r = tid; r < KB_ROWS; r += KB_GA_THREADS) {
+    for (int r = tid; r < KB_GA_ROWS; r += KB_GA_THREADS) {
       if (row0 + r >= n_keys) break;
 #pragma unroll
       for (int a = 0; a < NACC; ++a) out[a][row0 + r] = acc[a][r];
@@ -775,11 +792,11 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
     return;
   }
   // several parts: publish this part's rows, the last part to arrive sums and writes
-  uint64_t* mine = part_acc + ((int64_t)b * parts + part) * NACC * KB_ROWS;
-  for (int r = tid; r < KB_ROWS; r += KB_GA_THREADS)
+  uint64_t* mine = part_acc + ((int64_t)b * parts + part) * NACC * KB_GA_ROWS;
+  for (int r = tid; r < KB_GA_ROWS; r += KB_GA_THREADS)
 #pragma unroll
     for (int a = 0; a < NACC; ++a)
-      __hip_atomic_store(mine + a * KB_ROWS + r, (uint64_t)acc[a][r], __ATOMIC_RELAXED,
+      __hip_atomic_store(mine + a * KB_GA_ROWS + r, (uint64_t)acc[a][r], __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (tid == 0) {
@@ -790,14 +807,14 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
   __syncthreads();
   if (!last_s) return;
   if (tid == 0) __hip_atomic_store(arrive + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (int r = tid; r < KB_ROWS; r += KB_GA_THREADS) {
+  for (int r = tid; r < KB_GA_ROWS; r += KB_GA_THREADS) {
     if (row0 + r >= n_keys) break;
 #pragma unroll
     for (int a = 0; a < NACC; ++a) {
       uint64_t t = acc[a][r];
       for (int p = 0; p < parts; ++p)
         if (p != part)
-          t += __hip_atomic_load(part_acc + ((int64_t)b * parts + p) * NACC * KB_ROWS + a * KB_ROWS + r,
+          t += __hip_atomic_load(part_acc + ((int64_t)b * parts + p) * NACC * KB_GA_ROWS + a * KB_GA_ROWS + r,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       out[a][row0 + r] = t;
     }
@@ -849,15 +866,15 @@ int64_t keyed_sweep_tiles(int64_t n) {
   return n > 0 ? (n + t - 1) / t : 0;
 }
 
-// gather workgroups per bucket: one while the buckets fill half the CUs (C4, 245 buckets:
-// 1 part 0.339-0.340 ms, 2 parts 0.372 ms), else up to 4 (a key space of a few buckets
-// would otherwise leave its gather to a few CUs)
+// gather workgroups per bucket group (one workgroup per CU: its LDS rows): as many as one
+// round of them holds, 1 to 4 (C4: 123 groups of two buckets, 2 parts; round 4 with one
+// bucket per workgroup, 245 buckets: 1 part 0.339-0.340 ms, 2 parts 0.372 ms)
 constexpr int KB_GA_PARTS_MAX = 4;
 int keyed_sweep_parts(int64_t nb) {
-  const int64_t cus = keyed_cus();
-  if (nb <= 0 || 2 * nb >= cus) return 1;
-  const int64_t p = (cus + nb - 1) / nb;
-  return (int)(p > KB_GA_PARTS_MAX ? KB_GA_PARTS_MAX : p);
+  const int64_t cus = keyed_cus(), ng = (nb + KB_GA_BPG - 1) / KB_GA_BPG;
+  if (ng <= 0) return 1;
+  const int64_t p = cus / ng;
+  return (int)(p < 1 ? 1 : p > KB_GA_PARTS_MAX ? KB_GA_PARTS_MAX : p);
 }
 int64_t keyed_counts_words(int64_t n_keys, int64_t n) {
   const int64_t nb = keyed_buckets(n_keys);
@@ -868,8 +885,9 @@ int64_t keyed_sr_slots(int64_t n) {
   const int64_t t = keyed_sweep_tiles(n) * KB_SW_TILE;
   return t > n ? t : n;
 }
-int64_t keyed_part_words(int64_t n_keys, int na) {
-  return keyed_buckets(n_keys) * KB_GA_PARTS_MAX * (na > 0 ? na : 1) * (int64_t)KB_ROWS;
+int64_t keyed_part_words(int64_t n_keys, int na) {  // (bucket groups x parts x arrays x rows)
+  const int64_t ng = (keyed_buckets(n_keys) + KB_GA_BPG - 1) / KB_GA_BPG;
+  return ng * KB_GA_PARTS_MAX * (na > 0 ? na : 1) * (int64_t)KB_GA_ROWS;
 }
 
 // the one-sweep path (NA = 0 / 2): kb_sweep, kb_gather, kb_escape
@@ -886,7 +904,8 @@ static hipError_t run_sweep(int64_t n_keys, int64_t n, const int32_t* key, const
                        in[0], in[1], nb, kw.counts, kw.sr, kw.esc_n, kw.esc_row, kw.esc_cpu, kw.esc_mem,
                        tile, G);
   }
-  hipLaunchKernelGGL(kb_gather<NA>, dim3((unsigned)(nb * parts)), dim3(KB_GA_THREADS), 0, s, G, n_keys,
+  const int ng = (nb + KB_GA_BPG - 1) / KB_GA_BPG;  // bucket groups
+  hipLaunchKernelGGL(kb_gather<NA>, dim3((unsigned)(ng * parts)), dim3(KB_GA_THREADS), 0, s, G, n_keys,
                      nb, parts, (uint32_t)KB_SW_TILE, kw.counts, kw.sr, kw.part_acc, kw.arrive,
                      out[0], out[1]);
   if (NA >= 2 && n > 0)  // (few workgroups: each adds to one arrival counter; the list is short)
