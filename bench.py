@@ -725,7 +725,7 @@ def keyed_leg(eng, ptr, cpu, mem, used_cpu, used_mem, n, dev, stream, steps, war
                              "flight): each 8192-container tile counting-sorted by bucket in "
                              "LDS into 8-B records (row in bucket, low cpu bits, memory / 64; the "
                              "rest on an escape list) written as one contiguous run, then per "
-                             "bucket the tiles' segments summed in LDS; keys read once, no "
+                             "pair of buckets the tiles' segments summed in LDS; keys read once, no "
                              "histogram pass, no global atomics on the common path"},
         "equals_csr_reduce": diff_rows == 0, "rows_differing": diff_rows,
     }
