@@ -132,6 +132,27 @@ def test_gpu_keyed_record_fields(eng):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nk", [1, 4096, 4097, 2 * 4096 + 7, 5 * 4096, 97 * 4096 + 11])
+def test_gpu_keyed_bucket_groups(eng, nk):
+    """The gather's bucket pairs and parts: one bucket, a key space ending exactly on a
+    bucket, an odd bucket count (the last group a single bucket), few groups gathered by up
+    to 4 parts each, and a mid-size key space; a 300k-container list with a hot row on each
+    side of every pair's split and rows at both ends."""
+    rng = np.random.default_rng(nk)
+    key = rng.integers(-1, nk + 1, 300_001).astype(np.int32)
+    hot = [0, nk - 1, min(nk - 1, 4095), min(nk - 1, 4096)]
+    key[rng.random(key.size) < 0.2] = hot[0]
+    key[:len(hot)] = hot
+    cpu = (rng.integers(0, 41, key.size) * 50).astype(np.uint64)
+    mem = rng.integers(0, 8192, key.size).astype(np.int64) << 20
+    r = eng.get_pod_cpu_memory_requests_limits_keyed(nk, key, cpu, mem)
+    o = oracle_keyed(nk, key, cpu, mem)
+    assert np.array_equal(r.cpu_requests, o[0]) and np.array_equal(r.memory_requests, o[1])
+    ok = key[(key >= 0) & (key < nk)]
+    assert np.array_equal(eng.count_by_key(nk, key), np.bincount(ok, minlength=nk).astype(np.int64))
+
+
+@pytest.mark.gpu
 def test_gpu_keyed_atomic_fallback(eng):
     """More rows than the bucketed path holds (4096 buckets x 4096 rows): the device-atomic
     kernels."""
