@@ -249,7 +249,7 @@ def test_gpu_p2p_exchange_graph_replay(tmp_path):
             np.testing.assert_array_equal(got[k][S:], e, err_msg=f"rank {r} replay {k}")
 
 
-def _worker_fault(rank, world, port, n, pods, S, exchange, faultdiag, out):
+def _worker_fault(rank, world, port, n, pods, S, exchange, faultdiag, out, clamp_mode=-1):
     """One rank's step with the library of `faultdiag` on rank `world - 1` only (every
     bounded wait there gives up, so its reduce's look-back faults its device), the others
     the release library; then the exchange: the one-shot p2p push (`p2p`) or a gloo
@@ -272,6 +272,7 @@ def _worker_fault(rank, world, port, n, pods, S, exchange, faultdiag, out):
     err = torch.empty(S, dtype=torch.int32, device=dev)
     lib = faultdiag if rank == world - 1 else None
     with CapacityEngine(0, 1, lib_path=lib) as eng:
+        eng.set_clamp_in_fit(clamp_mode)  # -1: by size (here the fit's), 0: clamp_apply
         if exchange == "p2p":
             handles = [None] * world
             dist.all_gather_object(handles, eng.p2p_export(world, S))
@@ -296,8 +297,8 @@ def _worker_fault(rank, world, port, n, pods, S, exchange, faultdiag, out):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("exchange", ["p2p", "allreduce"])
-def test_gpu_fault_reaches_every_rank(tmp_path, exchange):
+@pytest.mark.parametrize("exchange,clamp_mode", [("p2p", -1), ("allreduce", -1), ("p2p", 0)])
+def test_gpu_fault_reaches_every_rank(tmp_path, exchange, clamp_mode):
     """A device fault on ONE rank (its reduce's look-back gave up: the fault-path build on
     the last rank) reaches every rank's totals: the faulted rank's partial carries
     SPEC_FAULT_MARK in its div-by-zero counts, so the healthy rank's finalize — after the
@@ -309,8 +310,8 @@ def test_gpu_fault_reaches_every_rank(tmp_path, exchange):
         pytest.fail("libkcc_faultdiag.so missing: __graft_entry__.build() builds it")
     n, pods, S, world = 20_011, 300_000, 300, 2
     out = str(tmp_path / "flt")
-    mp.spawn(_worker_fault, args=(world, _free_port(), n, pods, S, exchange, faultdiag, out),
-             nprocs=world, join=True)
+    mp.spawn(_worker_fault, args=(world, _free_port(), n, pods, S, exchange, faultdiag, out,
+                                  clamp_mode), nprocs=world, join=True)
     for r in range(world):
         got = np.load(out + f".{r}.npy")
         assert (got[S:2 * S] == 2).all(), f"rank {r}: spec_err {np.unique(got[S:2 * S])}"
