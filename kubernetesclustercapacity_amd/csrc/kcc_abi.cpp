@@ -115,6 +115,7 @@ struct Dev {
   // by the kernel); the peers' mapped mailboxes
   DevBuf p2p_mbox, p2p_arrive;
   DevBuf clamp_arrive;  // clamp_apply's fused finalize: arrivals (zero between launches)
+  DevBuf np_sync;       // node prep in the reduce launch: epoch and flag words (NpArgs::sync)
   unsigned char* p2p_peer[kcc::P2P_MAX_RANKS] = {};  // opened peer mailboxes (own: p2p_mbox)
   int p2p_W = 0, p2p_rank = -1;
   int64_t p2p_smax = 0;
@@ -297,6 +298,11 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
   KCC_HIP(ctx, ensure(dv.srec, sizeof(kcc::SpecRec) * S));
   KCC_HIP(ctx, ensure(dv.sperm, 4 * S));
   KCC_HIP(ctx, ensure(dv.counters, sizeof(unsigned long long) * kcc::CNT_N));
+  if (!dv.np_sync.p) {  // node prep in the reduce launch: epoch words (kcc::NpArgs::sync)
+    const size_t bytes = 4 * (kcc::NP_FLAGS + (size_t)kcc::reduce_tail_records());
+    KCC_HIP(ctx, ensure(dv.np_sync, bytes));
+    KCC_HIP(ctx, hipMemsetAsync(dv.np_sync.p, 0, bytes, dv.stream));
+  }
   if (!dv.clamp_arrive.p) {  // the fused finalize's arrivals: every launch leaves them zero
     KCC_HIP(ctx, ensure(dv.clamp_arrive, 64));
     KCC_HIP(ctx, hipMemsetAsync(dv.clamp_arrive.p, 0, 64, dv.stream));
@@ -505,6 +511,10 @@ hipError_t prof_event(Dev& dv, hipEvent_t* ev) {
   return hipEventCreateWithFlags(ev, hipEventDisableSystemFence);
 }
 
+#ifndef KCC_NP_IN_REDUCE
+#define KCC_NP_IN_REDUCE 1
+#endif
+
 // Chunk boundaries: node ranges of ~equal node count, multiples of CHUNK_ALIGN (a
 // multiple of FIT_GROUP: the fit's node groups do not straddle two chunks); at least
 // `min_nodes` nodes per chunk.
@@ -599,11 +609,38 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   dv.last_nc = nc;
   // the clamp in the fit needs no spec ranks (no clamp tables): the reduce launch carries
   // one workgroup that zeroes the counters, and spec_place counts the classes itself
-  const kcc::RankArgs ra = kcc::rank_args(n_specs, spec_cpu, spec_mem, clamp_of(dv),
-                                          as<unsigned long long>(dv.counters),
-                                          as<uint32_t>(dv.rank_arrive), nc);
+  kcc::RankArgs ra = kcc::rank_args(n_specs, spec_cpu, spec_mem, clamp_of(dv),
+                                    as<unsigned long long>(dv.counters),
+                                    as<uint32_t>(dv.rank_arrive), nc);
   kcc::PlaceArgs pa = place_args(dv, n_specs, spec_cpu, spec_mem, partial);
   pa.no_ranks = nc ? 1 : 0;
+  // the clamp in the fit with the ranks in the reduce launch: spec_place and node_prep's
+  // work ride there too, behind the reduce's workgroups (kcc::NpArgs) — one launch fewer
+  const bool np_fused = KCC_NP_IN_REDUCE && nc && fuse_rank;
+  kcc::NpArgs np{};
+  if (np_fused) {
+    ra.done_flag = as<uint32_t>(dv.np_sync);
+    np.n_place = (int32_t)((n_specs + 255) / 256);
+    np.n_rows = (int32_t)((n_nodes + kcc::NP_ROWS_PER_WG - 1) / kcc::NP_ROWS_PER_WG);
+    np.sync = as<uint32_t>(dv.np_sync);
+    np.pa = pa;
+    np.n = n_nodes;
+    np.alloc_cpu = alloc_cpu;
+    np.alloc_mem = alloc_mem;
+    np.alloc_pods = alloc_pods;
+    np.pod_count = pod_count;
+    np.used_cpu = used_cpu;
+    np.used_mem = used_mem;
+    np.fast_a = as<kcc::FitGroupA>(dv.fast_a);
+    np.fast_b = as<kcc::FitGroup>(dv.fast_b);
+    np.slow = as<kcc::SlowNode>(dv.slow);
+    np.slow_list = as<int64_t>(dv.slow_list);
+    np.fast_cl = fast_cl;
+    np.counters = as<unsigned long long>(dv.counters);
+    np.bcnt = clamp_of(dv).bcnt;
+    np.S = n_specs;
+    np.faults = as<unsigned long long>(dv.faults);
+  }
   if (n_specs > 0) {
     rc = clamp_clean(ctx, dv, s);
     if (rc) return rc;
@@ -622,7 +659,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                     used_cpu + lo[c], used_mem + lo[c], nullptr, nullptr,
                                     as<uint64_t>(dv.red_tail),
                                     as<unsigned long long>(dv.faults), rs,
-                                    fuse_rank ? &ra : nullptr));
+                                    fuse_rank ? &ra : nullptr, np_fused ? &np : nullptr));
     if (dv.prof_on) {
       KCC_HIP(ctx, hipEventRecord(pp.b, rs));
       pp.kind = 0;
@@ -638,6 +675,7 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     const int64_t n = hi[c] - lo[c];
     const bool place_here = fuse_place && c == 0;
     if (n_specs == 0 || (n == 0 && !place_here)) continue;
+    if (!np_fused)  // (else: in the reduce launch)
     KCC_HIP(ctx, kcc::launch_node_prep(n, alloc_cpu + lo[c], alloc_mem + lo[c], alloc_pods + lo[c],
                                        pod_count + lo[c], used_cpu + lo[c], used_mem + lo[c],
                                        as<kcc::FitGroupA>(dv.fast_a) + lo[c] / kcc::FIT_GROUP,
@@ -959,6 +997,7 @@ void kcc_destroy(kcc_ctx* ctx) {
         if (b->p) (void)hipFree(b->p);
     }
     if (dv.clamp_arrive.p) (void)hipFree(dv.clamp_arrive.p);
+    if (dv.np_sync.p) (void)hipFree(dv.np_sync.p);
     DevBuf* bufs[] = {&dv.c_rank, &dv.c_bcnt, &dv.c_cs, &dv.c_ms,
                       &dv.c_mrc, &dv.c_crm, &dv.c_dperm, &dv.c_C, &dv.c_H2, &dv.c_H3,
                       &dv.c_Crow, &dv.c_rec, &dv.c_dir,

@@ -12,13 +12,15 @@
 #if !defined(KCC_VARIANT_BUILD) &&                                                       \
     (defined(KCC_DIAG_RED_NOSTORE) || defined(KCC_DIAG_RED_LOADONLY) ||                  \
      defined(KCC_TIMELINE) || defined(KCC_DIAG_RED_GIVEUP) || defined(KCC_DIAG_P2P_GIVEUP) || \
-     defined(KCC_DIAG_INLIB_COMM) || defined(KCC_DIAG_GA_NOATOM))
+     defined(KCC_DIAG_INLIB_COMM) || defined(KCC_DIAG_GA_NOATOM) ||                     \
+     defined(KCC_DIAG_NP_NOSYNC) || defined(KCC_DIAG_NP_NOSC1))
 #error "a diagnostic KCC_* knob in a release build: use `make variant` (KCC_VARIANT_BUILD)"
 #endif
 
 namespace kcc {
 
 struct RankArgs;   // below: spec ranks, run as extra workgroups of a reduce launch
+struct NpArgs;     // below: node prep (clamp in the fit) behind a reduce launch's workgroups
 
 // ---- (a) segmented request reduce -------------------------------------------
 // One wavefront owns a contiguous range of reduce_range() containers and walks it in
@@ -102,7 +104,7 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
                          const uint64_t* cpu_lim, const int64_t* mem_lim,
                          uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem,
                          uint64_t* tail, unsigned long long* faults, hipStream_t s,
-                         const RankArgs* rank = nullptr);
+                         const RankArgs* rank = nullptr, const NpArgs* np = nullptr);
 
 // ---- (b) fit -----------------------------------------------------------------
 // Node streams of the fit kernel: groups of FIT_GROUP nodes, field-major inside the
@@ -276,6 +278,9 @@ struct RankArgs {
   // 1: the clamp in the fit needs no ranks — one workgroup that zeroes the counters and
   // writes the block class counts (bcnt) alone (PlaceArgs::no_ranks)
   int32_t zero_only;
+  // zero_only with node prep in the same launch (NpArgs): the counters and bcnt written
+  // through (sc1), then *done_flag = 1 for the node-prep workgroups
+  uint32_t* done_flag;      // NpArgs::sync (the epoch at NP_EPOCH, the flag at NP_DONE)
 };
 RankArgs rank_args(int64_t n_specs, const uint64_t* spec_cpu, const int64_t* spec_mem,
                    const ClampWork& cw, unsigned long long* counters, uint32_t* arrive,
@@ -302,6 +307,50 @@ struct PlaceArgs {
   int32_t no_ranks;
 };
 
+
+// Node prep of the clamp in the fit (one node chunk, S <= CLAMP_LDS_SPECS) as workgroups
+// behind a reduce launch's (KCC_NP_IN_REDUCE): n_place workgroups of spec_place (after the
+// zero_only rank workgroup's flag), then n_rows workgroups of 1024 rows each (node_prep's
+// clamp-in-fit work, after every reduce wave has signalled).  The reduce's node sums go
+// out write-through (sc1) and each reduce wave adds 1 to sync[16] when done (its stores
+// performed); the node-prep workgroups read them at agent scope.  The last of them resets
+// the sync words.  Dispatch order makes the waits safe: on every XCD all the reduce's
+// workgroups are dispatched before any node-prep workgroup, and no reduce wave waits on
+// one.  Every wait is bounded; a give-up counts in faults[FAULT_RED].
+struct NpArgs {
+  int32_t n_place, n_rows;  // workgroups (256 threads)
+  uint32_t* sync;           // NP_EPOCH, NP_DONE, NP_ARRIVE, NP_FLAGS (reduce_tail_records() words)
+  // set by launch_reduce: the reduce's CSR offsets, first container, range and wave count
+  const int64_t* ptr;
+  int64_t c0;
+  int32_t range, red_waves;
+  PlaceArgs pa;
+  int64_t n;                // rows
+  const uint64_t* alloc_cpu;
+  const int64_t* alloc_mem;
+  const int64_t* alloc_pods;
+  const int64_t* pod_count;
+  const uint64_t* used_cpu;
+  const int64_t* used_mem;
+  FitGroupA* fast_a;
+  FitGroup* fast_b;
+  SlowNode* slow;
+  int64_t* slow_list;
+  int32_t* fast_cl;
+  unsigned long long* counters;
+  const uint32_t* bcnt;
+  int64_t S;
+  unsigned long long* faults;
+};
+constexpr int NP_ROWS_PER_WG = 1024;  // 256 threads x 4 rows
+// NpArgs::sync (uint32 words, 64-B lines): [NP_EPOCH] the last launch's epoch (a launch's
+// epoch E is one past it; its last node-prep workgroup to finish publishes E), [NP_DONE]
+// the spec ranks' done flag (= E), [NP_ARRIVE] the node-prep arrivals (zero between
+// launches), then [NP_FLAGS + w] reduce wave w's flag (= E once its node sums are stored).
+// Epoch flags need no reset, and a node-prep workgroup waits for the waves that store its
+// rows alone: one counter of every wave's arrival took the ~3200 same-address atomics of
+// the 8-way C4 rank serially (~25 ns apiece, 80 us)
+constexpr int NP_EPOCH = 0, NP_DONE = 16, NP_ARRIVE = 32, NP_FLAGS = 64;
 
 // counters (CNT_*): exact-path (node, spec) pairs, class-B specs, and per node chunk
 // of a pipelined call (kcc_capacity_partial_async) the rows in that chunk's slow_list.

@@ -236,14 +236,35 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
          (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, 63);
 }
 
-template <int NA>
-__global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
+__device__ void np_body(const NpArgs& np, int32_t j, uint32_t* scratch);
+
+// NPM: node prep behind the reduce's workgroups (NpArgs): the node sums written through
+// (sc1) and every wave's completion counted
+#ifdef KCC_DIAG_NP_NOSYNC  // timing diagnostics only (wrong results): node prep does not wait
+constexpr bool KCC_NP_NOSYNC = true;
+#else
+constexpr bool KCC_NP_NOSYNC = false;
+#endif
+#ifdef KCC_DIAG_NP_NOSC1  // timing diagnostics only: the node sums stored plainly
+constexpr bool KCC_NP_NOSC1 = true;
+#else
+constexpr bool KCC_NP_NOSC1 = false;
+#endif
+template <int NA, bool NPM>
+__global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra, NpArgs np) {
   __shared__ __attribute__((aligned(16))) uint64_t pre_s[RED_WAVES_PER_BLOCK][NA][RED_TILE];
   static_assert(sizeof(pre_s) >= 16 * RANK_L, "the rank workgroups stage RANK_L 16-B keys");
+  const int32_t npb = NPM ? np.n_place + np.n_rows : 0;  // the last workgroups
+  if constexpr (NPM) {
+    if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - npb) {
+      np_body(np, (int32_t)blockIdx.x - ((int32_t)gridDim.x - npb), reinterpret_cast<uint32_t*>(&pre_s[0][0][0]));
+      return;
+    }
+  }
   // the spec ranks' workgroups: behind the reduce's (RedArgs::ranks_last; dispatched as its
   // first waves retire, they run in the reduce's tail) or in front of them
-  const int32_t rank0 = a.ranks_last ? (int32_t)gridDim.x - ra.n_blocks : 0;  // first rank block
-  const int32_t red0 = a.ranks_last ? 0 : ra.n_blocks;                        // first reduce block
+  const int32_t rank0 = a.ranks_last ? (int32_t)gridDim.x - npb - ra.n_blocks : 0;  // first rank block
+  const int32_t red0 = a.ranks_last ? 0 : ra.n_blocks;                              // first reduce block
   if constexpr (NA == 2) {  // (launch_reduce: the ranks ride the 2-array reduce only)
     if (ra.n_blocks > 0 && (int32_t)blockIdx.x >= rank0 && (int32_t)blockIdx.x < rank0 + ra.n_blocks) {
       spec_rank_body(ra, (int32_t)blockIdx.x - rank0, &pre_s[0][0][0]);
@@ -263,6 +284,16 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
   // are local to the launch)
   const int64_t wb = c0 + (int64_t)w * range;
   if (wb >= n_cont) return;  // wave-uniform; no block-level barrier in this kernel
+  // NPM: this launch's epoch (the node-prep workgroups publish it only after every storing
+  // wave's flag); the wave's stores performed, then its flag
+  const uint32_t epoch = NPM ? __hip_atomic_load(np.sync + NP_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
+  auto red_signal = [&]() {
+    if constexpr (NPM && !KCC_NP_NOSYNC) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if ((threadIdx.x & 63) == 0)
+        __hip_atomic_store(np.sync + NP_FLAGS + w, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
   KCC_TL(4096 + (blockIdx.x - red0) % 4096, 0);
   const int32_t len = (int32_t)(n_cont - wb < range ? n_cont - wb : range);
   __builtin_assume(len >= 1);  // (wb < n_cont: the tile loop runs, its first loads need no guard)
@@ -329,7 +360,10 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
     const int64_t pend_j = 64 * pend_blk + lane;
     if (pend_j >= own_lo) {
 #pragma unroll
-      for (int k = 0; k < NA; ++k) out[k][pend_j] = resF[k];
+      for (int k = 0; k < NA; ++k) {
+        if constexpr (NPM && !KCC_NP_NOSC1) __hip_atomic_store(out[k] + pend_j, resF[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else out[k][pend_j] = resF[k];
+      }
     }
     pend = false;
   };
@@ -351,7 +385,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
 #pragma unroll
     for (int k = 0; k < NA; ++k)
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, resF[k]), ro[k],
-                                            (int)voff, 0, 0);
+                                            (int)voff, 0, NPM && !KCC_NP_NOSC1 ? 16 : 0);  // (16: sc1)
     pend = false;
   };
 
@@ -489,7 +523,10 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
     if (j >= own_lo && j < cur) {
 #ifndef KCC_DIAG_RED_NOSTORE
 #pragma unroll
-      for (int k = 0; k < NA; ++k) out[k][j] = res[k];
+      for (int k = 0; k < NA; ++k) {
+        if constexpr (NPM && !KCC_NP_NOSC1) __hip_atomic_store(out[k] + j, res[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else out[k][j] = res[k];
+      }
 #endif
     }
   }
@@ -558,9 +595,13 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra) {
     }
     if (lane == 0) {
 #pragma unroll
-      for (int k = 0; k < NA; ++k) out[k][node0] = acc[k];
+      for (int k = 0; k < NA; ++k) {
+        if constexpr (NPM && !KCC_NP_NOSC1) __hip_atomic_store(out[k] + node0, acc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else out[k][node0] = acc[k];
+      }
     }
   }
+  red_signal();
   KCC_TL(4096 + (blockIdx.x - red0) % 4096, 1);
 }
 
@@ -575,6 +616,210 @@ constexpr int64_t FAST_P_ABS = 1ll << 20;       // |allocatable pods| <= 2^20
 constexpr int64_t FAST_CL_ABS = 1ll << 20;      // |allocPods - podCount| <= 2^20
 constexpr uint64_t FAST_C_MAX = 1ull << 51;     // 1 <= spec cpu < 2^51
 constexpr int64_t FAST_M_MAX = 1ll << 51;       // 1 <= spec mem < 2^51
+
+// ---- node prep behind the reduce (NpArgs, the clamp in the fit) ---------------------
+[[maybe_unused]] constexpr uint32_t NP_SPIN_MAX = 1u << 22;  // polls before a wait gives up (~2 s)
+// thread 0 waits until *w == epoch (bounded: a give-up counts as a reduce fault), then the
+// workgroup goes on.  Polls ~0.5 us apart (each is an uncached load of one line)
+__device__ void np_wait(const uint32_t* w, uint32_t epoch, unsigned long long* faults) {
+  if (threadIdx.x == 0) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+      if (++spins >= NP_SPIN_MAX) {
+        atomicAdd(&faults[FAULT_RED], 1ull);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(20);
+    }
+  }
+  __syncthreads();
+}
+
+// rows [i0, i1): wave 0 waits for the flags of the reduce waves that store their sums — the
+// wave where a node's last container lies, the one before a range boundary for an empty
+// node there: waves [(ptr[i0] - c0) / range - 1, (ptr[i1] - c0) / range] (every storing
+// wave is in some workgroup's window) — then the workgroup goes on
+__device__ void np_wait_rows(const NpArgs& np, int64_t i0, int64_t i1, uint32_t epoch) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int64_t r = np.range;
+    int64_t wlo = (np.ptr[i0] - np.c0) / r - 1, whi = (np.ptr[i1] - np.c0) / r;
+    wlo = wlo < 0 ? 0 : wlo;
+    whi = whi > np.red_waves - 1 ? np.red_waves - 1 : whi;
+    for (int64_t b = wlo; b <= whi; b += 64) {
+      const int64_t wi = b + lane;
+      uint32_t spins = 0;
+      while (__ballot(wi <= whi && __hip_atomic_load(np.sync + NP_FLAGS + wi, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT) != epoch)) {
+        if (++spins >= NP_SPIN_MAX) {
+          if (lane == 0) atomicAdd(&np.faults[FAULT_RED], 1ull);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(20);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// 1024 rows (thread t: rows i0 + t + 256 q): node_prep's clamp-in-fit work (NC, one node
+// chunk; see node_prep_kernel): the free capacity, the slow rows, the node stream (one
+// stream position per workgroup, the rows padded to whole groups), the clamp values, and
+// the rows clamped for every spec
+__device__ void np_rows(const NpArgs& np, int32_t rb, uint32_t* scratch) {
+  constexpr int SUB = NP_ROWS_PER_WG / 256;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t n = np.n, i0 = (int64_t)rb * NP_ROWS_PER_WG;
+  // the inputs this launch does not write go out first
+  uint64_t ac[SUB];
+  int64_t am[SUB], aP[SUB], pc[SUB];
+#pragma unroll
+  for (int q = 0; q < SUB; ++q) {
+    const int64_t i = i0 + q * 256 + tid;
+    const bool valid = i < n;
+    ac[q] = valid ? np.alloc_cpu[i] : 0;
+    am[q] = valid ? np.alloc_mem[i] : 0;
+    aP[q] = valid ? np.alloc_pods[i] : 0;
+    pc[q] = valid ? np.pod_count[i] : 0;
+  }
+  const uint32_t epoch = __hip_atomic_load(np.sync + NP_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  np_wait(np.sync + NP_DONE, epoch, np.faults);  // the counters zeroed, the class counts written
+  uint64_t cls_n = 0;  // class A | class B << 32
+  {
+    const unsigned long long* bc = reinterpret_cast<const unsigned long long*>(np.bcnt);
+    for (int64_t b = lane; b < (np.S + 63) / 64; b += 64)
+      cls_n += __hip_atomic_load(bc + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cls_n = readlane_u64(wave_incl_scan_u64(cls_n), 63);
+  }
+  const bool want_b = (cls_n >> 32) != 0;
+  const int64_t nN = (int64_t)(uint32_t)cls_n + (int64_t)(cls_n >> 32);
+  const bool slow_all = nN < np.S;
+  if (!KCC_NP_NOSYNC) np_wait_rows(np, i0, i0 + NP_ROWS_PER_WG < n ? i0 + NP_ROWS_PER_WG : n, epoch);  // the rows' sums stored
+  uint64_t uc[SUB];
+  int64_t um[SUB];
+#pragma unroll
+  for (int q = 0; q < SUB; ++q) {
+    const int64_t i = i0 + q * 256 + tid;
+    const bool valid = i < n;
+    uc[q] = valid ? __hip_atomic_load(np.used_cpu + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    um[q] = valid ? __hip_atomic_load(np.used_mem + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  }
+  uint64_t r_fm[SUB];
+  uint32_t r_fc[SUB];
+  int32_t r_P[SUB], r_cl[SUB];
+  unsigned long long sbal[SUB];
+  uint64_t always_sum = 0;
+#pragma unroll
+  for (int q = 0; q < SUB; ++q) {
+    const int64_t i = i0 + q * 256 + tid;
+    const bool valid = i < n;
+    bool ok = false;
+    r_fm[q] = 0;
+    r_fc[q] = 0;
+    r_P[q] = 0;
+    r_cl[q] = 0;
+    if (valid) {
+      const uint64_t fc = ac[q] > uc[q] ? ac[q] - uc[q] : 0;                                      // CC:119-123
+      const int64_t fm = am[q] > um[q] ? (int64_t)((uint64_t)am[q] - (uint64_t)um[q]) : 0;       // CC:125-129
+      const int64_t P = aP[q];
+      const int64_t cl = (int64_t)((uint64_t)P - (uint64_t)pc[q]);                               // CC:135
+      ok = fc < FAST_FC_MAX && fm >= 0 && fm < FAST_FM_MAX && P >= -FAST_P_ABS && P <= FAST_P_ABS &&
+           cl >= -FAST_CL_ABS && cl <= FAST_CL_ABS;
+      if (ok) {
+        r_fm[q] = (uint64_t)fm;
+        r_fc[q] = (uint32_t)fc;
+        r_P[q] = (int32_t)P;
+        r_cl[q] = (int32_t)cl;
+        if (nN > 0 && P <= 0) always_sum += (uint64_t)(0 - cl);  // x >= P for every spec: w = Penc - cl
+      }
+      if (slow_all || !ok) {
+        SlowNode sn;
+        sn.fc = fc;
+        sn.fm = fm;
+        sn.P = P;
+        sn.cl = cl;
+        np.slow[i] = sn;
+      }
+    }
+    const unsigned long long bl = __ballot(valid && !ok);
+    if (bl) {
+      unsigned long long base = 0;
+      if (lane == 0) base = atomicAdd(&np.counters[CNT_SLOW_ROWS], (unsigned long long)__popcll(bl));
+      base = __shfl(base, 0);
+      if (valid && !ok) np.slow_list[base + __popcll(bl & ((1ull << lane) - 1ull))] = i;
+    }
+    sbal[q] = __ballot(r_fc[q] > 0 && r_fm[q] > 0 && r_P[q] > 0);  // 0 unless ok
+  }
+  {  // rows clamped for every spec: one wave-summed add
+    uint64_t v = always_sum;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    if (lane == 0 && v) atomicAdd(&np.counters[CNT_CLAMP_ALL], (unsigned long long)v);
+  }
+  // the workgroup's stream position: one returning atomic, rows padded to whole groups
+  uint32_t* np_wc = scratch;                                       // [4]
+  unsigned long long* np_base = reinterpret_cast<unsigned long long*>(scratch + 8);
+  uint32_t wave_streamed = 0;
+#pragma unroll
+  for (int q = 0; q < SUB; ++q) wave_streamed += (uint32_t)__popcll(sbal[q]);
+  if (lane == 0) np_wc[wv] = wave_streamed;
+  __syncthreads();
+  const uint32_t tot = np_wc[0] + np_wc[1] + np_wc[2] + np_wc[3];
+  if (tid == 0) {
+    const uint32_t padded = (tot + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP;
+    *np_base = padded ? atomicAdd(&np.counters[CNT_STREAM], (unsigned long long)padded) : 0ull;
+  }
+  __syncthreads();
+  uint32_t before = 0;
+  for (int u = 0; u < wv; ++u) before += np_wc[u];
+  const uint64_t base = *np_base;
+  auto put = [&](uint64_t pos, uint64_t fmv, uint32_t fcv, uint32_t Pv, int32_t clv) {
+    const int kk = (int)(pos % FIT_GROUP);
+    np.fast_cl[pos] = clv;
+    FitGroupA& g = np.fast_a[pos / FIT_GROUP];
+    g.fm[kk] = fmv;
+    g.fc[kk] = fcv;
+    g.P[kk] = Pv;
+    if (want_b) {
+      FitGroup& gb = np.fast_b[pos / FIT_GROUP];
+      gb.fc[kk] = (double)fcv;             // exact
+      gb.fm[kk] = (double)fmv;             // exact (< 2^50)
+      gb.Pb[kk] = FIT_BIAS + (double)Pv;   // exact (P <= 2^20)
+    }
+  };
+  uint32_t done = 0;
+#pragma unroll
+  for (int q = 0; q < SUB; ++q) {
+    if ((sbal[q] >> lane) & 1ull)
+      put(base + before + done + (uint32_t)__popcll(sbal[q] & ((1ull << lane) - 1ull)), r_fm[q], r_fc[q],
+          (uint32_t)r_P[q], r_cl[q]);
+    done += (uint32_t)__popcll(sbal[q]);
+  }
+  const uint32_t pad = (tot + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP - tot;
+  if ((uint32_t)tid < pad) put(base + tot + tid, 0ull, 0u, 0u, 0);  // the last group's padding
+}
+
+__device__ void np_body(const NpArgs& np, int32_t j, uint32_t* scratch) {
+  if (j < np.n_place) {  // spec_place, after the class counts
+    np_wait(np.sync + NP_DONE,
+            __hip_atomic_load(np.sync + NP_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u, np.faults);
+    spec_place_body(np.pa, j);
+  } else {
+    np_rows(np, j - np.n_place, scratch);
+  }
+  // the last node-prep workgroup to finish publishes the epoch: every storing reduce wave
+  // (each in some row workgroup's window), the rank workgroup and every node-prep workgroup
+  // have read it by then
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t total = (uint32_t)(np.n_place + np.n_rows);
+    if (__hip_atomic_fetch_add(np.sync + NP_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1u) {
+      const uint32_t e = __hip_atomic_load(np.sync + NP_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(np.sync + NP_ARRIVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(np.sync + NP_EPOCH, e + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 constexpr int64_t CLASS_A_M_MIN = 1ll << 18;    // class A: spec mem >= 2^18, so fm/m < 2^32
 
 __device__ __forceinline__ int32_t spec_class(uint64_t c, int64_t m) {
@@ -1441,7 +1686,11 @@ __device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds) {
     // writes what spec_place and node_prep read of the ranks' output — the class counts
     // of every 64-spec block (bcnt) — from the classes of the S <= CLAMP_LDS_SPECS specs
     // (wave w: blocks w, w + 4, ...; one ballot per block)
-    if (tid < CNT_N && tid != CNT_SPECS_A && tid != CNT_SPECS_B) ra.counters[tid] = 0;
+    const bool wt = ra.done_flag != nullptr;  // node prep in this launch: write through
+    if (tid < CNT_N && tid != CNT_SPECS_A && tid != CNT_SPECS_B) {
+      if (wt) __hip_atomic_store(ra.counters + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else ra.counters[tid] = 0;
+    }
     const int lane = tid & 63;
     const int64_t nqb = (ra.S + 63) / 64;
     int32_t cls[CLAMP_LDS_SPECS / 256];
@@ -1456,9 +1705,22 @@ __device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds) {
       const uint32_t na = (uint32_t)__popcll(__ballot(cls[u] == SPEC_A));
       const uint32_t nb = (uint32_t)__popcll(__ballot(cls[u] == SPEC_B));
       if (qb < nqb && lane == 0) {
-        ra.bcnt[2 * qb] = na;
-        ra.bcnt[2 * qb + 1] = nb;
+        if (wt) {
+          __hip_atomic_store(ra.bcnt + 2 * qb, na, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(ra.bcnt + 2 * qb + 1, nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          ra.bcnt[2 * qb] = na;
+          ra.bcnt[2 * qb + 1] = nb;
+        }
       }
+    }
+    if (wt) {  // every wave's stores performed, then the flag
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_store(ra.done_flag + NP_DONE,
+                           __hip_atomic_load(ra.done_flag + NP_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
   }
@@ -1505,9 +1767,11 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   // class totals and this block's prefix: the wave's lanes take every 64th block (the
   // counts packed A | B << 32), then one DPP scan each
   uint64_t tot = 0, pre = 0;
-  const uint64_t* bc = reinterpret_cast<const uint64_t*>(cw.bcnt);
+  // (agent-scope loads: with node prep in the reduce launch, the rank workgroup wrote them
+  // through in the same launch, possibly on another XCD)
+  const unsigned long long* bc = reinterpret_cast<const unsigned long long*>(cw.bcnt);
   for (int64_t b = lane; b < nqb; b += 64) {
-    const uint64_t v = bc[b];
+    const uint64_t v = __hip_atomic_load(bc + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     tot += v;
     pre += b < qb ? v : 0ull;
   }
@@ -2496,8 +2760,8 @@ int64_t reduce_resident_waves(bool limits) {
   static std::atomic<int64_t> cache[2][MAX_DEVS];
   int64_t r = RED_WAVES_PER_BLOCK *
               resident_blocks(cache[limits ? 1 : 0],
-                              limits ? reinterpret_cast<const void*>(reduce_kernel<4>)
-                                     : reinterpret_cast<const void*>(reduce_kernel<2>),
+                              limits ? reinterpret_cast<const void*>(reduce_kernel<4, false>)
+                                     : reinterpret_cast<const void*>(reduce_kernel<2, false>),
                               256, 0, 2048);
   return r;
 }
@@ -2523,9 +2787,12 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
                          const uint64_t* cpu_lim, const int64_t* mem_lim,
                          uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem,
                          uint64_t* tail, unsigned long long* faults, hipStream_t s,
-                         const RankArgs* rank) {
+                         const RankArgs* rank, const NpArgs* npa) {
   RankArgs ra{};
   if (rank) ra = *rank;
+  NpArgs np{};
+  if (npa) np = *npa;
+  const int32_t npb = np.n_place + np.n_rows;
   const bool limits = cpu_lim && mem_lim && lim_cpu && lim_mem;
   const bool red = n_nodes > 0 && n_containers > 0;
   if (n_nodes >= RED_MAX_NODES) return hipErrorInvalidValue;
@@ -2538,8 +2805,9 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
                    (e = hipMemsetAsync(lim_mem, 0, 8 * (size_t)n_nodes, s)) != hipSuccess))
       return e;
   }
-  if (!red && ra.n_blocks == 0) return hipSuccess;
-  if (limits && ra.n_blocks > 0) return hipErrorInvalidValue;  // (the ranks ride NA = 2 only)
+  if (!red && ra.n_blocks == 0 && npb == 0) return hipSuccess;
+  if (limits && (ra.n_blocks > 0 || npb > 0)) return hipErrorInvalidValue;  // (NA = 2 only)
+  if (npb > 0 && (ra.n_blocks != 1 || !ra.zero_only || !ra.done_flag)) return hipErrorInvalidValue;
   // the rank workgroups: behind the reduce's on long reduces, so they take the slots of
   // its first waves to finish; in front on short ones, where the reduce's range is sized
   // for the slots they leave (one round of workgroups: a reduce workgroup that waited for
@@ -2549,8 +2817,12 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
   const int32_t range = red ? reduce_range(n_containers, limits, reserve) : RED_TILE;
   const int64_t waves = red ? (n_containers + range - 1) / range : 0;
   if (waves > reduce_tail_records()) return hipErrorInvalidValue;
-  const unsigned blocks =
-      (unsigned)((waves + RED_WAVES_PER_BLOCK - 1) / RED_WAVES_PER_BLOCK + ra.n_blocks);
+  const int64_t red_blocks = (waves + RED_WAVES_PER_BLOCK - 1) / RED_WAVES_PER_BLOCK;
+  const unsigned blocks = (unsigned)(red_blocks + ra.n_blocks + npb);
+  np.ptr = node_ptr;
+  np.c0 = c0;
+  np.range = range;
+  np.red_waves = (int32_t)waves;
   RedArgs a{};
   a.n_nodes = n_nodes;
   a.c0 = c0;
@@ -2569,9 +2841,11 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
   a.faults = faults;
   a.ranks_last = ranks_last ? 1 : 0;
   if (limits)
-    hipLaunchKernelGGL(reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, a, ra);
+    hipLaunchKernelGGL((reduce_kernel<4, false>), dim3(blocks), dim3(256), 0, s, a, ra, np);
+  else if (npb > 0)
+    hipLaunchKernelGGL((reduce_kernel<2, true>), dim3(blocks), dim3(256), 0, s, a, ra, np);
   else
-    hipLaunchKernelGGL(reduce_kernel<2>, dim3(blocks), dim3(256), 0, s, a, ra);
+    hipLaunchKernelGGL((reduce_kernel<2, false>), dim3(blocks), dim3(256), 0, s, a, ra, np);
   return hipGetLastError();
 }
 
