@@ -2573,7 +2573,8 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
       }
       claim_publish((k + 1u) & 1u);
       {  // priority 3, 2, 1, 0 through the quarters of the share (round 5 A/B: boosted
-         // through the static first claim only, or then 1 / 0 by halves: slower / equal)
+         // through the static first claim only, or then 1 / 0 by halves: slower / equal;
+         // 3 only until the loop starts, then 2, 2, 1, 0 or 2, 1, 0, 0: equal / slower)
         pr_done += (uint32_t)cnt;
         const uint32_t lv = (4u * pr_done) / pr_share;
         if (lv == 0) __builtin_amdgcn_s_setprio(3);
