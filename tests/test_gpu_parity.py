@@ -547,3 +547,55 @@ def test_reduce_lookback_never_timed_out(engine):
     """Every reduce launch of this session assembled its range-cut nodes from the pieces
     the other waves published (decoupled look-back): no wait gave up."""
     assert engine.reduce_faults() == 0
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_node_prep_in_reduce_range_boundaries(engine, seed):
+    """Node prep inside the reduce launch (clamp in the fit, one node chunk: kcc::NpArgs)
+    waits for the flags of the reduce waves storing its rows.  CSR offsets built against
+    that window: empty nodes at every multiple of 512 containers (every possible range
+    boundary), leading and trailing empty nodes, one node spanning ~300k containers (many
+    ranges), the rest cut at random.  Three calls in a row (the epoch advances): node sums
+    and totals == the oracle."""
+    import torch
+    n = 20_000
+    c = synth.make_cluster(n, 2_000_000, seed=seed, chunk=1024)
+    total = int(c.node_ptr[-1])
+    rng = np.random.default_rng(seed)
+    mult = np.arange(512, total, 512)
+    giant0 = total // 3
+    mult = mult[(mult < giant0) | (mult > giant0 + 300_000)]
+    fixed = np.concatenate([np.zeros(3, np.int64), np.repeat(mult, 2), np.full(3, total, np.int64)])
+    assert fixed.size < n - 100
+    free = rng.integers(0, total, n - 1 - fixed.size)
+    free = free[(free < giant0) | (free > giant0 + 300_000)]
+    free = np.concatenate([free, rng.integers(0, giant0, n - 1 - fixed.size - free.size)])
+    ptr = np.concatenate([[0], np.sort(np.concatenate([fixed, free]))[: n - 1], [total]]).astype(np.int64)
+    assert ptr.size == n + 1 and np.all(np.diff(ptr) >= 0)
+    sc, sm = synth.make_specs(700, seed=seed)
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)  # noqa: E731
+    uc, um, _, _ = coracle.reduce_requests(ptr, c.cpu_req, c.mem_req, c.cpu_lim, c.mem_lim)
+    ot, oe = coracle.fit(c.alloc_cpu, c.alloc_mem, c.alloc_pods, c.pod_count, uc, um, sc, sm, NT)
+    used_cpu = torch.empty(n, dtype=torch.int64, device=dev)
+    used_mem = torch.empty(n, dtype=torch.int64, device=dev)
+    totals = torch.empty(sc.size, dtype=torch.int64, device=dev)
+    err = torch.empty(sc.size, dtype=torch.int32, device=dev)
+    args = (T(ptr), T(c.cpu_req), T(c.mem_req), T(c.alloc_cpu), T(c.alloc_mem),
+            T(c.alloc_pods), T(c.pod_count), used_cpu, used_mem, T(sc), T(sm))
+    stream = torch.cuda.Stream(dev)
+    engine.set_clamp_in_fit(1)
+    try:
+        for k in range(3):
+            totals.fill_(-7)
+            used_cpu.fill_(-7)
+            with torch.cuda.stream(stream):
+                engine.capacity_async(ptr, *args, totals, err, stream=stream)
+            stream.synchronize()
+            np.testing.assert_array_equal(used_cpu.cpu().numpy().view(np.uint64), uc, err_msg=f"call {k}")
+            np.testing.assert_array_equal(used_mem.cpu().numpy(), um, err_msg=f"call {k}")
+            np.testing.assert_array_equal(totals.cpu().numpy(), ot, err_msg=f"call {k}")
+            np.testing.assert_array_equal(err.cpu().numpy(), oe, err_msg=f"call {k}")
+    finally:
+        engine.set_clamp_in_fit(-1)
+    assert engine.reduce_faults() == 0  # no wait gave up
