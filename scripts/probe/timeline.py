@@ -69,7 +69,8 @@ t = buf.astype(np.float64)
 if a.dump:
     np.save(a.dump, buf)
 npr = t[0:1024]
-t0 = npr[:, 2][npr[:, 2] > 0].min()
+# t0: node_prep's first entry, or (node prep inside the reduce launch) the reduce's first
+t0 = npr[:, 2][npr[:, 2] > 0].min() if (npr[:, 2] > 0).any() else t[4096:8192, 0][t[4096:8192, 0] > 0].min()
 us = lambda x: (x - t0) / 100.0  # noqa: E731
 print(f"config {a.config} shard 1/{a.shard}: {n} nodes, {S} specs")
 
