@@ -672,6 +672,7 @@ __device__ void np_rows(const NpArgs& np, int32_t rb, uint32_t* scratch) {
   constexpr int SUB = NP_ROWS_PER_WG / 256;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t n = np.n, i0 = (int64_t)rb * NP_ROWS_PER_WG;
+  KCC_TL(rb % 1024, 2);
   // the inputs this launch does not write go out first
   uint64_t ac[SUB];
   int64_t am[SUB], aP[SUB], pc[SUB];
@@ -686,6 +687,7 @@ __device__ void np_rows(const NpArgs& np, int32_t rb, uint32_t* scratch) {
   }
   const uint32_t epoch = __hip_atomic_load(np.sync + NP_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   np_wait(np.sync + NP_DONE, epoch, np.faults);  // the counters zeroed, the class counts written
+  KCC_TL(rb % 1024, 6);
   uint64_t cls_n = 0;  // class A | class B << 32
   {
     const unsigned long long* bc = reinterpret_cast<const unsigned long long*>(np.bcnt);
@@ -697,6 +699,7 @@ __device__ void np_rows(const NpArgs& np, int32_t rb, uint32_t* scratch) {
   const int64_t nN = (int64_t)(uint32_t)cls_n + (int64_t)(cls_n >> 32);
   const bool slow_all = nN < np.S;
   if (!KCC_NP_NOSYNC) np_wait_rows(np, i0, i0 + NP_ROWS_PER_WG < n ? i0 + NP_ROWS_PER_WG : n, epoch);  // the rows' sums stored
+  KCC_TL(rb % 1024, 3);
   uint64_t uc[SUB];
   int64_t um[SUB];
 #pragma unroll
@@ -752,7 +755,8 @@ __device__ void np_rows(const NpArgs& np, int32_t rb, uint32_t* scratch) {
     }
     sbal[q] = __ballot(r_fc[q] > 0 && r_fm[q] > 0 && r_P[q] > 0);  // 0 unless ok
   }
-  {  // rows clamped for every spec: one wave-summed add
+  KCC_TL(rb % 1024, 4);
+  {  // rows clamped for every spec: one wave-summed add (one per workgroup: equal, round 5)
     uint64_t v = always_sum;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
@@ -772,6 +776,7 @@ __device__ void np_rows(const NpArgs& np, int32_t rb, uint32_t* scratch) {
     *np_base = padded ? atomicAdd(&np.counters[CNT_STREAM], (unsigned long long)padded) : 0ull;
   }
   __syncthreads();
+  KCC_TL(rb % 1024, 5);
   uint32_t before = 0;
   for (int u = 0; u < wv; ++u) before += np_wc[u];
   const uint64_t base = *np_base;
@@ -799,6 +804,7 @@ __device__ void np_rows(const NpArgs& np, int32_t rb, uint32_t* scratch) {
   }
   const uint32_t pad = (tot + FIT_GROUP - 1) / FIT_GROUP * FIT_GROUP - tot;
   if ((uint32_t)tid < pad) put(base + tot + tid, 0ull, 0u, 0u, 0);  // the last group's padding
+  KCC_TL(rb % 1024, 1);
 }
 
 __device__ void np_body(const NpArgs& np, int32_t j, uint32_t* scratch) {

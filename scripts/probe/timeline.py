@@ -86,6 +86,15 @@ def show(label, rows, k0, k1):
           f"  dur min/med/max {d.min():6.2f}/{np.median(d):6.2f}/{d.max():6.2f}")
 
 
+if not (npr[:, 0] > 0).any():  # node prep inside the reduce launch (np_rows stamps)
+    show("np_rows entry -> ranks' flag", npr, 2, 6)
+    show("np_rows flag -> rows' waves done", npr, 6, 3)
+    show("np_rows waves -> rows computed", npr, 3, 4)
+    show("np_rows computed -> stream position", npr, 4, 5)
+    show("np_rows position -> stream written", npr, 5, 1)
+    show("np_rows whole", npr, 2, 1)
+    rr = t[4096:8192]
+    show("reduce workgroups (wave 0)", rr, 0, 1)
 show("node_prep entry -> prologue done", npr, 2, 0)
 show("  entry -> table loads in LDS", npr, 2, 6)
 show("  member masks (LDS atomics)", npr, 6, 7)
