@@ -10,11 +10,11 @@ mkdir -p gpurun_out
 [ "${SKIP_TESTS:-0}" = 1 ] || timeout -k 10 700 python -u -m pytest tests/test_gpu_shards_configs.py tests/test_gpu_parity.py tests/test_faults_graphs.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1 || { tail -20 gpurun_out/pytest_$TAG.log; exit 1; }
 [ "${SKIP_TESTS:-0}" = 1 ] || tail -2 gpurun_out/pytest_$TAG.log
 timeout -k 10 400 python3 -u scripts/ab_variants.py run --step --config C4 --shard 8 --rounds 7 --reps 20 \
-  base sk10 sk20 sk30 > gpurun_out/ab_${TAG}_step_s8.txt 2>&1 || exit $?
+  base ffin > gpurun_out/ab_${TAG}_step_s8.txt 2>&1 || exit $?
 grep '^{' gpurun_out/ab_${TAG}_step_s8.txt
 timeout -k 10 300 python3 -u scripts/ab_variants.py run --step --config C4 --shard 4 --rounds 7 --reps 20 \
-  base sk10 sk20 sk30 > gpurun_out/ab_${TAG}_step_s4.txt 2>&1 || exit $?
+  base ffin > gpurun_out/ab_${TAG}_step_s4.txt 2>&1 || exit $?
 grep '^{' gpurun_out/ab_${TAG}_step_s4.txt
 timeout -k 10 300 python3 -u scripts/ab_variants.py run --step --config C4 --shard 1 --rounds 5 --reps 10 \
-  base sk10 sk20 sk30 > gpurun_out/ab_${TAG}_step_s1.txt 2>&1 || exit $?
+  base ffin > gpurun_out/ab_${TAG}_step_s1.txt 2>&1 || exit $?
 grep '^{' gpurun_out/ab_${TAG}_step_s1.txt
