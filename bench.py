@@ -95,6 +95,9 @@ def parse():
                     help="skip the list-order (keyed) reduce leg (SURVEY §8f row 1)")
     ap.add_argument("--no-parse", action="store_true",
                     help="skip the quantity-string parse leg (SURVEY §8f row 2)")
+    ap.add_argument("--no-cold", action="store_true",
+                    help="skip the cold-cache steps (a 1 GiB read between steps evicts the "
+                         "256 MiB Infinity Cache and the L2s; roofline.frac_cold)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU time of the oracle's fit sample")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -435,6 +438,7 @@ def main():
             torch.cuda.synchronize()
     red_ms_tot, red_launches, fit_ms_tot, fit_launches = eng.profile_read()
     eng.profile_enable(False)
+    cold = None if args.no_cold else cold_leg(eng, step, stream, dev, args.steps, dist, world)
     ar_ms = (sum(a.elapsed_time(b) for a, b in ar_events) / len(ar_events)) if ar_events else None
     elapsed = t_end - t_start
     own_ms_step = elapsed / args.steps * 1e3  # this rank's own timed steps
@@ -564,6 +568,15 @@ def main():
         "fast_path_fraction": 1.0 - (slow_pairs / pairs if pairs else 0.0),
         "gen_seconds": gen_s,
     }
+    if cold is not None:  # the same kernels with the Infinity Cache and L2s flushed
+        c_red = cold["reduce_ms_per_launch"]
+        c_fit = cold["fit_ms_per_launch"]
+        out["roofline_reduce"].update(
+            ms_per_launch_cold=c_red, achieved_cold=red_bytes / (c_red * 1e-3) / 1e9,
+            frac_cold=red_bytes / (c_red * 1e-3) / 1e9 / HBM_PEAK_GBS)
+        out["roofline_valu"].update(
+            ms_per_launch_cold=c_fit, frac_cold=fit_instr / chunks / (c_fit * 1e-3) / VALU_ISSUE_PEAK)
+        out["cold"] = cold
     if red_ms_tot >= fit_ms_tot:
         out["roofline"] = dict(out["roofline_reduce"], kernel="reduce_kernel<2>",
                                note="dominant kernel of the step (reduce vs fit time per step); "
@@ -656,6 +669,55 @@ def main():
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+COLD_FLUSH_BYTES = 1 << 30  # 4x the 256 MiB Infinity Cache (MI355X_MICROARCH.md)
+
+
+def cold_leg(eng, step, stream, dev, steps, dist, world):
+    """SURVEY §7 (HBM claims need a cold cache): `steps` more steps, each behind a streamed
+    read of a COLD_FLUSH_BYTES scratch buffer on the step's own stream, which evicts the
+    256 MiB Infinity Cache (MI355X_MICROARCH.md: a line stays resident only while
+    everything loaded or stored between two uses fits in ~256 MiB) and every XCD's 4 MiB
+    L2, so each step's inputs come from HBM.  A read, not a write: a written flush leaves
+    up to 256 MiB of DIRTY lines that the step itself must then write back (measured: the
+    C4 reduce 0.134 -> 0.181 ms, i.e. its 657 MB plus ~256 MB of the flush's write-back);
+    the read leaves clean lines, and the previous step's own writes are written back during
+    the flush, outside the timed pair.  Timed: each step alone, by HIP events on its stream
+    after the flush, and its reduce / fit launches by the library's per-kernel events
+    (kcc_profile_*).  Not part of `value` (the timed steps are warm, back to back)."""
+    import torch
+
+    scratch = torch.zeros(COLD_FLUSH_BYTES // 8, dtype=torch.int64, device=dev)
+    sink = torch.empty((), dtype=torch.int64, device=dev)
+    evs = []
+    eng.profile_enable(True)
+    with torch.cuda.stream(stream):
+        for i in range(steps):
+            torch.sum(scratch, out=sink)  # the flush: a streamed read on the step's stream
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(stream)
+            step()
+            ev[1].record(stream)
+            evs.append(ev)
+        torch.cuda.synchronize()
+    red_ms, red_n, fit_ms, fit_n = eng.profile_read()
+    eng.profile_enable(False)
+    del scratch, sink
+    step_ms = sorted(a.elapsed_time(b) for a, b in evs)
+    med = step_ms[len(step_ms) // 2]
+    if world > 1:
+        dist.barrier()
+    return {
+        "ms_per_step_median": med, "ms_per_step_min": step_ms[0],
+        "reduce_ms_per_launch": red_ms / max(red_n, 1),
+        "fit_ms_per_launch": fit_ms / max(fit_n, 1), "steps": steps,
+        "flush": f"{COLD_FLUSH_BYTES >> 20} MiB streamed read (torch.sum) on the step's "
+                 "stream before each step: evicts the 256 MiB Infinity Cache and the L2s, "
+                 "leaving clean lines",
+        "note": "each step timed alone by HIP events on its stream (the flush outside the "
+                "pair); per-kernel times from the library's events around each launch",
+    }
 
 
 def side_warmup(run, warmup, min_s=0.1):

@@ -50,7 +50,9 @@
 extern "C" {
 #endif
 
-#define KCC_ABI_VERSION 1
+/* 2 (round 5): kcc_fit_mskip_groups removed; partial[S..2S) carries the device fault mark
+ * (a count >= 2^48, see kcc_fit_partial_async).  1: the first release. */
+#define KCC_ABI_VERSION 2
 
 enum {
   KCC_OK = 0,
@@ -87,6 +89,12 @@ void kcc_destroy(kcc_ctx* ctx);
 const char* kcc_last_error(const kcc_ctx* ctx);
 /* Thread-local message of the last failed kcc_create (ctx did not exist yet). */
 const char* kcc_create_error(void);
+
+/* In-library all-reduce check (contexts of n_gpus > 1, host-array entry points): the
+ * context's FIRST all-reduce is verified against the host's sum of the devices' partials
+ * (KCC_ERCCL on a mismatch); later calls are not, unless every_call != 0 (then every call
+ * pays two device-to-host copies and stream syncs per device).  Default 0. */
+int kcc_set_allreduce_verify(kcc_ctx* ctx, int every_call);
 
 /* Pre-size the device workspace used by the *_async entry points (device 0 of ctx). */
 int kcc_reserve(kcc_ctx* ctx, int64_t max_nodes, int64_t max_containers, int64_t max_specs);
@@ -149,9 +157,11 @@ int kcc_capacity(kcc_ctx* ctx, int64_t n_nodes, int64_t n_containers,
 
 /* Device-level fit, split so that a node-sharded caller can all-reduce in between:
  *   kcc_fit_partial_async: partial[0..S)  = wrapping Σ over this call's nodes of q(i,s)
- *                          partial[S..2S) = number of divide-by-zero rows, + 2^48 per
- *                          launch on a faulted device (the fault mark: >= 2^48 after
- *                          any sum means a faulted shard; finalize -> KCC_SPEC_FAULT)
+ *                          partial[S..2S) = number of divide-by-zero rows (< 2^48), or
+ *                          on a faulted device that count plus one or more fault marks
+ *                          of 2^48 (a count >= 2^48 after any sum over shards means a
+ *                          faulted shard; a host-side finalize must test it BEFORE
+ *                          count > 0 -> DIVZERO; kcc_fit_finalize -> KCC_SPEC_FAULT)
  *                          (both in an internal spec order; zeroed by this call)
  *   <optional all-reduce(sum, int64) of partial[0..2S) over node shards>
  *   kcc_fit_finalize_async: totals[s], spec_err[s] in caller order.

@@ -34,6 +34,7 @@ _i64, _i32, _int, _vp, _dbl = C.c_int64, C.c_int32, C.c_int, C.c_void_p, C.c_dou
 # symbol -> (restype, argtypes); pointers are passed as c_void_p
 SIGNATURES = {
     "kcc_abi_version": (_int, []),
+    "kcc_set_allreduce_verify": (_int, [_vp, _int]),
     "kcc_build_info": (C.c_char_p, []),
     "kcc_create": (_int, [C.POINTER(_vp), _int, _int]),
     "kcc_destroy": (None, [_vp]),

@@ -141,6 +141,7 @@ struct kcc_ctx {
   // the in-library all-reduce (comms) has been checked against a host-side sum of the
   // devices' partials (the first host-array call of the context does it)
   bool allreduce_verified = false;
+  bool allreduce_verify_every = false;  // kcc_set_allreduce_verify(ctx, 1)
 };
 
 namespace {
@@ -302,6 +303,9 @@ int reserve_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont, int64_t 
     const size_t bytes = 4 * (kcc::NP_FLAGS + (size_t)kcc::reduce_tail_records());
     KCC_HIP(ctx, ensure(dv.np_sync, bytes));
     KCC_HIP(ctx, hipMemsetAsync(dv.np_sync.p, 0, bytes, dv.stream));
+    // the fused reduce runs on the caller's stream, which nothing orders after dv.stream:
+    // the zeroing completes here, on its own
+    KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
   }
   if (!dv.clamp_arrive.p) {  // the fused finalize's arrivals: every launch leaves them zero
     KCC_HIP(ctx, ensure(dv.clamp_arrive, 64));
@@ -819,8 +823,10 @@ int run_host(kcc_ctx* ctx, bool with_reduce, int64_t n_nodes, int64_t n_cont,
   if (!ctx->comms.empty()) {
     // the context's first all-reduce proves itself (as bench.py's exchange does before it
     // is timed): every device's result must equal the host's wrapping sum of the devices'
-    // partials (CC:138 summed over devices), else KCC_ERCCL
-    const bool verify = !ctx->allreduce_verified;
+    // partials (CC:138 summed over devices), else KCC_ERCCL.  Later calls are checked only
+    // with kcc_set_allreduce_verify(ctx, 1) (two device-to-host copies and stream syncs
+    // per device and call)
+    const bool verify = !ctx->allreduce_verified || ctx->allreduce_verify_every;
     const size_t words = 2 * (size_t)n_specs;
     std::vector<uint64_t> expect, got;
     if (verify) {
@@ -901,6 +907,12 @@ int run_host(kcc_ctx* ctx, bool with_reduce, int64_t n_nodes, int64_t n_cont,
 extern "C" {
 
 int kcc_abi_version(void) { return KCC_ABI_VERSION; }
+
+int kcc_set_allreduce_verify(kcc_ctx* ctx, int every_call) {
+  if (!ctx) return KCC_EINVAL;
+  ctx->allreduce_verify_every = every_call != 0;
+  return KCC_OK;
+}
 
 // The knobs an experiment build was compiled with (csrc/Makefile `variant` passes them in
 // KCC_VARIANT_FLAGS); the release library takes none (the Makefile refuses EXTRA there).

@@ -521,7 +521,8 @@ struct KeyedWork {
 // is counting-sorted by bucket in LDS and written contiguously into its own region of sr
 // (whole lines), with the bucket starts in its table row — no global histogram pass, no
 // scan, keys read once.  kb_gather then sums bucket b's segments of every tile into LDS
-// rows.  (With limits, NA = 4: the bucketed kb_hist / kb_scan / kb_scatter / kb_accum path.)
+// rows.  The four-kernel bucketed path (kb_hist / kb_scan / kb_scatter / kb_accum) serves
+// only the calls with limits (NA = 4).
 constexpr int KB_SW_THREADS = 1024;
 constexpr int KB_SW_PER = 8;  // containers per thread (the next tile's loads in registers)
 constexpr int64_t KB_SW_TILE = (int64_t)KB_SW_THREADS * KB_SW_PER;  // 8192

@@ -1814,7 +1814,10 @@ __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk) {
   sp.rec[pos] = rec;
   sp.perm[pos] = (int32_t)i;
   partial[i] = 0;
-  // (spec_place runs after this step's reduce: its look-back give-ups are in the words)
+  // (the give-ups of this step's reduce are in the words when spec_place runs after it;
+  // on the fused path its workgroups run inside the reduce launch, and a give-up that comes
+  // later in that launch is marked by the fit's by == 0 workgroup, which adds the mark too:
+  // a faulted call's count is >= SPEC_FAULT_MARK, not an exact multiple of it)
   partial[S + i] = device_faulted(pa.faults) ? (int64_t)SPEC_FAULT_MARK : 0;
   if (!normal || pa.no_ranks) return;
   cw.dperm[x] = (int32_t)pos;

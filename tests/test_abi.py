@@ -43,7 +43,7 @@ def test_binding_arities_match_header():
 
 def test_library_loads_and_reports_version():
     lib = _lib.load()
-    assert lib.kcc_abi_version() == 1
+    assert lib.kcc_abi_version() == 2
 
 
 def test_library_is_gfx950_code():

@@ -74,3 +74,27 @@ def test_inlib_allreduce_mismatch_returns_ercc(monkeypatch):
         np.testing.assert_array_equal(got_e, e)
     finally:
         eng.close()
+
+
+def test_inlib_allreduce_verify_every_call(monkeypatch):
+    """After a verified first all-reduce, a later corrupted one goes unchecked by default
+    and is caught with kcc_set_allreduce_verify(ctx, 1)."""
+    from kubernetesclustercapacity_amd import KccError
+    from kubernetesclustercapacity_amd._lib import KCC_ERCCL
+    monkeypatch.delenv("KCC_DRILL_CORRUPT_ALLREDUCE", raising=False)
+    c, sc, sm, t, e = _cluster()
+    eng = _engine()
+    args = (c.node_ptr, c.cpu_req, c.mem_req, c.alloc_cpu, c.alloc_mem, c.alloc_pods,
+            c.pod_count, sc, sm)
+    try:
+        got_t, _ = eng.capacity(*args)  # the first call verifies
+        np.testing.assert_array_equal(got_t, t)
+        monkeypatch.setenv("KCC_DRILL_CORRUPT_ALLREDUCE", "1")
+        got_t, _ = eng.capacity(*args)  # unchecked (the documented default): wrong word 0
+        assert not np.array_equal(got_t, t)
+        assert eng._lib.kcc_set_allreduce_verify(eng._h, 1) == 0
+        with pytest.raises(KccError) as ei:
+            eng.capacity(*args)
+        assert ei.value.code == KCC_ERCCL
+    finally:
+        eng.close()

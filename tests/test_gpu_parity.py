@@ -231,11 +231,13 @@ def test_class_a_wave_boundaries(engine):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
-def test_fit_memory_skip_thresholds(engine, mode):
-    """The fit's memory-bound skip at its thresholds: node groups whose
-    V = floor(fm / P) saturates the 32-bit V_min (free memory near 2^50, P = 1..3) or sits
-    exactly on a spec's request (fm = m x P, m x P - 1), against class-A waves whose largest
-    request is 2^32 - 2, 2^32 - 1 (no skip), 2^32, 2^40 or equal to V; both clamp modes."""
+def test_fit_fast_path_bounds_near_2_32_and_2_50(engine, mode):
+    """The class-A fast path at its bounds, against the oracle: free memory just below 2^50
+    (the f64 quotient's exactness bound) with P = 1..3, free memory exactly on
+    a spec's request times P (fm = m x P and m x P - 1, the quotient on / next to an integer
+    at the pod clamp), and class-A waves whose largest memory request is 3 x 2^30,
+    2^32 - 2, 2^32 - 1, 2^32 or 2^40 (the 32-bit quotient's low dword); both
+    clamp modes."""
     rng = np.random.default_rng(77)
     tops = [3 << 30, (1 << 32) - 2, (1 << 32) - 1, 1 << 32, 1 << 40]
     waves, lo = [], 1 << 18  # wave w (memory order): 63 requests in (top[w-1], top[w]] + top[w]

@@ -245,3 +245,132 @@ def test_reduce_lookback_tagged_words(asm):
     stores = [ln.strip() for ln in body.splitlines()
               if ln.strip().startswith("global_store_dwordx2") and ln.strip().endswith("sc1")]
     assert len(stores) >= 5, stores  # one publish + the four frees
+
+
+# ---- node prep inside the reduce launch (reduce_kernel<2, true>) --------
+# Node prep's row workgroups read the reduce's per-node sums with no release / acquire: the
+# hand-off is (1) every store of a node sum (out[], the used_* arrays) at agent scope (sc1,
+# through to the shared L2 and past this CU's L1), (2) an `s_waitcnt vmcnt(0)` before the
+# wave's flag store, so the flag cannot become visible before the sums, and (3) node prep
+# reading used_* and the flags at agent scope (sc1).  The release asm carries no source
+# positions, so the checks run on the same file built with line tables (-gline-tables-only
+# does not change the instructions: pinned below) and map every instruction to its
+# kcc_kernels.hip line.
+NPM = "reduce_kernelILi2ELb1E"
+VMEM = ("global_", "buffer_", "flat_")
+
+
+def _src_lines(pattern, within=None):
+    src = open(SRC).read().splitlines()
+    lo, hi = within if within else (0, len(src))
+    if within:  # (function names -> the lines from its definition to the next top-level `}`)
+        lo = next(i for i, ln in enumerate(src) if re.search(within[0], ln))
+        hi = next(i for i in range(lo + 1, len(src)) if src[i].startswith("}"))
+    return {i + 1 for i in range(lo, hi) if re.search(pattern, src[i])}
+
+
+def _asm_with_lines(tmp_path_factory, *defines):
+    out = tmp_path_factory.mktemp("isa_g") / "kcc_g.s"
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-S",
+                    "--cuda-device-only", "-gline-tables-only", *defines, SRC, "-o", str(out)],
+                   check=True, capture_output=True)
+    return out.read_text()
+
+
+@pytest.fixture(scope="module")
+def asm_g(tmp_path_factory):
+    return _asm_with_lines(tmp_path_factory)
+
+
+def _function(asm, name):
+    m = re.search(rf"^(_ZN3kcc12_GLOBAL__N_1\d+{name}\w*):\s*;", asm, re.M)
+    assert m, name
+    return asm[m.end():asm.index(".Lfunc_end", m.end())]
+
+
+def _kernels_file_ids(asm):
+    """The .file numbers of kcc_kernels.hip in a line-table build."""
+    return {int(m.group(1)) for m in
+            re.finditer(r'^\s*\.file\s+(\d+)\s+"[^"]*"\s+"[^"]*kcc_kernels\.hip"', asm, re.M)}
+
+
+def _instrs_with_lines(body, fids=frozenset()):
+    """[(source line in kcc_kernels.hip or None, instruction text)] in program order."""
+    out, cur = [], None
+    for ln in body.splitlines():
+        s = ln.strip()
+        m = re.match(r"\.loc\s+(\d+)\s+(\d+)", s)
+        if m:
+            cur = int(m.group(2)) if int(m.group(1)) in fids else None
+            continue
+        if not s or s.startswith((";", ".", "@")) or s.endswith(":"):
+            continue
+        out.append((cur, s.split(";")[0].strip()))
+    return out
+
+
+def npm_ordering_problems(asm_g):
+    """What breaks node prep's hand-off in reduce_kernel<2, true>'s ISA (empty: none)."""
+    fids = _kernels_file_ids(asm_g)
+    assert fids, "no .file entry for kcc_kernels.hip"
+    ins = _instrs_with_lines(_function(asm_g, NPM), fids)
+    red = (r"void reduce_kernel\(", None)
+    # (1) the node sums' stores: both branches of each store site (agent-scope atomic store /
+    # plain store) and the pending block's buffer store
+    store_lines = (_src_lines(r"__hip_atomic_store\(out\[k\]|^\s*else out\[k\]\[", red) |
+                   _src_lines(r"raw_buffer_store_b64\(.*resF\[k\]", red))
+    stores = [(l, s) for l, s in ins if l in store_lines and s.startswith(VMEM) and "store" in s]
+    problems = [f"node-sum store without sc1 (line {l}): {s}" for l, s in stores
+                if not s.endswith("sc1")]
+    if len([s for _, s in stores if s.startswith("buffer_store_dwordx2")]) < 2 or \
+            len([s for _, s in stores if s.startswith("global_store_dwordx2")]) < 3:
+        problems.append(f"node-sum stores not found: {stores}")
+    # (2) the per-wave flag: an s_waitcnt vmcnt(0) after the wave's last vector memory access
+    flag_lines = _src_lines(r"__hip_atomic_store\(np\.sync \+ NP_FLAGS \+ w", red)
+    flags = [i for i, (l, s) in enumerate(ins) if l in flag_lines and s.startswith(VMEM)]
+    if not flags:
+        problems.append("flag store not found")
+    for i in flags:
+        if not ins[i][1].startswith("global_store_dword ") or not ins[i][1].endswith("sc1"):
+            problems.append(f"flag store is not a 32-bit sc1 store: {ins[i][1]}")
+        for _, s in reversed(ins[:i]):
+            if s.startswith("s_waitcnt") and "vmcnt(0)" in s:
+                break
+            if s.startswith(VMEM):
+                problems.append(f"vector memory access `{s}` between the last vmcnt(0) and "
+                                f"the flag store `{ins[i][1]}`")
+                break
+    # (3) node prep reads the sums (np_rows) and polls the flags (np_wait_rows) at agent scope
+    rows = (r"void np_rows\(", None)
+    used_lines = _src_lines(r"np\.used_(cpu|mem) \+ i", rows)
+    loads = [s for l, s in ins if l in used_lines and s.startswith(VMEM) and "load" in s]
+    if len(loads) < 2:
+        problems.append(f"np_rows' used_* loads not found: {loads}")
+    problems += [f"np_rows used_* load without sc1: {s}" for s in loads if not s.endswith("sc1")]
+    poll_lines = _src_lines(r"np\.sync \+ NP_FLAGS \+ wi", (r"void np_wait_rows\(", None))
+    polls = [s for l, s in ins if l in poll_lines and s.startswith(VMEM) and "load" in s]
+    if not polls:
+        problems.append("np_wait_rows' flag polls not found")
+    problems += [f"flag poll without sc1: {s}" for s in polls if not s.endswith("sc1")]
+    return problems
+
+
+def test_npm_line_tables_same_instructions(asm, asm_g):
+    """The line-table build used below has exactly the release instructions."""
+    strip = lambda b: [s for _, s in _instrs_with_lines(b)]  # noqa: E731
+    assert strip(_function(asm, NPM)) == strip(_function(asm_g, NPM))
+
+
+def test_npm_node_sums_hand_off(asm_g):
+    """Node prep inside the reduce launch: every node-sum store is sc1, every
+    per-wave flag store follows an s_waitcnt vmcnt(0) with no vector memory access between,
+    and node prep's used_* loads and flag polls are sc1."""
+    assert npm_ordering_problems(asm_g) == []
+
+
+def test_npm_hand_off_check_catches_plain_stores(tmp_path_factory):
+    """The check above fails on the KCC_DIAG_NP_NOSC1 diagnostic build (node sums stored
+    plainly): it reads the ISA, not the source."""
+    bad = _asm_with_lines(tmp_path_factory, "-DKCC_VARIANT_BUILD", "-DKCC_DIAG_NP_NOSC1")
+    problems = npm_ordering_problems(bad)
+    assert any("node-sum store without sc1" in p for p in problems), problems
