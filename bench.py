@@ -694,7 +694,7 @@ def cold_leg(eng, step, stream, dev, steps, dist, world):
     eng.profile_enable(True)
     with torch.cuda.stream(stream):
         for i in range(steps):
-            torch.sum(scratch, out=sink)  # the flush: a streamed read on the step's stream
+            torch.sum(scratch, dim=0, out=sink)  # the flush: a streamed read on the step's stream
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record(stream)
             step()

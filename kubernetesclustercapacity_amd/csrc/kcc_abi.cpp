@@ -1612,14 +1612,18 @@ int keyed_work(kcc_ctx* ctx, Dev& dv, int64_t n_keys, int64_t n, int na, kcc::Ke
                const kcc::KeyedWork** out) {
   *out = nullptr;
   if (!kcc::keyed_bucketed(n_keys, n)) return KCC_OK;
+  {
+    int rc = faults_ws(ctx, dv, dv.stream);  // (the gather's bounded wait reports here)
+    if (rc) return rc;
+  }
   const size_t nb = (size_t)kcc::keyed_buckets(n_keys);
   const size_t m = (size_t)(n > 0 ? n : 1);
   KCC_HIP(ctx, ensure(dv.kb_counts, 4 * (size_t)kcc::keyed_counts_words(n_keys, n)));
   KCC_HIP(ctx, ensure(dv.kb_tot, 4 * nb));
   KCC_HIP(ctx, ensure(dv.kb_sr, 8 * (size_t)kcc::keyed_sr_slots(n)));
   KCC_HIP(ctx, ensure(dv.kb_part, 8 * (size_t)kcc::keyed_part_words(n_keys, na > 2 ? 2 : na)));
-  if (dv.kb_arrive.bytes < 4 * nb) {  // every gather leaves them zero
-    KCC_HIP(ctx, ensure(dv.kb_arrive, 4 * nb));
+  if (dv.kb_arrive.bytes < 8 * nb) {  // [arrivals | published parts]: every gather leaves them zero
+    KCC_HIP(ctx, ensure(dv.kb_arrive, 8 * nb));
     KCC_HIP(ctx, hipMemsetAsync(dv.kb_arrive.p, 0, dv.kb_arrive.bytes, dv.stream));
     KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
   }
@@ -1645,6 +1649,7 @@ int keyed_work(kcc_ctx* ctx, Dev& dv, int64_t n_keys, int64_t n, int na, kcc::Ke
   kw.esc_mem = na >= 2 ? as<uint64_t>(dv.kb_esc_mem) : nullptr;
   kw.part_acc = as<uint64_t>(dv.kb_part);
   kw.arrive = as<uint32_t>(dv.kb_arrive);
+  kw.faults = as<unsigned long long>(dv.faults);
   *out = &kw;
   return KCC_OK;
 }
@@ -1737,7 +1742,7 @@ int kcc_reduce_requests_keyed(kcc_ctx* ctx, int64_t n_keys, int64_t n_containers
                                 hipMemcpyDeviceToHost, dv.stream));
   }
   KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
-  return KCC_OK;
+  return check_faults(ctx);
 }
 
 int kcc_count_by_key_async(kcc_ctx* ctx, int64_t n_keys, int64_t n, const int32_t* d_key,
@@ -1775,7 +1780,7 @@ int kcc_count_by_key(kcc_ctx* ctx, int64_t n_keys, int64_t n, const int32_t* key
   KCC_HIP(ctx, hipMemcpyAsync(count, dv.pod_count.p, 8 * (size_t)n_keys, hipMemcpyDeviceToHost,
                               dv.stream));
   KCC_HIP(ctx, hipStreamSynchronize(dv.stream));
-  return KCC_OK;
+  return check_faults(ctx);
 }
 
 }  // extern "C"

@@ -511,11 +511,13 @@ struct KeyedWork {
   int32_t* esc_row;   // [n]   bits; memory not a multiple of 64 in [0, 2^38): all of it)
   uint64_t* esc_cpu;  // [n]
   uint64_t* esc_mem;  // [n]
-  // one-sweep path (kb_sweep + kb_gather): a bucket's records are gathered by
-  // keyed_sweep_parts(nb) workgroups; parts > 1 sum through part_acc, the last part to
-  // arrive (arrive[b], zero between calls) adds the others' rows and writes the bucket
-  uint64_t* part_acc; // [nb][parts][NACC][KB_ROWS]
-  uint32_t* arrive;   // [nb]
+  // one-sweep path (kb_sweep + kb_gather): a bucket group's records are gathered by
+  // keyed_sweep_parts(nb) workgroups; parts > 1 sum through part_acc: every part but the
+  // last to arrive (arrive[b]) publishes its rows and counts itself (arrive[groups + b]),
+  // the last adds them and writes the group's outputs
+  uint64_t* part_acc; // [groups][parts][NACC][KB_GA_ROWS]
+  uint32_t* arrive;   // [2 x groups]: arrivals, then the published parts (zero between calls)
+  unsigned long long* faults;  // the device's fault words (a gather wait that gave up)
 };
 // One-sweep keyed reduce (NA = 0 counts, 2 requests): each tile of KB_SW_TILE containers
 // is counting-sorted by bucket in LDS and written contiguously into its own region of sr

@@ -153,6 +153,26 @@ __device__ __forceinline__ int32_t rel_ptr(const int64_t* __restrict__ ptr, int6
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
+// One tile's registers instead of a two-tile ring: the next tile's loads go out as soon as
+// this tile's items are in the LDS strip (before its node walk), so the tile loop needs 32
+// fewer VGPRs
+#ifndef KCC_RED_LATE
+#define KCC_RED_LATE 0
+#endif
+constexpr bool RED_LATE = KCC_RED_LATE != 0;
+// Per-item prefixes from in-lane running sums (adds: one v_lshl_add_u64 each) and the lane's
+// exclusive base, instead of walking back from the lane's inclusive prefix (64-bit
+// subtracts: v_sub_co + v_subb each)
+#ifndef KCC_RED_FWD
+#define KCC_RED_FWD 0
+#endif
+constexpr bool RED_FWD = KCC_RED_FWD != 0;
+#if KCC_RED_LATE
+#define KCC_RED_WPE __attribute__((amdgpu_waves_per_eu(5)))
+#else
+#define KCC_RED_WPE
+#endif
+
 // Container loads use the default cache policy.  Measured (round 3, one process, outputs
 // identical): C4 reduce default 130.5 us, nt 181.8, sc1 183.5, nt sc1 181.5; the 8-way
 // shard 19.5 / 32.3 / 25.2 / 32.2 us: the 16-B lane loads of a wave coalesce in L1, which
@@ -226,6 +246,15 @@ constexpr uint32_t RED_OOB_OFFSET = 0x7ffffff0u;  // > any output's range (n_nod
 constexpr uint64_t RED_WORD_TAG = 0x4B43C0DEull << 32;  // upper half of a published word
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+// The rank bodies' few workgroup words live right after their 16 * RANK_L bytes of keys in
+// the caller's LDS buffer (RANK_LDS_WORDS u64 in all), not in __shared__ variables of their
+// own: those would add to every launch that carries them (the reduce's 32 KiB strips + 24 B
+// held a CU to 4 of its workgroups, where 5 fit in 160 KiB)
+constexpr int RANK_LDS_WORDS = 2 * RANK_L + 4;
+__device__ __forceinline__ uint32_t* rank_small(uint64_t* lds) {
+  return reinterpret_cast<uint32_t*>(lds + 2 * RANK_L);  // [0] last, [4..7] per-wave counts
+}
+
 __device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds);
 __device__ void spec_place_body(const PlaceArgs& pa, int64_t blk);
 
@@ -251,9 +280,9 @@ constexpr bool KCC_NP_NOSC1 = true;
 constexpr bool KCC_NP_NOSC1 = false;
 #endif
 template <int NA, bool NPM>
-__global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra, NpArgs np) {
+__global__ __launch_bounds__(256) KCC_RED_WPE void reduce_kernel(RedArgs a, RankArgs ra, NpArgs np) {
   __shared__ __attribute__((aligned(16))) uint64_t pre_s[RED_WAVES_PER_BLOCK][NA][RED_TILE];
-  static_assert(sizeof(pre_s) >= 16 * RANK_L, "the rank workgroups stage RANK_L 16-B keys");
+  static_assert(sizeof(pre_s) >= 8 * RANK_LDS_WORDS, "the rank workgroups stage RANK_L 16-B keys");
   const int32_t npb = NPM ? np.n_place + np.n_rows : 0;  // the last workgroups
   if constexpr (NPM) {
     if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - npb) {
@@ -309,10 +338,10 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra, NpA
   // reduced (static ring indices: the tile loop below is unrolled over the ring).
   // The first tiles' loads go out first: they depend on the range alone, while the node
   // search below is a chain of dependent loads
-  constexpr int RING = RED_PREFETCH + 1;
+  constexpr int RING = RED_LATE ? 1 : RED_PREFETCH + 1;
   uint64_t xs[RING][NA][RED_IPL];
 #pragma unroll
-  for (int u = 0; u < RED_PREFETCH; ++u)
+  for (int u = 0; u < (RED_LATE ? 1 : RED_PREFETCH); ++u)
 #pragma unroll
     for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 8 * RED_IPL, u * RED_TILE * 8, xs[u][k]);
   __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink them below the search)
@@ -393,14 +422,20 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra, NpA
 #ifndef KCC_DIAG_RED_NOSTORE
     issue_pending();
 #endif
+    if constexpr (!RED_LATE) {
 #pragma unroll
-    for (int k = 0; k < NA; ++k)
-      load_quad(rs[k], lane * 8 * RED_IPL, (tb + RED_PREFETCH * RED_TILE) * 8, nx[k]);
+      for (int k = 0; k < NA; ++k)
+        load_quad(rs[k], lane * 8 * RED_IPL, (tb + RED_PREFETCH * RED_TILE) * 8, nx[k]);
+    }
 #ifdef KCC_DIAG_RED_LOADONLY
 #pragma unroll
     for (int k = 0; k < NA; ++k)
 #pragma unroll
       for (int i = 0; i < RED_IPL; ++i) carry[k] += x[k][i];
+    if constexpr (RED_LATE) {
+#pragma unroll
+      for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 8 * RED_IPL, (tb + RED_TILE) * 8, nx[k]);
+    }
     return;
 #endif
     const int32_t p0l = tb + RED_IPL * lane;  // relative position of this lane's first item
@@ -420,23 +455,40 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra, NpA
     uint64_t tot[NA], P[NA];
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
-      P[k] = x[k][0];
+      if constexpr (RED_FWD) {  // the lane's in-lane inclusive prefixes, in place
 #pragma unroll
-      for (int i = 1; i < RED_IPL; ++i) P[k] += x[k][i];
+        for (int i = 1; i < RED_IPL; ++i) x[k][i] += x[k][i - 1];
+        P[k] = x[k][RED_IPL - 1];
+      } else {
+        P[k] = x[k][0];
+#pragma unroll
+        for (int i = 1; i < RED_IPL; ++i) P[k] += x[k][i];
+      }
     }
 #pragma unroll
     for (int k = 0; k < NA; k += 2) wave_incl_scan2_u64(P[k], P[k + 1]);
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
-      uint64_t pp[RED_IPL];  // the lane's items' inclusive prefixes, walked back from P
-      pp[RED_IPL - 1] = P[k];
+      uint64_t pp[RED_IPL];  // the lane's items' inclusive prefixes
+      if constexpr (RED_FWD) {  // the lane's exclusive base + its in-lane prefixes: adds only
+        const uint64_t base = P[k] - x[k][RED_IPL - 1];
 #pragma unroll
-      for (int i = RED_IPL - 1; i > 0; --i) pp[i - 1] = pp[i] - x[k][i];
+        for (int i = 0; i < RED_IPL - 1; ++i) pp[i] = base + x[k][i];
+        pp[RED_IPL - 1] = P[k];
+      } else {  // walked back from P
+        pp[RED_IPL - 1] = P[k];
+#pragma unroll
+        for (int i = RED_IPL - 1; i > 0; --i) pp[i - 1] = pp[i] - x[k][i];
+      }
       u64x2* dst = reinterpret_cast<u64x2*>(&pre[k][0]);  // pair h at strip_at(8 lane + 2 h)
 #pragma unroll
       for (int h = 0; h < RED_IPL / 2; ++h) dst[h * 64 + lane] = u64x2{pp[2 * h], pp[2 * h + 1]};
       tot[k] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(P[k] >> 32), 63) << 32) |
                (uint32_t)__builtin_amdgcn_readlane((uint32_t)P[k], 63);
+    }
+    if constexpr (RED_LATE) {  // this tile's items are in the strip: its registers take the next tile
+#pragma unroll
+      for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 8 * RED_IPL, (tb + RED_TILE) * 8, nx[k]);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -509,7 +561,8 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra, NpA
   for (int32_t tb = 0; tb < len; tb += RING * RED_TILE) {
 #pragma unroll
     for (int u = 0; u < RING; ++u)
-      if (tb + u * RED_TILE < len) tile(xs[u], xs[(u + RED_PREFETCH) % RING], tb + u * RED_TILE);
+      if (tb + u * RED_TILE < len)
+        tile(xs[u], xs[(u + (RED_LATE ? 0 : RED_PREFETCH)) % RING], tb + u * RED_TILE);
   }
 #if defined(KCC_DIAG_RED_LOADONLY) || defined(KCC_DIAG_RED_NOSTORE)
   if (carry[0] == 0x123456789ull) out[0][0] = carry[NA - 1] ^ res[0];
@@ -1457,7 +1510,7 @@ __device__ void spec_rank_count(const RankArgs& ra, int64_t blk, uint64_t* lds) 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();  // every storing wave has waited for its stores
-  __shared__ uint32_t last_s;
+  uint32_t& last_s = rank_small(lds)[0];
   if (tid == 0)
     last_s = ns == 1 ? 1u
                      : (uint32_t)(__hip_atomic_fetch_add(ra.arrive + qb, 1u, __ATOMIC_RELAXED,
@@ -1617,7 +1670,7 @@ __device__ void spec_rank_sort(const RankArgs& ra, int64_t blk, uint64_t* lds) {
   }
   // normal candidates in the slice (the count for a query at v = 2^51 - 1, whose
   // threshold (v + 1) << 13 does not fit)
-  __shared__ uint32_t nrm_s[4];
+  uint32_t* const nrm_s = rank_small(lds) + 4;
   {
     const uint32_t wsum = (uint32_t)readlane_u64(wave_incl_scan_u64(nrm), 63);
     if (lane == 0) nrm_s[wv] = wsum;
@@ -1660,7 +1713,7 @@ __device__ void spec_rank_sort(const RankArgs& ra, int64_t blk, uint64_t* lds) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every wave has waited for its stores
-  __shared__ uint32_t last_s;
+  uint32_t& last_s = rank_small(lds)[0];
   if (tid == 0)
     last_s = ns == 1 ? 1u
                      : (uint32_t)(__hip_atomic_fetch_add(ra.arrive + qb, 1u, __ATOMIC_RELAXED,
@@ -1743,7 +1796,7 @@ __device__ void spec_rank_body(const RankArgs& ra, int64_t blk, uint64_t* lds) {
 }
 
 __global__ __launch_bounds__(256) void spec_rank_kernel(RankArgs ra) {
-  __shared__ __attribute__((aligned(16))) uint64_t lds[2 * RANK_L];
+  __shared__ __attribute__((aligned(16))) uint64_t lds[RANK_LDS_WORDS];
   spec_rank_body(ra, blockIdx.x, lds);
 }
 

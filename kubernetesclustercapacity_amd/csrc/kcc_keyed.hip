@@ -26,6 +26,17 @@
 namespace kcc {
 namespace {
 
+// Diagnostic timeline (KCC_TIMELINE builds only): per-workgroup s_memrealtime stamps (100 MHz)
+// of the one-sweep path's phases — kb_gather workgroups in slots [0, 512), kb_sweep's in
+// [512, 1024) — read by kcc_debug_timeline_keyed (scripts/probe/keyed_timeline.py)
+#ifdef KCC_TIMELINE
+__device__ uint64_t kcc_tlk[1024][8];
+#define KCC_TLK(slot, k) \
+  do { if (threadIdx.x == 0) kcc_tlk[(slot) & 1023][(k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define KCC_TLK(slot, k) do { } while (0)
+#endif
+
 constexpr int KY_THREADS = 256;
 constexpr int KY_IPL = 4;                             // containers per lane
 constexpr int KY_BLOCK = KY_THREADS * KY_IPL;         // containers per workgroup
@@ -573,8 +584,10 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
     }
   };
   int64_t g = blockIdx.x;
+  KCC_TLK(512 + blockIdx.x, 0);
   if (g < G) issue(g);
   for (; g < G; g += gridDim.x) {
+    if (g == (int64_t)blockIdx.x + gridDim.x) KCC_TLK(512 + blockIdx.x, 1);  // first tile done
     const int64_t t0 = g * tile, t1 = min(t0 + tile, n);
     int32_t k[PER];
     uint64_t v[NS][PER];
@@ -672,46 +685,72 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, pr), rs, (int)(8 * j), 0, 2);
     }
   }
+  KCC_TLK(512 + blockIdx.x, 2);
 }
 
-// kb_gather: bucket b's records — segment [tab[g][b], tab[g][b + 1]) of every tile g —
-// summed into LDS rows (64-bit LDS atomics), its rows written once.  `parts` workgroups
-// share a bucket (tiles dealt round-robin): each sums its tiles; every part but the last to
-// arrive stores its rows into part_acc, the last one adds them and writes the outputs.
-// A wave works on KB_GA_U segments at once (their loads issued together: a segment is a few
-// hundred bytes, so one per wave would be latency-bound).
+// kb_gather: bucket group b's records — segment [tab[g][b0], tab[g][b0 + nbk]) of every tile
+// g — summed into LDS rows (64-bit LDS atomics), its rows written once.  `parts` workgroups
+// share a group (tiles dealt round-robin): each sums its tiles; the last to arrive adds the
+// others' rows and writes the outputs, and only the others publish theirs (part_acc).
+// XCD-aware placement: workgroup i runs on XCD i mod KB_XCDS, and the slots of one XCD are
+// a contiguous run of groups (both parts of a group included), so neighbouring groups — whose
+// segments of a tile are neighbours in its run and share the lines at their ends, and whose
+// table entries share lines — read them through one L2 (round 5's placement spread neighbours
+// over the 8 XCDs: each line at a segment end and each table line was fetched by several L2s,
+// 1.34x the records' bytes).
+// A wave works on two sub-batches of KB_GA_U2 segments, the next one's loads in flight while
+// the current one is summed (a segment is a few hundred bytes: one per wave would be
+// latency-bound).
 constexpr int KB_GA_THREADS = 1024;
 constexpr int KB_GA_WAVES = KB_GA_THREADS / 64;
-// segments per wave in flight, 128 records of each (C4 A/B, one part: 8 -> 0.3404 ms, 16 ->
-// 0.3394 ms; round 5: 24 equal, 32 spills)
-constexpr int KB_GA_U = 16;
+// segments per sub-batch (two in flight per wave: 2 x 8 x 128 records = round 5's 16 x 128
+// in one batch, whose loads all waited before any was summed)
+#ifndef KCC_KB_GA_U2
+#define KCC_KB_GA_U2 8
+#endif
+constexpr int KB_GA_U2 = KCC_KB_GA_U2;
+static_assert((KB_GA_U2 & (KB_GA_U2 - 1)) == 0 && KB_GA_U2 <= 64,
+              "a sub-batch's table entries are read by lanes lane & (KB_GA_U2 - 1)");
+#ifndef KCC_KB_GA_NT
+#define KCC_KB_GA_NT 0
+#endif
+#ifndef KCC_KB_GA_PIPE
+#define KCC_KB_GA_PIPE 0
+#endif
+constexpr bool KB_GA_PIPE = KCC_KB_GA_PIPE != 0;
 constexpr int KB_GA_CH = 2048;  // tiles per table chunk in LDS (a barrier each: 1024 measured slower)
+constexpr int KB_XCDS = 8;      // gfx950: 8 XCDs, workgroups dealt round-robin
 // buckets per gather workgroup: a tile's segments of KB_GA_BPG adjacent buckets are
 // contiguous in its run, so a workgroup reads them as one segment (half the segments, their
 // partial lines and their latency batches, for twice the LDS rows)
-#ifndef KCC_KB_GA_BPG
-#define KCC_KB_GA_BPG 2
-#endif
-constexpr int KB_GA_BPG = KCC_KB_GA_BPG;
+constexpr int KB_GA_BPG = 2;
 constexpr int KB_GA_ROWS = KB_GA_BPG * KB_ROWS;  // LDS rows per gather workgroup
 static_assert(KB_SW_TILE < 0xffff, "a segment's length and split point pack in 16 bits each");
+static_assert(2 * KB_GA_ROWS * 8 + 2 * KB_GA_CH * 4 + 64 <= 160 * 1024,
+              "kb_gather<2>'s LDS (rows of both arrays + the segment tables) fits one CU");
 // Tiles are read newest-first (the last-written records first, while the memory-side cache
 // may hold them): measured equal (0.3427 / 0.3432 ms), kept.
+[[maybe_unused]] constexpr uint32_t KB_GA_SPIN_MAX = 1u << 22;  // polls before the wait gives up
 
 template <int NA>
 __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
     int64_t G, int64_t n_keys, int nb, int parts, uint32_t stride, const uint32_t* __restrict__ tab,
     const uint64_t* __restrict__ sr, uint64_t* __restrict__ part_acc, uint32_t* __restrict__ arrive,
-    uint64_t* __restrict__ o0, uint64_t* __restrict__ o1) {
+    unsigned long long* __restrict__ faults, uint64_t* __restrict__ o0, uint64_t* __restrict__ o1) {
   constexpr int NACC = NA > 0 ? NA : 1;
   __shared__ unsigned long long acc[NACC][KB_GA_ROWS];
   __shared__ uint32_t seg_off[KB_GA_CH];  // start within the tile
   __shared__ uint32_t seg_len[KB_GA_CH];  // length | (where the group's second bucket starts) << 16
   __shared__ uint32_t last_s;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // this workgroup's slot: XCD x = blockIdx.x mod KB_XCDS holds slots [x q + min(x, r), ...)
+  const uint32_t W = gridDim.x, x = blockIdx.x % KB_XCDS, jx = blockIdx.x / KB_XCDS;
+  const uint32_t q = W / KB_XCDS, rr = W % KB_XCDS;
+  const uint32_t slot = x * q + (x < rr ? x : rr) + jx;
   // b: the bucket group (buckets KB_GA_BPG b .. + nbk - 1)
-  const int b = blockIdx.x / parts, part = blockIdx.x % parts;
+  const int b = (int)(slot / (uint32_t)parts), part = (int)(slot % (uint32_t)parts);
   const int b0 = KB_GA_BPG * b, nbk = nb - b0 < KB_GA_BPG ? nb - b0 : KB_GA_BPG;
+  KCC_TLK(blockIdx.x, 0);
   for (int r = tid; r < KB_GA_ROWS; r += KB_GA_THREADS)
 #pragma unroll
     for (int a = 0; a < NACC; ++a) acc[a][r] = 0ull;
@@ -734,36 +773,67 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
   for (int64_t c0 = 0; c0 < my_tiles; c0 += KB_GA_CH) {
     const int ch = (int)min((int64_t)KB_GA_CH, my_tiles - c0);
     __syncthreads();  // the previous chunk's table entries are consumed
-    for (int i = tid; i < ch; i += KB_GA_THREADS) {
-      const int64_t g = (int64_t)part + (my_tiles - 1 - (c0 + i)) * parts;
+    // the chunk's table entries: every thread's loads issued before any is used (one round
+    // trip per chunk, not one per KB_GA_THREADS entries)
+    constexpr int TQ = KB_GA_CH / KB_GA_THREADS;
+    uint32_t e0[TQ], e1[TQ], e2[TQ];
+#pragma unroll
+    for (int q = 0; q < TQ; ++q) {
+      const int i = tid + q * KB_GA_THREADS;
+      const int64_t g = (int64_t)part + (my_tiles - 1 - (c0 + (i < ch ? i : 0))) * parts;
       const uint32_t* row = tab + g * (nb + 1) + b0;
-      const uint32_t s0 = row[0];
-      seg_off[i] = s0;
-      // (tile runs < 2^16 records: 0xffff is "no second bucket", past every index)
-      seg_len[i] = (row[nbk] - s0) | (KB_GA_BPG > 1 && nbk > 1 ? row[1] - s0 : 0xffffu) << 16;
+      e0[q] = row[0];
+      e1[q] = row[nbk];
+      e2[q] = row[KB_GA_BPG > 1 && nbk > 1 ? 1 : 0];
+    }
+#pragma unroll
+    for (int q = 0; q < TQ; ++q) {
+      const int i = tid + q * KB_GA_THREADS;
+      if (i < ch) {
+        seg_off[i] = e0[q];
+        // (tile runs < 2^16 records: 0xffff is "no second bucket", past every index)
+        seg_len[i] = (e1[q] - e0[q]) | (KB_GA_BPG > 1 && nbk > 1 ? e2[q] - e0[q] : 0xffffu) << 16;
+      }
     }
     __syncthreads();
-    for (int i0 = wv * KB_GA_U; i0 < ch; i0 += KB_GA_WAVES * KB_GA_U) {
-      // KB_GA_U segments: the first 128 records of each loaded at once (two per lane)
-      uint64_t r[KB_GA_U][2];
-      uint32_t len[KB_GA_U], first[KB_GA_U];  // (record indices < 2^32: keyed_bucketed)
+    if (c0 == 0) KCC_TLK(blockIdx.x, 1);
+    // sub-batch t = segments [KB_GA_U2 t, KB_GA_U2 (t + 1)) of the chunk; wave wv takes
+    // t = wv, wv + KB_GA_WAVES, ...  Every load is issued whatever the segment's length (lanes
+    // past it re-read the segment's first record, a line the wave reads anyway), so each
+    // sub-batch issues the same instructions and the waits stay static
+    const int nsb = (ch + KB_GA_U2 - 1) / KB_GA_U2;
+    uint64_t ra[KB_GA_U2][2], rb[KB_GA_U2][2];
+    uint32_t la[KB_GA_U2], fa[KB_GA_U2], lb[KB_GA_U2], fb[KB_GA_U2];
+    auto load_sb = [&](int t, uint64_t (&r)[KB_GA_U2][2], uint32_t (&len)[KB_GA_U2],
+                       uint32_t (&first)[KB_GA_U2]) {
+      // the sub-batch's table entries: one LDS read per array by lanes 0..U2-1, then
+      // wave-uniform (SGPR) lengths and starts
+      const int ib = KB_GA_U2 * t, il = ib + (lane & (KB_GA_U2 - 1));
+      const bool lok = t < nsb && il < ch;
+      const uint32_t vlen = lok ? seg_len[il] : 0xffff0000u;  // length | mid << 16
+      const uint32_t voff = lok ? seg_off[il] : 0u;
 #pragma unroll
-      for (int u = 0; u < KB_GA_U; ++u) {
-        const int i = i0 + u;
-        const bool ok = i < ch;
-        const uint32_t gi = (uint32_t)(c0 + (ok ? i : 0));
+      for (int u = 0; u < KB_GA_U2; ++u) {
+        const bool ok = t < nsb && ib + u < ch;  // (wave-uniform)
+        const uint32_t gi = (uint32_t)(c0 + (ok ? ib + u : 0));
         const uint32_t g = (uint32_t)part + ((uint32_t)my_tiles - 1u - gi) * (uint32_t)parts;
-        len[u] = ok ? seg_len[i] : 0xffff0000u;  // length | mid << 16 (registers: an LDS
-        // read between the adds would wait for every LDS atomic issued before it)
-        first[u] = g * stride + (ok ? seg_off[i] : 0u);
+        // (registers, not LDS: an LDS read between the adds would wait for every LDS atomic
+        // issued before it)
+        len[u] = (uint32_t)__builtin_amdgcn_readlane((int)vlen, u);
+        first[u] = g * stride + (uint32_t)__builtin_amdgcn_readlane((int)voff, u);
+        const uint64_t* __restrict__ seg = sr + first[u];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const uint32_t o = (uint32_t)lane + 64u * h;
-          r[u][h] = o < (len[u] & 0xffffu) ? __builtin_nontemporal_load(sr + first[u] + o) : 0ull;
+          if constexpr (KCC_KB_GA_NT) r[u][h] = __builtin_nontemporal_load(seg + (o < (len[u] & 0xffffu) ? o : 0u));
+          else r[u][h] = seg[o < (len[u] & 0xffffu) ? o : 0u];
         }
       }
+    };
+    auto sum_sb = [&](uint64_t (&r)[KB_GA_U2][2], uint32_t (&len)[KB_GA_U2],
+                      uint32_t (&first)[KB_GA_U2]) {
 #pragma unroll
-      for (int u = 0; u < KB_GA_U; ++u) {
+      for (int u = 0; u < KB_GA_U2; ++u) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const uint32_t o = (uint32_t)lane + 64u * h;
@@ -772,12 +842,30 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
       }
       // the rest of long segments (skewed keys), 64 records a step
 #pragma unroll 1
-      for (int u = 0; u < KB_GA_U; ++u)
+      for (int u = 0; u < KB_GA_U2; ++u)
         for (uint32_t o = 128u + (uint32_t)lane; o < (len[u] & 0xffffu); o += 64u)
           add_rec(sr[first[u] + o], o >= (len[u] >> 16) ? (uint32_t)KB_ROWS : 0u);
+    };
+    if constexpr (KB_GA_PIPE) {  // the next sub-batch's loads in flight across iterations
+      if (wv < nsb) load_sb(wv, ra, la, fa);
+      for (int t = wv; t < nsb; t += 2 * KB_GA_WAVES) {
+        load_sb(t + KB_GA_WAVES, rb, lb, fb);  // (past nsb: a harmless re-read, summed as empty)
+        sum_sb(ra, la, fa);
+        if (t + KB_GA_WAVES >= nsb) break;
+        load_sb(t + 2 * KB_GA_WAVES, ra, la, fa);
+        sum_sb(rb, lb, fb);
+      }
+    } else {  // two sub-batches loaded at once; the first summed while the second arrives
+      for (int t = wv; t < nsb; t += 2 * KB_GA_WAVES) {
+        load_sb(t, ra, la, fa);
+        load_sb(t + KB_GA_WAVES, rb, lb, fb);
+        sum_sb(ra, la, fa);
+        sum_sb(rb, lb, fb);
+      }
     }
   }
   __syncthreads();
+  KCC_TLK(blockIdx.x, 2);
 #ifdef KCC_DIAG_GA_NOATOM
   if (dg == 0x123456789ull) acc[0][0] = dg;  // (keeps the sums alive)
 #endif
@@ -791,34 +879,80 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
     }
     return;
   }
-  // several parts: publish this part's rows, the last part to arrive sums and writes
-  uint64_t* mine = part_acc + ((int64_t)b * parts + part) * NACC * KB_GA_ROWS;
-  for (int r = tid; r < KB_GA_ROWS; r += KB_GA_THREADS)
-#pragma unroll
-    for (int a = 0; a < NACC; ++a)
-      __hip_atomic_store(mine + a * KB_GA_ROWS + r, (uint64_t)acc[a][r], __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  if (tid == 0) {
-    // release: this part's rows before its arrival; acquire: the others' rows after it
-    last_s = __hip_atomic_fetch_add(arrive + b, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+  // several parts: arrive first; every part but the last publishes its rows and then raises
+  // the group's ready count, the last waits for that count, adds the others' rows and writes
+  // the outputs (round 5 had every part publish before arriving: the last part's rows went
+  // to part_acc for nothing, 3x the output's bytes written).  The hand-off is the node-prep
+  // one (kcc_kernels.hip np_wait_rows): agent-scope stores, each wave's vmcnt(0) before the
+  // barrier, then the count; agent-scope loads after it.  A waiting part is resident and its
+  // peers have arrived (they are past their sums), so the wait is short; it is bounded anyway
+  uint32_t* const ready = arrive + (nb + KB_GA_BPG - 1) / KB_GA_BPG;
+  if (tid == 0)
+    last_s = __hip_atomic_fetch_add(arrive + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
              (uint32_t)parts - 1u;
+  __syncthreads();
+  KCC_TLK(blockIdx.x, 3);
+  const int64_t pstride = (int64_t)NACC * KB_GA_ROWS;
+  if (!last_s) {
+    uint64_t* mine = part_acc + ((int64_t)b * parts + part) * pstride;
+    for (int r = tid; r < KB_GA_ROWS; r += KB_GA_THREADS)
+#pragma unroll
+      for (int a = 0; a < NACC; ++a)
+        __hip_atomic_store(mine + a * KB_GA_ROWS + r, (uint64_t)acc[a][r], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(ready + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    KCC_TLK(blockIdx.x, 4);
+    return;
+  }
+  if (tid == 0) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load(ready + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+           (uint32_t)parts - 1u) {
+      if (++spins >= KB_GA_SPIN_MAX) {  // never on a healthy device: the sums are not trusted
+        if (faults) atomicAdd(faults + FAULT_RED, 1ull);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    __hip_atomic_store(arrive + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ready + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  if (!last_s) return;
-  if (tid == 0) __hip_atomic_store(arrive + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (int r = tid; r < KB_GA_ROWS; r += KB_GA_THREADS) {
-    if (row0 + r >= n_keys) break;
+  KCC_TLK(blockIdx.x, 5);
+  // the others' rows: each part's loads all issued before they are added (one round trip
+  // per part, not one per KB_GA_THREADS rows)
+  constexpr int RQ = KB_GA_ROWS / KB_GA_THREADS;
+  static_assert(KB_GA_ROWS % KB_GA_THREADS == 0, "whole row rounds");
+  uint64_t t[RQ][NACC];
 #pragma unroll
-    for (int a = 0; a < NACC; ++a) {
-      uint64_t t = acc[a][r];
-      for (int p = 0; p < parts; ++p)
-        if (p != part)
-          t += __hip_atomic_load(part_acc + ((int64_t)b * parts + p) * NACC * KB_GA_ROWS + a * KB_GA_ROWS + r,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      out[a][row0 + r] = t;
-    }
+  for (int q = 0; q < RQ; ++q)
+#pragma unroll
+    for (int a = 0; a < NACC; ++a) t[q][a] = acc[a][tid + q * KB_GA_THREADS];
+  for (int p = 0; p < parts; ++p) {
+    if (p == part) continue;
+    const uint64_t* src = part_acc + ((int64_t)b * parts + p) * pstride;
+    uint64_t v[RQ][NACC];
+#pragma unroll
+    for (int q = 0; q < RQ; ++q)
+#pragma unroll
+      for (int a = 0; a < NACC; ++a)
+        v[q][a] = __hip_atomic_load(src + a * KB_GA_ROWS + tid + q * KB_GA_THREADS, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int q = 0; q < RQ; ++q)
+#pragma unroll
+      for (int a = 0; a < NACC; ++a) t[q][a] += v[q][a];
   }
+#pragma unroll
+  for (int q = 0; q < RQ; ++q) {
+    const int r = tid + q * KB_GA_THREADS;
+    if (row0 + r < n_keys)
+#pragma unroll
+      for (int a = 0; a < NACC; ++a) out[a][row0 + r] = t[q][a];
+  }
+  KCC_TLK(blockIdx.x, 6);
 }
 
 }  // namespace
@@ -907,7 +1041,7 @@ static hipError_t run_sweep(int64_t n_keys, int64_t n, const int32_t* key, const
   const int ng = (nb + KB_GA_BPG - 1) / KB_GA_BPG;  // bucket groups
   hipLaunchKernelGGL(kb_gather<NA>, dim3((unsigned)(ng * parts)), dim3(KB_GA_THREADS), 0, s, G, n_keys,
                      nb, parts, (uint32_t)KB_SW_TILE, kw.counts, kw.sr, kw.part_acc, kw.arrive,
-                     out[0], out[1]);
+                     kw.faults, out[0], out[1]);
   if (NA >= 2 && n > 0)  // (few workgroups: each adds to one arrival counter; the list is short)
     hipLaunchKernelGGL(kb_escape, dim3(KB_ESC_WG), dim3(256), 0, s, kw.esc_n, kw.esc_row, kw.esc_cpu,
                        kw.esc_mem, out[0], out[1]);
@@ -995,3 +1129,12 @@ hipError_t launch_count_keyed(int64_t n_keys, int64_t n, const int32_t* key, int
 }
 
 }  // namespace kcc
+
+#ifdef KCC_TIMELINE
+// (timeline builds only) copy the keyed kernels' stamps to host[1024][8] and zero them
+extern "C" int kcc_debug_timeline_keyed(void* host) {
+  static uint64_t zero[1024][8];
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(kcc::kcc_tlk), sizeof(zero)) != hipSuccess) return -3;
+  return hipMemcpyToSymbol(HIP_SYMBOL(kcc::kcc_tlk), zero, sizeof(zero)) == hipSuccess ? 0 : -3;
+}
+#endif

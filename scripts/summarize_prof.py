@@ -55,6 +55,21 @@ def main(d, out=None, traffic_json=None):
         if hbm is not None:
             traffic[k] = {"hbm_bytes_per_launch": hbm * 1e6, "fetch_kib": f, "write_kib": w,
                           "avg_us": avg / 1e3, "clock_ghz": clk, "valu_issue_pct": issue}
+    # read requests by size (TCC_EA0_RDREQ_{32B,64B,128B}, when a pass collected them): the
+    # bytes the L2s asked the fabric for, a cross-check of the 2 x FETCH_SIZE correction
+    sized = [(k, p) for k, p in ((k, {c: sum(v) / len(v) for c, v in pmc[k].items()}) for k in pmc)
+             if "TCC_EA0_RDREQ_128B_sum" in p]
+    if sized:
+        lines += ["", "| kernel | RDREQ | 32B | 64B | 128B | read MB by size (32/64/128 B) | 2 x FETCH MB |",
+                  "|---|---|---|---|---|---|---|"]
+        for k, p in sized:
+            n32, n64, n128 = (p.get(f"TCC_EA0_RDREQ_{b}B_sum", 0.0) for b in (32, 64, 128))
+            mb = (32 * n32 + 64 * n64 + 128 * n128) / 1e6
+            f = p.get("FETCH_SIZE")
+            lines.append(f"| {k} | {p.get('TCC_EA0_RDREQ_sum', 0):.4g} | {n32:.4g} | {n64:.4g} | "
+                         f"{n128:.4g} | {mb:.4g} | {'-' if f is None else f'{2 * f * 1024 / 1e6:.4g}'} |")
+            if k in traffic:
+                traffic[k]["read_bytes_by_req_size"] = mb * 1e6
     extra = ["", "Raw per-dispatch counter averages:", ""]
     for k in sorted(pmc):
         extra.append(f"- {k}: " + ", ".join(f"{c}={sum(v) / len(v):.6g}"
