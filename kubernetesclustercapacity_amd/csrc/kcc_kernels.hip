@@ -236,6 +236,9 @@ __device__ __forceinline__ int32_t strip_at(int32_t p) {
 }
 constexpr uint32_t RED_OOB_OFFSET = 0x7ffffff0u;  // > any output's range (n_nodes < 2^28)
 [[maybe_unused]] constexpr uint32_t RED_SPIN_MAX = 1u << 18;       // look-back polls before a wait gives up
+// node-prep polls: s_sleep units (64 clocks) between them (4 and 1 measured equal, round 5)
+#define KCC_NP_SLEEP 20
+[[maybe_unused]] constexpr uint32_t NP_SPIN_MAX = 1u << 22;  // polls before a wait gives up (~2 s)
 // Look-back publication: tagged words.  Each 64-bit value of the piece travels as two
 // 64-bit words {tag:32 | half:32}, stored by 2 x NA lanes as relaxed agent-scope atomics;
 // the consumer polls the words until every tag matches and assembles the halves.  Every
@@ -266,6 +269,15 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }
 
 __device__ void np_body(const NpArgs& np, int32_t j, uint32_t* scratch);
+template <bool NC>
+__device__ void fit_body(int64_t n_nodes, uint32_t* __restrict__ queue,
+                         const FitGroupA* __restrict__ fast_a, const FitGroup* __restrict__ fast_b,
+                         const SlowNode* __restrict__ slow, const int64_t* __restrict__ slow_list,
+                         int64_t S, const SpecRec* __restrict__ specs, int64_t* __restrict__ partial,
+                         unsigned long long* __restrict__ counters, int32_t chunk, int32_t gx,
+                         int32_t gy, const int32_t* __restrict__ fast_cl,
+                         const unsigned long long* __restrict__ faults, const int32_t b,
+                         uint32_t* q_slot);
 
 // NPM: node prep behind the reduce's workgroups (NpArgs): the node sums written through
 // (sc1) and every wave's completion counted
@@ -283,16 +295,42 @@ template <int NA, bool NPM>
 __global__ __launch_bounds__(256) KCC_RED_WPE void reduce_kernel(RedArgs a, RankArgs ra, NpArgs np) {
   __shared__ __attribute__((aligned(16))) uint64_t pre_s[RED_WAVES_PER_BLOCK][NA][RED_TILE];
   static_assert(sizeof(pre_s) >= 8 * RANK_LDS_WORDS, "the rank workgroups stage RANK_L 16-B keys");
-  const int32_t npb = NPM ? np.n_place + np.n_rows : 0;  // the last workgroups
+  int32_t nfit = 0;  // (variant builds) the fit's workgroups, last of all
+#if KCC_FIT_IN_REDUCE
   if constexpr (NPM) {
-    if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - npb) {
-      np_body(np, (int32_t)blockIdx.x - ((int32_t)gridDim.x - npb), reinterpret_cast<uint32_t*>(&pre_s[0][0][0]));
+    nfit = np.fit_blocks;
+    if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - nfit) {
+      if (threadIdx.x == 0) {  // node prep's last workgroup sets the word (the finalize clears it)
+        uint32_t spins = 0;
+        while (__hip_atomic_load(np.sync + NP_GO, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+          if (++spins >= NP_SPIN_MAX) {
+            atomicAdd(&np.faults[FAULT_RED], 1ull);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(KCC_NP_SLEEP);
+        }
+      }
+      __syncthreads();
+      if (KCC_FIT_IN_REDUCE == 1)  // (2: timing diagnostic without the fences)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // node prep's stream, spec_place's records
+      fit_body<true>(np.n, np.fit_queue, np.fast_a, np.fast_b, np.slow, np.slow_list, np.S, np.fit_specs,
+                     np.fit_partial, np.counters, 0, np.fit_gx, np.fit_gy, np.fast_cl, np.faults,
+                     (int32_t)blockIdx.x - ((int32_t)gridDim.x - nfit),
+                     reinterpret_cast<uint32_t*>(&pre_s[0][0][0]));
+      return;
+    }
+  }
+#endif
+  const int32_t npb = NPM ? np.n_place + np.n_rows : 0;  // the last workgroups (before the fit's)
+  if constexpr (NPM) {
+    if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - nfit - npb) {
+      np_body(np, (int32_t)blockIdx.x - ((int32_t)gridDim.x - nfit - npb), reinterpret_cast<uint32_t*>(&pre_s[0][0][0]));
       return;
     }
   }
   // the spec ranks' workgroups: behind the reduce's (RedArgs::ranks_last; dispatched as its
   // first waves retire, they run in the reduce's tail) or in front of them
-  const int32_t rank0 = a.ranks_last ? (int32_t)gridDim.x - npb - ra.n_blocks : 0;  // first rank block
+  const int32_t rank0 = a.ranks_last ? (int32_t)gridDim.x - nfit - npb - ra.n_blocks : 0;  // first rank block
   const int32_t red0 = a.ranks_last ? 0 : ra.n_blocks;                              // first reduce block
   if constexpr (NA == 2) {  // (launch_reduce: the ranks ride the 2-array reduce only)
     if (ra.n_blocks > 0 && (int32_t)blockIdx.x >= rank0 && (int32_t)blockIdx.x < rank0 + ra.n_blocks) {
@@ -671,9 +709,6 @@ constexpr uint64_t FAST_C_MAX = 1ull << 51;     // 1 <= spec cpu < 2^51
 constexpr int64_t FAST_M_MAX = 1ll << 51;       // 1 <= spec mem < 2^51
 
 // ---- node prep behind the reduce (NpArgs, the clamp in the fit) ---------------------
-// node-prep polls: s_sleep units (64 clocks) between them (4 and 1 measured equal, round 5)
-#define KCC_NP_SLEEP 20
-[[maybe_unused]] constexpr uint32_t NP_SPIN_MAX = 1u << 22;  // polls before a wait gives up (~2 s)
 // thread 0 waits until *w == epoch (bounded: a give-up counts as a reduce fault), then the
 // workgroup goes on.  Polls ~0.5 us apart (each is an uncached load of one line)
 __device__ void np_wait(const uint32_t* w, uint32_t epoch, unsigned long long* faults) {
@@ -871,6 +906,11 @@ __device__ void np_body(const NpArgs& np, int32_t j, uint32_t* scratch) {
   // the last node-prep workgroup to finish publishes the epoch: every storing reduce wave
   // (each in some row workgroup's window), the rank workgroup and every node-prep workgroup
   // have read it by then
+#if KCC_FIT_IN_REDUCE
+  if (np.fit_blocks && KCC_FIT_IN_REDUCE == 1) {  // (the fit in this launch reads the stream)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  }
+#endif
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t total = (uint32_t)(np.n_place + np.n_rows);
@@ -878,6 +918,12 @@ __device__ void np_body(const NpArgs& np, int32_t j, uint32_t* scratch) {
       const uint32_t e = __hip_atomic_load(np.sync + NP_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(np.sync + NP_ARRIVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(np.sync + NP_EPOCH, e + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if KCC_FIT_IN_REDUCE
+      if (np.fit_blocks) {  // every node-prep workgroup released its stores before arriving
+        if (KCC_FIT_IN_REDUCE == 1) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+        __hip_atomic_store(np.sync + NP_GO, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#endif
     }
   }
 }
@@ -2332,17 +2378,19 @@ __device__ __forceinline__ double f64_at(const i32x16& v, int k) {
 // NC: the clamp in the fit (fast_cl, launch_fit) — its own instantiation, so the
 // clamp-correction layout's registers are not the larger loops' (one kernel holding both
 // spilled 52 SGPRs: C4 fit 116 -> 120 us)
+// (the body of fit_kernel; b = the workgroup's index in the fit's grid, q_slot = 2 words of
+// LDS)
 template <bool NC>
-__global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
+__device__ __forceinline__ void fit_body(
     int64_t n_nodes, uint32_t* __restrict__ queue, const FitGroupA* __restrict__ fast_a,
     const FitGroup* __restrict__ fast_b, const SlowNode* __restrict__ slow,
     const int64_t* __restrict__ slow_list, int64_t S, const SpecRec* __restrict__ specs,
     int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t chunk,
     int32_t gx, int32_t gy, const int32_t* __restrict__ fast_cl,
-    const unsigned long long* __restrict__ faults) {
+    const unsigned long long* __restrict__ faults, const int32_t b, uint32_t* q_slot) {
   // XCD-aware order (speed only, never correctness): workgroups are dealt round-robin
   // over the 8 XCDs, so give every spec group of one node chunk the same b % 8
-  const int32_t b = blockIdx.x, xcd = b & 7, r = b >> 3;
+  const int32_t xcd = b & 7, r = b >> 3;
   const int32_t bx = r % gx, by = (r / gx) * 8 + xcd;
   if (by >= gy) return;  // padding of gy up to a multiple of 8 (whole workgroup)
   // issue priority falls with the workgroup's progress through its share (below): the
@@ -2398,7 +2446,6 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
     q1 = sh < q1 ? (sh > FIT_QMIN ? sh : FIT_QMIN) : q1;
   }
 
-  __shared__ uint32_t q_slot[2];
   // lane 0 of wave 0 issues the claim in asm, so the compiler does not wait for it where
   // it is issued (its atomic-optimizer expansion reads the result at once); wave 0 waits
   // for it (vmcnt) at the end of the chunk — the loop bodies issue no other vector memory
@@ -2692,11 +2739,25 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
   KCC_TL(2048 + b % 4096, 3);
 }
 
+template <bool NC>
+__global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
+    int64_t n_nodes, uint32_t* __restrict__ queue, const FitGroupA* __restrict__ fast_a,
+    const FitGroup* __restrict__ fast_b, const SlowNode* __restrict__ slow,
+    const int64_t* __restrict__ slow_list, int64_t S, const SpecRec* __restrict__ specs,
+    int64_t* __restrict__ partial, unsigned long long* __restrict__ counters, int32_t chunk,
+    int32_t gx, int32_t gy, const int32_t* __restrict__ fast_cl,
+    const unsigned long long* __restrict__ faults) {
+  __shared__ uint32_t q_slot[2];
+  fit_body<NC>(n_nodes, queue, fast_a, fast_b, slow, slow_list, S, specs, partial, counters, chunk,
+               gx, gy, fast_cl, faults, (int32_t)blockIdx.x, q_slot);
+}
+
 __global__ void fit_finalize_kernel(int64_t S, const int64_t* __restrict__ partial,
                                     const int32_t* __restrict__ perm, int64_t* __restrict__ totals,
                                     int32_t* __restrict__ spec_err,
-                                    const unsigned long long* __restrict__ faults) {
+                                    const unsigned long long* __restrict__ faults, uint32_t* go) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (go && i == 0) *go = 0u;  // (variant builds: the fit in the reduce launch has passed it)
   if (i >= S) return;
   const int32_t dst = perm[i];
   const bool err = partial[S + i] != 0;
@@ -2883,7 +2944,11 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
   const int64_t waves = red ? (n_containers + range - 1) / range : 0;
   if (waves > reduce_tail_records()) return hipErrorInvalidValue;
   const int64_t red_blocks = (waves + RED_WAVES_PER_BLOCK - 1) / RED_WAVES_PER_BLOCK;
+#if KCC_FIT_IN_REDUCE
+  const unsigned blocks = (unsigned)(red_blocks + ra.n_blocks + npb + (npb > 0 ? np.fit_blocks : 0));
+#else
   const unsigned blocks = (unsigned)(red_blocks + ra.n_blocks + npb);
+#endif
   np.ptr = node_ptr;
   np.c0 = c0;
   np.range = range;
@@ -3037,6 +3102,22 @@ static int64_t fit_grid_y(int64_t n_nodes, int64_t n_specs, int64_t grid_nodes) 
   return gy;
 }
 
+#if KCC_FIT_IN_REDUCE
+void fit_in_reduce_grid(int64_t n_nodes, int64_t n_specs, int32_t* gx, int32_t* gy) {
+  static std::atomic<int64_t> cache[MAX_DEVS];
+  const int64_t res = resident_blocks(cache, reinterpret_cast<const void*>(reduce_kernel<2, true>),
+                                      256, 0, 1024);
+  const int64_t x = (n_specs + FIT_SPW - 1) / FIT_SPW;
+  int64_t y = res / x;
+  if (y >= 16) y = y / 8 * 8;
+  const int64_t claims = (fit_groups(n_nodes) + FIT_QCHUNK - 1) / FIT_QCHUNK;
+  if (y > claims) y = claims;
+  if (y < 1) y = 1;
+  *gx = (int32_t)x;
+  *gy = (int32_t)y;
+}
+#endif
+
 hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,
                       const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
@@ -3058,10 +3139,10 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
 
 hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial, const int32_t* perm,
                                int64_t* totals, int32_t* spec_err,
-                               const unsigned long long* faults, hipStream_t s) {
+                               const unsigned long long* faults, hipStream_t s, uint32_t* go) {
   if (n_specs <= 0) return hipSuccess;
   hipLaunchKernelGGL(fit_finalize_kernel, dim3(grid_for(n_specs, 256, 1 << 30)), dim3(256), 0, s,
-                     n_specs, partial, perm, totals, spec_err, faults);
+                     n_specs, partial, perm, totals, spec_err, faults, go);
   return hipGetLastError();
 }
 

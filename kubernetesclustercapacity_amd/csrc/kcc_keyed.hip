@@ -9,15 +9,19 @@
 // give the reference's sums bit for bit in any order.  kcc_count_by_key counts the pods
 // per key (len(pods), CC:106/135).
 //
-// Two implementations; keys < 0 or >= n_keys are skipped (pods whose
-// node is not a listed row):
-//  - bucketed (n_keys <= KB_NB_MAX * KB_ROWS, the default): rows are cut into buckets of
-//    KB_ROWS; kb_hist counts each tile's containers per bucket (LDS histogram), kb_scan
-//    turns the counts into scatter offsets, kb_scatter moves every container's (row in
-//    bucket, values) into its bucket's contiguous range (LDS cursors), and kb_accum sums
-//    each bucket in LDS (64-bit LDS atomics) and writes its rows once.  No global
-//    atomics; ~64 B of HBM traffic per container.
-//  - direct atomics (fallback): each lane takes KY_IPL consecutive containers, merges
+// Three implementations; keys < 0 or >= n_keys are skipped (pods whose
+// node is not a listed row).  Rows are cut into buckets of KB_ROWS (n_keys <= KB_NB_MAX *
+// KB_ROWS):
+//  - one sweep (requests without limits, and the pod counts: the default): kb_sweep
+//    counting-sorts each tile of containers by bucket in LDS and writes it as one
+//    contiguous run of 8-B records, kb_gather sums each pair of buckets' segments of every
+//    tile into LDS rows and writes them once, kb_escape adds what the records cannot hold;
+//  - bucketed (calls with limits, four arrays): kb_hist counts each tile's containers per
+//    bucket (LDS histogram), kb_scan turns the counts into scatter offsets, kb_scatter
+//    moves every container's (row in bucket, values) into its bucket's contiguous range
+//    (LDS cursors), and kb_accum sums each bucket in LDS (64-bit LDS atomics) and writes
+//    its rows once.  No global atomics;
+//  - direct atomics (more keys, or no workspace): each lane takes KY_IPL consecutive containers, merges
 //    runs of equal keys in registers (a pod's containers are consecutive in a List) and
 //    issues one 64-bit device atomic per array and run — device-scope atomics to random
 //    rows execute past the L2s at ~14 G/s, so this is the slow path.
