@@ -644,18 +644,6 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     np.bcnt = clamp_of(dv).bcnt;
     np.S = n_specs;
     np.faults = as<unsigned long long>(dv.faults);
-#if KCC_FIT_IN_REDUCE
-    if (n_nodes > 0) {  // (variant builds) the fit rides behind node prep in the same launch
-      int32_t gx = 0, gy = 0;
-      kcc::fit_in_reduce_grid(n_nodes, n_specs, &gx, &gy);
-      np.fit_gx = gx;
-      np.fit_gy = gy;
-      np.fit_blocks = gx * ((gy + 7) / 8 * 8);
-      np.fit_queue = as<uint32_t>(dv.fit_q);
-      np.fit_specs = spec_prep_of(dv).rec;
-      np.fit_partial = partial;
-    }
-#endif
   }
   if (n_specs > 0) {
     rc = clamp_clean(ctx, dv, s);
@@ -702,9 +690,6 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                        c, lo[c], n_nodes, s, dv.fit_dense,
                                        place_here ? &pa : nullptr, fast_cl));
     if (n == 0) continue;
-#if KCC_FIT_IN_REDUCE
-    if (np_fused) continue;  // (the fit ran in the reduce launch)
-#endif
     ProfPair pp{};
     if (dv.prof_on) {
       KCC_HIP(ctx, prof_event(dv, &pp.a));
@@ -728,15 +713,6 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   // the clamp launch's last workgroup also finalizes (no fit_finalize launch)
   if (n_specs > 0 && nc) {  // the fit applied the clamp: no clamp_apply, nothing dirty
     dv.clamp_dirty = false;
-#if KCC_FIT_IN_REDUCE
-    if (np_fused && n_nodes > 0) {  // the finalize clears the go word (no partial API here)
-      if (!totals) return fail(ctx, KCC_EINVAL, "fit-in-reduce variant: kcc_capacity_async only");
-      KCC_HIP(ctx, kcc::launch_fit_finalize(n_specs, partial, as<int32_t>(dv.sperm), totals, spec_err,
-                                            as<const unsigned long long>(dv.faults), s,
-                                            as<uint32_t>(dv.np_sync) + kcc::NP_GO));
-      return KCC_OK;
-    }
-#endif
     if (totals) return fit_finalize_dev(ctx, dv, n_specs, partial, totals, spec_err, s);
     return KCC_OK;
   }

@@ -19,12 +19,6 @@
 
 namespace kcc {
 
-// Experiment (variant builds): the fit's workgroups ride behind node prep's in
-// the reduce launch (one kernel boundary fewer on the clamp-in-fit ranks)
-#ifndef KCC_FIT_IN_REDUCE
-#define KCC_FIT_IN_REDUCE 0
-#endif
-
 struct RankArgs;   // below: spec ranks, run as extra workgroups of a reduce launch
 struct NpArgs;     // below: node prep (clamp in the fit) behind a reduce launch's workgroups
 
@@ -347,15 +341,6 @@ struct NpArgs {
   const uint32_t* bcnt;
   int64_t S;
   unsigned long long* faults;
-#if KCC_FIT_IN_REDUCE
-  // (variant builds) the fit's workgroups behind node prep's in the same launch: they wait
-  // for [NP_GO] (set by node prep's last workgroup, cleared by the finalize), then run the
-  // fit's body
-  int32_t fit_blocks, fit_gx, fit_gy;
-  uint32_t* fit_queue;
-  const SpecRec* fit_specs;
-  int64_t* fit_partial;
-#endif
 };
 constexpr int NP_ROWS_PER_WG = 1024;  // 256 threads x 4 rows
 // NpArgs::sync (uint32 words, 64-B lines): [NP_EPOCH] the last launch's epoch (a launch's
@@ -365,7 +350,7 @@ constexpr int NP_ROWS_PER_WG = 1024;  // 256 threads x 4 rows
 // Epoch flags need no reset, and a node-prep workgroup waits for the waves that store its
 // rows alone: one counter of every wave's arrival took the ~3200 same-address atomics of
 // the 8-way C4 rank serially (~25 ns apiece, 80 us)
-constexpr int NP_EPOCH = 0, NP_DONE = 16, NP_ARRIVE = 32, NP_GO = 48, NP_FLAGS = 64;
+constexpr int NP_EPOCH = 0, NP_DONE = 16, NP_ARRIVE = 32, NP_FLAGS = 64;
 
 // counters (CNT_*): exact-path (node, spec) pairs, class-B specs, and per node chunk
 // of a pipelined call (kcc_capacity_partial_async) the rows in that chunk's slow_list.
@@ -449,13 +434,7 @@ inline int64_t fit_queue_words(int64_t S) { return (S + 255) / 256 * FIT_QSUBS_M
 // partial[S + i] != 0; KCC_SPEC_FAULT for every spec while a fault word is set)
 hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial,
                                const int32_t* perm, int64_t* totals, int32_t* spec_err,
-                               const unsigned long long* faults, hipStream_t s,
-                               uint32_t* go = nullptr);
-#if KCC_FIT_IN_REDUCE
-// the fit grid (gx spec columns x gy workgroups each) for workgroups that run inside the
-// node-prep reduce launch (its occupancy)
-void fit_in_reduce_grid(int64_t n_nodes, int64_t n_specs, int32_t* gx, int32_t* gy);
-#endif
+                               const unsigned long long* faults, hipStream_t s);
 // dst[k] += src[k] (wrapping int64), k < n: folds one node shard's partial vector into
 // another on the same device (the host-array entry points with more shards than devices)
 hipError_t launch_partial_add(int64_t n, int64_t* dst, const int64_t* src, hipStream_t s);

@@ -153,25 +153,6 @@ __device__ __forceinline__ int32_t rel_ptr(const int64_t* __restrict__ ptr, int6
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
-// One tile's registers instead of a two-tile ring: the next tile's loads go out as soon as
-// this tile's items are in the LDS strip (before its node walk), so the tile loop needs 32
-// fewer VGPRs
-#ifndef KCC_RED_LATE
-#define KCC_RED_LATE 0
-#endif
-constexpr bool RED_LATE = KCC_RED_LATE != 0;
-// Per-item prefixes from in-lane running sums (adds: one v_lshl_add_u64 each) and the lane's
-// exclusive base, instead of walking back from the lane's inclusive prefix (64-bit
-// subtracts: v_sub_co + v_subb each)
-#ifndef KCC_RED_FWD
-#define KCC_RED_FWD 0
-#endif
-constexpr bool RED_FWD = KCC_RED_FWD != 0;
-#if KCC_RED_LATE
-#define KCC_RED_WPE __attribute__((amdgpu_waves_per_eu(5)))
-#else
-#define KCC_RED_WPE
-#endif
 
 // Container loads use the default cache policy.  Measured (round 3, one process, outputs
 // identical): C4 reduce default 130.5 us, nt 181.8, sc1 183.5, nt sc1 181.5; the 8-way
@@ -269,15 +250,6 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }
 
 __device__ void np_body(const NpArgs& np, int32_t j, uint32_t* scratch);
-template <bool NC>
-__device__ void fit_body(int64_t n_nodes, uint32_t* __restrict__ queue,
-                         const FitGroupA* __restrict__ fast_a, const FitGroup* __restrict__ fast_b,
-                         const SlowNode* __restrict__ slow, const int64_t* __restrict__ slow_list,
-                         int64_t S, const SpecRec* __restrict__ specs, int64_t* __restrict__ partial,
-                         unsigned long long* __restrict__ counters, int32_t chunk, int32_t gx,
-                         int32_t gy, const int32_t* __restrict__ fast_cl,
-                         const unsigned long long* __restrict__ faults, const int32_t b,
-                         uint32_t* q_slot);
 
 // NPM: node prep behind the reduce's workgroups (NpArgs): the node sums written through
 // (sc1) and every wave's completion counted
@@ -292,45 +264,19 @@ constexpr bool KCC_NP_NOSC1 = true;
 constexpr bool KCC_NP_NOSC1 = false;
 #endif
 template <int NA, bool NPM>
-__global__ __launch_bounds__(256) KCC_RED_WPE void reduce_kernel(RedArgs a, RankArgs ra, NpArgs np) {
+__global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra, NpArgs np) {
   __shared__ __attribute__((aligned(16))) uint64_t pre_s[RED_WAVES_PER_BLOCK][NA][RED_TILE];
   static_assert(sizeof(pre_s) >= 8 * RANK_LDS_WORDS, "the rank workgroups stage RANK_L 16-B keys");
-  int32_t nfit = 0;  // (variant builds) the fit's workgroups, last of all
-#if KCC_FIT_IN_REDUCE
+  const int32_t npb = NPM ? np.n_place + np.n_rows : 0;  // the last workgroups
   if constexpr (NPM) {
-    nfit = np.fit_blocks;
-    if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - nfit) {
-      if (threadIdx.x == 0) {  // node prep's last workgroup sets the word (the finalize clears it)
-        uint32_t spins = 0;
-        while (__hip_atomic_load(np.sync + NP_GO, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-          if (++spins >= NP_SPIN_MAX) {
-            atomicAdd(&np.faults[FAULT_RED], 1ull);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(KCC_NP_SLEEP);
-        }
-      }
-      __syncthreads();
-      if (KCC_FIT_IN_REDUCE == 1)  // (2: timing diagnostic without the fences)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // node prep's stream, spec_place's records
-      fit_body<true>(np.n, np.fit_queue, np.fast_a, np.fast_b, np.slow, np.slow_list, np.S, np.fit_specs,
-                     np.fit_partial, np.counters, 0, np.fit_gx, np.fit_gy, np.fast_cl, np.faults,
-                     (int32_t)blockIdx.x - ((int32_t)gridDim.x - nfit),
-                     reinterpret_cast<uint32_t*>(&pre_s[0][0][0]));
-      return;
-    }
-  }
-#endif
-  const int32_t npb = NPM ? np.n_place + np.n_rows : 0;  // the last workgroups (before the fit's)
-  if constexpr (NPM) {
-    if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - nfit - npb) {
-      np_body(np, (int32_t)blockIdx.x - ((int32_t)gridDim.x - nfit - npb), reinterpret_cast<uint32_t*>(&pre_s[0][0][0]));
+    if ((int32_t)blockIdx.x >= (int32_t)gridDim.x - npb) {
+      np_body(np, (int32_t)blockIdx.x - ((int32_t)gridDim.x - npb), reinterpret_cast<uint32_t*>(&pre_s[0][0][0]));
       return;
     }
   }
   // the spec ranks' workgroups: behind the reduce's (RedArgs::ranks_last; dispatched as its
   // first waves retire, they run in the reduce's tail) or in front of them
-  const int32_t rank0 = a.ranks_last ? (int32_t)gridDim.x - nfit - npb - ra.n_blocks : 0;  // first rank block
+  const int32_t rank0 = a.ranks_last ? (int32_t)gridDim.x - npb - ra.n_blocks : 0;  // first rank block
   const int32_t red0 = a.ranks_last ? 0 : ra.n_blocks;                              // first reduce block
   if constexpr (NA == 2) {  // (launch_reduce: the ranks ride the 2-array reduce only)
     if (ra.n_blocks > 0 && (int32_t)blockIdx.x >= rank0 && (int32_t)blockIdx.x < rank0 + ra.n_blocks) {
@@ -376,10 +322,10 @@ __global__ __launch_bounds__(256) KCC_RED_WPE void reduce_kernel(RedArgs a, Rank
   // reduced (static ring indices: the tile loop below is unrolled over the ring).
   // The first tiles' loads go out first: they depend on the range alone, while the node
   // search below is a chain of dependent loads
-  constexpr int RING = RED_LATE ? 1 : RED_PREFETCH + 1;
+  constexpr int RING = RED_PREFETCH + 1;
   uint64_t xs[RING][NA][RED_IPL];
 #pragma unroll
-  for (int u = 0; u < (RED_LATE ? 1 : RED_PREFETCH); ++u)
+  for (int u = 0; u < RED_PREFETCH; ++u)
 #pragma unroll
     for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 8 * RED_IPL, u * RED_TILE * 8, xs[u][k]);
   __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink them below the search)
@@ -460,20 +406,14 @@ __global__ __launch_bounds__(256) KCC_RED_WPE void reduce_kernel(RedArgs a, Rank
 #ifndef KCC_DIAG_RED_NOSTORE
     issue_pending();
 #endif
-    if constexpr (!RED_LATE) {
 #pragma unroll
-      for (int k = 0; k < NA; ++k)
-        load_quad(rs[k], lane * 8 * RED_IPL, (tb + RED_PREFETCH * RED_TILE) * 8, nx[k]);
-    }
+    for (int k = 0; k < NA; ++k)
+      load_quad(rs[k], lane * 8 * RED_IPL, (tb + RED_PREFETCH * RED_TILE) * 8, nx[k]);
 #ifdef KCC_DIAG_RED_LOADONLY
 #pragma unroll
     for (int k = 0; k < NA; ++k)
 #pragma unroll
       for (int i = 0; i < RED_IPL; ++i) carry[k] += x[k][i];
-    if constexpr (RED_LATE) {
-#pragma unroll
-      for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 8 * RED_IPL, (tb + RED_TILE) * 8, nx[k]);
-    }
     return;
 #endif
     const int32_t p0l = tb + RED_IPL * lane;  // relative position of this lane's first item
@@ -490,43 +430,32 @@ __global__ __launch_bounds__(256) KCC_RED_WPE void reduce_kernel(RedArgs a, Rank
     // --- 1. tile-local inclusive prefix sums -> LDS -----------------------------
     // the lane's 4-item total, scanned in place; the lane's items' prefixes then walk
     // back from it (x0 is dead once the total is formed: fewer live registers)
+    // the lane's in-lane inclusive prefixes in place; after the scan, each item's prefix is
+    // the lane's exclusive base plus its in-lane prefix: 64-bit adds only (one
+    // v_lshl_add_u64 each; round 5 walked back from the lane's inclusive prefix with 64-bit
+    // subtracts, v_sub_co + v_subb each: 83 -> 73 VALU per tile, C4 130.8 -> 130.6 us, the
+    // 8-way shard 20.1 -> 19.9 us, profiles/r06d_ab_reduce_fwd_*.txt)
     uint64_t tot[NA], P[NA];
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
-      if constexpr (RED_FWD) {  // the lane's in-lane inclusive prefixes, in place
 #pragma unroll
-        for (int i = 1; i < RED_IPL; ++i) x[k][i] += x[k][i - 1];
-        P[k] = x[k][RED_IPL - 1];
-      } else {
-        P[k] = x[k][0];
-#pragma unroll
-        for (int i = 1; i < RED_IPL; ++i) P[k] += x[k][i];
-      }
+      for (int i = 1; i < RED_IPL; ++i) x[k][i] += x[k][i - 1];
+      P[k] = x[k][RED_IPL - 1];
     }
 #pragma unroll
     for (int k = 0; k < NA; k += 2) wave_incl_scan2_u64(P[k], P[k + 1]);
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
       uint64_t pp[RED_IPL];  // the lane's items' inclusive prefixes
-      if constexpr (RED_FWD) {  // the lane's exclusive base + its in-lane prefixes: adds only
-        const uint64_t base = P[k] - x[k][RED_IPL - 1];
+      const uint64_t base = P[k] - x[k][RED_IPL - 1];
 #pragma unroll
-        for (int i = 0; i < RED_IPL - 1; ++i) pp[i] = base + x[k][i];
-        pp[RED_IPL - 1] = P[k];
-      } else {  // walked back from P
-        pp[RED_IPL - 1] = P[k];
-#pragma unroll
-        for (int i = RED_IPL - 1; i > 0; --i) pp[i - 1] = pp[i] - x[k][i];
-      }
+      for (int i = 0; i < RED_IPL - 1; ++i) pp[i] = base + x[k][i];
+      pp[RED_IPL - 1] = P[k];
       u64x2* dst = reinterpret_cast<u64x2*>(&pre[k][0]);  // pair h at strip_at(8 lane + 2 h)
 #pragma unroll
       for (int h = 0; h < RED_IPL / 2; ++h) dst[h * 64 + lane] = u64x2{pp[2 * h], pp[2 * h + 1]};
       tot[k] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(P[k] >> 32), 63) << 32) |
                (uint32_t)__builtin_amdgcn_readlane((uint32_t)P[k], 63);
-    }
-    if constexpr (RED_LATE) {  // this tile's items are in the strip: its registers take the next tile
-#pragma unroll
-      for (int k = 0; k < NA; ++k) load_quad(rs[k], lane * 8 * RED_IPL, (tb + RED_TILE) * 8, nx[k]);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -599,8 +528,7 @@ __global__ __launch_bounds__(256) KCC_RED_WPE void reduce_kernel(RedArgs a, Rank
   for (int32_t tb = 0; tb < len; tb += RING * RED_TILE) {
 #pragma unroll
     for (int u = 0; u < RING; ++u)
-      if (tb + u * RED_TILE < len)
-        tile(xs[u], xs[(u + (RED_LATE ? 0 : RED_PREFETCH)) % RING], tb + u * RED_TILE);
+      if (tb + u * RED_TILE < len) tile(xs[u], xs[(u + RED_PREFETCH) % RING], tb + u * RED_TILE);
   }
 #if defined(KCC_DIAG_RED_LOADONLY) || defined(KCC_DIAG_RED_NOSTORE)
   if (carry[0] == 0x123456789ull) out[0][0] = carry[NA - 1] ^ res[0];
@@ -906,11 +834,6 @@ __device__ void np_body(const NpArgs& np, int32_t j, uint32_t* scratch) {
   // the last node-prep workgroup to finish publishes the epoch: every storing reduce wave
   // (each in some row workgroup's window), the rank workgroup and every node-prep workgroup
   // have read it by then
-#if KCC_FIT_IN_REDUCE
-  if (np.fit_blocks && KCC_FIT_IN_REDUCE == 1) {  // (the fit in this launch reads the stream)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  }
-#endif
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t total = (uint32_t)(np.n_place + np.n_rows);
@@ -918,12 +841,6 @@ __device__ void np_body(const NpArgs& np, int32_t j, uint32_t* scratch) {
       const uint32_t e = __hip_atomic_load(np.sync + NP_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(np.sync + NP_ARRIVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(np.sync + NP_EPOCH, e + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#if KCC_FIT_IN_REDUCE
-      if (np.fit_blocks) {  // every node-prep workgroup released its stores before arriving
-        if (KCC_FIT_IN_REDUCE == 1) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
-        __hip_atomic_store(np.sync + NP_GO, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-#endif
     }
   }
 }
@@ -2755,9 +2672,8 @@ __global__ __launch_bounds__(256) KCC_FIT_ATTR void fit_kernel(
 __global__ void fit_finalize_kernel(int64_t S, const int64_t* __restrict__ partial,
                                     const int32_t* __restrict__ perm, int64_t* __restrict__ totals,
                                     int32_t* __restrict__ spec_err,
-                                    const unsigned long long* __restrict__ faults, uint32_t* go) {
+                                    const unsigned long long* __restrict__ faults) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (go && i == 0) *go = 0u;  // (variant builds: the fit in the reduce launch has passed it)
   if (i >= S) return;
   const int32_t dst = perm[i];
   const bool err = partial[S + i] != 0;
@@ -2944,11 +2860,7 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
   const int64_t waves = red ? (n_containers + range - 1) / range : 0;
   if (waves > reduce_tail_records()) return hipErrorInvalidValue;
   const int64_t red_blocks = (waves + RED_WAVES_PER_BLOCK - 1) / RED_WAVES_PER_BLOCK;
-#if KCC_FIT_IN_REDUCE
-  const unsigned blocks = (unsigned)(red_blocks + ra.n_blocks + npb + (npb > 0 ? np.fit_blocks : 0));
-#else
   const unsigned blocks = (unsigned)(red_blocks + ra.n_blocks + npb);
-#endif
   np.ptr = node_ptr;
   np.c0 = c0;
   np.range = range;
@@ -3102,22 +3014,6 @@ static int64_t fit_grid_y(int64_t n_nodes, int64_t n_specs, int64_t grid_nodes) 
   return gy;
 }
 
-#if KCC_FIT_IN_REDUCE
-void fit_in_reduce_grid(int64_t n_nodes, int64_t n_specs, int32_t* gx, int32_t* gy) {
-  static std::atomic<int64_t> cache[MAX_DEVS];
-  const int64_t res = resident_blocks(cache, reinterpret_cast<const void*>(reduce_kernel<2, true>),
-                                      256, 0, 1024);
-  const int64_t x = (n_specs + FIT_SPW - 1) / FIT_SPW;
-  int64_t y = res / x;
-  if (y >= 16) y = y / 8 * 8;
-  const int64_t claims = (fit_groups(n_nodes) + FIT_QCHUNK - 1) / FIT_QCHUNK;
-  if (y > claims) y = claims;
-  if (y < 1) y = 1;
-  *gx = (int32_t)x;
-  *gy = (int32_t)y;
-}
-#endif
-
 hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* fast_b,
                       const SlowNode* slow,
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
@@ -3139,10 +3035,10 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
 
 hipError_t launch_fit_finalize(int64_t n_specs, const int64_t* partial, const int32_t* perm,
                                int64_t* totals, int32_t* spec_err,
-                               const unsigned long long* faults, hipStream_t s, uint32_t* go) {
+                               const unsigned long long* faults, hipStream_t s) {
   if (n_specs <= 0) return hipSuccess;
   hipLaunchKernelGGL(fit_finalize_kernel, dim3(grid_for(n_specs, 256, 1 << 30)), dim3(256), 0, s,
-                     n_specs, partial, perm, totals, spec_err, faults, go);
+                     n_specs, partial, perm, totals, spec_err, faults);
   return hipGetLastError();
 }
 

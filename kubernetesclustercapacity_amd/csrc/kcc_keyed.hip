@@ -702,26 +702,16 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
 // table entries share lines — read them through one L2 (round 5's placement spread neighbours
 // over the 8 XCDs: each line at a segment end and each table line was fetched by several L2s,
 // 1.34x the records' bytes).
-// A wave works on two sub-batches of KB_GA_U2 segments, the next one's loads in flight while
-// the current one is summed (a segment is a few hundred bytes: one per wave would be
+// A wave works on two sub-batches of KB_GA_U2 segments at once, the first summed while the
+// second's loads are in flight (a segment is a few hundred bytes: one per wave would be
 // latency-bound).
 constexpr int KB_GA_THREADS = 1024;
 constexpr int KB_GA_WAVES = KB_GA_THREADS / 64;
-// segments per sub-batch (two in flight per wave: 2 x 8 x 128 records = round 5's 16 x 128
-// in one batch, whose loads all waited before any was summed)
-#ifndef KCC_KB_GA_U2
-#define KCC_KB_GA_U2 8
-#endif
-constexpr int KB_GA_U2 = KCC_KB_GA_U2;
+// segments per sub-batch (two per wave at once: 2 x 8 x 128 records, as round 5's one
+// batch of 16 x 128)
+constexpr int KB_GA_U2 = 8;
 static_assert((KB_GA_U2 & (KB_GA_U2 - 1)) == 0 && KB_GA_U2 <= 64,
               "a sub-batch's table entries are read by lanes lane & (KB_GA_U2 - 1)");
-#ifndef KCC_KB_GA_NT
-#define KCC_KB_GA_NT 0
-#endif
-#ifndef KCC_KB_GA_PIPE
-#define KCC_KB_GA_PIPE 0
-#endif
-constexpr bool KB_GA_PIPE = KCC_KB_GA_PIPE != 0;
 constexpr int KB_GA_CH = 2048;  // tiles per table chunk in LDS (a barrier each: 1024 measured slower)
 constexpr int KB_XCDS = 8;      // gfx950: 8 XCDs, workgroups dealt round-robin
 // buckets per gather workgroup: a tile's segments of KB_GA_BPG adjacent buckets are
@@ -829,8 +819,9 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const uint32_t o = (uint32_t)lane + 64u * h;
-          if constexpr (KCC_KB_GA_NT) r[u][h] = __builtin_nontemporal_load(seg + (o < (len[u] & 0xffffu) ? o : 0u));
-          else r[u][h] = seg[o < (len[u] & 0xffffu) ? o : 0u];
+          // (default policy: a non-temporal load measured equal, r06e; the neighbouring
+          // groups' reads of a shared end line hit in the XCD's L2)
+          r[u][h] = seg[o < (len[u] & 0xffffu) ? o : 0u];
         }
       }
     };
@@ -850,22 +841,14 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
         for (uint32_t o = 128u + (uint32_t)lane; o < (len[u] & 0xffffu); o += 64u)
           add_rec(sr[first[u] + o], o >= (len[u] >> 16) ? (uint32_t)KB_ROWS : 0u);
     };
-    if constexpr (KB_GA_PIPE) {  // the next sub-batch's loads in flight across iterations
-      if (wv < nsb) load_sb(wv, ra, la, fa);
-      for (int t = wv; t < nsb; t += 2 * KB_GA_WAVES) {
-        load_sb(t + KB_GA_WAVES, rb, lb, fb);  // (past nsb: a harmless re-read, summed as empty)
-        sum_sb(ra, la, fa);
-        if (t + KB_GA_WAVES >= nsb) break;
-        load_sb(t + 2 * KB_GA_WAVES, ra, la, fa);
-        sum_sb(rb, lb, fb);
-      }
-    } else {  // two sub-batches loaded at once; the first summed while the second arrives
-      for (int t = wv; t < nsb; t += 2 * KB_GA_WAVES) {
-        load_sb(t, ra, la, fa);
-        load_sb(t + KB_GA_WAVES, rb, lb, fb);
-        sum_sb(ra, la, fa);
-        sum_sb(rb, lb, fb);
-      }
+    // two sub-batches loaded at once, the first summed while the second arrives (the next
+    // pair's loads kept in flight across iterations measured equal, r06d: the compiler's
+    // loop-carried registers wait for them at the loop head)
+    for (int t = wv; t < nsb; t += 2 * KB_GA_WAVES) {
+      load_sb(t, ra, la, fa);
+      load_sb(t + KB_GA_WAVES, rb, lb, fb);  // (past nsb: a harmless re-read, summed as empty)
+      sum_sb(ra, la, fa);
+      sum_sb(rb, lb, fb);
     }
   }
   __syncthreads();
