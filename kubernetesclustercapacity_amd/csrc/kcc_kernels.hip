@@ -409,7 +409,6 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra, NpA
 #pragma unroll
     for (int k = 0; k < NA; ++k)
       load_quad(rs[k], lane * 8 * RED_IPL, (tb + RED_PREFETCH * RED_TILE) * 8, nx[k]);
-
 #ifdef KCC_DIAG_RED_LOADONLY
 #pragma unroll
     for (int k = 0; k < NA; ++k)
