@@ -654,18 +654,17 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
   for (int c = 0; c < k; ++c) {
     const int64_t n = hi[c] - lo[c];
     ProfPair pp{};
-    if (dv.prof_on) {
+    if (dv.prof_on) {  // (the launch's own dispatch timestamps: no event packets around it)
       KCC_HIP(ctx, prof_event(dv, &pp.a));
       KCC_HIP(ctx, prof_event(dv, &pp.b));
-      KCC_HIP(ctx, hipEventRecord(pp.a, rs));
     }
     KCC_HIP(ctx, kcc::launch_reduce(n, c0[c], c1[c] - c0[c], ptr + lo[c], cpu, mem, nullptr, nullptr,
                                     used_cpu + lo[c], used_mem + lo[c], nullptr, nullptr,
                                     as<uint64_t>(dv.red_tail),
                                     as<unsigned long long>(dv.faults), rs,
-                                    fuse_rank ? &ra : nullptr, np_fused ? &np : nullptr));
+                                    fuse_rank ? &ra : nullptr, np_fused ? &np : nullptr,
+                                    dv.prof_on ? pp.a : nullptr, dv.prof_on ? pp.b : nullptr));
     if (dv.prof_on) {
-      KCC_HIP(ctx, hipEventRecord(pp.b, rs));
       pp.kind = 0;
       dv.prof_pending.push_back(pp);
     }
@@ -694,7 +693,6 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
     if (dv.prof_on) {
       KCC_HIP(ctx, prof_event(dv, &pp.a));
       KCC_HIP(ctx, prof_event(dv, &pp.b));
-      KCC_HIP(ctx, hipEventRecord(pp.a, s));
     }
     KCC_HIP(ctx, kcc::launch_fit(n, as<kcc::FitGroupA>(dv.fast_a) + lo[c] / kcc::FIT_GROUP,
                                  as<kcc::FitGroup>(dv.fast_b) + lo[c] / kcc::FIT_GROUP,
@@ -702,9 +700,9 @@ int capacity_partial_dev(kcc_ctx* ctx, Dev& dv, int64_t n_nodes, int64_t n_cont,
                                  as<int64_t>(dv.slow_list) + lo[c], n_specs, spec_prep_of(dv),
                                  partial, as<unsigned long long>(dv.counters),
                                  as<uint32_t>(dv.fit_q), c, n_nodes, s,
-                                 as<const unsigned long long>(dv.faults), fast_cl));
+                                 as<const unsigned long long>(dv.faults), fast_cl,
+                                 dv.prof_on ? pp.a : nullptr, dv.prof_on ? pp.b : nullptr));
     if (dv.prof_on) {
-      KCC_HIP(ctx, hipEventRecord(pp.b, s));
       pp.kind = 1;
       dv.prof_pending.push_back(pp);
     }

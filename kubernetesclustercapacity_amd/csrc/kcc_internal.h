@@ -104,7 +104,10 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
                          const uint64_t* cpu_lim, const int64_t* mem_lim,
                          uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem,
                          uint64_t* tail, unsigned long long* faults, hipStream_t s,
-                         const RankArgs* rank = nullptr, const NpArgs* np = nullptr);
+                         const RankArgs* rank = nullptr, const NpArgs* np = nullptr,
+                         hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+// (ev_start / ev_stop, kcc_profile_*: the kernel's own dispatch timestamps, hipExtLaunchKernel —
+// event packets around the launch also timed the dispatch, ~3 us per launch)
 
 // ---- (b) fit -----------------------------------------------------------------
 // Node streams of the fit kernel: groups of FIT_GROUP nodes, field-major inside the
@@ -424,7 +427,8 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, uint32_t* queue, int chunk,
                       int64_t grid_nodes, hipStream_t s, const unsigned long long* faults,
-                      const int32_t* fast_cl = nullptr);
+                      const int32_t* fast_cl = nullptr, hipEvent_t ev_start = nullptr,
+                      hipEvent_t ev_stop = nullptr);
 // the fit's work queues: fit_queue_words(S) uint32 (a 64-B line per spec column of 256 and
 // sub-queue), zero before the first launch (each launch leaves them zero)
 constexpr int64_t FIT_QSUBS_MAX = 32;

@@ -9,6 +9,7 @@
 // Both are integer work: no MFMA (no contraction), HBM-bound (a) / VALU-bound (b).
 // Results are bit-exact to Go's uint64/int64 wrapping arithmetic.
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -2829,7 +2830,8 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
                          const uint64_t* cpu_lim, const int64_t* mem_lim,
                          uint64_t* used_cpu, int64_t* used_mem, uint64_t* lim_cpu, int64_t* lim_mem,
                          uint64_t* tail, unsigned long long* faults, hipStream_t s,
-                         const RankArgs* rank, const NpArgs* npa) {
+                         const RankArgs* rank, const NpArgs* npa, hipEvent_t ev_start,
+                         hipEvent_t ev_stop) {
   RankArgs ra{};
   if (rank) ra = *rank;
   NpArgs np{};
@@ -2882,12 +2884,11 @@ hipError_t launch_reduce(int64_t n_nodes, int64_t c0, int64_t n_containers, cons
   a.tail = tail;
   a.faults = faults;
   a.ranks_last = ranks_last ? 1 : 0;
-  if (limits)
-    hipLaunchKernelGGL((reduce_kernel<4, false>), dim3(blocks), dim3(256), 0, s, a, ra, np);
-  else if (npb > 0)
-    hipLaunchKernelGGL((reduce_kernel<2, true>), dim3(blocks), dim3(256), 0, s, a, ra, np);
+  auto kern = limits ? reduce_kernel<4, false> : npb > 0 ? reduce_kernel<2, true> : reduce_kernel<2, false>;
+  if (ev_start || ev_stop)  // (profiling: the dispatch packet's own timestamps)
+    hipExtLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, ev_start, ev_stop, 0, a, ra, np);
   else
-    hipLaunchKernelGGL((reduce_kernel<2, false>), dim3(blocks), dim3(256), 0, s, a, ra, np);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, a, ra, np);
   return hipGetLastError();
 }
 
@@ -3019,7 +3020,7 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
                       const int64_t* slow_list, int64_t n_specs, SpecPrep sp, int64_t* partial,
                       unsigned long long* counters, uint32_t* queue, int chunk,
                       int64_t grid_nodes, hipStream_t s, const unsigned long long* faults,
-                      const int32_t* fast_cl) {
+                      const int32_t* fast_cl, hipEvent_t ev_start, hipEvent_t ev_stop) {
   if (n_nodes <= 0 || n_specs <= 0) return hipSuccess;
   const int64_t gx = (n_specs + FIT_SPW - 1) / FIT_SPW;
   const int64_t gy = fit_grid_y(n_nodes, n_specs, grid_nodes);
@@ -3027,9 +3028,14 @@ hipError_t launch_fit(int64_t n_nodes, const FitGroupA* fast_a, const FitGroup* 
   const int64_t blocks = gx * ((gy + 7) / 8 * 8);
   if (blocks > 0x7fffffffLL || gy > 0x7fffffffLL) return hipErrorInvalidValue;
   auto kern = fast_cl ? fit_kernel<true> : fit_kernel<false>;
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, queue, fast_a,
-                     fast_b, slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)chunk,
-                     (int32_t)gx, (int32_t)gy, fast_cl, faults);
+  if (ev_start || ev_stop)  // (profiling: the dispatch packet's own timestamps)
+    hipExtLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, ev_start, ev_stop, 0, n_nodes,
+                          queue, fast_a, fast_b, slow, slow_list, n_specs, sp.rec, partial, counters,
+                          (int32_t)chunk, (int32_t)gx, (int32_t)gy, fast_cl, faults);
+  else
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, n_nodes, queue, fast_a,
+                       fast_b, slow, slow_list, n_specs, sp.rec, partial, counters, (int32_t)chunk,
+                       (int32_t)gx, (int32_t)gy, fast_cl, faults);
   return hipGetLastError();
 }
 
