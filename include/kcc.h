@@ -26,11 +26,12 @@
  *     state that a replay would freeze: the reduce's look-back records are left free by
  *     every launch, the exchange's epoch is a device word).  Container arrays must be
  *     16-byte aligned.
- *   - Device faults: the reduce's look-back waits and the exchange's flag waits are
- *     bounded; one that gives up (never on a healthy device) sets a sticky fault word
- *     of the device.  While it is set every finalize marks every spec KCC_SPEC_FAULT
- *     (totals 0) and the synchronous entry points return KCC_EFAULT; kcc_clear_faults
- *     resets it.  The fault also travels with the data: a partial produced on a
+ *   - Device faults: the reduce's look-back and node-prep waits, the keyed gather's
+ *     part wait and the exchange's flag waits are bounded; one that gives up (never on
+ *     a healthy device) sets a sticky fault word of the device.  While it is set every
+ *     finalize marks every spec KCC_SPEC_FAULT (totals 0) and the synchronous entry
+ *     points (the keyed ones included) return KCC_EFAULT; kcc_clear_faults resets it
+ *     and every device counter a give-up can leave set.  The fault also travels with the data: a partial produced on a
  *     faulted device (kcc_*_partial_async, kcc_fit_run_async) carries a fault mark in
  *     its per-spec counts, so every rank that sums it — over the p2p exchange, an RCCL
  *     or any other all-reduce, the in-library device fold — marks every spec

@@ -245,7 +245,7 @@ int check_faults(kcc_ctx* ctx) {
   }
   if (red == 0 && p2p == 0) return KCC_OK;
   return fail(ctx, KCC_EFAULT,
-              "device fault: " + std::to_string(red) + " reduce look-back wait(s) and " +
+              "device fault: " + std::to_string(red) + " reduce-side wait(s) (look-back, node prep, keyed gather) and " +
                   std::to_string(p2p) +
                   " exchange flag wait(s) gave up; results are not valid (every spec is marked "
                   "KCC_SPEC_FAULT) until kcc_clear_faults");
@@ -1348,6 +1348,10 @@ int kcc_clear_faults(kcc_ctx* ctx) {
     if (dv.faults.p) KCC_HIP(ctx, hipMemset(dv.faults.p, 0, dv.faults.bytes));
     // a wait that gave up left its record published: every tag back to free
     if (dv.red_tail.p) KCC_HIP(ctx, hipMemset(dv.red_tail.p, 0, dv.red_tail.bytes));
+    // and every counter a launch leaves zero: a gather part that gave up can have
+    // published its ready count after the last part reset it
+    for (DevBuf* b : {&dv.kb_arrive, &dv.rank_arrive, &dv.fit_q, &dv.clamp_arrive})
+      if (b->p) KCC_HIP(ctx, hipMemset(b->p, 0, b->bytes));
     KCC_HIP(ctx, hipDeviceSynchronize());
   }
   return KCC_OK;

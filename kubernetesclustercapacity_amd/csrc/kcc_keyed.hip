@@ -895,7 +895,12 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
   }
   if (tid == 0) {
     uint32_t spins = 0;
-    while (__hip_atomic_load(ready + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+#ifdef KCC_DIAG_RED_GIVEUP  // fault-path build: the wait gives up at once, as a timed-out one
+    if (faults) atomicAdd(faults + FAULT_RED, 1ull);
+    spins = KB_GA_SPIN_MAX;
+#endif
+    while (spins < KB_GA_SPIN_MAX &&
+           __hip_atomic_load(ready + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
            (uint32_t)parts - 1u) {
       if (++spins >= KB_GA_SPIN_MAX) {  // never on a healthy device: the sums are not trusted
         if (faults) atomicAdd(faults + FAULT_RED, 1ull);

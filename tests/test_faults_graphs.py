@@ -110,6 +110,40 @@ def test_sync_entry_points_return_efault(diag_engine):
     np.testing.assert_array_equal(e, oe)
 
 
+def test_keyed_entry_points_return_efault(diag_engine, engine):
+    """The keyed one-sweep path (requests, count_by_key): the gather's part wait gives up at
+    once in the fault-path build (several parts per bucket group at this key count), so the
+    synchronous entry points return KCC_EFAULT; the bucketed path (calls with limits) has no
+    wait and is exact once the faults are cleared.  The release build's next calls after
+    kcc_clear_faults are exact (it re-zeroes the gather's arrival and ready counts)."""
+    from kubernetesclustercapacity_amd import KccError
+    rng = np.random.default_rng(5)
+    nk, nc = 3_000, 200_000
+    key = rng.integers(0, nk, nc).astype(np.int32)
+    cpu = rng.integers(0, 1 << 20, nc).astype(np.uint64)
+    mem = rng.integers(0, 1 << 40, nc).astype(np.int64)
+    ok = np.argsort(key, kind="stable")
+    ptr = np.searchsorted(key[ok], np.arange(nk + 1)).astype(np.int64)
+    uc, um, _, _ = coracle.reduce_requests(ptr, cpu[ok], mem[ok])
+    diag_engine.clear_faults()
+    for call in (lambda: diag_engine.get_pod_cpu_memory_requests_limits_keyed(nk, key, cpu, mem),
+                 lambda: diag_engine.count_by_key(nk, key)):
+        with pytest.raises(KccError) as ei:
+            call()
+        assert ei.value.code == KCC_EFAULT, ei.value
+        assert "gave up" in str(ei.value)
+        diag_engine.clear_faults()
+    r = diag_engine.get_pod_cpu_memory_requests_limits_keyed(nk, key, cpu, mem, cpu, mem)
+    np.testing.assert_array_equal(r.cpu_requests, uc)
+    np.testing.assert_array_equal(r.memory_requests, um)
+    engine.clear_faults()
+    for _ in range(2):
+        r = engine.get_pod_cpu_memory_requests_limits_keyed(nk, key, cpu, mem)
+        np.testing.assert_array_equal(r.cpu_requests, uc)
+        np.testing.assert_array_equal(r.memory_requests, um)
+        np.testing.assert_array_equal(engine.count_by_key(nk, key), np.diff(ptr))
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_async_finalizes_mark_every_spec(diag_engine, mode):
     """kcc_capacity_async (mode 0: fused clamp finalize; 1: clamp in the fit + finalize)
