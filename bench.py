@@ -469,6 +469,10 @@ def main():
     fit_instr = streamed * ((S + 63) // 64) * valu_pn
     fit_valu = fit_instr / chunks / (fit_ms * 1e-3)
     red_gbs = red_bytes / (red_ms * 1e-3) / 1e9
+    # the clamp in the fit on one chunk: node prep's row work runs in the reduce launch
+    # (kcc_abi.cpp np_fused), so its bytes are that launch's too
+    np_fused = clamp_in_fit and chunks == 1
+    np_bytes = n * (32 + 16) + streamed * 20  # alloc + pod_count and used_* in, stream out
     c4_alone = args.config == "C4" and world == 1 and args.emulate_world <= 1  # the profiled run
     w_eff = args.emulate_world if args.emulate_world > 1 else world
     shard_key = (f"{args.config}/w{w_eff}" if w_eff > 1 and args.scaling == "strong" and chunks == 1
@@ -552,7 +556,11 @@ def main():
                     "value counts every node x spec pair; see dense_layout",
         },
         "roofline_reduce": {
-            "bound": "hbm", "kernel": "reduce_kernel<2> (its mark runs inside the spec_rank launch)",
+            "bound": "hbm",
+            "kernel": ("reduce_kernel<2, node prep> (the launch also runs spec_place and node "
+                       "prep's row work behind the reduce's workgroups, DESIGN §4.2)" if np_fused else
+                       "reduce_kernel<2>" + (" (+ the spec-rank workgroups in its launch)"
+                                             if chunks == 1 else "")),
             "achieved": red_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": red_gbs / HBM_PEAK_GBS, "bytes_per_launch": red_bytes, "ms_per_launch": red_ms,
             "traffic": red_traffic,
@@ -568,12 +576,21 @@ def main():
         "fast_path_fraction": 1.0 - (slow_pairs / pairs if pairs else 0.0),
         "gen_seconds": gen_s,
     }
+    if np_fused:
+        lb = red_bytes + np_bytes
+        out["roofline_reduce"].update(
+            launch_bytes=lb, launch_frac=lb / (red_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            launch_note="launch_bytes adds node prep's algorithmic bytes (48 B per row in, 20 B "
+                        "per streamed row out) to the reduce's: the bytes the whole launch moves")
     if cold is not None:  # the same kernels with the Infinity Cache and L2s flushed
         c_red = cold["reduce_ms_per_launch"]
         c_fit = cold["fit_ms_per_launch"]
         out["roofline_reduce"].update(
             ms_per_launch_cold=c_red, achieved_cold=red_bytes / (c_red * 1e-3) / 1e9,
             frac_cold=red_bytes / (c_red * 1e-3) / 1e9 / HBM_PEAK_GBS)
+        if np_fused:
+            out["roofline_reduce"]["launch_frac_cold"] = (
+                (red_bytes + np_bytes) / (c_red * 1e-3) / 1e9 / HBM_PEAK_GBS)
         out["roofline_valu"].update(
             ms_per_launch_cold=c_fit, frac_cold=fit_instr / chunks / (c_fit * 1e-3) / VALU_ISSUE_PEAK)
         out["cold"] = cold
