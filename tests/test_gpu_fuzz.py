@@ -85,13 +85,17 @@ SIZES_S = st.one_of(st.sampled_from([1, 63, 64, 65, 127, 128, 255, 256, 257, 700
 @settings(max_examples=200, derandomize=True, deadline=None,
           suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
 @given(seed=st.integers(0, 2**32 - 1), n=SIZES_N, s=SIZES_S,
-       layout=st.sampled_from(["correction", "in_fit", "dense"]))
-def test_capacity_fuzz(engine, seed, n, s, layout):
+       layout=st.sampled_from(["correction", "in_fit", "dense"]),
+       shards=st.sampled_from([0, 0, 2, 3]))
+def test_capacity_fuzz(engine, seed, n, s, layout, shards):
+    """shards > 0: the host-array calls cut the nodes into that many shards on the one
+    device (partials summed on the device, kcc_set_node_shards)."""
     ptr, cpu, mem, acpu, amem, apods, pcount, sc, sm = make_case(seed, n, s)
     uc, um, _, _ = coracle.reduce_requests(ptr, cpu, mem)
     ot, oe = coracle.fit(acpu, amem, apods, pcount, uc, um, sc, sm, NT)
     engine.set_clamp_in_fit({"correction": 0, "in_fit": 1, "dense": -1}[layout])
     engine.set_fit_dense(layout == "dense")
+    engine.set_node_shards(shards)
     try:
         r = engine.get_pod_cpu_memory_requests_limits(ptr, cpu, mem)
         np.testing.assert_array_equal(r.cpu_requests, uc)
@@ -105,6 +109,7 @@ def test_capacity_fuzz(engine, seed, n, s, layout):
     finally:
         engine.set_clamp_in_fit(-1)
         engine.set_fit_dense(False)
+        engine.set_node_shards(0)
 
 
 @settings(max_examples=60, derandomize=True, deadline=None,
