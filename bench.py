@@ -55,9 +55,12 @@ def pmc_traffic(kernel, shard=None):
     try:
         with open(TRAFFIC_FILE) as f:
             t = json.load(f)
-        # (round-3 profiles name the fit kernel `fit_kernel`; it is a template since,
-        # `fit_kernel<false>` for the clamp-correction layout)
-        names = (kernel, "fit_kernel<false>") if kernel == "fit_kernel" else (kernel,)
+        # (the profiles name a kernel as rocprofv3 printed it in their round: `fit_kernel`
+        # in round 3, `fit_kernel<false>` / `<true>` since; `reduce_kernel<2>` before round
+        # 6, `reduce_kernel<2, false>` / `<2, true>` (node prep in the launch) since)
+        names = {"fit_kernel": ("fit_kernel", "fit_kernel<false>", "fit_kernel<true>"),
+                 "reduce_kernel<2>": ("reduce_kernel<2>", "reduce_kernel<2, false>",
+                                      "reduce_kernel<2, true>")}.get(kernel, (kernel,))
         e = t["shards"][shard] if shard else t
         ks = e["kernels"]
         name = next(k for k in names if k in ks)

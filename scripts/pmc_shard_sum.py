@@ -36,7 +36,8 @@ def main(traffic_json, dirs):
                 wk = sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"])
                 ent[k] = {"hbm_bytes_per_launch": (2 * fk + wk) * 1024, "fetch_kib": fk, "write_kib": wk}
         shards[f"{cfg}/w{w}"] = {"source": f"pmcshard_{tag}", "kernels": ent}
-        for k in ("reduce_kernel<2>", "fit_kernel"):
+        for k in ("reduce_kernel<2>", "reduce_kernel<2, false>", "reduce_kernel<2, true>",
+                  "fit_kernel<false>", "fit_kernel<true>"):
             if k in ent:
                 print(f"{cfg} w{w} {k}: {ent[k]['hbm_bytes_per_launch'] / 1e6:.2f} MB per launch")
     t["shards_method"] = ("rank 0's node shard of a W-way strong-scaling split, run alone on one "
