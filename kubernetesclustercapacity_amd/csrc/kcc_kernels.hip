@@ -281,6 +281,11 @@ __global__ __launch_bounds__(256) void reduce_kernel(RedArgs a, RankArgs ra, NpA
   const int32_t red0 = a.ranks_last ? 0 : ra.n_blocks;                              // first reduce block
   if constexpr (NA == 2) {  // (launch_reduce: the ranks ride the 2-array reduce only)
     if (ra.n_blocks > 0 && (int32_t)blockIdx.x >= rank0 && (int32_t)blockIdx.x < rank0 + ra.n_blocks) {
+      // the rank workgroups' waves issue ahead of the reduce's waves on their CUs (the
+      // arbiter serves the oldest wave first, and the ranks, dispatched last, gate node
+      // prep): 2-way C4 rank step 168.4 -> 165.2 / 168.5 -> 165.6 us, 4-way 88.1 -> 87.6,
+      // C4 and the 8-way rank equal (round 6, profiles/r06t_ab_rank_prio.txt)
+      __builtin_amdgcn_s_setprio(3);
       spec_rank_body(ra, (int32_t)blockIdx.x - rank0, &pre_s[0][0][0]);
       return;
     }
