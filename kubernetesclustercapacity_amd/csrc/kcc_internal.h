@@ -530,9 +530,8 @@ struct KeyedWork {
 // rows.  The four-kernel bucketed path (kb_hist / kb_scan / kb_scatter / kb_accum) serves
 // only the calls with limits (NA = 4).
 constexpr int KB_SW_THREADS = 1024;
-constexpr int KB_SW_PER = 8;  // containers per thread (the next half's loads in registers)
-constexpr int64_t KB_SW_HALF = (int64_t)KB_SW_THREADS * KB_SW_PER;  // 8192
-constexpr int64_t KB_SW_TILE = 2 * KB_SW_HALF;  // 16384: one run and table row, two halves
+constexpr int KB_SW_PER = 8;  // containers per thread (the next tile's loads in registers)
+constexpr int64_t KB_SW_TILE = (int64_t)KB_SW_THREADS * KB_SW_PER;  // 8192
 // containers per sweep tile: KB_SW_TILE, or (beyond one round of one tile per CU) cut so
 // the tiles make whole rounds (C4: 2418 tiles = 9.4 rounds -> 2560 of 15472 = 10); a
 // tile's records keep the KB_SW_TILE stride in the staging buffer

@@ -48,7 +48,6 @@ constexpr int KY_BLOCK = KY_THREADS * KY_IPL;         // containers per workgrou
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // inclusive prefix sum of a 32-bit value over the wave's 64 lanes (DPP, all VALU)
 __device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
@@ -516,18 +515,13 @@ __global__ __launch_bounds__(256) void kb_escape(uint32_t* __restrict__ esc_n,
 }
 
 // ---- one-sweep path (NA = 0 counts / 2 requests) --------------------------------------
-// kb_sweep: tile g = containers [g * tile, ...) (tile <= KB_SW_TILE = 16384:
-// keyed_sweep_tile), swept as two halves of up to KB_SW_HALF = 8192 containers, 8 per
-// thread (16-B loads of quads).  Per half: each valid container's rank within its bucket
+// kb_sweep: tile g = containers [g * tile, ...) (tile <= KB_SW_TILE: keyed_sweep_tile), 8
+// per thread (16-B loads of quads).  Each valid container's rank within its bucket comes
 // from an LDS counter (two 16-bit counters per word), one exclusive scan of the counts
-// gives the half's bucket starts, and its records are counting-sorted into the half's part
-// of an LDS stage.  After the second half the tile leaves as ONE contiguous run in bucket
-// order — bucket b's first-half records, then its second-half ones — into the tile's own
-// region sr[g * KB_SW_TILE ...], its bucket starts into the tile's table row (tab[g][b],
-// tab[g][nb] = the tile's valid records).  No global histogram, no scan launch, and the
-// keys are read once.  Round 6: a table row and a run per 16384 containers instead of per
-// 8192 — kb_gather reads each bucket pair's records of a tile as one segment twice as long
-// (about 1 KB at C4 instead of 534 B), half as many segments and table entries.
+// gives the bucket starts, the records are counting-sorted into an LDS stage and leave as
+// ONE contiguous run of nvalid records (16-B stores: whole lines) into the tile's own
+// region sr[g * KB_SW_TILE ...], the starts into the tile's table row (tab[g][b],
+// tab[g][nb] = nvalid).  No global histogram, no scan launch, and the keys are read once.
 constexpr int KB_SW_WAVES = KB_SW_THREADS / 64;
 constexpr int KB_SW_CNT_WORDS = (int)(KB_NB_MAX / 2);  // two 16-bit bucket counts per word
 
@@ -536,11 +530,12 @@ __device__ __forceinline__ uint32_t kb_half(const uint32_t* w, int b) {
 }
 
 // Persistent and software-pipelined (round 5): one workgroup per CU walks the tiles
-// g = blockIdx.x, + gridDim.x, ..., half by half; the next half's loads (range-checked
-// buffer loads, so their count is static) go out before the current half's ranks, scan,
-// scatter (and, after the second half, the copy-out), so the CU's HBM traffic does not stop
-// for the LDS work.  Round 4's sweep took one 16384-container tile per workgroup launch —
-// load, then work, then store, every phase alone on the CU: C4 keyed 0.3327 -> 0.3257 ms.
+// g = blockIdx.x, + gridDim.x, ...; the next tile's loads (range-checked buffer loads, so
+// their count is static) go out before the current tile's ranks, scan, scatter and
+// stores, so the CU's HBM traffic does not stop for the LDS work.  Round 4's sweep took one
+// 16384-container tile per workgroup launch — load, then work, then store, every phase
+// alone on the CU: C4 keyed 0.3327 -> 0.3257 ms (sweep 255 -> 223 us, the gather 83 ->
+// 112 us over twice the segments).
 template <int NA>
 __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
     int64_t n, int64_t n_keys, const int32_t* __restrict__ key, const uint64_t* __restrict__ a0,
@@ -550,27 +545,20 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
   static_assert(NA == 0 || NA == 2, "one-sweep path: counts or requests");
   constexpr int NS = NA > 0 ? NA : 1;
   constexpr int PER = KB_SW_PER;
-  // the stage: the first half's records in bucket order at [0, KB_SW_HALF) with their
-  // buckets (u16) above them, then the tile's run in its final order
-  __shared__ uint64_t st[KB_SW_TILE];
-  __shared__ uint32_t cnt2[KB_SW_CNT_WORDS];   // the half's counts, then its bucket starts
-  __shared__ uint16_t sa[KB_NB_MAX + 1];       // the first half's bucket starts (sa[nb]: its count)
+  __shared__ uint64_t st[KB_SW_TILE];  // the tile's records, bucket order
+  __shared__ uint32_t cnt2[KB_SW_CNT_WORDS];
   __shared__ uint32_t wtot[KB_SW_WAVES];
-  uint16_t* const lbl = reinterpret_cast<uint16_t*>(st + KB_SW_HALF);
-  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nw = (nb + 1) / 2;
-  const int64_t half = tile / 2;  // (tile is a multiple of 8: keyed_sweep_tile)
-  // valid keys: 0 <= key < n_keys (as one unsigned compare; n_keys <= KB_NB_MAX * KB_ROWS)
-  const uint32_t nk32 = (uint32_t)n_keys;
-  // a half's loads: quads of consecutive containers (16-B buffer loads through descriptors
-  // that end at the half's end: outside, they read 0 and the validity test drops them)
+  // tile g's loads: quads of consecutive containers (16-B buffer loads through descriptors
+  // that end at the tile's end: outside, they read 0 and the validity test drops them)
   int32_t kn[PER];
   uint64_t vn[NS][PER];
-  auto issue = [&](int64_t g, int h) {
-    const int64_t t0 = g * tile + h * half, t1 = min(t0 + half, n);
+  auto issue = [&](int64_t g) {
+    const int64_t t0 = g * tile, t1 = min(t0 + tile, n);
     const int32_t len = (int32_t)(t1 > t0 ? t1 - t0 : 0);
     const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(key + (t1 > t0 ? t0 : 0)), (short)0, 4 * len, 0x00020000);
+        (void*)(key + t0), (short)0, 4 * len, 0x00020000);
 #pragma unroll
     for (int q = 0; q < PER / 4; ++q) {
       const int32_t o = 4 * (q * KB_SW_THREADS + tid);
@@ -585,7 +573,7 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
         const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(in[a] + (t1 > t0 ? t0 : 0)), (short)0, 8 * len, 0x00020000);
+            (void*)(in[a] + t0), (short)0, 8 * len, 0x00020000);
 #pragma unroll
         for (int q = 0; q < PER / 4; ++q) {
           const int32_t o = 4 * (q * KB_SW_THREADS + tid);
@@ -601,151 +589,102 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
   };
   int64_t g = blockIdx.x;
   KCC_TLK(512 + blockIdx.x, 0);
-  if (g < G) issue(g, 0);
+  if (g < G) issue(g);
   for (; g < G; g += gridDim.x) {
     if (g == (int64_t)blockIdx.x + gridDim.x) KCC_TLK(512 + blockIdx.x, 1);  // first tile done
-    uint32_t n_half0 = 0, n_tile = 0;
-#pragma unroll 1
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1) __syncthreads();  // the first half's scatter has read its starts (cnt2)
-      const int64_t t0 = g * tile + h * half, t1 = min(t0 + half, n);
-      const int32_t hlen = (int32_t)(t1 > t0 ? t1 - t0 : 0);  // the half's containers
-      int32_t k[PER];
-      uint64_t v[NS][PER];
+    const int64_t t0 = g * tile, t1 = min(t0 + tile, n);
+    int32_t k[PER];
+    uint64_t v[NS][PER];
 #pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        k[u] = kn[u];
+    for (int u = 0; u < PER; ++u) {
+      k[u] = kn[u];
 #pragma unroll
-        for (int a = 0; a < NS; ++a) v[a][u] = NA == 2 ? vn[a][u] : 0ull;
-      }
-      // in flight during this half's work: the second half, or the next tile's first
-      {
-        const int64_t gn = h == 0 ? g : g + gridDim.x;
-        if (gn < G) issue(gn, 1 - h);
-      }
-      for (int w = tid; w < nw; w += KB_SW_THREADS) cnt2[w] = 0;
-      __syncthreads();  // counters zeroed (and the previous tile's stage copied out)
-      uint64_t rec[PER];
-      uint32_t br[PER];
+      for (int a = 0; a < NS; ++a) v[a][u] = NA == 2 ? vn[a][u] : 0ull;
+    }
+    if (g + gridDim.x < G) issue(g + gridDim.x);  // in flight during this tile's work
+    for (int w = tid; w < nw; w += KB_SW_THREADS) cnt2[w] = 0;
+    __syncthreads();  // counters zeroed (and the previous tile's stage read)
+    uint64_t rec[PER];
+    uint32_t br[PER];
 #pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        const int32_t c = 4 * ((u / 4) * KB_SW_THREADS + tid) + (u & 3);
-        const bool valid = c < hlen && (uint32_t)k[u] < nk32;
-        const int b = valid ? k[u] >> KB_SHIFT : 0;
-        const uint32_t sh = 16u * (uint32_t)(b & 1);
-        const uint32_t rk = valid ? (atomicAdd(&cnt2[b >> 1], 1u << sh) >> sh) & 0xffffu : 0u;
-        br[u] = valid ? (uint32_t)b << 16 | rk : 0xffffffffu;
-        const uint32_t row = (uint32_t)k[u] & (KB_ROWS - 1);
-        if constexpr (NA == 2) {
-          rec[u] = kb_record(row, v[0][u], v[1][u]);
-          if (valid) {
-            const bool mem_ok = kb_mem_ok(v[1][u]);
-            if (!mem_ok || (v[0][u] >> KB_CPU_BITS) != 0) {  // rare: what the record cannot hold
-              const uint32_t e = atomicAdd(esc_n, 1u);
-              esc_row[e] = k[u];
-              esc_cpu[e] = v[0][u] & ~KB_CPU_LO;
-              esc_mem[e] = mem_ok ? 0ull : v[1][u];
-            }
+    for (int u = 0; u < PER; ++u) {
+      const int64_t c = t0 + 4 * ((int64_t)(u / 4) * KB_SW_THREADS + tid) + (u & 3);
+      const bool valid = c < t1 && k[u] >= 0 && (int64_t)k[u] < n_keys;
+      const int b = valid ? k[u] >> KB_SHIFT : 0;
+      const uint32_t sh = 16u * (uint32_t)(b & 1);
+      const uint32_t rk = valid ? (atomicAdd(&cnt2[b >> 1], 1u << sh) >> sh) & 0xffffu : 0u;
+      br[u] = valid ? (uint32_t)b << 16 | rk : 0xffffffffu;
+      const uint32_t row = (uint32_t)k[u] & (KB_ROWS - 1);
+      if constexpr (NA == 2) {
+        rec[u] = kb_record(row, v[0][u], v[1][u]);
+        if (valid) {
+          const bool mem_ok = kb_mem_ok(v[1][u]);
+          if (!mem_ok || (v[0][u] >> KB_CPU_BITS) != 0) {  // rare: what the record cannot hold
+            const uint32_t e = atomicAdd(esc_n, 1u);
+            esc_row[e] = k[u];
+            esc_cpu[e] = v[0][u] & ~KB_CPU_LO;
+            esc_mem[e] = mem_ok ? 0ull : v[1][u];
           }
-        } else {
-          rec[u] = row;
         }
+      } else {
+        rec[u] = row;
       }
-      __syncthreads();
-      uint32_t c4[4];
+    }
+    __syncthreads();
+    uint32_t c4[4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int w = 2 * tid + j;
+      const uint32_t x = w < nw ? cnt2[w] : 0u;
+      c4[2 * j] = x & 0xffffu;
+      c4[2 * j + 1] = x >> 16;
+    }
+    const uint32_t s4 = c4[0] + c4[1] + c4[2] + c4[3];
+    const uint32_t incl = wave_incl_scan32(s4);
+    if (lane == 63) wtot[wv] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, nvalid = 0;
+#pragma unroll
+    for (int w = 0; w < KB_SW_WAVES; ++w) {
+      const uint32_t t = wtot[w];
+      wbase += w < wv ? t : 0u;
+      nvalid += t;
+    }
+    {
+      uint32_t run = wbase + incl - s4;
+      uint32_t st4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        st4[j] = run;
+        run += c4[j];
+      }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int w = 2 * tid + j;
-        const uint32_t x = w < nw ? cnt2[w] : 0u;
-        c4[2 * j] = x & 0xffffu;
-        c4[2 * j + 1] = x >> 16;
+        if (w < nw) cnt2[w] = st4[2 * j] | st4[2 * j + 1] << 16;
       }
-      const uint32_t s4 = c4[0] + c4[1] + c4[2] + c4[3];
-      const uint32_t incl = wave_incl_scan32(s4);
-      if (lane == 63) wtot[wv] = incl;
-      __syncthreads();
-      uint32_t wbase = 0, nvalid = 0;
+      uint32_t* rowp = tab + g * (nb + 1);
 #pragma unroll
-      for (int w = 0; w < KB_SW_WAVES; ++w) {
-        const uint32_t t = wtot[w];
-        wbase += w < wv ? t : 0u;
-        nvalid += t;
-      }
-      {
-        uint32_t run = wbase + incl - s4;
-        uint32_t st4[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          st4[j] = run;
-          run += c4[j];
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int w = 2 * tid + j;
-          if (w < nw) cnt2[w] = st4[2 * j] | st4[2 * j + 1] << 16;
-        }
-        if (h == 0) {  // (the scan's barrier above ordered the previous tile's reads of sa)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (4 * tid + j < nb) sa[4 * tid + j] = (uint16_t)st4[j];
-          if (tid == 0) sa[nb] = (uint16_t)nvalid;
-        } else {  // the tile's bucket starts: the first half's before, this half's after
-          uint32_t* rowp = tab + g * (nb + 1);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int b = 4 * tid + j;
-            if (b < nb) rowp[b] = sa[b] + st4[j];
-          }
-          if (tid == 0) rowp[nb] = sa[nb] + nvalid;
-        }
-      }
-      n_half0 = h == 0 ? nvalid : n_half0;
-      n_tile = n_half0 + (h == 1 ? nvalid : 0u);
-      __syncthreads();
-      if (h == 0) {  // counting sort by bucket, each record's bucket beside it
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-          if (br[u] == 0xffffffffu) continue;
-          const uint32_t i = kb_half(cnt2, (int)(br[u] >> 16)) + (br[u] & 0xffffu);
-          st[i] = rec[u];
-          lbl[i] = (uint16_t)(br[u] >> 16);
-        }
-      } else {
-        // the final order: bucket b at sa[b] + sB[b] (sB = this half's starts), its
-        // first-half records, then its second-half ones.  A first-half record at slot i
-        // moves to i + sB[b] (read into registers before the stage is rewritten); a
-        // second-half record of rank r goes to sB[b] + sa[b + 1] + r
-        // (this thread's slots PER tid ..: four 16-B record reads and one of 8 labels)
-        static_assert(PER == 8, "one 16-B read of a thread's 8 labels");
-        u64x2 ar[PER / 2];
-#pragma unroll
-        for (int q = 0; q < PER / 2; ++q) ar[q] = reinterpret_cast<const u64x2*>(st)[PER / 2 * tid + q];
-        const u32x4 al = reinterpret_cast<const u32x4*>(lbl)[tid];
-        __syncthreads();  // every first-half slot and label read
-#pragma unroll
-        for (int q = 0; q < PER; ++q) {
-          const uint32_t i = (uint32_t)(PER * tid + q);
-          const uint32_t b = (al[q >> 1] >> (16 * (q & 1))) & 0xffffu;
-          if (i < n_half0) st[i + kb_half(cnt2, (int)b)] = (q & 1) ? ar[q >> 1].y : ar[q >> 1].x;
-        }
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-          if (br[u] == 0xffffffffu) continue;
-          const int b = (int)(br[u] >> 16);
-          st[kb_half(cnt2, b) + sa[b + 1] + (br[u] & 0xffffu)] = rec[u];
-        }
-      }
+      for (int j = 0; j < 4; ++j)
+        if (4 * tid + j < nb) rowp[4 * tid + j] = st4[j];
+      if (tid == 0) rowp[nb] = nvalid;
     }
-    __syncthreads();  // the run complete in the stage
-    // the run leaves as one contiguous piece: a fixed number of 16-B streaming stores per
-    // thread, through a descriptor that ends at n_tile records (past it they are dropped;
-    // an odd last record goes as a pair with the slot after it, in range of the tile's
-    // region but past n_tile: harmless)
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(sr + g * KB_SW_TILE), (short)0, 8 * (int)((n_tile + 1u) & ~1u), 0x00020000);
+    __syncthreads();
 #pragma unroll
-    for (int q = 0; q < KB_SW_TILE / (2 * KB_SW_THREADS); ++q) {
-      const uint32_t j = 2u * (uint32_t)(q * KB_SW_THREADS + tid);
+    for (int u = 0; u < PER; ++u) {
+      if (br[u] == 0xffffffffu) continue;
+      st[kb_half(cnt2, (int)(br[u] >> 16)) + (br[u] & 0xffffu)] = rec[u];
+    }
+    __syncthreads();
+    // the stage leaves as one contiguous run: a fixed number of 16-B streaming stores per
+    // thread, through a descriptor that ends at nvalid records (past it they are dropped;
+    // an odd last record goes as a pair with the zero slot after it, which is in range of
+    // the tile's region but past nvalid: harmless)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(sr + g * KB_SW_TILE), (short)0, 8 * (int)((nvalid + 1u) & ~1u), 0x00020000);
+#pragma unroll
+    for (int h = 0; h < KB_SW_TILE / (2 * KB_SW_THREADS); ++h) {
+      const uint32_t j = 2u * (uint32_t)(h * KB_SW_THREADS + tid);
       const u64x2 pr = *reinterpret_cast<const u64x2*>(&st[j]);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, pr), rs, (int)(8 * j), 0, 2);
     }
@@ -770,10 +709,7 @@ constexpr int KB_GA_THREADS = 1024;
 constexpr int KB_GA_WAVES = KB_GA_THREADS / 64;
 // segments per sub-batch (two per wave at once: 2 x 8 x 128 records, as round 5's one
 // batch of 16 x 128)
-constexpr int KB_GA_U2 = 4;
-// records of a segment loaded at once (the rest of a longer one 64 a step): 3 x 64 — a
-// bucket pair's segment of a 16384-container tile is ~126 records at C4
-constexpr int KB_GA_H = 3;
+constexpr int KB_GA_U2 = 8;
 static_assert((KB_GA_U2 & (KB_GA_U2 - 1)) == 0 && KB_GA_U2 <= 64,
               "a sub-batch's table entries are read by lanes lane & (KB_GA_U2 - 1)");
 constexpr int KB_GA_CH = 2048;  // tiles per table chunk in LDS (a barrier each: 1024 measured slower)
@@ -860,9 +796,9 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
     // past it re-read the segment's first record, a line the wave reads anyway), so each
     // sub-batch issues the same instructions and the waits stay static
     const int nsb = (ch + KB_GA_U2 - 1) / KB_GA_U2;
-    uint64_t ra[KB_GA_U2][KB_GA_H], rb[KB_GA_U2][KB_GA_H];
+    uint64_t ra[KB_GA_U2][2], rb[KB_GA_U2][2];
     uint32_t la[KB_GA_U2], fa[KB_GA_U2], lb[KB_GA_U2], fb[KB_GA_U2];
-    auto load_sb = [&](int t, uint64_t (&r)[KB_GA_U2][KB_GA_H], uint32_t (&len)[KB_GA_U2],
+    auto load_sb = [&](int t, uint64_t (&r)[KB_GA_U2][2], uint32_t (&len)[KB_GA_U2],
                        uint32_t (&first)[KB_GA_U2]) {
       // the sub-batch's table entries: one LDS read per array by lanes 0..U2-1, then
       // wave-uniform (SGPR) lengths and starts
@@ -881,7 +817,7 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
         first[u] = g * stride + (uint32_t)__builtin_amdgcn_readlane((int)voff, u);
         const uint64_t* __restrict__ seg = sr + first[u];
 #pragma unroll
-        for (int h = 0; h < KB_GA_H; ++h) {
+        for (int h = 0; h < 2; ++h) {
           const uint32_t o = (uint32_t)lane + 64u * h;
           // (default policy: a non-temporal load measured equal, r06e; the neighbouring
           // groups' reads of a shared end line hit in the XCD's L2)
@@ -889,12 +825,12 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
         }
       }
     };
-    auto sum_sb = [&](uint64_t (&r)[KB_GA_U2][KB_GA_H], uint32_t (&len)[KB_GA_U2],
+    auto sum_sb = [&](uint64_t (&r)[KB_GA_U2][2], uint32_t (&len)[KB_GA_U2],
                       uint32_t (&first)[KB_GA_U2]) {
 #pragma unroll
       for (int u = 0; u < KB_GA_U2; ++u) {
 #pragma unroll
-        for (int h = 0; h < KB_GA_H; ++h) {
+        for (int h = 0; h < 2; ++h) {
           const uint32_t o = (uint32_t)lane + 64u * h;
           if (o < (len[u] & 0xffffu)) add_rec(r[u][h], o >= (len[u] >> 16) ? (uint32_t)KB_ROWS : 0u);
         }
@@ -902,7 +838,7 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
       // the rest of long segments (skewed keys), 64 records a step
 #pragma unroll 1
       for (int u = 0; u < KB_GA_U2; ++u)
-        for (uint32_t o = 64u * KB_GA_H + (uint32_t)lane; o < (len[u] & 0xffffu); o += 64u)
+        for (uint32_t o = 128u + (uint32_t)lane; o < (len[u] & 0xffffu); o += 64u)
           add_rec(sr[first[u] + o], o >= (len[u] >> 16) ? (uint32_t)KB_ROWS : 0u);
     };
     // two sub-batches loaded at once, the first summed while the second arrives (the next
@@ -1049,7 +985,7 @@ int64_t keyed_sweep_tile(int64_t n) {
   if (n <= KB_SW_TILE * cus) return KB_SW_TILE;
   const int64_t rounds = (n + KB_SW_TILE * cus - 1) / (KB_SW_TILE * cus);
   const int64_t t = (n + rounds * cus - 1) / (rounds * cus);
-  return (t + 7) / 8 * 8;  // (two halves of quads, 16-B loads; <= KB_SW_TILE)
+  return (t + 3) / 4 * 4;  // (quads: 16-B loads; <= KB_SW_TILE, a multiple of 4)
 }
 int64_t keyed_sweep_tiles(int64_t n) {
   const int64_t t = keyed_sweep_tile(n);
