@@ -506,7 +506,7 @@ constexpr int KB_TILE = 65536;
 constexpr int64_t KB_NB_MAX = 4096;  // buckets (LDS cursors): n_keys <= 16M rows
 struct KeyedWork {
   uint32_t* counts;   // [keyed_tiles(n) * keyed_buckets(n_keys)] (one-sweep path: the tiles'
-                      // bucket starts, [keyed_sweep_tiles(n)][nb + 1])
+                      // bucket starts, u16 entries in blocks of 32 buckets, kcc_keyed.hip kb_tab_at)
   uint32_t* tot;      // [keyed_buckets(n_keys)]
   uint64_t* sr;       // [n] scattered 8-B records: row within the bucket, low 20 cpu
                       // bits, memory / 64 (kcc_keyed.hip kb_record)

@@ -520,13 +520,23 @@ __global__ __launch_bounds__(256) void kb_escape(uint32_t* __restrict__ esc_n,
 // from an LDS counter (two 16-bit counters per word), one exclusive scan of the counts
 // gives the bucket starts, the records are counting-sorted into an LDS stage and leave as
 // ONE contiguous run of nvalid records (16-B stores: whole lines) into the tile's own
-// region sr[g * KB_SW_TILE ...], the starts into the tile's table row (tab[g][b],
-// tab[g][nb] = nvalid).  No global histogram, no scan launch, and the keys are read once.
+// region sr[g * KB_SW_TILE ...], the starts into the tile's table entries (kb_tab_at:
+// entry (g, b), entry (g, nb) = nvalid).  No global histogram, no scan launch, and the keys are read once.
 constexpr int KB_SW_WAVES = KB_SW_THREADS / 64;
 constexpr int KB_SW_CNT_WORDS = (int)(KB_NB_MAX / 2);  // two 16-bit bucket counts per word
 
 __device__ __forceinline__ uint32_t kb_half(const uint32_t* w, int b) {
   return (w[b >> 1] >> (16 * (b & 1))) & 0xffffu;
+}
+
+// The tiles' bucket starts (the sweep's table): 16-bit entries (a tile holds < 2^16
+// records) in blocks of KB_TB buckets — entry (g, b) at [b / KB_TB][g][b % KB_TB] — so a
+// gather workgroup, whose bucket pair lies in one or two blocks, reads 64-B pieces of
+// them, and an XCD's groups (a contiguous run of buckets) read about 1/8 of the table
+// (round 5's [g][nb + 1] u32 rows: every XCD read the whole 4.8 MB table at C4)
+constexpr int KB_TB = 32;
+__device__ __forceinline__ int64_t kb_tab_at(int64_t G, int64_t g, int b) {
+  return ((int64_t)(b / KB_TB) * G + g) * KB_TB + (b % KB_TB);
 }
 
 // Persistent and software-pipelined (round 5): one workgroup per CU walks the tiles
@@ -663,11 +673,25 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
         const int w = 2 * tid + j;
         if (w < nw) cnt2[w] = st4[2 * j] | st4[2 * j + 1] << 16;
       }
-      uint32_t* rowp = tab + g * (nb + 1);
+      // (4 tid .. 4 tid + 3 lie in one block: one 8-B store; the entry nb = nvalid)
+      static_assert(KB_TB % 4 == 0, "a thread's four entries in one block");
+      if (4 * tid <= nb) {
+        // (32-bit block offset: the table holds < 2^32 entries, keyed_counts_words)
+        uint16_t* const t16 = reinterpret_cast<uint16_t*>(tab) + (uint32_t)g * KB_TB +
+                              (uint32_t)(4 * tid / KB_TB) * (uint32_t)(G * KB_TB) + (4 * tid) % KB_TB;
+        uint32_t e[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (4 * tid + j < nb) rowp[4 * tid + j] = st4[j];
-      if (tid == 0) rowp[nb] = nvalid;
+        for (int j = 0; j < 4; ++j) e[j] = 4 * tid + j == nb ? nvalid : st4[j];
+        if (4 * tid + 3 <= nb) {
+          *reinterpret_cast<uint2*>(t16) = make_uint2(e[0] | e[1] << 16, e[2] | e[3] << 16);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (4 * tid + j <= nb) t16[j] = (uint16_t)e[j];
+        }
+      }
+      if (tid == 0 && nb >= 4 * KB_SW_THREADS)  // (the entry nb past every thread's four)
+        reinterpret_cast<uint16_t*>(tab)[kb_tab_at(G, g, nb)] = (uint16_t)nvalid;
     }
     __syncthreads();
 #pragma unroll
@@ -692,7 +716,7 @@ __global__ __launch_bounds__(KB_SW_THREADS) void kb_sweep(
   KCC_TLK(512 + blockIdx.x, 2);
 }
 
-// kb_gather: bucket group b's records — segment [tab[g][b0], tab[g][b0 + nbk]) of every tile
+// kb_gather: bucket group b's records — segment [entry (g, b0), entry (g, b0 + nbk)) of every tile
 // g — summed into LDS rows (64-bit LDS atomics), its rows written once.  `parts` workgroups
 // share a group (tiles dealt round-robin): each sums its tiles; the last to arrive adds the
 // others' rows and writes the outputs, and only the others publish theirs (part_acc).
@@ -719,7 +743,7 @@ constexpr int KB_XCDS = 8;      // gfx950: 8 XCDs, workgroups dealt round-robin
 // partial lines and their latency batches, for twice the LDS rows)
 constexpr int KB_GA_BPG = 2;
 constexpr int KB_GA_ROWS = KB_GA_BPG * KB_ROWS;  // LDS rows per gather workgroup
-static_assert(KB_SW_TILE < 0xffff, "a segment's length and split point pack in 16 bits each");
+static_assert(KB_SW_TILE < 0xffff, "a segment's length and split point pack in 16 bits each; table entries are u16");
 static_assert(2 * KB_GA_ROWS * 8 + 2 * KB_GA_CH * 4 + 64 <= 160 * 1024,
               "kb_gather<2>'s LDS (rows of both arrays + the segment tables) fits one CU");
 // Tiles are read newest-first (the last-written records first, while the memory-side cache
@@ -775,10 +799,10 @@ __global__ __launch_bounds__(KB_GA_THREADS) void kb_gather(
     for (int q = 0; q < TQ; ++q) {
       const int i = tid + q * KB_GA_THREADS;
       const int64_t g = (int64_t)part + (my_tiles - 1 - (c0 + (i < ch ? i : 0))) * parts;
-      const uint32_t* row = tab + g * (nb + 1) + b0;
-      e0[q] = row[0];
-      e1[q] = row[nbk];
-      e2[q] = row[KB_GA_BPG > 1 && nbk > 1 ? 1 : 0];
+      const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tab);
+      e0[q] = t16[kb_tab_at(G, g, b0)];
+      e1[q] = t16[kb_tab_at(G, g, b0 + nbk)];
+      e2[q] = t16[kb_tab_at(G, g, KB_GA_BPG > 1 && nbk > 1 ? b0 + 1 : b0)];
     }
 #pragma unroll
     for (int q = 0; q < TQ; ++q) {
@@ -1004,7 +1028,8 @@ int keyed_sweep_parts(int64_t nb) {
 }
 int64_t keyed_counts_words(int64_t n_keys, int64_t n) {
   const int64_t nb = keyed_buckets(n_keys);
-  const int64_t a = keyed_tiles(n) * nb, b = keyed_sweep_tiles(n) * (nb + 1);
+  const int64_t a = keyed_tiles(n) * nb;
+  const int64_t b = (nb / KB_TB + 1) * keyed_sweep_tiles(n) * KB_TB / 2;  // (u16 entries, blocked)
   return a > b ? a : b;
 }
 int64_t keyed_sr_slots(int64_t n) {
