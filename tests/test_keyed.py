@@ -229,3 +229,25 @@ def test_gpu_keyed_sweep_tiles(eng, nc):
         assert np.array_equal(r.cpu_requests, o[0]) and np.array_equal(r.memory_requests, o[1])
     ok = key[(key >= 0) & (key < nk)]
     assert np.array_equal(eng.count_by_key(nk, key), np.bincount(ok, minlength=nk).astype(np.int64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nb", [1, 3, 4, 31, 32, 33, 127, 128, 129, 1023, 4095])
+def test_gpu_keyed_bucket_counts_table_blocks(eng, nb):
+    """The sweep's table (u16 bucket starts in blocks of 32 buckets, [b / 32][tile][b % 32],
+    kcc_keyed.hip kb_tab_at): key spaces whose bucket count sits at and around the block
+    edges and the 4-entry groups a sweep thread stores, the last entry (nb) in a block of
+    its own or shared, over several tiles per workgroup (more than 256 tiles), vs the
+    oracle; the pod counts through the same kernels."""
+    nk = (nb - 1) * 4096 + 1 + (nb * 37) % 4096  # nb buckets, the last one partial
+    rng = np.random.default_rng(nb)
+    nc = 2_300_000
+    key = rng.integers(0, nk, nc).astype(np.int32)
+    key[rng.random(nc) < 0.02] = -1
+    cpu = (rng.integers(0, 41, nc) * 25).astype(np.uint64)
+    mem = rng.integers(0, 4096, nc).astype(np.int64) << 20
+    o = oracle_keyed(nk, key, cpu, mem)
+    r = eng.get_pod_cpu_memory_requests_limits_keyed(nk, key, cpu, mem)
+    assert np.array_equal(r.cpu_requests, o[0]) and np.array_equal(r.memory_requests, o[1])
+    ok = key[(key >= 0) & (key < nk)]
+    assert np.array_equal(eng.count_by_key(nk, key), np.bincount(ok, minlength=nk).astype(np.int64))
